@@ -1,0 +1,53 @@
+"""Builds the in-tree gfx950 HIP library `fedbiomed_amd/_lib/libfbm_secagg.so`.
+
+    python -m fedbiomed_amd._build            # incremental (rebuilds when a source is newer)
+    python -m fedbiomed_amd._build --force
+
+hipcc cross-compiles for gfx950 without a GPU.  -ffp-contract=off is load-bearing: the
+quantise / average / dequantise FP64 sequences must round exactly like CPython + numpy.
+"""
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "_lib", "libfbm_secagg.so")
+SOURCES = ["fbm_lom.hip", "fbm_jl.hip", "fbm_capi.hip"]
+HEADERS = ["fbm_common.hpp", "fbm_mont.hpp", "fbm_internal.hpp"]
+ARCH = os.environ.get("FBM_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.sep not in c or os.path.exists(c)):
+            return c
+    return "hipcc"
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "fbm_secagg.h")]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    tmp = OUT + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+           "-I" + os.path.join(ROOT, "include")] + [os.path.join(CSRC, f) for f in SOURCES] + ["-o", tmp]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,332 @@
+"""Device-resident entry points: torch tensors in HBM -> C-ABI HIP kernels -> torch tensors.
+
+torch is plumbing here (device memory, the current HIP stream); all arithmetic runs in the
+hand-written gfx950 kernels of `fedbiomed_amd/csrc` behind `include/fbm_secagg.h`.  There is
+no CPU fallback: without a visible HIP device every call raises `NativeUnavailable`.
+
+Host-side work in this module is limited to argument validation and the per-call uniform
+parameters the reference computes in Python (`float(c)`, `(2c)/(T-1)`, slot sizes), so the
+Python semantics stay bit-identical.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .constants import ErrorNumbers, SAParameters
+from .exceptions import FedbiomedSecaggCrypterError, FedbiomedSecaggError
+
+U64_MAX = 2**64 - 1
+
+
+# ------------------------------------------------------------------------------------------
+# plumbing
+# ------------------------------------------------------------------------------------------
+def device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise N.NativeUnavailable("no HIP device is visible: the MI355X crypter has no CPU path")
+    N.load()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _stream() -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[ctypes.c_void_p]:
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _np_ptr(a: np.ndarray) -> ctypes.c_void_p:
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _raise(rc: int) -> None:
+    msg = N.last_error()
+    if rc == N.FBM_E_OVERFLOW:
+        raise FedbiomedSecaggError(f"{ErrorNumbers.FB417.value}: {msg}")
+    if rc == N.FBM_E_RANGE:
+        raise FedbiomedSecaggCrypterError(
+            f"{ErrorNumbers.FB624.value}: Cannot reverse quantize, received values exceed maximum number")
+    if rc == N.FBM_E_FDH:
+        raise OverflowError("int too big to convert")  # the reference's FDH counter.to_bytes(1)
+    if rc == N.FBM_E_INVERSE:
+        raise ZeroDivisionError("invert() no inverse exists")
+    if rc in (N.FBM_E_ARG, N.FBM_E_UNSUPPORTED):
+        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: {msg}")
+    raise RuntimeError(f"fedbiomed_amd HIP error {rc}: {msg}")
+
+
+def _call(fn, *args) -> None:
+    rc = fn(*args)
+    if rc != N.FBM_OK:
+        _raise(rc)
+
+
+def _check_stats(stats: torch.Tensor, lom_nodes: int = 0) -> int:
+    host = stats.cpu().numpy().astype(np.uint32)  # synchronises the stream
+    mb = ctypes.c_uint32(0)
+    rc = N.load().fbm_check_stats(_np_ptr(host), lom_nodes, ctypes.byref(mb))
+    if rc != N.FBM_OK:
+        _raise(rc)
+    return int(mb.value)
+
+
+def _stats(dev) -> torch.Tensor:
+    return torch.empty(N.STATS_WORDS, dtype=torch.int32, device=dev)
+
+
+def _x_dtype(x: torch.Tensor) -> int:
+    if x.dtype == torch.float32:
+        return N.FBM_F32
+    if x.dtype == torch.float64:
+        return N.FBM_F64
+    if x.dtype in (torch.int64, torch.uint64):
+        return N.FBM_U64
+    raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: unsupported input dtype {x.dtype}")
+
+
+# ------------------------------------------------------------------------------------------
+# parameters (Python-exact, as the reference computes them)
+# ------------------------------------------------------------------------------------------
+def quant_params(clip, target) -> Tuple[float, float, float, int]:
+    """(float(c), float(2c), float(T), T-1) for `quantize` (utils/_secagg_utils.py:82-119)."""
+    c = SAParameters.CLIPPING_RANGE if clip is None else clip
+    if target - 1 > U64_MAX:
+        # the reference's np.vectorize(otypes=[uint64]) raises on the clipped elements
+        raise OverflowError("Python int too large to convert to C unsigned long")
+    if c == 0:
+        raise ZeroDivisionError("float division by zero")
+    cf = float(c)
+    if cf != c or abs(cf) > 2.0**53 or c < 0:
+        raise FedbiomedSecaggCrypterError(
+            f"{ErrorNumbers.FB624.value}: clipping_range must be a positive value exactly representable "
+            f"in float64 for the device quantiser (got {c!r})")
+    return cf, float(2 * c), float(target), int(target - 1)
+
+
+def dequant_params(clip, target) -> Tuple[float, float]:
+    """(float(-c), (2c)/(T-1)) for `reverse_quantize` (utils/_secagg_utils.py:168-182)."""
+    c = SAParameters.CLIPPING_RANGE if clip is None else clip
+    step = (c - (-c)) / (target - 1)  # Python int/int true division, correctly rounded
+    return float(-c), float(step)
+
+
+def jl_slot(target: Optional[int], n_users: int) -> Tuple[int, int]:
+    """(element_size, comp_ratio) of the JL vector encoder (_jls.py:104-116, 587-591)."""
+    target = target or SAParameters.TARGET_RANGE
+    valuesize = math.ceil(math.log2(target) + math.log2(SAParameters.WEIGHT_RANGE))
+    es = valuesize + math.ceil(math.log2(n_users + 1))
+    cr = math.floor((SAParameters.KEY_SIZE // 2) / es)
+    return es, cr
+
+
+def int_limbs(v: int, n_limbs: int) -> np.ndarray:
+    return np.frombuffer(int(v).to_bytes(4 * n_limbs, "little"), dtype=np.uint32).copy()
+
+
+# ------------------------------------------------------------------------------------------
+# list <-> tensor conversions (the host-memory boundary, measured in DESIGN.md)
+# ------------------------------------------------------------------------------------------
+def floats_to_device(params: Sequence[float], dev=None) -> torch.Tensor:
+    dev = dev or device()
+    return torch.from_numpy(np.asarray(params, dtype=np.float64)).to(dev)
+
+
+def u64_to_device(rows, dev=None) -> torch.Tensor:
+    """list[int] or list[list[int]] -> int64 tensor holding the uint64 bit patterns.
+    np.array(..., dtype=uint64) raises exactly where the reference's conversion raises."""
+    dev = dev or device()
+    arr = np.array(rows, dtype=np.uint64)
+    return torch.from_numpy(arr.view(np.int64)).to(dev)
+
+
+def u64_from_device(t: torch.Tensor) -> List[int]:
+    return t.cpu().numpy().view(np.uint64).tolist()
+
+
+def ints_to_limbs(cts: Sequence[int], modulus: Optional[int] = None) -> np.ndarray:
+    """JL ciphertext ints -> [n, 64] uint32 little-endian limbs.  Values outside
+    [0, 2^2048) are reduced mod N^2 first (same residue, as the reference reduces in its
+    product); in-range values go through unchanged."""
+    out = bytearray(256 * len(cts))
+    for i, c in enumerate(cts):
+        c = int(c)
+        if c < 0 or c.bit_length() > 2048:
+            c %= modulus
+        out[256 * i:256 * (i + 1)] = c.to_bytes(256, "little")
+    return np.frombuffer(bytes(out), dtype=np.uint32).reshape(len(cts), 64)
+
+
+def limbs_to_ints(arr: np.ndarray) -> List[int]:
+    b = np.ascontiguousarray(arr, dtype=np.uint32).tobytes()
+    return [int.from_bytes(b[256 * i:256 * (i + 1)], "little") for i in range(len(b) // 256)]
+
+
+# ------------------------------------------------------------------------------------------
+# LOM
+# ------------------------------------------------------------------------------------------
+def _secret_block(secrets: Sequence[bytes]) -> np.ndarray:
+    for s in secrets:
+        if not isinstance(s, (bytes, bytearray)) or len(s) != 32:
+            n = len(s) * 8 if isinstance(s, (bytes, bytearray)) else "?"
+            raise FedbiomedSecaggError(
+                f"{ErrorNumbers.FB417.value}: Error while ciphering: got exception "
+                f"Invalid key size ({n}) for ChaCha20.")
+    return np.frombuffer(b"".join(bytes(s) for s in secrets) or b"\0", dtype=np.uint8).copy()
+
+
+def _nonce_block(nonce: bytes) -> np.ndarray:
+    if not isinstance(nonce, (bytes, bytearray)) or len(nonce) != 16:
+        raise FedbiomedSecaggError(
+            f"{ErrorNumbers.FB417.value}: Error while ciphering: got exception nonce must be 128-bits (16 bytes)")
+    return np.frombuffer(bytes(nonce), dtype=np.uint8).copy()
+
+
+def lom_protect(x: torch.Tensor, secrets: Sequence[bytes], signs: Sequence[int], nonce: bytes, tau: int,
+                n_nodes: int, clip=None, target=None, weight: int = 1, raw_seeds: bool = False) -> torch.Tensor:
+    """One party's masked vector (u64 bit patterns in an int64 tensor); raises the
+    reference's LOM overflow error when max(bit_length(q*w)) >= 64 - ceil(log2(n_nodes))."""
+    dev = x.device
+    lib = N.load()
+    target = target or SAParameters.TARGET_RANGE
+    c, c2, tf, tm1 = quant_params(clip, target) if x.dtype != torch.int64 else (1.0, 2.0, 1.0, 0)
+    if tau < 0 or tau > U64_MAX:
+        raise OverflowError("int too big to convert")
+    sec = _secret_block(secrets)
+    sg = np.asarray([1 if s > 0 else -1 for s in signs] or [0], dtype=np.int8)
+    nb = _nonce_block(nonce)
+    x = x.contiguous()
+    n = x.numel()
+    y = torch.empty(n, dtype=torch.int64, device=dev)
+    st = _stats(dev)
+    _call(lib.fbm_lom_protect, _ptr(x), _x_dtype(x), n, c, c2, tf, tm1, int(weight), _np_ptr(sec), _np_ptr(sg),
+          len(secrets), 1 if raw_seeds else 0, _np_ptr(nb), int(tau), _ptr(y), _ptr(st), _stream())
+    _check_stats(st, lom_nodes=n_nodes)
+    return y
+
+
+def prf_key(secret: bytes, nonce: bytes, tau: int, dev=None) -> bytes:
+    dev = dev or device()
+    sec = _secret_block([secret])
+    nb = _nonce_block(nonce)
+    if tau < 0 or tau >= 2**64:
+        raise OverflowError("int too big to convert")
+    out = torch.empty(32, dtype=torch.uint8, device=dev)
+    _call(N.load().fbm_prf_key, _np_ptr(sec), _np_ptr(nb), int(tau), _ptr(out), _stream())
+    return out.cpu().numpy().tobytes()
+
+
+def lom_aggregate(Y: torch.Tensor, total_weight: int, clip=None, target=None,
+                  want_out: bool = True, want_sums: bool = False):
+    """Column sum (mod 2^64) + average + dequantise of a [P, n] int64 (u64) tensor."""
+    dev = Y.device
+    lib = N.load()
+    target = target or SAParameters.TARGET_RANGE
+    if total_weight == 0:
+        raise ZeroDivisionError("division by zero")
+    if total_weight < 0 or total_weight > U64_MAX:
+        raise FedbiomedSecaggCrypterError(
+            f"{ErrorNumbers.FB624.value}: total_sample_size must be in [1, 2^64) for the device path")
+    negc, step = dequant_params(clip, target)
+    Y = Y.contiguous()
+    P, n = Y.shape
+    out = torch.empty(n, dtype=torch.float64, device=dev) if want_out else None
+    sums = torch.empty(n, dtype=torch.int64, device=dev) if want_sums else None
+    st = _stats(dev)
+    _call(lib.fbm_lom_aggregate, _ptr(Y), P, n, int(total_weight), negc, step, _ptr(out), _ptr(sums), _ptr(st),
+          _stream())
+    _check_stats(st)
+    return out, sums
+
+
+def dequantize(u: torch.Tensor, clip=None, target=None) -> torch.Tensor:
+    target = target or SAParameters.TARGET_RANGE
+    negc, step = dequant_params(clip, target)
+    u = u.contiguous()
+    out = torch.empty(u.numel(), dtype=torch.float64, device=u.device)
+    _call(N.load().fbm_dequantize, _ptr(u), u.numel(), negc, step, _ptr(out), _stream())
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# Joye-Libert
+# ------------------------------------------------------------------------------------------
+def _biprime_limbs(biprime: int) -> np.ndarray:
+    if biprime <= 0 or biprime.bit_length() > 1024:
+        raise FedbiomedSecaggCrypterError(
+            f"{ErrorNumbers.FB624.value}: biprime must be a positive integer of at most 1024 bits")
+    return int_limbs(biprime, 32)
+
+
+def _key_limbs(key: int) -> Tuple[np.ndarray, int]:
+    if abs(key).bit_length() > 2048:
+        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: key larger than 2048 bits")
+    return int_limbs(abs(key), 64), 1 if key < 0 else 0
+
+
+def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, clip=None, target=None,
+               weight: int = 1, slot: Optional[Tuple[int, int]] = None) -> torch.Tensor:
+    """One party's JL ciphertexts as an int32 [n_ct, 64] tensor of 32-bit limbs.
+    `slot` overrides the (element_size, comp_ratio) packing (UserKey.encrypt on raw
+    plaintexts = slot (es, 1) with an int64 input)."""
+    dev = x.device
+    lib = N.load()
+    target = target or SAParameters.TARGET_RANGE
+    es, cr = slot if slot else jl_slot(target, n_users)
+    c, c2, tf, tm1 = quant_params(clip, target) if x.dtype != torch.int64 else (1.0, 2.0, 1.0, 0)
+    if tau < 0 or tau > U64_MAX:
+        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: round must be in [0, 2^64)")
+    x = x.contiguous()
+    n = x.numel()
+    n_ct = (n + cr - 1) // cr
+    ct = torch.empty((n_ct, 64), dtype=torch.int32, device=dev)
+    if n_ct == 0:
+        return ct
+    bp = _biprime_limbs(biprime)
+    kl, kneg = _key_limbs(key)
+    ws = torch.empty(int(lib.fbm_jl_encrypt_workspace(n_ct)), dtype=torch.uint8, device=dev)
+    st = _stats(dev)
+    _call(lib.fbm_jl_encrypt, _ptr(x), _x_dtype(x), n, c, c2, tf, tm1, int(weight), es, cr, _np_ptr(bp),
+          _np_ptr(kl), kneg, int(tau), _ptr(ct), _ptr(ws), _ptr(st), _stream())
+    _check_stats(st)
+    return ct
+
+
+def jl_aggregate(cts: torch.Tensor, biprime: int, key: int, tau: int, n_expected: int, total_weight: int,
+                 clip=None, target=None, want_out: bool = True, want_sums: bool = False,
+                 slot: Optional[Tuple[int, int]] = None):
+    """Aggregate [P, n_ct, 64] int32 ciphertext limbs -> (float64 [n_out], int64 [n_out, 2] sums)."""
+    dev = cts.device
+    lib = N.load()
+    target = target or SAParameters.TARGET_RANGE
+    P, n_ct, _ = cts.shape
+    es, cr = slot if slot else jl_slot(target, P)
+    n_out = max(0, min(int(n_expected), n_ct * cr))
+    negc, step = dequant_params(clip, target)
+    if total_weight == 0:
+        raise ZeroDivisionError("division by zero")
+    if total_weight < 0 or total_weight > U64_MAX:
+        raise FedbiomedSecaggCrypterError(
+            f"{ErrorNumbers.FB624.value}: total_sample_size must be in [1, 2^64) for the device path")
+    if tau < 0 or tau > U64_MAX:
+        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: round must be in [0, 2^64)")
+    out = torch.empty(n_out, dtype=torch.float64, device=dev) if want_out else None
+    sums = torch.empty((n_out, 2), dtype=torch.int64, device=dev) if want_sums else None
+    if n_ct == 0:
+        return out, sums
+    bp = _biprime_limbs(biprime)
+    kl, kneg = _key_limbs(key)
+    cts = cts.contiguous()
+    ws = torch.empty(int(lib.fbm_jl_aggregate_workspace(n_ct)), dtype=torch.uint8, device=dev)
+    st = _stats(dev)
+    _call(lib.fbm_jl_aggregate, _ptr(cts), P, n_ct, es, cr, n_out, _np_ptr(bp), _np_ptr(kl), kneg, int(tau),
+          int(total_weight), negc, step, _ptr(out), _ptr(sums), _ptr(ws), _ptr(st), _stream())
+    _check_stats(st)
+    return out, sums

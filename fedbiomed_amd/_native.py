@@ -1,0 +1,90 @@
+"""ctypes binding of the C-ABI HIP library (include/fbm_secagg.h).
+
+The library is built in-tree (`python -m fedbiomed_amd._build` or
+`__graft_entry__.build()`) to `fedbiomed_amd/_lib/libfbm_secagg.so`.  There is NO
+CPU fallback: if the library or a GPU is missing, every compute call raises.
+
+torch is imported first so that the process has exactly one HIP runtime: torch's
+bundled `libamdhip64.so` has the same SONAME (`libamdhip64.so.7`) our library links
+against, so the dynamic loader binds us to the already-loaded copy.
+"""
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (loads the HIP runtime the library must share)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libfbm_secagg.so")
+
+FBM_OK = 0
+FBM_E_ARG = -1
+FBM_E_HIP = -2
+FBM_E_RANGE = -3
+FBM_E_OVERFLOW = -4
+FBM_E_FDH = -5
+FBM_E_INVERSE = -6
+FBM_E_ITER = -7
+FBM_E_UNSUPPORTED = -8
+
+FBM_F32 = 0
+FBM_F64 = 1
+FBM_U64 = 2
+STATS_WORDS = 4
+
+_lock = threading.Lock()
+_lib = None
+
+c_u64 = ctypes.c_uint64
+c_dbl = ctypes.c_double
+c_int = ctypes.c_int
+c_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); must match include/fbm_secagg.h exactly
+SIGNATURES = {
+    "fbm_abi_version": (c_int, []),
+    "fbm_last_error": (ctypes.c_char_p, []),
+    "fbm_check_stats": (c_int, [c_vp, c_int, c_vp]),
+    "fbm_lom_protect": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_vp, c_vp, c_int, c_int,
+                                c_vp, c_u64, c_vp, c_vp, c_vp]),
+    "fbm_prf_key": (c_int, [c_vp, c_vp, c_u64, c_vp, c_vp]),
+    "fbm_dequantize": (c_int, [c_vp, c_u64, c_dbl, c_dbl, c_vp, c_vp]),
+    "fbm_lom_aggregate": (c_int, [c_vp, c_int, c_u64, c_u64, c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp]),
+    "fbm_jl_encrypt_workspace": (c_u64, [c_u64]),
+    "fbm_jl_aggregate_workspace": (c_u64, [c_u64]),
+    "fbm_jl_encrypt": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_int, c_int, c_vp, c_vp,
+                               c_int, c_u64, c_vp, c_vp, c_vp, c_vp]),
+    "fbm_jl_aggregate": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_u64, c_vp, c_vp, c_int, c_u64, c_u64, c_dbl,
+                                 c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
+}
+
+
+class NativeUnavailable(RuntimeError):
+    """The HIP extension is not built or cannot be loaded."""
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Loads (once) and returns the C-ABI library; raises NativeUnavailable."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise NativeUnavailable(
+                f"HIP extension not built: {path} is missing (run `python -m fedbiomed_amd._build`)")
+        try:
+            lib = ctypes.CDLL(path)
+        except OSError as e:  # pragma: no cover - depends on the box
+            raise NativeUnavailable(f"cannot load {path}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.fbm_abi_version() != 1:
+            raise NativeUnavailable("ABI version mismatch")
+        _lib = lib
+        return lib
+
+
+def last_error() -> str:
+    return (load().fbm_last_error() or b"").decode(errors="replace")

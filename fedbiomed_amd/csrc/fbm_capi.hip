@@ -1,0 +1,472 @@
+// fedbiomed_amd -- C ABI (include/fbm_secagg.h): argument validation, per-call uniform
+// parameter setup (Montgomery constants, SHA-256 midstate, sliding-window schedule,
+// ChaCha20 IV words) and kernel launches.  All device memory belongs to the caller.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <vector>
+
+#include "fbm_internal.hpp"
+
+namespace fbm {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s launch failed: %s", what, hipGetErrorString(e));
+    return FBM_E_HIP;
+  }
+  return FBM_OK;
+}
+
+static int zero_stats(uint32_t* stats, hipStream_t s) {
+  if (!stats) {
+    set_error("stats buffer is required");
+    return FBM_E_ARG;
+  }
+  hipError_t e = hipMemsetAsync(stats, 0, FBM_STATS_WORDS * sizeof(uint32_t), s);
+  if (e != hipSuccess) {
+    set_error("hipMemsetAsync(stats): %s", hipGetErrorString(e));
+    return FBM_E_HIP;
+  }
+  return FBM_OK;
+}
+
+static int quant_params(double clip, double two_clip, double target_f, uint64_t target_m1, QuantParams& qp) {
+  if (!(clip > 0.0) || !(two_clip > 0.0) || !(target_f >= 1.0)) {
+    set_error("invalid quantisation parameters (clip=%g, target=%g)", clip, target_f);
+    return FBM_E_ARG;
+  }
+  qp.c = clip;
+  qp.two_c = two_clip;
+  qp.tf = target_f;
+  qp.tm1 = target_m1;
+  return FBM_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// host big-integer helpers (tiny, per call)
+// ---------------------------------------------------------------------------------------
+typedef std::vector<uint32_t> Big;  // little-endian 32-bit limbs
+
+static int big_bits(const Big& a) {
+  for (int i = (int)a.size() - 1; i >= 0; --i)
+    if (a[i]) return 32 * i + 32 - __builtin_clz(a[i]);
+  return 0;
+}
+
+static Big big_mul(const Big& a, const Big& b) {
+  Big r(a.size() + b.size(), 0u);
+  for (size_t i = 0; i < a.size(); ++i) {
+    uint64_t c = 0;
+    for (size_t j = 0; j < b.size(); ++j) {
+      const uint64_t t = (uint64_t)a[i] * b[j] + r[i + j] + c;
+      r[i + j] = (uint32_t)t;
+      c = t >> 32;
+    }
+    r[i + b.size()] = (uint32_t)c;
+  }
+  return r;
+}
+
+static int big_cmp(const Big& a, const Big& b) {
+  const size_t n = a.size() > b.size() ? a.size() : b.size();
+  for (size_t k = n; k-- > 0;) {
+    const uint32_t x = k < a.size() ? a[k] : 0u, y = k < b.size() ? b[k] : 0u;
+    if (x != y) return x > y ? 1 : -1;
+  }
+  return 0;
+}
+
+static void big_sub_inplace(Big& a, const Big& b) {  // a >= b
+  int64_t br = 0;
+  for (size_t k = 0; k < a.size(); ++k) {
+    const int64_t d = (int64_t)a[k] - (int64_t)(k < b.size() ? b[k] : 0u) + br;
+    a[k] = (uint32_t)d;
+    br = d < 0 ? -1 : 0;
+  }
+}
+
+// 2^e mod m by repeated doubling (m odd, > 1)
+static Big big_pow2_mod(int e, const Big& m) {
+  Big x(m.size() + 1, 0u);
+  x[0] = 1u;
+  for (int i = 0; i < e; ++i) {
+    uint32_t c = 0;
+    for (size_t k = 0; k < x.size(); ++k) {
+      const uint32_t nc = x[k] >> 31;
+      x[k] = (x[k] << 1) | c;
+      c = nc;
+    }
+    if (big_cmp(x, m) >= 0) big_sub_inplace(x, m);
+  }
+  return x;
+}
+
+static void to28_host(const Big& a, uint32_t* o, int nl) {
+  for (int k = 0; k < nl; ++k) {
+    const int bit = k * FBM_LB, wi = bit >> 5, sh = bit & 31;
+    const uint64_t lo = wi < (int)a.size() ? a[wi] : 0u;
+    const uint64_t hi = wi + 1 < (int)a.size() ? a[wi + 1] : 0u;
+    o[k] = (uint32_t)(((hi << 32) | lo) >> sh) & FBM_LMASK;
+  }
+}
+
+template <int NL>
+static void build_mont(const Big& m, MontCtxT<NL>& c) {
+  to28_host(m, c.M, NL);
+  const Big R2 = big_pow2_mod(2 * NL * FBM_LB, m);
+  to28_host(R2, c.R2, NL);
+  uint32_t inv = m[0];  // Newton: inv = m^-1 mod 2^32
+  for (int i = 0; i < 5; ++i) inv *= 2u - m[0] * inv;
+  c.mp = (0u - inv) & FBM_LMASK;
+}
+
+static int build_jl_params(const uint32_t* biprime, int es, int cr, uint64_t tau, JlParams& jp) {
+  memset(&jp, 0, sizeof(jp));
+  Big N(biprime, biprime + 32);
+  const int nb = big_bits(N);
+  if (nb < 2 || (N[0] & 1u) == 0u) {
+    set_error("biprime must be odd and >= 3 (device Montgomery path); got %d bits, %s", nb,
+              (N[0] & 1u) ? "odd" : "even");
+    return FBM_E_UNSUPPORTED;
+  }
+  if (es < 1 || cr < 1 || es > 100 || (int64_t)es * cr > 1024) {
+    set_error("invalid VES parameters es=%d cr=%d", es, cr);
+    return FBM_E_ARG;
+  }
+  Big M = big_mul(N, N);  // 64 limbs
+  while (M.size() > 64) M.pop_back();
+  build_mont<FBM_NL>(M, jp.mc);
+  build_mont<FBM_NLN>(N, jp.mn);
+  for (int i = 0; i < 32; ++i) jp.N32[i] = biprime[i];
+  jp.n_bits = nb;
+  jp.es = es;
+  jp.cr = cr;
+  jp.tau = tau;
+  // SHA-256 midstate over the 14 leading all-zero blocks of t.to_bytes(1024,'big')
+  uint32_t st[8], W[16];
+  fbm_sha256_init(st);
+  memset(W, 0, sizeof(W));
+  for (int b = 0; b < 14; ++b) fbm_sha256_compress(st, W);
+  memcpy(jp.mid, st, sizeof(st));
+  return FBM_OK;
+}
+
+// Left-to-right sliding window (width FBM_WIN) over |key|, odd-power table.
+static int build_schedule(const uint32_t* key, JlSched& sc, int& is_zero) {
+  memset(&sc, 0, sizeof(sc));
+  Big K(key, key + 64);
+  const int nb = big_bits(K);
+  is_zero = nb == 0;
+  if (is_zero) return FBM_OK;
+  auto bit = [&](int i) -> int { return (K[i >> 5] >> (i & 31)) & 1; };
+  int i = nb - 1;
+  int pending_sq = 0;
+  bool first = true;
+  while (i >= 0) {
+    if (!bit(i)) {
+      ++pending_sq;
+      --i;
+      continue;
+    }
+    int l = i - FBM_WIN + 1;
+    if (l < 0) l = 0;
+    while (!bit(l)) ++l;
+    int val = 0;
+    for (int j = i; j >= l; --j) val = (val << 1) | bit(j);
+    const int width = i - l + 1;
+    const int idx = (val - 1) / 2;
+    if (first) {
+      sc.first = idx;
+      first = false;
+    } else {
+      int nsq = pending_sq + width;
+      while (nsq > 2047) {
+        if (sc.n_ops >= FBM_MAX_OPS) return FBM_E_ARG;
+        sc.op[sc.n_ops++] = (uint16_t)(2047 << 5);
+        nsq -= 2047;
+      }
+      if (sc.n_ops >= FBM_MAX_OPS) return FBM_E_ARG;
+      sc.op[sc.n_ops++] = (uint16_t)((nsq << 5) | (idx + 1));
+    }
+    pending_sq = 0;
+    i = l - 1;
+  }
+  while (pending_sq > 0) {
+    const int nsq = pending_sq > 2047 ? 2047 : pending_sq;
+    if (sc.n_ops >= FBM_MAX_OPS) return FBM_E_ARG;
+    sc.op[sc.n_ops++] = (uint16_t)(nsq << 5);
+    pending_sq -= nsq;
+  }
+  return FBM_OK;
+}
+
+static uint64_t table_slots_for(uint64_t n_ct) {
+  const uint64_t cap = jl_table_slots();
+  uint64_t g = ((n_ct + 255) / 256) * 256;
+  return g < cap ? g : cap;
+}
+
+static uint64_t align256(uint64_t v) { return (v + 255) & ~255ull; }
+
+static void fill_peers(LomPeers& pe, const uint8_t* nonce, uint64_t tau) {
+  memset(&pe, 0, sizeof(pe));
+  uint32_t iv[4];
+  memcpy(iv, nonce, 16);
+  pe.ctr0 = (uint64_t)iv[0] | ((uint64_t)iv[1] << 32);
+  pe.n14 = iv[2];
+  pe.n15 = iv[3];
+  pe.tau = tau;
+  uint8_t tb[16] = {0};
+  for (int b = 0; b < 8; ++b) tb[15 - b] = (uint8_t)(tau >> (8 * b));
+  memcpy(pe.tau_be, tb, 16);
+}
+
+}  // namespace fbm
+
+using namespace fbm;
+
+extern "C" {
+
+int fbm_abi_version(void) { return FBM_ABI_VERSION; }
+
+const char* fbm_last_error(void) { return g_err; }
+
+int fbm_check_stats(const uint32_t* st, int lom_nodes, uint32_t* max_bits_out) {
+  if (!st) return FBM_E_ARG;
+  if (max_bits_out) *max_bits_out = st[FBM_STAT_MAXBITS];
+  const uint32_t f = st[FBM_STAT_ERRFLAGS];
+  if (f & FBM_ERR_FDH_OVERFLOW) {
+    set_error("FDH: more than 8 digests without gcd(r, N^2) == 1 (reference: OverflowError)");
+    return FBM_E_FDH;
+  }
+  if (f & FBM_ERR_NOT_INVERTIBLE) {
+    set_error("invert() no inverse exists");
+    return FBM_E_INVERSE;
+  }
+  if (f & FBM_ERR_ITER_CAP) {
+    set_error("bounded device loop hit its iteration cap");
+    return FBM_E_ITER;
+  }
+  if (f & FBM_ERR_DEQUANT_RANGE) {
+    set_error("Cannot reverse quantize, received values exceed maximum number");
+    return FBM_E_RANGE;
+  }
+  if (lom_nodes > 0) {
+    int node_bits = 0;
+    while ((1ll << node_bits) < (long long)lom_nodes) ++node_bits;  // ceil(log2(P))
+    if ((int)st[FBM_STAT_MAXBITS] >= 64 - node_bits) {
+      set_error("Secure aggregation overflow detected: values need %u bits, %d available", st[FBM_STAT_MAXBITS],
+                64 - node_bits);
+      return FBM_E_OVERFLOW;
+    }
+  }
+  return FBM_OK;
+}
+
+int fbm_lom_protect(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
+                    uint64_t target_m1, uint64_t weight, const uint8_t* secrets, const int8_t* signs, int n_peers,
+                    int raw_seeds, const uint8_t* nonce, uint64_t tau, uint64_t* y, uint32_t* stats, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc = zero_stats(stats, s);
+  if (rc) return rc;
+  QuantParams qp;
+  if ((rc = quant_params(clip, two_clip, target_f, target_m1, qp))) return rc;
+  if (x_dtype != FBM_F32 && x_dtype != FBM_F64 && x_dtype != FBM_U64) {
+    set_error("x_dtype must be FBM_F32, FBM_F64 or FBM_U64");
+    return FBM_E_ARG;
+  }
+  if (n_peers < 0 || n_peers > FBM_MAX_PEERS) {
+    set_error("n_peers=%d outside [0, %d]", n_peers, FBM_MAX_PEERS);
+    return FBM_E_UNSUPPORTED;
+  }
+  if ((n > 0 && ((!x && x_dtype != FBM_U64) || !y)) || !nonce || (n_peers > 0 && (!secrets || !signs))) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  // PRF.eval_vector guard (_lom.py:74-78) and (i + tau).to_bytes(8) range
+  if (n + 1000ull > (1ull << 61) || (n > 0 && tau > ~0ull - (n - 1))) {
+    set_error("Can not perform encryiton due to large input vector");
+    return FBM_E_ARG;
+  }
+  LomPeers pe;
+  fill_peers(pe, nonce, tau);
+  pe.n_peers = n_peers;
+  pe.raw_seeds = raw_seeds;
+  for (int p = 0; p < n_peers; ++p) {
+    memcpy(pe.secret[p], secrets + 32 * p, 32);
+    pe.sign[p] = signs[p] >= 0 ? 1 : -1;
+  }
+  return launch_lom_protect(x, x_dtype, n, qp, weight, pe, y, stats, s);
+}
+
+int fbm_prf_key(const uint8_t* secret, const uint8_t* nonce, uint64_t tau, uint8_t* seed_out, void* stream) {
+  if (!secret || !nonce || !seed_out) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  LomPeers pe;
+  fill_peers(pe, nonce, tau);
+  pe.n_peers = 1;
+  memcpy(pe.secret[0], secret, 32);
+  return launch_prf_key(pe, (uint32_t*)seed_out, (hipStream_t)stream);
+}
+
+int fbm_dequantize(const uint64_t* u, uint64_t n, double neg_clip, double step, double* out, void* stream) {
+  if (n > 0 && (!u || !out)) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  return launch_dequantize(u, n, neg_clip, step, out, (hipStream_t)stream);
+}
+
+int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t total_weight, double neg_clip,
+                      double step, double* out, uint64_t* sums, uint32_t* stats, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc = zero_stats(stats, s);
+  if (rc) return rc;
+  if (n_parties < 1 || total_weight == 0 || (n > 0 && !y)) {
+    set_error("invalid aggregate arguments (n_parties=%d, total_weight=%llu)", n_parties,
+              (unsigned long long)total_weight);
+    return FBM_E_ARG;
+  }
+  return launch_lom_aggregate(y, n_parties, n, total_weight, neg_clip, step, out, sums, stats, s);
+}
+
+// encrypt workspace: ops | pt [n_ct][32] | nude (blocked) | H [n_ct][64] | table
+uint64_t fbm_jl_encrypt_workspace(uint64_t n_ct) {
+  const uint64_t slots = table_slots_for(n_ct);
+  return align256(FBM_MAX_OPS * 4) + align256(n_ct * 32 * 4) + align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4) + align256(n_ct * 64 * 4) +
+         align256(slots * FBM_TABLE * FBM_NL * 4);
+}
+
+// aggregate workspace: ops | X (blocked) | H [n_ct][64] | E [n_ct][64] | inv [n_ct][64] | xs [n_ct][32] | table
+uint64_t fbm_jl_aggregate_workspace(uint64_t n_ct) {
+  const uint64_t slots = table_slots_for(n_ct);
+  return align256(FBM_MAX_OPS * 4) + align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4) + 3 * align256(n_ct * 64 * 4) + align256(n_ct * 32 * 4) +
+         align256(slots * FBM_TABLE * FBM_NL * 4);
+}
+
+int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
+                   uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime, const uint32_t* key,
+                   int key_negative, uint64_t tau, uint32_t* ct_out, void* workspace, uint32_t* stats,
+                   void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc = zero_stats(stats, s);
+  if (rc) return rc;
+  QuantParams qp;
+  if ((rc = quant_params(clip, two_clip, target_f, target_m1, qp))) return rc;
+  if (x_dtype != FBM_F32 && x_dtype != FBM_F64) {
+    set_error("x_dtype must be FBM_F32 or FBM_F64");
+    return FBM_E_ARG;
+  }
+  if (!biprime || !key) {
+    set_error("null biprime/key");
+    return FBM_E_ARG;
+  }
+  if (key_negative) {
+    set_error("negative user keys are not supported by the device encrypt path");
+    return FBM_E_UNSUPPORTED;
+  }
+  if (n == 0) return FBM_OK;
+  if (cr < 1) {
+    set_error("invalid cr=%d", cr);
+    return FBM_E_ARG;
+  }
+  const uint64_t n_ct = (n + (uint64_t)cr - 1) / (uint64_t)cr;
+  if (!x || !ct_out || !workspace) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  JlParams jp;
+  if ((rc = build_jl_params(biprime, es, cr, tau, jp))) return rc;
+  JlSched sc;
+  int is_zero = 0;
+  if ((rc = build_schedule(key, sc, is_zero))) {
+    set_error("exponent schedule overflow");
+    return rc;
+  }
+  jp.key_is_zero = is_zero;
+  const uint64_t slots = table_slots_for(n_ct);
+  uint8_t* ws = (uint8_t*)workspace;
+  uint32_t* ops = (uint32_t*)ws;
+  uint64_t off = align256(FBM_MAX_OPS * 4);
+  uint32_t* pt = (uint32_t*)(ws + off);
+  off += align256(n_ct * 32 * 4);
+  uint32_t* nude = (uint32_t*)(ws + off);
+  off += align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4);
+  uint32_t* H = (uint32_t*)(ws + off);
+  off += align256(n_ct * 64 * 4);
+  uint32_t* table = (uint32_t*)(ws + off);
+  if ((rc = launch_jl_pack(x, x_dtype, n, qp, weight, es, cr, n_ct, pt, s))) return rc;
+  if ((rc = launch_jl_nude(pt, n_ct, jp, nude, s))) return rc;
+  if (!is_zero && (rc = launch_jl_fdh(n_ct, jp, H, stats, s))) return rc;
+  return launch_jl_exp(H, n_ct, jp, sc, 0, nude, table, slots, ops, ct_out, s);
+}
+
+int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,
+                     const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau,
+                     uint64_t total_weight, double neg_clip, double step, double* out, uint64_t* sums,
+                     void* workspace, uint32_t* stats, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc = zero_stats(stats, s);
+  if (rc) return rc;
+  if (n_parties < 1 || !biprime || !key || total_weight == 0) {
+    set_error("invalid aggregate arguments");
+    return FBM_E_ARG;
+  }
+  if (n_ct == 0) return FBM_OK;
+  if (n_out > n_ct * (uint64_t)cr) n_out = n_ct * (uint64_t)cr;
+  if (!cts || !workspace) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  JlParams jp;
+  if ((rc = build_jl_params(biprime, es, cr, tau, jp))) return rc;
+  JlSched sc;
+  int is_zero = 0;
+  if ((rc = build_schedule(key, sc, is_zero))) {
+    set_error("exponent schedule overflow");
+    return rc;
+  }
+  jp.key_is_zero = is_zero;
+  const uint64_t slots = table_slots_for(n_ct);
+  uint8_t* ws = (uint8_t*)workspace;
+  uint32_t* ops = (uint32_t*)ws;
+  uint64_t off = align256(FBM_MAX_OPS * 4);
+  uint32_t* X = (uint32_t*)(ws + off);
+  off += align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4);
+  uint32_t* H = (uint32_t*)(ws + off);
+  off += align256(n_ct * 64 * 4);
+  uint32_t* E = (uint32_t*)(ws + off);
+  off += align256(n_ct * 64 * 4);
+  uint32_t* inv = (uint32_t*)(ws + off);
+  off += align256(n_ct * 64 * 4);
+  uint32_t* xs = (uint32_t*)(ws + off);
+  off += align256(n_ct * 32 * 4);
+  uint32_t* table = (uint32_t*)(ws + off);
+  if ((rc = launch_jl_prod(cts, n_parties, n_ct, jp, X, s))) return rc;
+  if (!is_zero && (rc = launch_jl_fdh(n_ct, jp, H, stats, s))) return rc;
+  if ((rc = launch_jl_exp(H, n_ct, jp, sc, 1, nullptr, table, slots, ops, E, s))) return rc;
+  if (key_negative && !is_zero) {
+    if ((rc = launch_jl_inv(n_ct, jp, E, xs, inv, stats, s))) return rc;  // xs doubles as y scratch
+  } else {
+    inv = E;  // positive (or zero) server key: v = prod * H^sk0, no inverse
+  }
+  if ((rc = launch_jl_fin(n_ct, jp, X, inv, xs, s))) return rc;
+  return launch_jl_decode(xs, es, cr, n_out, total_weight, neg_clip, step, out, sums, stats, s);
+}
+
+}  // extern "C"

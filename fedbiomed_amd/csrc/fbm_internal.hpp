@@ -1,0 +1,87 @@
+// fedbiomed_amd -- internal declarations shared by the kernel files and the C-ABI.
+#pragma once
+#include "fbm_common.hpp"
+#include "fbm_mont.hpp"
+#include "../../include/fbm_secagg.h"
+
+#define FBM_MAX_PEERS 64
+
+// stats words written by kernels (device u32[4], zeroed by the C-ABI before a launch)
+#define FBM_STAT_MAXBITS 0   // max bit length of q*w (LOM overflow guard, _lom.py:133-150)
+#define FBM_STAT_ERRFLAGS 1  // OR of FBM_ERR_* flags
+#define FBM_STAT_COUNT 4
+
+#define FBM_ERR_DEQUANT_RANGE 1u   // averaged value > 2^64-1 (reverse_quantize FB624)
+#define FBM_ERR_FDH_OVERFLOW 2u    // > 8 non-coprime FDH digests (reference: OverflowError)
+#define FBM_ERR_NOT_INVERTIBLE 4u  // server-key power not invertible mod N^2
+#define FBM_ERR_ITER_CAP 8u        // a bounded data-dependent loop hit its cap
+
+namespace fbm {
+
+struct LomPeers {
+  int n_peers;
+  int raw_seeds;                 // 1: secret[] already are the per-round seeds (PRF.eval_vector)
+  uint64_t ctr0;                 // nonce bytes 0-7 (LE) = 64-bit ChaCha20 block counter
+  uint32_t n14, n15;             // nonce bytes 8-15 (LE words)
+  uint64_t tau;                  // round
+  uint32_t tau_be[4];            // tau.to_bytes(16, 'big') as LE words
+  uint32_t secret[FBM_MAX_PEERS][8];
+  int8_t sign[FBM_MAX_PEERS];    // +1: mask += vec (peer < node), -1: mask -= vec
+};
+
+int check_launch(const char* what);
+void set_error(const char* fmt, ...);
+
+int launch_lom_protect(const void* x, int x_dtype, uint64_t n, const QuantParams& qp, uint64_t weight,
+                       const LomPeers& peers, uint64_t* y, uint32_t* stats, hipStream_t s);
+int launch_dequantize(const uint64_t* u, uint64_t n, double neg_c, double step, double* out, hipStream_t s);
+int launch_prf_key(const LomPeers& peers, uint32_t* seed_out, hipStream_t s);
+int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t total_weight, double neg_c,
+                         double step, double* out, uint64_t* sums, uint32_t* stats, hipStream_t s);
+
+// ---- Joye-Libert -------------------------------------------------------------------
+// exponent schedule (host-computed sliding window, uniform across lanes)
+#define FBM_WIN 5
+#define FBM_TABLE (1 << (FBM_WIN - 1))  // odd powers h^1, h^3, ..., h^31
+#define FBM_MAX_OPS 512
+
+// sliding-window schedule, passed by value (kernarg segment -> scalar loads).
+// op k (u16): (squarings before the multiply) << 5 | (table index + 1, 0 = none)
+struct JlSched {
+  int n_ops;
+  int first;       // table index of the leading window
+  uint16_t op[FBM_MAX_OPS];
+};
+
+struct JlParams {
+  MontCtx mc;                    // modulus M = N^2 (74 limbs)
+  MontCtxN mn;                   // modulus N (37 limbs) -- inverse mod N, N*pt
+  uint32_t N32[32];              // N, 32-bit limbs (<= 1024 bits)
+  int n_bits;                    // bit length of N
+  int es, cr;                    // VES slot size / slots per ciphertext
+  uint64_t tau;
+  uint32_t mid[8];               // SHA-256 state after the 14 all-zero message blocks
+  int key_is_zero;
+  int pad;
+};
+
+int launch_jl_pack(const void* x, int x_dtype, uint64_t n, const QuantParams& qp, uint64_t weight, int es, int cr,
+                   uint64_t n_ct, uint32_t* pt, hipStream_t s);
+int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, uint32_t* nude, hipStream_t s);
+int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s);
+int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const JlSched& sc, int mode,
+                  const uint32_t* nude, uint32_t* table, uint64_t table_slots, uint32_t* ops, uint32_t* out,
+                  hipStream_t s);
+int launch_jl_prod(const uint32_t* cts, int n_parties, uint64_t n_ct, const JlParams& jp, uint32_t* X,
+                   hipStream_t s);
+int launch_jl_inv(uint64_t n_ct, const JlParams& jp, const uint32_t* E, uint32_t* Y, uint32_t* inv, uint32_t* stats,
+                  hipStream_t s);
+int launch_jl_fin(uint64_t n_ct, const JlParams& jp, const uint32_t* X, const uint32_t* inv, uint32_t* xout,
+                  hipStream_t s);
+int launch_jl_decode(const uint32_t* xs, int es, int cr, uint64_t n_out, uint64_t total_weight, double neg_c,
+                     double step, double* out, uint64_t* sums, uint32_t* stats, hipStream_t s);
+
+// table slots the encrypt/aggregate kernels need for a given grid
+uint64_t jl_table_slots();
+
+}  // namespace fbm

@@ -1,0 +1,842 @@
+// fedbiomed_amd -- Joye-Libert kernels for gfx950.
+//
+// Encrypt (one party):  pack -> nude -> fdh -> exp(ENC)
+//   jl_pack_kernel   quantize + weight + VES.encode     (_secagg_utils.py:82-119,
+//                    _secagg_crypter.py:252-276, _jls.py:118-144,169-176)
+//   jl_nude_kernel   (N*pt + 1) mod N^2                   (_jls.py:494-496)
+//   jl_fdh_kernel    FDH.H(t_k), t_k = (k<<512)|tau       (_jls.py:451-467,727-762)
+//   jl_exp_kernel    H^sk mod N^2 (GMP mpz_powm via gmpy2, _jls.py:60-73,500-501) and
+//                    the final product with nude           (_jls.py:502)
+// Aggregate:  prod -> fdh -> exp(DEC) -> inv -> fin -> decode
+//   jl_prod_kernel   prod_u c_u mod N^2                    (_jls.py:353-374,691-693)
+//   jl_exp_kernel    H^|sk0| mod N^2                       (_jls.py:550-551)
+//   jl_inv_kernel    (H^|sk0|)^-1 mod N^2 (gmpy2.powmod with b<0 inverts; _jls.py:550-551)
+//   jl_fin_kernel    v = prod * inv mod N^2, x = ((v-1)//N) mod N   (_jls.py:553-558)
+//   jl_decode_kernel VES.decode + _apply_average + reverse_quantize
+//                    (_jls.py:146-192, _secagg_crypter.py:233-249, _secagg_utils.py:152-187)
+//
+// HBM layouts: 32-bit-limb integers are row-major [ct][words] (pt: 32 words, H / E / inv /
+// ciphertexts: 64 words = int.to_bytes(256,'little')); 28-bit-limb residues (nude, X) and
+// the per-lane exponent tables are limb-major [limb][lane] so a wave's accesses coalesce.
+#include "fbm_internal.hpp"
+
+namespace fbm {
+
+#define FBM_BLOCK 256
+
+// ------------------------------------------------------------------------------------
+// pack: one work-item per 32-bit limb of a packed plaintext
+// ------------------------------------------------------------------------------------
+// XT = float/double: quantise (crypter path);  XT = uint64_t: raw integers (JoyeLibert.protect)
+template <typename XT>
+__device__ __forceinline__ uint64_t jl_input(const XT* x, uint64_t i, const QuantParams& qp) {
+  return fbm_quantize((double)x[i], qp);
+}
+template <>
+__device__ __forceinline__ uint64_t jl_input<uint64_t>(const uint64_t* x, uint64_t i, const QuantParams&) {
+  return x[i];
+}
+
+template <typename XT>
+__global__ void __launch_bounds__(256) jl_pack_kernel(const XT* __restrict__ x, uint64_t n, QuantParams qp,
+                                                      uint64_t weight, int es, int cr, uint64_t n_ct,
+                                                      uint32_t* __restrict__ pt) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t ct = gid >> 5;
+  const int L = (int)(gid & 31);
+  if (ct >= n_ct) return;
+  const uint64_t first = ct * (uint64_t)cr;
+  const int cnt = (n - first) >= (uint64_t)cr ? cr : (int)(n - first);
+  const int lo_bit = 32 * L;
+  int j0 = lo_bit / es, j1 = (lo_bit + 31) / es;
+  if (j1 > cnt - 1) j1 = cnt - 1;
+  uint32_t w = 0;
+  for (int j = j0; j <= j1; ++j) {
+    const uint64_t q = jl_input<XT>(x, first + j, qp);
+    const unsigned __int128 v = (unsigned __int128)q * weight;
+    const int sh = es * j - lo_bit;
+    w |= sh >= 0 ? (uint32_t)(v << sh) : (uint32_t)(v >> (-sh));
+  }
+  pt[ct * 32 + L] = w;
+}
+
+// ------------------------------------------------------------------------------------
+// nude = N*pt + 1  (< 2^2048; the reduction mod N^2 happens in the final Montgomery
+// product, which accepts any a < R)  ->  [limb][ct] 28-bit limbs
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) jl_nude_kernel(const uint32_t* __restrict__ pt, uint64_t n_ct, JlParams jp,
+                                                      uint32_t* __restrict__ nude) {
+  const uint64_t ct = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ct >= n_ct) return;
+  uint32_t p32[32];
+  const uint4* src = reinterpret_cast<const uint4*>(pt + ct * 32);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint4 v = src[i];
+    p32[4 * i] = v.x; p32[4 * i + 1] = v.y; p32[4 * i + 2] = v.z; p32[4 * i + 3] = v.w;
+  }
+  uint32_t p28[FBM_NLN];
+  to28<32, FBM_NLN>(p32, p28);
+  uint64_t col[FBM_NL];
+#pragma unroll
+  for (int k = 0; k < FBM_NL; ++k) col[k] = 0;
+#pragma unroll
+  for (int i = 0; i < FBM_NLN; ++i) {
+#pragma unroll
+    for (int j = 0; j < FBM_NLN; ++j) col[i + j] += (uint64_t)jp.mn.M[i] * p28[j];
+  }
+  col[0] += 1;
+  uint64_t carry = 0;
+  uint32_t o[FBM_NL];
+#pragma unroll
+  for (int k = 0; k < FBM_NL; ++k) {
+    const uint64_t v = col[k] + carry;
+    o[k] = (uint32_t)v & FBM_LMASK;
+    carry = v >> FBM_LB;
+  }
+  col_store(nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255), o);
+}
+
+// ------------------------------------------------------------------------------------
+// FDH
+// ------------------------------------------------------------------------------------
+// gcd(u, N) == 1 for u < 2^2048 (64 limbs), N odd (<= 1024 bits).  Binary GCD, bounded.
+__device__ bool gcd_is_one(uint32_t (&u)[64], const uint32_t* N32, uint32_t& err) {
+  uint32_t v[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) v[i] = i < 32 ? N32[i] : 0u;
+  uint32_t any = 0;
+#pragma unroll
+  for (int i = 0; i < 64; ++i) any |= u[i];
+  if (any) {
+    int it = 0;
+    for (; it < 20000; ++it) {
+      // strip factors of two from u (N is odd, so they never divide the gcd)
+      while (u[0] == 0u) {
+#pragma unroll
+        for (int i = 0; i < 63; ++i) u[i] = u[i + 1];
+        u[63] = 0u;
+      }
+      const int s = __builtin_ctz(u[0]);
+      if (s) {
+#pragma unroll
+        for (int i = 0; i < 63; ++i) u[i] = (u[i] >> s) | (u[i + 1] << (32 - s));
+        u[63] >>= s;
+      }
+      int cmp = 0;
+#pragma unroll
+      for (int i = 63; i >= 0; --i)
+        if (cmp == 0) cmp = (u[i] > v[i]) - (u[i] < v[i]);
+      if (cmp == 0) break;
+      if (cmp < 0) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          const uint32_t t = u[i];
+          u[i] = v[i];
+          v[i] = t;
+        }
+      }
+      uint32_t br = 0;  // u -= v (u > v, both odd: result even and nonzero)
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const uint64_t d = (uint64_t)u[i] - v[i] - br;
+        u[i] = (uint32_t)d;
+        br = (uint32_t)(d >> 63);
+      }
+    }
+    if (it >= 20000) err |= FBM_ERR_ITER_CAP;
+  }
+  uint32_t rest = 0;
+#pragma unroll
+  for (int i = 1; i < 64; ++i) rest |= v[i];
+  return v[0] == 1u && rest == 0;
+}
+
+// FDH.H(t_k): message = t.to_bytes(1024,'big') || counter (1 byte).  Blocks 0..13 are
+// all zero for k < 2^64 (midstate from the host), block 14 carries k, block 15 tau,
+// block 16 the counter byte + padding (length 8200 bits).  While gcd(r, N^2) != 1 the
+// counter is bumped and r grows by one digest (r = D1 || D2 || ...); more than 8 digests
+// is the reference's OverflowError.
+__global__ void __launch_bounds__(256) jl_fdh_kernel(uint64_t n_ct, JlParams jp, uint32_t* __restrict__ H,
+                                                     uint32_t* __restrict__ stats) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_ct) return;
+  uint32_t err = 0;
+  uint32_t st[8], W[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) st[i] = jp.mid[i];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) W[i] = 0u;
+  W[14] = (uint32_t)(k >> 32);
+  W[15] = (uint32_t)k;
+  fbm_sha256_compress(st, W);
+  W[14] = (uint32_t)(jp.tau >> 32);
+  W[15] = (uint32_t)jp.tau;
+  fbm_sha256_compress(st, W);
+  uint32_t r[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) r[i] = 0u;
+  bool ok = false;
+  for (uint32_t c = 1; c <= 8 && !ok; ++c) {
+    uint32_t d[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = st[i];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) W[i] = 0u;
+    W[0] = (c << 24) | (0x80u << 16);
+    W[15] = 8200u;
+    fbm_sha256_compress(d, W);
+#pragma unroll
+    for (int i = 63; i >= 8; --i) r[i] = r[i - 8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = d[7 - i];
+    uint32_t u[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) u[i] = r[i];
+    ok = gcd_is_one(u, jp.N32, err);
+  }
+  if (!ok) err |= FBM_ERR_FDH_OVERFLOW;
+  uint4* o = reinterpret_cast<uint4*>(H + k * 64);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) o[i] = make_uint4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
+  if (err) atomicOr(stats + FBM_STAT_ERRFLAGS, err);
+}
+
+// ------------------------------------------------------------------------------------
+// exponentiation engine
+// ------------------------------------------------------------------------------------
+// per-lane exponent table: workgroup-blocked, entry e / limb k at tb[(e * NL + k) * 256]
+__device__ __forceinline__ void tbl_store(uint32_t* tb, int e, const uint32_t (&v)[FBM_NL]) {
+  col_store(tb + e * (FBM_NL * 256), v);
+}
+__device__ __forceinline__ void tbl_load(const uint32_t* tb, int e, uint32_t (&v)[FBM_NL]) {
+  col_load(tb + e * (FBM_NL * 256), v);
+}
+__device__ __forceinline__ void load_row64(const uint32_t* p, uint32_t (&w)[64]) {
+  const uint4* s = reinterpret_cast<const uint4*>(launder_v(p));
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint4 v = s[i];
+    w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+  }
+}
+__device__ __forceinline__ void store_row64(uint32_t* p, const uint32_t (&w)[64]) {
+  uint4* o = reinterpret_cast<uint4*>(launder_v(p));
+#pragma unroll
+  for (int i = 0; i < 16; ++i) o[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+// mode 0 (ENC): out[ct] = nude[ct] * H[ct]^key  mod N^2          (ciphertext)
+// mode 1 (DEC): out[ct] = H[ct]^key mod N^2 (plain)                (for the inverse)
+//
+// Sliding window (width FBM_WIN) over a host-built schedule: uniform control flow.
+// The kernel is ONE loop around ONE Montgomery product (~90 KB of fully unrolled code).
+// No residue is carried in registers across iterations: the running value lives in the
+// per-lane LDS column (the A operand of the next product) and each iteration re-loads its
+// B operand (from that column for a squaring, from the per-lane table for a multiply).
+// That keeps the product's 146 + 74 live VGPRs the kernel's peak (2 waves/SIMD).
+//   phase 0  to Montgomery:  a = R^2 (uniform)   b = h          -> table[0], LDS
+//   phase 1  h^2:            a = h*R             b = h*R        -> LDS (multiplier)
+//   phase 2  odd powers:     a = h^2             b = table[t-1] -> table[t]
+//   phase 3  window steps:   a = acc             b = acc | table[idx] -> LDS
+//   phase 4  final:          a = nude | 1        b = acc        -> out (fully reduced)
+__global__ void __launch_bounds__(FBM_BLOCK, 1) jl_exp_kernel(const uint32_t* __restrict__ H, uint64_t n_ct,
+                                                             JlParams jp, const uint32_t* __restrict__ ops,
+                                                             int n_ops, int first, int mode,
+                                                             const uint32_t* __restrict__ nude,
+                                                             uint32_t* __restrict__ table,
+                                                             uint32_t* __restrict__ out) {
+  __shared__ uint32_t lds_a[FBM_NL * FBM_BLOCK];
+  const int tid = threadIdx.x;
+  uint32_t* lds = lds_a + tid;
+  const int ls = FBM_BLOCK;
+  const uint64_t G = (uint64_t)gridDim.x * FBM_BLOCK;
+  const uint64_t gtid = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
+  uint32_t* tb = table + (uint64_t)blockIdx.x * (FBM_TABLE * FBM_NL * FBM_BLOCK) + tid;
+
+  // Uniform round loop (every lane runs the same number of rounds; lanes past the end
+  // redo the last ciphertext and skip the store): all control flow below is wave-uniform,
+  // so the phase machine compiles to scalar branches and no exec-masked merge keeps two
+  // copies of the residue alive.
+  const uint64_t rounds = (n_ct + G - 1) / G;
+  for (uint64_t r = 0; r < rounds; ++r) {
+    const uint64_t ct_raw = gtid + r * G;
+    const bool valid = ct_raw < n_ct;
+    const uint64_t ct = valid ? ct_raw : n_ct - 1;
+    int phase = 0, t = 0, k = 0, s = 0;
+#pragma unroll 1
+    for (;;) {
+      // opaque state: keeps the optimiser from threading the phase machine through the
+      // loop (which would clone the product once per phase)
+      phase = __builtin_amdgcn_readfirstlane(phase);
+      t = __builtin_amdgcn_readfirstlane(t);
+      k = __builtin_amdgcn_readfirstlane(k);
+      s = __builtin_amdgcn_readfirstlane(s);
+      asm volatile("" : "+s"(phase), "+s"(t), "+s"(k), "+s"(s));
+      uint32_t acc[FBM_NL];
+      // ---- stage B (and A where it changes) ----
+      bool mul = false;
+      int idx = -1;
+      if (phase == 3) {
+        const uint32_t op = __builtin_amdgcn_readfirstlane(ops[k]);
+        mul = s >= (int)(op >> 5);
+        idx = (int)(op & 31u) - 1;
+      }
+      if (phase == 0) {
+        uint32_t h[64];
+        if (jp.key_is_zero) {
+#pragma unroll
+          for (int i = 0; i < 64; ++i) h[i] = i == 0 ? 1u : 0u;
+        } else {
+          load_row64(H + ct * 64, h);
+        }
+        to28<64, FBM_NL>(h, acc);
+        lds_store_uniform<FBM_NL>(lds, ls, jp.mc.R2);
+      } else if (phase == 2) {
+        tbl_load(tb, t - 1, acc);
+      } else if (phase == 3 && mul) {
+        tbl_load(tb, idx, acc);
+      } else {  // squaring (phase 1, 3) or final (phase 4): b = running value
+        lds_load_col(lds, ls, acc);
+        if (phase == 4) {
+          if (mode == 0) {
+            uint32_t nv[FBM_NL];
+            col_load(nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255), nv);
+            lds_store_col(lds, ls, nv);
+          } else {
+            lds_store_one<FBM_NL>(lds, ls);
+          }
+        }
+      }
+      mont_mul(acc, lds, ls, jp.mc);
+      // ---- consume the result ----
+      if (phase == 4) {
+        mont_csub(acc, jp.mc.M);
+        uint32_t w[64];
+        from28<FBM_NL, 64>(acc, w);
+        if (valid) store_row64(out + ct * 64, w);
+        break;
+      }
+      if (phase == 0) {
+        lds_store_col(lds, ls, acc);
+        if (jp.key_is_zero) {
+          phase = 4;
+        } else {
+          tbl_store(tb, 0, acc);
+          phase = 1;
+        }
+      } else if (phase == 1) {
+        lds_store_col(lds, ls, acc);  // h^2 becomes the multiplier of phase 2
+        phase = 2;
+        t = 1;
+      } else if (phase == 2) {
+        tbl_store(tb, t, acc);
+        if (++t == FBM_TABLE) {
+          uint32_t v[FBM_NL];
+          tbl_load(tb, first, v);
+          lds_store_col(lds, ls, v);
+          phase = n_ops > 0 ? 3 : 4;
+          k = 0;
+          s = 0;
+        }
+      } else {  // phase 3
+        lds_store_col(lds, ls, acc);
+        if (mul) {
+          ++k;
+          s = 0;
+        } else {
+          ++s;
+          const uint32_t op = __builtin_amdgcn_readfirstlane(ops[k]);
+          if (s == (int)(op >> 5) && idx < 0) {
+            ++k;
+            s = 0;
+          }
+        }
+        if (k == n_ops) phase = 4;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// aggregate: product of the P ciphertexts, X = prod_u c_u * R  (Montgomery form, lazy)
+// Each c_u (any value < 2^2048) is first brought into the Montgomery domain with R^2.
+//   step 2u   : a = R^2,    b = c_u  -> c_u*R   (u = 0: X; else staged in LDS)
+//   step 2u+1 : a = c_u*R,  b = X    -> X      (u >= 1)
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(FBM_BLOCK, 1) jl_prod_kernel(const uint32_t* __restrict__ cts, int n_parties,
+                                                              uint64_t n_ct, JlParams jp,
+                                                              uint32_t* __restrict__ X) {
+  __shared__ uint32_t lds_a[FBM_NL * FBM_BLOCK];
+  const int tid = threadIdx.x;
+  uint32_t* lds = lds_a + tid;
+  const int ls = FBM_BLOCK;
+  const uint64_t ct_raw = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
+  const bool valid = ct_raw < n_ct;  // no early return: keep control flow wave-uniform
+  const uint64_t ct = valid ? ct_raw : n_ct - 1;
+  uint32_t* xp = X + (ct_raw >> 8) * (FBM_NL * 256) + (ct_raw & 255);  // X is padded to whole blocks
+  const int steps = 2 * n_parties - 1;
+#pragma unroll 1
+  for (int st = 0; st < steps; ++st) {
+    st = __builtin_amdgcn_readfirstlane(st);
+    asm volatile("" : "+s"(st));
+    uint32_t acc[FBM_NL];
+    const bool tomont = (st & 1) == 0;
+    if (tomont) {
+      uint32_t c32[64];
+      load_row64(cts + ((uint64_t)(st >> 1) * n_ct + ct) * 64, c32);
+      to28<64, FBM_NL>(c32, acc);
+      lds_store_uniform<FBM_NL>(lds, ls, jp.mc.R2);
+    } else {
+      col_load(xp, acc);
+    }
+    mont_mul(acc, lds, ls, jp.mc);
+    if (st == 0 || !tomont) col_store(xp, acc);
+    else lds_store_col(lds, ls, acc);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// inverse mod N^2 by Hensel lifting: y = e^-1 mod N (1024-bit binary extended Euclid),
+// inv = y * (2 - e*y) mod N^2.   e = H^|sk0| mod N^2 (plain).
+// ------------------------------------------------------------------------------------
+template <int W>
+__device__ __forceinline__ void shr1(uint32_t (&a)[W], uint32_t top) {
+#pragma unroll
+  for (int i = 0; i < W - 1; ++i) a[i] = (a[i] >> 1) | (a[i + 1] << 31);
+  a[W - 1] = (a[W - 1] >> 1) | (top << 31);
+}
+template <int W>
+__device__ __forceinline__ uint32_t add_into(uint32_t (&a)[W], const uint32_t* b) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const uint64_t s = (uint64_t)a[i] + b[i] + c;
+    a[i] = (uint32_t)s;
+    c = (uint32_t)(s >> 32);
+  }
+  return c;
+}
+template <int W>
+__device__ __forceinline__ uint32_t sub_from(uint32_t (&a)[W], const uint32_t (&b)[W]) {
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const uint64_t d = (uint64_t)a[i] - b[i] - br;
+    a[i] = (uint32_t)d;
+    br = (uint32_t)(d >> 63);
+  }
+  return br;
+}
+
+// stage 1: y = (E mod N)^-1 mod N   -> Y [ct][32]
+__global__ void __launch_bounds__(FBM_BLOCK, 1) jl_inv_modn_kernel(uint64_t n_ct, JlParams jp,
+                                                                  const uint32_t* __restrict__ E,
+                                                                  uint32_t* __restrict__ Y,
+                                                                  uint32_t* __restrict__ stats) {
+  __shared__ uint32_t lds_a[FBM_NL * FBM_BLOCK];
+  const int tid = threadIdx.x;
+  uint32_t* lds = lds_a + tid;
+  const int ls = FBM_BLOCK;
+  const uint64_t ct = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
+  if (ct >= n_ct) return;
+  uint32_t err = 0;
+
+  // --- e mod N = (e_hi * R_N + e_lo) mod N  with R_N = 2^1036 --------------------------
+  //   s0: a = R2N, b = hi       -> t1 = hi*R_N mod N     (lazy, < 2N)
+  //   s1: a = R2N, b = t1 + lo  -> x*R_N
+  //   s2: a = 1,   b = x*R_N    -> x mod N
+  uint32_t y28[FBM_NLN];
+  {
+    uint32_t e32[64];
+    load_row64(E + ct * 64, e32);
+    uint32_t e28[FBM_NL];
+    to28<64, FBM_NL>(e32, e28);
+    uint32_t lo[FBM_NLN];
+#pragma unroll
+    for (int k = 0; k < FBM_NLN; ++k) {
+      lo[k] = e28[k];
+      y28[k] = e28[k + FBM_NLN];
+    }
+    lds_store_uniform<FBM_NLN>(lds, ls, jp.mn.R2);
+    mont_mul(y28, lds, ls, jp.mn);  // hi * R_N mod N
+    {
+      uint32_t c = 0;
+#pragma unroll
+      for (int k = 0; k < FBM_NLN; ++k) {
+        const uint32_t v = y28[k] + lo[k] + c;
+        y28[k] = v & FBM_LMASK;
+        c = v >> FBM_LB;
+      }
+    }
+    mont_mul(y28, lds, ls, jp.mn);  // x * R_N mod N
+    lds_store_one<FBM_NLN>(lds, ls);
+    mont_mul(y28, lds, ls, jp.mn);  // x mod N
+    mont_csub(y28, jp.mn.M);
+  }
+  // --- y = (e mod N)^-1 mod N : binary extended Euclid on 32-bit limbs ------------------
+  uint32_t x1[32];
+  {
+    uint32_t u[32], v[32], x2[32];
+    from28<FBM_NLN, 32>(y28, u);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      v[i] = jp.N32[i];
+      x1[i] = i == 0 ? 1u : 0u;
+      x2[i] = 0u;
+    }
+    uint32_t any = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) any |= u[i];
+    bool ok = any != 0;
+    int it = 0;
+    for (; ok && it < 20000; ++it) {
+      uint32_t u1 = u[0] ^ 1u, v1 = v[0] ^ 1u;
+#pragma unroll
+      for (int i = 1; i < 32; ++i) {
+        u1 |= u[i];
+        v1 |= v[i];
+      }
+      if (u1 == 0u) break;  // u == 1 -> x1
+      if (v1 == 0u) {       // v == 1 -> x2
+#pragma unroll
+        for (int i = 0; i < 32; ++i) x1[i] = x2[i];
+        break;
+      }
+      if ((u[0] & 1u) == 0u) {
+        shr1<32>(u, 0u);
+        const uint32_t c = (x1[0] & 1u) ? add_into<32>(x1, jp.N32) : 0u;
+        shr1<32>(x1, c);
+        continue;
+      }
+      if ((v[0] & 1u) == 0u) {
+        shr1<32>(v, 0u);
+        const uint32_t c = (x2[0] & 1u) ? add_into<32>(x2, jp.N32) : 0u;
+        shr1<32>(x2, c);
+        continue;
+      }
+      int cmp = 0;
+#pragma unroll
+      for (int i = 31; i >= 0; --i)
+        if (cmp == 0) cmp = (u[i] > v[i]) - (u[i] < v[i]);
+      if (cmp == 0) {  // gcd != 1
+        ok = false;
+        break;
+      }
+      if (cmp > 0) {
+        sub_from<32>(u, v);
+        if (sub_from<32>(x1, x2)) add_into<32>(x1, jp.N32);
+      } else {
+        sub_from<32>(v, u);
+        if (sub_from<32>(x2, x1)) add_into<32>(x2, jp.N32);
+      }
+    }
+    if (it >= 20000) err |= FBM_ERR_ITER_CAP;
+    if (!ok) err |= FBM_ERR_NOT_INVERTIBLE;
+  }
+  uint4* yo = reinterpret_cast<uint4*>(Y + ct * 32);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) yo[i] = make_uint4(x1[4 * i], x1[4 * i + 1], x1[4 * i + 2], x1[4 * i + 3]);
+  if (err) atomicOr(stats + FBM_STAT_ERRFLAGS, err);
+}
+
+// stage 2 (Hensel lift): inv = y * (2 - E*y) mod N^2   -> inv [ct][64]
+__global__ void __launch_bounds__(FBM_BLOCK, 1) jl_inv_lift_kernel(uint64_t n_ct, JlParams jp,
+                                                                  const uint32_t* __restrict__ E,
+                                                                  const uint32_t* __restrict__ Y,
+                                                                  uint32_t* __restrict__ inv) {
+  __shared__ uint32_t lds_a[FBM_NL * FBM_BLOCK];
+  const int tid = threadIdx.x;
+  uint32_t* lds = lds_a + tid;
+  const int ls = FBM_BLOCK;
+  const uint64_t ct = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
+  if (ct >= n_ct) return;
+  uint32_t x1[32];
+  {
+    const uint4* yi = reinterpret_cast<const uint4*>(Y + ct * 32);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint4 v = yi[i];
+      x1[4 * i] = v.x; x1[4 * i + 1] = v.y; x1[4 * i + 2] = v.z; x1[4 * i + 3] = v.w;
+    }
+  }
+  // --- Hensel: inv = y * (2 - e*y) mod N^2 ------------------------------------------------
+  //   s0: a = y,  b = e  -> e*y/R      s1: a = R^2, b -> z = e*y      (w = 2 - z mod M)
+  //   s2: a = y,  b = w  -> y*w/R      s3: a = R^2, b -> y*w = inv
+  uint32_t acc[FBM_NL];
+  {
+    uint32_t e32[64];
+    load_row64(E + ct * 64, e32);
+    to28<64, FBM_NL>(e32, acc);
+  }
+  {
+    uint32_t x64[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) x64[i] = i < 32 ? x1[i] : 0u;
+    uint32_t y[FBM_NL];
+    to28<64, FBM_NL>(x64, y);
+    lds_store_col(lds, ls, y);
+  }
+#pragma unroll 1
+  for (int st = 0; st < 4; ++st) {
+    mont_mul(acc, lds, ls, jp.mc);
+    if (st == 0 || st == 2) {
+      lds_store_uniform<FBM_NL>(lds, ls, jp.mc.R2);
+    } else if (st == 1) {
+      mont_csub(acc, jp.mc.M);  // z < M
+      int32_t br = 0;           // w = 2 - z mod M   (M > 2)
+#pragma unroll
+      for (int k = 0; k < FBM_NL; ++k) {
+        const int32_t v = (int32_t)(k == 0 ? 2u : 0u) - (int32_t)acc[k] + br;
+        acc[k] = (uint32_t)v & FBM_LMASK;
+        br = v >> FBM_LB;
+      }
+      if (br) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int k = 0; k < FBM_NL; ++k) {
+          const uint32_t v = acc[k] + jp.mc.M[k] + c;
+          acc[k] = v & FBM_LMASK;
+          c = v >> FBM_LB;
+        }
+      }
+      uint32_t x64[64];
+#pragma unroll
+      for (int i = 0; i < 64; ++i) x64[i] = i < 32 ? x1[i] : 0u;
+      uint32_t y[FBM_NL];
+      to28<64, FBM_NL>(x64, y);
+      lds_store_col(lds, ls, y);
+    }
+  }
+  mont_csub(acc, jp.mc.M);
+  uint32_t w[64];
+  from28<FBM_NL, 64>(acc, w);
+  store_row64(inv + ct * 64, w);
+}
+
+// ------------------------------------------------------------------------------------
+// v = X * inv (plain) ; x = floor((v-1)/N)   (x < N, 32 words)
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(FBM_BLOCK, 1) jl_fin_kernel(uint64_t n_ct, JlParams jp,
+                                                             const uint32_t* __restrict__ X,
+                                                             const uint32_t* __restrict__ inv,
+                                                             uint32_t* __restrict__ xout) {
+  __shared__ uint32_t lds_a[FBM_NL * FBM_BLOCK];
+  const int tid = threadIdx.x;
+  const uint64_t ct = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
+  if (ct >= n_ct) return;
+  uint32_t* lds = lds_a + tid;
+  {
+    uint32_t xv[FBM_NL];
+    col_load(X + (ct >> 8) * (FBM_NL * 256) + (ct & 255), xv);
+    lds_store_col(lds, FBM_BLOCK, xv);
+  }
+  uint32_t acc[FBM_NL];
+  {
+    uint32_t i32[64];
+    load_row64(inv + ct * 64, i32);
+    to28<64, FBM_NL>(i32, acc);
+  }
+  mont_mul(acc, lds, FBM_BLOCK, jp.mc);  // (prod*R) * inv * R^-1 = prod * inv mod M
+  mont_csub(acc, jp.mc.M);
+  uint32_t D[64];
+  from28<FBM_NL, 64>(acc, D);
+  {  // D = v - 1  (v >= 1 for any unit)
+    uint32_t br = 1;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      const uint64_t d = (uint64_t)D[i] - br;
+      D[i] = (uint32_t)d;
+      br = (uint32_t)(d >> 63);
+    }
+  }
+  // binary long division by N; quotient q (< N), remainder r
+  uint32_t q[32], r[33];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) q[i] = 0u;
+#pragma unroll
+  for (int i = 0; i < 33; ++i) r[i] = 0u;
+  int top = 0;
+#pragma unroll
+  for (int i = 0; i < 64; ++i)
+    if (D[i]) top = i;
+  const int nbits = 32 * (top + 1);
+#pragma unroll 1
+  for (int s = top; s < 63; ++s) {  // left-align the significant words
+#pragma unroll
+    for (int i = 63; i > 0; --i) D[i] = D[i - 1];
+    D[0] = 0u;
+  }
+#pragma unroll 1
+  for (int b = 0; b < nbits; ++b) {
+    const uint32_t bit = D[63] >> 31;
+#pragma unroll
+    for (int i = 63; i > 0; --i) D[i] = (D[i] << 1) | (D[i - 1] >> 31);
+    D[0] <<= 1;
+#pragma unroll
+    for (int i = 32; i > 0; --i) r[i] = (r[i] << 1) | (r[i - 1] >> 31);
+    r[0] = (r[0] << 1) | bit;
+#pragma unroll
+    for (int i = 31; i > 0; --i) q[i] = (q[i] << 1) | (q[i - 1] >> 31);
+    q[0] <<= 1;
+    uint32_t t[33];
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 33; ++i) {
+      const uint64_t d = (uint64_t)r[i] - (i < 32 ? jp.N32[i] : 0u) - br;
+      t[i] = (uint32_t)d;
+      br = (uint32_t)(d >> 63);
+    }
+    if (!br) {
+#pragma unroll
+      for (int i = 0; i < 33; ++i) r[i] = t[i];
+      q[0] |= 1u;
+    }
+  }
+  uint4* o = reinterpret_cast<uint4*>(xout + ct * 32);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = make_uint4(q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]);
+}
+
+// ------------------------------------------------------------------------------------
+// decode + average + dequantise: one work-item per output element
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) jl_decode_kernel(const uint32_t* __restrict__ xs, int es, int cr,
+                                                        uint64_t n_out, uint64_t total_weight, double neg_c,
+                                                        double step, double* __restrict__ out,
+                                                        uint64_t* __restrict__ sums, uint32_t* __restrict__ stats) {
+  const uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= n_out) return;
+  const uint64_t k = o / (uint64_t)cr;
+  const int j = (int)(o - k * (uint64_t)cr);
+  const int bit = es * j;
+  const uint32_t* x = xs + k * 32;
+  unsigned __int128 v = 0;
+  const int w0 = bit >> 5, sh = bit & 31;
+#pragma unroll
+  for (int t = 0; t < 5; ++t) {
+    const int w = w0 + t;
+    const uint32_t word = (w < 32) ? x[w] : 0u;
+    const int pos = 32 * t - sh;
+    if (pos >= 0) {
+      if (pos < 128) v |= (unsigned __int128)word << pos;
+    } else {
+      v |= (unsigned __int128)(word >> (-pos));
+    }
+  }
+  if (es < 128) v &= (((unsigned __int128)1) << es) - 1;
+  if (sums) {
+    sums[2 * o] = (uint64_t)v;
+    sums[2 * o + 1] = (uint64_t)(v >> 64);
+  }
+  const double a = fbm_true_div_u128(v, total_weight);
+  if (a >= 18446744073709551616.0) {
+    atomicOr(stats + FBM_STAT_ERRFLAGS, FBM_ERR_DEQUANT_RANGE);
+    if (out) out[o] = 0.0;
+    return;
+  }
+  if (out) out[o] = fbm_dequantize(a, neg_c, step);
+}
+
+// ------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------
+static int g_num_cu = 0;
+
+uint64_t jl_table_slots() {
+  if (!g_num_cu) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      g_num_cu = prop.multiProcessorCount;
+    if (g_num_cu <= 0) g_num_cu = 256;
+  }
+  // one workgroup of FBM_BLOCK lanes per CU (one wave per SIMD: the product needs
+  // ~250 VGPRs + AGPR spill space at this stage of tuning)
+  return (uint64_t)g_num_cu * FBM_BLOCK;
+}
+
+static inline dim3 grid1(uint64_t items, unsigned block) { return dim3((unsigned)((items + block - 1) / block)); }
+
+int launch_jl_pack(const void* x, int x_dtype, uint64_t n, const QuantParams& qp, uint64_t weight, int es, int cr,
+                   uint64_t n_ct, uint32_t* pt, hipStream_t s) {
+  if (n_ct == 0) return FBM_OK;
+  if (x_dtype == FBM_F32)
+    hipLaunchKernelGGL(jl_pack_kernel<float>, grid1(n_ct * 32, 256), dim3(256), 0, s, (const float*)x, n, qp, weight,
+                       es, cr, n_ct, pt);
+  else if (x_dtype == FBM_F64)
+    hipLaunchKernelGGL(jl_pack_kernel<double>, grid1(n_ct * 32, 256), dim3(256), 0, s, (const double*)x, n, qp,
+                       weight, es, cr, n_ct, pt);
+  else
+    hipLaunchKernelGGL(jl_pack_kernel<uint64_t>, grid1(n_ct * 32, 256), dim3(256), 0, s, (const uint64_t*)x, n, qp,
+                       weight, es, cr, n_ct, pt);
+  return check_launch("jl_pack_kernel");
+}
+
+int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, uint32_t* nude, hipStream_t s) {
+  if (n_ct == 0) return FBM_OK;
+  hipLaunchKernelGGL(jl_nude_kernel, grid1(n_ct, 256), dim3(256), 0, s, pt, n_ct, jp, nude);
+  return check_launch("jl_nude_kernel");
+}
+
+int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s) {
+  if (n_ct == 0) return FBM_OK;
+  hipLaunchKernelGGL(jl_fdh_kernel, grid1(n_ct, 256), dim3(256), 0, s, n_ct, jp, H, stats);
+  return check_launch("jl_fdh_kernel");
+}
+
+// The schedule travels as a kernel argument (copied by the runtime at launch, so the
+// host struct may die immediately) and is spilled to device memory for the exp kernel,
+// which indexes it dynamically.
+__global__ void jl_sched_kernel(JlSched sc, uint32_t* __restrict__ ops) {
+  for (int i = threadIdx.x; i < sc.n_ops; i += blockDim.x) ops[i] = sc.op[i];
+}
+
+int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const JlSched& sc, int mode,
+                  const uint32_t* nude, uint32_t* table, uint64_t table_slots, uint32_t* ops, uint32_t* out,
+                  hipStream_t s) {
+  if (n_ct == 0) return FBM_OK;
+  hipLaunchKernelGGL(jl_sched_kernel, dim3(1), dim3(256), 0, s, sc, ops);
+  int rc = check_launch("jl_sched_kernel");
+  if (rc) return rc;
+  uint64_t g = (n_ct + FBM_BLOCK - 1) / FBM_BLOCK;
+  const uint64_t gmax = table_slots / FBM_BLOCK;
+  if (g > gmax) g = gmax;
+  hipLaunchKernelGGL(jl_exp_kernel, dim3((unsigned)g), dim3(FBM_BLOCK), 0, s, H, n_ct, jp, (const uint32_t*)ops,
+                     sc.n_ops, sc.first, mode, nude, table, out);
+  return check_launch("jl_exp_kernel");
+}
+
+int launch_jl_prod(const uint32_t* cts, int n_parties, uint64_t n_ct, const JlParams& jp, uint32_t* X,
+                   hipStream_t s) {
+  if (n_ct == 0) return FBM_OK;
+  hipLaunchKernelGGL(jl_prod_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, cts, n_parties, n_ct, jp, X);
+  return check_launch("jl_prod_kernel");
+}
+
+int launch_jl_inv(uint64_t n_ct, const JlParams& jp, const uint32_t* E, uint32_t* Y, uint32_t* inv, uint32_t* stats,
+                  hipStream_t s) {
+  if (n_ct == 0) return FBM_OK;
+  hipLaunchKernelGGL(jl_inv_modn_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, E, Y, stats);
+  int rc = check_launch("jl_inv_modn_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(jl_inv_lift_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, E, Y, inv);
+  return check_launch("jl_inv_lift_kernel");
+}
+
+int launch_jl_fin(uint64_t n_ct, const JlParams& jp, const uint32_t* X, const uint32_t* inv, uint32_t* xout,
+                  hipStream_t s) {
+  if (n_ct == 0) return FBM_OK;
+  hipLaunchKernelGGL(jl_fin_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, X, inv, xout);
+  return check_launch("jl_fin_kernel");
+}
+
+int launch_jl_decode(const uint32_t* xs, int es, int cr, uint64_t n_out, uint64_t total_weight, double neg_c,
+                     double step, double* out, uint64_t* sums, uint32_t* stats, hipStream_t s) {
+  if (n_out == 0) return FBM_OK;
+  hipLaunchKernelGGL(jl_decode_kernel, grid1(n_out, 256), dim3(256), 0, s, xs, es, cr, n_out, total_weight, neg_c,
+                     step, out, sums, stats);
+  return check_launch("jl_decode_kernel");
+}
+
+}  // namespace fbm

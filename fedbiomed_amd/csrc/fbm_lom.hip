@@ -1,0 +1,218 @@
+// fedbiomed_amd -- LOM (Low-Overhead Masking) kernels for gfx950.
+//
+//   lom_protect_kernel   = quantize (utils/_secagg_utils.py:82-119)
+//                        + weighting (secagg/_secagg_crypter.py:252-276, :367-373)
+//                        + PRF.eval_key per peer (secagg/_lom.py:30-56)
+//                        + PRF.eval_vector + signed mask sum + add (secagg/_lom.py:58-83, :152-175)
+//   lom_aggregate_kernel = LOM.aggregate u64 column sum (secagg/_lom.py:177-192)
+//                        + _apply_average (secagg/_secagg_crypter.py:233-249)
+//                        + reverse_quantize (utils/_secagg_utils.py:152-187)
+//
+// Layout in HBM: x (f32 or f64, n), y (u64, n) per party; aggregate input is a
+// P x n row-major u64 matrix (party-major) -> out f64 n (+ optional u64 sums).
+#include "fbm_internal.hpp"
+
+namespace fbm {
+
+// One work-item = one ChaCha20 block = 8 consecutive elements (64 B of keystream per
+// peer).  Peers are looped inside (uniform control flow); their 32-byte secrets arrive
+// as kernel arguments and their per-round seeds (eval_key, one ChaCha20 block each) are
+// derived once per workgroup into LDS.
+// XT = float/double: quantise + weight (crypter path); XT = uint64_t: raw integer input
+// (LOM.protect on a list of ints), x == nullptr means an all-zero input.
+template <typename XT>
+__device__ __forceinline__ uint64_t lom_input(const XT* x, uint64_t i, const QuantParams& qp) {
+  return fbm_quantize((double)x[i], qp);
+}
+template <>
+__device__ __forceinline__ uint64_t lom_input<uint64_t>(const uint64_t* x, uint64_t i, const QuantParams&) {
+  return x ? x[i] : 0ull;
+}
+
+template <typename XT>
+__global__ void __launch_bounds__(256) lom_protect_kernel(const XT* __restrict__ x, uint64_t n, QuantParams qp,
+                                                          uint64_t weight, LomPeers peers,
+                                                          uint64_t* __restrict__ y, uint32_t* __restrict__ stats) {
+  __shared__ uint32_t seeds[FBM_MAX_PEERS][8];
+  const int tid = threadIdx.x;
+  if (tid < peers.n_peers && peers.raw_seeds) {
+#pragma unroll
+    for (int w = 0; w < 8; ++w) seeds[tid][w] = peers.secret[tid][w];
+  } else if (tid < peers.n_peers) {
+    // PRF.eval_key: ChaCha20(secret, nonce) over tau.to_bytes(16,'big'), first 16 bytes
+    // of keystream XOR tau_be16, padded with 16 zero bytes.
+    uint32_t ks[16];
+    fbm_chacha20_block(peers.secret[tid], peers.ctr0, peers.n14, peers.n15, ks);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) seeds[tid][w] = ks[w] ^ peers.tau_be[w];
+#pragma unroll
+    for (int w = 4; w < 8; ++w) seeds[tid][w] = 0u;
+  }
+  __syncthreads();
+
+  const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + tid;
+  const uint64_t base = blk * 8;
+  if (base >= n) return;
+  const int cnt = (n - base) >= 8 ? 8 : (int)(n - base);
+
+  // quantise + weight
+  uint64_t val[8];
+  uint32_t maxbits = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint64_t q = 0;
+    if (j < cnt) q = lom_input<XT>(x, base + j, qp);
+    const uint64_t lo = q * weight;
+    const uint64_t hi = __umul64hi(q, weight);
+    val[j] = lo;
+    const uint32_t bl = fbm_bitlen128(hi, lo);
+    maxbits = bl > maxbits ? bl : maxbits;
+  }
+
+  // masks
+  uint64_t mask[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) mask[j] = 0;
+  const uint64_t ctr = peers.ctr0 + blk;
+  for (int p = 0; p < peers.n_peers; ++p) {
+    uint32_t key[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) key[w] = seeds[p][w];
+    uint32_t ks[16];
+    fbm_chacha20_block(key, ctr, peers.n14, peers.n15, ks);
+    const bool add = peers.sign[p] > 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t idx = base + (uint64_t)j + peers.tau;
+      const uint64_t m = (((uint64_t)ks[2 * j + 1] << 32) | ks[2 * j]) ^ fbm_bswap64(idx);
+      mask[j] = add ? mask[j] + m : mask[j] - m;
+    }
+  }
+
+  if (cnt == 8) {
+    ulonglong2* yo = reinterpret_cast<ulonglong2*>(y + base);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) yo[j] = make_ulonglong2(mask[2 * j] + val[2 * j], mask[2 * j + 1] + val[2 * j + 1]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j < cnt) y[base + j] = mask[j] + val[j];
+  }
+
+  // wave-level max of the bit lengths, one atomic per wave
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t o = __shfl_xor(maxbits, off, 64);
+    maxbits = o > maxbits ? o : maxbits;
+  }
+  if ((tid & 63) == 0) atomicMax(stats + FBM_STAT_MAXBITS, maxbits);
+}
+
+// Column sum over P parties (mod 2^64) + Python-exact average + dequantise.
+// Two elements per work-item (16-B loads per party row), grid-stride.
+__global__ void __launch_bounds__(256) lom_aggregate_kernel(const uint64_t* __restrict__ y, int n_parties,
+                                                            uint64_t n, uint64_t total_weight, double neg_c,
+                                                            double step, double* __restrict__ out,
+                                                            uint64_t* __restrict__ sums, uint32_t* __restrict__ stats) {
+  const uint64_t npair = (n + 1) / 2;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const bool vec = (n & 1) == 0;  // rows start 16-B aligned only when n is even
+  uint32_t err = 0;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < npair; t += stride) {
+    const uint64_t i = 2 * t;
+    uint64_t s0 = 0, s1 = 0;
+    if (vec) {
+      for (int p = 0; p < n_parties; ++p) {
+        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(y + (uint64_t)p * n + i);
+        s0 += v.x;
+        s1 += v.y;
+      }
+    } else {
+      for (int p = 0; p < n_parties; ++p) {
+        s0 += y[(uint64_t)p * n + i];
+        if (i + 1 < n) s1 += y[(uint64_t)p * n + i + 1];
+      }
+    }
+    const double a0 = fbm_true_div_u128(s0, total_weight);
+    const double a1 = fbm_true_div_u128(s1, total_weight);
+    // reverse_quantize guard: value > 2^64-1 (float >= 2^64) -> FB624
+    err |= (a0 >= 18446744073709551616.0) ? 1u : 0u;
+    const double o0 = fbm_dequantize(a0 >= 18446744073709551616.0 ? 0.0 : a0, neg_c, step);
+    if (i + 1 < n) {
+      err |= (a1 >= 18446744073709551616.0) ? 1u : 0u;
+      const double o1 = fbm_dequantize(a1 >= 18446744073709551616.0 ? 0.0 : a1, neg_c, step);
+      if (vec) {
+        if (out) *reinterpret_cast<double2*>(out + i) = make_double2(o0, o1);
+        if (sums) *reinterpret_cast<ulonglong2*>(sums + i) = make_ulonglong2(s0, s1);
+      } else {
+        if (out) { out[i] = o0; out[i + 1] = o1; }
+        if (sums) { sums[i] = s0; sums[i + 1] = s1; }
+      }
+    } else {
+      if (out) out[i] = o0;
+      if (sums) sums[i] = s0;
+    }
+  }
+  if (err && out) atomicOr(stats + FBM_STAT_ERRFLAGS, FBM_ERR_DEQUANT_RANGE);
+}
+
+int launch_lom_protect(const void* x, int x_dtype, uint64_t n, const QuantParams& qp, uint64_t weight,
+                       const LomPeers& peers, uint64_t* y, uint32_t* stats, hipStream_t s) {
+  if (n == 0) return FBM_OK;
+  const uint64_t nblk = (n + 7) / 8;
+  const dim3 grid((unsigned)((nblk + 255) / 256)), block(256);
+  if (x_dtype == FBM_F32)
+    hipLaunchKernelGGL(lom_protect_kernel<float>, grid, block, 0, s, (const float*)x, n, qp, weight, peers, y, stats);
+  else if (x_dtype == FBM_F64)
+    hipLaunchKernelGGL(lom_protect_kernel<double>, grid, block, 0, s, (const double*)x, n, qp, weight, peers, y, stats);
+  else
+    hipLaunchKernelGGL(lom_protect_kernel<uint64_t>, grid, block, 0, s, (const uint64_t*)x, n, qp, weight, peers, y,
+                       stats);
+  return check_launch("lom_protect_kernel");
+}
+
+// reverse_quantize of already-truncated values: -c + step * double(u)  (numpy order, no FMA)
+__global__ void __launch_bounds__(256) dequantize_kernel(const uint64_t* __restrict__ u, uint64_t n, double neg_c,
+                                                         double step, double* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double du = (double)u[i];
+  const double prod = step * du;
+  out[i] = neg_c + prod;
+}
+
+int launch_dequantize(const uint64_t* u, uint64_t n, double neg_c, double step, double* out, hipStream_t s) {
+  if (n == 0) return FBM_OK;
+  hipLaunchKernelGGL(dequantize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, u, n, neg_c, step, out);
+  return check_launch("dequantize_kernel");
+}
+
+// PRF.eval_key for one (secret, nonce, tau): 32-byte seed to device memory
+__global__ void prf_key_kernel(LomPeers peers, uint32_t* __restrict__ seed_out) {
+  if (threadIdx.x != 0) return;
+  uint32_t ks[16];
+  fbm_chacha20_block(peers.secret[0], peers.ctr0, peers.n14, peers.n15, ks);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) seed_out[w] = ks[w] ^ peers.tau_be[w];
+#pragma unroll
+  for (int w = 4; w < 8; ++w) seed_out[w] = 0u;
+}
+
+int launch_prf_key(const LomPeers& peers, uint32_t* seed_out, hipStream_t s) {
+  hipLaunchKernelGGL(prf_key_kernel, dim3(1), dim3(64), 0, s, peers, seed_out);
+  return check_launch("prf_key_kernel");
+}
+
+int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t total_weight, double neg_c, double step,
+                         double* out, uint64_t* sums, uint32_t* stats, hipStream_t s) {
+  if (n == 0) return FBM_OK;
+  const uint64_t npair = (n + 1) / 2;
+  uint64_t g = (npair + 255) / 256;
+  const uint64_t gmax = 256ull * 8ull;  // 256 CUs x 8 workgroups, grid-stride beyond
+  if (g > gmax) g = gmax;
+  hipLaunchKernelGGL(lom_aggregate_kernel, dim3((unsigned)g), dim3(256), 0, s, y, n_parties, n, total_weight, neg_c,
+                     step, out, sums, stats);
+  return check_launch("lom_aggregate_kernel");
+}
+
+}  // namespace fbm

@@ -1,0 +1,253 @@
+"""Drop-in secure-aggregation crypters backed by the MI355X HIP kernels.
+
+Mirrors the reference boundary `fedbiomed/common/secagg/_secagg_crypter.py`:
+  SecaggCrypter.encrypt     (:45-137)   SecaggCrypter.aggregate     (:139-230)
+  SecaggLomCrypter.__init__ (:303-316)  SecaggLomCrypter.encrypt    (:318-392)
+  SecaggLomCrypter.aggregate(:394-455)  _apply_average (:233-249)   _apply_weighting (:252-276)
+Same signatures, same argument validation, same exceptions and messages; the arithmetic
+(quantise, weight, PRF masks / VES pack + FDH + 2048-bit modexp, sums, unmask, average,
+dequantise) runs on the GPU through `fedbiomed_amd._device` -> `include/fbm_secagg.h`.
+
+Besides the list API, `encrypt_tensor` / `aggregate_tensor` take device tensors directly
+(the fast path for callers that already hold the flattened model in HBM).
+"""
+
+from __future__ import annotations
+
+import logging
+import secrets
+import time
+from typing import Dict, List, Optional, Union
+
+import torch
+
+from .. import _device as D
+from ..constants import ErrorNumbers, SAParameters
+from ..exceptions import FedbiomedSecaggCrypterError
+
+logger = logging.getLogger("fedbiomed_amd")
+
+
+def _check_weight(weight: Optional[int], jl: bool) -> None:
+    if weight is None:
+        return
+    if 2 ** weight.bit_length() > SAParameters.WEIGHT_RANGE:
+        if jl:
+            raise FedbiomedSecaggCrypterError(
+                f"{ErrorNumbers.FB624.value}: The weight is too large. The weight should be less than "
+                f"{SAParameters.WEIGHT_RANGE}, but got {weight}")
+        raise FedbiomedSecaggCrypterError(
+            f"{ErrorNumbers.FB624.value}: The weight is too large. The weight should be less than "
+            f"{SAParameters.WEIGHT_RANGE}.")
+    if weight < 0:
+        raise FedbiomedSecaggCrypterError(
+            f"{ErrorNumbers.FB624.value}: Cannot apply weight to parameters, values outside of bounds")
+
+
+def _check_float_list(params) -> None:
+    if not isinstance(params, list):
+        raise FedbiomedSecaggCrypterError(
+            f"{ErrorNumbers.FB624.value}: Expected argument `params` type list but got {type(params)}")
+    if not all(isinstance(p, float) for p in params):
+        raise FedbiomedSecaggCrypterError(
+            f"{ErrorNumbers.FB624.value}: The parameters to encrypt should list of floats. "
+            f"There are one or more than a value that is not type of float.")
+
+
+def _check_int_lists(params) -> None:
+    if not isinstance(params, list) or not all(isinstance(p, list) for p in params):
+        raise FedbiomedSecaggCrypterError(
+            f"{ErrorNumbers.FB624.value}: The parameters to aggregate should be a "
+            f"list containing list of parameters")
+    if not all(all(isinstance(p_, int) for p_ in p) for p in params):
+        raise FedbiomedSecaggCrypterError(
+            f"{ErrorNumbers.FB624.value}: Invalid parameter type. The parameters "
+            f"should be of type of integers.")
+
+
+def _warn_clipping(x: torch.Tensor, clip) -> None:
+    """`_check_clipping_range` (utils/_secagg_utils.py:190-205): one warning if any |x| > c."""
+    c = SAParameters.CLIPPING_RANGE if clip is None else clip
+    if x.numel() and x.dtype != torch.int64 and bool(((x < -c) | (x > c)).any()):
+        logger.warning("There are some numbers in the local vector that exceeds clipping range. "
+                       "Please increase the clipping range to account for value")
+
+
+class SecaggCrypter:
+    """Joye-Libert secure aggregation (encrypt on nodes, aggregate on the researcher)."""
+
+    # ---- device fast path ------------------------------------------------------------------
+    def encrypt_tensor(self, num_nodes: int, current_round: int, params: torch.Tensor, key: int, biprime: int,
+                       clipping_range: Union[int, None] = None, weight: Optional[int] = None,
+                       target_range: Optional[int] = None) -> torch.Tensor:
+        """Device tensor (f32/f64) in HBM -> int32 [n_ct, 64] ciphertext limbs in HBM."""
+        if not isinstance(key, int):
+            raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: The argument `key` must be integer")
+        target_range = target_range or SAParameters.TARGET_RANGE
+        _check_weight(weight, jl=True)
+        _warn_clipping(params, clipping_range)
+        try:
+            return D.jl_encrypt(params, biprime, key, current_round, num_nodes, clip=clipping_range,
+                                target=target_range, weight=1 if weight is None else weight)
+        except (TypeError, ValueError) as exp:
+            raise FedbiomedSecaggCrypterError(
+                f"{ErrorNumbers.FB624.value} Error during parameter encryption. {exp}") from exp
+
+    def aggregate_tensor(self, current_round: int, cts: torch.Tensor, key: int, biprime: int,
+                         total_sample_size: int, clipping_range: Union[int, None] = None,
+                         num_expected_params: int = 1, target_range: Optional[int] = None,
+                         want_sums: bool = False):
+        """[P, n_ct, 64] int32 ciphertext limbs in HBM -> float64 [n] averaged parameters."""
+        if not isinstance(key, int):
+            raise TypeError("The key should be type of integer")
+        target_range = target_range or SAParameters.TARGET_RANGE
+        out, sums = D.jl_aggregate(cts, biprime, key, current_round, num_expected_params, total_sample_size,
+                                   clip=clipping_range, target=target_range, want_sums=want_sums)
+        return (out, sums) if want_sums else out
+
+    # ---- reference API -----------------------------------------------------------------------
+    def encrypt(self, num_nodes: int, current_round: int, params: List[float], key: int, biprime: int,
+                clipping_range: Union[int, None] = None, weight: Optional[int] = None,
+                target_range: Optional[int] = None) -> List[int]:
+        """Encrypts model parameters (reference `_secagg_crypter.py:45-137`)."""
+        start = time.process_time()
+        _check_float_list(params)
+        if not isinstance(key, int):
+            raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: The argument `key` must be integer")
+        target_range = target_range or SAParameters.TARGET_RANGE
+        D.quant_params(clipping_range, target_range)  # OverflowError / range checks as the reference
+        if not params:
+            return []
+        x = D.floats_to_device(params)
+        ct = self.encrypt_tensor(num_nodes, current_round, x, key, biprime, clipping_range, weight, target_range)
+        out = D.limbs_to_ints(ct.cpu().numpy())
+        logger.debug(f"Encryption of the parameters took {time.process_time() - start} seconds.")
+        return out
+
+    def aggregate(self, current_round: int, num_nodes: int, params: List[List[int]], key: int, biprime: int,
+                  total_sample_size: int, clipping_range: Union[int, None] = None, num_expected_params: int = 1,
+                  target_range: Optional[int] = None) -> List[float]:
+        """Decrypts the sum of the parties' ciphertexts (reference `_secagg_crypter.py:139-230`)."""
+        start = time.process_time()
+        if len(params) != num_nodes:
+            raise FedbiomedSecaggCrypterError(
+                f"{ErrorNumbers.FB624.value}: Num of parameters that are received from nodes "
+                f"does not match the number of nodes has been set for the encrypter. There might "
+                f"be some nodes did not answered to training request or num of clients of "
+                "`ParameterEncrypter` has not been set properly before train request.")
+        _check_int_lists(params)
+        if not isinstance(key, int):
+            raise TypeError("The key should be type of integer")
+        if not params:
+            raise FedbiomedSecaggCrypterError(
+                f"{ErrorNumbers.FB624.value}: The aggregation of encrypted parameters "
+                f"is not successful: list_y_u_tau should be a non-empty list.")
+        n2 = biprime * biprime
+        n_ct = min(len(p) for p in params)  # zip(*list_y_u_tau) truncates (_jls.py:691-693)
+        if n_ct == 0:
+            return []
+        import numpy as np
+
+        limbs = np.stack([D.ints_to_limbs(p[:n_ct], n2) for p in params])
+        dev = D.device()
+        cts = torch.from_numpy(limbs.view(np.int32)).to(dev)
+        out = self.aggregate_tensor(current_round, cts, key, biprime, total_sample_size, clipping_range,
+                                    num_expected_params, target_range)
+        logger.info(f"Aggregating {len(params)} parameters from {num_nodes} nodes.")
+        res = out.cpu().numpy().tolist()
+        logger.debug(f"Aggregation is completed in {round(time.process_time() - start, ndigits=2)} seconds.")
+        return res
+
+    @staticmethod
+    def _apply_average(params: List[int], total_weight: int) -> List:
+        """Reference `_secagg_crypter.py:233-249` (host helper, Python semantics)."""
+        if any(v < 0 for v in params):
+            raise FedbiomedSecaggCrypterError(
+                f"{ErrorNumbers.FB624.value}: Cannot compute weighted average, values outside of bounds")
+        return [e / total_weight for e in params]
+
+    @staticmethod
+    def _apply_weighting(params: List[int], weight: int, target_range: int = SAParameters.TARGET_RANGE) -> List[int]:
+        """Reference `_secagg_crypter.py:252-276` (host helper, Python semantics)."""
+        m = [e * weight for e in params]
+        max_val = target_range - 1
+        if any(v > max_val or v < 0 for v in params):
+            raise FedbiomedSecaggCrypterError(
+                f"{ErrorNumbers.FB624.value}: Cannot apply weight to parameters, values outside of bounds")
+        return m
+
+
+class SecaggLomCrypter(SecaggCrypter):
+    """Low-Overhead Masking secure aggregation (reference `_secagg_crypter.py:300-455`)."""
+
+    def __init__(self, nonce: Optional[str] = None):
+        if nonce:
+            nonce = str.encode(nonce).zfill(16)[:16]
+        self._nonce: bytes = nonce if nonce else secrets.token_bytes(16)
+
+    @property
+    def nonce(self) -> bytes:
+        return self._nonce
+
+    def encrypt_tensor(self, current_round: int, node_id: str, params: torch.Tensor,
+                       pairwise_secrets: Dict[str, bytes], node_ids: List[str],
+                       clipping_range: Union[int, None] = None, weight: Optional[int] = None,
+                       target_range: Optional[int] = None) -> torch.Tensor:
+        """Device tensor (f32/f64) -> masked uint64 vector (int64 tensor) in HBM."""
+        target_range = target_range or SAParameters.TARGET_RANGE
+        _check_weight(weight, jl=False)
+        _warn_clipping(params, clipping_range)
+        if params.numel() == 0:
+            raise FedbiomedSecaggCrypterError(
+                f"{ErrorNumbers.FB624.value} Error during parameter encryption. max() arg is an empty sequence")
+        peers = [p for p in node_ids if p != node_id]
+        secrets_ = [pairwise_secrets[p] for p in peers]
+        signs = [1 if p < node_id else -1 for p in peers]
+        if len(node_ids) == 0:
+            raise FedbiomedSecaggCrypterError(
+                f"{ErrorNumbers.FB624.value} Error during parameter encryption. math domain error")
+        return D.lom_protect(params, secrets_, signs, self._nonce, current_round, len(node_ids),
+                             clip=clipping_range, target=target_range, weight=1 if weight is None else weight)
+
+    def aggregate_tensor(self, Y: torch.Tensor, total_sample_size: int, clipping_range: Union[int, None] = None,
+                         target_range: Optional[int] = None, want_sums: bool = False):
+        """[P, n] masked vectors in HBM -> float64 [n] averaged parameters."""
+        out, sums = D.lom_aggregate(Y, total_sample_size, clipping_range, target_range or SAParameters.TARGET_RANGE,
+                                    want_sums=want_sums)
+        return (out, sums) if want_sums else out
+
+    def encrypt(self, current_round: int, node_id: str, params: List[float], pairwise_secrets: Dict[str, bytes],
+                node_ids: List[str], clipping_range: Union[int, None] = None, weight: Optional[int] = None,
+                target_range: Optional[int] = None) -> List[int]:
+        start = time.process_time()
+        _check_float_list(params)
+        target_range = target_range or SAParameters.TARGET_RANGE
+        D.quant_params(clipping_range, target_range)
+        if not params:
+            raise FedbiomedSecaggCrypterError(
+                f"{ErrorNumbers.FB624.value} Error during parameter encryption. max() arg is an empty sequence")
+        x = D.floats_to_device(params)
+        y = self.encrypt_tensor(current_round, node_id, x, pairwise_secrets, node_ids, clipping_range, weight,
+                                target_range)
+        out = D.u64_from_device(y)
+        logger.debug(f"Encryption of the parameters took {time.process_time() - start} seconds.")
+        return out
+
+    def aggregate(self, params: List[List[int]], total_sample_size: int, clipping_range: Union[int, None] = None,
+                  target_range: Optional[int] = None) -> List[float]:
+        start = time.process_time()
+        _check_int_lists(params)
+        num_nodes = len(params)
+        try:
+            Y = D.u64_to_device(params)
+        except (ValueError, TypeError) as e:
+            raise FedbiomedSecaggCrypterError(
+                f"{ErrorNumbers.FB624.value}: The aggregation of encrypted parameters "
+                f"is not successful: {e}") from e
+        if Y.dim() != 2 or Y.shape[1] == 0:
+            return []
+        out = self.aggregate_tensor(Y, total_sample_size, clipping_range, target_range)
+        logger.info(f"Aggregating {len(params)} parameters from {num_nodes} nodes.")
+        res = out.cpu().numpy().tolist()
+        logger.debug(f"Aggregation is completed in {round(time.process_time() - start, ndigits=2)} seconds.")
+        return res

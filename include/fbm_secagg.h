@@ -1,0 +1,129 @@
+/*
+ * fbm_secagg.h -- C ABI of the MI355X (gfx950) secure-aggregation crypter for Fed-BioMed.
+ *
+ * Drop-in boundary for the reference's Python crypter: these entry points are what the
+ * bodies of `SecaggCrypter.encrypt/aggregate` and `SecaggLomCrypter.encrypt/aggregate`
+ * (reference fedbiomed/common/secagg/_secagg_crypter.py:45,139,318,394) call, through
+ * ctypes, instead of the pure-Python / gmpy2 / OpenSSL implementation.  The Python host
+ * side (fedbiomed_amd/) keeps the reference's signatures, validation and exceptions.
+ *
+ * Conventions
+ *  - every compute entry point is ASYNCHRONOUS on `stream` (a hipStream_t, NULL = default
+ *    stream) and takes DEVICE pointers only; nothing is allocated inside the library.
+ *  - `stats` is a caller-provided device buffer of FBM_STATS_WORDS uint32; the library
+ *    zeroes it on `stream` and kernels record device-side conditions in it.  After the
+ *    stream is synchronised the caller reads it back and maps it with fbm_check_stats().
+ *  - big integers are little-endian arrays of uint32 limbs (== int.to_bytes(.., 'little')).
+ *  - return value: FBM_OK or a negative FBM_E_* code; fbm_last_error() has the message
+ *    (thread-local).
+ */
+#ifndef FBM_SECAGG_H
+#define FBM_SECAGG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FBM_ABI_VERSION 1
+
+#define FBM_OK 0
+#define FBM_E_ARG (-1)         /* bad argument (type/shape/range)            -> FB624      */
+#define FBM_E_HIP (-2)         /* HIP runtime / launch failure                             */
+#define FBM_E_RANGE (-3)       /* averaged value > 2^64-1 (reverse_quantize)  -> FB624      */
+#define FBM_E_OVERFLOW (-4)    /* LOM overflow guard (_lom.py:133-150)        -> FB417      */
+#define FBM_E_FDH (-5)         /* > 8 non-coprime FDH digests (_jls.py:742-760: OverflowError) */
+#define FBM_E_INVERSE (-6)     /* H^|sk0| not invertible mod N^2 (gmpy2: ZeroDivisionError) */
+#define FBM_E_ITER (-7)        /* a bounded data-dependent device loop hit its cap          */
+#define FBM_E_UNSUPPORTED (-8) /* parameters outside the device path's domain (documented)  */
+
+#define FBM_F32 0
+#define FBM_F64 1
+#define FBM_U64 2 /* raw integer input (LOM.protect / JoyeLibert.protect on ints); no quantisation */
+
+#define FBM_STATS_WORDS 4
+
+int fbm_abi_version(void);
+const char* fbm_last_error(void);
+
+/* Map a stats block (already copied to host) to a status code.
+ * lom_nodes > 0 applies the LOM overflow guard for that many nodes
+ * (error iff max_bits >= 64 - ceil(log2(lom_nodes))).  max_bits_out may be NULL. */
+int fbm_check_stats(const uint32_t* host_stats, int lom_nodes, uint32_t* max_bits_out);
+
+/* ---- quantisation parameters (reference fedbiomed/common/utils/_secagg_utils.py:82-119)
+ * clip      = float(c)          two_clip = float(2*c)
+ * target_f  = float(T)          target_m1 = T - 1   (T <= 2^64)
+ * weight    = multiplier applied after quantisation (1 = none), < 2^17            */
+
+/* LOM encrypt of one party: quantise -> *weight -> + sum of +/- ChaCha20 pairwise masks.
+ * Replaces SecaggLomCrypter.encrypt body (_secagg_crypter.py:318-392) = quantize +
+ * _apply_weighting + LOM.protect (_lom.py:105-175) incl. PRF.eval_key/eval_vector (:30-83).
+ *   x          device, n elements of dtype x_dtype (FBM_F32 / FBM_F64)
+ *   secrets    HOST, n_peers x 32 bytes: the pairwise secrets of the peers (node order)
+ *   signs      HOST, n_peers: +1 if peer_id < node_id (mask += PRF), -1 otherwise
+ *   raw_seeds  0: secrets are pairwise secrets (seed = PRF.eval_key per round);
+ *              1: secrets already are PRF seeds (PRF.eval_vector semantics)
+ *   nonce      HOST, 16 bytes (str.encode(nonce).zfill(16)[:16])
+ *   y          device, n uint64 (masked output)
+ * With x_dtype == FBM_U64, x holds integers used as-is (x == NULL: zeros) and only the
+ * weight multiplies them (weight 1 = LOM.protect semantics).                           */
+int fbm_lom_protect(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
+                    uint64_t target_m1, uint64_t weight, const uint8_t* secrets, const int8_t* signs, int n_peers,
+                    int raw_seeds, const uint8_t* nonce, uint64_t tau, uint64_t* y, uint32_t* stats, void* stream);
+
+/* PRF.eval_key (_lom.py:30-56): seed_out (device, 32 bytes) = ChaCha20(secret, nonce)
+ * keystream[0:16] XOR tau.to_bytes(16,'big') || 16 zero bytes.   secret, nonce: HOST.   */
+int fbm_prf_key(const uint8_t* secret, const uint8_t* nonce, uint64_t tau, uint8_t* seed_out, void* stream);
+
+/* reverse_quantize (utils/_secagg_utils.py:152-187) of values already truncated to
+ * uint64 (the reference's np.array(weights, dtype=uint64)): out = -c + step*double(u).   */
+int fbm_dequantize(const uint64_t* u, uint64_t n, double neg_clip, double step, double* out, void* stream);
+
+/* LOM aggregate: column sum mod 2^64 over n_parties rows, then the crypter's average and
+ * dequantisation.  Replaces SecaggLomCrypter.aggregate (_secagg_crypter.py:394-455) =
+ * LOM.aggregate (_lom.py:177-192) + _apply_average (:233-249) + reverse_quantize.
+ *   y      device, n_parties x n uint64 (row-major, party-major)
+ *   neg_clip = float(-c), step = (2c)/(T-1) as a Python float
+ *   out    device, n float64 (may be NULL); sums device, n uint64 (may be NULL)           */
+int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t total_weight, double neg_clip,
+                      double step, double* out, uint64_t* sums, uint32_t* stats, void* stream);
+
+/* ---- Joye-Libert (reference fedbiomed/common/secagg/_jls.py) -------------------------
+ * biprime: HOST, 32 limbs (N, odd, 3 <= N < 2^1024)
+ * key:     HOST, 64 limbs |sk| (< 2^2048);  key_negative: sign of sk
+ * es, cr:  VES slot bits / slots per ciphertext (JoyeLibert vector encoder, _jls.py:104-116)
+ * tau:     round (< 2^64); n_ct = ceil(n / cr)                                           */
+
+/* bytes of device workspace fbm_jl_encrypt / fbm_jl_aggregate need */
+uint64_t fbm_jl_encrypt_workspace(uint64_t n_ct);
+uint64_t fbm_jl_aggregate_workspace(uint64_t n_ct);
+
+/* JL encrypt of one party: quantise, weight, VES-pack, c_k = (N*pt_k+1) * H(t_k)^sk mod N^2.
+ * Replaces SecaggCrypter.encrypt (_secagg_crypter.py:45-137) = quantize + _apply_weighting +
+ * JoyeLibert.protect (_jls.py:593-644) + UserKey.encrypt (:473-505) + FDH.H (:727-762).
+ *   ct_out: device, n_ct x 64 uint32 limbs                                                */
+int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
+                   uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,
+                   const uint32_t* key, int key_negative, uint64_t tau, uint32_t* ct_out, void* workspace,
+                   uint32_t* stats, void* stream);
+
+/* JL aggregate: prod_u c_u * H(t_k)^sk0 mod N^2, x = ((v-1)//N) mod N, VES decode,
+ * average, dequantise.  Replaces SecaggCrypter.aggregate (_secagg_crypter.py:139-230) =
+ * JoyeLibert.aggregate (_jls.py:646-699) + ServerKey.decrypt (:520-562) + VES.decode +
+ * _apply_average + reverse_quantize.
+ *   cts:  device, n_parties x n_ct x 64 uint32 limbs (each < 2^2048)
+ *   n_out = number of decoded values (the reference's num_expected_params rule applied)
+ *   out:  device, n_out float64 (may be NULL)
+ *   sums: device, n_out x 2 uint64 (lo, hi) decoded integer sums (may be NULL)            */
+int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,
+                     const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau,
+                     uint64_t total_weight, double neg_clip, double step, double* out, uint64_t* sums,
+                     void* workspace, uint32_t* stats, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FBM_SECAGG_H */

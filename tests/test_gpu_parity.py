@@ -1,0 +1,268 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden vectors
+and the CPU oracle.  Bit-exact for every integer and float64 output (the reference's
+float results are themselves exact IEEE sequences; tolerance = 0 ulp)."""
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from tests.golden_util import F, I, fbits
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from fedbiomed_amd import _device as D
+
+    return D.device()
+
+
+def _bits(xs):
+    return [fbits(v) for v in xs]
+
+
+# ---------------------------------------------------------------- quantisation
+def test_quantize_golden(golden, dev):
+    from fedbiomed_amd.utils import quantize
+
+    for case in golden["quantize"]["quantize"]:
+        x = [F(v) for v in case["x"]]
+        got = quantize(x, case["clip"], I(case["target"]))
+        assert got == [I(v) for v in case["q"]], (case["clip"], case["target"])
+
+
+def test_reverse_quantize_golden(golden, dev):
+    from fedbiomed_amd.utils import reverse_quantize
+
+    for case in golden["quantize"]["reverse_quantize"]:
+        v = [F(x) for x in case["v"]] if "v" in case else [I(x) for x in case["v_int"]]
+        got = reverse_quantize(v, case["clip"], I(case["target"]))
+        assert _bits(got) == [s[2:] for s in case["out"]]
+
+
+def test_true_division_golden(golden, dev):
+    # average step e / W for e < 2^64 through the LOM aggregate kernel (one party, sums = e)
+    from fedbiomed_amd import _device as D
+
+    for case in golden["quantize"]["true_div"]:
+        e, w = I(case["e"]), I(case["w"])
+        if e >= 2**64:
+            continue
+        Y = D.u64_to_device([[e]], dev)
+        # out = -c + step * trunc(e/w): pick c, T so that out == trunc(e/w) exactly when it is small
+        out, _ = D.lom_aggregate(Y, w, clip=1, target=3)  # step = 2/2 = 1.0, -c = -1
+        q = F(case["q"])
+        if q < 2**53:
+            assert out.item() == -1.0 + float(int(q)), (e, w)
+
+
+def test_quantize_reference_tests(dev):
+    # reference tests/test_joye_libert.py:465-509
+    from fedbiomed_amd.utils import quantize
+
+    assert quantize([-10.0, -5.0, -1.5, 0.0, 2.5, 5.0, 10.0], 5, 10) == [0, 0, 3, 5, 7, 9, 9]
+    assert quantize([-4.0, -3.0, -1.0, 0.0, 3.0, 5.0], None, 5) == [0, 0, 1, 2, 4, 4]
+    assert quantize([-5.0, 0.0, 5.0], 5, 2**64) == [0, 2**63, 2**64 - 1]
+    with pytest.raises(OverflowError):
+        quantize([7.0], 7, 2**64 + 1)
+
+
+# ---------------------------------------------------------------- LOM
+def test_prf_golden(golden, dev):
+    from fedbiomed_amd.secagg import PRF
+
+    for case in golden["lom"]["prf"]:
+        prf = PRF(bytes.fromhex(case["nonce"]))
+        seed = prf.eval_key(bytes.fromhex(case["secret"]), case["tau"])
+        assert seed.hex() == case["seed"]
+        assert prf.eval_vector(seed, case["tau"], case["n"]).hex() == case["vector"]
+
+
+def test_lom_protect_golden(golden, dev):
+    from fedbiomed_amd import workload as W
+    from fedbiomed_amd.secagg import LOM
+
+    for case in golden["lom"]["protect"]:
+        nonce = bytes.fromhex(case["nonce"])
+        ids = case["ids"]
+        ys = []
+        for u in ids:
+            y = LOM(nonce).protect(u, W.pairwise_secrets_for(u, ids), case["tau"], [I(v) for v in case["x"][u]], ids)
+            assert y == [I(v) for v in case["y"][u]], u
+            ys.append(y)
+        assert LOM(nonce).aggregate(ys) == [I(v) for v in case["agg"]]
+
+
+def test_lom_crypter_golden(golden, dev):
+    from fedbiomed_amd import workload as W
+    from fedbiomed_amd.secagg import SecaggLomCrypter
+
+    for case in golden["lom"]["crypter"]:
+        ids = case["ids"]
+        target = I(case["target"]) if case["target"] else None
+        cr = SecaggLomCrypter(case["nonce_str"])
+        encs = []
+        for u in ids:
+            y = cr.encrypt(case["tau"], u, [F(v) for v in case["x"][u]], W.pairwise_secrets_for(u, ids), ids,
+                           clipping_range=case["clip"], weight=case["weights"][u], target_range=target)
+            assert y == [I(v) for v in case["enc"][u]], u
+            encs.append(y)
+        agg = cr.aggregate(encs, case["total"], clipping_range=case["clip"], target_range=target)
+        assert _bits(agg) == [s[2:] for s in case["agg"]]
+
+
+def test_lom_overflow_error(golden, dev):
+    from fedbiomed_amd import workload as W
+    from fedbiomed_amd.exceptions import FedbiomedSecaggError
+    from fedbiomed_amd.secagg import SecaggLomCrypter
+
+    ids = W.node_ids(3)
+    with pytest.raises(FedbiomedSecaggError) as ei:
+        SecaggLomCrypter("abc").encrypt(1, ids[0], [1.0, -2.0], W.pairwise_secrets_for(ids[0], ids), ids,
+                                        clipping_range=10**14, weight=1000, target_range=2**55)
+    assert "FB417" in str(ei.value)
+    assert golden["lom"]["overflow_error"]["type"] == "FedbiomedSecaggError"
+
+
+def test_lom_edge_cases(dev):
+    from fedbiomed_amd import workload as W
+    from fedbiomed_amd.exceptions import FedbiomedSecaggCrypterError, FedbiomedSecaggError
+    from fedbiomed_amd.secagg import SecaggLomCrypter
+
+    ids = W.node_ids(2)
+    cr = SecaggLomCrypter("x")
+    assert cr.nonce == b"000000000000000x"
+    with pytest.raises(FedbiomedSecaggCrypterError):
+        cr.encrypt(1, ids[0], [], W.pairwise_secrets_for(ids[0], ids), ids)  # max() of empty
+    with pytest.raises(FedbiomedSecaggCrypterError):
+        cr.encrypt(1, ids[0], [1.0, 2], W.pairwise_secrets_for(ids[0], ids), ids)  # not all floats
+    with pytest.raises(FedbiomedSecaggCrypterError):
+        cr.encrypt(1, ids[0], [1.0], W.pairwise_secrets_for(ids[0], ids), ids, weight=2**17)
+    with pytest.raises(FedbiomedSecaggError):
+        cr.encrypt(1, ids[0], [1.0], {ids[1]: b"short"}, ids)
+    # ragged / odd sizes through the aggregate kernel (scalar tail path)
+    for n in (1, 7, 8, 9, 1001):
+        ys = [cr.encrypt(3, u, [0.25] * n, W.pairwise_secrets_for(u, ids), ids, weight=2) for u in ids]
+        agg = cr.aggregate(ys, 4)
+        from oracle import secagg_oracle as O
+
+        assert _bits(agg) == _bits(O.lom_crypter_aggregate(ys, 4))
+
+
+def test_lom_large_mask_cancellation(dev):
+    """Size-independent property at a bench-scale vector: sum of masked = sum of q*w."""
+    from fedbiomed_amd import _device as D, workload as W
+    from fedbiomed_amd.secagg import SecaggLomCrypter
+
+    n, P = 1_000_003, 5
+    ids = W.node_ids(P)
+    cr = SecaggLomCrypter(W.LOM_NONCE)
+    xs = [torch.from_numpy(W.party_params(p, n)).to(dev) for p in range(P)]
+    Y = torch.stack([cr.encrypt_tensor(1, u, xs[p], W.pairwise_secrets_for(u, ids), ids, weight=W.party_weight(p))
+                     for p, u in enumerate(ids)])
+    out, sums = cr.aggregate_tensor(Y, sum(W.party_weight(p) for p in range(P)), want_sums=True)
+    qsum = torch.zeros(n, dtype=torch.int64, device=dev)
+    for p in range(P):
+        q = D.lom_protect(xs[p], [], [], b"\0" * 16, 0, 1, weight=W.party_weight(p))
+        qsum += q
+    assert torch.equal(sums, qsum)
+    # and a sampled float check against the oracle's average/dequantise
+    from oracle import secagg_oracle as O
+
+    idx = np.random.default_rng(0).choice(n, 2000, replace=False)
+    s_np = sums.cpu().numpy().view(np.uint64)[idx]
+    ref = O.reverse_quantize(O.apply_average([int(v) for v in s_np], sum(W.party_weight(p) for p in range(P))))
+    assert np.array_equal(out.cpu().numpy()[idx].view(np.uint64), ref.view(np.uint64))
+
+
+# ---------------------------------------------------------------- Joye-Libert
+def test_jl_small_modulus_golden(golden, dev):
+    """UserKey.encrypt / ServerKey.decrypt on raw plaintexts with small and 1024-bit moduli
+    (reference tests/test_joye_libert.py:229-253, 425-455), incl. FDH gcd retries."""
+    from fedbiomed_amd import _device as D
+
+    for case in golden["jl"]["jl_small"]:
+        n = I(case["n"])
+        pts = torch.tensor(case["pt"], dtype=torch.int64, device=dev)
+        cts = []
+        for key, ct in zip(case["keys"], case["ct"]):
+            got = D.jl_encrypt(pts, n, key, case["tau"], len(case["keys"]), slot=(100, 1))
+            assert D.limbs_to_ints(got.cpu().numpy()) == [I(c) for c in ct], (case["n"], key)
+            cts.append(got)
+        _, sums = D.jl_aggregate(torch.stack(cts), n, -sum(case["keys"]), case["tau"], len(case["pt"]), 1,
+                                 want_out=False, want_sums=True, slot=(100, 1))
+        s = sums.cpu().numpy().view(np.uint64)
+        assert [int(a) | (int(b) << 64) for a, b in s] == [I(d) for d in case["dec"]]
+
+
+@pytest.mark.parametrize("idx", range(6))
+def test_jl_crypter_golden(golden, dev, idx):
+    from fedbiomed_amd.secagg import SecaggCrypter
+    from fedbiomed_amd import _device as D
+
+    case = golden["jl"]["crypter"][idx]
+    bp = I(case["biprime"])
+    target = I(case["target"]) if case["target"] else None
+    P = case["n_parties"]
+    jc = SecaggCrypter()
+    encs = []
+    for p in range(P):
+        got = jc.encrypt(P, case["tau"], [F(v) for v in case["x"][p]], I(case["keys"][p]), bp,
+                         clipping_range=case["clip"], weight=case["weights"][p], target_range=target)
+        assert got == [I(c) for c in case["enc"][p]], p
+        encs.append(got)
+    n = len(case["x"][0])
+    agg = jc.aggregate(case["tau"], P, encs, I(case["sk0"]), bp, case["total"], clipping_range=case["clip"],
+                       num_expected_params=n, target_range=target)
+    assert _bits(agg) == [s[2:] for s in case["agg"]]
+    # decoded integer sums, and the wrong-key path (floor division of a non-multiple of N)
+    limbs = torch.from_numpy(np.stack([D.ints_to_limbs(e) for e in encs]).view(np.int32)).to(dev)
+    for key, exp in ((I(case["sk0"]), case["sums"]), (I(case["sk0"]) + 1, case["sums_badkey"])):
+        _, sums = D.jl_aggregate(limbs, bp, key, case["tau"], n, 1, target=target, want_out=False, want_sums=True)
+        s = sums.cpu().numpy().view(np.uint64)
+        assert [int(a) | (int(b) << 64) for a, b in s] == [I(v) for v in exp]
+
+
+def test_jl_edge_cases(dev):
+    from fedbiomed_amd import workload as W
+    from fedbiomed_amd.exceptions import FedbiomedSecaggCrypterError
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    jc = SecaggCrypter()
+    assert jc.encrypt(2, 1, [], 10, W.BIPRIME0) == []
+    with pytest.raises(FedbiomedSecaggCrypterError):
+        jc.encrypt(2, 1, [1.0], "10", W.BIPRIME0)
+    with pytest.raises(FedbiomedSecaggCrypterError):
+        jc.encrypt(2, 1, [1.0], 10, W.BIPRIME0, weight=2**17)
+    with pytest.raises(FedbiomedSecaggCrypterError):
+        jc.aggregate(1, 3, [[1], [2]], -20, W.BIPRIME0, 2)
+    with pytest.raises(FedbiomedSecaggCrypterError):
+        jc.aggregate(1, 2, [[1], [2.0]], -20, W.BIPRIME0, 2)
+    # reference test_secagg_crypter round trip: keys 10/10/-20, weights
+    params = [0.5, -1.25, 2.0, 0.0] * 9
+    e1 = jc.encrypt(2, 1, params, 10, W.BIPRIME0, weight=3)
+    e2 = jc.encrypt(2, 1, params, 10, W.BIPRIME0, weight=5)
+    out = jc.aggregate(1, 2, [e1, e2], -20, W.BIPRIME0, 8, num_expected_params=len(params))
+    assert all(math.isclose(a, b, abs_tol=1e-3) for a, b in zip(out, params))
+
+
+def test_jl_roundtrip_property(dev):
+    """Bench-shaped JL round trip at a few thousand ciphertexts: decoded sums == sum q*w."""
+    from fedbiomed_amd import _device as D, workload as W
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    n, P = 30_000, 4
+    jc = SecaggCrypter()
+    keys = [W.jl_user_key(p) for p in range(P)]
+    xs = [torch.from_numpy(W.party_params(p, n)).to(dev) for p in range(P)]
+    cts = torch.stack([jc.encrypt_tensor(P, 1, xs[p], keys[p], W.BIPRIME0, weight=W.party_weight(p))
+                       for p in range(P)])
+    out, sums = jc.aggregate_tensor(1, cts, -sum(keys), W.BIPRIME0, sum(W.party_weight(p) for p in range(P)),
+                                    num_expected_params=n, want_sums=True)
+    qsum = torch.zeros(n, dtype=torch.int64, device=dev)
+    for p in range(P):
+        qsum += D.lom_protect(xs[p], [], [], b"\0" * 16, 0, 1, weight=W.party_weight(p))
+    assert torch.equal(sums[:, 0], qsum) and int(sums[:, 1].abs().sum()) == 0

@@ -1,0 +1,101 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library builds/loads, exports every
+symbol include/fbm_secagg.h declares, and the host-side parameter logic matches the
+reference's Python formulas.  No GPU compute is called here."""
+
+import ctypes
+import math
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "fbm_secagg.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|uint64_t|const char\*)\s+(fbm_\w+)\s*\(", text, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from fedbiomed_amd import _build, _native
+
+    _build.build()
+    return _native.load()
+
+
+def test_header_declares_abi():
+    syms = declared_symbols()
+    assert "fbm_lom_protect" in syms and "fbm_jl_encrypt" in syms and "fbm_jl_aggregate" in syms
+    assert len(syms) >= 10
+
+
+def test_library_exports_every_declared_symbol(lib):
+    from fedbiomed_amd import _native
+
+    for s in declared_symbols():
+        assert hasattr(lib, s), f"missing export {s}"
+        assert s in _native.SIGNATURES, f"no ctypes signature for {s}"
+    assert lib.fbm_abi_version() == 1
+
+
+def test_check_stats_lom_guard(lib):
+    # host-only helper: error iff max_bits >= 64 - ceil(log2(P))  (_lom.py:133-150)
+    def rc(max_bits, nodes):
+        st = np.array([max_bits, 0, 0, 0], dtype=np.uint32)
+        return lib.fbm_check_stats(ctypes.c_void_p(st.ctypes.data), nodes, None)
+
+    for nodes in (1, 2, 3, 4, 5, 16, 17):
+        limit = 64 - math.ceil(math.log2(nodes))
+        assert rc(limit - 1, nodes) == 0
+        assert rc(limit, nodes) == -4
+    st = np.array([0, 1, 0, 0], dtype=np.uint32)  # dequant range flag
+    assert lib.fbm_check_stats(ctypes.c_void_p(st.ctypes.data), 0, None) == -3
+
+
+def test_jl_slot_matches_reference_formula():
+    from fedbiomed_amd import _device as D
+    from oracle import secagg_oracle as O
+
+    for T in (2**13, 2**55, 10, 2**20 + 3):
+        for P in (1, 2, 3, 4, 7, 8, 15, 16, 100):
+            assert D.jl_slot(T, P) == O.jl_slot(T, P)
+    assert D.jl_slot(None, 8) == (34, 30)
+    assert D.jl_slot(None, 4) == (33, 31)
+
+
+def test_quant_params_semantics():
+    from fedbiomed_amd import _device as D
+
+    assert D.quant_params(None, 2**13) == (3.0, 6.0, 8192.0, 8191)
+    with pytest.raises(OverflowError):
+        D.quant_params(7, 2**64 + 1)
+    with pytest.raises(ZeroDivisionError):
+        D.dequant_params(3, 1)
+    negc, step = D.dequant_params(3, 2**13)
+    assert negc == -3.0 and step == 6 / 8191
+
+
+def test_limb_roundtrip():
+    from fedbiomed_amd import _device as D
+
+    rng = np.random.default_rng(0)
+    vals = [int.from_bytes(rng.bytes(256), "little") for _ in range(17)] + [0, 1, 2**2048 - 1]
+    arr = D.ints_to_limbs(vals)
+    assert arr.shape == (len(vals), 64)
+    assert D.limbs_to_ints(arr) == vals
+    n2 = 12345**2
+    assert D.limbs_to_ints(D.ints_to_limbs([-5, 2**2048 + 7], n2)) == [(-5) % n2, (2**2048 + 7) % n2]
+
+
+def test_product_path_does_not_import_oracle():
+    # the product must never route through the CPU oracle
+    for dirpath, _, files in os.walk(os.path.join(ROOT, "fedbiomed_amd")):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in re.sub(r"#.*", "", src).replace('"""', "").split("import")[0] or \
+                    "from oracle" not in src and "import oracle" not in src, f

@@ -1,0 +1,177 @@
+// Integer / FP64 VALU issue-rate microbenchmark for the JL Montgomery engine design
+// (which multiply primitive should carry the 2048-bit modmul on gfx950?).
+// Each kernel runs 8 independent dependency chains per lane, ITER iterations; the
+// host reports per-instruction throughput in Gop/s (lane-ops) for the whole chip.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+
+#define ITER 4096
+#define CH 8
+
+__global__ void k_mad64(uint64_t* out, uint32_t s) {
+  uint32_t a = threadIdx.x + s, b = blockIdx.x * 7 + s;
+  uint64_t acc[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) acc[c] = c + a;
+  for (int i = 0; i < ITER; ++i) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      uint64_t r, cc;
+      asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cc) : "v"(a + c), "v"(b), "v"(acc[c]));
+      acc[c] = r;
+    }
+  }
+  uint64_t x = 0;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) x ^= acc[c];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+
+__global__ void k_mullo(uint64_t* out, uint32_t s) {
+  uint32_t a = threadIdx.x + s, b = blockIdx.x * 7 + s;
+  uint32_t acc[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) acc[c] = c + a;
+  for (int i = 0; i < ITER; ++i) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      uint32_t r;
+      asm volatile("v_mul_lo_u32 %0, %1, %2" : "=v"(r) : "v"(acc[c]), "v"(b));
+      acc[c] = r;
+    }
+  }
+  uint64_t x = 0;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) x ^= acc[c];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+
+__global__ void k_mulhi(uint64_t* out, uint32_t s) {
+  uint32_t a = threadIdx.x + s, b = blockIdx.x * 7 + s;
+  uint32_t acc[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) acc[c] = c + a;
+  for (int i = 0; i < ITER; ++i) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      uint32_t r;
+      asm volatile("v_mul_hi_u32 %0, %1, %2" : "=v"(r) : "v"(acc[c]), "v"(b));
+      acc[c] = r;
+    }
+  }
+  uint64_t x = 0;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) x ^= acc[c];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+
+__global__ void k_addc(uint64_t* out, uint32_t s) {
+  uint32_t a = threadIdx.x + s;
+  uint32_t acc[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) acc[c] = c + a;
+  for (int i = 0; i < ITER; ++i) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      uint32_t r;
+      asm volatile("v_add_co_u32 %0, vcc, %1, %2" : "=v"(r) : "v"(acc[c]), "v"(a) : "vcc");
+      acc[c] = r;
+    }
+  }
+  uint64_t x = 0;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) x ^= acc[c];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+
+__global__ void k_add3(uint64_t* out, uint32_t s) {
+  uint32_t a = threadIdx.x + s;
+  uint32_t acc[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) acc[c] = c + a;
+  for (int i = 0; i < ITER; ++i) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      uint32_t r;
+      asm volatile("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(acc[c]), "v"(a), "v"(s));
+      acc[c] = r;
+    }
+  }
+  uint64_t x = 0;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) x ^= acc[c];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+
+__global__ void k_fma64(uint64_t* out, uint32_t s) {
+  double a = threadIdx.x * 1e-3 + s, b = 0.999999;
+  double acc[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) acc[c] = c + a;
+  for (int i = 0; i < ITER; ++i) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      double r;
+      asm volatile("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(acc[c]), "v"(b), "v"(a));
+      acc[c] = r;
+    }
+  }
+  double x = 0;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) x += acc[c];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (uint64_t)x;
+}
+
+__global__ void k_mul24(uint64_t* out, uint32_t s) {
+  uint32_t a = threadIdx.x + s, b = blockIdx.x * 7 + s;
+  uint32_t acc[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) acc[c] = c + a;
+  for (int i = 0; i < ITER; ++i) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      uint32_t r;
+      asm volatile("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(acc[c]), "v"(b), "v"(a));
+      acc[c] = r;
+    }
+  }
+  uint64_t x = 0;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) x ^= acc[c];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+
+typedef void (*kfn)(uint64_t*, uint32_t);
+
+int main() {
+  const int blocks = 256 * 8, threads = 256;
+  uint64_t* d;
+  hipMalloc(&d, sizeof(uint64_t) * blocks * threads);
+  struct { const char* name; kfn f; } ks[] = {
+      {"v_mad_u64_u32", k_mad64}, {"v_mul_lo_u32", k_mullo}, {"v_mul_hi_u32", k_mulhi},
+      {"v_add_co_u32", k_addc},   {"v_add3_u32", k_add3},    {"v_fma_f64", k_fma64},
+      {"v_mad_u32_u24", k_mul24}};
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  for (auto& k : ks) {
+    hipLaunchKernelGGL(k.f, dim3(blocks), dim3(threads), 0, 0, d, 1u);
+    hipDeviceSynchronize();
+    float best = 1e30f;
+    for (int r = 0; r < 5; ++r) {
+      hipEventRecord(e0);
+      hipLaunchKernelGGL(k.f, dim3(blocks), dim3(threads), 0, 0, d, 1u);
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+      float ms;
+      hipEventElapsedTime(&ms, e0, e1);
+      if (ms < best) best = ms;
+    }
+    double ops = (double)blocks * threads * ITER * CH;
+    printf("%-16s %8.3f ms  %8.1f G lane-ops/s  (%.2f cyc/wave-instr @2.4GHz/1024 SIMDs)\n", k.name, best,
+           ops / best / 1e6, (1024.0 * 2.4e9) / (ops / 64.0 / (best * 1e-3)));
+  }
+  return 0;
+}
