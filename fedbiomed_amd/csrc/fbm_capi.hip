@@ -368,8 +368,8 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
   if (rc) return rc;
   QuantParams qp;
   if ((rc = quant_params(clip, two_clip, target_f, target_m1, qp))) return rc;
-  if (x_dtype != FBM_F32 && x_dtype != FBM_F64) {
-    set_error("x_dtype must be FBM_F32 or FBM_F64");
+  if (x_dtype != FBM_F32 && x_dtype != FBM_F64 && x_dtype != FBM_U64) {
+    set_error("x_dtype must be FBM_F32, FBM_F64 or FBM_U64");
     return FBM_E_ARG;
   }
   if (!biprime || !key) {

@@ -361,8 +361,9 @@ __global__ void __launch_bounds__(FBM_BLOCK, 1) jl_exp_kernel(const uint32_t* __
 // ------------------------------------------------------------------------------------
 // aggregate: product of the P ciphertexts, X = prod_u c_u * R  (Montgomery form, lazy)
 // Each c_u (any value < 2^2048) is first brought into the Montgomery domain with R^2.
-//   step 2u   : a = R^2,    b = c_u  -> c_u*R   (u = 0: X; else staged in LDS)
-//   step 2u+1 : a = c_u*R,  b = X    -> X      (u >= 1)
+//   step 0    : a = R^2,    b = c_0  -> X = c_0*R
+//   step 2u-1 : a = R^2,    b = c_u  -> c_u*R staged in LDS      (u >= 1)
+//   step 2u   : a = c_u*R,  b = X    -> X                         (u >= 1)
 // ------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(FBM_BLOCK, 1) jl_prod_kernel(const uint32_t* __restrict__ cts, int n_parties,
                                                               uint64_t n_ct, JlParams jp,
@@ -381,10 +382,10 @@ __global__ void __launch_bounds__(FBM_BLOCK, 1) jl_prod_kernel(const uint32_t* _
     st = __builtin_amdgcn_readfirstlane(st);
     asm volatile("" : "+s"(st));
     uint32_t acc[FBM_NL];
-    const bool tomont = (st & 1) == 0;
+    const bool tomont = (st == 0) || (st & 1);
     if (tomont) {
       uint32_t c32[64];
-      load_row64(cts + ((uint64_t)(st >> 1) * n_ct + ct) * 64, c32);
+      load_row64(cts + ((uint64_t)((st + 1) >> 1) * n_ct + ct) * 64, c32);
       to28<64, FBM_NL>(c32, acc);
       lds_store_uniform<FBM_NL>(lds, ls, jp.mc.R2);
     } else {
@@ -443,9 +444,9 @@ __global__ void __launch_bounds__(FBM_BLOCK, 1) jl_inv_modn_kernel(uint64_t n_ct
   uint32_t err = 0;
 
   // --- e mod N = (e_hi * R_N + e_lo) mod N  with R_N = 2^1036 --------------------------
-  //   s0: a = R2N, b = hi       -> t1 = hi*R_N mod N     (lazy, < 2N)
-  //   s1: a = R2N, b = t1 + lo  -> x*R_N
-  //   s2: a = 1,   b = x*R_N    -> x mod N
+  //   t1 = mont(R2N, hi) = hi*R_N mod N            (lazy, < 2N)
+  //   t2 = mont(1, mont(R2N, lo)) = lo mod N        (lazy, < 2N; lo may be >= N)
+  //   y  = t1 + t2 < 4N, then three conditional subtractions -> e mod N
   uint32_t y28[FBM_NLN];
   {
     uint32_t e32[64];
@@ -460,18 +461,18 @@ __global__ void __launch_bounds__(FBM_BLOCK, 1) jl_inv_modn_kernel(uint64_t n_ct
     }
     lds_store_uniform<FBM_NLN>(lds, ls, jp.mn.R2);
     mont_mul(y28, lds, ls, jp.mn);  // hi * R_N mod N
-    {
-      uint32_t c = 0;
-#pragma unroll
-      for (int k = 0; k < FBM_NLN; ++k) {
-        const uint32_t v = y28[k] + lo[k] + c;
-        y28[k] = v & FBM_LMASK;
-        c = v >> FBM_LB;
-      }
-    }
-    mont_mul(y28, lds, ls, jp.mn);  // x * R_N mod N
+    mont_mul(lo, lds, ls, jp.mn);   // lo * R_N mod N
     lds_store_one<FBM_NLN>(lds, ls);
-    mont_mul(y28, lds, ls, jp.mn);  // x mod N
+    mont_mul(lo, lds, ls, jp.mn);   // lo mod N
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < FBM_NLN; ++k) {
+      const uint32_t v = y28[k] + lo[k] + c;
+      y28[k] = v & FBM_LMASK;
+      c = v >> FBM_LB;
+    }
+    mont_csub(y28, jp.mn.M);
+    mont_csub(y28, jp.mn.M);
     mont_csub(y28, jp.mn.M);
   }
   // --- y = (e mod N)^-1 mod N : binary extended Euclid on 32-bit limbs ------------------
@@ -729,13 +730,14 @@ __global__ void __launch_bounds__(256) jl_decode_kernel(const uint32_t* __restri
     sums[2 * o] = (uint64_t)v;
     sums[2 * o + 1] = (uint64_t)(v >> 64);
   }
+  if (!out) return;
   const double a = fbm_true_div_u128(v, total_weight);
-  if (a >= 18446744073709551616.0) {
+  if (a >= 18446744073709551616.0) {  // reverse_quantize guard (only when dequantising)
     atomicOr(stats + FBM_STAT_ERRFLAGS, FBM_ERR_DEQUANT_RANGE);
-    if (out) out[o] = 0.0;
+    out[o] = 0.0;
     return;
   }
-  if (out) out[o] = fbm_dequantize(a, neg_c, step);
+  out[o] = fbm_dequantize(a, neg_c, step);
 }
 
 // ------------------------------------------------------------------------------------

@@ -166,7 +166,7 @@ def test_lom_large_mask_cancellation(dev):
     out, sums = cr.aggregate_tensor(Y, sum(W.party_weight(p) for p in range(P)), want_sums=True)
     qsum = torch.zeros(n, dtype=torch.int64, device=dev)
     for p in range(P):
-        q = D.lom_protect(xs[p], [], [], b"\0" * 16, 0, 1, weight=W.party_weight(p))
+        q = D.lom_protect(xs[p], [], [], b"\0" * 16, 0, 0, weight=W.party_weight(p))
         qsum += q
     assert torch.equal(sums, qsum)
     # and a sampled float check against the oracle's average/dequantise
@@ -264,5 +264,5 @@ def test_jl_roundtrip_property(dev):
                                     num_expected_params=n, want_sums=True)
     qsum = torch.zeros(n, dtype=torch.int64, device=dev)
     for p in range(P):
-        qsum += D.lom_protect(xs[p], [], [], b"\0" * 16, 0, 1, weight=W.party_weight(p))
+        qsum += D.lom_protect(xs[p], [], [], b"\0" * 16, 0, 0, weight=W.party_weight(p))
     assert torch.equal(sums[:, 0], qsum) and int(sums[:, 1].abs().sum()) == 0

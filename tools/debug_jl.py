@@ -1,0 +1,70 @@
+"""Stage-by-stage check of the JL aggregate pipeline on the GPU (debug aid)."""
+import numpy as np, torch, sys
+sys.path.insert(0, ".")
+from fedbiomed_amd import _device as D, _native as N, workload as W
+from fedbiomed_amd.secagg import SecaggCrypter
+from oracle import secagg_oracle as O
+
+dev = D.device()
+P, n, tau = int(sys.argv[1]) if len(sys.argv) > 1 else 2, int(sys.argv[2]) if len(sys.argv) > 2 else 70, 1
+keys = [W.jl_user_key(p) for p in range(P)]
+xs = [[float(v) for v in W.party_params(p, n)] for p in range(P)]
+import time; t0 = time.time()
+jc = SecaggCrypter()
+encs = [jc.encrypt(P, tau, xs[p], keys[p], W.BIPRIME0, weight=W.party_weight(p)) for p in range(P)]
+ok = [encs[p] == O.jl_encrypt(xs[p], tau, keys[p], W.BIPRIME0, P, weight=W.party_weight(p)) for p in range(P)]
+print("encrypt ok:", ok, time.time() - t0)
+N2 = W.BIPRIME0 ** 2
+n_ct = len(encs[0])
+lib = N.load()
+limbs = torch.from_numpy(np.stack([D.ints_to_limbs(e) for e in encs]).view(np.int32)).to(dev)
+ws_bytes = int(lib.fbm_jl_aggregate_workspace(n_ct))
+ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)
+es, cr = D.jl_slot(None, P)
+sk0 = -sum(keys)
+negc, step = D.dequant_params(None, 2**13)
+out = torch.empty(n, dtype=torch.float64, device=dev)
+sums = torch.empty((n, 2), dtype=torch.int64, device=dev)
+st = torch.zeros(4, dtype=torch.int32, device=dev)
+bp = D._biprime_limbs(W.BIPRIME0); kl, kneg = D._key_limbs(sk0)
+rc = lib.fbm_jl_aggregate(D._ptr(limbs), P, n_ct, es, cr, n, D._np_ptr(bp), D._np_ptr(kl), kneg, tau, 1, negc, step,
+                          D._ptr(out), D._ptr(sums), D._ptr(ws), D._ptr(st), D._stream())
+torch.cuda.synchronize()
+print("rc", rc, N.last_error(), "stats", st.cpu().numpy())
+w = ws.cpu().numpy()
+def al(v): return (v + 255) & ~255
+off = al(512 * 4)
+nb = (n_ct + 255) // 256
+Xraw = w[off:off + nb * 256 * 74 * 4].view(np.uint32).reshape(nb, 74, 256); off += al(nb * 256 * 74 * 4)
+H = w[off:off + n_ct * 256].view(np.uint32).reshape(n_ct, 64); off += al(n_ct * 256)
+E = w[off:off + n_ct * 256].view(np.uint32).reshape(n_ct, 64); off += al(n_ct * 256)
+INV = w[off:off + n_ct * 256].view(np.uint32).reshape(n_ct, 64); off += al(n_ct * 256)
+XS = w[off:off + n_ct * 128].view(np.uint32).reshape(n_ct, 32)
+def from28(l): return sum(int(v) << (28 * i) for i, v in enumerate(l))
+def from32(l): return sum(int(v) << (32 * i) for i, v in enumerate(l))
+R = 2 ** (28 * 74)
+bad = {"H": 0, "X": 0, "E": 0, "inv": 0, "x": 0}
+first_bad = {}
+for k in range(n_ct):
+    h = O.fdh((k << 512) | tau, N2)
+    def chk(name, cond):
+        if not cond:
+            bad[name] += 1
+            first_bad.setdefault(name, k)
+    chk("H", from32(H[k]) == h)
+    prod = 1
+    for e in encs: prod = prod * e[k] % N2
+    X = from28(Xraw[k // 256, :, k % 256])
+    chk("X", X % N2 == prod * R % N2)
+    e_ = pow(h, -sk0, N2)
+    chk("E", from32(E[k]) == e_)
+    inv = pow(e_, -1, N2)
+    chk("inv", from32(INV[k]) == inv)
+    v = prod * inv % N2
+    x = ((v - 1) // W.BIPRIME0) % W.BIPRIME0
+    chk("x", from32(XS[k]) == x)
+print("n_ct", n_ct, "bad", bad, "first", first_bad)
+s_np = sums.cpu().numpy().view(np.uint64)
+ref = O.jl_aggregate_ints(encs, tau, sk0, W.BIPRIME0, n)
+diff = [i for i in range(n) if int(s_np[i, 0]) | (int(s_np[i, 1]) << 64) != ref[i]]
+print("sum mismatches", len(diff), diff[:10])
