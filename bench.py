@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""Headline benchmark: secure-aggregation encrypt+aggregate throughput on MI355X.
+
+Metric (BASELINE.json): "params/s secagg encrypt+aggregate (device-resident), 10M-elem
+vector @1/8 GPU".  One step = every party encrypts its device-resident parameter vector
+(Joye-Libert by default: quantise, weight, VES-pack, FDH, 2048-bit modexp) followed by one
+aggregate (ciphertext product, server-key exponentiation, inverse, unmask, decode, average,
+dequantise).  value = params processed by all ranks / wall time of K steps (max over ranks).
+
+Scaling: element-range sharding with no data-path collective (fedbiomed_amd/distributed.py):
+each rank owns one 10M-element stripe (global offsets), so per-GPU work is fixed -> "weak".
+`--strong` splits a fixed total instead.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scheme jl|lom] [--n 10000000] [--parties 8]
+"""
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MAD_PEAK_TOPS = 30.27        # measured v_mad_u64_u32 lane-op rate, whole chip (tools/microbench/intrate.hip)
+MADS_PER_MONTMUL = 74 * 148  # 28-bit-limb product: 74 rows x (74 a*b + 74 m*M) v_mad_u64_u32
+
+
+def montmuls_per_exp(key: int, win: int = 5) -> int:
+    """Montgomery products of one jl_exp_kernel ciphertext: to-Montgomery + 16-entry odd-power
+    table + sliding-window schedule (mirror of build_schedule in fbm_capi.hip) + final product."""
+    k = abs(key)
+    if k == 0:
+        return 2
+    bits = bin(k)[2:]
+    nb = len(bits)
+    i, sq, mul, first = nb - 1, 0, 0, True
+    bit = lambda j: (k >> j) & 1  # noqa: E731
+    pending = 0
+    while i >= 0:
+        if not bit(i):
+            pending += 1
+            i -= 1
+            continue
+        lo = max(i - win + 1, 0)
+        while not bit(lo):
+            lo += 1
+        if first:
+            first = False
+        else:
+            sq += pending + (i - lo + 1)
+            mul += 1
+        pending = 0
+        i = lo - 1
+    sq += pending
+    return 1 + 16 + sq + mul + 1
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scheme", choices=["jl", "lom"], default="jl")
+    ap.add_argument("--n", type=int, default=10_000_000, help="elements per GPU (weak) or total (--strong)")
+    ap.add_argument("--parties", type=int, default=8)
+    ap.add_argument("--strong", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=None, help="elements in the timed CPU-oracle sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-lom-extra", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+
+    from fedbiomed_amd import _device as D, _native, distributed, workload as W
+    from fedbiomed_amd.secagg import SecaggCrypter, SecaggLomCrypter
+
+    rank, world, local = distributed.env_rank()
+    if world > 1:
+        distributed.init("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    P, tau = args.parties, 1
+    ids = W.node_ids(P)
+    weights = [W.party_weight(p) for p in range(P)]
+    total_w = sum(weights)
+    es, cr = D.jl_slot(None, P)
+
+    # ---- this rank's stripe (global element offset) ----
+    if args.strong:
+        align = cr if args.scheme == "jl" else 8
+        lo, hi = distributed.shard_range(args.n, world, rank, align)
+        n_total = args.n
+    else:
+        per = ((args.n + cr * 8 - 1) // (cr * 8)) * (cr * 8) if world > 1 else args.n
+        lo, hi = rank * per, rank * per + args.n
+        n_total = args.n * world
+    n = hi - lo
+    # synthetic device-resident inputs (float32 model vectors, SURVEY §8(d) recipe)
+    xs = [torch.from_numpy(W.party_params(p + 1000 * rank, n)).to(dev) for p in range(P)]
+    keys = [W.jl_user_key(p) for p in range(P)]
+    sk0 = -sum(keys)
+    jc, lc = SecaggCrypter(), SecaggLomCrypter(W.LOM_NONCE)
+    secrets_ = [W.pairwise_secrets_for(u, ids) for u in ids]
+
+    def step_jl():
+        cts = [jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=weights[p], ct_offset=lo // cr)
+               for p in range(P)]
+        return jc.aggregate_tensor(tau, torch.stack(cts), sk0, W.BIPRIME0, total_w, num_expected_params=n,
+                                   ct_offset=lo // cr)
+
+    def step_lom():
+        ys = [lc.encrypt_tensor(tau, u, xs[p], secrets_[p], ids, weight=weights[p], elem_offset=lo)
+              for p, u in enumerate(ids)]
+        return lc.aggregate_tensor(torch.stack(ys), total_w)
+
+    def timed(step, steps, warmup, prof=False):
+        for _ in range(warmup):
+            step()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        if prof:
+            _native.prof_enable(True)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if prof:
+            _native.prof_enable(False)
+        if world > 1:
+            torch.distributed.barrier()
+        el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+        return el.item(), (_native.prof_report() if prof else {})
+
+    step = step_jl if args.scheme == "jl" else step_lom
+    elapsed, kprof = timed(step, args.steps, args.warmup, prof=True)
+    value = n_total * args.steps / elapsed
+    ms_per_step = 1000.0 * elapsed / args.steps
+
+    # ---- roofline of the dominant kernel, from the live per-kernel HIP events ----
+    n_ct = (n + cr - 1) // cr
+    if args.scheme == "jl":
+        cnt, ms = kprof.get("jl_exp", (0, 0.0))
+        # algorithmic bytes: encrypt/party 4N + 256*#ct, aggregate 256*P*#ct + 8N
+        alg_bytes = args.steps * (P * (4 * n + 256 * n_ct) + (256 * P * n_ct + 8 * n))
+        mm = P * montmuls_per_exp(keys[0]) + montmuls_per_exp(sk0)
+        mads = args.steps * n_ct * mm * MADS_PER_MONTMUL
+        kname = "jl_exp_kernel"
+    else:
+        cnt, ms = kprof.get("lom_aggregate", (0, 0.0))
+        alg_bytes = args.steps * 8 * (P + 1) * n
+        mads, kname = 0, "lom_aggregate_kernel"
+    sec = ms / 1000.0 if ms > 0 else float("nan")
+    achieved = alg_bytes / sec / 1e9 if ms > 0 else None
+    roof = {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+            "avg_launch_ms": (ms / cnt) if cnt else None, "launches": cnt}
+    line = {
+        "metric": "params/s secagg encrypt+aggregate (device-resident), 10M-elem vector @1/8 GPU",
+        "value": value, "unit": "params/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong" if args.strong else "weak",
+        "vs_baseline": None, "dtype": "u32-limb bigint (JL) / u64 (LOM); f32 in, f64 out",
+        "data": "synthetic (float32 N(0,0.05^2) + 0.1% +/-4.0 outliers per party; biprime0; random 2040-bit keys)",
+        "config": {"workload": f"{'Joye-Libert' if args.scheme == 'jl' else 'LOM'} encrypt (all {P} parties) + "
+                               f"aggregate, {n:,} elements per GPU", "scheme": args.scheme, "parties": P,
+                   "elements_per_gpu": n, "elements_total": n_total, "ciphertexts_per_party_per_gpu":
+                   n_ct if args.scheme == "jl" else None, "parallelism": f"element-range x{world}"},
+        "roofline": roof,
+        "kernels_ms": {k: {"launches": c, "total_ms": round(t, 3)} for k, (c, t) in sorted(kprof.items())},
+    }
+    if args.scheme == "jl" and cnt:
+        ach = mads / sec / 1e12
+        line["roofline_valu"] = {"bound": "int-valu (v_mad_u64_u32)", "achieved": ach, "peak": MAD_PEAK_TOPS,
+                                 "unit": "T lane-mad/s", "frac": ach / MAD_PEAK_TOPS,
+                                 "montmuls_per_ct_step": mm}
+
+    # ---- secondary: LOM at the same size (cheap), so both schemes are on record ----
+    if args.scheme == "jl" and not args.no_lom_extra:
+        el2, kp2 = timed(step_lom, max(args.steps, 5), 1, prof=True)
+        c2, m2 = kp2.get("lom_aggregate", (0, 0.0))
+        ab = max(args.steps, 5) * 8 * (P + 1) * n
+        line["lom"] = {"value": n_total * max(args.steps, 5) / el2, "unit": "params/s",
+                       "ms_per_step": 1000 * el2 / max(args.steps, 5),
+                       "aggregate_hbm_GBps": ab / (m2 / 1000) / 1e9 if m2 else None,
+                       "aggregate_hbm_frac": (ab / (m2 / 1000) / 1e9) / HBM_PEAK_GBS if m2 else None,
+                       "kernels_ms": {k: {"launches": c, "total_ms": round(t, 3)} for k, (c, t) in sorted(kp2.items())}}
+
+    # ---- CPU baseline: the oracle (CPU restatement of the reference, GMP powm) on a bounded sample ----
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import secagg_oracle as O
+
+        ns = args.cpu_sample or (20_000 if args.scheme == "jl" else 500_000)
+        xs_c = [[float(v) for v in W.party_params(p, ns)] for p in range(P)]
+        t0 = time.perf_counter()
+        if args.scheme == "jl":
+            cts = [O.jl_encrypt(xs_c[p], tau, keys[p], W.BIPRIME0, P, weight=weights[p]) for p in range(P)]
+            O.jl_crypter_aggregate(cts, tau, sk0, W.BIPRIME0, total_w, ns)
+        else:
+            non = O.lom_nonce(W.LOM_NONCE)
+            ys = [O.lom_encrypt(xs_c[p], tau, u, secrets_[p], ids, non, weight=weights[p])
+                  for p, u in enumerate(ids)]
+            O.lom_crypter_aggregate(ys, total_w)
+        tc = time.perf_counter() - t0
+        line["cpu_baseline"] = {"value": ns / tc, "unit": "params/s", "cores": 1, "kind": "port",
+                                "sample": f"{ns:,} elements x {P} parties, encrypt all + aggregate, "
+                                          f"{tc:.1f} s on 1 host core (oracle/secagg_oracle.py; GMP mpz_powm "
+                                          f"via ctypes as gmpy2 does)"}
+        line["gpu_over_cpu"] = value / (ns / tc)
+    if rank == 0:
+        print(json.dumps(line))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -190,7 +190,8 @@ def _nonce_block(nonce: bytes) -> np.ndarray:
 
 
 def lom_protect(x: torch.Tensor, secrets: Sequence[bytes], signs: Sequence[int], nonce: bytes, tau: int,
-                n_nodes: int, clip=None, target=None, weight: int = 1, raw_seeds: bool = False) -> torch.Tensor:
+                n_nodes: int, clip=None, target=None, weight: int = 1, raw_seeds: bool = False,
+                elem_offset: int = 0) -> torch.Tensor:
     """One party's masked vector (u64 bit patterns in an int64 tensor); raises the
     reference's LOM overflow error when max(bit_length(q*w)) >= 64 - ceil(log2(n_nodes))."""
     dev = x.device
@@ -207,7 +208,8 @@ def lom_protect(x: torch.Tensor, secrets: Sequence[bytes], signs: Sequence[int],
     y = torch.empty(n, dtype=torch.int64, device=dev)
     st = _stats(dev)
     _call(lib.fbm_lom_protect, _ptr(x), _x_dtype(x), n, c, c2, tf, tm1, int(weight), _np_ptr(sec), _np_ptr(sg),
-          len(secrets), 1 if raw_seeds else 0, _np_ptr(nb), int(tau), _ptr(y), _ptr(st), _stream())
+          len(secrets), 1 if raw_seeds else 0, _np_ptr(nb), int(tau), int(elem_offset), _ptr(y), _ptr(st),
+          _stream())
     _check_stats(st, lom_nodes=n_nodes)
     return y
 
@@ -272,7 +274,7 @@ def _key_limbs(key: int) -> Tuple[np.ndarray, int]:
 
 
 def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, clip=None, target=None,
-               weight: int = 1, slot: Optional[Tuple[int, int]] = None) -> torch.Tensor:
+               weight: int = 1, slot: Optional[Tuple[int, int]] = None, ct_offset: int = 0) -> torch.Tensor:
     """One party's JL ciphertexts as an int32 [n_ct, 64] tensor of 32-bit limbs.
     `slot` overrides the (element_size, comp_ratio) packing (UserKey.encrypt on raw
     plaintexts = slot (es, 1) with an int64 input)."""
@@ -294,14 +296,14 @@ def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, 
     ws = torch.empty(int(lib.fbm_jl_encrypt_workspace(n_ct)), dtype=torch.uint8, device=dev)
     st = _stats(dev)
     _call(lib.fbm_jl_encrypt, _ptr(x), _x_dtype(x), n, c, c2, tf, tm1, int(weight), es, cr, _np_ptr(bp),
-          _np_ptr(kl), kneg, int(tau), _ptr(ct), _ptr(ws), _ptr(st), _stream())
+          _np_ptr(kl), kneg, int(tau), int(ct_offset), _ptr(ct), _ptr(ws), _ptr(st), _stream())
     _check_stats(st)
     return ct
 
 
 def jl_aggregate(cts: torch.Tensor, biprime: int, key: int, tau: int, n_expected: int, total_weight: int,
                  clip=None, target=None, want_out: bool = True, want_sums: bool = False,
-                 slot: Optional[Tuple[int, int]] = None):
+                 slot: Optional[Tuple[int, int]] = None, ct_offset: int = 0):
     """Aggregate [P, n_ct, 64] int32 ciphertext limbs -> (float64 [n_out], int64 [n_out, 2] sums)."""
     dev = cts.device
     lib = N.load()
@@ -327,6 +329,6 @@ def jl_aggregate(cts: torch.Tensor, biprime: int, key: int, tau: int, n_expected
     ws = torch.empty(int(lib.fbm_jl_aggregate_workspace(n_ct)), dtype=torch.uint8, device=dev)
     st = _stats(dev)
     _call(lib.fbm_jl_aggregate, _ptr(cts), P, n_ct, es, cr, n_out, _np_ptr(bp), _np_ptr(kl), kneg, int(tau),
-          int(total_weight), negc, step, _ptr(out), _ptr(sums), _ptr(ws), _ptr(st), _stream())
+          int(ct_offset), int(total_weight), negc, step, _ptr(out), _ptr(sums), _ptr(ws), _ptr(st), _stream())
     _check_stats(st)
     return out, sums

@@ -46,16 +46,18 @@ SIGNATURES = {
     "fbm_last_error": (ctypes.c_char_p, []),
     "fbm_check_stats": (c_int, [c_vp, c_int, c_vp]),
     "fbm_lom_protect": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_vp, c_vp, c_int, c_int,
-                                c_vp, c_u64, c_vp, c_vp, c_vp]),
+                                c_vp, c_u64, c_u64, c_vp, c_vp, c_vp]),
     "fbm_prf_key": (c_int, [c_vp, c_vp, c_u64, c_vp, c_vp]),
     "fbm_dequantize": (c_int, [c_vp, c_u64, c_dbl, c_dbl, c_vp, c_vp]),
     "fbm_lom_aggregate": (c_int, [c_vp, c_int, c_u64, c_u64, c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_encrypt_workspace": (c_u64, [c_u64]),
     "fbm_jl_aggregate_workspace": (c_u64, [c_u64]),
     "fbm_jl_encrypt": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_int, c_int, c_vp, c_vp,
-                               c_int, c_u64, c_vp, c_vp, c_vp, c_vp]),
-    "fbm_jl_aggregate": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_u64, c_vp, c_vp, c_int, c_u64, c_u64, c_dbl,
-                                 c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
+                               c_int, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),
+    "fbm_jl_aggregate": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_u64, c_vp, c_vp, c_int, c_u64, c_u64, c_u64,
+                                 c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "fbm_prof_enable": (c_int, [c_int]),
+    "fbm_prof_report": (c_int, [ctypes.c_char_p, c_int]),
 }
 
 
@@ -88,3 +90,20 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
 
 def last_error() -> str:
     return (load().fbm_last_error() or b"").decode(errors="replace")
+
+
+def prof_enable(on: bool) -> None:
+    load().fbm_prof_enable(1 if on else 0)
+
+
+def prof_report() -> dict:
+    """{kernel: (launches, total_ms)} of the launches recorded since the last report."""
+    lib = load()
+    need = lib.fbm_prof_report(None, 0)  # non-destructive size query
+    buf = ctypes.create_string_buffer(need + 4096)
+    lib.fbm_prof_report(buf, len(buf))
+    out = {}
+    for line in buf.value.decode().splitlines():
+        name, cnt, ms = line.split()
+        out[name] = (int(cnt), float(ms))
+    return out

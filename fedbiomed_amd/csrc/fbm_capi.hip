@@ -6,6 +6,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <map>
+#include <mutex>
+#include <string>
 #include <vector>
 
 #include "fbm_internal.hpp"
@@ -133,7 +136,7 @@ static void build_mont(const Big& m, MontCtxT<NL>& c) {
   c.mp = (0u - inv) & FBM_LMASK;
 }
 
-static int build_jl_params(const uint32_t* biprime, int es, int cr, uint64_t tau, JlParams& jp) {
+static int build_jl_params(const uint32_t* biprime, int es, int cr, uint64_t tau, uint64_t ct_offset, JlParams& jp) {
   memset(&jp, 0, sizeof(jp));
   Big N(biprime, biprime + 32);
   const int nb = big_bits(N);
@@ -155,6 +158,7 @@ static int build_jl_params(const uint32_t* biprime, int es, int cr, uint64_t tau
   jp.es = es;
   jp.cr = cr;
   jp.tau = tau;
+  jp.ct_offset = ct_offset;
   // SHA-256 midstate over the 14 leading all-zero blocks of t.to_bytes(1024,'big')
   uint32_t st[8], W[16];
   fbm_sha256_init(st);
@@ -221,6 +225,33 @@ static uint64_t table_slots_for(uint64_t n_ct) {
 
 static uint64_t align256(uint64_t v) { return (v + 255) & ~255ull; }
 
+// ---------------------------------------------------------------------------------------
+// optional per-kernel event timer (fbm_prof_enable / fbm_prof_report): records a HIP event
+// pair on the launch stream around each kernel launch; costs nothing when disabled.
+// ---------------------------------------------------------------------------------------
+struct ProfRec {
+  const char* name;
+  hipEvent_t a, b;
+};
+static std::mutex g_prof_mu;
+static bool g_prof_on = false;
+static std::vector<ProfRec> g_prof;
+static std::map<std::string, std::pair<long, double>> g_prof_agg;
+
+template <class F>
+static int timed(const char* name, hipStream_t s, F f) {
+  if (!g_prof_on) return f();
+  ProfRec r{name, nullptr, nullptr};
+  hipEventCreate(&r.a);
+  hipEventCreate(&r.b);
+  hipEventRecord(r.a, s);
+  const int rc = f();
+  hipEventRecord(r.b, s);
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  g_prof.push_back(r);
+  return rc;
+}
+
 static void fill_peers(LomPeers& pe, const uint8_t* nonce, uint64_t tau) {
   memset(&pe, 0, sizeof(pe));
   uint32_t iv[4];
@@ -278,7 +309,8 @@ int fbm_check_stats(const uint32_t* st, int lom_nodes, uint32_t* max_bits_out) {
 
 int fbm_lom_protect(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
                     uint64_t target_m1, uint64_t weight, const uint8_t* secrets, const int8_t* signs, int n_peers,
-                    int raw_seeds, const uint8_t* nonce, uint64_t tau, uint64_t* y, uint32_t* stats, void* stream) {
+                    int raw_seeds, const uint8_t* nonce, uint64_t tau, uint64_t elem_offset, uint64_t* y,
+                    uint32_t* stats, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   int rc = zero_stats(stats, s);
   if (rc) return rc;
@@ -296,8 +328,13 @@ int fbm_lom_protect(const void* x, int x_dtype, uint64_t n, double clip, double 
     set_error("null pointer argument");
     return FBM_E_ARG;
   }
-  // PRF.eval_vector guard (_lom.py:74-78) and (i + tau).to_bytes(8) range
-  if (n + 1000ull > (1ull << 61) || (n > 0 && tau > ~0ull - (n - 1))) {
+  // PRF.eval_vector guard (_lom.py:74-78) and (i + tau).to_bytes(8) range, on global indices
+  if ((elem_offset & 7ull) != 0) {
+    set_error("elem_offset must be a multiple of 8 (ChaCha20 block aligned shard)");
+    return FBM_E_ARG;
+  }
+  const uint64_t n_glob = elem_offset + n;
+  if (n_glob < n || n_glob + 1000ull > (1ull << 61) || (n > 0 && tau > ~0ull - (n_glob - 1))) {
     set_error("Can not perform encryiton due to large input vector");
     return FBM_E_ARG;
   }
@@ -305,11 +342,12 @@ int fbm_lom_protect(const void* x, int x_dtype, uint64_t n, double clip, double 
   fill_peers(pe, nonce, tau);
   pe.n_peers = n_peers;
   pe.raw_seeds = raw_seeds;
+  pe.elem_offset = elem_offset;
   for (int p = 0; p < n_peers; ++p) {
     memcpy(pe.secret[p], secrets + 32 * p, 32);
     pe.sign[p] = signs[p] >= 0 ? 1 : -1;
   }
-  return launch_lom_protect(x, x_dtype, n, qp, weight, pe, y, stats, s);
+  return timed("lom_protect", s, [&] { return launch_lom_protect(x, x_dtype, n, qp, weight, pe, y, stats, s); });
 }
 
 int fbm_prf_key(const uint8_t* secret, const uint8_t* nonce, uint64_t tau, uint8_t* seed_out, void* stream) {
@@ -342,7 +380,7 @@ int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t tot
               (unsigned long long)total_weight);
     return FBM_E_ARG;
   }
-  return launch_lom_aggregate(y, n_parties, n, total_weight, neg_clip, step, out, sums, stats, s);
+  return timed("lom_aggregate", s, [&] { return launch_lom_aggregate(y, n_parties, n, total_weight, neg_clip, step, out, sums, stats, s); });
 }
 
 // encrypt workspace: ops | pt [n_ct][32] | nude (blocked) | H [n_ct][64] | table
@@ -361,8 +399,8 @@ uint64_t fbm_jl_aggregate_workspace(uint64_t n_ct) {
 
 int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
                    uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime, const uint32_t* key,
-                   int key_negative, uint64_t tau, uint32_t* ct_out, void* workspace, uint32_t* stats,
-                   void* stream) {
+                   int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* ct_out, void* workspace,
+                   uint32_t* stats, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   int rc = zero_stats(stats, s);
   if (rc) return rc;
@@ -391,7 +429,7 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
     return FBM_E_ARG;
   }
   JlParams jp;
-  if ((rc = build_jl_params(biprime, es, cr, tau, jp))) return rc;
+  if ((rc = build_jl_params(biprime, es, cr, tau, ct_offset, jp))) return rc;
   JlSched sc;
   int is_zero = 0;
   if ((rc = build_schedule(key, sc, is_zero))) {
@@ -410,14 +448,14 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
   uint32_t* H = (uint32_t*)(ws + off);
   off += align256(n_ct * 64 * 4);
   uint32_t* table = (uint32_t*)(ws + off);
-  if ((rc = launch_jl_pack(x, x_dtype, n, qp, weight, es, cr, n_ct, pt, s))) return rc;
-  if ((rc = launch_jl_nude(pt, n_ct, jp, nude, s))) return rc;
-  if (!is_zero && (rc = launch_jl_fdh(n_ct, jp, H, stats, s))) return rc;
-  return launch_jl_exp(H, n_ct, jp, sc, 0, nude, table, slots, ops, ct_out, s);
+  if ((rc = timed("jl_pack", s, [&] { return launch_jl_pack(x, x_dtype, n, qp, weight, es, cr, n_ct, pt, s); }))) return rc;
+  if ((rc = timed("jl_nude", s, [&] { return launch_jl_nude(pt, n_ct, jp, nude, s); }))) return rc;
+  if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, H, stats, s); }))) return rc;
+  return timed("jl_exp", s, [&] { return launch_jl_exp(H, n_ct, jp, sc, 0, nude, table, slots, ops, ct_out, s); });
 }
 
 int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,
-                     const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau,
+                     const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau, uint64_t ct_offset,
                      uint64_t total_weight, double neg_clip, double step, double* out, uint64_t* sums,
                      void* workspace, uint32_t* stats, void* stream) {
   hipStream_t s = (hipStream_t)stream;
@@ -434,7 +472,7 @@ int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, 
     return FBM_E_ARG;
   }
   JlParams jp;
-  if ((rc = build_jl_params(biprime, es, cr, tau, jp))) return rc;
+  if ((rc = build_jl_params(biprime, es, cr, tau, ct_offset, jp))) return rc;
   JlSched sc;
   int is_zero = 0;
   if ((rc = build_schedule(key, sc, is_zero))) {
@@ -457,16 +495,57 @@ int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, 
   uint32_t* xs = (uint32_t*)(ws + off);
   off += align256(n_ct * 32 * 4);
   uint32_t* table = (uint32_t*)(ws + off);
-  if ((rc = launch_jl_prod(cts, n_parties, n_ct, jp, X, s))) return rc;
-  if (!is_zero && (rc = launch_jl_fdh(n_ct, jp, H, stats, s))) return rc;
-  if ((rc = launch_jl_exp(H, n_ct, jp, sc, 1, nullptr, table, slots, ops, E, s))) return rc;
+  if ((rc = timed("jl_prod", s, [&] { return launch_jl_prod(cts, n_parties, n_ct, jp, X, s); }))) return rc;
+  if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, H, stats, s); }))) return rc;
+  if ((rc = timed("jl_exp", s, [&] { return launch_jl_exp(H, n_ct, jp, sc, 1, nullptr, table, slots, ops, E, s); }))) return rc;
   if (key_negative && !is_zero) {
-    if ((rc = launch_jl_inv(n_ct, jp, E, xs, inv, stats, s))) return rc;  // xs doubles as y scratch
+    if ((rc = timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, E, xs, inv, stats, s); }))) return rc;  // xs doubles as y scratch
   } else {
     inv = E;  // positive (or zero) server key: v = prod * H^sk0, no inverse
   }
-  if ((rc = launch_jl_fin(n_ct, jp, X, inv, xs, s))) return rc;
-  return launch_jl_decode(xs, es, cr, n_out, total_weight, neg_clip, step, out, sums, stats, s);
+  if ((rc = timed("jl_fin", s, [&] { return launch_jl_fin(n_ct, jp, X, inv, xs, s); }))) return rc;
+  return timed("jl_decode", s, [&] { return launch_jl_decode(xs, es, cr, n_out, total_weight, neg_clip, step, out, sums, stats, s); });
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int fbm_prof_enable(int on) {
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  g_prof_on = on != 0;
+  return FBM_OK;
+}
+
+// Synchronises the recorded events and writes "name count total_ms\n" lines (sorted by
+// name) into buf; clears the records.  Returns the number of bytes needed.
+int fbm_prof_report(char* buf, int len) {
+  // Folds completed event pairs into g_prof_agg; the aggregate is only handed out (and
+  // cleared) when buf can hold all of it, so a size query (buf == NULL) loses nothing.
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  for (auto& r : g_prof) {
+    hipEventSynchronize(r.b);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, r.a, r.b);
+    auto& e = g_prof_agg[r.name];
+    e.first += 1;
+    e.second += ms;
+    hipEventDestroy(r.a);
+    hipEventDestroy(r.b);
+  }
+  g_prof.clear();
+  std::string out;
+  for (auto& kv : g_prof_agg) {
+    char line[160];
+    snprintf(line, sizeof(line), "%s %ld %.6f\n", kv.first.c_str(), kv.second.first, kv.second.second);
+    out += line;
+  }
+  const int need = (int)out.size() + 1;
+  if (buf && len >= need) {
+    memcpy(buf, out.c_str(), (size_t)need);
+    g_prof_agg.clear();
+  }
+  return need;
 }
 
 }  // extern "C"

@@ -24,6 +24,7 @@ struct LomPeers {
   uint64_t ctr0;                 // nonce bytes 0-7 (LE) = 64-bit ChaCha20 block counter
   uint32_t n14, n15;             // nonce bytes 8-15 (LE words)
   uint64_t tau;                  // round
+  uint64_t elem_offset;          // global index of x[0] (element-range shard; multiple of 8)
   uint32_t tau_be[4];            // tau.to_bytes(16, 'big') as LE words
   uint32_t secret[FBM_MAX_PEERS][8];
   int8_t sign[FBM_MAX_PEERS];    // +1: mask += vec (peer < node), -1: mask -= vec
@@ -60,6 +61,7 @@ struct JlParams {
   int n_bits;                    // bit length of N
   int es, cr;                    // VES slot size / slots per ciphertext
   uint64_t tau;
+  uint64_t ct_offset;            // global index of ciphertext 0 (element-range shard)
   uint32_t mid[8];               // SHA-256 state after the 14 all-zero message blocks
   int key_is_zero;
   int pad;

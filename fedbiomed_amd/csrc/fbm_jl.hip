@@ -159,8 +159,9 @@ __device__ bool gcd_is_one(uint32_t (&u)[64], const uint32_t* N32, uint32_t& err
 // is the reference's OverflowError.
 __global__ void __launch_bounds__(256) jl_fdh_kernel(uint64_t n_ct, JlParams jp, uint32_t* __restrict__ H,
                                                      uint32_t* __restrict__ stats) {
-  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_ct) return;
+  const uint64_t kl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (kl >= n_ct) return;
+  const uint64_t k = kl + jp.ct_offset;  // global ciphertext index in t_k = (k << 512) | tau
   uint32_t err = 0;
   uint32_t st[8], W[16];
 #pragma unroll
@@ -196,7 +197,7 @@ __global__ void __launch_bounds__(256) jl_fdh_kernel(uint64_t n_ct, JlParams jp,
     ok = gcd_is_one(u, jp.N32, err);
   }
   if (!ok) err |= FBM_ERR_FDH_OVERFLOW;
-  uint4* o = reinterpret_cast<uint4*>(H + k * 64);
+  uint4* o = reinterpret_cast<uint4*>(H + kl * 64);
 #pragma unroll
   for (int i = 0; i < 16; ++i) o[i] = make_uint4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
   if (err) atomicOr(stats + FBM_STAT_ERRFLAGS, err);

@@ -73,7 +73,7 @@ __global__ void __launch_bounds__(256) lom_protect_kernel(const XT* __restrict__
   uint64_t mask[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) mask[j] = 0;
-  const uint64_t ctr = peers.ctr0 + blk;
+  const uint64_t ctr = peers.ctr0 + (peers.elem_offset >> 3) + blk;  // global ChaCha20 block
   for (int p = 0; p < peers.n_peers; ++p) {
     uint32_t key[8];
 #pragma unroll
@@ -83,7 +83,7 @@ __global__ void __launch_bounds__(256) lom_protect_kernel(const XT* __restrict__
     const bool add = peers.sign[p] > 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const uint64_t idx = base + (uint64_t)j + peers.tau;
+      const uint64_t idx = peers.elem_offset + base + (uint64_t)j + peers.tau;
       const uint64_t m = (((uint64_t)ks[2 * j + 1] << 32) | ks[2 * j]) ^ fbm_bswap64(idx);
       mask[j] = add ? mask[j] + m : mask[j] - m;
     }

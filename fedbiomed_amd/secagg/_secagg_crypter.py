@@ -79,8 +79,9 @@ class SecaggCrypter:
     # ---- device fast path ------------------------------------------------------------------
     def encrypt_tensor(self, num_nodes: int, current_round: int, params: torch.Tensor, key: int, biprime: int,
                        clipping_range: Union[int, None] = None, weight: Optional[int] = None,
-                       target_range: Optional[int] = None) -> torch.Tensor:
-        """Device tensor (f32/f64) in HBM -> int32 [n_ct, 64] ciphertext limbs in HBM."""
+                       target_range: Optional[int] = None, ct_offset: int = 0) -> torch.Tensor:
+        """Device tensor (f32/f64) in HBM -> int32 [n_ct, 64] ciphertext limbs in HBM.
+        `ct_offset`: global index of this shard's first ciphertext (element-range sharding)."""
         if not isinstance(key, int):
             raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: The argument `key` must be integer")
         target_range = target_range or SAParameters.TARGET_RANGE
@@ -88,7 +89,7 @@ class SecaggCrypter:
         _warn_clipping(params, clipping_range)
         try:
             return D.jl_encrypt(params, biprime, key, current_round, num_nodes, clip=clipping_range,
-                                target=target_range, weight=1 if weight is None else weight)
+                                target=target_range, weight=1 if weight is None else weight, ct_offset=ct_offset)
         except (TypeError, ValueError) as exp:
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value} Error during parameter encryption. {exp}") from exp
@@ -96,13 +97,14 @@ class SecaggCrypter:
     def aggregate_tensor(self, current_round: int, cts: torch.Tensor, key: int, biprime: int,
                          total_sample_size: int, clipping_range: Union[int, None] = None,
                          num_expected_params: int = 1, target_range: Optional[int] = None,
-                         want_sums: bool = False):
+                         want_sums: bool = False, ct_offset: int = 0):
         """[P, n_ct, 64] int32 ciphertext limbs in HBM -> float64 [n] averaged parameters."""
         if not isinstance(key, int):
             raise TypeError("The key should be type of integer")
         target_range = target_range or SAParameters.TARGET_RANGE
         out, sums = D.jl_aggregate(cts, biprime, key, current_round, num_expected_params, total_sample_size,
-                                   clip=clipping_range, target=target_range, want_sums=want_sums)
+                                   clip=clipping_range, target=target_range, want_sums=want_sums,
+                                   ct_offset=ct_offset)
         return (out, sums) if want_sums else out
 
     # ---- reference API -----------------------------------------------------------------------
@@ -192,8 +194,9 @@ class SecaggLomCrypter(SecaggCrypter):
     def encrypt_tensor(self, current_round: int, node_id: str, params: torch.Tensor,
                        pairwise_secrets: Dict[str, bytes], node_ids: List[str],
                        clipping_range: Union[int, None] = None, weight: Optional[int] = None,
-                       target_range: Optional[int] = None) -> torch.Tensor:
-        """Device tensor (f32/f64) -> masked uint64 vector (int64 tensor) in HBM."""
+                       target_range: Optional[int] = None, elem_offset: int = 0) -> torch.Tensor:
+        """Device tensor (f32/f64) -> masked uint64 vector (int64 tensor) in HBM.
+        `elem_offset`: global index of this shard's first element (multiple of 8)."""
         target_range = target_range or SAParameters.TARGET_RANGE
         _check_weight(weight, jl=False)
         _warn_clipping(params, clipping_range)
@@ -207,7 +210,8 @@ class SecaggLomCrypter(SecaggCrypter):
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value} Error during parameter encryption. math domain error")
         return D.lom_protect(params, secrets_, signs, self._nonce, current_round, len(node_ids),
-                             clip=clipping_range, target=target_range, weight=1 if weight is None else weight)
+                             clip=clipping_range, target=target_range, weight=1 if weight is None else weight,
+                             elem_offset=elem_offset)
 
     def aggregate_tensor(self, Y: torch.Tensor, total_sample_size: int, clipping_range: Union[int, None] = None,
                          target_range: Optional[int] = None, want_sums: bool = False):

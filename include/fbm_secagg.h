@@ -68,11 +68,15 @@ int fbm_check_stats(const uint32_t* host_stats, int lom_nodes, uint32_t* max_bit
  *              1: secrets already are PRF seeds (PRF.eval_vector semantics)
  *   nonce      HOST, 16 bytes (str.encode(nonce).zfill(16)[:16])
  *   y          device, n uint64 (masked output)
+ *   elem_offset global index of x[0] when the element range is sharded across devices
+ *              (multiple of 8; 0 for a whole vector): PRF block counter and (i + tau) use
+ *              global indices, so shards concatenate to the unsharded result.
  * With x_dtype == FBM_U64, x holds integers used as-is (x == NULL: zeros) and only the
  * weight multiplies them (weight 1 = LOM.protect semantics).                           */
 int fbm_lom_protect(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
                     uint64_t target_m1, uint64_t weight, const uint8_t* secrets, const int8_t* signs, int n_peers,
-                    int raw_seeds, const uint8_t* nonce, uint64_t tau, uint64_t* y, uint32_t* stats, void* stream);
+                    int raw_seeds, const uint8_t* nonce, uint64_t tau, uint64_t elem_offset, uint64_t* y,
+                    uint32_t* stats, void* stream);
 
 /* PRF.eval_key (_lom.py:30-56): seed_out (device, 32 bytes) = ChaCha20(secret, nonce)
  * keystream[0:16] XOR tau.to_bytes(16,'big') || 16 zero bytes.   secret, nonce: HOST.   */
@@ -95,7 +99,9 @@ int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t tot
  * biprime: HOST, 32 limbs (N, odd, 3 <= N < 2^1024)
  * key:     HOST, 64 limbs |sk| (< 2^2048);  key_negative: sign of sk
  * es, cr:  VES slot bits / slots per ciphertext (JoyeLibert vector encoder, _jls.py:104-116)
- * tau:     round (< 2^64); n_ct = ceil(n / cr)                                           */
+ * tau:     round (< 2^64); n_ct = ceil(n / cr)
+ * ct_offset: global index of ciphertext 0 (t_k = ((k + ct_offset) << 512) | tau) when the
+ *          element range is sharded across devices on ciphertext boundaries; 0 otherwise.   */
 
 /* bytes of device workspace fbm_jl_encrypt / fbm_jl_aggregate need */
 uint64_t fbm_jl_encrypt_workspace(uint64_t n_ct);
@@ -107,8 +113,8 @@ uint64_t fbm_jl_aggregate_workspace(uint64_t n_ct);
  *   ct_out: device, n_ct x 64 uint32 limbs                                                */
 int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
                    uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,
-                   const uint32_t* key, int key_negative, uint64_t tau, uint32_t* ct_out, void* workspace,
-                   uint32_t* stats, void* stream);
+                   const uint32_t* key, int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* ct_out,
+                   void* workspace, uint32_t* stats, void* stream);
 
 /* JL aggregate: prod_u c_u * H(t_k)^sk0 mod N^2, x = ((v-1)//N) mod N, VES decode,
  * average, dequantise.  Replaces SecaggCrypter.aggregate (_secagg_crypter.py:139-230) =
@@ -120,8 +126,16 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
  *   sums: device, n_out x 2 uint64 (lo, hi) decoded integer sums (may be NULL)            */
 int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,
                      const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau,
-                     uint64_t total_weight, double neg_clip, double step, double* out, uint64_t* sums,
+                     uint64_t ct_offset, uint64_t total_weight, double neg_clip, double step, double* out, uint64_t* sums,
                      void* workspace, uint32_t* stats, void* stream);
+
+/* ---- instrumentation -------------------------------------------------------------------
+ * fbm_prof_enable(1) makes every entry point record a HIP event pair around each kernel
+ * launch (on the caller's stream); fbm_prof_report() synchronises them and returns the
+ * bytes needed for the "kernel count total_ms" lines; when len >= that, it writes them
+ * into buf and clears the aggregate (buf == NULL is a non-destructive size query).       */
+int fbm_prof_enable(int on);
+int fbm_prof_report(char* buf, int len);
 
 #ifdef __cplusplus
 }
