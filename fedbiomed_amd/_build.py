@@ -16,7 +16,6 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_lib", "libfbm_secagg.so")
 SOURCES = ["fbm_lom.hip", "fbm_jl.hip", "fbm_capi.hip"]
-HEADERS = ["fbm_common.hpp", "fbm_mont.hpp", "fbm_internal.hpp"]
 ARCH = os.environ.get("FBM_OFFLOAD_ARCH", "gfx950")
 
 
@@ -31,7 +30,9 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "fbm_secagg.h")]
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp"))]
+    inc = os.path.join(ROOT, "include")
+    deps += [os.path.join(inc, f) for f in os.listdir(inc) if f.endswith(".h")]
     return any(os.path.getmtime(d) > t for d in deps)
 
 

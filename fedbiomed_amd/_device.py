@@ -69,6 +69,40 @@ def _call(fn, *args) -> None:
         _raise(rc)
 
 
+class deferred_checks:
+    """Within this context the device status words of JL encrypts are checked once, at exit,
+    instead of after every call (each check synchronises its stream).  This lets the
+    encrypts of several parties issued on different HIP streams overlap on the GPU; any
+    error is still raised, from the `with` statement's exit.
+
+        with D.deferred_checks():
+            for p, s in enumerate(streams):
+                with torch.cuda.stream(s):
+                    cts[p] = D.jl_encrypt(...)
+    """
+
+    _active: List[list] = []
+
+    def __enter__(self):
+        deferred_checks._active.append([])
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        pending = deferred_checks._active.pop()
+        if exc_type is None and pending:
+            torch.cuda.synchronize()  # the status words were written on other streams
+            for st, nodes in pending:
+                _check_stats(st, nodes)
+        return False
+
+
+def _check_stats_or_defer(stats: torch.Tensor, lom_nodes: int = 0) -> None:
+    if deferred_checks._active:
+        deferred_checks._active[-1].append((stats, lom_nodes))
+    else:
+        _check_stats(stats, lom_nodes)
+
+
 def _check_stats(stats: torch.Tensor, lom_nodes: int = 0) -> int:
     host = stats.cpu().numpy().astype(np.uint32)  # synchronises the stream
     mb = ctypes.c_uint32(0)
@@ -297,7 +331,7 @@ def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, 
     st = _stats(dev)
     _call(lib.fbm_jl_encrypt, _ptr(x), _x_dtype(x), n, c, c2, tf, tm1, int(weight), es, cr, _np_ptr(bp),
           _np_ptr(kl), kneg, int(tau), int(ct_offset), _ptr(ct), _ptr(ws), _ptr(st), _stream())
-    _check_stats(st)
+    _check_stats_or_defer(st)
     return ct
 
 

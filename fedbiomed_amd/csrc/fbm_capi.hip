@@ -244,6 +244,10 @@ static int timed(const char* name, hipStream_t s, F f) {
   ProfRec r{name, nullptr, nullptr};
   hipEventCreate(&r.a);
   hipEventCreate(&r.b);
+  // Drain the stream first: a marker can otherwise complete while the previous kernel is
+  // still running, and its interval would absorb that kernel's tail (measured: per-kernel
+  // sums 2.3x the wall time).  Profiling mode therefore serialises host and device.
+  hipStreamSynchronize(s);
   hipEventRecord(r.a, s);
   const int rc = f();
   hipEventRecord(r.b, s);
@@ -386,15 +390,15 @@ int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t tot
 // encrypt workspace: ops | pt [n_ct][32] | nude (blocked) | H [n_ct][64] | table
 uint64_t fbm_jl_encrypt_workspace(uint64_t n_ct) {
   const uint64_t slots = table_slots_for(n_ct);
-  return align256(FBM_MAX_OPS * 4) + align256(n_ct * 32 * 4) + align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4) + align256(n_ct * 64 * 4) +
-         align256(slots * FBM_TABLE * FBM_NL * 4);
+  return align256(FBM_MAX_OPS * 4) + align256(FBM_CST_WORDS * 4) + align256(n_ct * 32 * 4) +
+         align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4) + align256(n_ct * 64 * 4) +
+         align256(slots * FBM_TENTRIES * FBM_NL * 4);
 }
 
-// aggregate workspace: ops | X (blocked) | H [n_ct][64] | E [n_ct][64] | inv [n_ct][64] | xs [n_ct][32] | table
 uint64_t fbm_jl_aggregate_workspace(uint64_t n_ct) {
   const uint64_t slots = table_slots_for(n_ct);
-  return align256(FBM_MAX_OPS * 4) + align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4) + 3 * align256(n_ct * 64 * 4) + align256(n_ct * 32 * 4) +
-         align256(slots * FBM_TABLE * FBM_NL * 4);
+  return align256(FBM_MAX_OPS * 4) + align256(FBM_CST_WORDS * 4) + align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4) +
+         3 * align256(n_ct * 64 * 4) + align256(n_ct * 32 * 4) + align256(slots * FBM_TENTRIES * FBM_NL * 4);
 }
 
 int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
@@ -424,6 +428,11 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
     return FBM_E_ARG;
   }
   const uint64_t n_ct = (n + (uint64_t)cr - 1) / (uint64_t)cr;
+  if (n_ct > FBM_JL_MAX_CT) {
+    set_error("%llu ciphertexts exceed FBM_JL_MAX_CT per call; split the range with ct_offset",
+              (unsigned long long)n_ct);
+    return FBM_E_UNSUPPORTED;
+  }
   if (!x || !ct_out || !workspace) {
     set_error("null pointer argument");
     return FBM_E_ARG;
@@ -441,6 +450,8 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
   uint8_t* ws = (uint8_t*)workspace;
   uint32_t* ops = (uint32_t*)ws;
   uint64_t off = align256(FBM_MAX_OPS * 4);
+  uint32_t* cst = (uint32_t*)(ws + off);
+  off += align256(FBM_CST_WORDS * 4);
   uint32_t* pt = (uint32_t*)(ws + off);
   off += align256(n_ct * 32 * 4);
   uint32_t* nude = (uint32_t*)(ws + off);
@@ -448,10 +459,11 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
   uint32_t* H = (uint32_t*)(ws + off);
   off += align256(n_ct * 64 * 4);
   uint32_t* table = (uint32_t*)(ws + off);
+  if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s); }))) return rc;
   if ((rc = timed("jl_pack", s, [&] { return launch_jl_pack(x, x_dtype, n, qp, weight, es, cr, n_ct, pt, s); }))) return rc;
   if ((rc = timed("jl_nude", s, [&] { return launch_jl_nude(pt, n_ct, jp, nude, s); }))) return rc;
   if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, H, stats, s); }))) return rc;
-  return timed("jl_exp", s, [&] { return launch_jl_exp(H, n_ct, jp, sc, 0, nude, table, slots, ops, ct_out, s); });
+  return timed("jl_exp", s, [&] { return launch_jl_exp(H, n_ct, jp, sc, 0, nude, table, slots, ops, cst, ct_out, s); });
 }
 
 int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,
@@ -464,6 +476,11 @@ int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, 
   if (n_parties < 1 || !biprime || !key || total_weight == 0) {
     set_error("invalid aggregate arguments");
     return FBM_E_ARG;
+  }
+  if (n_ct > FBM_JL_MAX_CT) {
+    set_error("%llu ciphertexts exceed FBM_JL_MAX_CT per call; split the range with ct_offset",
+              (unsigned long long)n_ct);
+    return FBM_E_UNSUPPORTED;
   }
   if (n_ct == 0) return FBM_OK;
   if (n_out > n_ct * (uint64_t)cr) n_out = n_ct * (uint64_t)cr;
@@ -484,6 +501,8 @@ int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, 
   uint8_t* ws = (uint8_t*)workspace;
   uint32_t* ops = (uint32_t*)ws;
   uint64_t off = align256(FBM_MAX_OPS * 4);
+  uint32_t* cst = (uint32_t*)(ws + off);
+  off += align256(FBM_CST_WORDS * 4);
   uint32_t* X = (uint32_t*)(ws + off);
   off += align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4);
   uint32_t* H = (uint32_t*)(ws + off);
@@ -495,9 +514,10 @@ int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, 
   uint32_t* xs = (uint32_t*)(ws + off);
   off += align256(n_ct * 32 * 4);
   uint32_t* table = (uint32_t*)(ws + off);
-  if ((rc = timed("jl_prod", s, [&] { return launch_jl_prod(cts, n_parties, n_ct, jp, X, s); }))) return rc;
+  if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s); }))) return rc;
+  if ((rc = timed("jl_prod", s, [&] { return launch_jl_prod(cts, n_parties, n_ct, jp, cst, X, s); }))) return rc;
   if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, H, stats, s); }))) return rc;
-  if ((rc = timed("jl_exp", s, [&] { return launch_jl_exp(H, n_ct, jp, sc, 1, nullptr, table, slots, ops, E, s); }))) return rc;
+  if ((rc = timed("jl_exp", s, [&] { return launch_jl_exp(H, n_ct, jp, sc, 1, nullptr, table, slots, ops, cst, E, s); }))) return rc;
   if (key_negative && !is_zero) {
     if ((rc = timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, E, xs, inv, stats, s); }))) return rc;  // xs doubles as y scratch
   } else {

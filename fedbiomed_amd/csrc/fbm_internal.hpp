@@ -45,6 +45,16 @@ int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t 
 #define FBM_WIN 5
 #define FBM_TABLE (1 << (FBM_WIN - 1))  // odd powers h^1, h^3, ..., h^31
 #define FBM_MAX_OPS 512
+#define FBM_TENTRIES (FBM_TABLE + 1)    // + one scratch column (h, then h^2)
+#define FBM_TSCRATCH FBM_TABLE
+
+// per-call device constants (words): M, R^2 (74 limbs, padded to 128) and the broadcast
+// columns 1 and R^2 (limb k at word k*256)
+#define FBM_CST_M 0
+#define FBM_CST_R2 128
+#define FBM_CST_ONE 256
+#define FBM_CST_R2COL (256 + FBM_NL * 256)
+#define FBM_CST_WORDS (256 + 2 * FBM_NL * 256)
 
 // sliding-window schedule, passed by value (kernarg segment -> scalar loads).
 // op k (u16): (squarings before the multiply) << 5 | (table index + 1, 0 = none)
@@ -71,11 +81,12 @@ int launch_jl_pack(const void* x, int x_dtype, uint64_t n, const QuantParams& qp
                    uint64_t n_ct, uint32_t* pt, hipStream_t s);
 int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, uint32_t* nude, hipStream_t s);
 int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s);
+int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32_t* cst, hipStream_t s);
 int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const JlSched& sc, int mode,
-                  const uint32_t* nude, uint32_t* table, uint64_t table_slots, uint32_t* ops, uint32_t* out,
-                  hipStream_t s);
-int launch_jl_prod(const uint32_t* cts, int n_parties, uint64_t n_ct, const JlParams& jp, uint32_t* X,
-                   hipStream_t s);
+                  const uint32_t* nude, uint32_t* table, uint64_t table_slots, const uint32_t* ops,
+                  const uint32_t* cst, uint32_t* out, hipStream_t s);
+int launch_jl_prod(const uint32_t* cts, int n_parties, uint64_t n_ct, const JlParams& jp, const uint32_t* cst,
+                   uint32_t* X, hipStream_t s);
 int launch_jl_inv(uint64_t n_ct, const JlParams& jp, const uint32_t* E, uint32_t* Y, uint32_t* inv, uint32_t* stats,
                   hipStream_t s);
 int launch_jl_fin(uint64_t n_ct, const JlParams& jp, const uint32_t* X, const uint32_t* inv, uint32_t* xout,

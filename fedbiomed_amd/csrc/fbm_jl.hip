@@ -19,6 +19,7 @@
 // ciphertexts: 64 words = int.to_bytes(256,'little')); 28-bit-limb residues (nude, X) and
 // the per-lane exponent tables are limb-major [limb][lane] so a wave's accesses coalesce.
 #include "fbm_internal.hpp"
+#include "fbm_mont_asm.hpp"
 
 namespace fbm {
 
@@ -227,175 +228,140 @@ __device__ __forceinline__ void store_row64(uint32_t* p, const uint32_t (&w)[64]
   for (int i = 0; i < 16; ++i) o[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
 }
 
+// ------------------------------------------------------------------------------------
+// The two hot kernels below run on the assembly Montgomery product (fbm_mont_asm.hpp):
+// the running residue lives in the lane's LDS column (75 limb rows, 2 workgroups/CU =
+// 2 waves/SIMD), B operands come from that column (squaring) or from workgroup-blocked
+// global columns (table entries, nude, scratch, broadcast constants).  Everything around
+// the products is wave-uniform.
+// ------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ uint32_t lds_addr(uint32_t* p) { return (uint32_t)(uintptr_t)(lds_u32*)p; }
+
+// LDS column <-> workgroup-blocked global column (limb stride 256 words)
+__device__ __forceinline__ void lds_to_glb(const uint32_t* lds, uint32_t* g) {
+  uint32_t v[FBM_NL];
+  lds_load_col(lds, FBM_BLOCK, v);
+  col_store(g, v);
+}
+__device__ __forceinline__ void glb_to_lds(const uint32_t* g, uint32_t* lds) {
+  uint32_t v[FBM_NL];
+  col_load(g, v);
+  lds_store_col(lds, FBM_BLOCK, v);
+}
+
 // mode 0 (ENC): out[ct] = nude[ct] * H[ct]^key  mod N^2          (ciphertext)
 // mode 1 (DEC): out[ct] = H[ct]^key mod N^2 (plain)                (for the inverse)
-//
-// Sliding window (width FBM_WIN) over a host-built schedule: uniform control flow.
-// The kernel is ONE loop around ONE Montgomery product (~90 KB of fully unrolled code).
-// No residue is carried in registers across iterations: the running value lives in the
-// per-lane LDS column (the A operand of the next product) and each iteration re-loads its
-// B operand (from that column for a squaring, from the per-lane table for a multiply).
-// That keeps the product's 146 + 74 live VGPRs the kernel's peak (2 waves/SIMD).
-//   phase 0  to Montgomery:  a = R^2 (uniform)   b = h          -> table[0], LDS
-//   phase 1  h^2:            a = h*R             b = h*R        -> LDS (multiplier)
-//   phase 2  odd powers:     a = h^2             b = table[t-1] -> table[t]
-//   phase 3  window steps:   a = acc             b = acc | table[idx] -> LDS
-//   phase 4  final:          a = nude | 1        b = acc        -> out (fully reduced)
-__global__ void __launch_bounds__(FBM_BLOCK, 1) jl_exp_kernel(const uint32_t* __restrict__ H, uint64_t n_ct,
-                                                             JlParams jp, const uint32_t* __restrict__ ops,
-                                                             int n_ops, int first, int mode,
+// Sliding window (width FBM_WIN, 16 odd powers) over the device copy of the host-built
+// schedule.  Per-lane table: 17 blocked columns (entry 16 = h / h^2 scratch).
+//   a = R^2 (uniform), b = h         -> h*R              -> table[0]
+//   a = h*R,  b = a                  -> h^2*R            -> table[16]
+//   a = h^(2t-1)*R, b = table[16]    -> h^(2t+1)*R       -> table[t], t = 1..15
+//   a = table[first], then per op: nsq squarings, one product with table[idx]
+//   a = acc,  b = nude | 1           -> c | h^key (plain, lazily reduced) -> csub -> out
+// Uniform round loop over ciphertexts (lanes past the end redo the last one, store nothing).
+__global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __restrict__ H, uint64_t n_ct,
+                                                             const uint32_t* __restrict__ cst, uint32_t mp,
+                                                             const uint32_t* __restrict__ ops, int n_ops,
+                                                             int first, int mode, int key_is_zero,
                                                              const uint32_t* __restrict__ nude,
                                                              uint32_t* __restrict__ table,
                                                              uint32_t* __restrict__ out) {
-  __shared__ uint32_t lds_a[FBM_NL * FBM_BLOCK];
+  __shared__ uint32_t lds_a[(FBM_NL + 1) * FBM_BLOCK];
   const int tid = threadIdx.x;
   uint32_t* lds = lds_a + tid;
-  const int ls = FBM_BLOCK;
+  const uint32_t aoff = lds_addr(lds);
+  const uint32_t* M = cst + FBM_CST_M;
   const uint64_t G = (uint64_t)gridDim.x * FBM_BLOCK;
   const uint64_t gtid = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
-  uint32_t* tb = table + (uint64_t)blockIdx.x * (FBM_TABLE * FBM_NL * FBM_BLOCK) + tid;
-
-  // Uniform round loop (every lane runs the same number of rounds; lanes past the end
-  // redo the last ciphertext and skip the store): all control flow below is wave-uniform,
-  // so the phase machine compiles to scalar branches and no exec-masked merge keeps two
-  // copies of the residue alive.
+  // byte offset of this lane's table entry 0 (entries FBM_NL*256 words apart)
+  const uint32_t tb0 = (uint32_t)(((uint64_t)blockIdx.x * FBM_TENTRIES * FBM_NL * FBM_BLOCK + tid) * 4);
+  const uint32_t tstride = FBM_NL * FBM_BLOCK * 4;
   const uint64_t rounds = (n_ct + G - 1) / G;
+#pragma unroll 1
   for (uint64_t r = 0; r < rounds; ++r) {
     const uint64_t ct_raw = gtid + r * G;
     const bool valid = ct_raw < n_ct;
     const uint64_t ct = valid ? ct_raw : n_ct - 1;
-    int phase = 0, t = 0, k = 0, s = 0;
-#pragma unroll 1
-    for (;;) {
-      // opaque state: keeps the optimiser from threading the phase machine through the
-      // loop (which would clone the product once per phase)
-      phase = __builtin_amdgcn_readfirstlane(phase);
-      t = __builtin_amdgcn_readfirstlane(t);
-      k = __builtin_amdgcn_readfirstlane(k);
-      s = __builtin_amdgcn_readfirstlane(s);
-      asm volatile("" : "+s"(phase), "+s"(t), "+s"(k), "+s"(s));
-      uint32_t acc[FBM_NL];
-      // ---- stage B (and A where it changes) ----
-      bool mul = false;
-      int idx = -1;
-      if (phase == 3) {
-        const uint32_t op = __builtin_amdgcn_readfirstlane(ops[k]);
-        mul = s >= (int)(op >> 5);
-        idx = (int)(op & 31u) - 1;
-      }
-      if (phase == 0) {
-        uint32_t h[64];
-        if (jp.key_is_zero) {
+    {  // h -> 28-bit limbs -> scratch entry 16
+      uint32_t h[64];
+      if (key_is_zero) {
 #pragma unroll
-          for (int i = 0; i < 64; ++i) h[i] = i == 0 ? 1u : 0u;
-        } else {
-          load_row64(H + ct * 64, h);
-        }
-        to28<64, FBM_NL>(h, acc);
-        lds_store_uniform<FBM_NL>(lds, ls, jp.mc.R2);
-      } else if (phase == 2) {
-        tbl_load(tb, t - 1, acc);
-      } else if (phase == 3 && mul) {
-        tbl_load(tb, idx, acc);
-      } else {  // squaring (phase 1, 3) or final (phase 4): b = running value
-        lds_load_col(lds, ls, acc);
-        if (phase == 4) {
-          if (mode == 0) {
-            uint32_t nv[FBM_NL];
-            col_load(nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255), nv);
-            lds_store_col(lds, ls, nv);
-          } else {
-            lds_store_one<FBM_NL>(lds, ls);
-          }
-        }
+        for (int i = 0; i < 64; ++i) h[i] = i == 0 ? 1u : 0u;
+      } else {
+        load_row64(H + ct * 64, h);
       }
-      mont_mul(acc, lds, ls, jp.mc);
-      // ---- consume the result ----
-      if (phase == 4) {
-        mont_csub(acc, jp.mc.M);
-        uint32_t w[64];
-        from28<FBM_NL, 64>(acc, w);
-        if (valid) store_row64(out + ct * 64, w);
-        break;
+      uint32_t h28[FBM_NL];
+      to28<64, FBM_NL>(h, h28);
+      col_store(table + (tb0 + FBM_TSCRATCH * tstride) / 4, h28);
+    }
+    lds_store_uniform<FBM_NL>(lds, FBM_BLOCK, cst + FBM_CST_R2);
+    fbm_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, M, mp);  // h*R
+    if (!key_is_zero) {
+      lds_to_glb(lds, table + tb0 / 4);
+      fbm_mm_lds(aoff, aoff, M, mp);  // h^2*R
+      lds_to_glb(lds, table + (tb0 + FBM_TSCRATCH * tstride) / 4);
+      glb_to_lds(table + tb0 / 4, lds);
+#pragma unroll 1
+      for (int t = 1; t < FBM_TABLE; ++t) {
+        fbm_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, M, mp);
+        lds_to_glb(lds, table + (tb0 + (uint32_t)t * tstride) / 4);
       }
-      if (phase == 0) {
-        lds_store_col(lds, ls, acc);
-        if (jp.key_is_zero) {
-          phase = 4;
-        } else {
-          tbl_store(tb, 0, acc);
-          phase = 1;
-        }
-      } else if (phase == 1) {
-        lds_store_col(lds, ls, acc);  // h^2 becomes the multiplier of phase 2
-        phase = 2;
-        t = 1;
-      } else if (phase == 2) {
-        tbl_store(tb, t, acc);
-        if (++t == FBM_TABLE) {
-          uint32_t v[FBM_NL];
-          tbl_load(tb, first, v);
-          lds_store_col(lds, ls, v);
-          phase = n_ops > 0 ? 3 : 4;
-          k = 0;
-          s = 0;
-        }
-      } else {  // phase 3
-        lds_store_col(lds, ls, acc);
-        if (mul) {
-          ++k;
-          s = 0;
-        } else {
-          ++s;
-          const uint32_t op = __builtin_amdgcn_readfirstlane(ops[k]);
-          if (s == (int)(op >> 5) && idx < 0) {
-            ++k;
-            s = 0;
-          }
-        }
-        if (k == n_ops) phase = 4;
+      glb_to_lds(table + (tb0 + (uint32_t)first * tstride) / 4, lds);
+#pragma unroll 1
+      for (int k = 0; k < n_ops; ++k) {
+        const uint32_t op = __builtin_amdgcn_readfirstlane(ops[k]);
+        const int nsq = (int)(op >> 5);
+        const int idx = (int)(op & 31u) - 1;
+#pragma unroll 1
+        for (int q = 0; q < nsq; ++q) fbm_mm_lds(aoff, aoff, M, mp);
+        if (idx >= 0) fbm_mm_glb(aoff, table, tb0 + (uint32_t)idx * tstride, M, mp);
       }
     }
+    if (mode == 0)
+      fbm_mm_glb(aoff, nude, (uint32_t)((((ct >> 8) * (FBM_NL * 256)) + (ct & 255)) * 4), M, mp);
+    else
+      fbm_mm_glb(aoff, cst + FBM_CST_ONE, 0u, M, mp);
+    uint32_t acc[FBM_NL];
+    lds_load_col(lds, FBM_BLOCK, acc);
+    mont_csub(acc, launder_s(M));
+    uint32_t w[64];
+    from28<FBM_NL, 64>(acc, w);
+    if (valid) store_row64(out + ct * 64, w);
   }
 }
 
 // ------------------------------------------------------------------------------------
 // aggregate: product of the P ciphertexts, X = prod_u c_u * R  (Montgomery form, lazy)
-// Each c_u (any value < 2^2048) is first brought into the Montgomery domain with R^2.
-//   step 0    : a = R^2,    b = c_0  -> X = c_0*R
-//   step 2u-1 : a = R^2,    b = c_u  -> c_u*R staged in LDS      (u >= 1)
-//   step 2u   : a = c_u*R,  b = X    -> X                         (u >= 1)
+//   a = R^2, b = c_0 -> c_0*R;  then per u >= 1:  *c_u (drops R), *R^2 (restores R)
+// c_u (any value < 2^2048) is staged as a 28-bit column in X's slot, which finally
+// receives the product.
 // ------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(FBM_BLOCK, 1) jl_prod_kernel(const uint32_t* __restrict__ cts, int n_parties,
-                                                              uint64_t n_ct, JlParams jp,
-                                                              uint32_t* __restrict__ X) {
-  __shared__ uint32_t lds_a[FBM_NL * FBM_BLOCK];
+__global__ void __launch_bounds__(FBM_BLOCK, 2) jl_prod_kernel(const uint32_t* __restrict__ cts, int n_parties,
+                                                              uint64_t n_ct, const uint32_t* __restrict__ cst,
+                                                              uint32_t mp, uint32_t* __restrict__ X) {
+  __shared__ uint32_t lds_a[(FBM_NL + 1) * FBM_BLOCK];
   const int tid = threadIdx.x;
   uint32_t* lds = lds_a + tid;
-  const int ls = FBM_BLOCK;
+  const uint32_t aoff = lds_addr(lds);
+  const uint32_t* M = cst + FBM_CST_M;
   const uint64_t ct_raw = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
-  const bool valid = ct_raw < n_ct;  // no early return: keep control flow wave-uniform
+  const bool valid = ct_raw < n_ct;  // no early return: X is padded to whole blocks
   const uint64_t ct = valid ? ct_raw : n_ct - 1;
-  uint32_t* xp = X + (ct_raw >> 8) * (FBM_NL * 256) + (ct_raw & 255);  // X is padded to whole blocks
-  const int steps = 2 * n_parties - 1;
+  const uint32_t xoff = (uint32_t)(((ct_raw >> 8) * (FBM_NL * 256) + (ct_raw & 255)) * 4);
+  lds_store_uniform<FBM_NL>(lds, FBM_BLOCK, cst + FBM_CST_R2);
 #pragma unroll 1
-  for (int st = 0; st < steps; ++st) {
-    st = __builtin_amdgcn_readfirstlane(st);
-    asm volatile("" : "+s"(st));
-    uint32_t acc[FBM_NL];
-    const bool tomont = (st == 0) || (st & 1);
-    if (tomont) {
-      uint32_t c32[64];
-      load_row64(cts + ((uint64_t)((st + 1) >> 1) * n_ct + ct) * 64, c32);
-      to28<64, FBM_NL>(c32, acc);
-      lds_store_uniform<FBM_NL>(lds, ls, jp.mc.R2);
-    } else {
-      col_load(xp, acc);
+  for (int u = 0; u < n_parties; ++u) {
+    {
+      uint32_t c32[64], c28[FBM_NL];
+      load_row64(cts + ((uint64_t)u * n_ct + ct) * 64, c32);
+      to28<64, FBM_NL>(c32, c28);
+      col_store(X + xoff / 4, c28);
     }
-    mont_mul(acc, lds, ls, jp.mc);
-    if (st == 0 || !tomont) col_store(xp, acc);
-    else lds_store_col(lds, ls, acc);
+    fbm_mm_glb(aoff, X, xoff, M, mp);
+    if (u > 0) fbm_mm_glb(aoff, cst + FBM_CST_R2COL, 0u, M, mp);
   }
+  lds_to_glb(lds, X + xoff / 4);
 }
 
 // ------------------------------------------------------------------------------------
@@ -754,9 +720,9 @@ uint64_t jl_table_slots() {
       g_num_cu = prop.multiProcessorCount;
     if (g_num_cu <= 0) g_num_cu = 256;
   }
-  // one workgroup of FBM_BLOCK lanes per CU (one wave per SIMD: the product needs
-  // ~250 VGPRs + AGPR spill space at this stage of tuning)
-  return (uint64_t)g_num_cu * FBM_BLOCK;
+  // two workgroups of FBM_BLOCK lanes per CU: 2 waves/SIMD (244 VGPRs per lane in the
+  // assembly product; 2 x 75 KB LDS columns per CU)
+  return (uint64_t)g_num_cu * 2 * FBM_BLOCK;
 }
 
 static inline dim3 grid1(uint64_t items, unsigned block) { return dim3((unsigned)((items + block - 1) / block)); }
@@ -788,32 +754,47 @@ int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stat
   return check_launch("jl_fdh_kernel");
 }
 
-// The schedule travels as a kernel argument (copied by the runtime at launch, so the
-// host struct may die immediately) and is spilled to device memory for the exp kernel,
-// which indexes it dynamically.
-__global__ void jl_sched_kernel(JlSched sc, uint32_t* __restrict__ ops) {
-  for (int i = threadIdx.x; i < sc.n_ops; i += blockDim.x) ops[i] = sc.op[i];
+// Per-call device constants: the schedule travels as a kernel argument (copied by the
+// runtime at launch, so the host struct may die immediately) and is spilled to device
+// memory for the exp kernel, which indexes it dynamically; M and R^2 for the scalar
+// loads of the assembly product; broadcast columns of 1 and R^2 (limb k at word k*256,
+// read by every lane at offset 0).
+__global__ void jl_setup_kernel(JlSched sc, MontCtx mc, uint32_t* __restrict__ ops, uint32_t* __restrict__ cst) {
+  const int t = threadIdx.x;
+  for (int i = t; i < sc.n_ops; i += blockDim.x) ops[i] = sc.op[i];
+  if (t < 128) {
+    cst[FBM_CST_M + t] = t < FBM_NL ? mc.M[t] : 0u;
+    cst[FBM_CST_R2 + t] = t < FBM_NL ? mc.R2[t] : 0u;
+  }
+  for (int i = t; i < FBM_NL * 256; i += blockDim.x) {
+    const int k = i >> 8, l = i & 255;
+    cst[FBM_CST_ONE + i] = (l == 0 && k == 0) ? 1u : 0u;
+    cst[FBM_CST_R2COL + i] = l == 0 ? mc.R2[k] : 0u;
+  }
+}
+
+int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32_t* cst, hipStream_t s) {
+  hipLaunchKernelGGL(jl_setup_kernel, dim3(1), dim3(256), 0, s, sc, jp.mc, ops, cst);
+  return check_launch("jl_setup_kernel");
 }
 
 int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const JlSched& sc, int mode,
-                  const uint32_t* nude, uint32_t* table, uint64_t table_slots, uint32_t* ops, uint32_t* out,
-                  hipStream_t s) {
+                  const uint32_t* nude, uint32_t* table, uint64_t table_slots, const uint32_t* ops,
+                  const uint32_t* cst, uint32_t* out, hipStream_t s) {
   if (n_ct == 0) return FBM_OK;
-  hipLaunchKernelGGL(jl_sched_kernel, dim3(1), dim3(256), 0, s, sc, ops);
-  int rc = check_launch("jl_sched_kernel");
-  if (rc) return rc;
   uint64_t g = (n_ct + FBM_BLOCK - 1) / FBM_BLOCK;
   const uint64_t gmax = table_slots / FBM_BLOCK;
   if (g > gmax) g = gmax;
-  hipLaunchKernelGGL(jl_exp_kernel, dim3((unsigned)g), dim3(FBM_BLOCK), 0, s, H, n_ct, jp, (const uint32_t*)ops,
-                     sc.n_ops, sc.first, mode, nude, table, out);
+  hipLaunchKernelGGL(jl_exp_kernel, dim3((unsigned)g), dim3(FBM_BLOCK), 0, s, H, n_ct, cst, jp.mc.mp, ops, sc.n_ops,
+                     sc.first, mode, jp.key_is_zero, nude, table, out);
   return check_launch("jl_exp_kernel");
 }
 
-int launch_jl_prod(const uint32_t* cts, int n_parties, uint64_t n_ct, const JlParams& jp, uint32_t* X,
-                   hipStream_t s) {
+int launch_jl_prod(const uint32_t* cts, int n_parties, uint64_t n_ct, const JlParams& jp, const uint32_t* cst,
+                   uint32_t* X, hipStream_t s) {
   if (n_ct == 0) return FBM_OK;
-  hipLaunchKernelGGL(jl_prod_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, cts, n_parties, n_ct, jp, X);
+  hipLaunchKernelGGL(jl_prod_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, cts, n_parties, n_ct, cst,
+                     jp.mc.mp, X);
   return check_launch("jl_prod_kernel");
 }
 

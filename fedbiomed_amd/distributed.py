@@ -51,3 +51,88 @@ def init(backend: str = "nccl"):
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend, rank=rank, world_size=world)
     return rank, world, local
+
+
+# ------------------------------------------------------------------------------------------
+# party-per-rank exchange (the one real collective of the path)
+#
+# In a deployment each party's update is encrypted on its own node; when several parties'
+# encrypted updates sit on different GPUs of one node (one rank each), the aggregate needs
+# every party's value at every index.  The exchange is then:
+#   LOM: sum the local parties' masked u64 vectors on the device (the LOM aggregate is a
+#        plain sum mod 2^64), then ONE reduce-scatter over ranks (u64 sum == int64 sum mod
+#        2^64, two's complement) leaves rank r with the global masked sum of stripe r ->
+#        average + dequantise locally -> all-gather the float64 stripes.
+#   JL:  the ciphertext product is not an RCCL reduction, so ranks all-to-all their
+#        parties' ciphertexts by ciphertext stripe (256 B each), then each rank aggregates
+#        its stripe with ct_offset and the float64 stripes are all-gathered.
+# Backend "nccl" is RCCL over xGMI on the GPU box; the same code runs on gloo (CPU tensors)
+# in the tests.  gloo lacks reduce_scatter, so it takes all-reduce + slice.
+# ------------------------------------------------------------------------------------------
+def _dist():
+    import torch.distributed as dist
+
+    return dist
+
+
+def stripe_bounds(n_total: int, world: int, align: int):
+    """Equal-capacity stripes for collectives: (per_rank_capacity, [(lo, hi) per rank])."""
+    per = -(-n_total // world)
+    per = -(-per // align) * align
+    return per, [(min(r * per, n_total), min((r + 1) * per, n_total)) for r in range(world)]
+
+
+def reduce_scatter_u64(local_sum, n_total: int):
+    """Global mod-2^64 sum of every rank's `local_sum` (int64 [n_total], u64 bit patterns);
+    returns this rank's stripe (8-aligned, see stripe_bounds)."""
+    import torch
+
+    dist = _dist()
+    world, rank = dist.get_world_size(), dist.get_rank()
+    per, bounds = stripe_bounds(n_total, world, 8)
+    buf = torch.zeros(per * world, dtype=torch.int64, device=local_sum.device)
+    buf[:n_total] = local_sum
+    lo, hi = bounds[rank]
+    if dist.get_backend() == "nccl":
+        out = torch.empty(per, dtype=torch.int64, device=local_sum.device)
+        dist.reduce_scatter_tensor(out, buf, op=dist.ReduceOp.SUM)
+        return out[: hi - lo]
+    dist.all_reduce(buf, op=dist.ReduceOp.SUM)
+    return buf[lo:hi].clone()
+
+
+def all_gather_stripes(stripe, n_total: int, align: int):
+    """Inverse of the stripe split: every rank gets the full [n_total] vector."""
+    import torch
+
+    dist = _dist()
+    world, rank = dist.get_world_size(), dist.get_rank()
+    per, bounds = stripe_bounds(n_total, world, align)
+    buf = torch.zeros(per, dtype=stripe.dtype, device=stripe.device)
+    buf[: stripe.numel()] = stripe
+    out = torch.empty(per * world, dtype=stripe.dtype, device=stripe.device)
+    dist.all_gather_into_tensor(out, buf)
+    return torch.cat([out[r * per: r * per + (hi - lo)] for r, (lo, hi) in enumerate(bounds)])
+
+
+def all_to_all_ciphertexts(cts_local, parties_per_rank: int):
+    """cts_local: [P_local, n_ct, 64] int32 limbs of this rank's parties (whole vector).
+    Returns ([P_total, stripe_ct, 64] int32, ct_offset) = every party's ciphertexts for this
+    rank's ciphertext stripe; party order = rank-major (rank 0's parties first)."""
+    import torch
+
+    dist = _dist()
+    world, rank = dist.get_world_size(), dist.get_rank()
+    P_local, n_ct, W = cts_local.shape
+    if P_local != parties_per_rank:
+        raise ValueError("every rank must hold the same number of parties")
+    per, bounds = stripe_bounds(n_ct, world, 1)
+    # ct-major, padded to equal stripes: rows [r*per, (r+1)*per) go to rank r
+    send = torch.zeros((per * world, P_local, W), dtype=cts_local.dtype, device=cts_local.device)
+    send[:n_ct] = cts_local.permute(1, 0, 2)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send)
+    lo, hi = bounds[rank]
+    # recv block s = source rank s's parties for my stripe: [per, P_local, W]
+    recv = recv.view(world, per, P_local, W)[:, : hi - lo]
+    return recv.permute(0, 2, 1, 3).reshape(world * P_local, hi - lo, W).contiguous(), lo

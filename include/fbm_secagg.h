@@ -103,6 +103,11 @@ int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t tot
  * ct_offset: global index of ciphertext 0 (t_k = ((k + ct_offset) << 512) | tau) when the
  *          element range is sharded across devices on ciphertext boundaries; 0 otherwise.   */
 
+/* largest n_ct one call accepts (the device addresses 28-bit-limb columns with 32-bit byte
+ * offsets: n_ct * 296 B < 4 GiB); larger vectors are split by ct_offset (element-range
+ * shards), which is also how they spread over GPUs.                                      */
+#define FBM_JL_MAX_CT 14000000ull
+
 /* bytes of device workspace fbm_jl_encrypt / fbm_jl_aggregate need */
 uint64_t fbm_jl_encrypt_workspace(uint64_t n_ct);
 uint64_t fbm_jl_aggregate_workspace(uint64_t n_ct);

@@ -6,6 +6,29 @@ from fedbiomed_amd.secagg import SecaggCrypter
 from oracle import secagg_oracle as O
 
 dev = D.device()
+if len(sys.argv) > 3 and sys.argv[3] == "small":
+    import json
+    sys.path.insert(0, "tests")
+    from golden_util import I
+    g = json.load(open("tests/golden/jl.json"))
+    for case in g["jl_small"]:
+        nn = I(case["n"]); N2s = nn * nn
+        pts = torch.tensor(case["pt"], dtype=torch.int64, device=dev)
+        cts = [D.jl_encrypt(pts, nn, key, case["tau"], len(case["keys"]), slot=(100, 1)) for key in case["keys"]]
+        ints = [D.limbs_to_ints(c.cpu().numpy()) for c in cts]
+        ok = [ints[i] == [I(c) for c in case["ct"][i]] for i in range(len(cts))]
+        prod = [1] * len(case["pt"])
+        for ci in ints:
+            prod = [a * b % N2s for a, b in zip(prod, ci)]
+        sk0 = -sum(case["keys"])
+        hs = [O.fdh((k << 512) | case["tau"], N2s) for k in range(len(case["pt"]))]
+        _, sums = D.jl_aggregate(torch.stack(cts), nn, sk0, case["tau"], len(case["pt"]), 1, want_out=False,
+                                 want_sums=True, slot=(100, 1))
+        s_np = sums.cpu().numpy().view(np.uint64)
+        got = [int(a) | (int(b) << 64) for a, b in s_np]
+        print("N", nn, "keys", case["keys"], "sk0", sk0, "enc ok", ok, "got", got, "want", [I(d) for d in case["dec"]],
+              "H", hs[:2], "prod", prod[:2])
+    sys.exit(0)
 P, n, tau = int(sys.argv[1]) if len(sys.argv) > 1 else 2, int(sys.argv[2]) if len(sys.argv) > 2 else 70, 1
 keys = [W.jl_user_key(p) for p in range(P)]
 xs = [[float(v) for v in W.party_params(p, n)] for p in range(P)]
@@ -27,13 +50,13 @@ out = torch.empty(n, dtype=torch.float64, device=dev)
 sums = torch.empty((n, 2), dtype=torch.int64, device=dev)
 st = torch.zeros(4, dtype=torch.int32, device=dev)
 bp = D._biprime_limbs(W.BIPRIME0); kl, kneg = D._key_limbs(sk0)
-rc = lib.fbm_jl_aggregate(D._ptr(limbs), P, n_ct, es, cr, n, D._np_ptr(bp), D._np_ptr(kl), kneg, tau, 1, negc, step,
+rc = lib.fbm_jl_aggregate(D._ptr(limbs), P, n_ct, es, cr, n, D._np_ptr(bp), D._np_ptr(kl), kneg, tau, 0, 1, negc, step,
                           D._ptr(out), D._ptr(sums), D._ptr(ws), D._ptr(st), D._stream())
 torch.cuda.synchronize()
 print("rc", rc, N.last_error(), "stats", st.cpu().numpy())
 w = ws.cpu().numpy()
 def al(v): return (v + 255) & ~255
-off = al(512 * 4)
+off = al(512 * 4) + al((256 + 2 * 74 * 256) * 4)  # ops | cst
 nb = (n_ct + 255) // 256
 Xraw = w[off:off + nb * 256 * 74 * 4].view(np.uint32).reshape(nb, 74, 256); off += al(nb * 256 * 74 * 4)
 H = w[off:off + n_ct * 256].view(np.uint32).reshape(n_ct, 64); off += al(n_ct * 256)
