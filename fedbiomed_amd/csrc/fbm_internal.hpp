@@ -51,6 +51,7 @@ int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t 
 // per-call device constants (words): M, R^2 (74 limbs, padded to 128) and the broadcast
 // columns 1 and R^2 (limb k at word k*256)
 #define FBM_CST_M 0
+#define FBM_CST_CTR 120  // exp-kernel chunk counter (in M's padding; zeroed by jl_setup_kernel)
 #define FBM_CST_R2 128
 #define FBM_CST_ONE 256
 #define FBM_CST_R2COL (256 + FBM_NL * 256)

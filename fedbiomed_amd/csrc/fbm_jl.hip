@@ -259,28 +259,36 @@ __device__ __forceinline__ void glb_to_lds(const uint32_t* g, uint32_t* lds) {
 //   a = h^(2t-1)*R, b = table[16]    -> h^(2t+1)*R       -> table[t], t = 1..15
 //   a = table[first], then per op: nsq squarings, one product with table[idx]
 //   a = acc,  b = nude | 1           -> c | h^key (plain, lazily reduced) -> csub -> out
-// Uniform round loop over ciphertexts (lanes past the end redo the last one, store nothing).
+// Lanes past n_ct (last chunk) redo the last ciphertext and store nothing.
 __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __restrict__ H, uint64_t n_ct,
-                                                             const uint32_t* __restrict__ cst, uint32_t mp,
+                                                             uint32_t* __restrict__ cst, uint32_t mp,
                                                              const uint32_t* __restrict__ ops, int n_ops,
                                                              int first, int mode, int key_is_zero,
                                                              const uint32_t* __restrict__ nude,
                                                              uint32_t* __restrict__ table,
                                                              uint32_t* __restrict__ out) {
   __shared__ uint32_t lds_a[(FBM_NL + 1) * FBM_BLOCK];
+  __shared__ uint32_t chunk_s;
   const int tid = threadIdx.x;
   uint32_t* lds = lds_a + tid;
   const uint32_t aoff = lds_addr(lds);
   const uint32_t* M = cst + FBM_CST_M;
-  const uint64_t G = (uint64_t)gridDim.x * FBM_BLOCK;
-  const uint64_t gtid = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
   // byte offset of this lane's table entry 0 (entries FBM_NL*256 words apart)
   const uint32_t tb0 = (uint32_t)(((uint64_t)blockIdx.x * FBM_TENTRIES * FBM_NL * FBM_BLOCK + tid) * 4);
   const uint32_t tstride = FBM_NL * FBM_BLOCK * 4;
-  const uint64_t rounds = (n_ct + G - 1) / G;
+  const uint32_t n_chunks = (uint32_t)((n_ct + FBM_BLOCK - 1) / FBM_BLOCK);
+  // Persistent workgroups pull 256-ciphertext chunks from a counter (zeroed by
+  // jl_setup_kernel): a workgroup leaves as soon as the chunks run out, so the tail of
+  // one launch leaves CUs free for a concurrent launch on another stream (the parties'
+  // encrypts), instead of every workgroup idling through a partial last round.
 #pragma unroll 1
-  for (uint64_t r = 0; r < rounds; ++r) {
-    const uint64_t ct_raw = gtid + r * G;
+  for (;;) {
+    if (tid == 0) chunk_s = atomicAdd(cst + FBM_CST_CTR, 1u);
+    __syncthreads();
+    const uint32_t chunk = __builtin_amdgcn_readfirstlane(chunk_s);
+    __syncthreads();
+    if (chunk >= n_chunks) break;
+    const uint64_t ct_raw = (uint64_t)chunk * FBM_BLOCK + tid;
     const bool valid = ct_raw < n_ct;
     const uint64_t ct = valid ? ct_raw : n_ct - 1;
     {  // h -> 28-bit limbs -> scratch entry 16
@@ -785,7 +793,7 @@ int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const Jl
   uint64_t g = (n_ct + FBM_BLOCK - 1) / FBM_BLOCK;
   const uint64_t gmax = table_slots / FBM_BLOCK;
   if (g > gmax) g = gmax;
-  hipLaunchKernelGGL(jl_exp_kernel, dim3((unsigned)g), dim3(FBM_BLOCK), 0, s, H, n_ct, cst, jp.mc.mp, ops, sc.n_ops,
+  hipLaunchKernelGGL(jl_exp_kernel, dim3((unsigned)g), dim3(FBM_BLOCK), 0, s, H, n_ct, (uint32_t*)cst, jp.mc.mp, ops, sc.n_ops,
                      sc.first, mode, jp.key_is_zero, nude, table, out);
   return check_launch("jl_exp_kernel");
 }

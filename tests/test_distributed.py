@@ -1,0 +1,189 @@
+"""Multi-GPU plan of the secagg path (fedbiomed_amd/distributed.py).
+
+CPU (gloo, world_size 2, 127.0.0.1): the party-per-rank exchange -- LOM reduce-scatter of
+masked u64 sums, JL all-to-all of ciphertext stripes, all-gather of float64 stripes --
+composed with the CPU oracle as the per-rank compute, must reproduce the single-process
+oracle result bit for bit.  GPU: element-range shards computed with global offsets
+(elem_offset / ct_offset) concatenate to the unsharded device result.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from fedbiomed_amd import distributed as Dd
+from fedbiomed_amd import workload as W
+from oracle import secagg_oracle as O
+
+P, TAU = 4, 3
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, fn_name, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, globals()[fn_name](rank, world)))
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        q.put((rank, e))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(fn_name, world=2):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn_name, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, v = q.get(timeout=240)
+        out[r] = v
+    for p in procs:
+        p.join(timeout=60)
+    for r, v in out.items():
+        if isinstance(v, Exception):
+            raise v
+    return out
+
+
+# ---- per-rank bodies (module level: spawn pickles them by name) --------------------------
+N_LOM = 1003  # ragged: not a multiple of 8 * world
+
+
+def _lom_party_per_rank(rank, world):
+    ids = W.node_ids(P)
+    nonce = O.lom_nonce(W.LOM_NONCE)
+    mine = [p for p in range(P) if p % world == rank]
+    ys = [O.lom_encrypt([float(v) for v in W.party_params(p, N_LOM)], TAU, ids[p],
+                        W.pairwise_secrets_for(ids[p], ids), ids, nonce, weight=W.party_weight(p)) for p in mine]
+    local = torch.from_numpy(O.lom_aggregate(ys).view(np.int64).copy())
+    stripe = Dd.reduce_scatter_u64(local, N_LOM)
+    sums = [int(v) for v in stripe.numpy().view(np.uint64)]
+    total_w = sum(W.party_weight(p) for p in range(P))
+    out = torch.from_numpy(np.asarray(O.reverse_quantize(O.apply_average(sums, total_w)), dtype=np.float64))
+    return Dd.all_gather_stripes(out, N_LOM, 8).numpy()
+
+
+N_JL = 100
+
+
+def _jl_party_per_rank(rank, world):
+    from fedbiomed_amd import _device as D
+
+    keys = [W.jl_user_key(p) for p in range(P)]
+    mine = [p for p in range(P) if (p // (P // world)) == rank]  # rank-major party blocks
+    cts = [O.jl_encrypt([float(v) for v in W.party_params(p, N_JL)], TAU, keys[p], W.BIPRIME0, P,
+                        weight=W.party_weight(p)) for p in mine]
+    limbs = torch.from_numpy(np.stack([D.ints_to_limbs(c) for c in cts]).view(np.int32).copy())
+    stripe, k0 = Dd.all_to_all_ciphertexts(limbs, P // world)
+    es, cr = O.jl_slot(None, P)
+    e_lo, e_hi = min(k0 * cr, N_JL), min((k0 + stripe.shape[1]) * cr, N_JL)
+    ints = [D.limbs_to_ints(stripe[u].numpy()) for u in range(P)]
+    total_w = sum(W.party_weight(p) for p in range(P))
+    out = O.jl_crypter_aggregate(ints, TAU, -sum(keys), W.BIPRIME0, total_w, e_hi - e_lo, k0=k0)
+    out = torch.from_numpy(np.asarray(out, dtype=np.float64))
+    return Dd.all_gather_stripes(out, N_JL, cr).numpy(), (e_lo, e_hi)
+
+
+# ---- tests ---------------------------------------------------------------------------------
+@pytest.mark.parametrize("n,world,align", [(0, 2, 8), (7, 2, 8), (1003, 2, 8), (10_000_000, 8, 8),
+                                           (10_000_000, 8, 30), (100, 3, 31)])
+def test_shard_range_tiles(n, world, align):
+    prev = 0
+    for r in range(world):
+        lo, hi = Dd.shard_range(n, world, r, align)
+        assert lo == prev and lo <= hi and (lo % align == 0 or lo == n)
+        prev = hi
+    assert prev == n
+    per, bounds = Dd.stripe_bounds(n, world, align)
+    assert per % align == 0 and bounds[-1][1] == n and all(b[0] % align == 0 or b[0] == n for b in bounds)
+
+
+def test_lom_party_per_rank_gloo():
+    res = _spawn("_lom_party_per_rank")
+    ids = W.node_ids(P)
+    nonce = O.lom_nonce(W.LOM_NONCE)
+    ys = [O.lom_encrypt([float(v) for v in W.party_params(p, N_LOM)], TAU, ids[p], W.pairwise_secrets_for(ids[p], ids),
+                        ids, nonce, weight=W.party_weight(p)) for p in range(P)]
+    ref = O.lom_crypter_aggregate(ys, sum(W.party_weight(p) for p in range(P)))
+    for r in range(2):
+        assert res[r].view(np.uint64).tolist() == np.asarray(ref, dtype=np.float64).view(np.uint64).tolist()
+
+
+def test_jl_party_per_rank_gloo():
+    res = _spawn("_jl_party_per_rank")
+    keys = [W.jl_user_key(p) for p in range(P)]
+    cts = [O.jl_encrypt([float(v) for v in W.party_params(p, N_JL)], TAU, keys[p], W.BIPRIME0, P,
+                        weight=W.party_weight(p)) for p in range(P)]
+    ref = O.jl_crypter_aggregate(cts, TAU, -sum(keys), W.BIPRIME0, sum(W.party_weight(p) for p in range(P)), N_JL)
+    assert res[0][1][0] == 0 and res[1][1][1] == N_JL and res[0][1][1] == res[1][1][0]
+    for r in range(2):
+        assert res[r][0].view(np.uint64).tolist() == np.asarray(ref, dtype=np.float64).view(np.uint64).tolist()
+
+
+def test_jl_stripe_oracle_offsets():
+    """The oracle's k0 stripes concatenate to the whole-vector ciphertexts (CPU)."""
+    keys = W.jl_user_key(0)
+    x = [float(v) for v in W.party_params(0, 200)]
+    es, cr = O.jl_slot(None, 4)
+    whole = O.jl_encrypt(x, TAU, keys, W.BIPRIME0, 4)
+    lo, hi = Dd.jl_shard(200, 2, 1, cr)
+    part = O.jl_encrypt(x[lo:hi], TAU, keys, W.BIPRIME0, 4, k0=lo // cr)
+    assert part == whole[lo // cr:]
+
+
+# ---- GPU: sharded offsets reproduce the unsharded device result ------------------------------
+@pytest.mark.gpu
+def test_lom_elem_offset_shards_gpu():
+    from fedbiomed_amd.secagg import SecaggLomCrypter
+
+    dev = torch.device("cuda", 0)
+    n, world = 100_003, 3
+    ids = W.node_ids(3)
+    x = torch.from_numpy(W.party_params(1, n)).to(dev)
+    lc = SecaggLomCrypter(W.LOM_NONCE)
+    sec = W.pairwise_secrets_for(ids[1], ids)
+    whole = lc.encrypt_tensor(TAU, ids[1], x, sec, ids, weight=77)
+    parts = []
+    for r in range(world):
+        lo, hi = Dd.lom_shard(n, world, r)
+        parts.append(lc.encrypt_tensor(TAU, ids[1], x[lo:hi], sec, ids, weight=77, elem_offset=lo))
+    assert torch.equal(torch.cat(parts), whole)
+
+
+@pytest.mark.gpu
+def test_jl_ct_offset_shards_gpu():
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    dev = torch.device("cuda", 0)
+    n, world, Pp = 5_000, 3, 3
+    keys = [W.jl_user_key(p) for p in range(Pp)]
+    xs = [torch.from_numpy(W.party_params(p, n)).to(dev) for p in range(Pp)]
+    jc = SecaggCrypter()
+    es, cr = O.jl_slot(None, Pp)
+    whole = torch.stack([jc.encrypt_tensor(Pp, TAU, xs[p], keys[p], W.BIPRIME0, weight=10 + p) for p in range(Pp)])
+    out_whole = jc.aggregate_tensor(TAU, whole, -sum(keys), W.BIPRIME0, 33, num_expected_params=n)
+    outs = []
+    for r in range(world):
+        lo, hi = Dd.jl_shard(n, world, r, cr)
+        cts = torch.stack([jc.encrypt_tensor(Pp, TAU, xs[p][lo:hi], keys[p], W.BIPRIME0, weight=10 + p,
+                                             ct_offset=lo // cr) for p in range(Pp)])
+        assert torch.equal(cts, whole[:, lo // cr:(hi + cr - 1) // cr])
+        outs.append(jc.aggregate_tensor(TAU, cts, -sum(keys), W.BIPRIME0, 33, num_expected_params=hi - lo,
+                                        ct_offset=lo // cr))
+    assert torch.equal(torch.cat(outs), out_whole)

@@ -1,0 +1,21 @@
+#!/bin/bash
+# One measurement pass on the GPU box (run through gpurun from the repo root):
+# parity tests, the default bench line, a rocprofv3 kernel trace (+stats) and two
+# separate PMC passes (FETCH_SIZE, WRITE_SIZE) for the HBM traffic of the bench step.
+# Every GPU step has its own time limit; the chain stops at the first failure.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/${1:-r1}
+mkdir -p $O
+cd $R
+timeout -k 10 500 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.txt 2>&1 &&
+timeout -k 10 300 python bench.py --steps 2 --warmup 1 > $O/bench.json 2> $O/bench.err &&
+cd /tmp && export TMPDIR=/tmp &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-lom-extra > $O/prof_bench.json 2> $O/prof.err &&
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-lom-extra > /dev/null 2> $O/pmc_fetch.err &&
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-lom-extra > /dev/null 2> $O/pmc_write.err
+rc=$?
+echo "rc=$rc"
+tail -3 $O/pytest_gpu.txt
+cat $O/bench.json
+find $O -name "*.csv" | head -20
+exit $rc
