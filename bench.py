@@ -27,7 +27,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
-MAD_PEAK_TOPS = 30.27        # measured v_mad_u64_u32 lane-op rate, whole chip (tools/microbench/intrate.hip)
+MAD_PEAK_TOPS = 36.48        # measured v_mad_u64_u32 peak, whole chip, best occupancy (tools/microbench/madpeak.hip,
+                             # profiles/r1_madpeak.txt: 35.3 T at 2 waves/SIMD, 36.5 T at 4)
 MADS_PER_MONTMUL = 74 * 148  # 28-bit-limb product: 74 rows x (74 a*b + 74 m*M) v_mad_u64_u32
 
 
@@ -61,6 +62,25 @@ def montmuls_per_exp(key: int, win: int = 5) -> int:
     return 1 + 16 + sq + mul + 1
 
 
+def committed_traffic(kernel: str, scheme: str, n_ct: int):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
+    workload (profiles/*_hbm_traffic.json, written by tools/prof_summary.py), else None."""
+    import glob
+
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic.json")), reverse=True):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        cfg = d.get("meta", {}).get("bench_config") or {}
+        if cfg.get("scheme") == scheme and (scheme != "jl" or cfg.get("ciphertexts_per_party_per_gpu") == n_ct):
+            k = d.get("kernels", {}).get("fbm::" + kernel)
+            if k:
+                return k["hbm_bytes_per_launch"]
+    return None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -73,6 +93,10 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=None, help="elements in the timed CPU-oracle sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-lom-extra", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-to-host (H2D/D2H-inclusive) legs")
+    ap.add_argument("--e2e-list-n", type=int, default=1_000_000, help="elements for the list-API end-to-end leg")
+    ap.add_argument("--serial", action="store_true",
+                    help="no per-party streams in the timed steps (rocprof passes: per-kernel times unconfounded)")
     return ap.parse_args()
 
 
@@ -163,6 +187,8 @@ def main():
         return el.item(), (_native.prof_report() if prof else {})
 
     step = step_jl if args.scheme == "jl" else step_lom
+    if args.serial:
+        step = (lambda f: (lambda serial=False: f(serial=True)))(step)
     elapsed, _ = timed(step, args.steps, args.warmup)
     value = n_total * args.steps / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
@@ -186,7 +212,8 @@ def main():
     sec = ms / 1000.0 if ms > 0 else float("nan")
     achieved = alg_bytes / sec / 1e9 if ms > 0 else None
     roof = {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "traffic": committed_traffic(kname, args.scheme, n_ct),
             "avg_launch_ms": (ms / cnt) if cnt else None, "launches": cnt}
     line = {
         "metric": "params/s secagg encrypt+aggregate (device-resident), 10M-elem vector @1/8 GPU",
@@ -217,6 +244,44 @@ def main():
                        "aggregate_hbm_GBps": ab / (m2 / 1000) / 1e9 if m2 else None,
                        "aggregate_hbm_frac": (ab / (m2 / 1000) / 1e9) / HBM_PEAK_GBS if m2 else None,
                        "kernels_ms": {k: {"launches": c, "total_ms": round(t, 3)} for k, (c, t) in sorted(kp2.items())}}
+
+    # ---- end-to-end legs (host memory in, host memory out): never `value` ----
+    if rank == 0 and world == 1 and args.scheme == "jl" and not args.no_e2e:
+        # (a) pinned host float32 vectors -> H2D -> encrypt -> D2H ciphertext limbs (each party),
+        #     H2D of all ciphertexts -> aggregate -> D2H float64: the PCIe-inclusive rate
+        xs_h = [xs[p].cpu().pin_memory() for p in range(P)]
+        ct_h = [torch.empty((n_ct, 64), dtype=torch.int32).pin_memory() for _ in range(P)]
+        out_h = torch.empty(n, dtype=torch.float64).pin_memory()
+
+        def step_e2e():
+            for p in range(P):
+                x_d = xs_h[p].to(dev, non_blocking=True)
+                ct_h[p].copy_(jc.encrypt_tensor(P, tau, x_d, keys[p], W.BIPRIME0, weight=weights[p]),
+                              non_blocking=True)
+            cts_d = torch.stack([c.to(dev, non_blocking=True) for c in ct_h])
+            out_h.copy_(jc.aggregate_tensor(tau, cts_d, sk0, W.BIPRIME0, total_w, num_expected_params=n),
+                        non_blocking=True)
+            torch.cuda.synchronize()
+
+        step_e2e()
+        t0 = time.perf_counter()
+        step_e2e()
+        te = time.perf_counter() - t0
+        # (b) the reference's list API (List[float] in, List[int] out per party; List[List[int]] in,
+        #     List[float] out), on a bounded sample: Python int <-> limb conversion dominates
+        nl = min(args.e2e_list_n, n)
+        xl = [xs_h[p][:nl].tolist() for p in range(P)]
+        t0 = time.perf_counter()
+        cl = [jc.encrypt(P, tau, xl[p], keys[p], W.BIPRIME0, weight=weights[p]) for p in range(P)]
+        jc.aggregate(tau, P, cl, sk0, W.BIPRIME0, total_w, num_expected_params=nl)
+        tl = time.perf_counter() - t0
+        line["end_to_end"] = {
+            "pinned_host_tensors": {"value": n / te, "unit": "params/s", "ms_per_step": 1000 * te,
+                                    "elements": n, "note": "H2D + encrypt x P + D2H + H2D + aggregate + D2H, "
+                                                           "one stream"},
+            "list_api": {"value": nl / tl, "unit": "params/s", "ms_per_step": 1000 * tl, "elements": nl,
+                         "note": "SecaggCrypter.encrypt (List[float] -> List[int]) x P + aggregate "
+                                 "(List[List[int]] -> List[float])"}}
 
     # ---- CPU baseline: the oracle (CPU restatement of the reference, GMP powm) on a bounded sample ----
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
