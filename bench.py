@@ -29,15 +29,18 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MAD_PEAK_TOPS = 36.48        # measured v_mad_u64_u32 peak, whole chip, best occupancy (tools/microbench/madpeak.hip,
                              # profiles/r1_madpeak.txt: 35.3 T at 2 waves/SIMD, 36.5 T at 4)
-MADS_PER_MONTMUL = 74 * 148  # 28-bit-limb product: 74 rows x (74 a*b + 74 m*M) v_mad_u64_u32
+MADS_PER_MONTMUL = 74 * 148  # general 28-bit-limb product: 74 rows x (74 a*b + 74 m*M) v_mad_u64_u32
+# square (tools/gen_mont_asm.py square()): 2701 doubled cross products + 111 diagonal + 74*74 m*M
+MADS_PER_SQUARE = sum(73 - r for r in range(74)) + 74 + 37 + 74 * 74
 
 
-def montmuls_per_exp(key: int, win: int = 5) -> int:
-    """Montgomery products of one jl_exp_kernel ciphertext: to-Montgomery + 16-entry odd-power
-    table + sliding-window schedule (mirror of build_schedule in fbm_capi.hip) + final product."""
+def products_per_exp(key: int, win: int = 5):
+    """(squarings, general products) of one jl_exp_kernel ciphertext: to-Montgomery, h^2,
+    15 odd powers, the sliding-window schedule (mirror of build_schedule in fbm_capi.hip),
+    final product with nude / 1."""
     k = abs(key)
     if k == 0:
-        return 2
+        return 0, 2
     bits = bin(k)[2:]
     nb = len(bits)
     i, sq, mul, first = nb - 1, 0, 0, True
@@ -59,7 +62,12 @@ def montmuls_per_exp(key: int, win: int = 5) -> int:
         pending = 0
         i = lo - 1
     sq += pending
-    return 1 + 16 + sq + mul + 1
+    return 1 + sq, 1 + 15 + mul + 1
+
+
+def mads_per_exp(key: int) -> int:
+    sq, gen = products_per_exp(key)
+    return sq * MADS_PER_SQUARE + gen * MADS_PER_MONTMUL
 
 
 def committed_traffic(kernel: str, scheme: str, n_ct: int):
@@ -202,8 +210,8 @@ def main():
         cnt, ms = kprof.get("jl_exp", (0, 0.0))
         # algorithmic bytes: encrypt/party 4N + 256*#ct, aggregate 256*P*#ct + 8N
         alg_bytes = prof_steps * (P * (4 * n + 256 * n_ct) + (256 * P * n_ct + 8 * n))
-        mm = P * montmuls_per_exp(keys[0]) + montmuls_per_exp(sk0)
-        mads = prof_steps * n_ct * mm * MADS_PER_MONTMUL
+        mm = P * sum(products_per_exp(keys[0])) + sum(products_per_exp(sk0))
+        mads = prof_steps * n_ct * (P * mads_per_exp(keys[0]) + mads_per_exp(sk0))
         kname = "jl_exp_kernel"
     else:
         cnt, ms = kprof.get("lom_aggregate", (0, 0.0))
@@ -232,7 +240,8 @@ def main():
         ach = mads / sec / 1e12
         line["roofline_valu"] = {"bound": "int-valu (v_mad_u64_u32)", "achieved": ach, "peak": MAD_PEAK_TOPS,
                                  "unit": "T lane-mad/s", "frac": ach / MAD_PEAK_TOPS,
-                                 "montmuls_per_ct_step": mm}
+                                 "products_per_ct_step": mm,
+                                 "note": "executed v_mad_u64_u32 (squares 8288, general products 10952 each)"}
 
     # ---- secondary: LOM at the same size (cheap), so both schemes are on record ----
     if args.scheme == "jl" and not args.no_lom_extra:

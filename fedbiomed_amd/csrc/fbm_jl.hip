@@ -253,7 +253,7 @@ __device__ __forceinline__ void glb_to_lds(const uint32_t* g, uint32_t* lds) {
 // mode 0 (ENC): out[ct] = nude[ct] * H[ct]^key  mod N^2          (ciphertext)
 // mode 1 (DEC): out[ct] = H[ct]^key mod N^2 (plain)                (for the inverse)
 // Sliding window (width FBM_WIN, 16 odd powers) over the device copy of the host-built
-// schedule.  Per-lane table: 17 blocked columns (entry 16 = h / h^2 scratch).
+// schedule; squarings use the dedicated assembly square (fbm_sq_lds).  Per-lane table: 17 blocked columns (entry 16 = h / h^2 scratch).
 //   a = R^2 (uniform), b = h         -> h*R              -> table[0]
 //   a = h*R,  b = a                  -> h^2*R            -> table[16]
 //   a = h^(2t-1)*R, b = table[16]    -> h^(2t+1)*R       -> table[t], t = 1..15
@@ -277,6 +277,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
   const uint32_t tb0 = (uint32_t)(((uint64_t)blockIdx.x * FBM_TENTRIES * FBM_NL * FBM_BLOCK + tid) * 4);
   const uint32_t tstride = FBM_NL * FBM_BLOCK * 4;
   const uint32_t n_chunks = (uint32_t)((n_ct + FBM_BLOCK - 1) / FBM_BLOCK);
+  lds_a[FBM_NL * FBM_BLOCK + tid] = 0u;  // zero row: the squaring's odd-row diagonal reads it
   // Persistent workgroups pull 256-ciphertext chunks from a counter (zeroed by
   // jl_setup_kernel): a workgroup leaves as soon as the chunks run out, so the tail of
   // one launch leaves CUs free for a concurrent launch on another stream (the parties'
@@ -307,7 +308,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
     fbm_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, M, mp);  // h*R
     if (!key_is_zero) {
       lds_to_glb(lds, table + tb0 / 4);
-      fbm_mm_lds(aoff, aoff, M, mp);  // h^2*R
+      fbm_sq_lds(aoff, M, mp);  // h^2*R
       lds_to_glb(lds, table + (tb0 + FBM_TSCRATCH * tstride) / 4);
       glb_to_lds(table + tb0 / 4, lds);
 #pragma unroll 1
@@ -322,7 +323,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
         const int nsq = (int)(op >> 5);
         const int idx = (int)(op & 31u) - 1;
 #pragma unroll 1
-        for (int q = 0; q < nsq; ++q) fbm_mm_lds(aoff, aoff, M, mp);
+        for (int q = 0; q < nsq; ++q) fbm_sq_lds(aoff, M, mp);
         if (idx >= 0) fbm_mm_glb(aoff, table, tb0 + (uint32_t)idx * tstride, M, mp);
       }
     }

@@ -28,7 +28,8 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 constexpr int NL = FBM_NL;
 
 // io: blocked columns [block][limb][256]; b: same layout (multiplier for odd steps)
-__global__ void __launch_bounds__(256, 1) k_cpp(uint32_t* io, const uint32_t* bm, MontCtx c, int reps) {
+// mode 0: alternate squaring / multiply by bm;  mode 1: squarings only
+__global__ void __launch_bounds__(256, 1) k_cpp(uint32_t* io, const uint32_t* bm, MontCtx c, int reps, int mode) {
   __shared__ uint32_t lds_a[NL * 256];
   const int tid = threadIdx.x;
   uint32_t* g = io + (uint64_t)blockIdx.x * NL * 256 + tid;
@@ -40,7 +41,7 @@ __global__ void __launch_bounds__(256, 1) k_cpp(uint32_t* io, const uint32_t* bm
   for (int r = 0; r < reps; ++r) {
     r = __builtin_amdgcn_readfirstlane(r);
     asm volatile("" : "+s"(r));
-    if (r & 1) {  // acc <- acc * b
+    if ((r & 1) && mode == 0) {  // acc <- acc * b
       lds_store_col(lds, 256, acc);
       col_load(gb, acc);
     } else {      // acc <- acc^2
@@ -51,18 +52,22 @@ __global__ void __launch_bounds__(256, 1) k_cpp(uint32_t* io, const uint32_t* bm
   col_store(g, acc);
 }
 
+// use_sq: squarings through fbm_sq_lds (else the general product with b == a)
 __global__ void __launch_bounds__(256, 2) k_asm(uint32_t* io, const uint32_t* bm, const uint32_t* M, uint32_t mp,
-                                                int reps) {
+                                                int reps, int mode, int use_sq) {
   __shared__ uint32_t lds_a[(NL + 1) * 256];
   const int tid = threadIdx.x;
   const uint32_t off = (uint32_t)(uintptr_t)((lds_u32*)lds_a + tid);
   uint32_t* g = io + (uint64_t)blockIdx.x * NL * 256 + tid;
   for (int k = 0; k < NL; ++k) lds_a[k * 256 + tid] = g[k * 256];
+  lds_a[NL * 256 + tid] = 0u;  // zero row read by the squaring's odd diagonals
   const uint32_t boff = (uint32_t)(((uint64_t)blockIdx.x * NL * 256 + tid) * 4);
 #pragma unroll 1
   for (int r = 0; r < reps; ++r) {
-    if (r & 1)
+    if ((r & 1) && mode == 0)
       fbm_mm_glb(off, bm, boff, M, mp);
+    else if (use_sq)
+      fbm_sq_lds(off, M, mp);
     else
       fbm_mm_lds(off, off, M, mp);
   }
@@ -104,37 +109,42 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(d1, h.data(), words * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(d2, h.data(), words * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(db, hb.data(), words * 4, hipMemcpyHostToDevice));
-  hipEvent_t e0, e1, e2;
+  hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  CK(hipEventCreate(&e2));
-  // warm-up launches (one rep) then the timed ones
-  hipLaunchKernelGGL(k_cpp, dim3(blocks), dim3(256), 0, 0, d1, db, c, 0);
-  hipLaunchKernelGGL(k_asm, dim3(blocks), dim3(256), 0, 0, d2, db, dM, c.mp, 0);
-  CK(hipDeviceSynchronize());
-  CK(hipEventRecord(e0));
-  hipLaunchKernelGGL(k_cpp, dim3(blocks), dim3(256), 0, 0, d1, db, c, reps);
-  CK(hipEventRecord(e1));
-  hipLaunchKernelGGL(k_asm, dim3(blocks), dim3(256), 0, 0, d2, db, dM, c.mp, reps);
-  CK(hipEventRecord(e2));
-  CK(hipDeviceSynchronize());
-  float t_cpp = 0, t_asm = 0;
-  CK(hipEventElapsedTime(&t_cpp, e0, e1));
-  CK(hipEventElapsedTime(&t_asm, e1, e2));
-  std::vector<uint32_t> r1(words), r2(words);
-  CK(hipMemcpy(r1.data(), d1, words * 4, hipMemcpyDeviceToHost));
-  CK(hipMemcpy(r2.data(), d2, words * 4, hipMemcpyDeviceToHost));
-  size_t diff = 0, first = (size_t)-1;
-  for (size_t i = 0; i < words; ++i)
-    if (r1[i] != r2[i]) {
-      if (first == (size_t)-1) first = i;
-      ++diff;
+  uint32_t* d3;
+  CK(hipMalloc(&d3, words * 4));
+  int bad = 0;
+  for (int mode = 0; mode < 2; ++mode) {
+    float t[3];
+    std::vector<uint32_t> r[3];
+    uint32_t* dd[3] = {d1, d2, d3};
+    for (int v = 0; v < 3; ++v) {
+      CK(hipMemcpy(dd[v], h.data(), words * 4, hipMemcpyHostToDevice));
+      if (v == 0) hipLaunchKernelGGL(k_cpp, dim3(blocks), dim3(256), 0, 0, dd[v], db, c, 0, mode);
+      else hipLaunchKernelGGL(k_asm, dim3(blocks), dim3(256), 0, 0, dd[v], db, dM, c.mp, 0, mode, v == 2);
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(e0));
+      if (v == 0) hipLaunchKernelGGL(k_cpp, dim3(blocks), dim3(256), 0, 0, dd[v], db, c, reps, mode);
+      else hipLaunchKernelGGL(k_asm, dim3(blocks), dim3(256), 0, 0, dd[v], db, dM, c.mp, reps, mode, v == 2);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&t[v], e0, e1));
+      r[v].resize(words);
+      CK(hipMemcpy(r[v].data(), dd[v], words * 4, hipMemcpyDeviceToHost));
     }
-  const double mm = (double)blocks * 256 * reps;
-  const double mads = mm * 74 * 148;
-  printf("{\"blocks\": %d, \"reps\": %d, \"cpp_ms\": %.3f, \"asm_ms\": %.3f, \"cpp_Mmontmul_s\": %.1f, "
-         "\"asm_Mmontmul_s\": %.1f, \"asm_Tmad_s\": %.2f, \"mismatch_words\": %zu, \"first_mismatch\": %lld}\n",
-         blocks, reps, t_cpp, t_asm, mm / t_cpp / 1e3, mm / t_asm / 1e3, mads / t_asm / 1e9, diff,
-         (long long)(first == (size_t)-1 ? -1 : (long long)first));
-  return diff ? 2 : 0;
+    size_t diff1 = 0, diff2 = 0;
+    for (size_t i = 0; i < words; ++i) {
+      diff1 += r[0][i] != r[1][i];
+      diff2 += r[0][i] != r[2][i];
+    }
+    bad |= (diff1 || diff2);
+    const double mm = (double)blocks * 256 * reps;
+    printf("{\"mode\": \"%s\", \"blocks\": %d, \"reps\": %d, \"cpp_ms\": %.3f, \"asm_ms\": %.3f, "
+           "\"asm_sq_ms\": %.3f, \"cpp_Gprod_s\": %.3f, \"asm_Gprod_s\": %.3f, \"asm_sq_Gprod_s\": %.3f, "
+           "\"asm_Tmad_s\": %.2f, \"mismatch_asm\": %zu, \"mismatch_asm_sq\": %zu}\n",
+           mode ? "square-only" : "square/multiply", blocks, reps, t[0], t[1], t[2], mm / t[0] / 1e6,
+           mm / t[1] / 1e6, mm / t[2] / 1e6, mm * 74 * 148 / t[1] / 1e9, diff1, diff2);
+  }
+  return bad ? 2 : 0;
 }
