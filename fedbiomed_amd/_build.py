@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_lib", "libfbm_secagg.so")
-SOURCES = ["fbm_lom.hip", "fbm_jl.hip", "fbm_capi.hip"]
+SOURCES = ["fbm_lom.hip", "fbm_jl.hip", "fbm_ass.hip", "fbm_capi.hip"]
 ARCH = os.environ.get("FBM_OFFLOAD_ARCH", "gfx950")
 
 

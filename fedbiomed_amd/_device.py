@@ -366,3 +366,64 @@ def jl_aggregate(cts: torch.Tensor, biprime: int, key: int, tau: int, n_expected
           int(ct_offset), int(total_weight), negc, step, _ptr(out), _ptr(sums), _ptr(ws), _ptr(st), _stream())
     _check_stats(st)
     return out, sums
+
+
+# ------------------------------------------------------------------------------------------
+# additive secret sharing (secagg/_additive_ss.py)
+# ------------------------------------------------------------------------------------------
+I64_MIN, U64_LIM = -(2**63), 2**64
+
+
+def ass_split(secret: torch.Tensor, n_shares: int, bit_length: Optional[int] = None, unsigned: bool = False,
+              seed: Optional[bytes] = None, nonce: Optional[bytes] = None, elem_offset: int = 0) -> torch.Tensor:
+    """Device int64 vector (uint64 bit patterns if `unsigned`) -> int64 [n_shares, n, 2]
+    int128 shares (lo, hi).  `seed` (32 B) / `nonce` (8 B) default to fresh OS randomness."""
+    import secrets as _secrets
+
+    lib = N.load()
+    secret = secret.contiguous()
+    n = secret.numel()
+    shares = torch.empty((n_shares, n, 2), dtype=torch.int64, device=secret.device)
+    seed = seed if seed is not None else _secrets.token_bytes(32)
+    nonce = nonce if nonce is not None else _secrets.token_bytes(8)
+    if len(seed) != 32 or len(nonce) != 8:
+        raise ValueError("seed must be 32 bytes and nonce 8 bytes")
+    sb = np.frombuffer(seed, dtype=np.uint8).copy()
+    nb = np.frombuffer(nonce, dtype=np.uint8).copy()
+    _call(lib.fbm_ass_split, _ptr(secret), N.FBM_U64 if unsigned else N.FBM_I64, n, int(n_shares),
+          -1 if bit_length is None else int(bit_length), _np_ptr(sb), _np_ptr(nb), int(elem_offset), _ptr(shares),
+          _stream())
+    return shares
+
+
+def ass_reconstruct(shares: torch.Tensor) -> torch.Tensor:
+    """int64 [P, n, 2] int128 shares -> int64 [n, 2] int128 exact column sum."""
+    lib = N.load()
+    shares = shares.contiguous()
+    P, n, _ = shares.shape
+    out = torch.empty((n, 2), dtype=torch.int64, device=shares.device)
+    _call(lib.fbm_ass_reconstruct, _ptr(shares), int(P), n, _ptr(out), _stream())
+    return out
+
+
+def ints_to_int128(values: Sequence[int]) -> np.ndarray:
+    """Python ints in [-2^127, 2^127) -> int64 [n, 2] (lo, hi) two's complement."""
+    out = np.empty((len(values), 2), dtype=np.int64)
+    u = out.view(np.uint64)
+    for i, v in enumerate(values):
+        v = int(v)
+        if not -(2**127) <= v < 2**127:
+            raise ValueError("value outside the int128 range of the device additive-sharing path")
+        w = v & (2**128 - 1)
+        u[i, 0] = w & (2**64 - 1)
+        u[i, 1] = w >> 64
+    return out
+
+
+def int128_to_ints(arr: np.ndarray) -> List[int]:
+    u = np.ascontiguousarray(arr).view(np.uint64).reshape(-1, 2)
+    out = []
+    for lo, hi in u.tolist():
+        w = (hi << 64) | lo
+        out.append(w - 2**128 if w >> 127 else w)
+    return out

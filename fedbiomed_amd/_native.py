@@ -30,6 +30,7 @@ FBM_E_UNSUPPORTED = -8
 FBM_F32 = 0
 FBM_F64 = 1
 FBM_U64 = 2
+FBM_I64 = 3
 STATS_WORDS = 4
 
 _lock = threading.Lock()
@@ -56,6 +57,8 @@ SIGNATURES = {
                                c_int, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_aggregate": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_u64, c_vp, c_vp, c_int, c_u64, c_u64, c_u64,
                                  c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "fbm_ass_split": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_vp, c_vp, c_u64, c_vp, c_vp]),
+    "fbm_ass_reconstruct": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp]),
     "fbm_prof_enable": (c_int, [c_int]),
     "fbm_prof_report": (c_int, [ctypes.c_char_p, c_int]),
 }

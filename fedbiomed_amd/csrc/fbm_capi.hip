@@ -527,6 +527,41 @@ int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, 
   return timed("jl_decode", s, [&] { return launch_jl_decode(xs, es, cr, n_out, total_weight, neg_clip, step, out, sums, stats, s); });
 }
 
+int fbm_ass_split(const void* secret, int secret_dtype, uint64_t n, int n_shares, int bit_length,
+                  const uint8_t* seed, const uint8_t* nonce, uint64_t elem_offset, int64_t* shares, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n_shares < 1 || bit_length > 64 || !seed || !nonce || (secret_dtype != FBM_U64 && secret_dtype != FBM_I64)) {
+    set_error("invalid additive-sharing arguments (n_shares >= 1, bit_length <= 64, 64-bit secrets)");
+    return FBM_E_ARG;
+  }
+  if (n == 0) return FBM_OK;
+  if (!secret || !shares) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  uint32_t key[8], nw[2];
+  memcpy(key, seed, 32);
+  memcpy(nw, nonce, 8);
+  return timed("ass_split", s, [&] {
+    return launch_ass_split((const uint64_t*)secret, n, key, nw[0], nw[1], elem_offset, n_shares, bit_length,
+                            secret_dtype == FBM_I64, shares, s);
+  });
+}
+
+int fbm_ass_reconstruct(const int64_t* shares, int n_shares, uint64_t n, int64_t* out, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n_shares < 1) {
+    set_error("n_shares must be >= 1");
+    return FBM_E_ARG;
+  }
+  if (n == 0) return FBM_OK;
+  if (!shares || !out) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  return timed("ass_reconstruct", s, [&] { return launch_ass_reconstruct(shares, n_shares, n, out, s); });
+}
+
 }  // extern "C"
 
 extern "C" {

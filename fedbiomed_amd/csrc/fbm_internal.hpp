@@ -95,6 +95,11 @@ int launch_jl_fin(uint64_t n_ct, const JlParams& jp, const uint32_t* X, const ui
 int launch_jl_decode(const uint32_t* xs, int es, int cr, uint64_t n_out, uint64_t total_weight, double neg_c,
                      double step, double* out, uint64_t* sums, uint32_t* stats, hipStream_t s);
 
+int launch_ass_split(const uint64_t* secret, uint64_t n, const uint32_t* key, uint32_t n14, uint32_t n15,
+                     uint64_t elem_offset, int n_shares, int bit_length, int is_signed, int64_t* shares,
+                     hipStream_t s);
+int launch_ass_reconstruct(const int64_t* shares, int n_shares, uint64_t n, int64_t* out, hipStream_t s);
+
 // table slots the encrypt/aggregate kernels need for a given grid
 uint64_t jl_table_slots();
 

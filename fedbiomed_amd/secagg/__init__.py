@@ -1,4 +1,5 @@
+from ._additive_ss import AdditiveSecret, AdditiveShare, AdditiveShares
 from ._lom import LOM, PRF
 from ._secagg_crypter import SecaggCrypter, SecaggLomCrypter
 
-__all__ = ["LOM", "PRF", "SecaggCrypter", "SecaggLomCrypter"]
+__all__ = ["AdditiveSecret", "AdditiveShare", "AdditiveShares", "LOM", "PRF", "SecaggCrypter", "SecaggLomCrypter"]

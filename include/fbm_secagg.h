@@ -42,6 +42,7 @@ extern "C" {
 #define FBM_F32 0
 #define FBM_F64 1
 #define FBM_U64 2 /* raw integer input (LOM.protect / JoyeLibert.protect on ints); no quantisation */
+#define FBM_I64 3 /* signed 64-bit integers (additive secret sharing)                           */
 
 #define FBM_STATS_WORDS 4
 
@@ -133,6 +134,22 @@ int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, 
                      const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau,
                      uint64_t ct_offset, uint64_t total_weight, double neg_clip, double step, double* out, uint64_t* sums,
                      void* workspace, uint32_t* stats, void* stream);
+
+/* ---- additive secret sharing of vectors (reference fedbiomed/common/secagg/_additive_ss.py) ----
+ * fbm_ass_split replaces AdditiveSecret.split / _shares_int (:40-98) for a list secret:
+ * every element v (secret_dtype FBM_U64 or FBM_I64) gets n_shares-1 shares uniform in
+ * [0, 2^b] (b = bit_length >= 0, or the bit length of |v| when bit_length < 0, as
+ * random.randint(0, 2**b)) and a last share v - sum(others).
+ *   shares   device, n_shares x n int128 as (lo, hi) int64 pairs, share-major
+ *   seed     HOST, 32 bytes: ChaCha20 key; nonce HOST, 8 bytes (stream id)
+ *   elem_offset  global index of secret[0] (element-range shards draw disjoint streams)
+ * The reference's MT19937 stream is not reproduced: the contract is sum == v exactly and the
+ * share ranges.
+ * fbm_ass_reconstruct replaces AdditiveShares.reconstruct (:252-267): exact int128 column sum.
+ */
+int fbm_ass_split(const void* secret, int secret_dtype, uint64_t n, int n_shares, int bit_length,
+                  const uint8_t* seed, const uint8_t* nonce, uint64_t elem_offset, int64_t* shares, void* stream);
+int fbm_ass_reconstruct(const int64_t* shares, int n_shares, uint64_t n, int64_t* out, void* stream);
 
 /* ---- instrumentation -------------------------------------------------------------------
  * fbm_prof_enable(1) makes every entry point record a HIP event pair around each kernel
