@@ -379,7 +379,6 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
   const uint32_t tb0 = (uint32_t)(((uint64_t)blockIdx.x * FBM_TENTRIES * FBM_NL * FBM_BLOCK + tid) * 4);
   const uint32_t tstride = FBM_NL * FBM_BLOCK * 4;
   const uint32_t n_chunks = (uint32_t)((n_ct + FBM_BLOCK - 1) / FBM_BLOCK);
-  lds_a[FBM_NL * FBM_BLOCK + tid] = 0u;  // zero row: the squaring's odd-row diagonal reads it
   // Persistent workgroups pull 256-ciphertext chunks from a counter (zeroed by
   // jl_setup_kernel): a workgroup leaves as soon as the chunks run out, so the tail of
   // one launch leaves CUs free for a concurrent launch on another stream (the parties'

@@ -165,64 +165,66 @@ def product(bsrc):
 # 25 % fewer multiplies.  Row r adds only the doubled cross products 2 a_r a_k (k > r) --
 # a contiguous suffix of the row's multiply sequence, entered by a computed jump
 # (s_setpc_b64: every v_mad_u64_u32 is 8 bytes) -- plus the diagonal a_{r/2}^2 of column r
-# (read from the LDS column at a row-dependent address; odd r reads row 74, kept zero by
-# the caller).  Diagonals of columns 74..146 are added after the loop from the B registers.
+# (even r only, read from the LDS column along a running address: rows are unrolled in
+# odd/even pairs so the parity is static).  Diagonals of columns 74..146 are added after the
+# loop from the B registers.
 # Every column holds the same total as in the general product when its m is computed, so
 # the Montgomery quotients and the result are identical.  Column bound: <= 37 doubled
 # products (< 2^57) + 1 diagonal + 74 m*M products (< 2^56) + carries < 2^63.3.
 # The a*b pass is in place and the m*M pass shifts the window (A_{k-1} <- A_k + m M_k),
-# so the accumulator window has 74 pairs (A_73 is re-zeroed every row).
-# Register plan: A_k v[2k:2k+1] (k=0..73), B_k = a_k v148..v221, a_r (doubled in place)
-# v222, a_{r+1} v223, T v[224:225], m v226, mp v227, LDS address of a_r v228, scratch
-# v229, a_{r/2} / a_{(r+1)/2} v230 / v231;  s[30:31] jump target, s34 row, s35 scratch.
+# so the accumulator window has 74 pairs (A_73 is written, not accumulated, by each row).
+# Register plan: A_k v[2k:2k+1] (k=0..73), B_k = a_k v148..v221, a_r of even / odd rows
+# (doubled in place) v222 / v223, T v[224:225], m v226, mp v227, LDS address v228, scratch
+# v229, diagonal limb v230, its LDS address v231;  s[30:31] jump target, s34 row, s35 scratch.
 # ------------------------------------------------------------------------------------------
 SQ_A = lambda k: f"v[{2 * k}:{2 * k + 1}]"  # noqa: E731
 SQ_ALO = lambda k: f"v{2 * k}"  # noqa: E731
 SQ_B = lambda j: f"v{148 + j}"  # noqa: E731
-SQ_AI, SQ_AN, SQ_T, SQ_TLO, SQ_MV, SQ_MPV, SQ_AADR, SQ_TMP, SQ_DI, SQ_DN = (
-    "v222", "v223", "v[224:225]", "v224", "v226", "v227", "v228", "v229", "v230", "v231")
-ZERO_ROW = NL * 1024  # byte offset of LDS row 74 (zero)
+SQ_AI = ("v222", "v223")  # a_r of even / odd rows (doubled in place)
+SQ_T, SQ_TLO, SQ_MV, SQ_MPV, SQ_AADR, SQ_TMP, SQ_DI, SQ_DADDR = (
+    "v[224:225]", "v224", "v226", "v227", "v228", "v229", "v230", "v231")
 
 
-def sq_row(first):
-    out = [f"ds_read_b32 {SQ_AN}, {SQ_AADR} offset:1024",
-           # address of a_{(r+1)/2} (r+1 even) or of the zero row (r+1 odd)
-           "s_add_u32 s30, s34, 1",
-           "s_lshl_b32 s35, s30, 9",
-           "s_bitcmp1_b32 s30, 0",
-           f"s_cselect_b32 s35, {hex(ZERO_ROW)}, s35",
-           f"v_add_u32 {SQ_TMP}, s35, %[a]",
-           f"ds_read_b32 {SQ_DN}, {SQ_TMP}",
-           f"v_mad_u64_u32 {SQ_A(0)}, vcc, {SQ_DI}, {SQ_DI}, {'0' if first else SQ_A(0)}",
-           f"v_lshlrev_b32 {SQ_AI}, 1, {SQ_AI}",
-           f"v_mul_lo_u32 {SQ_MV}, {SQ_ALO(0)}, {SQ_MPV}",
-           f"v_and_b32 {SQ_MV}, {MASK}, {SQ_MV}"]
-    if first:
-        out += [f"v_mad_u64_u32 {SQ_A(k)}, vcc, {SQ_AI}, {SQ_B(k)}, 0" for k in range(1, NL)]
-    else:
-        out += ["s_getpc_b64 s[30:31]",
-                ".Lfbm_sq_pc_%=:",
-                "s_lshl_b32 s35, s34, 3",
-                "s_add_u32 s30, s30, s35",
-                "s_addc_u32 s31, s31, 0",
-                "s_add_u32 s30, s30, .Lfbm_sq_tri_%= - .Lfbm_sq_pc_%=",
-                "s_addc_u32 s31, s31, 0",
-                "s_setpc_b64 s[30:31]",
-                ".Lfbm_sq_tri_%=:"]
-        out += [f"v_mad_u64_u32 {SQ_A(k)}, vcc, {SQ_AI}, {SQ_B(k)}, {SQ_A(k)}" for k in range(1, NL)]
-    out.append(f"v_mad_u64_u32 {SQ_T}, vcc, {SQ_MV}, {Ms(0)}, {SQ_A(0)}")
-    out += [f"v_mad_u64_u32 {SQ_A(k - 1)}, vcc, {SQ_MV}, {Ms(k)}, {SQ_A(k)}" for k in range(1, NL)]
-    out += [f"v_mov_b32 v{2 * NA}, 0", f"v_mov_b32 v{2 * NA + 1}, 0",
-            f"v_lshrrev_b64 {SQ_T}, 28, {SQ_T}",
-            f"v_lshl_add_u64 {SQ_A(0)}, {SQ_T}, 0, {SQ_A(0)}",
-            f"v_add_u32 {SQ_AADR}, 0x400, {SQ_AADR}",
-            "s_waitcnt lgkmcnt(0)",
-            f"v_mov_b32 {SQ_AI}, {SQ_AN}",
-            f"v_mov_b32 {SQ_DI}, {SQ_DN}"]
+def sq_tri(tag, first=False):
+    """Doubled cross products of one row: A_k += (2 a_r) b_k for k > r.  Entered at k = r+1 by
+    the caller's computed jump (or whole, for row 0).  k = 73 writes instead of adding: the
+    previous row's shift pass left A_73 holding a value already consumed."""
+    ai = SQ_AI[0] if tag in ("0", "e") else SQ_AI[1]
+    out = [f"v_mad_u64_u32 {SQ_A(k)}, vcc, {ai}, {SQ_B(k)}, {'0' if first else SQ_A(k)}" for k in range(1, NA)]
+    out.append(f"v_mad_u64_u32 {SQ_A(NA)}, vcc, {ai}, {SQ_B(NA)}, 0")
     return out
 
 
+def sq_jump(tag, entry_sgpr_expr):
+    """s[30:31] <- address of tri-block entry (k = entry); entry index from s34."""
+    return ["s_getpc_b64 s[30:31]",
+            f".Lfbm_sq_pc{tag}_%=:"] + entry_sgpr_expr + [
+            "s_add_u32 s30, s30, s35",
+            "s_addc_u32 s31, s31, 0",
+            f"s_add_u32 s30, s30, .Lfbm_sq_tri{tag}_%= - .Lfbm_sq_pc{tag}_%=",
+            "s_addc_u32 s31, s31, 0",
+            "s_setpc_b64 s[30:31]",
+            f".Lfbm_sq_tri{tag}_%=:"]
+
+
+def sq_reduce(last=False):
+    """Montgomery quotient of column r and the shifting m*M pass, then carry into A_0."""
+    out = [f"v_mad_u64_u32 {SQ_T}, vcc, {SQ_MV}, {Ms(0)}, {SQ_A(0)}"]
+    out += [f"v_mad_u64_u32 {SQ_A(k - 1)}, vcc, {SQ_MV}, {Ms(k)}, {SQ_A(k)}" for k in range(1, NA)]
+    out.append(f"v_mad_u64_u32 {SQ_A(NA - 1)}, vcc, {SQ_MV}, {Ms(NA)}, {'0' if last else SQ_A(NA)}")
+    out += [f"v_lshrrev_b64 {SQ_T}, 28, {SQ_T}", f"v_lshl_add_u64 {SQ_A(0)}, {SQ_T}, 0, {SQ_A(0)}"]
+    return out
+
+
+def sq_quotient(ai):
+    return [f"v_mul_lo_u32 {SQ_MV}, {SQ_ALO(0)}, {SQ_MPV}", f"v_lshlrev_b32 {ai}, 1, {ai}",
+            f"v_and_b32 {SQ_MV}, {MASK}, {SQ_MV}"]
+
+
 def square():
+    """Rows: 0 (peeled, even), pairs (r odd, r+1 even) for r = 1, 3, ..., 71, 73 (peeled, odd:
+    no cross products left).  Even rows add the diagonal a_{r/2}^2 (prefetched from LDS along a
+    running address); odd rows have none.  AADR = address of a_{r-1} at the top of a pair."""
     body = load_modulus()
     body.append(f"v_add_u32 {SQ_TMP}, 0x10000, %[a]")
     for j in range(NL):
@@ -230,12 +232,31 @@ def square():
             body.append(f"ds_read_b32 {SQ_B(j)}, %[a] offset:{j * 1024}")
         else:
             body.append(f"ds_read_b32 {SQ_B(j)}, {SQ_TMP} offset:{(j - 64) * 1024}")
-    body += [f"v_mov_b32 {SQ_MPV}, %[mp]", f"v_mov_b32 {SQ_AADR}, %[a]", f"ds_read_b32 {SQ_AI}, {SQ_AADR}",
-             f"ds_read_b32 {SQ_DI}, {SQ_AADR}", "s_mov_b32 s34, 0", "s_waitcnt lgkmcnt(0)"]
-    body += sq_row(True)
-    body += ["s_mov_b32 s34, 1", "1:"]
-    body += sq_row(False)
-    body += ["s_add_u32 s34, s34, 1", f"s_cmp_lg_u32 s34, {NL}", "s_cbranch_scc1 1b"]
+    body += [f"v_mov_b32 {SQ_MPV}, %[mp]", f"v_mov_b32 {SQ_AADR}, %[a]", f"ds_read_b32 {SQ_AI[0]}, %[a]",
+             f"ds_read_b32 {SQ_DI}, %[a]", f"v_add_u32 {SQ_DADDR}, 0x400, %[a]", "s_waitcnt lgkmcnt(0)"]
+    # ---- row 0 (even; diagonal a_0^2; all cross products) ----
+    body += [f"ds_read_b32 {SQ_AI[1]}, {SQ_AADR} offset:1024",
+             f"v_mad_u64_u32 {SQ_A(0)}, vcc, {SQ_DI}, {SQ_DI}, 0",
+             f"ds_read_b32 {SQ_DI}, {SQ_DADDR}"]  # diagonal of row 2: a_1
+    body += sq_quotient(SQ_AI[0]) + sq_tri("0", first=True) + sq_reduce()
+    body += ["s_waitcnt lgkmcnt(0)", "s_mov_b32 s34, 1", "1:"]
+    # ---- odd row r (a_r in AI[1]; entry k = r+1 -> index r) ----
+    body += [f"ds_read_b32 {SQ_AI[0]}, {SQ_AADR} offset:2048"]
+    body += sq_quotient(SQ_AI[1])
+    body += sq_jump("o", ["s_lshl_b32 s35, s34, 3"]) + sq_tri("o") + sq_reduce()
+    body += ["s_waitcnt lgkmcnt(0)"]
+    # ---- even row r+1 (a_{r+1} in AI[0]; diagonal a_{(r+1)/2}; entry index r+1) ----
+    body += [f"ds_read_b32 {SQ_AI[1]}, {SQ_AADR} offset:3072",
+             f"v_mad_u64_u32 {SQ_A(0)}, vcc, {SQ_DI}, {SQ_DI}, {SQ_A(0)}",
+             f"v_add_u32 {SQ_DADDR}, 0x400, {SQ_DADDR}"]
+    body += sq_quotient(SQ_AI[0])
+    body += [f"ds_read_b32 {SQ_DI}, {SQ_DADDR}"]  # diagonal of the next even row
+    body += sq_jump("e", ["s_add_u32 s35, s34, 1", "s_lshl_b32 s35, s35, 3"]) + sq_tri("e") + sq_reduce()
+    body += [f"v_add_u32 {SQ_AADR}, 0x800, {SQ_AADR}", "s_waitcnt lgkmcnt(0)",
+             "s_add_u32 s34, s34, 2", f"s_cmp_lg_u32 s34, {NL - 1}", "s_cbranch_scc1 1b"]
+    # ---- row 73 (odd; no cross products; A_73 holds a consumed value -> addend 0) ----
+    body += [f"v_mul_lo_u32 {SQ_MV}, {SQ_ALO(0)}, {SQ_MPV}", f"v_and_b32 {SQ_MV}, {MASK}, {SQ_MV}"]
+    body += sq_reduce(last=True)
     # diagonals of columns 74..146 (column 2h lands at window position 2h - 74)
     body += [f"v_mad_u64_u32 {SQ_A(2 * h - NL)}, vcc, {SQ_B(h)}, {SQ_B(h)}, {SQ_A(2 * h - NL)}"
              for h in range((NL + 1) // 2, NL)]
@@ -255,6 +276,10 @@ def square():
                  st(k, SQ_ALO(k))]
     body += [st(NA, SQ_TLO), "s_waitcnt lgkmcnt(0)"]
     return body
+
+
+def sq_row_len():
+    return len(sq_tri("o")) + len(sq_reduce()) + 12
 
 
 def sq_clobbers():
@@ -291,7 +316,7 @@ def main():
 // See tools/gen_mont_asm.py for the register plan and the arithmetic; fbm_mont.hpp's
 // mont_mul<74> is the same computation in C++.
 // {len(lds)} instructions (B from LDS), {len(glb)} (B from global), {len(sq)} (square); row loop
-// bodies {len(row(False))} and {len(sq_row(False))} (the square's a*b part is entered part-way).
+// bodies {len(row(False))} and ~{sq_row_len()} per square row (its a*b part is entered part-way).
 #pragma once
 #include <stdint.h>
 
@@ -322,7 +347,6 @@ __device__ __forceinline__ void fbm_mm_glb(uint32_t a_off, const uint32_t* bb, u
 }}
 
 // a <- a^2 R^-1 (identical to fbm_mm_lds(a_off, a_off, ...), ~25 % fewer multiplies).
-// LDS row 74 of the column (byte a_off + 74*1024) must hold 0.
 __device__ __forceinline__ void fbm_sq_lds(uint32_t a_off, const uint32_t* M, uint32_t mp) {{
   asm volatile(
 {c_string(sq)}

@@ -60,7 +60,6 @@ __global__ void __launch_bounds__(256, 2) k_asm(uint32_t* io, const uint32_t* bm
   const uint32_t off = (uint32_t)(uintptr_t)((lds_u32*)lds_a + tid);
   uint32_t* g = io + (uint64_t)blockIdx.x * NL * 256 + tid;
   for (int k = 0; k < NL; ++k) lds_a[k * 256 + tid] = g[k * 256];
-  lds_a[NL * 256 + tid] = 0u;  // zero row read by the squaring's odd diagonals
   const uint32_t boff = (uint32_t)(((uint64_t)blockIdx.x * NL * 256 + tid) * 4);
 #pragma unroll 1
   for (int r = 0; r < reps; ++r) {
