@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "fbm_internal.hpp"
+#include "fbm_safegcd.hpp"
 
 namespace fbm {
 
@@ -155,6 +156,7 @@ static int build_jl_params(const uint32_t* biprime, int es, int cr, uint64_t tau
   build_mont<FBM_NLN>(N, jp.mn);
   for (int i = 0; i < 32; ++i) jp.N32[i] = biprime[i];
   jp.n_bits = nb;
+  fbm_n30_setup(jp.N32, jp.n30);
   jp.es = es;
   jp.cr = cr;
   jp.tau = tau;
@@ -525,6 +527,32 @@ int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, 
   }
   if ((rc = timed("jl_fin", s, [&] { return launch_jl_fin(n_ct, jp, X, inv, xs, s); }))) return rc;
   return timed("jl_decode", s, [&] { return launch_jl_decode(xs, es, cr, n_out, total_weight, neg_clip, step, out, sums, stats, s); });
+}
+
+int fbm_test_modinv(const uint32_t* x, const uint32_t* n, uint32_t* out, int* batches) {
+  if (!x || !n || !out || !(n[0] & 1u)) {
+    set_error("fbm_test_modinv: null pointer or even modulus");
+    return FBM_E_ARG;
+  }
+  FbmN30 N;
+  fbm_n30_setup(n, N);
+  FbmInvState st;
+  fbm_modinv_init(st, x, N);
+  int b = 0;
+  while (!fbm_s30_is_zero(st.g) && b < FBM_INV_MAX_BATCHES) {
+    fbm_modinv_batch(st, N);
+    ++b;
+  }
+  if (batches) *batches = b;
+  if (!fbm_s30_is_zero(st.g)) {
+    set_error("modular inverse did not converge");
+    return FBM_E_ITER;
+  }
+  if (!fbm_modinv_finish(st, N, out)) {
+    set_error("not invertible");
+    return FBM_E_INVERSE;
+  }
+  return FBM_OK;
 }
 
 int fbm_ass_split(const void* secret, int secret_dtype, uint64_t n, int n_shares, int bit_length,

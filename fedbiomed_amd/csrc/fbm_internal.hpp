@@ -2,6 +2,7 @@
 #pragma once
 #include "fbm_common.hpp"
 #include "fbm_mont.hpp"
+#include "fbm_safegcd.hpp"
 #include "../../include/fbm_secagg.h"
 
 #define FBM_MAX_PEERS 64
@@ -74,6 +75,7 @@ struct JlParams {
   uint64_t tau;
   uint64_t ct_offset;            // global index of ciphertext 0 (element-range shard)
   uint32_t mid[8];               // SHA-256 state after the 14 all-zero message blocks
+  FbmN30 n30;                    // N in signed-30 limbs + N^-1 mod 2^30 (modular inverse)
   int key_is_zero;
   int pad;
 };

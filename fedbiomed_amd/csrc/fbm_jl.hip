@@ -20,6 +20,7 @@
 // the per-lane exponent tables are limb-major [limb][lane] so a wave's accesses coalesce.
 #include "fbm_internal.hpp"
 #include "fbm_mont_asm.hpp"
+#include "fbm_safegcd.hpp"
 
 namespace fbm {
 
@@ -507,18 +508,16 @@ __device__ __forceinline__ uint32_t sub_from(uint32_t (&a)[W], const uint32_t (&
   return br;
 }
 
-// stage 1: y = (E mod N)^-1 mod N   -> Y [ct][32]
-__global__ void __launch_bounds__(FBM_BLOCK, 1) jl_inv_modn_kernel(uint64_t n_ct, JlParams jp,
-                                                                  const uint32_t* __restrict__ E,
-                                                                  uint32_t* __restrict__ Y,
-                                                                  uint32_t* __restrict__ stats) {
+// stage 1a: E mod N -> Y [ct][32]
+__global__ void __launch_bounds__(FBM_BLOCK, 1) jl_emodn_kernel(uint64_t n_ct, JlParams jp,
+                                                               const uint32_t* __restrict__ E,
+                                                               uint32_t* __restrict__ Y) {
   __shared__ uint32_t lds_a[FBM_NL * FBM_BLOCK];
   const int tid = threadIdx.x;
   uint32_t* lds = lds_a + tid;
   const int ls = FBM_BLOCK;
   const uint64_t ct = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
   if (ct >= n_ct) return;
-  uint32_t err = 0;
 
   // --- e mod N = (e_hi * R_N + e_lo) mod N  with R_N = 2^1036 --------------------------
   //   t1 = mont(R2N, hi) = hi*R_N mod N            (lazy, < 2N)
@@ -552,70 +551,49 @@ __global__ void __launch_bounds__(FBM_BLOCK, 1) jl_inv_modn_kernel(uint64_t n_ct
     mont_csub(y28, jp.mn.M);
     mont_csub(y28, jp.mn.M);
   }
-  // --- y = (e mod N)^-1 mod N : binary extended Euclid on 32-bit limbs ------------------
-  uint32_t x1[32];
-  {
-    uint32_t u[32], v[32], x2[32];
-    from28<FBM_NLN, 32>(y28, u);
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      v[i] = jp.N32[i];
-      x1[i] = i == 0 ? 1u : 0u;
-      x2[i] = 0u;
-    }
-    uint32_t any = 0;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) any |= u[i];
-    bool ok = any != 0;
-    int it = 0;
-    for (; ok && it < 20000; ++it) {
-      uint32_t u1 = u[0] ^ 1u, v1 = v[0] ^ 1u;
-#pragma unroll
-      for (int i = 1; i < 32; ++i) {
-        u1 |= u[i];
-        v1 |= v[i];
-      }
-      if (u1 == 0u) break;  // u == 1 -> x1
-      if (v1 == 0u) {       // v == 1 -> x2
-#pragma unroll
-        for (int i = 0; i < 32; ++i) x1[i] = x2[i];
-        break;
-      }
-      if ((u[0] & 1u) == 0u) {
-        shr1<32>(u, 0u);
-        const uint32_t c = (x1[0] & 1u) ? add_into<32>(x1, jp.N32) : 0u;
-        shr1<32>(x1, c);
-        continue;
-      }
-      if ((v[0] & 1u) == 0u) {
-        shr1<32>(v, 0u);
-        const uint32_t c = (x2[0] & 1u) ? add_into<32>(x2, jp.N32) : 0u;
-        shr1<32>(x2, c);
-        continue;
-      }
-      int cmp = 0;
-#pragma unroll
-      for (int i = 31; i >= 0; --i)
-        if (cmp == 0) cmp = (u[i] > v[i]) - (u[i] < v[i]);
-      if (cmp == 0) {  // gcd != 1
-        ok = false;
-        break;
-      }
-      if (cmp > 0) {
-        sub_from<32>(u, v);
-        if (sub_from<32>(x1, x2)) add_into<32>(x1, jp.N32);
-      } else {
-        sub_from<32>(v, u);
-        if (sub_from<32>(x2, x1)) add_into<32>(x2, jp.N32);
-      }
-    }
-    if (it >= 20000) err |= FBM_ERR_ITER_CAP;
-    if (!ok) err |= FBM_ERR_NOT_INVERTIBLE;
-  }
+  uint32_t u[32];
+  from28<FBM_NLN, 32>(y28, u);
   uint4* yo = reinterpret_cast<uint4*>(Y + ct * 32);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) yo[i] = make_uint4(x1[4 * i], x1[4 * i + 1], x1[4 * i + 2], x1[4 * i + 3]);
-  if (err) atomicOr(stats + FBM_STAT_ERRFLAGS, err);
+  for (int i = 0; i < 8; ++i) yo[i] = make_uint4(u[4 * i], u[4 * i + 1], u[4 * i + 2], u[4 * i + 3]);
+}
+
+// stage 1b: y = (e mod N)^-1 mod N in place in Y, by Bernstein-Yang divsteps
+// (fbm_safegcd.hpp): branch-free batches of 30 divsteps; the loop leaves when every lane
+// of the wave is done (a finished lane is a fixed point of further batches).
+__global__ void __launch_bounds__(FBM_BLOCK) jl_inv_modn_kernel(uint64_t n_ct, JlParams jp,
+                                                               uint32_t* __restrict__ Y,
+                                                               uint32_t* __restrict__ stats) {
+  const uint64_t ct_raw = (uint64_t)blockIdx.x * FBM_BLOCK + threadIdx.x;
+  const uint64_t ct = ct_raw < n_ct ? ct_raw : n_ct - 1;  // all lanes take part in the vote
+  uint32_t err = 0;
+  uint32_t x1[32];
+  {
+    uint32_t u[32];
+    const uint4* yi = reinterpret_cast<const uint4*>(Y + ct * 32);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint4 v = yi[i];
+      u[4 * i] = v.x; u[4 * i + 1] = v.y; u[4 * i + 2] = v.z; u[4 * i + 3] = v.w;
+    }
+    FbmInvState st;
+    fbm_modinv_init(st, u, jp.n30);
+    for (int b = 0; b < FBM_INV_MAX_BATCHES; ++b) {
+      if (__all(fbm_s30_is_zero(st.g))) break;
+      fbm_modinv_batch(st, jp.n30);
+    }
+    if (!fbm_s30_is_zero(st.g)) {
+      err |= FBM_ERR_ITER_CAP;
+    } else if (!fbm_modinv_finish(st, jp.n30, x1)) {
+      err |= FBM_ERR_NOT_INVERTIBLE;
+    }
+  }
+  if (ct_raw < n_ct) {
+    uint4* yo = reinterpret_cast<uint4*>(Y + ct * 32);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) yo[i] = make_uint4(x1[4 * i], x1[4 * i + 1], x1[4 * i + 2], x1[4 * i + 3]);
+    if (err) atomicOr(stats + FBM_STAT_ERRFLAGS, err);
+  }
 }
 
 // stage 2 (Hensel lift): inv = y * (2 - E*y) mod N^2   -> inv [ct][64]
@@ -911,8 +889,11 @@ int launch_jl_prod(const uint32_t* cts, int n_parties, uint64_t n_ct, const JlPa
 int launch_jl_inv(uint64_t n_ct, const JlParams& jp, const uint32_t* E, uint32_t* Y, uint32_t* inv, uint32_t* stats,
                   hipStream_t s) {
   if (n_ct == 0) return FBM_OK;
-  hipLaunchKernelGGL(jl_inv_modn_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, E, Y, stats);
-  int rc = check_launch("jl_inv_modn_kernel");
+  hipLaunchKernelGGL(jl_emodn_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, E, Y);
+  int rc = check_launch("jl_emodn_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(jl_inv_modn_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, Y, stats);
+  rc = check_launch("jl_inv_modn_kernel");
   if (rc) return rc;
   hipLaunchKernelGGL(jl_inv_lift_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, E, Y, inv);
   return check_launch("jl_inv_lift_kernel");

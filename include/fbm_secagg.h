@@ -151,6 +151,11 @@ int fbm_ass_split(const void* secret, int secret_dtype, uint64_t n, int n_shares
                   const uint8_t* seed, const uint8_t* nonce, uint64_t elem_offset, int64_t* shares, void* stream);
 int fbm_ass_reconstruct(const int64_t* shares, int n_shares, uint64_t n, int64_t* out, void* stream);
 
+/* ---- host test hook (no GPU): the device modular-inverse routine (Bernstein-Yang divsteps,
+ * fedbiomed_amd/csrc/fbm_safegcd.hpp) run on the host, for unit tests.
+ * x, n, out: 32 little-endian words (n odd);  batches: number of 30-divstep batches used. */
+int fbm_test_modinv(const uint32_t* x, const uint32_t* n, uint32_t* out, int* batches);
+
 /* ---- instrumentation -------------------------------------------------------------------
  * fbm_prof_enable(1) makes every entry point record a HIP event pair around each kernel
  * launch (on the caller's stream); fbm_prof_report() synchronises them and returns the

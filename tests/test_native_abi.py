@@ -99,3 +99,46 @@ def test_product_path_does_not_import_oracle():
                 src = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in re.sub(r"#.*", "", src).replace('"""', "").split("import")[0] or \
                     "from oracle" not in src and "import oracle" not in src, f
+
+
+def test_device_modinv_on_host():
+    """The device modular inverse (Bernstein-Yang divsteps) run through the host test hook
+    against Python's pow(x, -1, N): random 1024-bit and small odd moduli, edge inputs,
+    non-invertible inputs; batch count within the constant-time bound."""
+    import ctypes
+    import random
+
+    import numpy as np
+
+    from fedbiomed_amd import _native as N
+    from fedbiomed_amd.workload import BIPRIME0
+
+    lib = N.load()
+
+    def limbs(v):
+        return np.frombuffer(int(v).to_bytes(128, "little"), dtype=np.uint32).copy()
+
+    def inv(x, n):
+        xa, na, out = limbs(x), limbs(n), np.zeros(32, dtype=np.uint32)
+        b = ctypes.c_int(0)
+        rc = lib.fbm_test_modinv(xa.ctypes.data, na.ctypes.data, out.ctypes.data, ctypes.byref(b))
+        return rc, int.from_bytes(out.tobytes(), "little"), b.value
+
+    rng = random.Random(5)
+    moduli = [BIPRIME0, 3, 15, 123457, 2**1024 - 1, (1 << 1023) + 1, rng.getrandbits(1024) | 1 | (1 << 1023)]
+    worst = 0
+    for n in moduli:
+        xs = [1, 2, n - 1, n - 2, (n + 1) // 2] + [rng.randrange(1, n) for _ in range(60)]
+        for x in xs:
+            x %= n
+            rc, got, b = inv(x, n)
+            worst = max(worst, b)
+            try:
+                want = pow(x, -1, n)
+            except ValueError:
+                assert rc == N.FBM_E_INVERSE, (n, x)
+                continue
+            assert rc == N.FBM_OK and got == want, (n, x)
+    assert inv(0, BIPRIME0)[0] == N.FBM_E_INVERSE
+    assert inv(15, 45)[0] == N.FBM_E_INVERSE
+    assert worst <= 99
