@@ -11,7 +11,7 @@ Scaling: element-range sharding with no data-path collective (fedbiomed_amd/dist
 each rank owns one 10M-element stripe (global offsets), so per-GPU work is fixed -> "weak".
 `--strong` splits a fixed total instead.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--scheme jl|lom] [--n 10000000] [--parties 8]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scheme jl|lom] [--elements 10000000] [--parties 8]
 """
 
 import argparse
@@ -95,7 +95,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scheme", choices=["jl", "lom"], default="jl")
-    ap.add_argument("--n", type=int, default=10_000_000, help="elements per GPU (weak) or total (--strong)")
+    ap.add_argument("--elements", "--n", dest="n", type=int, default=10_000_000,
+                    help="elements per GPU (weak) or total (--strong)")
     ap.add_argument("--parties", type=int, default=8)
     ap.add_argument("--strong", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=None, help="elements in the timed CPU-oracle sample")
@@ -103,6 +104,7 @@ def parse():
     ap.add_argument("--no-lom-extra", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-to-host (H2D/D2H-inclusive) legs")
     ap.add_argument("--e2e-list-n", type=int, default=1_000_000, help="elements for the list-API end-to-end leg")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, the real runs) or gloo (rehearsal)")
     ap.add_argument("--serial", action="store_true",
                     help="no per-party streams in the timed steps (rocprof passes: per-kernel times unconfounded)")
     return ap.parse_args()
@@ -116,8 +118,11 @@ def main():
     from fedbiomed_amd.secagg import SecaggCrypter, SecaggLomCrypter
 
     rank, world, local = distributed.env_rank()
+    # more ranks than visible GPUs only happens in a rehearsal (--dist-backend gloo on a
+    # one-GPU box): ranks then share devices round-robin
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
-        distributed.init("nccl")
+        distributed.init(args.dist_backend, device=local)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     P, tau = args.parties, 1

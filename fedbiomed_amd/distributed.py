@@ -11,7 +11,7 @@ of the stripes' results is bit-identical to the unsharded result.
 from __future__ import annotations
 
 import os
-from typing import Tuple
+from typing import Optional, Tuple
 
 
 def shard_range(n_total: int, world: int, rank: int, align: int) -> Tuple[int, int]:
@@ -40,12 +40,15 @@ def env_rank() -> Tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init(backend: str = "nccl"):
-    """One process per GPU; backend "nccl" is RCCL on ROCm (gloo for CPU tests)."""
+def init(backend: str = "nccl", device: Optional[int] = None):
+    """One process per GPU; backend "nccl" is RCCL on ROCm (gloo for CPU tests).
+    `device` overrides LOCAL_RANK as the rank's GPU (rehearsals with shared devices)."""
     import torch
     import torch.distributed as dist
 
     rank, world, local = env_rank()
+    if device is not None:
+        local = device
     if world > 1 and not dist.is_initialized():
         if backend == "nccl":
             torch.cuda.set_device(local)
