@@ -171,8 +171,9 @@ def main():
                                    ct_offset=lo // cr)
 
     def step_lom(serial=False):
-        ys = [lc.encrypt_tensor(tau, u, xs[p], secrets_[p], ids, weight=weights[p], elem_offset=lo)
-              for p, u in enumerate(ids)]
+        with D.deferred_checks():  # overflow-guard status checked once per step, no per-party sync
+            ys = [lc.encrypt_tensor(tau, u, xs[p], secrets_[p], ids, weight=weights[p], elem_offset=lo)
+                  for p, u in enumerate(ids)]
         return lc.aggregate_tensor(torch.stack(ys), total_w)
 
     def timed(step, steps, warmup, prof=False):

@@ -12,6 +12,7 @@ Python semantics stay bit-identical.
 from __future__ import annotations
 
 import ctypes
+import logging
 import math
 from typing import List, Optional, Sequence, Tuple
 
@@ -23,6 +24,9 @@ from .constants import ErrorNumbers, SAParameters
 from .exceptions import FedbiomedSecaggCrypterError, FedbiomedSecaggError
 
 U64_MAX = 2**64 - 1
+FBM_WARN_CLIPPED = 16  # stats flag: some |x| > clipping range (a warning, not an error)
+
+logger = logging.getLogger("fedbiomed_amd")
 
 
 # ------------------------------------------------------------------------------------------
@@ -70,7 +74,7 @@ def _call(fn, *args) -> None:
 
 
 class deferred_checks:
-    """Within this context the device status words of JL encrypts are checked once, at exit,
+    """Within this context the device status words of JL / LOM encrypts are checked once, at exit,
     instead of after every call (each check synchronises its stream).  This lets the
     encrypts of several parties issued on different HIP streams overlap on the GPU; any
     error is still raised, from the `with` statement's exit.
@@ -105,6 +109,9 @@ def _check_stats_or_defer(stats: torch.Tensor, lom_nodes: int = 0) -> None:
 
 def _check_stats(stats: torch.Tensor, lom_nodes: int = 0) -> int:
     host = stats.cpu().numpy().astype(np.uint32)  # synchronises the stream
+    if int(host[1]) & FBM_WARN_CLIPPED:  # _check_clipping_range (utils/_secagg_utils.py:189-204)
+        logger.warning("There are some numbers in the local vector that exceeds clipping range. "
+                       "Please increase the clipping range to account for value")
     mb = ctypes.c_uint32(0)
     rc = N.load().fbm_check_stats(_np_ptr(host), lom_nodes, ctypes.byref(mb))
     if rc != N.FBM_OK:
@@ -244,7 +251,7 @@ def lom_protect(x: torch.Tensor, secrets: Sequence[bytes], signs: Sequence[int],
     _call(lib.fbm_lom_protect, _ptr(x), _x_dtype(x), n, c, c2, tf, tm1, int(weight), _np_ptr(sec), _np_ptr(sg),
           len(secrets), 1 if raw_seeds else 0, _np_ptr(nb), int(tau), int(elem_offset), _ptr(y), _ptr(st),
           _stream())
-    _check_stats(st, lom_nodes=n_nodes)
+    _check_stats_or_defer(st, lom_nodes=n_nodes)
     return y
 
 

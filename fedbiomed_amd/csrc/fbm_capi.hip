@@ -462,7 +462,7 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
   off += align256(n_ct * 64 * 4);
   uint32_t* table = (uint32_t*)(ws + off);
   if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s); }))) return rc;
-  if ((rc = timed("jl_pack", s, [&] { return launch_jl_pack(x, x_dtype, n, qp, weight, es, cr, n_ct, pt, s); }))) return rc;
+  if ((rc = timed("jl_pack", s, [&] { return launch_jl_pack(x, x_dtype, n, qp, weight, es, cr, n_ct, pt, stats, s); }))) return rc;
   if ((rc = timed("jl_nude", s, [&] { return launch_jl_nude(pt, n_ct, jp, nude, s); }))) return rc;
   if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, H, stats, s); }))) return rc;
   return timed("jl_exp", s, [&] { return launch_jl_exp(H, n_ct, jp, sc, 0, nude, table, slots, ops, cst, ct_out, s); });

@@ -49,6 +49,9 @@ FBM_HD uint64_t fbm_quantize(double x, const QuantParams& p) {
   return qt < p.tm1 ? qt : p.tm1;
 }
 
+// _check_clipping_range (utils/_secagg_utils.py:189-204): x < -c or x > c (NaN: no)
+FBM_HD bool fbm_outside_clip(double x, const QuantParams& p) { return x < -p.c || x > p.c; }
+
 // Number of significant bits of the 128-bit value hi:lo (Python int.bit_length()).
 FBM_HD uint32_t fbm_bitlen128(uint64_t hi, uint64_t lo) {
   if (hi) return 128u - (uint32_t)__builtin_clzll(hi);

@@ -16,8 +16,15 @@
 #define FBM_ERR_FDH_OVERFLOW 2u    // > 8 non-coprime FDH digests (reference: OverflowError)
 #define FBM_ERR_NOT_INVERTIBLE 4u  // server-key power not invertible mod N^2
 #define FBM_ERR_ITER_CAP 8u        // a bounded data-dependent loop hit its cap
+#define FBM_WARN_CLIPPED 16u       // not an error: some |x| > clipping range (the reference's
+                                   // _check_clipping_range warning, _secagg_utils.py:189-204)
 
 namespace fbm {
+
+// wave-level OR of a per-lane warning/error condition into the stats flags (one atomic per wave)
+__device__ __forceinline__ void flag_if_any(bool cond, uint32_t* stats, uint32_t bit) {
+  if (__ballot(cond) && (threadIdx.x & 63) == 0) atomicOr(stats + FBM_STAT_ERRFLAGS, bit);
+}
 
 struct LomPeers {
   int n_peers;
@@ -81,7 +88,7 @@ struct JlParams {
 };
 
 int launch_jl_pack(const void* x, int x_dtype, uint64_t n, const QuantParams& qp, uint64_t weight, int es, int cr,
-                   uint64_t n_ct, uint32_t* pt, hipStream_t s);
+                   uint64_t n_ct, uint32_t* pt, uint32_t* stats, hipStream_t s);
 int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, uint32_t* nude, hipStream_t s);
 int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s);
 int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32_t* cst, hipStream_t s);

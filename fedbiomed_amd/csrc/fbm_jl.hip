@@ -31,22 +31,28 @@ namespace fbm {
 // ------------------------------------------------------------------------------------
 // XT = float/double: quantise (crypter path);  XT = uint64_t: raw integers (JoyeLibert.protect)
 template <typename XT>
-__device__ __forceinline__ uint64_t jl_input(const XT* x, uint64_t i, const QuantParams& qp) {
-  return fbm_quantize((double)x[i], qp);
+__device__ __forceinline__ uint64_t jl_input(const XT* x, uint64_t i, const QuantParams& qp, bool& clipped) {
+  const double v = (double)x[i];
+  clipped |= fbm_outside_clip(v, qp);
+  return fbm_quantize(v, qp);
 }
 template <>
-__device__ __forceinline__ uint64_t jl_input<uint64_t>(const uint64_t* x, uint64_t i, const QuantParams&) {
+__device__ __forceinline__ uint64_t jl_input<uint64_t>(const uint64_t* x, uint64_t i, const QuantParams&, bool&) {
   return x[i];
 }
 
 template <typename XT>
 __global__ void __launch_bounds__(256) jl_pack_kernel(const XT* __restrict__ x, uint64_t n, QuantParams qp,
                                                       uint64_t weight, int es, int cr, uint64_t n_ct,
-                                                      uint32_t* __restrict__ pt) {
+                                                      uint32_t* __restrict__ pt, uint32_t* __restrict__ stats) {
   const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t ct = gid >> 5;
   const int L = (int)(gid & 31);
-  if (ct >= n_ct) return;
+  bool clipped = false;
+  if (ct >= n_ct) {
+    flag_if_any(false, stats, FBM_WARN_CLIPPED);
+    return;
+  }
   const uint64_t first = ct * (uint64_t)cr;
   const int cnt = (n - first) >= (uint64_t)cr ? cr : (int)(n - first);
   const int lo_bit = 32 * L;
@@ -54,12 +60,13 @@ __global__ void __launch_bounds__(256) jl_pack_kernel(const XT* __restrict__ x, 
   if (j1 > cnt - 1) j1 = cnt - 1;
   uint32_t w = 0;
   for (int j = j0; j <= j1; ++j) {
-    const uint64_t q = jl_input<XT>(x, first + j, qp);
+    const uint64_t q = jl_input<XT>(x, first + j, qp, clipped);
     const unsigned __int128 v = (unsigned __int128)q * weight;
     const int sh = es * j - lo_bit;
     w |= sh >= 0 ? (uint32_t)(v << sh) : (uint32_t)(v >> (-sh));
   }
   pt[ct * 32 + L] = w;
+  flag_if_any(clipped, stats, FBM_WARN_CLIPPED);
 }
 
 // ------------------------------------------------------------------------------------
@@ -816,17 +823,17 @@ uint64_t jl_table_slots() {
 static inline dim3 grid1(uint64_t items, unsigned block) { return dim3((unsigned)((items + block - 1) / block)); }
 
 int launch_jl_pack(const void* x, int x_dtype, uint64_t n, const QuantParams& qp, uint64_t weight, int es, int cr,
-                   uint64_t n_ct, uint32_t* pt, hipStream_t s) {
+                   uint64_t n_ct, uint32_t* pt, uint32_t* stats, hipStream_t s) {
   if (n_ct == 0) return FBM_OK;
   if (x_dtype == FBM_F32)
     hipLaunchKernelGGL(jl_pack_kernel<float>, grid1(n_ct * 32, 256), dim3(256), 0, s, (const float*)x, n, qp, weight,
-                       es, cr, n_ct, pt);
+                       es, cr, n_ct, pt, stats);
   else if (x_dtype == FBM_F64)
     hipLaunchKernelGGL(jl_pack_kernel<double>, grid1(n_ct * 32, 256), dim3(256), 0, s, (const double*)x, n, qp,
-                       weight, es, cr, n_ct, pt);
+                       weight, es, cr, n_ct, pt, stats);
   else
     hipLaunchKernelGGL(jl_pack_kernel<uint64_t>, grid1(n_ct * 32, 256), dim3(256), 0, s, (const uint64_t*)x, n, qp,
-                       weight, es, cr, n_ct, pt);
+                       weight, es, cr, n_ct, pt, stats);
   return check_launch("jl_pack_kernel");
 }
 

@@ -21,11 +21,13 @@ namespace fbm {
 // XT = float/double: quantise + weight (crypter path); XT = uint64_t: raw integer input
 // (LOM.protect on a list of ints), x == nullptr means an all-zero input.
 template <typename XT>
-__device__ __forceinline__ uint64_t lom_input(const XT* x, uint64_t i, const QuantParams& qp) {
-  return fbm_quantize((double)x[i], qp);
+__device__ __forceinline__ uint64_t lom_input(const XT* x, uint64_t i, const QuantParams& qp, bool& clipped) {
+  const double v = (double)x[i];
+  clipped |= fbm_outside_clip(v, qp);
+  return fbm_quantize(v, qp);
 }
 template <>
-__device__ __forceinline__ uint64_t lom_input<uint64_t>(const uint64_t* x, uint64_t i, const QuantParams&) {
+__device__ __forceinline__ uint64_t lom_input<uint64_t>(const uint64_t* x, uint64_t i, const QuantParams&, bool&) {
   return x ? x[i] : 0ull;
 }
 
@@ -52,8 +54,8 @@ __global__ void __launch_bounds__(256) lom_protect_kernel(const XT* __restrict__
 
   const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + tid;
   const uint64_t base = blk * 8;
-  if (base >= n) return;
-  const int cnt = (n - base) >= 8 ? 8 : (int)(n - base);
+  const int cnt = base >= n ? 0 : ((n - base) >= 8 ? 8 : (int)(n - base));
+  bool clipped = false;
 
   // quantise + weight
   uint64_t val[8];
@@ -61,13 +63,16 @@ __global__ void __launch_bounds__(256) lom_protect_kernel(const XT* __restrict__
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     uint64_t q = 0;
-    if (j < cnt) q = lom_input<XT>(x, base + j, qp);
+    if (j < cnt) q = lom_input<XT>(x, base + j, qp, clipped);
     const uint64_t lo = q * weight;
     const uint64_t hi = __umul64hi(q, weight);
     val[j] = lo;
     const uint32_t bl = fbm_bitlen128(hi, lo);
     maxbits = bl > maxbits ? bl : maxbits;
   }
+
+  flag_if_any(clipped, stats, FBM_WARN_CLIPPED);
+  if (cnt == 0) return;
 
   // masks
   uint64_t mask[8];

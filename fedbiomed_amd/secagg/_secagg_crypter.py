@@ -65,14 +65,6 @@ def _check_int_lists(params) -> None:
             f"should be of type of integers.")
 
 
-def _warn_clipping(x: torch.Tensor, clip) -> None:
-    """`_check_clipping_range` (utils/_secagg_utils.py:190-205): one warning if any |x| > c."""
-    c = SAParameters.CLIPPING_RANGE if clip is None else clip
-    if x.numel() and x.dtype != torch.int64 and bool(((x < -c) | (x > c)).any()):
-        logger.warning("There are some numbers in the local vector that exceeds clipping range. "
-                       "Please increase the clipping range to account for value")
-
-
 class SecaggCrypter:
     """Joye-Libert secure aggregation (encrypt on nodes, aggregate on the researcher)."""
 
@@ -86,7 +78,6 @@ class SecaggCrypter:
             raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: The argument `key` must be integer")
         target_range = target_range or SAParameters.TARGET_RANGE
         _check_weight(weight, jl=True)
-        _warn_clipping(params, clipping_range)
         try:
             return D.jl_encrypt(params, biprime, key, current_round, num_nodes, clip=clipping_range,
                                 target=target_range, weight=1 if weight is None else weight, ct_offset=ct_offset)
@@ -199,7 +190,6 @@ class SecaggLomCrypter(SecaggCrypter):
         `elem_offset`: global index of this shard's first element (multiple of 8)."""
         target_range = target_range or SAParameters.TARGET_RANGE
         _check_weight(weight, jl=False)
-        _warn_clipping(params, clipping_range)
         if params.numel() == 0:
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value} Error during parameter encryption. max() arg is an empty sequence")

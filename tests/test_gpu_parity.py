@@ -266,3 +266,27 @@ def test_jl_roundtrip_property(dev):
     for p in range(P):
         qsum += D.lom_protect(xs[p], [], [], b"\0" * 16, 0, 0, weight=W.party_weight(p))
     assert torch.equal(sums[:, 0], qsum) and int(sums[:, 1].abs().sum()) == 0
+
+
+@pytest.mark.gpu
+def test_clipping_warning_semantics(dev, caplog):
+    """_check_clipping_range (utils/_secagg_utils.py:189-204): one warning when some value is
+    outside [-c, c] (inf included), none for in-range values or NaN -- raised from the
+    kernels' status word, for quantize, LOM and JL encrypt alike."""
+    import logging
+
+    from fedbiomed_amd.secagg import SecaggCrypter, SecaggLomCrypter
+    from fedbiomed_amd.utils import quantize
+    from fedbiomed_amd.workload import BIPRIME0
+
+    msg = "exceeds clipping range"
+    cases = [([0.5, -2.9, 3.0, -3.0], False), ([float("nan"), 1.0], False), ([3.0000001], True),
+             ([float("-inf"), 0.0], True)]
+    for vals, warn in cases:
+        caplog.clear()
+        with caplog.at_level(logging.WARNING, logger="fedbiomed_amd"):
+            quantize(vals, 3)
+            SecaggCrypter().encrypt(2, 1, vals, 5, BIPRIME0, clipping_range=3)
+            SecaggLomCrypter("n").encrypt(1, "a", vals, {"b": b"\x01" * 32}, ["a", "b"], clipping_range=3)
+        hits = sum(msg in r.getMessage() for r in caplog.records)
+        assert hits == (3 if warn else 0), (vals, hits)
