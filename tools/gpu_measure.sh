@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${1:-r1}
 mkdir -p $O
 cd $R
-timeout -k 10 500 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.txt 2>&1 &&
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1 &&
 timeout -k 10 300 python bench.py --steps 2 --warmup 1 > $O/bench.json 2> $O/bench.err &&
 cd /tmp && export TMPDIR=/tmp &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 1 --warmup 0 --serial --no-cpu-baseline --no-lom-extra --no-e2e > $O/prof_bench.json 2> $O/prof.err &&
