@@ -36,19 +36,25 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
+    """`out` / `defines`: variant builds for A/B measurement (tools/ab.sh); the product is OUT."""
+    if out == OUT and not defines and not force and not needs_build():
         return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    tmp = OUT + ".tmp"
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = out + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-           "-I" + os.path.join(ROOT, "include")] + [os.path.join(CSRC, f) for f in SOURCES] + ["-o", tmp]
+           "-I" + os.path.join(ROOT, "include")] + ["-D" + d for d in defines] + \
+        [os.path.join(CSRC, f) for f in SOURCES] + ["-o", tmp]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    # python -m fedbiomed_amd._build [--force] [--out PATH] [-DNAME[=V] ...]
+    args = sys.argv[1:]
+    out = args[args.index("--out") + 1] if "--out" in args else OUT
+    defs = [a[2:] for a in args if a.startswith("-D")]
+    print(build(force="--force" in args, verbose=True, out=out, defines=defs))

@@ -16,6 +16,8 @@ import threading
 import torch  # noqa: F401  (loads the HIP runtime the library must share)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libfbm_secagg.so")
+# A/B measurement of kernel variants (tools/ab.sh): load another build of the same library
+LIB_PATH = os.environ.get("FBM_LIB_PATH", LIB_PATH)
 
 FBM_OK = 0
 FBM_E_ARG = -1

@@ -114,48 +114,84 @@ __global__ void __launch_bounds__(256) lom_protect_kernel(const XT* __restrict__
 }
 
 // Column sum over P parties (mod 2^64) + Python-exact average + dequantise.
-// Two elements per work-item (16-B loads per party row), grid-stride.
+// EPT consecutive elements per work-item (EPT*8-byte loads per party row), grid-stride.
+// PC > 0: party count known at compile time (every row load of a work-item is issued
+// before the first add); PC == 0: runtime count.
+#ifndef FBM_AGG_EPT
+#define FBM_AGG_EPT 2
+#endif
+#ifndef FBM_AGG_WG_PER_CU
+#define FBM_AGG_WG_PER_CU 0  // 0: one pass, no grid-stride (A/B: no measurable difference)
+#endif
+
+__device__ __forceinline__ double lom_avg_dequant(uint64_t s, uint64_t total_weight, double neg_c, double step,
+                                                  uint32_t& err) {
+  const double a = fbm_true_div_u128(s, total_weight);
+  // reverse_quantize guard: value > 2^64-1 (float >= 2^64) -> FB624
+  err |= (a >= 18446744073709551616.0) ? 1u : 0u;
+  return fbm_dequantize(a >= 18446744073709551616.0 ? 0.0 : a, neg_c, step);
+}
+
+template <int EPT, int PC>
 __global__ void __launch_bounds__(256) lom_aggregate_kernel(const uint64_t* __restrict__ y, int n_parties,
                                                             uint64_t n, uint64_t total_weight, double neg_c,
                                                             double step, double* __restrict__ out,
                                                             uint64_t* __restrict__ sums, uint32_t* __restrict__ stats) {
-  const uint64_t npair = (n + 1) / 2;
+  const int P = PC > 0 ? PC : n_parties;
+  const uint64_t ngrp = (n + EPT - 1) / EPT;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const bool vec = (n & 1) == 0;  // rows start 16-B aligned only when n is even
+  // rows start (EPT*8)-byte aligned only when n is a multiple of EPT (and y is aligned)
+  const bool vec = (n % EPT) == 0 && (reinterpret_cast<uintptr_t>(y) % (EPT * 8)) == 0;
   uint32_t err = 0;
-  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < npair; t += stride) {
-    const uint64_t i = 2 * t;
-    uint64_t s0 = 0, s1 = 0;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ngrp; t += stride) {
+    const uint64_t i = (uint64_t)EPT * t;
+    uint64_t sm[EPT];
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) sm[e] = 0;
     if (vec) {
-      for (int p = 0; p < n_parties; ++p) {
-        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(y + (uint64_t)p * n + i);
-        s0 += v.x;
-        s1 += v.y;
+#pragma unroll
+      for (int p = 0; p < (PC > 0 ? PC : 1); ++p) {
+        if (PC == 0) break;
+        const uint64_t* row = static_cast<const uint64_t*>(__builtin_assume_aligned(y + (uint64_t)p * n + i, EPT * 8));
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) sm[e] += row[e];
+      }
+      if (PC == 0) {
+        for (int p = 0; p < P; ++p) {
+          const uint64_t* row =
+              static_cast<const uint64_t*>(__builtin_assume_aligned(y + (uint64_t)p * n + i, EPT * 8));
+#pragma unroll
+          for (int e = 0; e < EPT; ++e) sm[e] += row[e];
+        }
       }
     } else {
-      for (int p = 0; p < n_parties; ++p) {
-        s0 += y[(uint64_t)p * n + i];
-        if (i + 1 < n) s1 += y[(uint64_t)p * n + i + 1];
-      }
+      for (int p = 0; p < P; ++p)
+#pragma unroll
+        for (int e = 0; e < EPT; ++e)
+          if (i + e < n) sm[e] += y[(uint64_t)p * n + i + e];
     }
-    const double a0 = fbm_true_div_u128(s0, total_weight);
-    const double a1 = fbm_true_div_u128(s1, total_weight);
-    // reverse_quantize guard: value > 2^64-1 (float >= 2^64) -> FB624
-    err |= (a0 >= 18446744073709551616.0) ? 1u : 0u;
-    const double o0 = fbm_dequantize(a0 >= 18446744073709551616.0 ? 0.0 : a0, neg_c, step);
-    if (i + 1 < n) {
-      err |= (a1 >= 18446744073709551616.0) ? 1u : 0u;
-      const double o1 = fbm_dequantize(a1 >= 18446744073709551616.0 ? 0.0 : a1, neg_c, step);
-      if (vec) {
-        if (out) *reinterpret_cast<double2*>(out + i) = make_double2(o0, o1);
-        if (sums) *reinterpret_cast<ulonglong2*>(sums + i) = make_ulonglong2(s0, s1);
-      } else {
-        if (out) { out[i] = o0; out[i + 1] = o1; }
-        if (sums) { sums[i] = s0; sums[i + 1] = s1; }
+    double o[EPT];
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) o[e] = (i + e < n) ? lom_avg_dequant(sm[e], total_weight, neg_c, step, err) : 0.0;
+    if (vec) {
+      if (out) {
+        double* od = static_cast<double*>(__builtin_assume_aligned(out + i, EPT * 8));
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) od[e] = o[e];
+      }
+      if (sums) {
+        uint64_t* sd = static_cast<uint64_t*>(__builtin_assume_aligned(sums + i, EPT * 8));
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) sd[e] = sm[e];
       }
     } else {
-      if (out) out[i] = o0;
-      if (sums) sums[i] = s0;
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) {
+        if (i + e < n) {
+          if (out) out[i + e] = o[e];
+          if (sums) sums[i + e] = sm[e];
+        }
+      }
     }
   }
   if (err && out) atomicOr(stats + FBM_STAT_ERRFLAGS, FBM_ERR_DEQUANT_RANGE);
@@ -211,12 +247,24 @@ int launch_prf_key(const LomPeers& peers, uint32_t* seed_out, hipStream_t s) {
 int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t total_weight, double neg_c, double step,
                          double* out, uint64_t* sums, uint32_t* stats, hipStream_t s) {
   if (n == 0) return FBM_OK;
-  const uint64_t npair = (n + 1) / 2;
-  uint64_t g = (npair + 255) / 256;
-  const uint64_t gmax = 256ull * 8ull;  // 256 CUs x 8 workgroups, grid-stride beyond
-  if (g > gmax) g = gmax;
-  hipLaunchKernelGGL(lom_aggregate_kernel, dim3((unsigned)g), dim3(256), 0, s, y, n_parties, n, total_weight, neg_c,
-                     step, out, sums, stats);
+  constexpr int EPT = FBM_AGG_EPT;
+  const uint64_t ngrp = (n + EPT - 1) / EPT;
+  uint64_t g = (ngrp + 255) / 256;
+  const uint64_t gmax = 256ull * FBM_AGG_WG_PER_CU;  // 256 CUs, grid-stride beyond
+  if (FBM_AGG_WG_PER_CU > 0 && g > gmax) g = gmax;
+  const dim3 grid((unsigned)g), block(256);
+#define FBM_AGG_CASE(PC)                                                                                          \
+  case PC:                                                                                                        \
+    hipLaunchKernelGGL((lom_aggregate_kernel<EPT, PC>), grid, block, 0, s, y, n_parties, n, total_weight, neg_c, \
+                       step, out, sums, stats);                                                                   \
+    break;
+  switch (n_parties) {
+    FBM_AGG_CASE(2) FBM_AGG_CASE(3) FBM_AGG_CASE(4) FBM_AGG_CASE(8) FBM_AGG_CASE(16)
+    default:
+      hipLaunchKernelGGL((lom_aggregate_kernel<EPT, 0>), grid, block, 0, s, y, n_parties, n, total_weight, neg_c,
+                         step, out, sums, stats);
+  }
+#undef FBM_AGG_CASE
   return check_launch("lom_aggregate_kernel");
 }
 

@@ -152,6 +152,38 @@ def test_lom_edge_cases(dev):
         assert _bits(agg) == _bits(O.lom_crypter_aggregate(ys, 4))
 
 
+def test_lom_protect_vector_load_paths(dev):
+    """The protect kernel loads whole 8-element blocks with 16-B vector loads when the input
+    is 16-B aligned and falls back to element loads otherwise: f32 / f64 / u64 inputs, each
+    as an aligned tensor and as a view one element in (misaligned), ragged lengths."""
+    from fedbiomed_amd import _device as D, workload as W
+    from fedbiomed_amd.secagg import SecaggLomCrypter
+    from oracle import secagg_oracle as O
+
+    ids = W.node_ids(3)
+    nonce = O.lom_nonce(W.LOM_NONCE)
+    cr = SecaggLomCrypter(W.LOM_NONCE)
+    for n in (8, 13, 1001):
+        base = W.party_params(1, n + 1).astype(np.float64)
+        for dt in (torch.float32, torch.float64):
+            full = torch.from_numpy(base).to(dt).to(dev)
+            for view in (full[:n], full[1:]):
+                xs = view.cpu().numpy().astype(np.float64).tolist()
+                for u in ids:
+                    got = cr.encrypt_tensor(2, u, view, W.pairwise_secrets_for(u, ids), ids, weight=3)
+                    ref = O.lom_encrypt(xs, 2, u, W.pairwise_secrets_for(u, ids), ids, nonce, weight=3)
+                    assert np.array_equal(got.cpu().numpy().view(np.uint64), ref), (n, dt, u)
+        ints = torch.arange(5, 5 + n + 1, dtype=torch.int64, device=dev) * 977
+        for view in (ints[:n], ints[1:]):
+            xi = [int(v) for v in view.cpu().numpy()]
+            u = ids[1]
+            peers = [p for p in ids if p != u]
+            sec = [O.prf_eval_key(W.pairwise_secrets_for(u, ids)[p], nonce, 4) for p in peers]
+            got = D.lom_protect(view, sec, [1 if p < u else -1 for p in peers], nonce, 4, len(ids), raw_seeds=True)
+            ref = O.lom_protect(u, W.pairwise_secrets_for(u, ids), 4, xi, ids, nonce)
+            assert np.array_equal(got.cpu().numpy().view(np.uint64), ref), n
+
+
 def test_lom_large_mask_cancellation(dev):
     """Size-independent property at a bench-scale vector: sum of masked = sum of q*w."""
     from fedbiomed_amd import _device as D, workload as W

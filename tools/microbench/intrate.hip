@@ -143,6 +143,46 @@ __global__ void k_mul24(uint64_t* out, uint32_t s) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = x;
 }
 
+#define K32(NAME, ASM)                                                                  \
+  __global__ void NAME(uint64_t* out, uint32_t s) {                                     \
+    uint32_t a = threadIdx.x + s;                                                       \
+    uint32_t acc[CH];                                                                   \
+    _Pragma("unroll") for (int c = 0; c < CH; ++c) acc[c] = c + a;                      \
+    for (int i = 0; i < ITER; ++i) {                                                    \
+      _Pragma("unroll") for (int c = 0; c < CH; ++c) {                                  \
+        uint32_t r;                                                                     \
+        asm volatile(ASM : "=v"(r) : "v"(acc[c]), "v"(a));                              \
+        acc[c] = r;                                                                     \
+      }                                                                                 \
+    }                                                                                   \
+    uint64_t x = 0;                                                                     \
+    _Pragma("unroll") for (int c = 0; c < CH; ++c) x ^= acc[c];                         \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = x;                                     \
+  }
+K32(k_add32, "v_add_u32 %0, %1, %2")
+K32(k_xor32, "v_xor_b32 %0, %1, %2")
+K32(k_align, "v_alignbit_b32 %0, %1, %1, 16")
+K32(k_perm, "v_perm_b32 %0, %1, %1, %2")
+K32(k_lshlor, "v_lshl_or_b32 %0, %1, 7, %2")
+K32(k_xad, "v_xad_u32 %0, %1, %2, %1")
+K32(k_bfi, "v_pk_add_u16 %0, %1, %2")
+
+// ChaCha20 double-rounds as the LOM kernel runs them (ITER/64 blocks per lane); ops counted
+// as 976 per block (the kernel's add/xor/rotate count).
+#include "../../fedbiomed_amd/csrc/fbm_common.hpp"
+#define CHACHA_BLOCKS (ITER / 16)
+__global__ void k_chacha(uint64_t* out, uint32_t s) {
+  uint32_t key[8];
+  for (int w = 0; w < 8; ++w) key[w] = threadIdx.x * 31u + w + s;
+  uint32_t x = 0;
+  for (int b = 0; b < CHACHA_BLOCKS; ++b) {
+    uint32_t ks[16];
+    fbm_chacha20_block(key, (uint64_t)blockIdx.x * 1000 + b, s, x, ks);
+    for (int w = 0; w < 16; ++w) x ^= ks[w];
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+
 typedef void (*kfn)(uint64_t*, uint32_t);
 
 int main() {
@@ -152,7 +192,8 @@ int main() {
   struct { const char* name; kfn f; } ks[] = {
       {"v_mad_u64_u32", k_mad64}, {"v_mul_lo_u32", k_mullo}, {"v_mul_hi_u32", k_mulhi},
       {"v_add_co_u32", k_addc},   {"v_add3_u32", k_add3},    {"v_fma_f64", k_fma64},
-      {"v_mad_u32_u24", k_mul24}};
+      {"v_mad_u32_u24", k_mul24}, {"v_add_u32", k_add32}, {"v_xor_b32", k_xor32},
+      {"v_alignbit_b32", k_align}, {"v_perm_b32", k_perm}, {"v_lshl_or_b32", k_lshlor}, {"v_xad_u32", k_xad}, {"v_pk_add_u16", k_bfi}, {"chacha20 (976/blk)", k_chacha}};
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
@@ -170,6 +211,7 @@ int main() {
       if (ms < best) best = ms;
     }
     double ops = (double)blocks * threads * ITER * CH;
+    if (k.f == k_chacha) ops = (double)blocks * threads * CHACHA_BLOCKS * 976.0;
     printf("%-16s %8.3f ms  %8.1f G lane-ops/s  (%.2f cyc/wave-instr @2.4GHz/1024 SIMDs)\n", k.name, best,
            ops / best / 1e6, (1024.0 * 2.4e9) / (ops / 64.0 / (best * 1e-3)));
   }
