@@ -413,6 +413,56 @@ def ass_reconstruct(shares: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def ass_split_wide(secret: torch.Tensor, n_shares: int, l_out: int, bit_length: Optional[int] = None,
+                   seed: Optional[bytes] = None, nonce: Optional[bytes] = None, elem_offset: int = 0) -> torch.Tensor:
+    """int32 [l_in, n] two's-complement limbs (limb-major) -> int32 [n_shares, l_out, n] shares."""
+    import secrets as _secrets
+
+    lib = N.load()
+    secret = secret.contiguous()
+    l_in, n = secret.shape
+    shares = torch.empty((n_shares, l_out, n), dtype=torch.int32, device=secret.device)
+    seed = seed if seed is not None else _secrets.token_bytes(32)
+    nonce = nonce if nonce is not None else _secrets.token_bytes(8)
+    if len(seed) != 32 or len(nonce) != 8:
+        raise ValueError("seed must be 32 bytes and nonce 8 bytes")
+    sb = np.frombuffer(seed, dtype=np.uint8).copy()
+    nb = np.frombuffer(nonce, dtype=np.uint8).copy()
+    _call(lib.fbm_ass_split_wide, _ptr(secret), n, int(l_in), int(n_shares),
+          -1 if bit_length is None else int(bit_length), int(l_out), _np_ptr(sb), _np_ptr(nb), int(elem_offset),
+          _ptr(shares), _stream())
+    return shares
+
+
+def ass_reconstruct_wide(shares: torch.Tensor) -> torch.Tensor:
+    """int32 [P, l, n] two's-complement limbs -> int32 [l, n] column sum mod 2^(32 l)."""
+    lib = N.load()
+    shares = shares.contiguous()
+    P, L, n = shares.shape
+    out = torch.empty((L, n), dtype=torch.int32, device=shares.device)
+    _call(lib.fbm_ass_reconstruct_wide, _ptr(shares), int(P), int(L), n, _ptr(out), _stream())
+    return out
+
+
+def ints_to_limbs_tc(values: Sequence[int], n_limbs: int) -> np.ndarray:
+    """Python ints -> int32 [n_limbs, n] two's-complement u32 limbs, limb-major."""
+    mod = 1 << (32 * n_limbs)
+    blob = b"".join((int(v) % mod).to_bytes(4 * n_limbs, "little") for v in values)
+    return np.frombuffer(blob, dtype="<u4").reshape(len(values), n_limbs).T.copy().view(np.int32)
+
+
+def limbs_tc_to_ints(arr: np.ndarray) -> List[int]:
+    """int32 [n_limbs, n] two's-complement limbs (limb-major) -> Python ints."""
+    L = arr.shape[0]
+    rows = np.ascontiguousarray(arr.view(np.uint32).T).astype("<u4")
+    top = 1 << (32 * L - 1)
+    out = []
+    for r in rows:
+        w = int.from_bytes(r.tobytes(), "little")
+        out.append(w - (top << 1) if w & top else w)
+    return out
+
+
 def ints_to_int128(values: Sequence[int]) -> np.ndarray:
     """Python ints in [-2^127, 2^127) -> int64 [n, 2] (lo, hi) two's complement."""
     out = np.empty((len(values), 2), dtype=np.int64)

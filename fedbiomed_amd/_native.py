@@ -61,6 +61,8 @@ SIGNATURES = {
                                  c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fbm_ass_split": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_vp, c_vp, c_u64, c_vp, c_vp]),
     "fbm_ass_reconstruct": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp]),
+    "fbm_ass_split_wide": (c_int, [c_vp, c_u64, c_int, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_vp, c_vp]),
+    "fbm_ass_reconstruct_wide": (c_int, [c_vp, c_int, c_int, c_u64, c_vp, c_vp]),
     "fbm_test_modinv": (c_int, [c_vp, c_vp, c_vp, c_vp]),
     "fbm_prof_enable": (c_int, [c_int]),
     "fbm_prof_report": (c_int, [ctypes.c_char_p, c_int]),

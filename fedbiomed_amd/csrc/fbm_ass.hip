@@ -83,6 +83,141 @@ __global__ void __launch_bounds__(256) ass_reconstruct_kernel(const int64_t* __r
   *reinterpret_cast<longlong2*>(out + i * 2) = make_longlong2((int64_t)(uint64_t)acc, (int64_t)(uint64_t)(acc >> 64));
 }
 
+// ------------------------------------------------------------------------------------------
+// Wide path: secrets of any size (the reference's scalar use is the 2040-bit JL user key,
+// node/secagg/_secagg_setups.py:248-268; researcher/secagg/_secagg_context.py:380).
+// Values are two's-complement u32 limbs, limb-major: word (s*L + k)*n + i (share s, limb k,
+// element i), so a wave's access to one limb is coalesced.  Share draw r uniform on [0, 2^b]:
+// x = first b+64 bits of the share's ChaCha20 stream (LE words), r = (x >> 64) + carry,
+// carry = [x mod 2^64 + (x >> b) >= 2^64] -- that is floor(x (2^b + 1) / 2^(b+64)), the
+// multiply-high (Lemire) map of the 128-bit path above, for any b.
+struct AssWide {
+  uint32_t key[8];
+  uint32_t n14, n15;
+  uint64_t elem_offset;
+  int n_shares;
+  int bit_length;  // < 0: bit length of |v| per element
+  int l_in, l_out; // limbs of a secret / of a share
+  int blocks;      // ChaCha20 blocks per share draw (ceil((b_max + 64) / 512))
+};
+
+// word w (w < 16*blocks) of the draw stream of (element e, share s); one block is cached
+struct AssStream {
+  uint32_t ks[16];
+  uint64_t cur;
+  __device__ __forceinline__ uint32_t word(const AssWide& p, uint64_t base, int w) {
+    const uint64_t blk = base + (uint64_t)(w >> 4);
+    if (blk != cur) {
+      fbm_chacha20_block(p.key, blk, p.n14, p.n15, ks);
+      cur = blk;
+    }
+    return ks[w & 15];
+  }
+};
+
+__global__ void __launch_bounds__(256) ass_split_wide_kernel(const uint32_t* __restrict__ secret, uint64_t n,
+                                                             AssWide p, uint32_t* __restrict__ shares) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int L = p.l_out;
+  auto sec = [&](int k) -> uint32_t {  // sign-extended secret limb k
+    if (k < p.l_in) return secret[(uint64_t)k * n + i];
+    return (secret[(uint64_t)(p.l_in - 1) * n + i] >> 31) ? 0xffffffffu : 0u;
+  };
+  const bool neg = sec(p.l_in - 1) >> 31;
+  int b = p.bit_length;
+  if (b < 0) {  // bit length of |v|: of v for v >= 0, of ~v + 1 otherwise
+    b = 0;
+    uint32_t carry = 1;
+    for (int k = 0; k < p.l_in; ++k) {
+      uint32_t w = sec(k);
+      if (neg) {
+        const uint64_t t = (uint64_t)(~w) + carry;
+        w = (uint32_t)t;
+        carry = (uint32_t)(t >> 32);
+      }
+      if (w) b = 32 * k + 32 - __builtin_clz(w);
+    }
+  }
+  uint32_t* last = shares + (uint64_t)(p.n_shares - 1) * L * n;  // running v - sum(shares)
+  for (int k = 0; k < L; ++k) last[(uint64_t)k * n + i] = sec(k);
+  const int xw = (b + 64 + 31) / 32;  // words of x
+  const uint32_t topmask = ((b + 64) & 31) ? ((1u << ((b + 64) & 31)) - 1u) : 0xffffffffu;
+  for (int sh = 0; sh < p.n_shares - 1; ++sh) {
+    const uint64_t base = ((p.elem_offset + i) * (uint64_t)(p.n_shares - 1) + (uint64_t)sh) * (uint64_t)p.blocks;
+    AssStream st;
+    st.cur = ~0ull;
+    auto xword = [&](int w) -> uint32_t {
+      if (w >= xw) return 0u;
+      const uint32_t v = st.word(p, base, w);
+      return w == xw - 1 ? (v & topmask) : v;
+    };
+    // q = x >> b (64 bits: x has b + 64 bits)
+    const int wq = b >> 5, sq = b & 31;
+    const unsigned __int128 v96 = ((unsigned __int128)xword(wq + 2) << 64) |
+                                  ((unsigned __int128)xword(wq + 1) << 32) | (unsigned __int128)xword(wq);
+    const uint64_t q = (uint64_t)(v96 >> sq);
+    const uint64_t xl = (uint64_t)xword(0) | ((uint64_t)xword(1) << 32);
+    uint32_t carry = (xl + q < xl) ? 1u : 0u;
+    // r = (x >> 64) + carry; share limb k = word k + 2; last -= r
+    uint32_t* out = shares + (uint64_t)sh * L * n;
+    uint32_t borrow = 0;
+    for (int k = 0; k < L; ++k) {
+      const uint64_t rk = (uint64_t)xword(k + 2) + carry;
+      const uint32_t r = (uint32_t)rk;
+      carry = (uint32_t)(rk >> 32);
+      out[(uint64_t)k * n + i] = r;
+      const uint64_t l = (uint64_t)last[(uint64_t)k * n + i] - r - borrow;
+      last[(uint64_t)k * n + i] = (uint32_t)l;
+      borrow = (uint32_t)(l >> 63);
+    }
+  }
+}
+
+// exact column sum of P two's-complement L-limb values (result L limbs, wraps mod 2^(32L):
+// the caller sizes L so the true sum fits)
+__global__ void __launch_bounds__(256) ass_reconstruct_wide_kernel(const uint32_t* __restrict__ shares,
+                                                                   int n_shares, int L, uint64_t n,
+                                                                   uint32_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t carry = 0;  // signed carry into limb k, kept as a two's-complement 64-bit value
+  for (int k = 0; k < L; ++k) {
+    int64_t acc = (int64_t)carry;
+    for (int s = 0; s < n_shares; ++s) acc += (int64_t)(uint64_t)shares[((uint64_t)s * L + k) * n + i];
+    out[(uint64_t)k * n + i] = (uint32_t)(uint64_t)acc;
+    carry = (uint64_t)(acc >> 32);  // arithmetic shift: limbs are unsigned digits, carry may be 0..P
+  }
+}
+
+int launch_ass_split_wide(const uint32_t* secret, uint64_t n, int l_in, const uint32_t* key, uint32_t n14,
+                          uint32_t n15, uint64_t elem_offset, int n_shares, int bit_length, int l_out,
+                          uint32_t* shares, hipStream_t s) {
+  if (n == 0) return FBM_OK;
+  AssWide p;
+  for (int w = 0; w < 8; ++w) p.key[w] = key[w];
+  p.n14 = n14;
+  p.n15 = n15;
+  p.elem_offset = elem_offset;
+  p.n_shares = n_shares;
+  p.bit_length = bit_length;
+  p.l_in = l_in;
+  p.l_out = l_out;
+  const int bmax = bit_length >= 0 ? bit_length : 32 * l_in;
+  p.blocks = (bmax + 64 + 511) / 512;
+  hipLaunchKernelGGL(ass_split_wide_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, secret, n, p,
+                     shares);
+  return check_launch("ass_split_wide_kernel");
+}
+
+int launch_ass_reconstruct_wide(const uint32_t* shares, int n_shares, int l, uint64_t n, uint32_t* out,
+                                hipStream_t s) {
+  if (n == 0) return FBM_OK;
+  hipLaunchKernelGGL(ass_reconstruct_wide_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, shares,
+                     n_shares, l, n, out);
+  return check_launch("ass_reconstruct_wide_kernel");
+}
+
 int launch_ass_split(const uint64_t* secret, uint64_t n, const uint32_t* key, uint32_t n14, uint32_t n15,
                      uint64_t elem_offset, int n_shares, int bit_length, int is_signed, int64_t* shares,
                      hipStream_t s) {

@@ -590,6 +590,48 @@ int fbm_ass_reconstruct(const int64_t* shares, int n_shares, uint64_t n, int64_t
   return timed("ass_reconstruct", s, [&] { return launch_ass_reconstruct(shares, n_shares, n, out, s); });
 }
 
+int fbm_ass_split_wide(const uint32_t* secret, uint64_t n, int l_in, int n_shares, int bit_length, int l_out,
+                       const uint8_t* seed, const uint8_t* nonce, uint64_t elem_offset, uint32_t* shares,
+                       void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int bmax = bit_length >= 0 ? bit_length : 32 * l_in;
+  int pbits = 0;
+  while ((1ll << pbits) < (long long)n_shares) ++pbits;
+  if (n_shares < 1 || l_in < 1 || l_in > 4096 || l_out < l_in || !seed || !nonce ||
+      32ll * l_out < (long long)bmax + pbits + 2 || bmax > (1 << 20)) {
+    set_error("invalid wide additive-sharing arguments (n_shares >= 1, 1 <= l_in <= l_out, "
+              "32*l_out >= bits + ceil(log2 n_shares) + 2)");
+    return FBM_E_ARG;
+  }
+  if (n == 0) return FBM_OK;
+  if (!secret || !shares) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  uint32_t key[8], nw[2];
+  memcpy(key, seed, 32);
+  memcpy(nw, nonce, 8);
+  return timed("ass_split_wide", s, [&] {
+    return launch_ass_split_wide(secret, n, l_in, key, nw[0], nw[1], elem_offset, n_shares, bit_length, l_out,
+                                 shares, s);
+  });
+}
+
+int fbm_ass_reconstruct_wide(const uint32_t* shares, int n_shares, int l, uint64_t n, uint32_t* out, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n_shares < 1 || l < 1) {
+    set_error("n_shares and l must be >= 1");
+    return FBM_E_ARG;
+  }
+  if (n == 0) return FBM_OK;
+  if (!shares || !out) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  return timed("ass_reconstruct_wide", s,
+               [&] { return launch_ass_reconstruct_wide(shares, n_shares, l, n, out, s); });
+}
+
 }  // extern "C"
 
 extern "C" {

@@ -108,6 +108,11 @@ int launch_ass_split(const uint64_t* secret, uint64_t n, const uint32_t* key, ui
                      uint64_t elem_offset, int n_shares, int bit_length, int is_signed, int64_t* shares,
                      hipStream_t s);
 int launch_ass_reconstruct(const int64_t* shares, int n_shares, uint64_t n, int64_t* out, hipStream_t s);
+int launch_ass_split_wide(const uint32_t* secret, uint64_t n, int l_in, const uint32_t* key, uint32_t n14,
+                          uint32_t n15, uint64_t elem_offset, int n_shares, int bit_length, int l_out,
+                          uint32_t* shares, hipStream_t s);
+int launch_ass_reconstruct_wide(const uint32_t* shares, int n_shares, int l, uint64_t n, uint32_t* out,
+                                hipStream_t s);
 
 // table slots the encrypt/aggregate kernels need for a given grid
 uint64_t jl_table_slots();

@@ -3,12 +3,12 @@
 
 `AdditiveSecret.split` (:40-98), `AdditiveShare.__add__` (:134-160) and
 `AdditiveShares.reconstruct` (:252-267) keep the reference's classes, signatures, validation
-and exceptions; the per-element work (share draws, exact sums) runs in `fbm_ass_split` /
-`fbm_ass_reconstruct` (fedbiomed_amd/csrc/fbm_ass.hip).  Device domain: secrets in
-[-2^63, 2^64) and shares/sums in the int128 range -- the per-element (vector) use.  The
-2040-bit scalar key shares of the JL key setup (`node/secagg/_secagg_setups.py:248-268`,
-setup-time, out of scope) keep using the reference implementation; values outside the
-device domain raise FedbiomedValueError instead of being computed on the host.
+and exceptions; the per-element work (share draws, exact sums) runs on the device:
+`fbm_ass_split` / `fbm_ass_reconstruct` (int128 lanes) for secrets in [-2^63, 2^64) -- the
+per-element vector use -- and `fbm_ass_split_wide` / `fbm_ass_reconstruct_wide`
+(two's-complement u32 limbs of any width) for everything else, e.g. the 2040-bit JL user key
+the key setup splits (`node/secagg/_secagg_setups.py:248-268`) and the server-key shares the
+researcher sums (`researcher/secagg/_secagg_context.py:380-382`).
 
 The reference draws shares from Python's MT19937 (`random.randint`); here they come from a
 counter-based ChaCha20 stream.  What both guarantee -- and what the tests pin -- is the
@@ -27,6 +27,11 @@ import torch
 
 from .. import _device as D
 from ..exceptions import FedbiomedTypeError, FedbiomedValueError
+
+
+def _in_64bit_domain(values: List[int]) -> bool:
+    lo, hi = min(values), max(values)
+    return not (lo < D.I64_MIN or hi >= D.U64_LIM or (lo < 0 and hi >= 2**63))
 
 
 def _device_domain(values: List[int]) -> bool:
@@ -60,13 +65,19 @@ class AdditiveSecret:
                     raise FedbiomedValueError("Bit length must be greater or equal than the secret's bit length")
         if not values:
             return AdditiveShares([AdditiveShare([]) for _ in range(num_shares)])
-        unsigned = _device_domain(values)
-        if bit_length is not None and bit_length > 64:
-            raise FedbiomedValueError("The device additive secret sharing supports bit_length <= 64")
-        host = np.array([v if not unsigned or v < 2**63 else v - 2**64 for v in values], dtype=np.int64)
-        sec = torch.from_numpy(host).to(D.device())
-        shares = D.ass_split(sec, num_shares, bit_length, unsigned=unsigned)
-        rows = [D.int128_to_ints(s) for s in shares.cpu().numpy()]
+        if _in_64bit_domain(values) and (bit_length is None or bit_length <= 64):
+            unsigned = _device_domain(values)
+            host = np.array([v if not unsigned or v < 2**63 else v - 2**64 for v in values], dtype=np.int64)
+            sec = torch.from_numpy(host).to(D.device())
+            shares = D.ass_split(sec, num_shares, bit_length, unsigned=unsigned)
+            rows = [D.int128_to_ints(s) for s in shares.cpu().numpy()]
+        else:  # wide limbs: e.g. the 2040-bit JL user key of the key setup
+            bmax = max(abs(v).bit_length() for v in values) if bit_length is None else bit_length
+            l_in = (max(abs(v).bit_length() for v in values) + 1 + 31) // 32 + 1
+            l_out = max(l_in + 1, (bmax + (num_shares - 1).bit_length() + 2 + 31) // 32 + 1)
+            sec = torch.from_numpy(D.ints_to_limbs_tc(values, l_in)).to(D.device())
+            shares = D.ass_split_wide(sec, num_shares, l_out, bit_length)
+            rows = [D.limbs_tc_to_ints(s) for s in shares.cpu().numpy()]
         if isinstance(self._secret, int):
             return AdditiveShares([AdditiveShare(r[0]) for r in rows])
         return AdditiveShares([AdditiveShare(r) for r in rows])
@@ -112,15 +123,19 @@ class AdditiveShare:
 
 
 def _reconstruct(rows: List[List[int]]) -> List[int]:
-    """Exact column sum of equal-length int rows on the device (int128 domain)."""
+    """Exact column sum of equal-length int rows on the device: int128 lanes when the
+    values and their sum fit, two's-complement u32 limbs of any width otherwise."""
     if not rows or not rows[0]:
         return []
-    try:
+    bits = max(abs(int(v)).bit_length() for r in rows for v in r)
+    if bits + len(rows).bit_length() < 126:
         arr = np.stack([D.ints_to_int128(r) for r in rows])
-    except ValueError as e:
-        raise FedbiomedValueError(str(e)) from e
-    out = D.ass_reconstruct(torch.from_numpy(arr).to(D.device()))
-    return D.int128_to_ints(out.cpu().numpy())
+        out = D.ass_reconstruct(torch.from_numpy(arr).to(D.device()))
+        return D.int128_to_ints(out.cpu().numpy())
+    L = (bits + len(rows).bit_length() + 2 + 31) // 32
+    arr = np.stack([D.ints_to_limbs_tc(r, L) for r in rows])
+    out = D.ass_reconstruct_wide(torch.from_numpy(arr).to(D.device()))
+    return D.limbs_tc_to_ints(out.cpu().numpy())
 
 
 class AdditiveShares(list):

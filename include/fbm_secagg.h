@@ -151,6 +151,20 @@ int fbm_ass_split(const void* secret, int secret_dtype, uint64_t n, int n_shares
                   const uint8_t* seed, const uint8_t* nonce, uint64_t elem_offset, int64_t* shares, void* stream);
 int fbm_ass_reconstruct(const int64_t* shares, int n_shares, uint64_t n, int64_t* out, void* stream);
 
+/* Wide additive sharing: secrets of any size, e.g. the 2040-bit JL user key the reference
+ * splits at setup (node/secagg/_secagg_setups.py:248-268) and the server-key shares it sums
+ * (researcher/secagg/_secagg_context.py:380-382).  Same contract as fbm_ass_split, with
+ * two's-complement u32 limbs, limb-major (word k*n + i of element i):
+ *   secret  device, l_in x n words;  shares device, n_shares x l_out x n words, where
+ *   l_out >= words of (b + ceil(log2 n_shares) + 2) bits (the caller sizes it; b <= 32*l_in
+ *   when bit_length < 0);  bit_length >= 0 overrides the per-element |v| bit length.
+ * fbm_ass_reconstruct_wide: out (l x n words) = column sum mod 2^(32 l) of n_shares
+ *   l-limb values -- exact when the caller's l holds the true sum. */
+int fbm_ass_split_wide(const uint32_t* secret, uint64_t n, int l_in, int n_shares, int bit_length, int l_out,
+                       const uint8_t* seed, const uint8_t* nonce, uint64_t elem_offset, uint32_t* shares,
+                       void* stream);
+int fbm_ass_reconstruct_wide(const uint32_t* shares, int n_shares, int l, uint64_t n, uint32_t* out, void* stream);
+
 /* ---- host test hook (no GPU): the device modular-inverse routine (Bernstein-Yang divsteps,
  * fedbiomed_amd/csrc/fbm_safegcd.hpp) run on the host, for unit tests.
  * x, n, out: 32 little-endian words (n odd);  batches: number of 30-divstep batches used. */

@@ -55,7 +55,6 @@ def dev():
 @pytest.mark.gpu
 def test_reconstruct_reference_shares(golden, dev):
     """Reconstruct the reference's own shares (int and list secrets) bit-exactly."""
-    from fedbiomed_amd.exceptions import FedbiomedValueError
     from fedbiomed_amd.secagg import AdditiveShare, AdditiveShares
 
     for case in golden["ass"]["cases"]:
@@ -66,11 +65,7 @@ def test_reconstruct_reference_shares(golden, dev):
         else:
             shares = AdditiveShares([AdditiveShare(I(s)) for s in sh])
             want = I(case["reconstruct"])
-        if max(abs(I(x)) for s in sh for x in (s if isinstance(s, list) else [s])) >= 2**126:
-            with pytest.raises(FedbiomedValueError):  # 2040-bit key shares: reference-side only
-                shares.reconstruct()
-            continue
-        assert shares.reconstruct() == want
+        assert shares.reconstruct() == want  # incl. the 2040-bit key shares (wide limb path)
         assert sum(shares).value == want  # __radd__/__add__ path (a single AdditiveShare)
 
 
@@ -126,3 +121,64 @@ def test_split_bit_length_and_offsets(dev):
     sh = AdditiveSecret(12345678901234567890).split(3)
     assert isinstance(sh[0].value, int) and sh.reconstruct() == 12345678901234567890
     assert AdditiveSecret([-7, 9]).split(2, bit_length=None).reconstruct() == [-7, 9]
+
+
+@pytest.mark.gpu
+def test_split_wide_key_setup(dev):
+    """The JL key setup's use (node/secagg/_secagg_setups.py:248-268): a 2040-bit user key
+    split into one share per party, the shares summed back -- and wide vectors, negative
+    values, explicit bit lengths, shard offsets."""
+    import random
+
+    from fedbiomed_amd.secagg import AdditiveSecret, AdditiveShare, AdditiveShares
+
+    rnd = random.Random(5)
+    for P in (1, 2, 3, 8, 17):
+        sk = rnd.getrandbits(2040)
+        shares = AdditiveSecret(sk).split(P).to_list()
+        assert len(shares) == P and sum(shares) == sk
+        b = sk.bit_length()
+        assert all(0 <= v <= 2**b for v in shares[:-1])
+        # the setup's own sequence: last share kept, the others summed as AdditiveShares
+        mine = AdditiveShare(shares.pop(-1))
+        if not shares:  # one party: sum([]) == 0 and share + 0 raises, as in the reference
+            continue
+        assert (mine + sum(AdditiveShares([AdditiveShare(v) for v in shares]))).value == sk
+    # server key: sum of negative 2040-bit shares (researcher/secagg/_secagg_context.py:380)
+    neg = [-rnd.getrandbits(2040) for _ in range(5)]
+    assert AdditiveShares([AdditiveShare(v) for v in neg]).reconstruct() == sum(neg)
+    # list secrets beyond 64 bits, mixed signs, bit_length given
+    vals = [0, 1, -1, 2**64, -(2**64) - 5, 2**200 + 3, -(2**130)]
+    sh = AdditiveSecret(vals).split(4)
+    assert sh.reconstruct() == vals
+    sh = AdditiveSecret([2**70, 5]).split(3, bit_length=300)
+    assert sh.reconstruct() == [2**70, 5]
+    assert all(0 <= v <= 2**300 for s in sh.to_list()[:-1] for v in s)
+    # device tensors: shards with element offsets reproduce the unsharded draw
+    vals = [rnd.getrandbits(500) - 2**499 for _ in range(3000)]
+    sec = torch.from_numpy(D.ints_to_limbs_tc(vals, 17)).to(dev)
+    seed, nonce = bytes(range(32)), b"12345678"
+    whole = D.ass_split_wide(sec, 6, 18, seed=seed, nonce=nonce)
+    parts = [D.ass_split_wide(sec[:, a:b], 6, 18, seed=seed, nonce=nonce, elem_offset=a)
+             for a, b in [(0, 1000), (1000, 2999), (2999, 3000)]]
+    assert torch.equal(torch.cat(parts, dim=2), whole)
+    assert D.limbs_tc_to_ints(D.ass_reconstruct_wide(whole).cpu().numpy()) == vals
+    first = D.limbs_tc_to_ints(whole[0].cpu().numpy())
+    assert all(0 <= v <= 2**abs(x).bit_length() for v, x in zip(first, vals))
+    assert len(set(first)) > 2990  # draws are not degenerate
+
+
+def test_wide_limb_roundtrip_and_draw_map():
+    """Host checks of the wide path's conversions and of the share-draw map the kernel
+    uses: r = (x >> 64) + [x mod 2^64 + (x >> b) >= 2^64] == floor(x (2^b + 1) / 2^(b+64))."""
+    import random
+
+    vals = [0, 1, -1, 2**64, -(2**64) - 5, 2**200 + 3, -(2**130), 2**255 - 1, -(2**255)]
+    assert D.limbs_tc_to_ints(D.ints_to_limbs_tc(vals, 8)) == vals
+    rnd = random.Random(3)
+    for b in (0, 1, 31, 32, 33, 63, 64, 65, 100, 2040):
+        for _ in range(200):
+            x = rnd.getrandbits(b + 64)
+            carry = int((x & (2**64 - 1)) + (x >> b) >= 2**64)
+            r = (x >> 64) + carry
+            assert r == (x * (2**b + 1)) >> (b + 64) and 0 <= r <= 2**b
