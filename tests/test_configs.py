@@ -1,0 +1,169 @@
+"""BASELINE.json configurations as GPU parity cases, at their own sizes.
+
+  cfg 1  LOM mask+unmask, 1k elements, 2 parties             -> bit-exact vs the oracle, whole vector
+  cfg 2  JL encrypt+aggregate, 100k elements, 4 parties        -> sampled ciphertexts bit-exact vs the
+                                                                  oracle + exact decoded sums (all elements)
+  cfg 3  LOM round of the 101 notebook's MNIST net, 4 nodes    -> one party bit-exact, mask cancellation
+         (1,199,882 parameters)                     exact over all elements
+  cfg 5  LOM masking + additive secret sharing, 100M elements, -> mask cancellation exact, sampled
+         16 parties                                               windows bit-exact, split/reconstruct exact
+cfg 4 (JL 10M x 8 parties) is the bench workload; its element-range sharding is covered by
+tests/test_distributed.py.  Oracle = oracle/secagg_oracle.py (pinned to the reference's own
+vectors in tests/test_oracle_golden.py).  Tolerance: 0 -- integers compared exactly, float64
+outputs compared as bit patterns.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from fedbiomed_amd import _device as D, workload as W
+from oracle import secagg_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    return D.device()
+
+
+def _u64(t: torch.Tensor) -> np.ndarray:
+    return t.cpu().numpy().view(np.uint64)
+
+
+def _qw(x: np.ndarray, w: int) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        return O.quantize(x) * np.uint64(w)
+
+
+def _lom_window_oracle(u, ids, tau, qw_window, offset, nonce):
+    """LOM.protect (secagg/_lom.py:105-175) restricted to elements [offset, offset+len):
+    ChaCha20 blocks from offset/8 on (the keystream is counter-indexed)."""
+    n = len(qw_window)
+    mask = np.zeros(n, dtype=np.uint64)
+    idx = (np.arange(offset, offset + n, dtype=np.uint64) + np.uint64(tau)).byteswap()
+    sec = W.pairwise_secrets_for(u, ids)
+    with np.errstate(over="ignore"):
+        for p in ids:
+            if p == u:
+                continue
+            seed = O.prf_eval_key(sec[p], nonce, tau)
+            ks = O.chacha20_blocks(seed, nonce, offset // 8, (n + 7) // 8).astype("<u4").view("<u8").reshape(-1)[:n]
+            vec = ks ^ idx
+            mask = mask + vec if p < u else mask - vec
+        return mask + qw_window
+
+
+def test_cfg1_lom_1k_2_parties(dev):
+    from fedbiomed_amd.secagg import SecaggLomCrypter
+
+    n, P, tau = 1000, 2, 1
+    ids, ws = W.node_ids(P), [W.party_weight(p) for p in range(P)]
+    cr = SecaggLomCrypter(W.LOM_NONCE)
+    xs = [W.party_params(p, n).astype(np.float64).tolist() for p in range(P)]
+    ys = [cr.encrypt(tau, u, xs[p], W.pairwise_secrets_for(u, ids), ids, weight=ws[p]) for p, u in enumerate(ids)]
+    for p, u in enumerate(ids):
+        ref = O.lom_encrypt(xs[p], tau, u, W.pairwise_secrets_for(u, ids), ids, O.lom_nonce(W.LOM_NONCE),
+                            weight=ws[p])
+        assert ys[p] == [int(v) for v in ref]
+    out = cr.aggregate(ys, sum(ws))
+    assert np.array_equal(np.asarray(out).view(np.uint64), O.lom_crypter_aggregate(ys, sum(ws)).view(np.uint64))
+
+
+def test_cfg2_jl_100k_4_parties(dev):
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    n, P, tau = 100_000, 4, 1
+    ws = [W.party_weight(p) for p in range(P)]
+    keys = [W.jl_user_key(p) for p in range(P)]
+    es, cr_ = O.jl_slot(None, P)
+    jc = SecaggCrypter()
+    xs = [W.party_params(p, n) for p in range(P)]
+    cts = torch.stack([jc.encrypt_tensor(P, tau, torch.from_numpy(xs[p]).to(dev), keys[p], W.BIPRIME0, weight=ws[p])
+                       for p in range(P)])
+    n_ct = (n + cr_ - 1) // cr_
+    assert tuple(cts.shape) == (P, n_ct, 64)
+    # sampled ciphertexts (first, last/partial, random) bit-exact vs the oracle
+    rng = np.random.default_rng(2)
+    ks = sorted({0, n_ct - 1, *rng.choice(n_ct, 24, replace=False).tolist()})
+    for p in range(P):
+        qw = [int(v) for v in _qw(xs[p], ws[p])]
+        got = D.limbs_to_ints(cts[p, ks].cpu().numpy())
+        for k, g in zip(ks, got):
+            ref = O.jl_encrypt_ints(qw[k * cr_:(k + 1) * cr_], tau, keys[p], W.BIPRIME0, P, k0=k)[0]
+            assert g == ref, (p, k)
+    # aggregate: the decoded integer sums are exactly sum_p q_p w_p for every element
+    out, sums = jc.aggregate_tensor(tau, cts, -sum(keys), W.BIPRIME0, sum(ws), num_expected_params=n,
+                                    want_sums=True)
+    sums = sums.cpu().numpy().view(np.uint64).reshape(n, 2)
+    want = np.zeros(n, dtype=np.uint64)
+    for p in range(P):
+        want += _qw(xs[p], ws[p])
+    assert (sums[:, 1] == 0).all() and np.array_equal(sums[:, 0], want)
+    ref = O.reverse_quantize(O.apply_average([int(v) for v in want], sum(ws)))
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), ref.view(np.uint64))
+
+
+def test_cfg3_lom_mnist_round_4_nodes(dev):
+    from fedbiomed_amd.secagg import SecaggLomCrypter
+
+    n, P, tau = 1_199_882, 4, 3
+    ids, ws = W.node_ids(P), [W.party_weight(p) for p in range(P)]
+    nonce = O.lom_nonce(W.LOM_NONCE)
+    cr = SecaggLomCrypter(W.LOM_NONCE)
+    xs = [W.party_params(p, n) for p in range(P)]
+    Y = torch.stack([cr.encrypt_tensor(tau, u, torch.from_numpy(xs[p]).to(dev), W.pairwise_secrets_for(u, ids), ids,
+                                       weight=ws[p]) for p, u in enumerate(ids)])
+    ref = O.lom_encrypt(xs[1].astype(np.float64), tau, ids[1], W.pairwise_secrets_for(ids[1], ids), ids, nonce,
+                        weight=ws[1])
+    assert np.array_equal(_u64(Y[1]), ref)
+    out, sums = cr.aggregate_tensor(Y, sum(ws), want_sums=True)
+    want = np.zeros(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        for p in range(P):
+            want += _qw(xs[p], ws[p])
+    assert np.array_equal(_u64(sums), want)
+    idx = np.random.default_rng(3).choice(n, 5000, replace=False)
+    refo = O.reverse_quantize(O.apply_average([int(v) for v in want[idx]], sum(ws)))
+    assert np.array_equal(out.cpu().numpy()[idx].view(np.uint64), refo.view(np.uint64))
+
+
+def test_cfg5_lom_ass_100m_16_parties(dev):
+    from fedbiomed_amd.secagg import AdditiveSecret, AdditiveShares, SecaggLomCrypter
+
+    n, P, tau = 100_000_000, 16, 1
+    ids, ws = W.node_ids(P), [W.party_weight(p) for p in range(P)]
+    nonce = O.lom_nonce(W.LOM_NONCE)
+    cr = SecaggLomCrypter(W.LOM_NONCE)
+    gen = torch.Generator(device=dev)
+    Y = torch.empty((P, n), dtype=torch.int64, device=dev)
+    qsum = torch.zeros(n, dtype=torch.int64, device=dev)
+    x1 = None
+    for p, u in enumerate(ids):
+        gen.manual_seed(500 + p)
+        x = torch.randn(n, generator=gen, device=dev, dtype=torch.float32) * 0.05
+        x[:: 997] = 4.0 * (1 - 2 * (p & 1))  # clipped entries
+        Y[p] = cr.encrypt_tensor(tau, u, x, W.pairwise_secrets_for(u, ids), ids, weight=ws[p])
+        qsum += D.lom_protect(x, [], [], b"\0" * 16, 0, 0, weight=ws[p])  # q*w, no masks
+        if p == 5:
+            x1 = x
+    # masks cancel exactly over all 100M elements (u64 wrap == int64 wrap)
+    out, sums = cr.aggregate_tensor(Y, sum(ws), want_sums=True)
+    assert torch.equal(sums, qsum)
+    # party 5 bit-exact on windows at the start, an interior, the end (ChaCha counter-indexed)
+    for off, m in ((0, 4096), (57_345_672, 4096), (n - 1000, 1000)):
+        xw = x1[off:off + m].cpu().numpy()
+        ref = _lom_window_oracle(ids[5], ids, tau, _qw(xw, ws[5]), off, nonce)
+        assert np.array_equal(_u64(Y[5, off:off + m]), ref), off
+    idx = np.random.default_rng(5).choice(n, 3000, replace=False)
+    s_np = _u64(sums)[idx]
+    refo = O.reverse_quantize(O.apply_average([int(v) for v in s_np], sum(ws)))
+    assert np.array_equal(out.cpu().numpy()[idx].view(np.uint64), refo.view(np.uint64))
+    del Y, out
+    # additive secret sharing of the 100M summed vector into 16 shares, and back (exact)
+    shares = AdditiveSecret.split_tensor(sums, P, unsigned=True)
+    rec = AdditiveShares.reconstruct_tensor(shares)
+    assert torch.equal(rec[:, 0], sums) and bool((rec[:, 1] == 0).all())
+    hi = shares[:-1, :, 1]
+    assert bool(((hi == 0) | (hi == 1)).all())  # first P-1 shares in [0, 2^64]
