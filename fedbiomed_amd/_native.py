@@ -46,6 +46,7 @@ c_vp = ctypes.c_void_p
 # name -> (restype, argtypes); must match include/fbm_secagg.h exactly
 SIGNATURES = {
     "fbm_abi_version": (c_int, []),
+    "fbm_jl_window": (c_int, []),
     "fbm_last_error": (ctypes.c_char_p, []),
     "fbm_check_stats": (c_int, [c_vp, c_int, c_vp]),
     "fbm_lom_protect": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_vp, c_vp, c_int, c_int,

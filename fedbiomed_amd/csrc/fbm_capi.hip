@@ -199,21 +199,21 @@ static int build_schedule(const uint32_t* key, JlSched& sc, int& is_zero) {
       first = false;
     } else {
       int nsq = pending_sq + width;
-      while (nsq > 2047) {
+      while (nsq > FBM_OP_MAXSQ) {
         if (sc.n_ops >= FBM_MAX_OPS) return FBM_E_ARG;
-        sc.op[sc.n_ops++] = (uint16_t)(2047 << 5);
-        nsq -= 2047;
+        sc.op[sc.n_ops++] = (uint16_t)(FBM_OP_MAXSQ << FBM_OP_SHIFT);
+        nsq -= FBM_OP_MAXSQ;
       }
       if (sc.n_ops >= FBM_MAX_OPS) return FBM_E_ARG;
-      sc.op[sc.n_ops++] = (uint16_t)((nsq << 5) | (idx + 1));
+      sc.op[sc.n_ops++] = (uint16_t)((nsq << FBM_OP_SHIFT) | (idx + 1));
     }
     pending_sq = 0;
     i = l - 1;
   }
   while (pending_sq > 0) {
-    const int nsq = pending_sq > 2047 ? 2047 : pending_sq;
+    const int nsq = pending_sq > FBM_OP_MAXSQ ? FBM_OP_MAXSQ : pending_sq;
     if (sc.n_ops >= FBM_MAX_OPS) return FBM_E_ARG;
-    sc.op[sc.n_ops++] = (uint16_t)(nsq << 5);
+    sc.op[sc.n_ops++] = (uint16_t)(nsq << FBM_OP_SHIFT);
     pending_sq -= nsq;
   }
   return FBM_OK;
@@ -278,6 +278,8 @@ using namespace fbm;
 extern "C" {
 
 int fbm_abi_version(void) { return FBM_ABI_VERSION; }
+
+int fbm_jl_window(void) { return FBM_WIN; }
 
 const char* fbm_last_error(void) { return g_err; }
 

@@ -50,8 +50,12 @@ int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t 
 
 // ---- Joye-Libert -------------------------------------------------------------------
 // exponent schedule (host-computed sliding window, uniform across lanes)
-#define FBM_WIN 5
-#define FBM_TABLE (1 << (FBM_WIN - 1))  // odd powers h^1, h^3, ..., h^31
+#ifndef FBM_WIN
+#define FBM_WIN 6  // A/B on MI355X: +1.7 % over 5 (325 vs 354 general products per ciphertext)
+#endif
+#define FBM_TABLE (1 << (FBM_WIN - 1))  // odd powers h^1, h^3, ..., h^(2^FBM_WIN - 1)
+#define FBM_OP_SHIFT 6                  // op = nsq << 6 | (table index + 1); windows up to 6 bits
+#define FBM_OP_MAXSQ 1023
 #define FBM_MAX_OPS 512
 #define FBM_TENTRIES (FBM_TABLE + 1)    // + one scratch column (h, then h^2)
 #define FBM_TSCRATCH FBM_TABLE
@@ -66,7 +70,7 @@ int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t 
 #define FBM_CST_WORDS (256 + 2 * FBM_NL * 256)
 
 // sliding-window schedule, passed by value (kernarg segment -> scalar loads).
-// op k (u16): (squarings before the multiply) << 5 | (table index + 1, 0 = none)
+// op k (u16): (squarings before the multiply) << FBM_OP_SHIFT | (table index + 1, 0 = none)
 struct JlSched {
   int n_ops;
   int first;       // table index of the leading window

@@ -362,8 +362,9 @@ __device__ __forceinline__ void glb_to_lds(const uint32_t* g, uint32_t* lds) {
 
 // mode 0 (ENC): out[ct] = nude[ct] * H[ct]^key  mod N^2          (ciphertext)
 // mode 1 (DEC): out[ct] = H[ct]^key mod N^2 (plain)                (for the inverse)
-// Sliding window (width FBM_WIN, 16 odd powers) over the device copy of the host-built
-// schedule; squarings use the dedicated assembly square (fbm_sq_lds).  Per-lane table: 17 blocked columns (entry 16 = h / h^2 scratch).
+// Sliding window (width FBM_WIN, FBM_TABLE odd powers) over the device copy of the host-built
+// schedule; squarings use the dedicated assembly square (fbm_sq_lds).  Per-lane table:
+// FBM_TENTRIES blocked columns (the last = h / h^2 scratch).
 //   a = R^2 (uniform), b = h         -> h*R              -> table[0]
 //   a = h*R,  b = a                  -> h^2*R            -> table[16]
 //   a = h^(2t-1)*R, b = table[16]    -> h^(2t+1)*R       -> table[t], t = 1..15
@@ -429,8 +430,8 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
 #pragma unroll 1
       for (int k = 0; k < n_ops; ++k) {
         const uint32_t op = __builtin_amdgcn_readfirstlane(ops[k]);
-        const int nsq = (int)(op >> 5);
-        const int idx = (int)(op & 31u) - 1;
+        const int nsq = (int)(op >> FBM_OP_SHIFT);
+        const int idx = (int)(op & ((1u << FBM_OP_SHIFT) - 1u)) - 1;
 #pragma unroll 1
         for (int q = 0; q < nsq; ++q) fbm_sq_lds(aoff, M, mp);
         if (idx >= 0) fbm_mm_glb(aoff, table, tb0 + (uint32_t)idx * tstride, M, mp);

@@ -165,6 +165,10 @@ int fbm_ass_split_wide(const uint32_t* secret, uint64_t n, int l_in, int n_share
                        void* stream);
 int fbm_ass_reconstruct_wide(const uint32_t* shares, int n_shares, int l, uint64_t n, uint32_t* out, void* stream);
 
+/* Sliding-window width of the JL exponentiation (odd-power table of 2^(w-1) entries); lets the
+ * bench count the products one ciphertext costs (its VALU roofline). */
+int fbm_jl_window(void);
+
 /* ---- host test hook (no GPU): the device modular-inverse routine (Bernstein-Yang divsteps,
  * fedbiomed_amd/csrc/fbm_safegcd.hpp) run on the host, for unit tests.
  * x, n, out: 32 little-endian words (n odd);  batches: number of 30-divstep batches used. */
