@@ -155,6 +155,33 @@ static int build_jl_params(const uint32_t* biprime, int es, int cr, uint64_t tau
   build_mont<FBM_NL>(M, jp.mc);
   build_mont<FBM_NLN>(N, jp.mn);
   for (int i = 0; i < 32; ++i) jp.N32[i] = biprime[i];
+  {  // N^-1 mod 2^1024 by Newton: y <- y (2 - N y); y = N is correct to 3 bits for odd N
+    uint32_t y[32], t[32];
+    for (int i = 0; i < 32; ++i) y[i] = biprime[i];
+    auto mullo = [](const uint32_t* a, const uint32_t* b, uint32_t* r) {  // r = a*b mod 2^1024
+      uint32_t acc[32] = {0};
+      for (int i = 0; i < 32; ++i) {
+        uint64_t c = 0;
+        for (int j = 0; i + j < 32; ++j) {
+          const uint64_t v = (uint64_t)a[i] * b[j] + acc[i + j] + c;
+          acc[i + j] = (uint32_t)v;
+          c = v >> 32;
+        }
+      }
+      memcpy(r, acc, sizeof(acc));
+    };
+    for (int it = 0; it < 9; ++it) {  // 3 -> 6 -> ... -> 1536 bits
+      mullo(biprime, y, t);           // t = N y
+      uint64_t br = 0;                // t = 2 - t  (mod 2^1024)
+      for (int i = 0; i < 32; ++i) {
+        const uint64_t d = (uint64_t)(i == 0 ? 2u : 0u) - t[i] - br;
+        t[i] = (uint32_t)d;
+        br = (d >> 63) & 1u;
+      }
+      mullo(y, t, y);
+    }
+    memcpy(jp.Ninv32, y, sizeof(y));
+  }
   jp.n_bits = nb;
   fbm_n30_setup(jp.N32, jp.n30);
   jp.es = es;

@@ -81,6 +81,7 @@ struct JlParams {
   MontCtx mc;                    // modulus M = N^2 (74 limbs)
   MontCtxN mn;                   // modulus N (37 limbs) -- inverse mod N, N*pt
   uint32_t N32[32];              // N, 32-bit limbs (<= 1024 bits)
+  uint32_t Ninv32[32];           // N^-1 mod 2^1024 (exact division (v-1)/N in jl_fin_kernel)
   int n_bits;                    // bit length of N
   int es, cr;                    // VES slot size / slots per ciphertext
   uint64_t tau;

@@ -714,6 +714,47 @@ __global__ void __launch_bounds__(FBM_BLOCK, 1) jl_fin_kernel(uint64_t n_ct, JlP
       br = (uint32_t)(d >> 63);
     }
   }
+  // (v-1)/N is exact whenever the keys are consistent (v = 1 + N x mod N^2): x = (v-1) N^-1
+  // mod 2^1024, accepted iff x N == v - 1.  Otherwise (a wrong server key: the reference
+  // still returns floor((v-1)/N) mod N) fall back to binary long division.
+  {
+    uint32_t x[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) x[i] = 0u;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      uint64_t c = 0;
+#pragma unroll
+      for (int j = 0; i + j < 32; ++j) {
+        const uint64_t v = (uint64_t)D[i] * jp.Ninv32[j] + x[i + j] + c;
+        x[i + j] = (uint32_t)v;
+        c = v >> 32;
+      }
+    }
+    uint32_t diff = 0;  // x*N (2048 bits) vs D
+    uint32_t pr[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) pr[i] = 0u;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      uint64_t c = 0;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        const uint64_t v = (uint64_t)x[i] * jp.N32[j] + pr[i + j] + c;
+        pr[i + j] = (uint32_t)v;
+        c = v >> 32;
+      }
+      pr[i + 32] = (uint32_t)c;
+    }
+#pragma unroll
+    for (int i = 0; i < 64; ++i) diff |= pr[i] ^ D[i];
+    if (diff == 0) {
+      uint4* o = reinterpret_cast<uint4*>(xout + ct * 32);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = make_uint4(x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]);
+      return;
+    }
+  }
   // binary long division by N; quotient q (< N), remainder r
   uint32_t q[32], r[33];
 #pragma unroll
