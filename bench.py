@@ -296,7 +296,57 @@ def main():
         cl = [jc.encrypt(P, tau, xl[p], keys[p], W.BIPRIME0, weight=weights[p]) for p in range(P)]
         jc.aggregate(tau, P, cl, sk0, W.BIPRIME0, total_w, num_expected_params=nl)
         tl = time.perf_counter() - t0
+        # (c) over the wire: the same updates through a msgpack Serializer configured as the
+        #     reference's (strict_types, one {"__type__": "int"} map per big int) vs the
+        #     EncryptedParams hook (one bin per update), encrypt -> dumps -> loads -> aggregate
+        import math
+
+        import msgpack
+
+        from fedbiomed_amd import wire
+
+        def ref_default(o):
+            w = wire.to_wire(o)
+            if w is not None:
+                return w
+            if isinstance(o, int):
+                return {"__type__": "int", "value": o.to_bytes(math.ceil(o.bit_length() / 8) + 1, "big", signed=True)}
+            raise TypeError(type(o))
+
+        def ref_hook(o):
+            o = wire.from_wire(o)
+            if isinstance(o, dict) and o.get("__type__") == "int":
+                return int.from_bytes(o["value"], "big", signed=True)
+            return o
+
+        def over_wire(updates):
+            blobs = [msgpack.packb({"params": u}, default=ref_default, strict_types=True) for u in updates]
+            recv = [msgpack.unpackb(b, object_hook=ref_hook, strict_map_key=False)["params"] for b in blobs]
+            return recv, sum(len(b) for b in blobs)
+
+        t0 = time.perf_counter()
+        recv, ref_bytes = over_wire(cl)
+        t_ref_ser = time.perf_counter() - t0
+        wire.enable()
+        try:
+            t0 = time.perf_counter()
+            cw = [jc.encrypt(P, tau, xl[p], keys[p], W.BIPRIME0, weight=weights[p]) for p in range(P)]
+            recv, wire_bytes = over_wire(cw)
+            jc.aggregate(tau, P, recv, sk0, W.BIPRIME0, total_w, num_expected_params=nl)
+            tw = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            over_wire(cw)
+            t_wire_ser = time.perf_counter() - t0
+        finally:
+            wire.enable(False)
         line["end_to_end"] = {
+            "wire": {"elements": nl, "parties": P,
+                     "reference_encoding": {"bytes": ref_bytes, "dumps_loads_ms": 1000 * t_ref_ser,
+                                            "list_api_plus_wire_params_per_s": nl / (tl + t_ref_ser)},
+                     "encrypted_params_blob": {"bytes": wire_bytes, "dumps_loads_ms": 1000 * t_wire_ser,
+                                               "list_api_plus_wire_params_per_s": nl / tw},
+                     "note": "P updates through msgpack (reference Serializer rules) and back, then aggregate; "
+                             "blob = fedbiomed_amd.wire hook (SURVEY 8(f)2)"},
             "pinned_host_tensors": {"value": n / te, "unit": "params/s", "ms_per_step": 1000 * te,
                                     "elements": n, "note": "H2D + encrypt x P + D2H + H2D + aggregate + D2H, "
                                                            "one stream"},

@@ -19,9 +19,10 @@ import secrets
 import time
 from typing import Dict, List, Optional, Union
 
+import numpy as np
 import torch
 
-from .. import _device as D
+from .. import _device as D, wire
 from ..constants import ErrorNumbers, SAParameters
 from ..exceptions import FedbiomedSecaggCrypterError
 
@@ -113,7 +114,10 @@ class SecaggCrypter:
             return []
         x = D.floats_to_device(params)
         ct = self.encrypt_tensor(num_nodes, current_round, x, key, biprime, clipping_range, weight, target_range)
-        out = D.limbs_to_ints(ct.cpu().numpy())
+        packed = ct.cpu().numpy().view(np.uint32)
+        out = D.limbs_to_ints(packed)
+        if wire.enabled():
+            out = wire.EncryptedParams(out, "jl", packed)
         logger.debug(f"Encryption of the parameters took {time.process_time() - start} seconds.")
         return out
 
@@ -139,9 +143,9 @@ class SecaggCrypter:
         n_ct = min(len(p) for p in params)  # zip(*list_y_u_tau) truncates (_jls.py:691-693)
         if n_ct == 0:
             return []
-        import numpy as np
-
-        limbs = np.stack([D.ints_to_limbs(p[:n_ct], n2) for p in params])
+        limbs = wire.packed_rows(params, "jl", n_ct)
+        if limbs is None:
+            limbs = np.stack([D.ints_to_limbs(p[:n_ct], n2) for p in params])
         dev = D.device()
         cts = torch.from_numpy(limbs.view(np.int32)).to(dev)
         out = self.aggregate_tensor(current_round, cts, key, biprime, total_sample_size, clipping_range,
@@ -223,7 +227,10 @@ class SecaggLomCrypter(SecaggCrypter):
         x = D.floats_to_device(params)
         y = self.encrypt_tensor(current_round, node_id, x, pairwise_secrets, node_ids, clipping_range, weight,
                                 target_range)
-        out = D.u64_from_device(y)
+        packed = y.cpu().numpy().view(np.uint64)
+        out = packed.tolist()
+        if wire.enabled():
+            out = wire.EncryptedParams(out, "lom", packed)
         logger.debug(f"Encryption of the parameters took {time.process_time() - start} seconds.")
         return out
 
@@ -232,8 +239,10 @@ class SecaggLomCrypter(SecaggCrypter):
         start = time.process_time()
         _check_int_lists(params)
         num_nodes = len(params)
+        packed = wire.packed_rows(params, "lom")
         try:
-            Y = D.u64_to_device(params)
+            Y = (torch.from_numpy(packed.view(np.int64)).to(D.device()) if packed is not None
+                 else D.u64_to_device(params))
         except (ValueError, TypeError) as e:
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value}: The aggregation of encrypted parameters "
