@@ -31,6 +31,10 @@ __device__ __forceinline__ uint64_t lom_input<uint64_t>(const uint64_t* x, uint6
   return x ? x[i] : 0ull;
 }
 
+#ifndef FBM_LOM_WG_PER_CU
+#define FBM_LOM_WG_PER_CU 10  // A/B on MI355X: 0.365 -> 0.30 ms per 10M x 7-peer protect (0 = one work-item per block)
+#endif
+
 template <typename XT>
 __global__ void __launch_bounds__(256) lom_protect_kernel(const XT* __restrict__ x, uint64_t n, QuantParams qp,
                                                           uint64_t weight, LomPeers peers,
@@ -52,65 +56,68 @@ __global__ void __launch_bounds__(256) lom_protect_kernel(const XT* __restrict__
   }
   __syncthreads();
 
-  const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + tid;
-  const uint64_t base = blk * 8;
-  const int cnt = base >= n ? 0 : ((n - base) >= 8 ? 8 : (int)(n - base));
+  const uint64_t nblk = (n + 7) / 8;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   bool clipped = false;
-
-  // quantise + weight
-  uint64_t val[8];
   uint32_t maxbits = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    uint64_t q = 0;
-    if (j < cnt) q = lom_input<XT>(x, base + j, qp, clipped);
-    const uint64_t lo = q * weight;
-    const uint64_t hi = __umul64hi(q, weight);
-    val[j] = lo;
-    const uint32_t bl = fbm_bitlen128(hi, lo);
-    maxbits = bl > maxbits ? bl : maxbits;
-  }
+  // grid-stride over ChaCha20 blocks (a grid of FBM_LOM_WG_PER_CU workgroups per CU keeps
+  // every wave resident for the whole launch: no ramp, no partial last round)
+  for (uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + tid; blk < nblk; blk += stride) {
+    const uint64_t base = blk * 8;
+    const int cnt = (n - base) >= 8 ? 8 : (int)(n - base);
 
-  flag_if_any(clipped, stats, FBM_WARN_CLIPPED);
-  if (cnt == 0) return;
-
-  // masks
-  uint64_t mask[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) mask[j] = 0;
-  const uint64_t ctr = peers.ctr0 + (peers.elem_offset >> 3) + blk;  // global ChaCha20 block
-  for (int p = 0; p < peers.n_peers; ++p) {
-    uint32_t key[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) key[w] = seeds[p][w];
-    uint32_t ks[16];
-    fbm_chacha20_block(key, ctr, peers.n14, peers.n15, ks);
-    const bool add = peers.sign[p] > 0;
+    // quantise + weight
+    uint64_t val[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const uint64_t idx = peers.elem_offset + base + (uint64_t)j + peers.tau;
-      const uint64_t m = (((uint64_t)ks[2 * j + 1] << 32) | ks[2 * j]) ^ fbm_bswap64(idx);
-      mask[j] = add ? mask[j] + m : mask[j] - m;
+      uint64_t q = 0;
+      if (j < cnt) q = lom_input<XT>(x, base + j, qp, clipped);
+      const uint64_t lo = q * weight;
+      const uint64_t hi = __umul64hi(q, weight);
+      val[j] = lo;
+      const uint32_t bl = fbm_bitlen128(hi, lo);
+      maxbits = bl > maxbits ? bl : maxbits;
+    }
+
+    // masks
+    uint64_t mask[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mask[j] = 0;
+    const uint64_t ctr = peers.ctr0 + (peers.elem_offset >> 3) + blk;  // global ChaCha20 block
+    for (int p = 0; p < peers.n_peers; ++p) {
+      uint32_t key[8];
+#pragma unroll
+      for (int w = 0; w < 8; ++w) key[w] = seeds[p][w];
+      uint32_t ks[16];
+      fbm_chacha20_block(key, ctr, peers.n14, peers.n15, ks);
+      const bool add = peers.sign[p] > 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint64_t idx = peers.elem_offset + base + (uint64_t)j + peers.tau;
+        const uint64_t m = (((uint64_t)ks[2 * j + 1] << 32) | ks[2 * j]) ^ fbm_bswap64(idx);
+        mask[j] = add ? mask[j] + m : mask[j] - m;
+      }
+    }
+
+    if (cnt == 8) {
+      ulonglong2* yo = reinterpret_cast<ulonglong2*>(y + base);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) yo[j] = make_ulonglong2(mask[2 * j] + val[2 * j], mask[2 * j + 1] + val[2 * j + 1]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j < cnt) y[base + j] = mask[j] + val[j];
     }
   }
 
-  if (cnt == 8) {
-    ulonglong2* yo = reinterpret_cast<ulonglong2*>(y + base);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) yo[j] = make_ulonglong2(mask[2 * j] + val[2 * j], mask[2 * j + 1] + val[2 * j + 1]);
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (j < cnt) y[base + j] = mask[j] + val[j];
-  }
-
+  flag_if_any(clipped, stats, FBM_WARN_CLIPPED);
   // wave-level max of the bit lengths, one atomic per wave
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const uint32_t o = __shfl_xor(maxbits, off, 64);
     maxbits = o > maxbits ? o : maxbits;
   }
-  if ((tid & 63) == 0) atomicMax(stats + FBM_STAT_MAXBITS, maxbits);
+  if ((tid & 63) == 0 && maxbits) atomicMax(stats + FBM_STAT_MAXBITS, maxbits);
 }
 
 // Column sum over P parties (mod 2^64) + Python-exact average + dequantise.
@@ -201,7 +208,9 @@ int launch_lom_protect(const void* x, int x_dtype, uint64_t n, const QuantParams
                        const LomPeers& peers, uint64_t* y, uint32_t* stats, hipStream_t s) {
   if (n == 0) return FBM_OK;
   const uint64_t nblk = (n + 7) / 8;
-  const dim3 grid((unsigned)((nblk + 255) / 256)), block(256);
+  uint64_t g = (nblk + 255) / 256;
+  if (FBM_LOM_WG_PER_CU > 0 && g > 256ull * FBM_LOM_WG_PER_CU) g = 256ull * FBM_LOM_WG_PER_CU;
+  const dim3 grid((unsigned)g), block(256);
   if (x_dtype == FBM_F32)
     hipLaunchKernelGGL(lom_protect_kernel<float>, grid, block, 0, s, (const float*)x, n, qp, weight, peers, y, stats);
   else if (x_dtype == FBM_F64)
