@@ -380,7 +380,7 @@ int fbm_lom_protect(const void* x, int x_dtype, uint64_t n, double clip, double 
   pe.elem_offset = elem_offset;
   for (int p = 0; p < n_peers; ++p) {
     memcpy(pe.secret[p], secrets + 32 * p, 32);
-    pe.sign[p] = signs[p] >= 0 ? 1 : -1;
+    if (signs[p] >= 0) pe.add_bits |= 1ull << p;
   }
   return timed("lom_protect", s, [&] { return launch_lom_protect(x, x_dtype, n, qp, weight, pe, y, stats, s); });
 }

@@ -35,7 +35,7 @@ struct LomPeers {
   uint64_t elem_offset;          // global index of x[0] (element-range shard; multiple of 8)
   uint32_t tau_be[4];            // tau.to_bytes(16, 'big') as LE words
   uint32_t secret[FBM_MAX_PEERS][8];
-  int8_t sign[FBM_MAX_PEERS];    // +1: mask += vec (peer < node), -1: mask -= vec
+  uint64_t add_bits;             // bit p set: mask += vec (peer < node), clear: mask -= vec
 };
 
 int check_launch(const char* what);

@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(256) lom_protect_kernel(const XT* __restrict__
       for (int w = 0; w < 8; ++w) key[w] = seeds[p][w];
       uint32_t ks[16];
       fbm_chacha20_block(key, ctr, peers.n14, peers.n15, ks);
-      const bool add = peers.sign[p] > 0;
+      const bool add = (peers.add_bits >> p) & 1ull;  // scalar: no per-peer memory load
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const uint64_t idx = peers.elem_offset + base + (uint64_t)j + peers.tau;
