@@ -418,11 +418,12 @@ int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t tot
   return timed("lom_aggregate", s, [&] { return launch_lom_aggregate(y, n_parties, n, total_weight, neg_clip, step, out, sums, stats, s); });
 }
 
-// encrypt workspace: ops | pt [n_ct][32] | nude (blocked) | H [n_ct][64] | table
+// encrypt workspace: ops | cst | pt [n_ct][32] | nude (blocked) | H [n_ct][64] |
+//                    H^-1 [n_ct][64] + y [n_ct][32] (negative keys) | table
 uint64_t fbm_jl_encrypt_workspace(uint64_t n_ct) {
   const uint64_t slots = table_slots_for(n_ct);
   return align256(FBM_MAX_OPS * 4) + align256(FBM_CST_WORDS * 4) + align256(n_ct * 32 * 4) +
-         align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4) + align256(n_ct * 64 * 4) +
+         align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4) + 2 * align256(n_ct * 64 * 4) + align256(n_ct * 32 * 4) +
          align256(slots * FBM_TENTRIES * FBM_NL * 4);
 }
 
@@ -448,10 +449,6 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
   if (!biprime || !key) {
     set_error("null biprime/key");
     return FBM_E_ARG;
-  }
-  if (key_negative) {
-    set_error("negative user keys are not supported by the device encrypt path");
-    return FBM_E_UNSUPPORTED;
   }
   if (n == 0) return FBM_OK;
   if (cr < 1) {
@@ -489,12 +486,23 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
   off += align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4);
   uint32_t* H = (uint32_t*)(ws + off);
   off += align256(n_ct * 64 * 4);
+  uint32_t* Hinv = (uint32_t*)(ws + off);
+  off += align256(n_ct * 64 * 4);
+  uint32_t* Y = (uint32_t*)(ws + off);
+  off += align256(n_ct * 32 * 4);
   uint32_t* table = (uint32_t*)(ws + off);
   if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s); }))) return rc;
   if ((rc = timed("jl_pack", s, [&] { return launch_jl_pack(x, x_dtype, n, qp, weight, es, cr, n_ct, pt, stats, s); }))) return rc;
   if ((rc = timed("jl_nude", s, [&] { return launch_jl_nude(pt, n_ct, jp, nude, s); }))) return rc;
   if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, H, stats, s); }))) return rc;
-  return timed("jl_exp", s, [&] { return launch_jl_exp(H, n_ct, jp, sc, 0, nude, table, slots, ops, cst, ct_out, s); });
+  const uint32_t* base = H;
+  if (key_negative && !is_zero) {
+    // gmpy2.powmod with a negative exponent (_jls.py:60-73): invert H(t_k) mod N^2 first,
+    // then raise the inverse to |key|
+    if ((rc = timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, H, Y, Hinv, stats, s); }))) return rc;
+    base = Hinv;
+  }
+  return timed("jl_exp", s, [&] { return launch_jl_exp(base, n_ct, jp, sc, 0, nude, table, slots, ops, cst, ct_out, s); });
 }
 
 int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,

@@ -258,6 +258,28 @@ def test_jl_crypter_golden(golden, dev, idx):
         assert [int(a) | (int(b) << 64) for a, b in s] == [I(v) for v in exp]
 
 
+def test_jl_negative_user_keys(dev):
+    """gmpy2.powmod with a negative exponent inverts first (_jls.py:60-73): user keys of
+    either sign, ciphertexts bit-exact vs the oracle, and the round trip through the
+    matching server key."""
+    from fedbiomed_amd import workload as W
+    from fedbiomed_amd.secagg import SecaggCrypter
+    from oracle import secagg_oracle as O
+
+    P, n, tau = 3, 150, 4
+    keys = [-W.jl_user_key(0), W.jl_user_key(1), -W.jl_user_key(2)]
+    ws = [W.party_weight(p) for p in range(P)]
+    xs = [W.party_params(p, n).astype(np.float64).tolist() for p in range(P)]
+    jc = SecaggCrypter()
+    cts = [jc.encrypt(P, tau, xs[p], keys[p], W.BIPRIME0, weight=ws[p]) for p in range(P)]
+    for p in (0, 1):
+        assert cts[p] == O.jl_encrypt(xs[p], tau, keys[p], W.BIPRIME0, P, weight=ws[p]), p
+    sk0 = -sum(keys)
+    out = jc.aggregate(tau, P, cts, sk0, W.BIPRIME0, sum(ws), num_expected_params=n)
+    ref = O.jl_crypter_aggregate(cts, tau, sk0, W.BIPRIME0, sum(ws), n)
+    assert _bits(out) == _bits(ref)
+
+
 def test_jl_edge_cases(dev):
     from fedbiomed_amd import workload as W
     from fedbiomed_amd.exceptions import FedbiomedSecaggCrypterError
