@@ -12,6 +12,7 @@ Python semantics stay bit-identical.
 from __future__ import annotations
 
 import ctypes
+import os
 import logging
 import math
 from typing import List, Optional, Sequence, Tuple
@@ -314,6 +315,15 @@ def _key_limbs(key: int) -> Tuple[np.ndarray, int]:
     return int_limbs(abs(key), 64), 1 if key < 0 else 0
 
 
+JL_MAX_CT = 14_000_000  # include/fbm_secagg.h FBM_JL_MAX_CT: ciphertexts per library call
+
+
+def jl_chunk_ct() -> int:
+    """Ciphertexts per library call (FBM_JL_CHUNK_CT lowers it, for tests of the striping)."""
+    v = int(os.environ.get("FBM_JL_CHUNK_CT", JL_MAX_CT))
+    return max(1, min(v, JL_MAX_CT))
+
+
 def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, clip=None, target=None,
                weight: int = 1, slot: Optional[Tuple[int, int]] = None, ct_offset: int = 0) -> torch.Tensor:
     """One party's JL ciphertexts as an int32 [n_ct, 64] tensor of 32-bit limbs.
@@ -334,11 +344,16 @@ def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, 
         return ct
     bp = _biprime_limbs(biprime)
     kl, kneg = _key_limbs(key)
-    ws = torch.empty(int(lib.fbm_jl_encrypt_workspace(n_ct)), dtype=torch.uint8, device=dev)
-    st = _stats(dev)
-    _call(lib.fbm_jl_encrypt, _ptr(x), _x_dtype(x), n, c, c2, tf, tm1, int(weight), es, cr, _np_ptr(bp),
-          _np_ptr(kl), kneg, int(tau), int(ct_offset), _ptr(ct), _ptr(ws), _ptr(st), _stream())
-    _check_stats_or_defer(st)
+    chunk = jl_chunk_ct()  # calls above the library's per-call cap run as ct_offset stripes
+    ws = torch.empty(int(lib.fbm_jl_encrypt_workspace(min(n_ct, chunk))), dtype=torch.uint8, device=dev)
+    for k0 in range(0, n_ct, chunk):
+        k1 = min(n_ct, k0 + chunk)
+        xs = x[k0 * cr:min(n, k1 * cr)]
+        st = _stats(dev)  # one status word per call (each call zeroes its own)
+        _call(lib.fbm_jl_encrypt, _ptr(xs), _x_dtype(x), xs.numel(), c, c2, tf, tm1, int(weight), es, cr,
+              _np_ptr(bp), _np_ptr(kl), kneg, int(tau), int(ct_offset) + k0, _ptr(ct[k0:k1]), _ptr(ws), _ptr(st),
+              _stream())
+        _check_stats_or_defer(st)
     return ct
 
 
@@ -366,12 +381,20 @@ def jl_aggregate(cts: torch.Tensor, biprime: int, key: int, tau: int, n_expected
         return out, sums
     bp = _biprime_limbs(biprime)
     kl, kneg = _key_limbs(key)
+    chunk = jl_chunk_ct()
     cts = cts.contiguous()
-    ws = torch.empty(int(lib.fbm_jl_aggregate_workspace(n_ct)), dtype=torch.uint8, device=dev)
-    st = _stats(dev)
-    _call(lib.fbm_jl_aggregate, _ptr(cts), P, n_ct, es, cr, n_out, _np_ptr(bp), _np_ptr(kl), kneg, int(tau),
-          int(ct_offset), int(total_weight), negc, step, _ptr(out), _ptr(sums), _ptr(ws), _ptr(st), _stream())
-    _check_stats(st)
+    ws = torch.empty(int(lib.fbm_jl_aggregate_workspace(min(n_ct, chunk))), dtype=torch.uint8, device=dev)
+    for k0 in range(0, n_ct, chunk):
+        k1 = min(n_ct, k0 + chunk)
+        part = cts[:, k0:k1].contiguous() if (k0, k1) != (0, n_ct) else cts
+        e0, e1 = k0 * cr, min(n_out, k1 * cr)
+        if e1 <= e0:
+            break
+        st = _stats(dev)
+        _call(lib.fbm_jl_aggregate, _ptr(part), P, k1 - k0, es, cr, e1 - e0, _np_ptr(bp), _np_ptr(kl), kneg,
+              int(tau), int(ct_offset) + k0, int(total_weight), negc, step, _ptr(out[e0:e1] if want_out else None),
+              _ptr(sums[e0:e1] if want_sums else None), _ptr(ws), _ptr(st), _stream())
+        _check_stats(st)
     return out, sums
 
 

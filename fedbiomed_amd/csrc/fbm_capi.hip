@@ -355,9 +355,9 @@ int fbm_lom_protect(const void* x, int x_dtype, uint64_t n, double clip, double 
     set_error("x_dtype must be FBM_F32, FBM_F64 or FBM_U64");
     return FBM_E_ARG;
   }
-  if (n_peers < 0 || n_peers > FBM_MAX_PEERS) {
-    set_error("n_peers=%d outside [0, %d]", n_peers, FBM_MAX_PEERS);
-    return FBM_E_UNSUPPORTED;
+  if (n_peers < 0) {
+    set_error("n_peers=%d < 0", n_peers);
+    return FBM_E_ARG;
   }
   if ((n > 0 && ((!x && x_dtype != FBM_U64) || !y)) || !nonce || (n_peers > 0 && (!secrets || !signs))) {
     set_error("null pointer argument");
@@ -373,16 +373,26 @@ int fbm_lom_protect(const void* x, int x_dtype, uint64_t n, double clip, double 
     set_error("Can not perform encryiton due to large input vector");
     return FBM_E_ARG;
   }
-  LomPeers pe;
-  fill_peers(pe, nonce, tau);
-  pe.n_peers = n_peers;
-  pe.raw_seeds = raw_seeds;
-  pe.elem_offset = elem_offset;
-  for (int p = 0; p < n_peers; ++p) {
-    memcpy(pe.secret[p], secrets + 32 * p, 32);
-    if (signs[p] >= 0) pe.add_bits |= 1ull << p;
+  // peers in groups of FBM_MAX_PEERS (the kernel-argument block): the first group with the
+  // quantise/weight/overflow statistics, later groups accumulated in place
+  for (int g0 = 0; g0 == 0 || g0 < n_peers; g0 += FBM_MAX_PEERS) {
+    const int gn = n_peers - g0 < FBM_MAX_PEERS ? n_peers - g0 : FBM_MAX_PEERS;
+    LomPeers pe;
+    fill_peers(pe, nonce, tau);
+    pe.n_peers = gn < 0 ? 0 : gn;
+    pe.raw_seeds = raw_seeds;
+    pe.elem_offset = elem_offset;
+    for (int p = 0; p < pe.n_peers; ++p) {
+      memcpy(pe.secret[p], secrets + 32 * (g0 + p), 32);
+      if (signs[g0 + p] >= 0) pe.add_bits |= 1ull << p;
+    }
+    if (g0 == 0)
+      rc = timed("lom_protect", s, [&] { return launch_lom_protect(x, x_dtype, n, qp, weight, pe, y, stats, s); });
+    else
+      rc = timed("lom_protect", s, [&] { return launch_lom_mask_accumulate(n, pe, y, s); });
+    if (rc) return rc;
   }
-  return timed("lom_protect", s, [&] { return launch_lom_protect(x, x_dtype, n, qp, weight, pe, y, stats, s); });
+  return FBM_OK;
 }
 
 int fbm_prf_key(const uint8_t* secret, const uint8_t* nonce, uint64_t tau, uint8_t* seed_out, void* stream) {

@@ -31,6 +31,23 @@ __device__ __forceinline__ uint64_t lom_input<uint64_t>(const uint64_t* x, uint6
   return x ? x[i] : 0ull;
 }
 
+// Per-round peer seeds into LDS, one peer per thread: PRF.eval_key (_lom.py:30-56) =
+// ChaCha20(secret, nonce) over tau.to_bytes(16,'big'), first 16 bytes of keystream XOR
+// tau_be16, padded with 16 zero bytes -- or the seeds themselves when the caller has them.
+__device__ __forceinline__ void lom_seeds_to_lds(const LomPeers& peers, uint32_t (*seeds)[8], int tid) {
+  if (tid < peers.n_peers && peers.raw_seeds) {
+#pragma unroll
+    for (int w = 0; w < 8; ++w) seeds[tid][w] = peers.secret[tid][w];
+  } else if (tid < peers.n_peers) {
+    uint32_t ks[16];
+    fbm_chacha20_block(peers.secret[tid], peers.ctr0, peers.n14, peers.n15, ks);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) seeds[tid][w] = ks[w] ^ peers.tau_be[w];
+#pragma unroll
+    for (int w = 4; w < 8; ++w) seeds[tid][w] = 0u;
+  }
+}
+
 #ifndef FBM_LOM_WG_PER_CU
 #define FBM_LOM_WG_PER_CU 10  // A/B on MI355X: 0.365 -> 0.30 ms per 10M x 7-peer protect (0 = one work-item per block)
 #endif
@@ -41,19 +58,7 @@ __global__ void __launch_bounds__(256) lom_protect_kernel(const XT* __restrict__
                                                           uint64_t* __restrict__ y, uint32_t* __restrict__ stats) {
   __shared__ uint32_t seeds[FBM_MAX_PEERS][8];
   const int tid = threadIdx.x;
-  if (tid < peers.n_peers && peers.raw_seeds) {
-#pragma unroll
-    for (int w = 0; w < 8; ++w) seeds[tid][w] = peers.secret[tid][w];
-  } else if (tid < peers.n_peers) {
-    // PRF.eval_key: ChaCha20(secret, nonce) over tau.to_bytes(16,'big'), first 16 bytes
-    // of keystream XOR tau_be16, padded with 16 zero bytes.
-    uint32_t ks[16];
-    fbm_chacha20_block(peers.secret[tid], peers.ctr0, peers.n14, peers.n15, ks);
-#pragma unroll
-    for (int w = 0; w < 4; ++w) seeds[tid][w] = ks[w] ^ peers.tau_be[w];
-#pragma unroll
-    for (int w = 4; w < 8; ++w) seeds[tid][w] = 0u;
-  }
+  lom_seeds_to_lds(peers, seeds, tid);
   __syncthreads();
 
   const uint64_t nblk = (n + 7) / 8;
@@ -118,6 +123,52 @@ __global__ void __launch_bounds__(256) lom_protect_kernel(const XT* __restrict__
     maxbits = o > maxbits ? o : maxbits;
   }
   if ((tid & 63) == 0 && maxbits) atomicMax(stats + FBM_STAT_MAXBITS, maxbits);
+}
+
+// y += signed masks of a further group of peers (nodes with more than FBM_MAX_PEERS peers:
+// the C-ABI runs lom_protect_kernel on the first group, then this kernel per later group).
+// In place, no quantisation, no statistics; seeds are already per-round (eval_key done).
+__global__ void __launch_bounds__(256) lom_mask_accumulate_kernel(uint64_t n, LomPeers peers, uint64_t* y) {
+  __shared__ uint32_t seeds[FBM_MAX_PEERS][8];
+  const int tid = threadIdx.x;
+  lom_seeds_to_lds(peers, seeds, tid);
+  __syncthreads();
+  const uint64_t nblk = (n + 7) / 8;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + tid; blk < nblk; blk += stride) {
+    const uint64_t base = blk * 8;
+    const int cnt = (n - base) >= 8 ? 8 : (int)(n - base);
+    uint64_t mask[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mask[j] = 0;
+    const uint64_t ctr = peers.ctr0 + (peers.elem_offset >> 3) + blk;
+    for (int p = 0; p < peers.n_peers; ++p) {
+      uint32_t key[8];
+#pragma unroll
+      for (int w = 0; w < 8; ++w) key[w] = seeds[p][w];
+      uint32_t ks[16];
+      fbm_chacha20_block(key, ctr, peers.n14, peers.n15, ks);
+      const bool add = (peers.add_bits >> p) & 1ull;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint64_t idx = peers.elem_offset + base + (uint64_t)j + peers.tau;
+        const uint64_t m = (((uint64_t)ks[2 * j + 1] << 32) | ks[2 * j]) ^ fbm_bswap64(idx);
+        mask[j] = add ? mask[j] + m : mask[j] - m;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j < cnt) y[base + j] += mask[j];
+  }
+}
+
+int launch_lom_mask_accumulate(uint64_t n, const LomPeers& peers, uint64_t* y, hipStream_t s) {
+  if (n == 0 || peers.n_peers == 0) return FBM_OK;
+  const uint64_t nblk = (n + 7) / 8;
+  uint64_t g = (nblk + 255) / 256;
+  if (g > 256ull * FBM_LOM_WG_PER_CU) g = 256ull * FBM_LOM_WG_PER_CU;
+  hipLaunchKernelGGL(lom_mask_accumulate_kernel, dim3((unsigned)g), dim3(256), 0, s, n, peers, y);
+  return check_launch("lom_mask_accumulate_kernel");
 }
 
 // Column sum over P parties (mod 2^64) + Python-exact average + dequantise.

@@ -280,6 +280,47 @@ def test_jl_negative_user_keys(dev):
     assert _bits(out) == _bits(ref)
 
 
+def test_jl_call_striping(dev, monkeypatch):
+    """Vectors above the library's per-call ciphertext cap run as ct_offset stripes; forced
+    here with a 7-ciphertext cap: identical ciphertexts and aggregate."""
+    from fedbiomed_amd import workload as W
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    P, n, tau = 3, 1000, 2
+    keys = [W.jl_user_key(p) for p in range(P)]
+    ws = [W.party_weight(p) for p in range(P)]
+    xs = [torch.from_numpy(W.party_params(p, n)).to(dev) for p in range(P)]
+    jc = SecaggCrypter()
+    whole = torch.stack([jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=ws[p]) for p in range(P)])
+    out_w = jc.aggregate_tensor(tau, whole, -sum(keys), W.BIPRIME0, sum(ws), num_expected_params=n - 5)
+    monkeypatch.setenv("FBM_JL_CHUNK_CT", "7")
+    striped = torch.stack([jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=ws[p]) for p in range(P)])
+    assert torch.equal(striped, whole)
+    out_s = jc.aggregate_tensor(tau, striped, -sum(keys), W.BIPRIME0, sum(ws), num_expected_params=n - 5)
+    assert torch.equal(out_s.view(torch.int64), out_w.view(torch.int64)) and out_s.numel() == n - 5
+
+
+def test_lom_more_than_64_peers(dev):
+    """Nodes with more peers than one kernel-argument block (64): later peer groups are
+    accumulated in place; bit-exact vs the oracle and masks cancel over 70 parties."""
+    from fedbiomed_amd import workload as W
+    from fedbiomed_amd.secagg import SecaggLomCrypter
+    from oracle import secagg_oracle as O
+
+    P, n, tau = 70, 203, 5
+    ids = W.node_ids(P)
+    ws = [1 + p for p in range(P)]
+    cr = SecaggLomCrypter(W.LOM_NONCE)
+    xs = [W.party_params(p, n).astype(np.float64).tolist() for p in range(P)]
+    ys = [cr.encrypt(tau, u, xs[p], W.pairwise_secrets_for(u, ids), ids, weight=ws[p]) for p, u in enumerate(ids)]
+    for p in (0, 37, 69):
+        ref = O.lom_encrypt(xs[p], tau, ids[p], W.pairwise_secrets_for(ids[p], ids), ids, O.lom_nonce(W.LOM_NONCE),
+                            weight=ws[p])
+        assert ys[p] == [int(v) for v in ref], p
+    out = cr.aggregate(ys, sum(ws))
+    assert _bits(out) == _bits(O.lom_crypter_aggregate(ys, sum(ws)))
+
+
 def test_jl_edge_cases(dev):
     from fedbiomed_amd import workload as W
     from fedbiomed_amd.exceptions import FedbiomedSecaggCrypterError
