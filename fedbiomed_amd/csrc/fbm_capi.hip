@@ -428,8 +428,8 @@ int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t tot
   return timed("lom_aggregate", s, [&] { return launch_lom_aggregate(y, n_parties, n, total_weight, neg_clip, step, out, sums, stats, s); });
 }
 
-// encrypt workspace: ops | cst | pt [n_ct][32] | nude (blocked) | H [n_ct][64] |
-//                    H^-1 [n_ct][64] + y [n_ct][32] (negative keys) | table
+// encrypt workspace: ops | cst | pt [n_ct][32] | nude (blocked) | H [n_ct][64] | table |
+//                    H^-1 [n_ct][64] + y [n_ct][32] (negative keys)
 uint64_t fbm_jl_encrypt_workspace(uint64_t n_ct) {
   const uint64_t slots = table_slots_for(n_ct);
   return align256(FBM_MAX_OPS * 4) + align256(FBM_CST_WORDS * 4) + align256(n_ct * 32 * 4) +
@@ -496,11 +496,11 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
   off += align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4);
   uint32_t* H = (uint32_t*)(ws + off);
   off += align256(n_ct * 64 * 4);
-  uint32_t* Hinv = (uint32_t*)(ws + off);
+  uint32_t* table = (uint32_t*)(ws + off);
+  off += align256(slots * FBM_TENTRIES * FBM_NL * 4);
+  uint32_t* Hinv = (uint32_t*)(ws + off);  // negative keys only (after the table: keeps its placement)
   off += align256(n_ct * 64 * 4);
   uint32_t* Y = (uint32_t*)(ws + off);
-  off += align256(n_ct * 32 * 4);
-  uint32_t* table = (uint32_t*)(ws + off);
   if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s); }))) return rc;
   if ((rc = timed("jl_pack", s, [&] { return launch_jl_pack(x, x_dtype, n, qp, weight, es, cr, n_ct, pt, stats, s); }))) return rc;
   if ((rc = timed("jl_nude", s, [&] { return launch_jl_nude(pt, n_ct, jp, nude, s); }))) return rc;
