@@ -96,8 +96,9 @@ class deferred_checks:
         pending = deferred_checks._active.pop()
         if exc_type is None and pending:
             torch.cuda.synchronize()  # the status words were written on other streams
-            for st, nodes in pending:
-                _check_stats(st, nodes)
+            host = torch.stack([st for st, _ in pending]).cpu().numpy()  # one copy for all of them
+            for (_, nodes), row in zip(pending, host):
+                _check_stats_host(row, nodes)
         return False
 
 
@@ -109,7 +110,11 @@ def _check_stats_or_defer(stats: torch.Tensor, lom_nodes: int = 0) -> None:
 
 
 def _check_stats(stats: torch.Tensor, lom_nodes: int = 0) -> int:
-    host = stats.cpu().numpy().astype(np.uint32)  # synchronises the stream
+    return _check_stats_host(stats.cpu().numpy(), lom_nodes)  # .cpu() synchronises the stream
+
+
+def _check_stats_host(host: np.ndarray, lom_nodes: int = 0) -> int:
+    host = np.ascontiguousarray(host).astype(np.uint32)
     if int(host[1]) & FBM_WARN_CLIPPED:  # _check_clipping_range (utils/_secagg_utils.py:189-204)
         logger.warning("There are some numbers in the local vector that exceeds clipping range. "
                        "Please increase the clipping range to account for value")
@@ -233,7 +238,7 @@ def _nonce_block(nonce: bytes) -> np.ndarray:
 
 def lom_protect(x: torch.Tensor, secrets: Sequence[bytes], signs: Sequence[int], nonce: bytes, tau: int,
                 n_nodes: int, clip=None, target=None, weight: int = 1, raw_seeds: bool = False,
-                elem_offset: int = 0) -> torch.Tensor:
+                elem_offset: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """One party's masked vector (u64 bit patterns in an int64 tensor); raises the
     reference's LOM overflow error when max(bit_length(q*w)) >= 64 - ceil(log2(n_nodes))."""
     dev = x.device
@@ -247,7 +252,12 @@ def lom_protect(x: torch.Tensor, secrets: Sequence[bytes], signs: Sequence[int],
     nb = _nonce_block(nonce)
     x = x.contiguous()
     n = x.numel()
-    y = torch.empty(n, dtype=torch.int64, device=dev)
+    if out is not None:  # caller-owned destination, e.g. row p of the aggregate's [P, n] matrix
+        if out.dtype != torch.int64 or out.numel() != n or not out.is_contiguous() or out.device != dev:
+            raise ValueError("out must be a contiguous int64 tensor of x.numel() elements on x's device")
+        y = out
+    else:
+        y = torch.empty(n, dtype=torch.int64, device=dev)
     st = _stats(dev)
     _call(lib.fbm_lom_protect, _ptr(x), _x_dtype(x), n, c, c2, tf, tm1, int(weight), _np_ptr(sec), _np_ptr(sg),
           len(secrets), 1 if raw_seeds else 0, _np_ptr(nb), int(tau), int(elem_offset), _ptr(y), _ptr(st),

@@ -189,9 +189,11 @@ class SecaggLomCrypter(SecaggCrypter):
     def encrypt_tensor(self, current_round: int, node_id: str, params: torch.Tensor,
                        pairwise_secrets: Dict[str, bytes], node_ids: List[str],
                        clipping_range: Union[int, None] = None, weight: Optional[int] = None,
-                       target_range: Optional[int] = None, elem_offset: int = 0) -> torch.Tensor:
+                       target_range: Optional[int] = None, elem_offset: int = 0,
+                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Device tensor (f32/f64) -> masked uint64 vector (int64 tensor) in HBM.
-        `elem_offset`: global index of this shard's first element (multiple of 8)."""
+        `elem_offset`: global index of this shard's first element (multiple of 8); `out`: an
+        int64 destination (e.g. this party's row of the [P, n] matrix aggregate_tensor takes)."""
         target_range = target_range or SAParameters.TARGET_RANGE
         _check_weight(weight, jl=False)
         if params.numel() == 0:
@@ -205,7 +207,7 @@ class SecaggLomCrypter(SecaggCrypter):
                 f"{ErrorNumbers.FB624.value} Error during parameter encryption. math domain error")
         return D.lom_protect(params, secrets_, signs, self._nonce, current_round, len(node_ids),
                              clip=clipping_range, target=target_range, weight=1 if weight is None else weight,
-                             elem_offset=elem_offset)
+                             elem_offset=elem_offset, out=out)
 
     def aggregate_tensor(self, Y: torch.Tensor, total_sample_size: int, clipping_range: Union[int, None] = None,
                          target_range: Optional[int] = None, want_sums: bool = False):
