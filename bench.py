@@ -104,6 +104,8 @@ def parse():
     ap.add_argument("--no-lom-extra", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-to-host (H2D/D2H-inclusive) legs")
     ap.add_argument("--e2e-list-n", type=int, default=1_000_000, help="elements for the list-API end-to-end leg")
+    ap.add_argument("--no-factor-overlap", action="store_true",
+                    help="JL: compute the decryption factor inside the aggregate (after the encrypts)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, the real runs) or gloo (rehearsal)")
     ap.add_argument("--serial", action="store_true",
                     help="no per-party streams in the timed steps (rocprof passes: per-kernel times unconfounded)")
@@ -148,14 +150,26 @@ def main():
     jc, lc = SecaggCrypter(), SecaggLomCrypter(W.LOM_NONCE)
     secrets_ = [W.pairwise_secrets_for(u, ids) for u in ids]
 
+    n_ct_step = (n + cr - 1) // cr
     # one HIP stream per party: the parties' encrypts are independent, so the tail round
     # of one exponentiation launch overlaps the next party's launch
     streams = [torch.cuda.Stream(device=dev) for _ in range(P)]
     main = torch.cuda.current_stream(dev)
 
+    factor_stream = torch.cuda.Stream(device=dev)
+    overlap_factor = not args.no_factor_overlap
+
     def step_jl(serial=False):
         cts = [None] * P
+        factor = None
         with D.deferred_checks():
+            if overlap_factor:
+                # the researcher's decryption factor H(t_k)^sk0 depends on (tau, k, sk0) only: it
+                # runs beside the parties' encrypts instead of after them (same work, same step)
+                f_s = main if serial else factor_stream
+                f_s.wait_stream(main)
+                with torch.cuda.stream(f_s):
+                    factor = jc.decrypt_factor_tensor(tau, n_ct_step, sk0, W.BIPRIME0, ct_offset=lo // cr)
             for p in range(P):
                 s_p = main if serial else streams[p]
                 s_p.wait_stream(main)
@@ -163,12 +177,14 @@ def main():
                     cts[p] = jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=weights[p],
                                                ct_offset=lo // cr)
         if not serial:
-            for st in streams:
+            for st in streams + [factor_stream]:
                 main.wait_stream(st)
             for p in range(P):
                 cts[p].record_stream(main)
+            if factor is not None:
+                factor.record_stream(main)
         return jc.aggregate_tensor(tau, torch.stack(cts), sk0, W.BIPRIME0, total_w, num_expected_params=n,
-                                   ct_offset=lo // cr)
+                                   ct_offset=lo // cr, decrypt_factor=factor)
 
     Y = torch.empty((P, n), dtype=torch.int64, device=dev) if args.scheme == "lom" or not args.no_lom_extra else None
 

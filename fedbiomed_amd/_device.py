@@ -367,10 +367,34 @@ def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, 
     return ct
 
 
+def jl_decrypt_factor(n_ct: int, biprime: int, key: int, tau: int, ct_offset: int = 0, dev=None) -> torch.Tensor:
+    """ServerKey's H(t_k)^key mod N^2 for ciphertexts [ct_offset, ct_offset + n_ct) of round
+    `tau` as int32 [n_ct, 64] limbs -- needs no ciphertext, so it can run while parties encrypt."""
+    dev = dev or device()
+    lib = N.load()
+    if tau < 0 or tau > U64_MAX:
+        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: round must be in [0, 2^64)")
+    f = torch.empty((n_ct, 64), dtype=torch.int32, device=dev)
+    if n_ct == 0:
+        return f
+    bp = _biprime_limbs(biprime)
+    kl, kneg = _key_limbs(key)
+    chunk = jl_chunk_ct()
+    ws = torch.empty(int(lib.fbm_jl_aggregate_workspace(min(n_ct, chunk))), dtype=torch.uint8, device=dev)
+    for k0 in range(0, n_ct, chunk):
+        k1 = min(n_ct, k0 + chunk)
+        st = _stats(dev)
+        _call(lib.fbm_jl_decrypt_factor, k1 - k0, _np_ptr(bp), _np_ptr(kl), kneg, int(tau), int(ct_offset) + k0,
+              _ptr(f[k0:k1]), _ptr(ws), _ptr(st), _stream())
+        _check_stats_or_defer(st)
+    return f
+
+
 def jl_aggregate(cts: torch.Tensor, biprime: int, key: int, tau: int, n_expected: int, total_weight: int,
                  clip=None, target=None, want_out: bool = True, want_sums: bool = False,
-                 slot: Optional[Tuple[int, int]] = None, ct_offset: int = 0):
-    """Aggregate [P, n_ct, 64] int32 ciphertext limbs -> (float64 [n_out], int64 [n_out, 2] sums)."""
+                 slot: Optional[Tuple[int, int]] = None, ct_offset: int = 0, factor: Optional[torch.Tensor] = None):
+    """Aggregate [P, n_ct, 64] int32 ciphertext limbs -> (float64 [n_out], int64 [n_out, 2] sums).
+    `factor`: the round's precomputed jl_decrypt_factor (same key, tau, ct range), or None."""
     dev = cts.device
     lib = N.load()
     target = target or SAParameters.TARGET_RANGE
@@ -389,6 +413,10 @@ def jl_aggregate(cts: torch.Tensor, biprime: int, key: int, tau: int, n_expected
     sums = torch.empty((n_out, 2), dtype=torch.int64, device=dev) if want_sums else None
     if n_ct == 0:
         return out, sums
+    if factor is not None:
+        factor = factor.contiguous()
+        if factor.dtype != torch.int32 or tuple(factor.shape) != (n_ct, 64) or factor.device != dev:
+            raise ValueError("factor must be the int32 [n_ct, 64] jl_decrypt_factor of these ciphertexts")
     bp = _biprime_limbs(biprime)
     kl, kneg = _key_limbs(key)
     chunk = jl_chunk_ct()
@@ -401,9 +429,13 @@ def jl_aggregate(cts: torch.Tensor, biprime: int, key: int, tau: int, n_expected
         if e1 <= e0:
             break
         st = _stats(dev)
-        _call(lib.fbm_jl_aggregate, _ptr(part), P, k1 - k0, es, cr, e1 - e0, _np_ptr(bp), _np_ptr(kl), kneg,
-              int(tau), int(ct_offset) + k0, int(total_weight), negc, step, _ptr(out[e0:e1] if want_out else None),
-              _ptr(sums[e0:e1] if want_sums else None), _ptr(ws), _ptr(st), _stream())
+        o, sm = _ptr(out[e0:e1] if want_out else None), _ptr(sums[e0:e1] if want_sums else None)
+        if factor is None:
+            _call(lib.fbm_jl_aggregate, _ptr(part), P, k1 - k0, es, cr, e1 - e0, _np_ptr(bp), _np_ptr(kl), kneg,
+                  int(tau), int(ct_offset) + k0, int(total_weight), negc, step, o, sm, _ptr(ws), _ptr(st), _stream())
+        else:
+            _call(lib.fbm_jl_aggregate_factor, _ptr(part), P, k1 - k0, es, cr, e1 - e0, _np_ptr(bp),
+                  _ptr(factor[k0:k1]), int(total_weight), negc, step, o, sm, _ptr(ws), _ptr(st), _stream())
         _check_stats(st)
     return out, sums
 

@@ -515,14 +515,79 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
   return timed("jl_exp", s, [&] { return launch_jl_exp(base, n_ct, jp, sc, 0, nude, table, slots, ops, cst, ct_out, s); });
 }
 
-int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,
-                     const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau, uint64_t ct_offset,
-                     uint64_t total_weight, double neg_clip, double step, double* out, uint64_t* sums,
-                     void* workspace, uint32_t* stats, void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  int rc = zero_stats(stats, s);
-  if (rc) return rc;
-  if (n_parties < 1 || !biprime || !key || total_weight == 0) {
+// aggregate workspace: ops | cst | X (blocked) | H [n_ct][64] | E [n_ct][64] | F [n_ct][64] |
+//                      xs [n_ct][32] | table    (fbm_jl_aggregate_workspace)
+struct JlAggWs {
+  uint32_t *ops, *cst, *X, *H, *E, *F, *xs, *table;
+  uint64_t slots;
+};
+static JlAggWs agg_ws(void* workspace, uint64_t n_ct) {
+  JlAggWs w;
+  uint8_t* ws = (uint8_t*)workspace;
+  w.slots = table_slots_for(n_ct);
+  uint64_t off = 0;
+  w.ops = (uint32_t*)ws;
+  off += align256(FBM_MAX_OPS * 4);
+  w.cst = (uint32_t*)(ws + off);
+  off += align256(FBM_CST_WORDS * 4);
+  w.X = (uint32_t*)(ws + off);
+  off += align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4);
+  w.H = (uint32_t*)(ws + off);
+  off += align256(n_ct * 64 * 4);
+  w.E = (uint32_t*)(ws + off);
+  off += align256(n_ct * 64 * 4);
+  w.F = (uint32_t*)(ws + off);
+  off += align256(n_ct * 64 * 4);
+  w.xs = (uint32_t*)(ws + off);
+  off += align256(n_ct * 32 * 4);
+  w.table = (uint32_t*)(ws + off);
+  return w;
+}
+
+// ServerKey's factor H(t_k)^sk0 mod N^2 (inverse first for sk0 < 0): depends on the round,
+// the ciphertext index and the key only -- not on the parties' ciphertexts.
+static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau,
+                          uint64_t ct_offset, uint32_t* factor, const JlAggWs& w, uint32_t* stats, hipStream_t s) {
+  JlParams jp;
+  int rc;
+  if ((rc = build_jl_params(biprime, 1, 1, tau, ct_offset, jp))) return rc;
+  JlSched sc;
+  int is_zero = 0;
+  if ((rc = build_schedule(key, sc, is_zero))) {
+    set_error("exponent schedule overflow");
+    return rc;
+  }
+  jp.key_is_zero = is_zero;
+  const bool inv = key_negative && !is_zero;
+  uint32_t* E = inv ? w.E : factor;
+  if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, w.ops, w.cst, s); }))) return rc;
+  if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, w.H, stats, s); }))) return rc;
+  if ((rc = timed("jl_exp", s, [&] { return launch_jl_exp(w.H, n_ct, jp, sc, 1, nullptr, w.table, w.slots, w.ops, w.cst, E, s); })))
+    return rc;
+  if (inv && (rc = timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, E, w.xs, factor, stats, s); })))  // xs: y scratch
+    return rc;
+  return FBM_OK;
+}
+
+// v = prod_u c_u * factor mod N^2, x = (v-1)/N, decode + average + dequantise
+static int jl_combine_impl(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,
+                           const uint32_t* biprime, const uint32_t* factor, uint64_t total_weight, double neg_clip,
+                           double step, double* out, uint64_t* sums, const JlAggWs& w, uint32_t* stats, hipStream_t s) {
+  JlParams jp;
+  int rc;
+  if ((rc = build_jl_params(biprime, es, cr, 0, 0, jp))) return rc;
+  JlSched none;
+  memset(&none, 0, sizeof(none));
+  if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, none, w.ops, w.cst, s); }))) return rc;
+  if ((rc = timed("jl_prod", s, [&] { return launch_jl_prod(cts, n_parties, n_ct, jp, w.cst, w.X, s); }))) return rc;
+  if ((rc = timed("jl_fin", s, [&] { return launch_jl_fin(n_ct, jp, w.X, factor, w.xs, s); }))) return rc;
+  return timed("jl_decode", s, [&] {
+    return launch_jl_decode(w.xs, es, cr, n_out, total_weight, neg_clip, step, out, sums, stats, s);
+  });
+}
+
+static int jl_agg_checks(int n_parties, uint64_t n_ct, const uint32_t* biprime, uint64_t total_weight) {
+  if (n_parties < 1 || !biprime || total_weight == 0) {
     set_error("invalid aggregate arguments");
     return FBM_E_ARG;
   }
@@ -531,49 +596,62 @@ int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, 
               (unsigned long long)n_ct);
     return FBM_E_UNSUPPORTED;
   }
+  return FBM_OK;
+}
+
+int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,
+                     const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau, uint64_t ct_offset,
+                     uint64_t total_weight, double neg_clip, double step, double* out, uint64_t* sums,
+                     void* workspace, uint32_t* stats, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc = zero_stats(stats, s);
+  if (rc) return rc;
+  if ((rc = jl_agg_checks(n_parties, n_ct, biprime, total_weight))) return rc;
+  if (!key) {
+    set_error("null key");
+    return FBM_E_ARG;
+  }
   if (n_ct == 0) return FBM_OK;
   if (n_out > n_ct * (uint64_t)cr) n_out = n_ct * (uint64_t)cr;
   if (!cts || !workspace) {
     set_error("null pointer argument");
     return FBM_E_ARG;
   }
-  JlParams jp;
-  if ((rc = build_jl_params(biprime, es, cr, tau, ct_offset, jp))) return rc;
-  JlSched sc;
-  int is_zero = 0;
-  if ((rc = build_schedule(key, sc, is_zero))) {
-    set_error("exponent schedule overflow");
-    return rc;
+  const JlAggWs w = agg_ws(workspace, n_ct);
+  if ((rc = jl_factor_impl(n_ct, biprime, key, key_negative, tau, ct_offset, w.F, w, stats, s))) return rc;
+  return jl_combine_impl(cts, n_parties, n_ct, es, cr, n_out, biprime, w.F, total_weight, neg_clip, step, out, sums, w,
+                         stats, s);
+}
+
+int fbm_jl_decrypt_factor(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau,
+                          uint64_t ct_offset, uint32_t* factor, void* workspace, uint32_t* stats, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc = zero_stats(stats, s);
+  if (rc) return rc;
+  if ((rc = jl_agg_checks(1, n_ct, biprime, 1))) return rc;
+  if (n_ct == 0) return FBM_OK;
+  if (!key || !factor || !workspace) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
   }
-  jp.key_is_zero = is_zero;
-  const uint64_t slots = table_slots_for(n_ct);
-  uint8_t* ws = (uint8_t*)workspace;
-  uint32_t* ops = (uint32_t*)ws;
-  uint64_t off = align256(FBM_MAX_OPS * 4);
-  uint32_t* cst = (uint32_t*)(ws + off);
-  off += align256(FBM_CST_WORDS * 4);
-  uint32_t* X = (uint32_t*)(ws + off);
-  off += align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4);
-  uint32_t* H = (uint32_t*)(ws + off);
-  off += align256(n_ct * 64 * 4);
-  uint32_t* E = (uint32_t*)(ws + off);
-  off += align256(n_ct * 64 * 4);
-  uint32_t* inv = (uint32_t*)(ws + off);
-  off += align256(n_ct * 64 * 4);
-  uint32_t* xs = (uint32_t*)(ws + off);
-  off += align256(n_ct * 32 * 4);
-  uint32_t* table = (uint32_t*)(ws + off);
-  if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s); }))) return rc;
-  if ((rc = timed("jl_prod", s, [&] { return launch_jl_prod(cts, n_parties, n_ct, jp, cst, X, s); }))) return rc;
-  if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, H, stats, s); }))) return rc;
-  if ((rc = timed("jl_exp", s, [&] { return launch_jl_exp(H, n_ct, jp, sc, 1, nullptr, table, slots, ops, cst, E, s); }))) return rc;
-  if (key_negative && !is_zero) {
-    if ((rc = timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, E, xs, inv, stats, s); }))) return rc;  // xs doubles as y scratch
-  } else {
-    inv = E;  // positive (or zero) server key: v = prod * H^sk0, no inverse
+  return jl_factor_impl(n_ct, biprime, key, key_negative, tau, ct_offset, factor, agg_ws(workspace, n_ct), stats, s);
+}
+
+int fbm_jl_aggregate_factor(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,
+                            const uint32_t* biprime, const uint32_t* factor, uint64_t total_weight, double neg_clip,
+                            double step, double* out, uint64_t* sums, void* workspace, uint32_t* stats, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc = zero_stats(stats, s);
+  if (rc) return rc;
+  if ((rc = jl_agg_checks(n_parties, n_ct, biprime, total_weight))) return rc;
+  if (n_ct == 0) return FBM_OK;
+  if (n_out > n_ct * (uint64_t)cr) n_out = n_ct * (uint64_t)cr;
+  if (!cts || !factor || !workspace) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
   }
-  if ((rc = timed("jl_fin", s, [&] { return launch_jl_fin(n_ct, jp, X, inv, xs, s); }))) return rc;
-  return timed("jl_decode", s, [&] { return launch_jl_decode(xs, es, cr, n_out, total_weight, neg_clip, step, out, sums, stats, s); });
+  return jl_combine_impl(cts, n_parties, n_ct, es, cr, n_out, biprime, factor, total_weight, neg_clip, step, out, sums,
+                         agg_ws(workspace, n_ct), stats, s);
 }
 
 int fbm_test_modinv(const uint32_t* x, const uint32_t* n, uint32_t* out, int* batches) {

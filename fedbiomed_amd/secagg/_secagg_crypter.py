@@ -89,15 +89,27 @@ class SecaggCrypter:
     def aggregate_tensor(self, current_round: int, cts: torch.Tensor, key: int, biprime: int,
                          total_sample_size: int, clipping_range: Union[int, None] = None,
                          num_expected_params: int = 1, target_range: Optional[int] = None,
-                         want_sums: bool = False, ct_offset: int = 0):
-        """[P, n_ct, 64] int32 ciphertext limbs in HBM -> float64 [n] averaged parameters."""
+                         want_sums: bool = False, ct_offset: int = 0,
+                         decrypt_factor: Optional[torch.Tensor] = None):
+        """[P, n_ct, 64] int32 ciphertext limbs in HBM -> float64 [n] averaged parameters.
+        `decrypt_factor`: this round's `decrypt_factor_tensor` (computed ahead, e.g. while the
+        nodes encrypt), or None to compute it here."""
         if not isinstance(key, int):
             raise TypeError("The key should be type of integer")
         target_range = target_range or SAParameters.TARGET_RANGE
         out, sums = D.jl_aggregate(cts, biprime, key, current_round, num_expected_params, total_sample_size,
                                    clip=clipping_range, target=target_range, want_sums=want_sums,
-                                   ct_offset=ct_offset)
+                                   ct_offset=ct_offset, factor=decrypt_factor)
         return (out, sums) if want_sums else out
+
+    def decrypt_factor_tensor(self, current_round: int, num_ciphertexts: int, key: int, biprime: int,
+                              ct_offset: int = 0) -> torch.Tensor:
+        """The server key's per-ciphertext factor H(t_k)^key mod N^2 of round `current_round`
+        (int32 [num_ciphertexts, 64] in HBM).  It does not depend on the parties' ciphertexts,
+        so the researcher can compute it before they arrive and pass it to aggregate_tensor."""
+        if not isinstance(key, int):
+            raise TypeError("The key should be type of integer")
+        return D.jl_decrypt_factor(num_ciphertexts, biprime, key, current_round, ct_offset=ct_offset)
 
     # ---- reference API -----------------------------------------------------------------------
     def encrypt(self, num_nodes: int, current_round: int, params: List[float], key: int, biprime: int,

@@ -135,6 +135,20 @@ int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, 
                      uint64_t ct_offset, uint64_t total_weight, double neg_clip, double step, double* out, uint64_t* sums,
                      void* workspace, uint32_t* stats, void* stream);
 
+/* The aggregate in two halves (fbm_jl_aggregate = factor, then combine, bit for bit):
+ * fbm_jl_decrypt_factor: ServerKey.decrypt's H(t_k)^sk0 mod N^2 (_jls.py:520-562; inverse
+ *   first for sk0 < 0) for ciphertexts [ct_offset, ct_offset + n_ct) of round tau --
+ *   independent of the parties' ciphertexts, so a researcher can compute it while the
+ *   nodes train/encrypt.  factor: device, n_ct x 64 u32 limbs.
+ * fbm_jl_aggregate_factor: the ciphertext product (_jls.py:353-374,691-693), v = prod *
+ *   factor, x = (v-1)/N, VES decode, average, dequantise -- as fbm_jl_aggregate.
+ * Both take fbm_jl_aggregate_workspace(n_ct) bytes of workspace. */
+int fbm_jl_decrypt_factor(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau,
+                          uint64_t ct_offset, uint32_t* factor, void* workspace, uint32_t* stats, void* stream);
+int fbm_jl_aggregate_factor(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,
+                            const uint32_t* biprime, const uint32_t* factor, uint64_t total_weight, double neg_clip,
+                            double step, double* out, uint64_t* sums, void* workspace, uint32_t* stats, void* stream);
+
 /* ---- additive secret sharing of vectors (reference fedbiomed/common/secagg/_additive_ss.py) ----
  * fbm_ass_split replaces AdditiveSecret.split / _shares_int (:40-98) for a list secret:
  * every element v (secret_dtype FBM_U64 or FBM_I64) gets n_shares-1 shares uniform in

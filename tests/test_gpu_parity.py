@@ -321,6 +321,35 @@ def test_lom_more_than_64_peers(dev):
     assert _bits(out) == _bits(O.lom_crypter_aggregate(ys, sum(ws)))
 
 
+@pytest.mark.parametrize("neg", [True, False])
+def test_jl_decrypt_factor_split(dev, monkeypatch, neg):
+    """aggregate = decrypt_factor (no ciphertexts needed) + combine, bit for bit, for negative
+    and positive server keys, with a shard offset and forced call striping."""
+    from fedbiomed_amd import workload as W
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    P, n, tau, k0 = 3, 900, 6, 11
+    keys = [W.jl_user_key(p) for p in range(P)]
+    sk0 = -sum(keys) if neg else 12345
+    ws = [W.party_weight(p) for p in range(P)]
+    jc = SecaggCrypter()
+    cts = torch.stack([jc.encrypt_tensor(P, tau, torch.from_numpy(W.party_params(p, n)).to(dev), keys[p],
+                                         W.BIPRIME0, weight=ws[p], ct_offset=k0) for p in range(P)])
+    n_ct = cts.shape[1]
+    fused, s1 = jc.aggregate_tensor(tau, cts, sk0, W.BIPRIME0, sum(ws), num_expected_params=n, want_sums=True,
+                                    ct_offset=k0)
+    f = jc.decrypt_factor_tensor(tau, n_ct, sk0, W.BIPRIME0, ct_offset=k0)
+    split, s2 = jc.aggregate_tensor(tau, cts, sk0, W.BIPRIME0, sum(ws), num_expected_params=n, want_sums=True,
+                                    ct_offset=k0, decrypt_factor=f)
+    assert torch.equal(s1, s2) and torch.equal(fused.view(torch.int64), split.view(torch.int64))
+    monkeypatch.setenv("FBM_JL_CHUNK_CT", "4")
+    f4 = jc.decrypt_factor_tensor(tau, n_ct, sk0, W.BIPRIME0, ct_offset=k0)
+    assert torch.equal(f4, f)
+    _, s3 = jc.aggregate_tensor(tau, cts, sk0, W.BIPRIME0, sum(ws), num_expected_params=n, want_sums=True,
+                                ct_offset=k0, decrypt_factor=f4)
+    assert torch.equal(s3, s1)
+
+
 def test_jl_edge_cases(dev):
     from fedbiomed_amd import workload as W
     from fedbiomed_amd.exceptions import FedbiomedSecaggCrypterError
