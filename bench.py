@@ -406,6 +406,16 @@ def main():
                                 "sample": f"{ns:,} elements x {P} parties, encrypt all + aggregate, "
                                           f"{tc:.1f} s on 1 host core (oracle/secagg_oracle.py; GMP mpz_powm "
                                           f"via ctypes as gmpy2 does)"}
+        cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")  # tools/calibrate_cpu.py
+        if os.path.exists(cal):
+            with open(cal) as fh:
+                c = json.load(fh).get(args.scheme)
+            if c:
+                r = c["reference_over_oracle_time"]
+                line["cpu_baseline"]["reference_equivalent"] = {
+                    "value": ns / tc / r, "unit": "params/s",
+                    "note": f"the reference crypter itself ran {r:.3f}x the oracle's time on this sample in the "
+                            "build container (profiles/cpu_calibration.json); it cannot run on the GPU box"}
         line["gpu_over_cpu"] = value / (ns / tc)
     if rank == 0:
         print(json.dumps(line))
