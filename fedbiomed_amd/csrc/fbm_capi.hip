@@ -271,15 +271,26 @@ template <class F>
 static int timed(const char* name, hipStream_t s, F f) {
   if (!g_prof_on) return f();
   ProfRec r{name, nullptr, nullptr};
-  hipEventCreate(&r.a);
-  hipEventCreate(&r.b);
+  if (hipEventCreate(&r.a) != hipSuccess) return f();
+  if (hipEventCreate(&r.b) != hipSuccess) {
+    (void)hipEventDestroy(r.a);
+    return f();
+  }
   // Drain the stream first: a marker can otherwise complete while the previous kernel is
   // still running, and its interval would absorb that kernel's tail (measured: per-kernel
   // sums 2.3x the wall time).  Profiling mode therefore serialises host and device.
-  hipStreamSynchronize(s);
-  hipEventRecord(r.a, s);
+  // A failed drain or marker only loses this timing record, never the launch itself.
+  if (hipStreamSynchronize(s) != hipSuccess || hipEventRecord(r.a, s) != hipSuccess) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+    return f();
+  }
   const int rc = f();
-  hipEventRecord(r.b, s);
+  if (hipEventRecord(r.b, s) != hipSuccess) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+    return rc;
+  }
   std::lock_guard<std::mutex> g(g_prof_mu);
   g_prof.push_back(r);
   return rc;
@@ -774,14 +785,15 @@ int fbm_prof_report(char* buf, int len) {
   // cleared) when buf can hold all of it, so a size query (buf == NULL) loses nothing.
   std::lock_guard<std::mutex> g(g_prof_mu);
   for (auto& r : g_prof) {
-    hipEventSynchronize(r.b);
     float ms = 0.f;
-    hipEventElapsedTime(&ms, r.a, r.b);
-    auto& e = g_prof_agg[r.name];
-    e.first += 1;
-    e.second += ms;
-    hipEventDestroy(r.a);
-    hipEventDestroy(r.b);
+    const bool ok = hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess;
+    if (ok) {
+      auto& e = g_prof_agg[r.name];
+      e.first += 1;
+      e.second += ms;
+    }
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
   }
   g_prof.clear();
   std::string out;

@@ -86,24 +86,21 @@ __global__ void __launch_bounds__(256) jl_nude_kernel(const uint32_t* __restrict
   }
   uint32_t p28[FBM_NLN];
   to28<32, FBM_NLN>(p32, p28);
-  uint64_t col[FBM_NL];
-#pragma unroll
-  for (int k = 0; k < FBM_NL; ++k) col[k] = 0;
-#pragma unroll
-  for (int i = 0; i < FBM_NLN; ++i) {
-#pragma unroll
-    for (int j = 0; j < FBM_NLN; ++j) col[i + j] += (uint64_t)jp.mn.M[i] * p28[j];
-  }
-  col[0] += 1;
-  uint64_t carry = 0;
-  uint32_t o[FBM_NL];
+  // Product scanning, one output column at a time (a column holds <= 37 products < 2^56,
+  // so a u64 accumulator plus the carry cannot overflow): every index is a compile-time
+  // constant, so nothing lives in scratch (a row-wise accumulator array did, and its
+  // spill traffic made this kernel HBM-bound at ~30x its algorithmic bytes).
+  uint32_t* dst = launder_v(nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255));
+  uint64_t carry = 1;  // the "+1" of N*pt + 1
 #pragma unroll
   for (int k = 0; k < FBM_NL; ++k) {
-    const uint64_t v = col[k] + carry;
-    o[k] = (uint32_t)v & FBM_LMASK;
-    carry = v >> FBM_LB;
+    uint64_t acc = carry;
+#pragma unroll
+    for (int i = (k < FBM_NLN ? 0 : k - FBM_NLN + 1); i <= (k < FBM_NLN ? k : FBM_NLN - 1); ++i)
+      acc += (uint64_t)jp.mn.M[i] * p28[k - i];
+    dst[k * 256] = (uint32_t)acc & FBM_LMASK;
+    carry = acc >> FBM_LB;
   }
-  col_store(nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255), o);
 }
 
 // ------------------------------------------------------------------------------------
