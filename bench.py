@@ -29,9 +29,9 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MAD_PEAK_TOPS = 36.48        # measured v_mad_u64_u32 peak, whole chip, best occupancy (tools/microbench/madpeak.hip,
                              # profiles/r1_madpeak.txt: 35.3 T at 2 waves/SIMD, 36.5 T at 4)
-MADS_PER_MONTMUL = 74 * 148  # general 28-bit-limb product: 74 rows x (74 a*b + 74 m*M) v_mad_u64_u32
-# square (tools/gen_mont_asm.py square()): 2701 doubled cross products + 111 diagonal + 74*74 m*M
-MADS_PER_SQUARE = sum(73 - r for r in range(74)) + 74 + 37 + 74 * 74
+# v_mad_u64_u32 per lane of one N-adic product modulo N^2 (tools/gen_nadic_asm.py: 37 rows x
+# (37 x0*b0 + 37 q*N + 37 x0*b1 + 37 x1*b0 + 37 q'*N), the square without x1*b0) are read
+# from the library (fbm_jl_mads), so the count always matches the engine that ran.
 
 
 def products_per_exp(key: int, win: int = 5):
@@ -65,9 +65,9 @@ def products_per_exp(key: int, win: int = 5):
     return 1 + sq, 1 + (2 ** (win - 1) - 1) + mul + 1
 
 
-def mads_per_exp(key: int, win: int = 5) -> int:
+def mads_per_exp(key: int, win: int, mads_mul: int, mads_sq: int) -> int:
     sq, gen = products_per_exp(key, win)
-    return sq * MADS_PER_SQUARE + gen * MADS_PER_MONTMUL
+    return sq * mads_sq + gen * mads_mul
 
 
 def committed_traffic(kernel: str, scheme: str, n_ct: int):
@@ -236,7 +236,9 @@ def main():
         alg_bytes = prof_steps * (P * (4 * n + 256 * n_ct) + (256 * P * n_ct + 8 * n))
         win = _native.load().fbm_jl_window()
         mm = sum(sum(products_per_exp(k, win)) for k in keys) + sum(products_per_exp(sk0, win))
-        mads_step = n_ct * (sum(mads_per_exp(k, win) for k in keys) + mads_per_exp(sk0, win))
+        mads_mul, mads_sq = _native.load().fbm_jl_mads(0), _native.load().fbm_jl_mads(1)
+        mads_step = n_ct * (sum(mads_per_exp(k, win, mads_mul, mads_sq) for k in keys)
+                            + mads_per_exp(sk0, win, mads_mul, mads_sq))
         mads = prof_steps * mads_step
         kname = "jl_exp_kernel"
     else:
@@ -269,7 +271,9 @@ def main():
                                  "products_per_ct_step": mm, "window": win,
                                  "step_achieved": mads_step / (ms_per_step / 1000) / 1e12,
                                  "step_frac": mads_step / (ms_per_step / 1000) / 1e12 / MAD_PEAK_TOPS,
-                                 "note": "executed v_mad_u64_u32 (squares 8288, general products 10952 each); "
+                                 "mads_per_square": mads_sq, "mads_per_product": mads_mul,
+                                 "note": "executed v_mad_u64_u32 of the N-adic engine (per square / product "
+                                         "above); "
                                          "achieved/frac: serialised jl_exp launches (HIP events); step_*: the "
                                          "timed step (parties on concurrent streams, all kernels)"}
 

@@ -47,6 +47,7 @@ c_vp = ctypes.c_void_p
 SIGNATURES = {
     "fbm_abi_version": (c_int, []),
     "fbm_jl_window": (c_int, []),
+    "fbm_jl_mads": (c_int, [c_int]),
     "fbm_last_error": (ctypes.c_char_p, []),
     "fbm_check_stats": (c_int, [c_vp, c_int, c_vp]),
     "fbm_lom_protect": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_vp, c_vp, c_int, c_int,
@@ -68,6 +69,7 @@ SIGNATURES = {
     "fbm_ass_split_wide": (c_int, [c_vp, c_u64, c_int, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_vp, c_vp]),
     "fbm_ass_reconstruct_wide": (c_int, [c_vp, c_int, c_int, c_u64, c_vp, c_vp]),
     "fbm_test_modinv": (c_int, [c_vp, c_vp, c_vp, c_vp]),
+    "fbm_test_nadic_consts": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fbm_prof_enable": (c_int, [c_int]),
     "fbm_prof_report": (c_int, [ctypes.c_char_p, c_int]),
 }

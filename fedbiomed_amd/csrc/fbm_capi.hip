@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "fbm_internal.hpp"
+#include "fbm_nadic_asm.hpp"
 #include "fbm_safegcd.hpp"
 
 namespace fbm {
@@ -137,6 +138,63 @@ static void build_mont(const Big& m, MontCtxT<NL>& c) {
   c.mp = (0u - inv) & FBM_LMASK;
 }
 
+// (q, r) = (a div m, a mod m) by binary long division (host, per call; a < 2^2080, m odd)
+static void big_divmod(const Big& a, const Big& m, Big& q, Big& r) {
+  const int nb = big_bits(a);
+  q.assign(a.size(), 0u);
+  r.assign(m.size() + 1, 0u);
+  for (int i = nb - 1; i >= 0; --i) {
+    uint32_t c = (a[i >> 5] >> (i & 31)) & 1u;
+    for (size_t k = 0; k < r.size(); ++k) {
+      const uint32_t nc = r[k] >> 31;
+      r[k] = (r[k] << 1) | c;
+      c = nc;
+    }
+    if (big_cmp(r, m) >= 0) {
+      big_sub_inplace(r, m);
+      q[i >> 5] |= 1u << (i & 31);
+    }
+  }
+}
+
+// Constants of the N-adic engine (tools/gen_nadic_asm.py): R = 2^(37*28) = 2^1036.
+static void build_nadic(const Big& N, const Big& M, const MontCtxN& mn, NadicCtx& na) {
+  memset(&na, 0, sizeof(na));
+  const int L = FBM_NLN;
+  // K = (1 - R) mod N, K'_i = (2^28 - 1) + K_i
+  Big Rm = big_pow2_mod(L * FBM_LB, N);  // R mod N  (N odd >= 3 -> Rm != 0)
+  Big K(N.size() + 1, 0u);
+  K[0] = 1u;
+  if (big_cmp(Rm, K) > 0) {  // K = N + 1 - Rm
+    Big t(N.begin(), N.end());
+    t.push_back(0u);
+    uint64_t c = 1;
+    for (size_t k = 0; k < t.size(); ++k) {
+      c += t[k];
+      t[k] = (uint32_t)c;
+      c >>= 32;
+    }
+    big_sub_inplace(t, Rm);
+    K = t;
+  } else {  // Rm == 1 -> K = 0
+    K.assign(1, 0u);
+  }
+  uint32_t k28[FBM_NLN];
+  to28_host(K, k28, L);
+  for (int j = 0; j < 10; ++j) na.nk[j] = mn.M[j];
+  for (int j = 10; j < L; ++j) na.nk[16 + j - 10] = mn.M[j];
+  for (int j = 0; j < L; ++j) na.nk[43 + j] = FBM_LMASK + k28[j];
+  // R^2, R^3 mod N^2 = u0 + u1 N
+  for (int e = 2; e <= 3; ++e) {
+    const Big u = big_pow2_mod(e * L * FBM_LB, M);
+    Big q, r;
+    big_divmod(u, N, q, r);
+    uint32_t* dst = e == 2 ? na.r2na : na.r3na;
+    to28_host(r, dst, L);
+    to28_host(q, dst + L, L);
+  }
+}
+
 static int build_jl_params(const uint32_t* biprime, int es, int cr, uint64_t tau, uint64_t ct_offset, JlParams& jp) {
   memset(&jp, 0, sizeof(jp));
   Big N(biprime, biprime + 32);
@@ -154,6 +212,7 @@ static int build_jl_params(const uint32_t* biprime, int es, int cr, uint64_t tau
   while (M.size() > 64) M.pop_back();
   build_mont<FBM_NL>(M, jp.mc);
   build_mont<FBM_NLN>(N, jp.mn);
+  build_nadic(N, M, jp.mn, jp.na);
   for (int i = 0; i < 32; ++i) jp.N32[i] = biprime[i];
   {  // N^-1 mod 2^1024 by Newton: y <- y (2 - N y); y = N is correct to 3 bits for odd N
     uint32_t y[32], t[32];
@@ -318,6 +377,7 @@ extern "C" {
 int fbm_abi_version(void) { return FBM_ABI_VERSION; }
 
 int fbm_jl_window(void) { return FBM_WIN; }
+int fbm_jl_mads(int square) { return square ? FBM_NA_MADS_SQR : FBM_NA_MADS_MUL; }
 
 const char* fbm_last_error(void) { return g_err; }
 
@@ -521,9 +581,12 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
     // gmpy2.powmod with a negative exponent (_jls.py:60-73): invert H(t_k) mod N^2 first,
     // then raise the inverse to |key|
     if ((rc = timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, H, Y, Hinv, stats, s); }))) return rc;
+    // the inverse is a full-width residue: hand it to the exponentiation as N-adic digits
+    if ((rc = timed("jl_split", s, [&] { return launch_jl_nadic_split(n_ct, jp, Hinv, Y, Hinv, s); }))) return rc;
     base = Hinv;
   }
-  return timed("jl_exp", s, [&] { return launch_jl_exp(base, n_ct, jp, sc, 0, nude, table, slots, ops, cst, ct_out, s); });
+  const int mode = (key_negative && !is_zero) ? FBM_EXP_H_NADIC : 0;
+  return timed("jl_exp", s, [&] { return launch_jl_exp(base, n_ct, jp, sc, mode, nude, table, slots, ops, cst, ct_out, s); });
 }
 
 // aggregate workspace: ops | cst | X (blocked) | H [n_ct][64] | E [n_ct][64] | F [n_ct][64] |
@@ -573,7 +636,7 @@ static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t
   uint32_t* E = inv ? w.E : factor;
   if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, w.ops, w.cst, s); }))) return rc;
   if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, w.H, stats, s); }))) return rc;
-  if ((rc = timed("jl_exp", s, [&] { return launch_jl_exp(w.H, n_ct, jp, sc, 1, nullptr, w.table, w.slots, w.ops, w.cst, E, s); })))
+  if ((rc = timed("jl_exp", s, [&] { return launch_jl_exp(w.H, n_ct, jp, sc, FBM_EXP_DEC, nullptr, w.table, w.slots, w.ops, w.cst, E, s); })))
     return rc;
   if (inv && (rc = timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, E, w.xs, factor, stats, s); })))  // xs: y scratch
     return rc;
@@ -663,6 +726,21 @@ int fbm_jl_aggregate_factor(const uint32_t* cts, int n_parties, uint64_t n_ct, i
   }
   return jl_combine_impl(cts, n_parties, n_ct, es, cr, n_out, biprime, factor, total_weight, neg_clip, step, out, sums,
                          agg_ws(workspace, n_ct), stats, s);
+}
+
+int fbm_test_nadic_consts(const uint32_t* n32, uint32_t* nk, uint32_t* r2na, uint32_t* r3na, uint32_t* np) {
+  if (!n32 || !nk || !r2na || !r3na || !np) {
+    set_error("fbm_test_nadic_consts: null pointer");
+    return FBM_E_ARG;
+  }
+  JlParams jp;
+  int rc = build_jl_params(n32, 34, 30, 1, 0, jp);
+  if (rc) return rc;
+  memcpy(nk, jp.na.nk, sizeof(jp.na.nk));
+  memcpy(r2na, jp.na.r2na, sizeof(jp.na.r2na));
+  memcpy(r3na, jp.na.r3na, sizeof(jp.na.r3na));
+  *np = jp.mn.mp;
+  return FBM_OK;
 }
 
 int fbm_test_modinv(const uint32_t* x, const uint32_t* n, uint32_t* out, int* batches) {

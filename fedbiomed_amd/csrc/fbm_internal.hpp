@@ -68,7 +68,13 @@ int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t 
 #define FBM_CST_R2 128
 #define FBM_CST_ONE 256
 #define FBM_CST_R2COL (256 + FBM_NL * 256)
-#define FBM_CST_WORDS (256 + 2 * FBM_NL * 256)
+// N-adic exponentiation engine (fbm_nadic_asm.hpp): its 80-word constants block (N limbs
+// and K'_i, the layout the assembly's scalar loads expect) and R^2 mod N^2 as two N-adic
+// digits (74 limbs, the uniform A operand that brings h into Montgomery form)
+#define FBM_CST_NK (256 + 2 * FBM_NL * 256)
+#define FBM_CST_R2NA (FBM_CST_NK + 128)
+#define FBM_CST_R3NA (FBM_CST_R2NA + 128)  // R^3 mod N^2 (digits): the high part of a wide h
+#define FBM_CST_WORDS (FBM_CST_R3NA + 128)
 
 // sliding-window schedule, passed by value (kernarg segment -> scalar loads).
 // op k (u16): (squarings before the multiply) << FBM_OP_SHIFT | (table index + 1, 0 = none)
@@ -78,9 +84,20 @@ struct JlSched {
   uint16_t op[FBM_MAX_OPS];
 };
 
+// N-adic constants (tools/gen_nadic_asm.py): words 0..9 = N_0..N_9, 16..42 = N_10..N_36,
+// 43..79 = K'_i = (2^28 - 1) + K_i with K = (1 - 2^1036) mod N; r2na / r3na = the digits
+// of R^2 = 2^2072 / R^3 = 2^3108 mod N^2 (u mod N, u div N), 37 limbs each.
+struct NadicCtx {
+  uint32_t nk[80];
+  uint32_t r2na[FBM_NL];
+  uint32_t r3na[FBM_NL];
+  uint32_t pad[4];
+};
+
 struct JlParams {
   MontCtx mc;                    // modulus M = N^2 (74 limbs)
-  MontCtxN mn;                   // modulus N (37 limbs) -- inverse mod N, N*pt
+  MontCtxN mn;                   // modulus N (37 limbs) -- inverse mod N, N*pt, N-adic np
+  NadicCtx na;                   // N-adic engine constants (jl_exp_kernel)
   uint32_t N32[32];              // N, 32-bit limbs (<= 1024 bits)
   uint32_t Ninv32[32];           // N^-1 mod 2^1024 (exact division (v-1)/N in jl_fin_kernel)
   int n_bits;                    // bit length of N
@@ -103,6 +120,10 @@ int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const Jl
                   const uint32_t* cst, uint32_t* out, hipStream_t s);
 int launch_jl_prod(const uint32_t* cts, int n_parties, uint64_t n_ct, const JlParams& jp, const uint32_t* cst,
                    uint32_t* X, hipStream_t s);
+#define FBM_EXP_DEC 1      // jl_exp mode bits: plain power (no nude product)
+#define FBM_EXP_H_NADIC 2  // H rows are N-adic digit pairs (jl_split_kernel)
+int launch_jl_nadic_split(uint64_t n_ct, const JlParams& jp, const uint32_t* E, uint32_t* Y, uint32_t* out,
+                          hipStream_t s);
 int launch_jl_inv(uint64_t n_ct, const JlParams& jp, const uint32_t* E, uint32_t* Y, uint32_t* inv, uint32_t* stats,
                   hipStream_t s);
 int launch_jl_fin(uint64_t n_ct, const JlParams& jp, const uint32_t* X, const uint32_t* inv, uint32_t* xout,

@@ -3,7 +3,7 @@
 // Encrypt (one party):  pack -> nude -> fdh -> exp(ENC)
 //   jl_pack_kernel   quantize + weight + VES.encode     (_secagg_utils.py:82-119,
 //                    _secagg_crypter.py:252-276, _jls.py:118-144,169-176)
-//   jl_nude_kernel   (N*pt + 1) mod N^2                   (_jls.py:494-496)
+//   jl_nude_kernel   N*pt + 1 as N-adic digits (1, pt)     (_jls.py:494-496)
 //   jl_fdh_kernel    FDH.H(t_k), t_k = (k<<512)|tau       (_jls.py:451-467,727-762)
 //   jl_exp_kernel    H^sk mod N^2 (GMP mpz_powm via gmpy2, _jls.py:60-73,500-501) and
 //                    the final product with nude           (_jls.py:502)
@@ -20,6 +20,7 @@
 // the per-lane exponent tables are limb-major [limb][lane] so a wave's accesses coalesce.
 #include "fbm_internal.hpp"
 #include "fbm_mont_asm.hpp"
+#include "fbm_nadic_asm.hpp"
 #include "fbm_safegcd.hpp"
 
 namespace fbm {
@@ -70,8 +71,8 @@ __global__ void __launch_bounds__(256) jl_pack_kernel(const XT* __restrict__ x, 
 }
 
 // ------------------------------------------------------------------------------------
-// nude = N*pt + 1  (< 2^2048; the reduction mod N^2 happens in the final Montgomery
-// product, which accepts any a < R)  ->  [limb][ct] 28-bit limbs
+// nude = N*pt + 1 as the N-adic digit pair (1, pt)  ->  [limb][ct] 28-bit limbs (the last
+// operand of jl_exp_kernel's encrypt; pt < 2^1024 < R is a valid one-off digit)
 // ------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) jl_nude_kernel(const uint32_t* __restrict__ pt, uint64_t n_ct, JlParams jp,
                                                       uint32_t* __restrict__ nude) {
@@ -86,21 +87,13 @@ __global__ void __launch_bounds__(256) jl_nude_kernel(const uint32_t* __restrict
   }
   uint32_t p28[FBM_NLN];
   to28<32, FBM_NLN>(p32, p28);
-  // Product scanning, one output column at a time (a column holds <= 37 products < 2^56,
-  // so a u64 accumulator plus the carry cannot overflow): every index is a compile-time
-  // constant, so nothing lives in scratch (a row-wise accumulator array did, and its
-  // spill traffic made this kernel HBM-bound at ~30x its algorithmic bytes).
+  // N*pt + 1 in N-adic digits is (1, pt): no arithmetic, only the layout of the
+  // exponentiation's B operand (blocked column, digit 0 in limbs 0..36, digit 1 in 37..73)
   uint32_t* dst = launder_v(nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255));
-  uint64_t carry = 1;  // the "+1" of N*pt + 1
 #pragma unroll
-  for (int k = 0; k < FBM_NL; ++k) {
-    uint64_t acc = carry;
+  for (int k = 0; k < FBM_NLN; ++k) dst[k * 256] = k == 0 ? 1u : 0u;
 #pragma unroll
-    for (int i = (k < FBM_NLN ? 0 : k - FBM_NLN + 1); i <= (k < FBM_NLN ? k : FBM_NLN - 1); ++i)
-      acc += (uint64_t)jp.mn.M[i] * p28[k - i];
-    dst[k * 256] = (uint32_t)acc & FBM_LMASK;
-    carry = acc >> FBM_LB;
-  }
+  for (int k = 0; k < FBM_NLN; ++k) dst[(FBM_NLN + k) * 256] = p28[k];
 }
 
 // ------------------------------------------------------------------------------------
@@ -357,19 +350,81 @@ __device__ __forceinline__ void glb_to_lds(const uint32_t* g, uint32_t* lds) {
   lds_store_col(lds, FBM_BLOCK, v);
 }
 
+// x <- x - n if x >= n (28-bit limbs, branch-free); returns whether it subtracted
+template <int L>
+__device__ __forceinline__ uint32_t csub28(uint32_t (&x)[L], const uint32_t (&n)[L]) {
+  uint32_t d[L];
+  int32_t br = 0;
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    const int32_t v = (int32_t)x[k] - (int32_t)n[k] + br;
+    d[k] = (uint32_t)v & FBM_LMASK;
+    br = v >> FBM_LB;
+  }
+  const uint32_t ge = br == 0;
+#pragma unroll
+  for (int k = 0; k < L; ++k) x[k] = ge ? d[k] : x[k];
+  return ge;
+}
+
+// N-adic result (t, s) in the lane's LDS column (t < N + 1, s < 2N: the last product of
+// the exponentiation has a (1, .) operand) -> the canonical residue V = t + s N < N^2,
+// 64 words.  NK: the engine's constants block (N limbs at words 0..9, 16..42).
+__device__ __forceinline__ void na_final(const uint32_t* lds, const uint32_t* NK, uint32_t (&w)[64]) {
+  const uint32_t* nk = launder_s(NK);
+  uint32_t n[FBM_NLN], t[FBM_NLN], sd[FBM_NLN];
+#pragma unroll
+  for (int j = 0; j < FBM_NLN; ++j) n[j] = j < 10 ? nk[j] : nk[6 + j];
+#pragma unroll
+  for (int k = 0; k < FBM_NLN; ++k) {
+    t[k] = lds[k * FBM_BLOCK];
+    sd[k] = lds[(FBM_NLN + k) * FBM_BLOCK];
+  }
+  // t + s N = (t mod N) + N (s + [t >= N])  ->  reduce s + carry mod N
+  uint32_t cy = csub28(t, n);
+  cy += csub28(t, n);  // (a second one only matters for digits >= 2N: none here, kept cheap)
+#pragma unroll
+  for (int k = 0; k < FBM_NLN; ++k) {
+    const uint32_t v = sd[k] + cy;
+    sd[k] = v & FBM_LMASK;
+    cy = v >> FBM_LB;
+  }
+  csub28(sd, n);
+  csub28(sd, n);
+  csub28(sd, n);
+  // V = t + s N by columns (each < 37 products < 2^56 + t limb + carry)
+  uint32_t v28[FBM_NL];
+  uint64_t carry = 0;
+#pragma unroll
+  for (int k = 0; k < FBM_NL; ++k) {
+    uint64_t acc = carry + (k < FBM_NLN ? t[k] : 0u);
+#pragma unroll
+    for (int i = (k < FBM_NLN ? 0 : k - FBM_NLN + 1); i <= (k < FBM_NLN ? k : FBM_NLN - 1); ++i)
+      acc += (uint64_t)n[i] * sd[k - i];
+    v28[k] = (uint32_t)acc & FBM_LMASK;
+    carry = acc >> FBM_LB;
+  }
+  from28<FBM_NL, 64>(v28, w);
+}
+
 // mode 0 (ENC): out[ct] = nude[ct] * H[ct]^key  mod N^2          (ciphertext)
 // mode 1 (DEC): out[ct] = H[ct]^key mod N^2 (plain)                (for the inverse)
-// Sliding window (width FBM_WIN, FBM_TABLE odd powers) over the device copy of the host-built
-// schedule; squarings use the dedicated assembly square (fbm_sq_lds).  Per-lane table:
+// | FBM_EXP_H_NADIC: H rows hold the N-adic digits (h mod N, h div N) of any h < N^2
+//   (jl_split_kernel; the inverse H^-1 of a negative-key encrypt)
+// N-adic engine (fbm_nadic_asm.hpp): a residue is the digit pair (x0, x1), X = x0 + x1 N,
+// 74 limbs = 2 x 37 in the same blocked columns.  Sliding window (width FBM_WIN,
+// FBM_TABLE odd powers) over the device copy of the host-built schedule.  Per-lane table:
 // FBM_TENTRIES blocked columns (the last = h / h^2 scratch).
-//   a = R^2 (uniform), b = h         -> h*R              -> table[0]
-//   a = h*R,  b = a                  -> h^2*R            -> table[16]
-//   a = h^(2t-1)*R, b = table[16]    -> h^(2t+1)*R       -> table[t], t = 1..15
+//   a = R^2 (uniform, N-adic digits), b = (h, 0)  -> h*R              -> table[0]
+//   a = h*R,  squared                              -> h^2*R            -> table[16]
+//   a = h^(2t-1)*R, b = table[16]                  -> h^(2t+1)*R       -> table[t], t = 1..15
 //   a = table[first], then per op: nsq squarings, one product with table[idx]
-//   a = acc,  b = nude | 1           -> c | h^key (plain, lazily reduced) -> csub -> out
+//   a = acc,  b = nude = (1, pt) | 1 = (1, 0)      -> c | h^key (digits) -> t + s N -> out
+// h < 2^1036 (one FDH digest: always, for a 1024-bit N) IS the digit pair (h, 0); a wider h
+// (FDH retries, small moduli) enters as h_lo R + h_hi R^2 (one more product, that wave only).
 // Lanes past n_ct (last chunk) redo the last ciphertext and store nothing.
 __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __restrict__ H, uint64_t n_ct,
-                                                             uint32_t* __restrict__ cst, uint32_t mp,
+                                                             uint32_t* __restrict__ cst, uint32_t np,
                                                              const uint32_t* __restrict__ ops, int n_ops,
                                                              int first, int mode, int key_is_zero,
                                                              const uint32_t* __restrict__ nude,
@@ -380,7 +435,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
   const int tid = threadIdx.x;
   uint32_t* lds = lds_a + tid;
   const uint32_t aoff = lds_addr(lds);
-  const uint32_t* M = cst + FBM_CST_M;
+  const uint32_t* NK = cst + FBM_CST_NK;
   // byte offset of this lane's table entry 0 (entries FBM_NL*256 words apart)
   const uint32_t tb0 = (uint32_t)(((uint64_t)blockIdx.x * FBM_TENTRIES * FBM_NL * FBM_BLOCK + tid) * 4);
   const uint32_t tstride = FBM_NL * FBM_BLOCK * 4;
@@ -399,6 +454,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
     const uint64_t ct_raw = (uint64_t)chunk * FBM_BLOCK + tid;
     const bool valid = ct_raw < n_ct;
     const uint64_t ct = valid ? ct_raw : n_ct - 1;
+    bool wide = false;
     {  // h -> 28-bit limbs -> scratch entry 16
       uint32_t h[64];
       if (key_is_zero) {
@@ -408,19 +464,74 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
         load_row64(H + ct * 64, h);
       }
       uint32_t h28[FBM_NL];
-      to28<64, FBM_NL>(h, h28);
+      if (mode & FBM_EXP_H_NADIC) {  // (h mod N, h div N) as two 1024-bit rows
+        uint32_t d0[32], d1[32], l0[FBM_NLN], l1[FBM_NLN];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+          d0[i] = h[i];
+          d1[i] = h[32 + i];
+        }
+        to28<32, FBM_NLN>(d0, l0);
+        to28<32, FBM_NLN>(d1, l1);
+#pragma unroll
+        for (int k = 0; k < FBM_NLN; ++k) {
+          h28[k] = l0[k];
+          h28[FBM_NLN + k] = l1[k];
+        }
+      } else {  // h = h_lo + h_hi R (R = 2^1036): the 74-limb decomposition is (h_lo, h_hi)
+        to28<64, FBM_NL>(h, h28);
+        uint32_t hi = 0;
+#pragma unroll
+        for (int k = FBM_NLN; k < FBM_NL; ++k) hi |= h28[k];
+        wide = hi != 0u;
+        if (wide) {  // FDH retries (small moduli only): h_hi R^2 = (h_hi, 0) * R^3 R^-1 -> entry 1
+#pragma unroll
+          for (int k = 0; k < FBM_NLN; ++k) {
+            h28[k] = h28[FBM_NLN + k];
+            h28[FBM_NLN + k] = 0u;
+          }
+        }
+      }
       col_store(table + (tb0 + FBM_TSCRATCH * tstride) / 4, h28);
     }
-    lds_store_uniform<FBM_NL>(lds, FBM_BLOCK, cst + FBM_CST_R2);
-    fbm_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, M, mp);  // h*R
+    if (__any(wide)) {  // wave-uniform: lanes with a narrow h multiply 0 and add nothing
+      lds_store_uniform<FBM_NL>(lds, FBM_BLOCK, cst + FBM_CST_R3NA);
+      fbm_na_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, NK, np);  // h_hi*R^2 (wide lanes)
+      lds_to_glb(lds, table + (tb0 + tstride) / 4);
+      uint32_t h[64];
+      load_row64(H + ct * 64, h);
+      uint32_t h28[FBM_NL];
+      to28<64, FBM_NL>(h, h28);
+#pragma unroll
+      for (int k = FBM_NLN; k < FBM_NL; ++k) h28[k] = 0u;  // (h_lo, 0)
+      col_store(table + (tb0 + FBM_TSCRATCH * tstride) / 4, h28);
+    }
+    lds_store_uniform<FBM_NL>(lds, FBM_BLOCK, cst + FBM_CST_R2NA);
+    fbm_na_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, NK, np);  // h*R (narrow) | h_lo*R (wide)
+    if (__any(wide)) {  // h R = h_lo R + h_hi R^2: digit-wise sum (< 6N + 2, fine as an operand)
+      uint32_t a[FBM_NL], b[FBM_NL];
+      lds_load_col(lds, FBM_BLOCK, a);
+      col_load(table + (tb0 + tstride) / 4, b);
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int k = 0; k < FBM_NLN; ++k) {
+          const uint32_t v = a[d * FBM_NLN + k] + (wide ? b[d * FBM_NLN + k] : 0u) + c;
+          a[d * FBM_NLN + k] = v & FBM_LMASK;
+          c = v >> FBM_LB;
+        }
+      }
+      lds_store_col(lds, FBM_BLOCK, a);
+    }
     if (!key_is_zero) {
       lds_to_glb(lds, table + tb0 / 4);
-      fbm_sq_lds(aoff, M, mp);  // h^2*R
+      fbm_na_sq_lds(aoff, NK, np);  // h^2*R
       lds_to_glb(lds, table + (tb0 + FBM_TSCRATCH * tstride) / 4);
       glb_to_lds(table + tb0 / 4, lds);
 #pragma unroll 1
       for (int t = 1; t < FBM_TABLE; ++t) {
-        fbm_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, M, mp);
+        fbm_na_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, NK, np);
         lds_to_glb(lds, table + (tb0 + (uint32_t)t * tstride) / 4);
       }
       glb_to_lds(table + (tb0 + (uint32_t)first * tstride) / 4, lds);
@@ -430,19 +541,16 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
         const int nsq = (int)(op >> FBM_OP_SHIFT);
         const int idx = (int)(op & ((1u << FBM_OP_SHIFT) - 1u)) - 1;
 #pragma unroll 1
-        for (int q = 0; q < nsq; ++q) fbm_sq_lds(aoff, M, mp);
-        if (idx >= 0) fbm_mm_glb(aoff, table, tb0 + (uint32_t)idx * tstride, M, mp);
+        for (int q = 0; q < nsq; ++q) fbm_na_sq_lds(aoff, NK, np);
+        if (idx >= 0) fbm_na_mm_glb(aoff, table, tb0 + (uint32_t)idx * tstride, NK, np);
       }
     }
-    if (mode == 0)
-      fbm_mm_glb(aoff, nude, (uint32_t)((((ct >> 8) * (FBM_NL * 256)) + (ct & 255)) * 4), M, mp);
+    if ((mode & FBM_EXP_DEC) == 0)
+      fbm_na_mm_glb(aoff, nude, (uint32_t)((((ct >> 8) * (FBM_NL * 256)) + (ct & 255)) * 4), NK, np);
     else
-      fbm_mm_glb(aoff, cst + FBM_CST_ONE, 0u, M, mp);
-    uint32_t acc[FBM_NL];
-    lds_load_col(lds, FBM_BLOCK, acc);
-    mont_csub(acc, launder_s(M));
+      fbm_na_mm_glb(aoff, cst + FBM_CST_ONE, 0u, NK, np);
     uint32_t w[64];
-    from28<FBM_NL, 64>(acc, w);
+    na_final(lds, NK, w);
     if (valid) store_row64(out + ct * 64, w);
   }
 }
@@ -561,6 +669,58 @@ __global__ void __launch_bounds__(FBM_BLOCK, 1) jl_emodn_kernel(uint64_t n_ct, J
   uint4* yo = reinterpret_cast<uint4*>(Y + ct * 32);
 #pragma unroll
   for (int i = 0; i < 8; ++i) yo[i] = make_uint4(u[4 * i], u[4 * i + 1], u[4 * i + 2], u[4 * i + 3]);
+}
+
+// N-adic digits of e < N^2 (negative-key encrypt: the inverse H^-1 mod N^2 enters the
+// exponentiation as (e mod N, e div N)); r = Y = e mod N from jl_emodn_kernel, and
+// q = (e - r) / N exactly, as (e - r) * N^-1 mod 2^1024 (q < N).  out [ct][64]: words
+// 0..31 = r, 32..63 = q  (out may alias E: each lane reads its row before writing it).
+__global__ void __launch_bounds__(FBM_BLOCK) jl_split_kernel(uint64_t n_ct, JlParams jp,
+                                                            const uint32_t* E, const uint32_t* __restrict__ Y,
+                                                            uint32_t* out) {
+  const uint64_t ct = (uint64_t)blockIdx.x * FBM_BLOCK + threadIdx.x;
+  if (ct >= n_ct) return;
+  uint32_t e[64], r[32];
+  load_row64(E + ct * 64, e);
+  {
+    const uint4* yi = reinterpret_cast<const uint4*>(Y + ct * 32);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint4 v = yi[i];
+      r[4 * i] = v.x; r[4 * i + 1] = v.y; r[4 * i + 2] = v.z; r[4 * i + 3] = v.w;
+    }
+  }
+  // d = (e - r) mod 2^1024 (only the low half matters for the product mod 2^1024)
+  uint32_t d[32];
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const uint64_t v = (uint64_t)e[i] - r[i] - br;
+    d[i] = (uint32_t)v;
+    br = (uint32_t)(v >> 63);
+  }
+  // q = d * N^-1 mod 2^1024, product scanning over 32-bit words (3-word column sums)
+  uint32_t q[32];
+  uint64_t lo = 0, hi = 0;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+#pragma unroll
+    for (int i = 0; i <= k; ++i) {
+      const uint64_t p = (uint64_t)d[i] * jp.Ninv32[k - i];
+      const uint64_t t = lo + (uint32_t)p;
+      lo = t;
+      hi += (p >> 32);
+    }
+    q[k] = (uint32_t)lo;
+    const uint64_t c = (lo >> 32) + hi;
+    lo = c & 0xffffffffull;
+    hi = c >> 32;
+  }
+  uint4* o = reinterpret_cast<uint4*>(out + ct * 64);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = make_uint4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[8 + i] = make_uint4(q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]);
 }
 
 // stage 1b: y = (e mod N)^-1 mod N in place in Y, by Bernstein-Yang divsteps
@@ -893,12 +1053,16 @@ int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stat
 // memory for the exp kernel, which indexes it dynamically; M and R^2 for the scalar
 // loads of the assembly product; broadcast columns of 1 and R^2 (limb k at word k*256,
 // read by every lane at offset 0).
-__global__ void jl_setup_kernel(JlSched sc, MontCtx mc, uint32_t* __restrict__ ops, uint32_t* __restrict__ cst) {
+__global__ void jl_setup_kernel(JlSched sc, MontCtx mc, NadicCtx na, uint32_t* __restrict__ ops,
+                                uint32_t* __restrict__ cst) {
   const int t = threadIdx.x;
   for (int i = t; i < sc.n_ops; i += blockDim.x) ops[i] = sc.op[i];
   if (t < 128) {
     cst[FBM_CST_M + t] = t < FBM_NL ? mc.M[t] : 0u;
     cst[FBM_CST_R2 + t] = t < FBM_NL ? mc.R2[t] : 0u;
+    cst[FBM_CST_NK + t] = t < 80 ? na.nk[t] : 0u;
+    cst[FBM_CST_R2NA + t] = t < FBM_NL ? na.r2na[t] : 0u;
+    cst[FBM_CST_R3NA + t] = t < FBM_NL ? na.r3na[t] : 0u;
   }
   for (int i = t; i < FBM_NL * 256; i += blockDim.x) {
     const int k = i >> 8, l = i & 255;
@@ -908,7 +1072,7 @@ __global__ void jl_setup_kernel(JlSched sc, MontCtx mc, uint32_t* __restrict__ o
 }
 
 int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32_t* cst, hipStream_t s) {
-  hipLaunchKernelGGL(jl_setup_kernel, dim3(1), dim3(256), 0, s, sc, jp.mc, ops, cst);
+  hipLaunchKernelGGL(jl_setup_kernel, dim3(1), dim3(256), 0, s, sc, jp.mc, jp.na, ops, cst);
   return check_launch("jl_setup_kernel");
 }
 
@@ -919,7 +1083,7 @@ int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const Jl
   uint64_t g = (n_ct + FBM_BLOCK - 1) / FBM_BLOCK;
   const uint64_t gmax = table_slots / FBM_BLOCK;
   if (g > gmax) g = gmax;
-  hipLaunchKernelGGL(jl_exp_kernel, dim3((unsigned)g), dim3(FBM_BLOCK), 0, s, H, n_ct, (uint32_t*)cst, jp.mc.mp, ops, sc.n_ops,
+  hipLaunchKernelGGL(jl_exp_kernel, dim3((unsigned)g), dim3(FBM_BLOCK), 0, s, H, n_ct, (uint32_t*)cst, jp.mn.mp, ops, sc.n_ops,
                      sc.first, mode, jp.key_is_zero, nude, table, out);
   return check_launch("jl_exp_kernel");
 }
@@ -943,6 +1107,16 @@ int launch_jl_inv(uint64_t n_ct, const JlParams& jp, const uint32_t* E, uint32_t
   if (rc) return rc;
   hipLaunchKernelGGL(jl_inv_lift_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, E, Y, inv);
   return check_launch("jl_inv_lift_kernel");
+}
+
+int launch_jl_nadic_split(uint64_t n_ct, const JlParams& jp, const uint32_t* E, uint32_t* Y, uint32_t* out,
+                          hipStream_t s) {
+  if (n_ct == 0) return FBM_OK;
+  hipLaunchKernelGGL(jl_emodn_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, E, Y);
+  int rc = check_launch("jl_emodn_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(jl_split_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, E, Y, out);
+  return check_launch("jl_split_kernel");
 }
 
 int launch_jl_fin(uint64_t n_ct, const JlParams& jp, const uint32_t* X, const uint32_t* inv, uint32_t* xout,

@@ -182,11 +182,18 @@ int fbm_ass_reconstruct_wide(const uint32_t* shares, int n_shares, int l, uint64
 /* Sliding-window width of the JL exponentiation (odd-power table of 2^(w-1) entries); lets the
  * bench count the products one ciphertext costs (its VALU roofline). */
 int fbm_jl_window(void);
+/* v_mad_u64_u32 per lane of one product of the JL exponentiation engine (N-adic Montgomery
+ * product modulo N^2, fedbiomed_amd/csrc/fbm_nadic_asm.hpp): square != 0 -> a squaring. */
+int fbm_jl_mads(int square);
 
 /* ---- host test hook (no GPU): the device modular-inverse routine (Bernstein-Yang divsteps,
  * fedbiomed_amd/csrc/fbm_safegcd.hpp) run on the host, for unit tests.
  * x, n, out: 32 little-endian words (n odd);  batches: number of 30-divstep batches used. */
 int fbm_test_modinv(const uint32_t* x, const uint32_t* n, uint32_t* out, int* batches);
+/* host test hook (no GPU): the N-adic engine's per-modulus constants as the library builds
+ * them -- nk: 80 words (N limbs, K'_i), r2na / r3na: 74 limbs (digits of R^2 / R^3 mod N^2,
+ * R = 2^1036), np = -N^-1 mod 2^28. */
+int fbm_test_nadic_consts(const uint32_t* n32, uint32_t* nk, uint32_t* r2na, uint32_t* r3na, uint32_t* np);
 
 /* ---- instrumentation -------------------------------------------------------------------
  * fbm_prof_enable(1) makes every entry point record a HIP event pair around each kernel

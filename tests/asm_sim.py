@@ -1,0 +1,142 @@
+"""Single-lane interpreter for the generated gfx950 assembly products (test infrastructure).
+
+Runs the instruction list a generator (tools/gen_nadic_asm.py) emits for ONE lane, with
+LDS / global memory / the scalar constants block as dictionaries, so the register plan,
+offsets, loop control and arithmetic of the assembly can be checked on the CPU against
+Python integers before it ever runs on a GPU.  Only the instructions the generators use
+are implemented; anything else raises.
+"""
+
+import re
+
+M32 = (1 << 32) - 1
+M64 = (1 << 64) - 1
+_PAIR = re.compile(r"^([vs])\[(\d+):(\d+)\]$")
+_ONE = re.compile(r"^([vs])(\d+)$")
+
+
+class Lane:
+    def __init__(self, args, lds=None, glb=None, smem=None):
+        self.r = {}
+        self.args = args            # placeholder name -> int value (addresses, scalars)
+        self.lds = lds if lds is not None else {}
+        self.glb = glb if glb is not None else {}
+        self.smem = smem if smem is not None else {}
+        self.scc = 0
+        self.m0 = 0
+
+    # -- operands -------------------------------------------------------------------------
+    def _sub(self, tok):
+        m = re.fullmatch(r"%\[(\w+)\]", tok)
+        return ("arg", m.group(1)) if m else None
+
+    def get(self, tok, width=32):
+        a = self._sub(tok)
+        if a:
+            return self.args[a[1]]
+        if tok in ("vcc",):
+            return 0
+        if tok == "m0":
+            return self.r["m0"]
+        m = _PAIR.match(tok)
+        if m:
+            k, lo, hi = m.group(1), int(m.group(2)), int(m.group(3))
+            v = 0
+            for i in range(hi, lo - 1, -1):
+                v = (v << 32) | self.r.get(f"{k}{i}", 0)
+            return v
+        m = _ONE.match(tok)
+        if m:
+            if tok not in self.r:
+                raise KeyError(f"read of unwritten register {tok}")
+            return self.r[tok]
+        return int(tok, 0)
+
+    def put(self, tok, val):
+        if tok == "m0":
+            self.r["m0"] = val & M32
+            return
+        m = _PAIR.match(tok)
+        if m:
+            k, lo, hi = m.group(1), int(m.group(2)), int(m.group(3))
+            for i in range(lo, hi + 1):
+                self.r[f"{k}{i}"] = val & M32
+                val >>= 32
+            return
+        if _ONE.match(tok):
+            self.r[tok] = val & M32
+            return
+        raise ValueError(f"bad destination {tok}")
+
+    # -- execution ------------------------------------------------------------------------
+    def run(self, lines, max_steps=10_000_000):
+        prog, labels = [], {}
+        for ln in lines:
+            ln = ln.strip()
+            if ln.endswith(":"):
+                labels[ln[:-1]] = len(prog)
+                continue
+            prog.append(ln)
+        pc, steps, counts = 0, 0, {}
+        while pc < len(prog):
+            steps += 1
+            if steps > max_steps:
+                raise RuntimeError("step cap")
+            ln = prog[pc]
+            pc += 1
+            op, _, rest = ln.partition(" ")
+            counts[op] = counts.get(op, 0) + 1
+            ops = [t.strip() for t in rest.split(",")] if rest else []
+            off = 0
+            if ops and "offset:" in ops[-1]:
+                last, _, o = ops[-1].partition("offset:")
+                off = int(o, 0)
+                ops[-1] = last.strip()
+            if op in ("s_waitcnt", "s_nop"):
+                continue
+            if op.startswith("s_load_dword"):
+                n = {"s_load_dwordx2": 2, "s_load_dwordx8": 8, "s_load_dwordx16": 16}[op]
+                m = _PAIR.match(ops[0])
+                base = self.get(ops[1]) + int(ops[2], 0)
+                for i in range(n):
+                    self.r[f"s{int(m.group(2)) + i}"] = self.smem[base + 4 * i]
+            elif op == "global_load_dword":
+                addr = self.get(ops[2]) + self.get(ops[1]) + off
+                self.put(ops[0], self.glb[addr])
+            elif op == "ds_read_b32":
+                addr = self.get(ops[1]) + off
+                self.put(ops[0], self.lds.get(addr, 0))
+            elif op == "ds_write_b32":
+                addr = self.get(ops[0]) + off
+                self.lds[addr] = self.get(ops[1])
+            elif op in ("v_mov_b32", "s_mov_b32"):
+                self.put(ops[0], self.get(ops[1]))
+            elif op in ("v_add_u32", "s_add_u32"):
+                self.put(ops[0], self.get(ops[1]) + self.get(ops[2]))
+            elif op == "v_sub_u32":
+                self.put(ops[0], self.get(ops[1]) - self.get(ops[2]))
+            elif op == "v_and_b32":
+                self.put(ops[0], self.get(ops[1]) & self.get(ops[2]))
+            elif op == "v_mul_lo_u32":
+                self.put(ops[0], self.get(ops[1]) * self.get(ops[2]))
+            elif op == "v_lshlrev_b32":
+                self.put(ops[0], self.get(ops[2]) << self.get(ops[1]))
+            elif op == "v_mad_u64_u32":
+                a, b = self.get(ops[2]), self.get(ops[3])
+                assert a <= M32 and b <= M32
+                self.put(ops[0], (a * b + self.get(ops[4], 64)) & M64)
+            elif op == "v_lshrrev_b64":
+                self.put(ops[0], self.get(ops[2], 64) >> self.get(ops[1]))
+            elif op == "v_lshl_add_u64":
+                self.put(ops[0], ((self.get(ops[1], 64) << self.get(ops[2])) + self.get(ops[3], 64)) & M64)
+            elif op == "s_movrels_b32":
+                m = _ONE.match(ops[1])
+                self.put(ops[0], self.r[f"s{int(m.group(2)) + self.r['m0']}"])
+            elif op == "s_cmp_lg_u32":
+                self.scc = int(self.get(ops[0]) != self.get(ops[1]))
+            elif op == "s_cbranch_scc1":
+                if self.scc:
+                    pc = labels[ops[0].rstrip("bf")]
+            else:
+                raise NotImplementedError(op)
+        return counts

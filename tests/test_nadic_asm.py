@@ -1,0 +1,167 @@
+"""The generated N-adic assembly product (fedbiomed_amd/csrc/fbm_nadic_asm.hpp, from
+tools/gen_nadic_asm.py), run instruction by instruction for one lane on the CPU
+(tests/asm_sim.py), against Python integers: X*Y*R^-1 mod N^2 for digits < 2N (and the
+one-off operand shapes the exponentiation uses), digits staying < 2N."""
+
+import importlib.util
+import os
+import random
+
+import pytest
+
+from tests.asm_sim import Lane  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LB, L = 28, 37
+MASK = (1 << LB) - 1
+R = 1 << (LB * L)
+
+
+def _gen():
+    spec = importlib.util.spec_from_file_location("gen_nadic_asm", os.path.join(ROOT, "tools", "gen_nadic_asm.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+GEN = _gen()
+MM, SQ = GEN.product(False), GEN.product(True)
+
+
+def limbs(x, n=L):
+    return [(x >> (LB * k)) & MASK for k in range(n)]
+
+
+def consts(N):
+    """80-word constants block: N_0..N_9 at words 0..9, N_10..N_36 and K'_0..K'_36 at 16..79
+    (the layout fbm_capi.hip's host setup writes)."""
+    K = (1 - R) % N
+    kp = [MASK + v for v in limbs(K)]
+    nl = limbs(N)
+    words = [0] * 80
+    words[0:10] = nl[0:10]
+    words[16:16 + 27] = nl[10:37]
+    words[43:80] = kp
+    np_ = (-pow(N, -1, 1 << LB)) % (1 << LB)
+    return words, np_
+
+
+def run(N, a, b=None):
+    """a, b: (digit0, digit1) pairs; b None = square.  Returns the result digits."""
+    words, np_ = consts(N)
+    NK, BB = 0x4000, 0x100000
+    smem = {NK + 4 * i: w for i, w in enumerate(words)}
+    lds = {}
+    for k, v in enumerate(limbs(a[0]) + limbs(a[1])):
+        lds[k * 1024] = v
+    glb = {}
+    if b is not None:
+        for k, v in enumerate(limbs(b[0]) + limbs(b[1])):
+            glb[BB + k * 1024] = v
+    lane = Lane({"a": 0, "b": 0, "bb": BB, "NK": NK, "np": np_}, lds=lds, glb=glb, smem=smem)
+    counts = lane.run(MM if b is not None else SQ)
+    out = [lds[k * 1024] for k in range(2 * L)]
+    assert all(v <= MASK for v in out)
+    d0 = sum(v << (LB * k) for k, v in enumerate(out[:L]))
+    d1 = sum(v << (LB * k) for k, v in enumerate(out[L:]))
+    return d0, d1, counts
+
+
+def _rand_n(rng, bits):
+    return rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+
+
+@pytest.mark.parametrize("bits", [24, 1024])
+def test_nadic_asm_product_and_square(bits):
+    rng = random.Random(bits)
+    N = _rand_n(rng, bits)
+    M = N * N
+    rinv = pow(R, -1, M)
+    for trial in range(3):
+        a = (rng.randrange(2 * N), rng.randrange(2 * N))
+        b = (rng.randrange(2 * N), rng.randrange(2 * N))
+        if trial == 0:
+            a, b = (2 * N - 1, 2 * N - 1), (2 * N - 1, 2 * N - 1)
+        A, B = (a[0] + a[1] * N) % M, (b[0] + b[1] * N) % M
+        t, s, counts = run(N, a, b)
+        assert (t + s * N) % M == A * B * rinv % M
+        assert t < 2 * N and s < 2 * N
+        assert counts["v_mad_u64_u32"] == 37 * 186
+        t, s, counts = run(N, a)
+        assert (t + s * N) % M == A * A * rinv % M
+        assert t < 2 * N and s < 2 * N
+        assert counts["v_mad_u64_u32"] == 37 * 149
+
+
+def test_nadic_asm_wide_operands():
+    """(h, 0) with h < R (the FDH digest entering the exponentiation) and (1, pt) with
+    pt < 2^1024 (N*pt + 1): results stay exact, digits < 3N + 1."""
+    rng = random.Random(5)
+    for bits in (24, 1024):
+        N = _rand_n(rng, bits)
+        M = N * N
+        rinv = pow(R, -1, M)
+        h = rng.getrandbits(1036)
+        r2 = (R * R) % M
+        a = (r2 % N, r2 // N)
+        t, s, _ = run(N, a, (h, 0))
+        assert (t + s * N) % M == h * R % M
+        assert t < 3 * N + 1 and s < 3 * N + 1
+        pt = rng.getrandbits(1024)
+        x = (rng.randrange(2 * N), rng.randrange(2 * N))
+        t, s, _ = run(N, x, (1, pt))
+        assert (t + s * N) % M == (x[0] + x[1] * N) * (1 + N * pt) * rinv % M
+
+
+def test_library_constants_match_and_drive_the_asm():
+    """The constants the library builds on the host (fbm_test_nadic_consts: N limbs, K'_i,
+    R^2 / R^3 digits, np) equal the formulas above, and a short square-and-multiply chain of the
+    simulated assembly on them gives h^e mod N^2 for the default biprime."""
+    import numpy as np
+
+    from fedbiomed_amd import _build, _native, workload as W
+
+    _build.build()
+    lib = _native.load()
+    for N in (W.BIPRIME0, 0xC9F2B5, (1 << 1023) + 12345677):
+        n32 = np.frombuffer(N.to_bytes(128, "little"), dtype=np.uint32).copy()
+        nk = np.zeros(80, np.uint32)
+        r2 = np.zeros(74, np.uint32)
+        r3 = np.zeros(74, np.uint32)
+        npv = np.zeros(1, np.uint32)
+        assert lib.fbm_test_nadic_consts(n32.ctypes.data, nk.ctypes.data, r2.ctypes.data, r3.ctypes.data,
+                                         npv.ctypes.data) == 0
+        words, np_ = consts(N)
+        assert [int(v) for v in nk] == words
+        assert int(npv[0]) == np_
+        for e, got in ((2, r2), (3, r3)):
+            u = pow(R, e, N * N)
+            assert [int(v) for v in got] == limbs(u % N) + limbs(u // N)
+    # h^e mod N^2 through the simulated engine, as jl_exp_kernel sequences it (binary method)
+    N = W.BIPRIME0
+    M = N * N
+    rng = random.Random(9)
+    h, e = rng.getrandbits(256), rng.getrandbits(12) | (1 << 11)
+    u = (R * R) % M
+    x = run(N, (u % N, u // N), (h, 0))[:2]          # h R
+    hr = x
+    for bit in bin(e)[3:]:
+        x = run(N, x)[:2]
+        if bit == "1":
+            x = run(N, x, hr)[:2]
+    # a wide h (FDH retries on a small modulus): h R = h_lo R + h_hi R^2, summed digit-wise
+    Ns = 0xC9F2B5
+    Ms = Ns * Ns
+    hw = rng.getrandbits(1792)
+    hl, hh = hw % R, hw // R
+    u2, u3 = pow(R, 2, Ms), pow(R, 3, Ms)
+    lo = run(Ns, (u2 % Ns, u2 // Ns), (hl, 0))[:2]
+    hi = run(Ns, (u3 % Ns, u3 // Ns), (hh, 0))[:2]
+    s0, s1 = lo[0] + hi[0], lo[1] + hi[1]
+    assert (s0 + s1 * Ns) % Ms == hw * R % Ms and s0 < 6 * Ns + 2 and s1 < 6 * Ns + 2
+    sq = run(Ns, (s0, s1))[:2]
+    assert (sq[0] + sq[1] * Ns) % Ms == hw * hw * R % Ms
+    pt = rng.getrandbits(1000)
+    t, s, _ = run(N, x, (1, pt))                       # * (N pt + 1), drops R
+    assert (t + s * N) % M == (1 + N * pt) * pow(h, e, M) % M
+    assert t <= N and s < 2 * N

@@ -1,0 +1,287 @@
+#!/usr/bin/env python3
+"""Generate fedbiomed_amd/csrc/fbm_nadic_asm.hpp: the gfx950 assembly Montgomery product
+modulo N^2 in N-adic form (the Joye-Libert exponentiation engine).
+
+Why N-adic: the JL modulus is N^2 with N known (1024-bit biprime).  A residue X mod N^2 is
+carried as two 37-limb digits (x0, x1), X = x0 + x1 N (mod N^2), and since N^2 = 0 the
+product needs no x1*y1 term:
+
+    X Y = x0 y0 + N (x0 y1 + x1 y0)                      (mod N^2)
+
+With R = 2^1036 (37 limbs of 28 bits) and one Montgomery reduction modulo N of x0 y0,
+x0 y0 + m N = t R  (m = the reduction's quotient digits), we get N R^-1 = N (R^-1 mod N)
+(mod N^2) and therefore
+
+    X Y R^-1 = t + N * REDC_N(x0 y1 + x1 y0 - m)          (mod N^2)
+
+i.e. the Montgomery product modulo N^2 is two interleaved Montgomery products modulo N
+that share their row loop: the t part reduces x0*y0 and hands its quotient digit q_i of
+row i straight to the s part, which adds (K'_i - q_i) in that row's retiring column.
+-m is taken as (R - 1 - m) + K with K = (1 - R) mod N, so every column stays non-negative:
+K'_i = (2^28 - 1) + K_i (host constants).  Per product 37 rows x (37 + 37 + 74 + 37)
+= 6 845 v_mad_u64_u32 (square: x0*x0 and x0*(2 x1): 5 476) against 10 952 / 8 288 for
+the 74-limb Montgomery product modulo N^2 (fbm_mont_asm.hpp) -- the same arithmetic
+result class at 0.63x / 0.66x of the multiplies.
+
+Bounds (N < 2^1024, R = 2^1036 >= 2^12 N): digits < 2N in -> digits < 2N out
+(t < N + 4N^2/R, s < N + 1 + (8N^2 + N)/R).  A digit up to R - 1 in one operand (the
+hash h < 2^1036 entering as (h, 0), the plaintext digit of N*pt + 1 = (1, pt)) gives
+digits < 3N + 1, which the next product brings back below 2N.  Columns: at most
+111 products < 2^56 plus carries: < 2^63.
+
+Register plan (per lane, wave64):
+  v[2k:2k+1]      k=0..35  t-window accumulators At_k (64-bit)
+  v[72+2k:73+2k]  k=0..35  s-window accumulators As_k
+  v144..v180      B digit 0 limbs b0_j   (square: x0)
+  v181..v217      B digit 1 limbs b1_j   (square: 2 x1, 29-bit limbs)
+  v218, v219      x0_i, x1_i of the current row;  v220, v221 the next row's (prefetch)
+  v[222:223]      Tt = retiring column of the t part;  v[224:225] Ts (s part)
+  v226 q, v227 q', v228 np = -N^-1 mod 2^28, v229 LDS address of x0_i, v230 scratch,
+  v231 K'_i - q
+  s20..s29, s36..s62   N_0..N_9, N_10..N_36 (uniform, loaded once per product)
+  s63..s99             K'_0..K'_36 (row i reads K'_i by s_movrels with m0 = i)
+  s34 row counter, s35 K'_i;  vcc: unused carry-out of v_mad_u64_u32;  scc, m0 clobbered.
+
+Operands: A is the lane's LDS column (limb k of the 74 at byte a_off + k*1024: rows 0..36
+digit 0, rows 37..73 digit 1; 75 rows allocated, the last row's prefetch reads row 74)
+and receives the result; B comes from global memory (uniform base + per-lane byte offset,
+limb stride 1024 B: the workgroup-blocked layout of tables and residue columns) or, for
+the square, from the A column itself.  The constants block (80 words, see
+NadicCtx in fbm_internal.hpp) holds N_0..N_9 at words 0..9 and
+N_10..N_36, K'_0..K'_36 at words 16..79.
+
+Usage:  python tools/gen_nadic_asm.py   (rewrites the header; the build does not run this)
+"""
+
+import os
+
+L = 37
+NW = L - 1  # window accumulators per part
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "fedbiomed_amd", "csrc", "fbm_nadic_asm.hpp")
+MASK = "0xfffffff"
+
+
+def At(k):
+    return f"v[{2 * k}:{2 * k + 1}]"
+
+
+def AtLo(k):
+    return f"v{2 * k}"
+
+
+def As(k):
+    return f"v[{72 + 2 * k}:{73 + 2 * k}]"
+
+
+def AsLo(k):
+    return f"v{72 + 2 * k}"
+
+
+def B0(j):
+    return f"v{144 + j}"
+
+
+def B1(j):
+    return f"v{181 + j}"
+
+
+def Ns(j):
+    return f"s{20 + j}" if j < 10 else f"s{36 + j - 10}"
+
+
+KBASE = "s63"
+X0, X1, X0N, X1N = "v218", "v219", "v220", "v221"
+TT, TTLO, TS, TSLO = "v[222:223]", "v222", "v[224:225]", "v224"
+Q, Q2, NPV, AADR, TMP, CQ = "v226", "v227", "v228", "v229", "v230", "v231"
+ROW1 = 37 * 1024  # byte offset of digit 1 in the LDS column
+
+
+def load_consts():
+    return [
+        "s_load_dwordx8 s[20:27], %[NK], 0x0",
+        "s_load_dwordx2 s[28:29], %[NK], 0x20",
+        "s_load_dwordx16 s[36:51], %[NK], 0x40",
+        "s_load_dwordx16 s[52:67], %[NK], 0x80",
+        "s_load_dwordx16 s[68:83], %[NK], 0xc0",
+        "s_load_dwordx16 s[84:99], %[NK], 0x100",
+    ]
+
+
+def breg(j):
+    return B0(j) if j < L else B1(j - L)
+
+
+def load_b_global():
+    # the caller may just have stored this column (same lane): drain stores before loading
+    out = ["s_waitcnt vmcnt(0)", f"v_mov_b32 {TMP}, %[b]"]
+    for j in range(2 * L):
+        if j and j % 4 == 0:
+            out.append(f"v_add_u32 {TMP}, 0x1000, {TMP}")
+        out.append(f"global_load_dword {breg(j)}, {TMP}, %[bb] offset:{(j % 4) * 1024}")
+    return out
+
+
+def load_b_square():
+    out = [f"v_add_u32 {TMP}, 0x10000, %[a]"]
+    for j in range(2 * L):
+        if j < 64:
+            out.append(f"ds_read_b32 {breg(j)}, %[a] offset:{j * 1024}")
+        else:
+            out.append(f"ds_read_b32 {breg(j)}, {TMP} offset:{(j - 64) * 1024}")
+    out.append("s_waitcnt lgkmcnt(0)")
+    out += [f"v_lshlrev_b32 {B1(j)}, 1, {B1(j)}" for j in range(L)]
+    return out
+
+
+def row(first, sq):
+    """One row i of the fused t/s product.  x0_i (and x1_i) are in X0 (X1); s35 = K'_i."""
+    out = [f"ds_read_b32 {X0N}, {AADR} offset:1024"]
+    if not sq:
+        out.append(f"ds_read_b32 {X1N}, {AADR} offset:{ROW1 + 1024}")
+    kreg = KBASE if first else "s35"
+    # ---- t part: x0_i * b0, quotient q, q * N ----
+    out.append(f"v_mad_u64_u32 {TT}, vcc, {X0}, {B0(0)}, {'0' if first else At(0)}")
+    for j in range(1, L):
+        addend = "0" if (first or j == NW) else At(j)
+        out.append(f"v_mad_u64_u32 {At(j - 1)}, vcc, {X0}, {B0(j)}, {addend}")
+        if j == 3:
+            out.append(f"v_mul_lo_u32 {Q}, {TTLO}, {NPV}")
+        if j == 6:
+            out.append(f"v_and_b32 {Q}, {MASK}, {Q}")
+        if j == 8:
+            out.append(f"v_sub_u32 {CQ}, {kreg}, {Q}")  # K'_i - q_i  (>= 0: K'_i >= 2^28 - 1)
+    out.append(f"v_mad_u64_u32 {TT}, vcc, {Q}, {Ns(0)}, {TT}")
+    for j in range(1, L):
+        out.append(f"v_mad_u64_u32 {At(j - 1)}, vcc, {Q}, {Ns(j)}, {At(j - 1)}")
+    # ---- s part: x0_i * b1 (+ x1_i * b0), + (K'_i - q_i), quotient q', q' * N ----
+    out.append(f"v_mad_u64_u32 {TS}, vcc, {X0}, {B1(0)}, {'0' if first else As(0)}")
+    for j in range(1, L):
+        addend = "0" if (first or j == NW) else As(j)
+        out.append(f"v_mad_u64_u32 {As(j - 1)}, vcc, {X0}, {B1(j)}, {addend}")
+        if j == 12:
+            out.append(f"v_mad_u64_u32 {TS}, vcc, {CQ}, 1, {TS}")
+        if not sq and j == 24:
+            out.append(f"v_mad_u64_u32 {TS}, vcc, {X1}, {B0(0)}, {TS}")
+        if sq and j == 20:
+            out.append(f"v_mul_lo_u32 {Q2}, {TSLO}, {NPV}")
+        if sq and j == 26:
+            out.append(f"v_and_b32 {Q2}, {MASK}, {Q2}")
+    if not sq:
+        for j in range(1, L):
+            out.append(f"v_mad_u64_u32 {As(j - 1)}, vcc, {X1}, {B0(j)}, {As(j - 1)}")
+            if j == 3:
+                out.append(f"v_mul_lo_u32 {Q2}, {TSLO}, {NPV}")
+            if j == 6:
+                out.append(f"v_and_b32 {Q2}, {MASK}, {Q2}")
+    out.append(f"v_mad_u64_u32 {TS}, vcc, {Q2}, {Ns(0)}, {TS}")
+    for j in range(1, L):
+        out.append(f"v_mad_u64_u32 {As(j - 1)}, vcc, {Q2}, {Ns(j)}, {As(j - 1)}")
+    # ---- retire column i of both parts ----
+    out += [f"v_lshrrev_b64 {TT}, 28, {TT}", f"v_lshl_add_u64 {At(0)}, {TT}, 0, {At(0)}",
+            f"v_lshrrev_b64 {TS}, 28, {TS}", f"v_lshl_add_u64 {As(0)}, {TS}, 0, {As(0)}",
+            f"v_add_u32 {AADR}, 0x400, {AADR}", "s_waitcnt lgkmcnt(0)", f"v_mov_b32 {X0}, {X0N}"]
+    if not sq:
+        out.append(f"v_mov_b32 {X1}, {X1N}")
+    return out
+
+
+def normalise_store():
+    out = [f"v_add_u32 {TMP}, 0x10000, %[a]"]
+
+    def st(k, reg):
+        if k < 64:
+            return f"ds_write_b32 %[a], {reg} offset:{k * 1024}"
+        return f"ds_write_b32 {TMP}, {reg} offset:{(k - 64) * 1024}"
+
+    for acc, lo, carry, carry_lo, base in ((At, AtLo, TT, TTLO, 0), (As, AsLo, TS, TSLO, L)):
+        out += [f"v_lshrrev_b64 {carry}, 28, {acc(0)}", f"v_and_b32 {lo(0)}, {MASK}, {lo(0)}", st(base, lo(0))]
+        for k in range(1, NW):
+            out += [f"v_lshl_add_u64 {acc(k)}, {carry}, 0, {acc(k)}",
+                    f"v_lshrrev_b64 {carry}, 28, {acc(k)}",
+                    f"v_and_b32 {lo(k)}, {MASK}, {lo(k)}",
+                    st(base + k, lo(k))]
+        out.append(st(base + NW, carry_lo))
+    out.append("s_waitcnt lgkmcnt(0)")
+    return out
+
+
+def product(sq):
+    body = load_consts()
+    body += load_b_square() if sq else load_b_global()
+    body += [f"v_mov_b32 {NPV}, %[np]", f"v_mov_b32 {AADR}, %[a]", f"ds_read_b32 {X0}, {AADR}"]
+    if not sq:
+        body.append(f"ds_read_b32 {X1}, {AADR} offset:{ROW1}")
+    body += ["s_waitcnt vmcnt(0) lgkmcnt(0)"]
+    body += row(True, sq)
+    # s_movrels after an SALU write of m0 needs a wait state (the hazard is not checked in asm)
+    body += ["s_mov_b32 s34, 1", "1:", "s_mov_b32 m0, s34", "s_nop 1", f"s_movrels_b32 s35, {KBASE}"]
+    body += row(False, sq)
+    body += ["s_add_u32 s34, s34, 1", f"s_cmp_lg_u32 s34, {L}", "s_cbranch_scc1 1b"]
+    body += normalise_store()
+    return body
+
+
+def clobbers():
+    regs = [f'"v{i}"' for i in range(232)]
+    regs += [f'"s{i}"' for i in list(range(20, 30)) + [34, 35] + list(range(36, 100))]
+    out = [", ".join(regs[i:i + 16]) for i in range(0, len(regs), 16)]
+    return " \\\n  ".join(x + "," for x in out[:-1]) + " \\\n  " + out[-1]
+
+
+def c_string(lines):
+    return "\n".join(f'  "{ln}\\n"' for ln in lines)
+
+
+def count_mads(lines):
+    return sum(1 for ln in lines if ln.startswith("v_mad_u64_u32"))
+
+
+def main():
+    mm, sq = product(False), product(True)
+    mm_row, sq_row = row(False, False), row(False, True)
+    hdr = f"""// GENERATED by tools/gen_nadic_asm.py -- do not edit by hand.
+//
+// gfx950 assembly Montgomery product modulo N^2 in N-adic form: a residue is two 37-limb
+// digits (x0, x1), X = x0 + x1 N (mod N^2), radix 2^28, R = 2^1036.
+//   a (per-lane LDS column, 74 limbs) <- a * b * R^-1 (mod N^2), digits lazily < 2N.
+// See tools/gen_nadic_asm.py for the arithmetic, the bounds and the register plan.
+// {len(mm)} instructions (general, B from global), {len(sq)} (square); row loop bodies
+// {len(mm_row)} / {len(sq_row)} instructions with {count_mads(mm_row)} / {count_mads(sq_row)} v_mad_u64_u32.
+#pragma once
+#include <stdint.h>
+
+#define FBM_NA_MADS_MUL {L * count_mads(mm_row)}
+#define FBM_NA_MADS_SQR {L * count_mads(sq_row)}
+
+#define FBM_NA_CLOBBERS \\
+  {clobbers()}
+
+// B operand from global memory: limb k at bb + b_off + k*1024 (bytes; bb uniform).
+// NK: the 80-word constants block (N limbs, K'_i); np = -N^-1 mod 2^28.
+__device__ __forceinline__ void fbm_na_mm_glb(uint32_t a_off, const uint32_t* bb, uint32_t b_off,
+                                              const uint32_t* NK, uint32_t np) {{
+  asm volatile(
+{c_string(mm)}
+      :
+      : [a] "v"(a_off), [b] "v"(b_off), [bb] "s"(bb), [NK] "s"(NK), [np] "s"(np)
+      : "memory", "vcc", "scc", "m0", FBM_NA_CLOBBERS);
+}}
+
+// a <- a^2 R^-1 (mod N^2).
+__device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK, uint32_t np) {{
+  asm volatile(
+{c_string(sq)}
+      :
+      : [a] "v"(a_off), [NK] "s"(NK), [np] "s"(np)
+      : "memory", "vcc", "scc", "m0", FBM_NA_CLOBBERS);
+}}
+"""
+    with open(OUT, "w") as f:
+        f.write(hdr)
+    print(f"wrote {OUT}: general {len(mm)} / square {len(sq)} instructions; "
+          f"mads/product {L * count_mads(mm_row)} / {L * count_mads(sq_row)}")
+
+
+if __name__ == "__main__":
+    main()
