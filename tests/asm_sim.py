@@ -15,6 +15,17 @@ _PAIR = re.compile(r"^([vs])\[(\d+):(\d+)\]$")
 _ONE = re.compile(r"^([vs])(\d+)$")
 
 
+def _size(ln):
+    """Encoded size in bytes (gfx9): VOP3 / DS / FLAT / SMEM 8, VOP2 / SOP 4, +4 for a literal."""
+    op, _, rest = ln.partition(" ")
+    ops = [t.strip() for t in rest.split(",")] if rest else []
+    if op.startswith(("v_mad", "v_mul_lo", "v_lshrrev_b64", "v_lshl_add", "ds_", "global_", "s_load")):
+        return 8
+    lit = any(re.fullmatch(r"0x[0-9a-f]+|\d+", t) and int(t, 0) > 64 for t in ops[1:]) or any(
+        t.startswith(".L") for t in ops)
+    return 4 + (4 if lit else 0)
+
+
 class Lane:
     def __init__(self, args, lds=None, glb=None, smem=None):
         self.r = {}
@@ -68,15 +79,28 @@ class Lane:
             return
         raise ValueError(f"bad destination {tok}")
 
+    def _expr(self, tok):
+        """operand or a label difference '.La - .Lb' (byte distance, as the assembler resolves it)"""
+        m = re.fullmatch(r"(\.[\w%=]+)\s*-\s*(\.[\w%=]+)", tok)
+        if m:
+            return self._byte_labels[m.group(1)] - self._byte_labels[m.group(2)]
+        return self.get(tok)
+
     # -- execution ------------------------------------------------------------------------
     def run(self, lines, max_steps=10_000_000):
-        prog, labels = [], {}
+        prog, labels, baddr, byte_labels = [], {}, [], {}
+        pos = 0
         for ln in lines:
             ln = ln.strip()
             if ln.endswith(":"):
                 labels[ln[:-1]] = len(prog)
+                byte_labels[ln[:-1]] = pos
                 continue
             prog.append(ln)
+            baddr.append(pos)
+            pos += _size(ln)
+        at = {a: i for i, a in enumerate(baddr)}
+        self._byte_labels = byte_labels
         pc, steps, counts = 0, 0, {}
         while pc < len(prog):
             steps += 1
@@ -111,8 +135,12 @@ class Lane:
                 self.lds[addr] = self.get(ops[1])
             elif op in ("v_mov_b32", "s_mov_b32"):
                 self.put(ops[0], self.get(ops[1]))
-            elif op in ("v_add_u32", "s_add_u32"):
+            elif op == "v_add_u32":
                 self.put(ops[0], self.get(ops[1]) + self.get(ops[2]))
+            elif op == "s_add_u32":
+                v = self.get(ops[1]) + self._expr(ops[2])
+                self.scc = v >> 32
+                self.put(ops[0], v)
             elif op == "v_sub_u32":
                 self.put(ops[0], self.get(ops[1]) - self.get(ops[2]))
             elif op == "v_and_b32":
@@ -129,6 +157,19 @@ class Lane:
                 self.put(ops[0], self.get(ops[2], 64) >> self.get(ops[1]))
             elif op == "v_lshl_add_u64":
                 self.put(ops[0], ((self.get(ops[1], 64) << self.get(ops[2])) + self.get(ops[3], 64)) & M64)
+            elif op == "s_getpc_b64":
+                self.put(ops[0], baddr[pc] if pc < len(baddr) else pos)
+            elif op == "s_setpc_b64":
+                target = self.get(ops[0])
+                if target not in at:
+                    raise RuntimeError(f"jump into the middle of an instruction: {target}")
+                pc = at[target]
+            elif op == "s_addc_u32":
+                v = self.get(ops[1]) + self.get(ops[2]) + self.scc
+                self.scc = v >> 32
+                self.put(ops[0], v)
+            elif op == "s_lshl_b32":
+                self.put(ops[0], self.get(ops[1]) << self.get(ops[2]))
             elif op == "s_movrels_b32":
                 m = _ONE.match(ops[1])
                 self.put(ops[0], self.r[f"s{int(m.group(2)) + self.r['m0']}"])

@@ -25,7 +25,7 @@ def _gen():
 
 
 GEN = _gen()
-MM, SQ = GEN.product(False), GEN.product(True)
+MM, SQ, SQ_PLAIN = GEN.product(False), GEN.square_tri(), GEN.product(True)
 
 
 def limbs(x, n=L):
@@ -46,8 +46,9 @@ def consts(N):
     return words, np_
 
 
-def run(N, a, b=None):
-    """a, b: (digit0, digit1) pairs; b None = square.  Returns the result digits."""
+def run(N, a, b=None, square=None):
+    """a, b: (digit0, digit1) pairs; b None = square (`square`: which square body).
+    Returns the result digits and the executed-instruction counts."""
     words, np_ = consts(N)
     NK, BB = 0x4000, 0x100000
     smem = {NK + 4 * i: w for i, w in enumerate(words)}
@@ -59,7 +60,7 @@ def run(N, a, b=None):
         for k, v in enumerate(limbs(b[0]) + limbs(b[1])):
             glb[BB + k * 1024] = v
     lane = Lane({"a": 0, "b": 0, "bb": BB, "NK": NK, "np": np_}, lds=lds, glb=glb, smem=smem)
-    counts = lane.run(MM if b is not None else SQ)
+    counts = lane.run(MM if b is not None else (square or SQ))
     out = [lds[k * 1024] for k in range(2 * L)]
     assert all(v <= MASK for v in out)
     d0 = sum(v << (LB * k) for k, v in enumerate(out[:L]))
@@ -90,7 +91,11 @@ def test_nadic_asm_product_and_square(bits):
         t, s, counts = run(N, a)
         assert (t + s * N) % M == A * A * rinv % M
         assert t < 2 * N and s < 2 * N
-        assert counts["v_mad_u64_u32"] == 37 * 149
+        assert counts["v_mad_u64_u32"] == GEN.sq_mads() == 4847
+        # the triangular square is the plain square bit for bit (same column totals at
+        # every quotient, so the same quotients and the same result)
+        t2, s2, c2 = run(N, a, square=SQ_PLAIN)
+        assert (t2, s2) == (t, s) and c2["v_mad_u64_u32"] == 37 * 149
 
 
 def test_nadic_asm_wide_operands():

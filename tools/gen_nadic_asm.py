@@ -222,9 +222,176 @@ def product(sq):
     return body
 
 
+# ------------------------------------------------------------------------------------------
+# Squaring with a triangular t part: X^2 = x0^2 + N (2 x0 x1), and x0^2 needs each cross
+# product x0_i x0_k (i < k) once, doubled, plus the diagonals x0_h^2.  Row i adds
+# 2 x0_i x0_k for k > i -- a contiguous suffix of the row's t multiply sequence, entered by
+# a computed jump (s_setpc_b64; every entry is one 8-byte v_mad_u64_u32) -- and, for even i,
+# the diagonal x0_{i/2}^2 of column i (read from the LDS column along a running address:
+# rows are unrolled in odd/even pairs so the parity is static).  Diagonals of columns 38..72
+# are added after the loop from the B registers.  The t products are added in place
+# (At_k, k = window position) and the q*N pass shifts the window, so the t window has 37
+# pairs (At_36 is written, not accumulated, by each row's last cross product).  Column i is
+# complete when its quotient is taken: cross products of column i come from rows < i, the
+# diagonal from row i itself.  The s part (x0_i * 2 x1, full rows) is as in the general
+# square.  Column bound: 18 doubled products < 2^57 + 1 diagonal + 37 q*N < 2^56: < 2^63.
+# Register plan: At_k v[2k:2k+1] (k=0..36), As_k v[74+2k:75+2k] (k=0..35), b0 = x0
+# v146..v182, b1 = 2 x1 v183..v219, x0_i v220, next v221, 2 x0_i v222, Tt v[224:225],
+# Ts v[226:227], q v228, q' v229, np v230, LDS address v231, scratch v232, K'_i - q v233,
+# diagonal limb v234, its LDS address v235;  s[30:31] jump target, s34 row, s35 K'_i / offset.
+# ------------------------------------------------------------------------------------------
+def SAt(k):
+    return f"v[{2 * k}:{2 * k + 1}]"
+
+
+def SAtLo(k):
+    return f"v{2 * k}"
+
+
+def SAs(k):
+    return f"v[{74 + 2 * k}:{75 + 2 * k}]"
+
+
+def SAsLo(k):
+    return f"v{74 + 2 * k}"
+
+
+def SB0(j):
+    return f"v{146 + j}"
+
+
+def SB1(j):
+    return f"v{183 + j}"
+
+
+SX0, SX0N, SX0D = "v220", "v221", "v222"
+STT, STTLO, STS, STSLO = "v[224:225]", "v224", "v[226:227]", "v226"
+SQ, SQ2, SNPV, SAADR, STMP, SCQ, SDI, SDADDR = "v228", "v229", "v230", "v231", "v232", "v233", "v234", "v235"
+
+
+def sq_tri(tag, first=False):
+    """Doubled cross products 2 x0_i x0_k, k = 1..36 (entered at k = i + 1 by the jump;
+    whole, with addend 0, for row 0).  k = 36 writes: the shift consumed the old top."""
+    out = [f"v_mad_u64_u32 {SAt(k)}, vcc, {SX0D}, {SB0(k)}, {'0' if first else SAt(k)}" for k in range(1, L - 1)]
+    out.append(f"v_mad_u64_u32 {SAt(L - 1)}, vcc, {SX0D}, {SB0(L - 1)}, 0")
+    return out
+
+
+def sq_jump(tag, offset_expr):
+    """s[30:31] <- address of the tri-block entry k = i + 1 (byte offset 8 i, in s35)."""
+    return offset_expr + ["s_getpc_b64 s[30:31]",
+                          f".Lfbm_na_pc{tag}_%=:",
+                          "s_add_u32 s30, s30, s35",
+                          "s_addc_u32 s31, s31, 0",
+                          f"s_add_u32 s30, s30, .Lfbm_na_tri{tag}_%= - .Lfbm_na_pc{tag}_%=",
+                          "s_addc_u32 s31, s31, 0",
+                          "s_setpc_b64 s[30:31]",
+                          f".Lfbm_na_tri{tag}_%=:"]
+
+
+def sq_row(kind, kreg="s35"):
+    """kind: 'first' (row 0), 'odd', 'even' (loop rows), 'r35' (odd, only k = 36 crosses),
+    'last' (row 36, even, no crosses).  On entry X0 = x0_i; s35 = K'_i (kreg)."""
+    first = kind == "first"
+    even = kind in ("first", "even", "last")
+    out = [f"ds_read_b32 {SX0N}, {SAADR} offset:1024"]
+    if even:  # diagonal x0_{i/2}^2 of column i (DI holds it), then prefetch the next even row's
+        out.append(f"v_mad_u64_u32 {SAt(0)}, vcc, {SDI}, {SDI}, {'0' if first else SAt(0)}")
+        out += [f"v_add_u32 {SDADDR}, 0x400, {SDADDR}", f"ds_read_b32 {SDI}, {SDADDR}"]
+    out.append(f"v_mul_lo_u32 {SQ}, {SAtLo(0)}, {SNPV}")  # column i is complete
+    out.append(f"v_lshlrev_b32 {SX0D}, 1, {SX0}")
+    # ---- s part: x0_i * b1, + (K'_i - q), q' ----
+    out.append(f"v_mad_u64_u32 {STS}, vcc, {SX0}, {SB1(0)}, {'0' if first else SAs(0)}")
+    for j in range(1, L):
+        addend = "0" if (first or j == NW) else SAs(j)
+        out.append(f"v_mad_u64_u32 {SAs(j - 1)}, vcc, {SX0}, {SB1(j)}, {addend}")
+        if j == 2:
+            out.append(f"v_and_b32 {SQ}, {MASK}, {SQ}")
+        if j == 4:
+            out.append(f"v_sub_u32 {SCQ}, {kreg}, {SQ}")
+        if j == 12:
+            out.append(f"v_mad_u64_u32 {STS}, vcc, {SCQ}, 1, {STS}")
+        if j == 20:
+            out.append(f"v_mul_lo_u32 {SQ2}, {STSLO}, {SNPV}")
+        if j == 26:
+            out.append(f"v_and_b32 {SQ2}, {MASK}, {SQ2}")
+    # ---- t part: doubled cross products (suffix k > i) ----
+    if first:
+        out += sq_tri("0", first=True)
+    elif kind == "odd":
+        out += sq_jump("o", ["s_lshl_b32 s35, s34, 3"]) + sq_tri("o")
+    elif kind == "even":
+        out += sq_jump("e", ["s_add_u32 s35, s34, 1", "s_lshl_b32 s35, s35, 3"]) + sq_tri("e")
+    elif kind == "r35":
+        out.append(f"v_mad_u64_u32 {SAt(L - 1)}, vcc, {SX0D}, {SB0(L - 1)}, 0")
+    # ---- t: q * N (shifting the window);  s: q' * N ----
+    top = "0" if kind == "last" else SAt(L - 1)
+    out.append(f"v_mad_u64_u32 {STT}, vcc, {SQ}, {Ns(0)}, {SAt(0)}")
+    for k in range(1, L):
+        out.append(f"v_mad_u64_u32 {SAt(k - 1)}, vcc, {SQ}, {Ns(k)}, {SAt(k) if k < L - 1 else top}")
+    out.append(f"v_mad_u64_u32 {STS}, vcc, {SQ2}, {Ns(0)}, {STS}")
+    for j in range(1, L):
+        out.append(f"v_mad_u64_u32 {SAs(j - 1)}, vcc, {SQ2}, {Ns(j)}, {SAs(j - 1)}")
+    out += [f"v_lshrrev_b64 {STT}, 28, {STT}", f"v_lshl_add_u64 {SAt(0)}, {STT}, 0, {SAt(0)}",
+            f"v_lshrrev_b64 {STS}, 28, {STS}", f"v_lshl_add_u64 {SAs(0)}, {STS}, 0, {SAs(0)}",
+            f"v_add_u32 {SAADR}, 0x400, {SAADR}", "s_waitcnt lgkmcnt(0)", f"v_mov_b32 {SX0}, {SX0N}"]
+    return out
+
+
+def krow(row_expr):
+    """m0 <- row index, then s35 <- K'_row (s_movrels needs a wait state after the m0 write)."""
+    return row_expr + ["s_nop 1", f"s_movrels_b32 s35, {KBASE}"]
+
+
+def square_tri():
+    body = load_consts()
+    body.append(f"v_add_u32 {STMP}, 0x10000, %[a]")
+    for j in range(2 * L):
+        reg = SB0(j) if j < L else SB1(j - L)
+        if j < 64:
+            body.append(f"ds_read_b32 {reg}, %[a] offset:{j * 1024}")
+        else:
+            body.append(f"ds_read_b32 {reg}, {STMP} offset:{(j - 64) * 1024}")
+    body += [f"v_mov_b32 {SNPV}, %[np]", f"v_mov_b32 {SAADR}, %[a]", f"ds_read_b32 {SX0}, %[a]",
+             f"ds_read_b32 {SDI}, %[a]", f"v_mov_b32 {SDADDR}, %[a]", "s_waitcnt lgkmcnt(0)"]
+    body += [f"v_lshlrev_b32 {SB1(j)}, 1, {SB1(j)}" for j in range(L)]
+    body += sq_row("first", kreg=KBASE)
+    body += ["s_mov_b32 s34, 1", "1:"]
+    body += krow(["s_mov_b32 m0, s34"]) + sq_row("odd")
+    body += krow(["s_add_u32 m0, s34, 1"]) + sq_row("even")
+    body += ["s_add_u32 s34, s34, 2", f"s_cmp_lg_u32 s34, {L - 2}", "s_cbranch_scc1 1b"]
+    body += krow(["s_mov_b32 m0, 35"]) + sq_row("r35")
+    body += krow(["s_mov_b32 m0, 36"]) + sq_row("last")
+    # diagonals of columns 38..72: column 2h sits at window position 2h - 37
+    body += [f"v_mad_u64_u32 {SAt(2 * h - L)}, vcc, {SB0(h)}, {SB0(h)}, {SAt(2 * h - L)}" for h in range(19, L)]
+    body.append(f"v_add_u32 {STMP}, 0x10000, %[a]")
+
+    def st(k, reg):
+        if k < 64:
+            return f"ds_write_b32 %[a], {reg} offset:{k * 1024}"
+        return f"ds_write_b32 {STMP}, {reg} offset:{(k - 64) * 1024}"
+
+    for acc, lo, carry, carry_lo, base in ((SAt, SAtLo, STT, STTLO, 0), (SAs, SAsLo, STS, STSLO, L)):
+        body += [f"v_lshrrev_b64 {carry}, 28, {acc(0)}", f"v_and_b32 {lo(0)}, {MASK}, {lo(0)}", st(base, lo(0))]
+        for k in range(1, NW):
+            body += [f"v_lshl_add_u64 {acc(k)}, {carry}, 0, {acc(k)}",
+                     f"v_lshrrev_b64 {carry}, 28, {acc(k)}",
+                     f"v_and_b32 {lo(k)}, {MASK}, {lo(k)}",
+                     st(base + k, lo(k))]
+        body.append(st(base + NW, carry_lo))
+    body.append("s_waitcnt lgkmcnt(0)")
+    return body
+
+
+def sq_mads():
+    """v_mad_u64_u32 per square (triangular t part)."""
+    cross = L * (L - 1) // 2
+    return cross + L + L * L + (L * L + L + L * L)
+
+
 def clobbers():
-    regs = [f'"v{i}"' for i in range(232)]
-    regs += [f'"s{i}"' for i in list(range(20, 30)) + [34, 35] + list(range(36, 100))]
+    regs = [f'"v{i}"' for i in range(236)]
+    regs += [f'"s{i}"' for i in list(range(20, 32)) + [34, 35] + list(range(36, 100))]
     out = [", ".join(regs[i:i + 16]) for i in range(0, len(regs), 16)]
     return " \\\n  ".join(x + "," for x in out[:-1]) + " \\\n  " + out[-1]
 
@@ -238,21 +405,21 @@ def count_mads(lines):
 
 
 def main():
-    mm, sq = product(False), product(True)
-    mm_row, sq_row = row(False, False), row(False, True)
+    mm, sq = product(False), square_tri()
+    mm_row, sq_body = row(False, False), sq_row("odd")
     hdr = f"""// GENERATED by tools/gen_nadic_asm.py -- do not edit by hand.
 //
 // gfx950 assembly Montgomery product modulo N^2 in N-adic form: a residue is two 37-limb
 // digits (x0, x1), X = x0 + x1 N (mod N^2), radix 2^28, R = 2^1036.
 //   a (per-lane LDS column, 74 limbs) <- a * b * R^-1 (mod N^2), digits lazily < 2N.
 // See tools/gen_nadic_asm.py for the arithmetic, the bounds and the register plan.
-// {len(mm)} instructions (general, B from global), {len(sq)} (square); row loop bodies
-// {len(mm_row)} / {len(sq_row)} instructions with {count_mads(mm_row)} / {count_mads(sq_row)} v_mad_u64_u32.
+// {len(mm)} instructions (general, B from global), {len(sq)} (square, triangular x0^2); row
+// bodies {len(mm_row)} / <= {len(sq_body)} instructions; {L * count_mads(mm_row)} / {sq_mads()} v_mad_u64_u32 per product.
 #pragma once
 #include <stdint.h>
 
 #define FBM_NA_MADS_MUL {L * count_mads(mm_row)}
-#define FBM_NA_MADS_SQR {L * count_mads(sq_row)}
+#define FBM_NA_MADS_SQR {sq_mads()}
 
 #define FBM_NA_CLOBBERS \\
   {clobbers()}
@@ -268,7 +435,7 @@ __device__ __forceinline__ void fbm_na_mm_glb(uint32_t a_off, const uint32_t* bb
       : "memory", "vcc", "scc", "m0", FBM_NA_CLOBBERS);
 }}
 
-// a <- a^2 R^-1 (mod N^2).
+// a <- a^2 R^-1 (mod N^2): triangular x0^2 (computed-jump row suffixes), full x0 * 2 x1.
 __device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK, uint32_t np) {{
   asm volatile(
 {c_string(sq)}
@@ -280,7 +447,7 @@ __device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK
     with open(OUT, "w") as f:
         f.write(hdr)
     print(f"wrote {OUT}: general {len(mm)} / square {len(sq)} instructions; "
-          f"mads/product {L * count_mads(mm_row)} / {L * count_mads(sq_row)}")
+          f"mads/product {L * count_mads(mm_row)} / {sq_mads()}")
 
 
 if __name__ == "__main__":
