@@ -233,10 +233,11 @@ def product(sq):
 # (At_k, k = window position) and the q*N pass shifts the window, so the t window has 37
 # pairs (At_36 is written, not accumulated, by each row's last cross product).  Column i is
 # complete when its quotient is taken: cross products of column i come from rows < i, the
-# diagonal from row i itself.  The s part (x0_i * 2 x1, full rows) is as in the general
-# square.  Column bound: 18 doubled products < 2^57 + 1 diagonal + 37 q*N < 2^56: < 2^63.
+# diagonal from row i itself.  The s part runs full rows of (2 x0_i) * x1 (the doubled row
+# operand serves both parts).  Column bounds: t 18 doubled products < 2^57 + 1 diagonal +
+# 37 q*N < 2^56; s 37 doubled products + 37 q'*N: < 2^63.
 # Register plan: At_k v[2k:2k+1] (k=0..36), As_k v[74+2k:75+2k] (k=0..35), b0 = x0
-# v146..v182, b1 = 2 x1 v183..v219, x0_i v220, next v221, 2 x0_i v222, Tt v[224:225],
+# v146..v182, b1 = x1 v183..v219, x0_0 v220, next x0 v221, 2 x0_i v222, Tt v[224:225],
 # Ts v[226:227], q v228, q' v229, np v230, LDS address v231, scratch v232, K'_i - q v233,
 # diagonal limb v234, its LDS address v235;  s[30:31] jump target, s34 row, s35 K'_i / offset.
 # ------------------------------------------------------------------------------------------
@@ -299,12 +300,11 @@ def sq_row(kind, kreg="s35"):
         out.append(f"v_mad_u64_u32 {SAt(0)}, vcc, {SDI}, {SDI}, {'0' if first else SAt(0)}")
         out += [f"v_add_u32 {SDADDR}, 0x400, {SDADDR}", f"ds_read_b32 {SDI}, {SDADDR}"]
     out.append(f"v_mul_lo_u32 {SQ}, {SAtLo(0)}, {SNPV}")  # column i is complete
-    out.append(f"v_lshlrev_b32 {SX0D}, 1, {SX0}")
-    # ---- s part: x0_i * b1, + (K'_i - q), q' ----
-    out.append(f"v_mad_u64_u32 {STS}, vcc, {SX0}, {SB1(0)}, {'0' if first else SAs(0)}")
+    # ---- s part: (2 x0_i) * x1, + (K'_i - q), q' ----
+    out.append(f"v_mad_u64_u32 {STS}, vcc, {SX0D}, {SB1(0)}, {'0' if first else SAs(0)}")
     for j in range(1, L):
         addend = "0" if (first or j == NW) else SAs(j)
-        out.append(f"v_mad_u64_u32 {SAs(j - 1)}, vcc, {SX0}, {SB1(j)}, {addend}")
+        out.append(f"v_mad_u64_u32 {SAs(j - 1)}, vcc, {SX0D}, {SB1(j)}, {addend}")
         if j == 2:
             out.append(f"v_and_b32 {SQ}, {MASK}, {SQ}")
         if j == 4:
@@ -334,7 +334,7 @@ def sq_row(kind, kreg="s35"):
         out.append(f"v_mad_u64_u32 {SAs(j - 1)}, vcc, {SQ2}, {Ns(j)}, {SAs(j - 1)}")
     out += [f"v_lshrrev_b64 {STT}, 28, {STT}", f"v_lshl_add_u64 {SAt(0)}, {STT}, 0, {SAt(0)}",
             f"v_lshrrev_b64 {STS}, 28, {STS}", f"v_lshl_add_u64 {SAs(0)}, {STS}, 0, {SAs(0)}",
-            f"v_add_u32 {SAADR}, 0x400, {SAADR}", "s_waitcnt lgkmcnt(0)", f"v_mov_b32 {SX0}, {SX0N}"]
+            f"v_add_u32 {SAADR}, 0x400, {SAADR}", "s_waitcnt lgkmcnt(0)", f"v_lshlrev_b32 {SX0D}, 1, {SX0N}"]
     return out
 
 
@@ -353,8 +353,8 @@ def square_tri():
         else:
             body.append(f"ds_read_b32 {reg}, {STMP} offset:{(j - 64) * 1024}")
     body += [f"v_mov_b32 {SNPV}, %[np]", f"v_mov_b32 {SAADR}, %[a]", f"ds_read_b32 {SX0}, %[a]",
-             f"ds_read_b32 {SDI}, %[a]", f"v_mov_b32 {SDADDR}, %[a]", "s_waitcnt lgkmcnt(0)"]
-    body += [f"v_lshlrev_b32 {SB1(j)}, 1, {SB1(j)}" for j in range(L)]
+             f"ds_read_b32 {SDI}, %[a]", f"v_mov_b32 {SDADDR}, %[a]", "s_waitcnt lgkmcnt(0)",
+             f"v_lshlrev_b32 {SX0D}, 1, {SX0}"]
     body += sq_row("first", kreg=KBASE)
     body += ["s_mov_b32 s34, 1", "1:"]
     body += krow(["s_mov_b32 m0, s34"]) + sq_row("odd")
