@@ -72,10 +72,10 @@ def _rand_n(rng, bits):
     return rng.getrandbits(bits) | (1 << (bits - 1)) | 1
 
 
-@pytest.mark.parametrize("bits", [24, 1024])
+@pytest.mark.parametrize("bits", [2, 24, 1024])
 def test_nadic_asm_product_and_square(bits):
     rng = random.Random(bits)
-    N = _rand_n(rng, bits)
+    N = _rand_n(rng, bits)  # bits = 2: N = 3, a divisor of R - 1 (K = 0, K'_i = 2^28 - 1)
     M = N * N
     rinv = pow(R, -1, M)
     for trial in range(3):
@@ -128,7 +128,7 @@ def test_library_constants_match_and_drive_the_asm():
 
     _build.build()
     lib = _native.load()
-    for N in (W.BIPRIME0, 0xC9F2B5, (1 << 1023) + 12345677):
+    for N in (W.BIPRIME0, 0xC9F2B5, (1 << 1023) + 12345677, 3, 5):  # 3, 5 divide R - 1: K = 0
         n32 = np.frombuffer(N.to_bytes(128, "little"), dtype=np.uint32).copy()
         nk = np.zeros(80, np.uint32)
         r2 = np.zeros(74, np.uint32)

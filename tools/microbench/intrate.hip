@@ -167,6 +167,26 @@ K32(k_lshlor, "v_lshl_or_b32 %0, %1, 7, %2")
 K32(k_xad, "v_xad_u32 %0, %1, %2, %1")
 K32(k_bfi, "v_pk_add_u16 %0, %1, %2")
 
+// 64-bit shift / shift-add (the carry retire of the Montgomery rows)
+#define K64(NAME, ASM)                                                                  \
+  __global__ void NAME(uint64_t* out, uint32_t s) {                                     \
+    uint64_t a = threadIdx.x + s;                                                       \
+    uint64_t acc[CH];                                                                   \
+    _Pragma("unroll") for (int c = 0; c < CH; ++c) acc[c] = c + a;                      \
+    for (int i = 0; i < ITER; ++i) {                                                    \
+      _Pragma("unroll") for (int c = 0; c < CH; ++c) {                                  \
+        uint64_t r;                                                                     \
+        asm volatile(ASM : "=v"(r) : "v"(acc[c]), "v"(a));                              \
+        acc[c] = r;                                                                     \
+      }                                                                                 \
+    }                                                                                   \
+    uint64_t x = 0;                                                                     \
+    _Pragma("unroll") for (int c = 0; c < CH; ++c) x ^= acc[c];                         \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = x;                                     \
+  }
+K64(k_lshr64, "v_lshrrev_b64 %0, 28, %1")
+K64(k_lshladd64, "v_lshl_add_u64 %0, %1, 0, %2")
+
 // ChaCha20 double-rounds as the LOM kernel runs them (ITER/64 blocks per lane); ops counted
 // as 976 per block (the kernel's add/xor/rotate count).
 #include "../../fedbiomed_amd/csrc/fbm_common.hpp"
@@ -193,7 +213,8 @@ int main() {
       {"v_mad_u64_u32", k_mad64}, {"v_mul_lo_u32", k_mullo}, {"v_mul_hi_u32", k_mulhi},
       {"v_add_co_u32", k_addc},   {"v_add3_u32", k_add3},    {"v_fma_f64", k_fma64},
       {"v_mad_u32_u24", k_mul24}, {"v_add_u32", k_add32}, {"v_xor_b32", k_xor32},
-      {"v_alignbit_b32", k_align}, {"v_perm_b32", k_perm}, {"v_lshl_or_b32", k_lshlor}, {"v_xad_u32", k_xad}, {"v_pk_add_u16", k_bfi}, {"chacha20 (976/blk)", k_chacha}};
+      {"v_alignbit_b32", k_align}, {"v_perm_b32", k_perm}, {"v_lshl_or_b32", k_lshlor}, {"v_xad_u32", k_xad}, {"v_pk_add_u16", k_bfi},
+      {"v_lshrrev_b64", k_lshr64}, {"v_lshl_add_u64", k_lshladd64}, {"chacha20 (976/blk)", k_chacha}};
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
