@@ -203,6 +203,9 @@ __global__ void k_chacha(uint64_t* out, uint32_t s) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = x;
 }
 
+// SDWA form of a VOP2 op (is it issued at the VOP2 rate?  measured: no, 4.2 cycles)
+K32(k_xorsdwa, "v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0")
+
 typedef void (*kfn)(uint64_t*, uint32_t);
 
 int main() {
@@ -214,7 +217,7 @@ int main() {
       {"v_add_co_u32", k_addc},   {"v_add3_u32", k_add3},    {"v_fma_f64", k_fma64},
       {"v_mad_u32_u24", k_mul24}, {"v_add_u32", k_add32}, {"v_xor_b32", k_xor32},
       {"v_alignbit_b32", k_align}, {"v_perm_b32", k_perm}, {"v_lshl_or_b32", k_lshlor}, {"v_xad_u32", k_xad}, {"v_pk_add_u16", k_bfi},
-      {"v_lshrrev_b64", k_lshr64}, {"v_lshl_add_u64", k_lshladd64}, {"chacha20 (976/blk)", k_chacha}};
+      {"v_lshrrev_b64", k_lshr64}, {"v_lshl_add_u64", k_lshladd64}, {"v_xor_b32_sdwa", k_xorsdwa}, {"chacha20 (976/blk)", k_chacha}};
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
