@@ -101,3 +101,47 @@ def test_jl_random(dev, seed):
                        target_range=target)
     ref = O.jl_crypter_aggregate(cts, tau, sk0, W.BIPRIME0, sum(ws), n_exp, clip=clip, target=target)
     assert _bits(out) == _bits(ref)
+
+
+@pytest.mark.parametrize("bits", [2, 5, 17, 64, 300, 511, 1000, 1023, 1024])
+def test_jl_random_moduli(dev, bits):
+    """The N-adic exponentiation engine on random odd moduli of every size class (its digit
+    bounds scale with N / 2^1036; small moduli hit FDH retries, i.e. wide digests): raw
+    UserKey.encrypt of int64 plaintexts with keys of either sign and several lengths, and the
+    server decrypt of the party product, against the oracle's closed forms."""
+    import random
+
+    import torch
+
+    from fedbiomed_amd import _device as D
+
+    rng = random.Random(1000 + bits)
+    N = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+    if N < 3:
+        N = 3
+    n, P, tau = 37, 3, rng.getrandbits(64)
+    pts = [rng.getrandbits(63) for _ in range(n)]
+    keys = [rng.getrandbits(rng.choice([1, 40, 700, 2040])) * rng.choice([1, -1]) for _ in range(P)]
+    x = torch.tensor(pts, dtype=torch.int64, device=dev)
+    cts = []
+    for key in keys:
+        got = D.jl_encrypt(x, N, key, tau, P, slot=(100, 1))
+        ints = D.limbs_to_ints(got.cpu().numpy())
+        n2 = N * N
+        want = [((N * pt + 1) % n2) * O.powmod(O.fdh((k << 512) | tau, n2), key, n2) % n2
+                for k, pt in enumerate(pts)]
+        assert ints == want, (bits, key)
+        cts.append(got)
+    sk0 = -sum(keys)
+    _, sums = D.jl_aggregate(torch.stack(cts), N, sk0, tau, n, 1, want_out=False, want_sums=True, slot=(100, 1))
+    s = sums.cpu().numpy().view(np.uint64)
+    got = [int(a) | (int(b) << 64) for a, b in s]
+    n2 = N * N
+    want = []
+    for k in range(n):
+        prod = 1
+        for c in cts:
+            prod = prod * D.limbs_to_ints(c[k:k + 1].cpu().numpy())[0] % n2
+        v = prod * O.powmod(O.fdh((k << 512) | tau, n2), sk0, n2) % n2
+        want.append(((v - 1) // N) % N)
+    assert got == want, bits
