@@ -49,11 +49,16 @@ __device__ __forceinline__ void lom_seeds_to_lds(const LomPeers& peers, uint32_t
 }
 
 #ifndef FBM_LOM_WG_PER_CU
-#define FBM_LOM_WG_PER_CU 10  // A/B on MI355X: 0.365 -> 0.30 ms per 10M x 7-peer protect (0 = one work-item per block)
+// = the resident workgroups per CU of the 64-VGPR build (8 waves/SIMD); A/B on MI355X,
+// 10M x 7 peers: 0.277 ms (99 VGPRs, 10 per CU) -> 0.250 (64 VGPRs: quantise after the peer
+// loop) -> 0.242 (8 per CU).  0 = one work-item per block.
+#define FBM_LOM_WG_PER_CU 8
 #endif
 
+// __launch_bounds__(256, 8): at most 64 VGPRs, 8 waves per SIMD (the ChaCha20 chains need the
+// latency hiding; 65 VGPRs would cap the occupancy at 7)
 template <typename XT>
-__global__ void __launch_bounds__(256) lom_protect_kernel(const XT* __restrict__ x, uint64_t n, QuantParams qp,
+__global__ void __launch_bounds__(256, 8) lom_protect_kernel(const XT* __restrict__ x, uint64_t n, QuantParams qp,
                                                           uint64_t weight, LomPeers peers,
                                                           uint64_t* __restrict__ y, uint32_t* __restrict__ stats) {
   __shared__ uint32_t seeds[FBM_MAX_PEERS][8];
@@ -71,20 +76,8 @@ __global__ void __launch_bounds__(256) lom_protect_kernel(const XT* __restrict__
     const uint64_t base = blk * 8;
     const int cnt = (n - base) >= 8 ? 8 : (int)(n - base);
 
-    // quantise + weight
-    uint64_t val[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      uint64_t q = 0;
-      if (j < cnt) q = lom_input<XT>(x, base + j, qp, clipped);
-      const uint64_t lo = q * weight;
-      const uint64_t hi = __umul64hi(q, weight);
-      val[j] = lo;
-      const uint32_t bl = fbm_bitlen128(hi, lo);
-      maxbits = bl > maxbits ? bl : maxbits;
-    }
-
-    // masks
+    // masks (first: the quantised values are formed after the peer loop, so they do not
+    // hold registers across the ChaCha20 blocks)
     uint64_t mask[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) mask[j] = 0;
@@ -102,6 +95,19 @@ __global__ void __launch_bounds__(256) lom_protect_kernel(const XT* __restrict__
         const uint64_t m = (((uint64_t)ks[2 * j + 1] << 32) | ks[2 * j]) ^ fbm_bswap64(idx);
         mask[j] = add ? mask[j] + m : mask[j] - m;
       }
+    }
+
+    // quantise + weight
+    uint64_t val[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint64_t q = 0;
+      if (j < cnt) q = lom_input<XT>(x, base + j, qp, clipped);
+      const uint64_t lo = q * weight;
+      const uint64_t hi = __umul64hi(q, weight);
+      val[j] = lo;
+      const uint32_t bl = fbm_bitlen128(hi, lo);
+      maxbits = bl > maxbits ? bl : maxbits;
     }
 
     if (cnt == 8) {

@@ -48,7 +48,7 @@ class Lane:
         if tok in ("vcc",):
             return 0
         if tok == "m0":
-            return self.r["m0"]
+            return self.r.get("m0", 0)
         m = _PAIR.match(tok)
         if m:
             k, lo, hi = m.group(1), int(m.group(2)), int(m.group(3))

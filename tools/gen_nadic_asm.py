@@ -40,7 +40,8 @@ Register plan (per lane, wave64):
   v231 K'_i - q
   s20..s29, s36..s62   N_0..N_9, N_10..N_36 (uniform, loaded once per product)
   s63..s99             K'_0..K'_36 (row i reads K'_i by s_movrels with m0 = i)
-  s34 row counter, s35 K'_i;  vcc: unused carry-out of v_mad_u64_u32;  scc, m0 clobbered.
+  s34 row counter, s35 K'_i;  vcc: unused carry-out of v_mad_u64_u32;  scc clobbered;
+  m0 (reserved to the compiler) saved in s19 on entry and restored on exit.
 
 Operands: A is the lane's LDS column (limb k of the 74 at byte a_off + k*1024: rows 0..36
 digit 0, rows 37..73 digit 1; 75 rows allocated, the last row's prefetch reads row 74)
@@ -206,8 +207,11 @@ def normalise_store():
     return out
 
 
+M0_SAVE = "s19"  # m0 is reserved to the compiler: saved here (declared clobbered) and restored
+
+
 def product(sq):
-    body = load_consts()
+    body = [f"s_mov_b32 {M0_SAVE}, m0"] + load_consts()
     body += load_b_square() if sq else load_b_global()
     body += [f"v_mov_b32 {NPV}, %[np]", f"v_mov_b32 {AADR}, %[a]", f"ds_read_b32 {X0}, {AADR}"]
     if not sq:
@@ -219,6 +223,7 @@ def product(sq):
     body += row(False, sq)
     body += ["s_add_u32 s34, s34, 1", f"s_cmp_lg_u32 s34, {L}", "s_cbranch_scc1 1b"]
     body += normalise_store()
+    body.append(f"s_mov_b32 m0, {M0_SAVE}")
     return body
 
 
@@ -344,7 +349,7 @@ def krow(row_expr):
 
 
 def square_tri():
-    body = load_consts()
+    body = [f"s_mov_b32 {M0_SAVE}, m0"] + load_consts()
     body.append(f"v_add_u32 {STMP}, 0x10000, %[a]")
     for j in range(2 * L):
         reg = SB0(j) if j < L else SB1(j - L)
@@ -379,7 +384,7 @@ def square_tri():
                      f"v_and_b32 {lo(k)}, {MASK}, {lo(k)}",
                      st(base + k, lo(k))]
         body.append(st(base + NW, carry_lo))
-    body.append("s_waitcnt lgkmcnt(0)")
+    body += ["s_waitcnt lgkmcnt(0)", f"s_mov_b32 m0, {M0_SAVE}"]
     return body
 
 
@@ -391,7 +396,7 @@ def sq_mads():
 
 def clobbers():
     regs = [f'"v{i}"' for i in range(236)]
-    regs += [f'"s{i}"' for i in list(range(20, 32)) + [34, 35] + list(range(36, 100))]
+    regs += [f'"s{i}"' for i in list(range(19, 32)) + [34, 35] + list(range(36, 100))]
     out = [", ".join(regs[i:i + 16]) for i in range(0, len(regs), 16)]
     return " \\\n  ".join(x + "," for x in out[:-1]) + " \\\n  " + out[-1]
 
@@ -432,7 +437,7 @@ __device__ __forceinline__ void fbm_na_mm_glb(uint32_t a_off, const uint32_t* bb
 {c_string(mm)}
       :
       : [a] "v"(a_off), [b] "v"(b_off), [bb] "s"(bb), [NK] "s"(NK), [np] "s"(np)
-      : "memory", "vcc", "scc", "m0", FBM_NA_CLOBBERS);
+      : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
 }}
 
 // a <- a^2 R^-1 (mod N^2): triangular x0^2 (computed-jump row suffixes), full x0 * 2 x1.
@@ -441,7 +446,7 @@ __device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK
 {c_string(sq)}
       :
       : [a] "v"(a_off), [NK] "s"(NK), [np] "s"(np)
-      : "memory", "vcc", "scc", "m0", FBM_NA_CLOBBERS);
+      : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
 }}
 """
     with open(OUT, "w") as f:
