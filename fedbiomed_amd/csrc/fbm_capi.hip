@@ -728,6 +728,14 @@ int fbm_jl_aggregate_factor(const uint32_t* cts, int n_parties, uint64_t n_ct, i
                          agg_ws(workspace, n_ct), stats, s);
 }
 
+int fbm_test_fdh_gcd(const uint32_t* r8, const uint32_t* n32, uint32_t* err) {
+  if (!r8 || !n32 || !err || !(n32[0] & 1u)) {
+    set_error("fbm_test_fdh_gcd: null pointer or even modulus");
+    return FBM_E_ARG;
+  }
+  return host_gcd_is_one_r8(r8, n32, err);
+}
+
 int fbm_test_nadic_consts(const uint32_t* n32, uint32_t* nk, uint32_t* r2na, uint32_t* r3na, uint32_t* np) {
   if (!n32 || !nk || !r2na || !r3na || !np) {
     set_error("fbm_test_nadic_consts: null pointer");

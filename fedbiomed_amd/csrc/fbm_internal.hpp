@@ -122,6 +122,7 @@ int launch_jl_prod(const uint32_t* cts, int n_parties, uint64_t n_ct, const JlPa
                    uint32_t* X, hipStream_t s);
 #define FBM_EXP_DEC 1      // jl_exp mode bits: plain power (no nude product)
 #define FBM_EXP_H_NADIC 2  // H rows are N-adic digit pairs (jl_split_kernel)
+int host_gcd_is_one_r8(const uint32_t* r8, const uint32_t* n32, uint32_t* err);
 int launch_jl_nadic_split(uint64_t n_ct, const JlParams& jp, const uint32_t* E, uint32_t* Y, uint32_t* out,
                           hipStream_t s);
 int launch_jl_inv(uint64_t n_ct, const JlParams& jp, const uint32_t* E, uint32_t* Y, uint32_t* inv, uint32_t* stats,

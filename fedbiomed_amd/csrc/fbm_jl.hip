@@ -151,11 +151,14 @@ __device__ bool gcd_is_one(uint32_t (&u)[64], const uint32_t* N32, uint32_t& err
   return v[0] == 1u && rest == 0;
 }
 
-// gcd(r, N) == 1 for a one-digest r (8 limbs), N odd: the common case, ~15x less work than
-// the 64-limb binary gcd above.  Factors of two of r do not divide N, so they are stripped;
-// then t = N mod r' by binary long division over N's bits and a binary gcd of (t, r') on
-// 8 limbs.  r == 0 -> gcd = N >= 3 -> false (as the reference's math.gcd).
-__device__ bool gcd_is_one_r8(const uint32_t (&r)[8], const uint32_t* N32, int n_bits, uint32_t& err) {
+// gcd(r, N) == 1 for a one-digest r (8 limbs), N odd: the common case, far less work than
+// the 64-limb binary gcd above.  Factors of two of r do not divide N, so they are stripped
+// (v = r' odd); then t = N * 2^-1024 mod v by a word-serial Montgomery reduction of N by v
+// (2^-1024 is a unit mod the odd v, so gcd(t, v) = gcd(N, v); 32 rows of 8 multiply-adds
+// instead of 1024 shift-subtract steps of a bitwise N mod v), and a binary gcd of (t, v) on 8
+// limbs.  r == 0 -> gcd = N >= 3 -> false (as the reference's math.gcd).  __host__ too: unit
+// tested on the host through fbm_test_fdh_gcd (include/fbm_secagg.h).
+__host__ __device__ inline bool gcd_is_one_r8(const uint32_t (&r)[8], const uint32_t* N32, uint32_t& err) {
   uint32_t v[8];
   uint32_t any = 0;
 #pragma unroll
@@ -177,27 +180,35 @@ __device__ bool gcd_is_one_r8(const uint32_t (&r)[8], const uint32_t* N32, int n
       v[7] >>= sh;
     }
   }
-  // t = N mod v  (t < v < 2^256; 2t + 1 fits 9 limbs)
-  uint32_t t[9];
+  // t = REDC_v(N) = (N + M v) / 2^1024 <= v  (M < 2^1024; N < 2^1024): a window of 8 words
+  // plus a 64-bit top word slides over N one word per row.
+  uint32_t vinv = v[0];  // Newton: v^-1 mod 2^32 (v odd)
 #pragma unroll
-  for (int i = 0; i < 9; ++i) t[i] = 0u;
-  for (int b = n_bits - 1; b >= 0; --b) {
-    const uint32_t bit = (N32[b >> 5] >> (b & 31)) & 1u;
+  for (int i = 0; i < 5; ++i) vinv *= 2u - v[0] * vinv;
+  const uint32_t vp = 0u - vinv;
+  uint32_t w[8];
 #pragma unroll
-    for (int i = 8; i > 0; --i) t[i] = (t[i] << 1) | (t[i - 1] >> 31);
-    t[0] = (t[0] << 1) | bit;
-    uint32_t d[9], br = 0;
+  for (int i = 0; i < 8; ++i) w[i] = N32[i];
+  uint64_t top = N32[8];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const uint64_t x = (uint64_t)t[i] - (i < 8 ? v[i] : 0u) - br;
-      d[i] = (uint32_t)x;
-      br = (uint32_t)(x >> 63);
+  for (int i = 0; i < 32; ++i) {
+    const uint32_t m = w[0] * vp;
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t x = (uint64_t)w[j] + (uint64_t)m * v[j] + c;
+      w[j] = (uint32_t)x;
+      c = x >> 32;
     }
-    if (!br) {
+    top += c;  // w[0] is now 0: shift the window by one word
 #pragma unroll
-      for (int i = 0; i < 9; ++i) t[i] = d[i];
-    }
+    for (int j = 0; j < 7; ++j) w[j] = w[j + 1];
+    w[7] = (uint32_t)top;
+    top = (top >> 32) + (i + 9 < 32 ? N32[i + 9] : 0u);
   }
+  uint32_t t[8];  // t <= v < 2^256: the top word is 0
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t[i] = w[i];
   // binary gcd(t, v), v odd
   uint32_t u[8];
 #pragma unroll
@@ -289,7 +300,7 @@ __global__ void __launch_bounds__(256) jl_fdh_kernel(uint64_t n_ct, JlParams jp,
       uint32_t r8[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) r8[i] = r[i];
-      ok = gcd_is_one_r8(r8, jp.N32, jp.n_bits, err);
+      ok = gcd_is_one_r8(r8, jp.N32, err);
     } else {       // retries (only reachable for moduli with small factors)
       uint32_t u[64];
 #pragma unroll
@@ -1107,6 +1118,16 @@ int launch_jl_inv(uint64_t n_ct, const JlParams& jp, const uint32_t* E, uint32_t
   if (rc) return rc;
   hipLaunchKernelGGL(jl_inv_lift_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, E, Y, inv);
   return check_launch("jl_inv_lift_kernel");
+}
+
+// host test hook (fbm_test_fdh_gcd, include/fbm_secagg.h): the device's one-digest gcd test
+int host_gcd_is_one_r8(const uint32_t* r8, const uint32_t* n32, uint32_t* err) {
+  uint32_t r[8];
+  for (int i = 0; i < 8; ++i) r[i] = r8[i];
+  uint32_t e = 0;
+  const bool ok = gcd_is_one_r8(r, n32, e);
+  *err = e;
+  return ok ? 1 : 0;
 }
 
 int launch_jl_nadic_split(uint64_t n_ct, const JlParams& jp, const uint32_t* E, uint32_t* Y, uint32_t* out,

@@ -190,6 +190,10 @@ int fbm_jl_mads(int square);
  * fedbiomed_amd/csrc/fbm_safegcd.hpp) run on the host, for unit tests.
  * x, n, out: 32 little-endian words (n odd);  batches: number of 30-divstep batches used. */
 int fbm_test_modinv(const uint32_t* x, const uint32_t* n, uint32_t* out, int* batches);
+/* host test hook (no GPU): the FDH's one-digest coprimality test (fbm_jl.hip gcd_is_one_r8) --
+ * r8: 8 words (a 256-bit digest), n32: 32 words (odd N).  Returns 1 if gcd(r, N) == 1, 0 if
+ * not, a negative FBM_E_* code on bad arguments; *err receives device error flags. */
+int fbm_test_fdh_gcd(const uint32_t* r8, const uint32_t* n32, uint32_t* err);
 /* host test hook (no GPU): the N-adic engine's per-modulus constants as the library builds
  * them -- nk: 80 words (N limbs, K'_i), r2na / r3na: 74 limbs (digits of R^2 / R^3 mod N^2,
  * R = 2^1036), np = -N^-1 mod 2^28. */

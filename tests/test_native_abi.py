@@ -142,3 +142,31 @@ def test_device_modinv_on_host():
     assert inv(0, BIPRIME0)[0] == N.FBM_E_INVERSE
     assert inv(15, 45)[0] == N.FBM_E_INVERSE
     assert worst <= 99
+
+
+def test_fdh_gcd_on_host(lib):
+    """The FDH's one-digest coprimality test (Montgomery reduction of N by the odd part of
+    the digest, then a binary gcd) against math.gcd, on the host: random digests, digests
+    sharing a factor with N, zero, powers of two, and moduli from 3 to 1024 bits."""
+    import random
+
+    from fedbiomed_amd import workload as W
+
+    rng = random.Random(11)
+    moduli = [W.BIPRIME0, 3, 9, 15, 3 * 5 * 7 * 11 * 13 * 17 * 19 * 23, (1 << 1024) - 1,
+              rng.getrandbits(1024) | 1, rng.getrandbits(300) | 1]
+    p, q = 1000003, 998244353
+    moduli.append(p * q)
+    for N in moduli:
+        n32 = np.frombuffer(N.to_bytes(128, "little"), dtype=np.uint32).copy()
+        cases = [0, 1, 2, 1 << 255, (1 << 256) - 1, N % (1 << 256)]
+        cases += [rng.getrandbits(256) for _ in range(40)]
+        for f in (3, 5, 7, p, q):
+            if N % f == 0:
+                cases += [(rng.getrandbits(200) * f) % (1 << 256) for _ in range(5)]
+        for r in cases:
+            r8 = np.frombuffer(r.to_bytes(32, "little"), dtype=np.uint32).copy()
+            err = ctypes.c_uint32(0)
+            got = lib.fbm_test_fdh_gcd(r8.ctypes.data, n32.ctypes.data, ctypes.byref(err))
+            assert got == int(math.gcd(r, N) == 1), (N, r)
+            assert err.value == 0
