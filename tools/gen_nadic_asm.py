@@ -223,7 +223,7 @@ def product(sq):
     body += row(False, sq)
     body += ["s_add_u32 s34, s34, 1", f"s_cmp_lg_u32 s34, {L}", "s_cbranch_scc1 1b"]
     body += normalise_store()
-    body.append(f"s_mov_b32 m0, {M0_SAVE}")
+    body += [f"s_mov_b32 m0, {M0_SAVE}", "s_nop 1"]  # m0 read right after the asm: wait state
     return body
 
 
@@ -384,7 +384,7 @@ def square_tri():
                      f"v_and_b32 {lo(k)}, {MASK}, {lo(k)}",
                      st(base + k, lo(k))]
         body.append(st(base + NW, carry_lo))
-    body += ["s_waitcnt lgkmcnt(0)", f"s_mov_b32 m0, {M0_SAVE}"]
+    body += ["s_waitcnt lgkmcnt(0)", f"s_mov_b32 m0, {M0_SAVE}", "s_nop 1"]
     return body
 
 
