@@ -34,14 +34,13 @@ class Lane:
         self.glb = glb if glb is not None else {}
         self.smem = smem if smem is not None else {}
         self.scc = 0
-        self.m0 = 0
 
     # -- operands -------------------------------------------------------------------------
     def _sub(self, tok):
         m = re.fullmatch(r"%\[(\w+)\]", tok)
         return ("arg", m.group(1)) if m else None
 
-    def get(self, tok, width=32):
+    def get(self, tok):
         a = self._sub(tok)
         if a:
             return self.args[a[1]]
@@ -152,11 +151,11 @@ class Lane:
             elif op == "v_mad_u64_u32":
                 a, b = self.get(ops[2]), self.get(ops[3])
                 assert a <= M32 and b <= M32
-                self.put(ops[0], (a * b + self.get(ops[4], 64)) & M64)
+                self.put(ops[0], (a * b + self.get(ops[4])) & M64)
             elif op == "v_lshrrev_b64":
-                self.put(ops[0], self.get(ops[2], 64) >> self.get(ops[1]))
+                self.put(ops[0], self.get(ops[2]) >> self.get(ops[1]))
             elif op == "v_lshl_add_u64":
-                self.put(ops[0], ((self.get(ops[1], 64) << self.get(ops[2])) + self.get(ops[3], 64)) & M64)
+                self.put(ops[0], ((self.get(ops[1]) << self.get(ops[2])) + self.get(ops[3])) & M64)
             elif op == "s_getpc_b64":
                 self.put(ops[0], baddr[pc] if pc < len(baddr) else pos)
             elif op == "s_setpc_b64":
