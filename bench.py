@@ -251,6 +251,10 @@ def main():
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
             "traffic": committed_traffic(kname, args.scheme, n_ct),
             "avg_launch_ms": (ms / cnt) if cnt else None, "launches": cnt}
+    if args.scheme == "jl":
+        roof["note"] = ("jl_exp_kernel moves ~1e-4 of the HBM roofline's bytes by construction: it is bound by "
+                        "integer multiply issue (v_mad_u64_u32), reported in roofline_valu; traffic = the "
+                        "sliding-window table reads (DESIGN.md section 4)")
     line = {
         "metric": "params/s secagg encrypt+aggregate (device-resident), 10M-elem vector @1/8 GPU",
         "value": value, "unit": "params/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
