@@ -188,6 +188,19 @@ int launch_lom_mask_accumulate(uint64_t n, const LomPeers& peers, uint64_t* y, h
 #define FBM_AGG_WG_PER_CU 0  // 0: one pass, no grid-stride (A/B: no measurable difference)
 #endif
 
+#ifndef FBM_AGG_NT
+// 1: the masked rows are read with nontemporal loads (each byte is read exactly once; A/B on
+// MI355X, 10M x 8 parties: 0.133 -> 0.115 ms, 5.4 -> 6.3 TB/s)
+#define FBM_AGG_NT 1
+#endif
+__device__ __forceinline__ uint64_t agg_ld(const uint64_t* p) {
+#if FBM_AGG_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+
 __device__ __forceinline__ double lom_avg_dequant(uint64_t s, uint64_t total_weight, double neg_c, double step,
                                                   uint32_t& err) {
   const double a = fbm_true_div_u128(s, total_weight);
@@ -218,21 +231,21 @@ __global__ void __launch_bounds__(256) lom_aggregate_kernel(const uint64_t* __re
         if (PC == 0) break;
         const uint64_t* row = static_cast<const uint64_t*>(__builtin_assume_aligned(y + (uint64_t)p * n + i, EPT * 8));
 #pragma unroll
-        for (int e = 0; e < EPT; ++e) sm[e] += row[e];
+        for (int e = 0; e < EPT; ++e) sm[e] += agg_ld(row + e);
       }
       if (PC == 0) {
         for (int p = 0; p < P; ++p) {
           const uint64_t* row =
               static_cast<const uint64_t*>(__builtin_assume_aligned(y + (uint64_t)p * n + i, EPT * 8));
 #pragma unroll
-          for (int e = 0; e < EPT; ++e) sm[e] += row[e];
+          for (int e = 0; e < EPT; ++e) sm[e] += agg_ld(row + e);
         }
       }
     } else {
       for (int p = 0; p < P; ++p)
 #pragma unroll
         for (int e = 0; e < EPT; ++e)
-          if (i + e < n) sm[e] += y[(uint64_t)p * n + i + e];
+          if (i + e < n) sm[e] += agg_ld(y + (uint64_t)p * n + i + e);
     }
     double o[EPT];
 #pragma unroll
