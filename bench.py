@@ -107,6 +107,8 @@ def parse():
     ap.add_argument("--no-factor-overlap", action="store_true",
                     help="JL: compute the decryption factor inside the aggregate (after the encrypts)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, the real runs) or gloo (rehearsal)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="HIP streams for the parties' encrypts (0 = one per party); the decryption factor has its own")
     ap.add_argument("--serial", action="store_true",
                     help="no per-party streams in the timed steps (rocprof passes: per-kernel times unconfounded)")
     return ap.parse_args()
@@ -153,7 +155,9 @@ def main():
     n_ct_step = (n + cr - 1) // cr
     # one HIP stream per party: the parties' encrypts are independent, so the tail round
     # of one exponentiation launch overlaps the next party's launch
-    streams = [torch.cuda.Stream(device=dev) for _ in range(P)]
+    n_streams = args.streams if args.streams > 0 else P
+    pool = [torch.cuda.Stream(device=dev) for _ in range(n_streams)]
+    streams = [pool[p % n_streams] for p in range(P)]
     main = torch.cuda.current_stream(dev)
 
     factor_stream = torch.cuda.Stream(device=dev)
@@ -177,7 +181,7 @@ def main():
                     cts[p] = jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=weights[p],
                                                ct_offset=lo // cr)
         if not serial:
-            for st in streams + [factor_stream]:
+            for st in pool + [factor_stream]:
                 main.wait_stream(st)
             for p in range(P):
                 cts[p].record_stream(main)
@@ -316,7 +320,7 @@ def main():
                         x_d = xs_h[p].to(dev, non_blocking=True)
                         ct_h[p].copy_(jc.encrypt_tensor(P, tau, x_d, keys[p], W.BIPRIME0, weight=weights[p]),
                                       non_blocking=True)
-            for st in streams + [factor_stream]:
+            for st in pool + [factor_stream]:
                 main.wait_stream(st)
             factor.record_stream(main)
             cts_d = torch.stack([c.to(dev, non_blocking=True) for c in ct_h])
