@@ -107,6 +107,8 @@ def parse():
     ap.add_argument("--no-factor-overlap", action="store_true",
                     help="JL: compute the decryption factor inside the aggregate (after the encrypts)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, the real runs) or gloo (rehearsal)")
+    ap.add_argument("--no-prologue-first", action="store_true",
+                    help="JL: issue each party's encrypt whole (prologue and exponentiation back to back)")
     ap.add_argument("--streams", type=int, default=0,
                     help="HIP streams for the parties' encrypts (0 = one per party); the decryption factor has its own")
     ap.add_argument("--serial", action="store_true",
@@ -167,6 +169,17 @@ def main():
         cts = [None] * P
         factor = None
         with D.deferred_checks():
+            # every party's prologue (pack, N*pt+1, FDH) is issued before the first
+            # exponentiation: a running exponentiation holds every CU slot, and a prologue
+            # queued behind it would hold back its party's exponentiation (seen in the kernel
+            # trace: tails of one launch left idle while the next party's FDH waited)
+            pend = [None] * P
+            for p in range(P):
+                s_p = main if serial else streams[p]
+                s_p.wait_stream(main)
+                with torch.cuda.stream(s_p):
+                    pend[p] = jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=weights[p],
+                                                ct_offset=lo // cr, defer_exp=not args.no_prologue_first)
             if overlap_factor:
                 # the researcher's decryption factor H(t_k)^sk0 depends on (tau, k, sk0) only: it
                 # runs beside the parties' encrypts instead of after them (same work, same step)
@@ -175,11 +188,8 @@ def main():
                 with torch.cuda.stream(f_s):
                     factor = jc.decrypt_factor_tensor(tau, n_ct_step, sk0, W.BIPRIME0, ct_offset=lo // cr)
             for p in range(P):
-                s_p = main if serial else streams[p]
-                s_p.wait_stream(main)
-                with torch.cuda.stream(s_p):
-                    cts[p] = jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=weights[p],
-                                               ct_offset=lo // cr)
+                with torch.cuda.stream(main if serial else streams[p]):
+                    cts[p] = pend[p] if args.no_prologue_first else pend[p].finish()
         if not serial:
             for st in pool + [factor_stream]:
                 main.wait_stream(st)

@@ -343,11 +343,29 @@ def jl_chunk_ct() -> int:
     return max(1, min(v, JL_MAX_CT))
 
 
+class PendingEncrypt:
+    """A JL encrypt whose prologue kernels are issued and whose exponentiation is not yet
+    (jl_encrypt(..., defer_exp=True)); finish() issues it on the current stream and returns
+    the ciphertext tensor.  Holds the workspace and the status word until then."""
+
+    def __init__(self, args, ct, ws, st):
+        self._args, self._ct, self._ws, self._st = args, ct, ws, st
+
+    def finish(self) -> torch.Tensor:
+        if self._args is not None:
+            _call(N.load().fbm_jl_encrypt_phase, *self._args, _stream(), 2)
+            _check_stats_or_defer(self._st)
+            self._args = None
+        return self._ct
+
+
 def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, clip=None, target=None,
-               weight: int = 1, slot: Optional[Tuple[int, int]] = None, ct_offset: int = 0) -> torch.Tensor:
+               weight: int = 1, slot: Optional[Tuple[int, int]] = None, ct_offset: int = 0,
+               defer_exp: bool = False):
     """One party's JL ciphertexts as an int32 [n_ct, 64] tensor of 32-bit limbs.
     `slot` overrides the (element_size, comp_ratio) packing (UserKey.encrypt on raw
-    plaintexts = slot (es, 1) with an int64 input)."""
+    plaintexts = slot (es, 1) with an int64 input).  defer_exp: issue only the prologue and
+    return a PendingEncrypt (one library call's worth of ciphertexts at most)."""
     dev = x.device
     lib = N.load()
     target = target or SAParameters.TARGET_RANGE
@@ -365,6 +383,15 @@ def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, 
     kl, kneg = _key_limbs(key)
     chunk = jl_chunk_ct()  # calls above the library's per-call cap run as ct_offset stripes
     ws = torch.empty(int(lib.fbm_jl_encrypt_workspace(min(n_ct, chunk))), dtype=torch.uint8, device=dev)
+    if defer_exp:
+        if n_ct > chunk:
+            raise FedbiomedSecaggCrypterError(
+                f"{ErrorNumbers.FB624.value}: a deferred encrypt takes at most {chunk} ciphertexts")
+        st = _stats(dev)
+        args = (_ptr(x), _x_dtype(x), n, c, c2, tf, tm1, int(weight), es, cr, _np_ptr(bp), _np_ptr(kl), kneg,
+                int(tau), int(ct_offset), _ptr(ct), _ptr(ws), _ptr(st))
+        _call(lib.fbm_jl_encrypt_phase, *args, _stream(), 1)
+        return PendingEncrypt(args, ct, (ws, x, bp, kl), st)
     for k0 in range(0, n_ct, chunk):
         k1 = min(n_ct, k0 + chunk)
         xs = x[k0 * cr:min(n, k1 * cr)]

@@ -59,6 +59,8 @@ SIGNATURES = {
     "fbm_jl_aggregate_workspace": (c_u64, [c_u64]),
     "fbm_jl_encrypt": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_int, c_int, c_vp, c_vp,
                                c_int, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),
+    "fbm_jl_encrypt_phase": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_int, c_int, c_vp,
+                                     c_vp, c_int, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp, c_int]),
     "fbm_jl_aggregate": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_u64, c_vp, c_vp, c_int, c_u64, c_u64, c_u64,
                                  c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_decrypt_factor": (c_int, [c_u64, c_vp, c_vp, c_int, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),

@@ -514,13 +514,16 @@ uint64_t fbm_jl_aggregate_workspace(uint64_t n_ct) {
          3 * align256(n_ct * 64 * 4) + align256(n_ct * 32 * 4) + align256(slots * FBM_TENTRIES * FBM_NL * 4);
 }
 
-int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
-                   uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime, const uint32_t* key,
-                   int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* ct_out, void* workspace,
-                   uint32_t* stats, void* stream) {
+// phase bit 1: the prologue (status word, constants, pack, nude, FDH, and the inverse of H
+// for a negative key); bit 2: the exponentiation.  Both phases rebuild the same host
+// parameters from the same arguments and use the same workspace, so (1 then 2) == 3.
+static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
+                           uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,
+                           const uint32_t* key, int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* ct_out,
+                           void* workspace, uint32_t* stats, void* stream, int phase) {
   hipStream_t s = (hipStream_t)stream;
-  int rc = zero_stats(stats, s);
-  if (rc) return rc;
+  int rc;
+  if ((phase & 1) && (rc = zero_stats(stats, s))) return rc;
   QuantParams qp;
   if ((rc = quant_params(clip, two_clip, target_f, target_m1, qp))) return rc;
   if (x_dtype != FBM_F32 && x_dtype != FBM_F64 && x_dtype != FBM_U64) {
@@ -572,21 +575,44 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
   uint32_t* Hinv = (uint32_t*)(ws + off);  // negative keys only (after the table: keeps its placement)
   off += align256(n_ct * 64 * 4);
   uint32_t* Y = (uint32_t*)(ws + off);
-  if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s); }))) return rc;
-  if ((rc = timed("jl_pack", s, [&] { return launch_jl_pack(x, x_dtype, n, qp, weight, es, cr, n_ct, pt, stats, s); }))) return rc;
-  if ((rc = timed("jl_nude", s, [&] { return launch_jl_nude(pt, n_ct, jp, nude, s); }))) return rc;
-  if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, H, stats, s); }))) return rc;
-  const uint32_t* base = H;
-  if (key_negative && !is_zero) {
-    // gmpy2.powmod with a negative exponent (_jls.py:60-73): invert H(t_k) mod N^2 first,
-    // then raise the inverse to |key|
-    if ((rc = timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, H, Y, Hinv, stats, s); }))) return rc;
-    // the inverse is a full-width residue: hand it to the exponentiation as N-adic digits
-    if ((rc = timed("jl_split", s, [&] { return launch_jl_nadic_split(n_ct, jp, Hinv, Y, Hinv, s); }))) return rc;
-    base = Hinv;
+  const bool inverse = key_negative && !is_zero;
+  if (phase & 1) {
+    if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s); }))) return rc;
+    if ((rc = timed("jl_pack", s, [&] { return launch_jl_pack(x, x_dtype, n, qp, weight, es, cr, n_ct, pt, stats, s); }))) return rc;
+    if ((rc = timed("jl_nude", s, [&] { return launch_jl_nude(pt, n_ct, jp, nude, s); }))) return rc;
+    if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, H, stats, s); }))) return rc;
+    if (inverse) {
+      // gmpy2.powmod with a negative exponent (_jls.py:60-73): invert H(t_k) mod N^2 first,
+      // then raise the inverse to |key|
+      if ((rc = timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, H, Y, Hinv, stats, s); }))) return rc;
+      // the inverse is a full-width residue: hand it to the exponentiation as N-adic digits
+      if ((rc = timed("jl_split", s, [&] { return launch_jl_nadic_split(n_ct, jp, Hinv, Y, Hinv, s); }))) return rc;
+    }
   }
-  const int mode = (key_negative && !is_zero) ? FBM_EXP_H_NADIC : 0;
+  if (!(phase & 2)) return FBM_OK;
+  const uint32_t* base = inverse ? Hinv : H;
+  const int mode = inverse ? FBM_EXP_H_NADIC : 0;
   return timed("jl_exp", s, [&] { return launch_jl_exp(base, n_ct, jp, sc, mode, nude, table, slots, ops, cst, ct_out, s); });
+}
+
+int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
+                   uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime, const uint32_t* key,
+                   int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* ct_out, void* workspace,
+                   uint32_t* stats, void* stream) {
+  return jl_encrypt_impl(x, x_dtype, n, clip, two_clip, target_f, target_m1, weight, es, cr, biprime, key,
+                         key_negative, tau, ct_offset, ct_out, workspace, stats, stream, 3);
+}
+
+int fbm_jl_encrypt_phase(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
+                         uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,
+                         const uint32_t* key, int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* ct_out,
+                         void* workspace, uint32_t* stats, void* stream, int phase) {
+  if (phase < 1 || phase > 3) {
+    set_error("fbm_jl_encrypt_phase: phase must be 1, 2 or 3");
+    return FBM_E_ARG;
+  }
+  return jl_encrypt_impl(x, x_dtype, n, clip, two_clip, target_f, target_m1, weight, es, cr, biprime, key,
+                         key_negative, tau, ct_offset, ct_out, workspace, stats, stream, phase);
 }
 
 // aggregate workspace: ops | cst | X (blocked) | H [n_ct][64] | E [n_ct][64] | F [n_ct][64] |

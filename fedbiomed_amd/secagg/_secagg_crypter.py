@@ -79,16 +79,20 @@ class SecaggCrypter:
     # ---- device fast path ------------------------------------------------------------------
     def encrypt_tensor(self, num_nodes: int, current_round: int, params: torch.Tensor, key: int, biprime: int,
                        clipping_range: Union[int, None] = None, weight: Optional[int] = None,
-                       target_range: Optional[int] = None, ct_offset: int = 0) -> torch.Tensor:
+                       target_range: Optional[int] = None, ct_offset: int = 0, defer_exp: bool = False):
         """Device tensor (f32/f64) in HBM -> int32 [n_ct, 64] ciphertext limbs in HBM.
-        `ct_offset`: global index of this shard's first ciphertext (element-range sharding)."""
+        `ct_offset`: global index of this shard's first ciphertext (element-range sharding).
+        `defer_exp`: issue the prologue kernels only and return a PendingEncrypt whose
+        finish() issues the exponentiation (several parties on one device: every prologue
+        before the first exponentiation occupies the chip)."""
         if not isinstance(key, int):
             raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: The argument `key` must be integer")
         target_range = target_range or SAParameters.TARGET_RANGE
         _check_weight(weight, jl=True)
         try:
             return D.jl_encrypt(params, biprime, key, current_round, num_nodes, clip=clipping_range,
-                                target=target_range, weight=1 if weight is None else weight, ct_offset=ct_offset)
+                                target=target_range, weight=1 if weight is None else weight, ct_offset=ct_offset,
+                                defer_exp=defer_exp)
         except (TypeError, ValueError) as exp:
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value} Error during parameter encryption. {exp}") from exp

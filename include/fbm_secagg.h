@@ -121,6 +121,14 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
                    uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,
                    const uint32_t* key, int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* ct_out,
                    void* workspace, uint32_t* stats, void* stream);
+/* fbm_jl_encrypt in two phases on the same arguments and workspace: phase 1 = the prologue
+ * kernels (pack, N*pt+1 digits, FDH, the inverse of H for a negative key), phase 2 = the
+ * exponentiation, 3 = both (== fbm_jl_encrypt).  Lets a caller running several parties on one
+ * device issue every prologue before the first exponentiation takes the whole chip. */
+int fbm_jl_encrypt_phase(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
+                         uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,
+                         const uint32_t* key, int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* ct_out,
+                         void* workspace, uint32_t* stats, void* stream, int phase);
 
 /* JL aggregate: prod_u c_u * H(t_k)^sk0 mod N^2, x = ((v-1)//N) mod N, VES decode,
  * average, dequantise.  Replaces SecaggCrypter.aggregate (_secagg_crypter.py:139-230) =

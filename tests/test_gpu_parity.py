@@ -414,3 +414,24 @@ def test_clipping_warning_semantics(dev, caplog):
             SecaggLomCrypter("n").encrypt(1, "a", vals, {"b": b"\x01" * 32}, ["a", "b"], clipping_range=3)
         hits = sum(msg in r.getMessage() for r in caplog.records)
         assert hits == (3 if warn else 0), (vals, hits)
+
+
+def test_jl_deferred_exponentiation_equals_whole(dev):
+    """encrypt_tensor(defer_exp=True).finish() (prologue and exponentiation issued as two
+    library phases, fbm_jl_encrypt_phase) gives the same ciphertexts as one call, for keys of
+    either sign, with other work issued in between."""
+    import torch
+
+    from fedbiomed_amd import workload as W
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    jc = SecaggCrypter()
+    x = torch.from_numpy(W.party_params(3, 5000)).to(dev)
+    for key in (W.jl_user_key(1), -W.jl_user_key(2)):
+        whole = jc.encrypt_tensor(4, 9, x, key, W.BIPRIME0, weight=77)
+        pend = jc.encrypt_tensor(4, 9, x, key, W.BIPRIME0, weight=77, defer_exp=True)
+        other = jc.encrypt_tensor(4, 10, x * 2, W.jl_user_key(3), W.BIPRIME0)  # interleaved work
+        got = pend.finish()
+        assert torch.equal(got, whole)
+        assert pend.finish() is got  # idempotent
+        del other
