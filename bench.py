@@ -169,27 +169,51 @@ def main():
         cts = [None] * P
         factor = None
         with D.deferred_checks():
-            # every party's prologue (pack, N*pt+1, FDH) is issued before the first
-            # exponentiation: a running exponentiation holds every CU slot, and a prologue
-            # queued behind it would hold back its party's exponentiation (seen in the kernel
-            # trace: tails of one launch left idle while the next party's FDH waited)
-            pend = [None] * P
-            for p in range(P):
-                s_p = main if serial else streams[p]
-                s_p.wait_stream(main)
-                with torch.cuda.stream(s_p):
-                    pend[p] = jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=weights[p],
-                                                ct_offset=lo // cr, defer_exp=not args.no_prologue_first)
-            if overlap_factor:
-                # the researcher's decryption factor H(t_k)^sk0 depends on (tau, k, sk0) only: it
-                # runs beside the parties' encrypts instead of after them (same work, same step)
+            if args.no_prologue_first:
+                if overlap_factor:
+                    f_s = main if serial else factor_stream
+                    f_s.wait_stream(main)
+                    with torch.cuda.stream(f_s):
+                        factor = jc.decrypt_factor_tensor(tau, n_ct_step, sk0, W.BIPRIME0, ct_offset=lo // cr)
+                for p in range(P):
+                    s_p = main if serial else streams[p]
+                    s_p.wait_stream(main)
+                    with torch.cuda.stream(s_p):
+                        cts[p] = jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=weights[p],
+                                                   ct_offset=lo // cr)
+            else:
+                # Kernel order: every prologue (the parties' pack / N*pt+1 / FDH, the factor's FDH),
+                # then every exponentiation, then the factor's inverse.  A running exponentiation
+                # holds every CU slot, and the hardware queues are FIFO across the streams mapped
+                # onto them: a small kernel queued behind an exponentiation waits for CU slots and
+                # holds back whatever follows it on its queue (seen in the kernel trace).
+                pend = [None] * P
+                for p in range(P):
+                    s_p = main if serial else streams[p]
+                    s_p.wait_stream(main)
+                    with torch.cuda.stream(s_p):
+                        pend[p] = jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=weights[p],
+                                                    ct_offset=lo // cr, defer_exp=True)
                 f_s = main if serial else factor_stream
-                f_s.wait_stream(main)
-                with torch.cuda.stream(f_s):
-                    factor = jc.decrypt_factor_tensor(tau, n_ct_step, sk0, W.BIPRIME0, ct_offset=lo // cr)
-            for p in range(P):
-                with torch.cuda.stream(main if serial else streams[p]):
-                    cts[p] = pend[p] if args.no_prologue_first else pend[p].finish()
+                if overlap_factor:
+                    f_s.wait_stream(main)
+                    with torch.cuda.stream(f_s):
+                        pf = jc.decrypt_factor_tensor(tau, n_ct_step, sk0, W.BIPRIME0, ct_offset=lo // cr,
+                                                      phased=True)
+                if not serial:  # the exponentiations start once all prologues are done
+                    for st in pool + [factor_stream]:
+                        main.wait_stream(st)
+                    for st in pool + [factor_stream]:
+                        st.wait_stream(main)
+                if overlap_factor:
+                    with torch.cuda.stream(f_s):
+                        pf.exponentiate()
+                for p in range(P):
+                    with torch.cuda.stream(main if serial else streams[p]):
+                        cts[p] = pend[p].finish()
+                if overlap_factor:
+                    with torch.cuda.stream(f_s):
+                        factor = pf.finish()
         if not serial:
             for st in pool + [factor_stream]:
                 main.wait_stream(st)

@@ -403,9 +403,36 @@ def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, 
     return ct
 
 
-def jl_decrypt_factor(n_ct: int, biprime: int, key: int, tau: int, ct_offset: int = 0, dev=None) -> torch.Tensor:
+class PendingFactor:
+    """A decryption factor issued phase by phase (jl_decrypt_factor(..., phased=True) issues
+    constants + FDH): exponentiate() and then finish() (the inverse of a negative key) issue the
+    rest on the current stream; finish() returns the factor tensor."""
+
+    def __init__(self, args, f, keep, st):
+        self._args, self._f, self._keep, self._st, self._done = args, f, keep, st, 1
+
+    def _phase(self, bit):
+        if not self._done & bit:
+            _call(N.load().fbm_jl_decrypt_factor_phase, *self._args, _stream(), bit)
+            self._done |= bit
+
+    def exponentiate(self) -> "PendingFactor":
+        self._phase(2)
+        return self
+
+    def finish(self) -> torch.Tensor:
+        self._phase(2)
+        if not self._done & 4:
+            self._phase(4)
+            _check_stats_or_defer(self._st)
+        return self._f
+
+
+def jl_decrypt_factor(n_ct: int, biprime: int, key: int, tau: int, ct_offset: int = 0, dev=None,
+                      phased: bool = False):
     """ServerKey's H(t_k)^key mod N^2 for ciphertexts [ct_offset, ct_offset + n_ct) of round
-    `tau` as int32 [n_ct, 64] limbs -- needs no ciphertext, so it can run while parties encrypt."""
+    `tau` as int32 [n_ct, 64] limbs -- needs no ciphertext, so it can run while parties encrypt.
+    phased: issue only the first phase (constants + FDH) and return a PendingFactor."""
     dev = dev or device()
     lib = N.load()
     if tau < 0 or tau > U64_MAX:
@@ -417,6 +444,14 @@ def jl_decrypt_factor(n_ct: int, biprime: int, key: int, tau: int, ct_offset: in
     kl, kneg = _key_limbs(key)
     chunk = jl_chunk_ct()
     ws = torch.empty(int(lib.fbm_jl_aggregate_workspace(min(n_ct, chunk))), dtype=torch.uint8, device=dev)
+    if phased:
+        if n_ct > chunk:
+            raise FedbiomedSecaggCrypterError(
+                f"{ErrorNumbers.FB624.value}: a phased decryption factor takes at most {chunk} ciphertexts")
+        st = _stats(dev)
+        args = (n_ct, _np_ptr(bp), _np_ptr(kl), kneg, int(tau), int(ct_offset), _ptr(f), _ptr(ws), _ptr(st))
+        _call(lib.fbm_jl_decrypt_factor_phase, *args, _stream(), 1)
+        return PendingFactor(args, f, (ws, bp, kl), st)
     for k0 in range(0, n_ct, chunk):
         k1 = min(n_ct, k0 + chunk)
         st = _stats(dev)

@@ -64,6 +64,7 @@ SIGNATURES = {
     "fbm_jl_aggregate": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_u64, c_vp, c_vp, c_int, c_u64, c_u64, c_u64,
                                  c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_decrypt_factor": (c_int, [c_u64, c_vp, c_vp, c_int, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),
+    "fbm_jl_decrypt_factor_phase": (c_int, [c_u64, c_vp, c_vp, c_int, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp, c_int]),
     "fbm_jl_aggregate_factor": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_u64, c_vp, c_vp, c_u64, c_dbl, c_dbl,
                                         c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fbm_ass_split": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_vp, c_vp, c_u64, c_vp, c_vp]),

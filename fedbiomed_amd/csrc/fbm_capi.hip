@@ -646,8 +646,10 @@ static JlAggWs agg_ws(void* workspace, uint64_t n_ct) {
 
 // ServerKey's factor H(t_k)^sk0 mod N^2 (inverse first for sk0 < 0): depends on the round,
 // the ciphertext index and the key only -- not on the parties' ciphertexts.
+// phase bits: 1 = constants + FDH, 2 = the exponentiation, 4 = the inverse (negative key)
 static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau,
-                          uint64_t ct_offset, uint32_t* factor, const JlAggWs& w, uint32_t* stats, hipStream_t s) {
+                          uint64_t ct_offset, uint32_t* factor, const JlAggWs& w, uint32_t* stats, hipStream_t s,
+                          int phase = 7) {
   JlParams jp;
   int rc;
   if ((rc = build_jl_params(biprime, 1, 1, tau, ct_offset, jp))) return rc;
@@ -660,11 +662,15 @@ static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t
   jp.key_is_zero = is_zero;
   const bool inv = key_negative && !is_zero;
   uint32_t* E = inv ? w.E : factor;
-  if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, w.ops, w.cst, s); }))) return rc;
-  if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, w.H, stats, s); }))) return rc;
-  if ((rc = timed("jl_exp", s, [&] { return launch_jl_exp(w.H, n_ct, jp, sc, FBM_EXP_DEC, nullptr, w.table, w.slots, w.ops, w.cst, E, s); })))
+  if (phase & 1) {
+    if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, w.ops, w.cst, s); }))) return rc;
+    if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, w.H, stats, s); }))) return rc;
+  }
+  if ((phase & 2) &&
+      (rc = timed("jl_exp", s, [&] { return launch_jl_exp(w.H, n_ct, jp, sc, FBM_EXP_DEC, nullptr, w.table, w.slots, w.ops, w.cst, E, s); })))
     return rc;
-  if (inv && (rc = timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, E, w.xs, factor, stats, s); })))  // xs: y scratch
+  if ((phase & 4) && inv &&
+      (rc = timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, E, w.xs, factor, stats, s); })))  // xs: y scratch
     return rc;
   return FBM_OK;
 }
@@ -735,6 +741,26 @@ int fbm_jl_decrypt_factor(uint64_t n_ct, const uint32_t* biprime, const uint32_t
     return FBM_E_ARG;
   }
   return jl_factor_impl(n_ct, biprime, key, key_negative, tau, ct_offset, factor, agg_ws(workspace, n_ct), stats, s);
+}
+
+int fbm_jl_decrypt_factor_phase(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative,
+                                uint64_t tau, uint64_t ct_offset, uint32_t* factor, void* workspace, uint32_t* stats,
+                                void* stream, int phase) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc;
+  if (phase < 1 || phase > 7) {
+    set_error("fbm_jl_decrypt_factor_phase: phase must be a non-empty subset of {1, 2, 4}");
+    return FBM_E_ARG;
+  }
+  if ((phase & 1) && (rc = zero_stats(stats, s))) return rc;
+  if ((rc = jl_agg_checks(1, n_ct, biprime, 1))) return rc;
+  if (n_ct == 0) return FBM_OK;
+  if (!key || !factor || !workspace) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  return jl_factor_impl(n_ct, biprime, key, key_negative, tau, ct_offset, factor, agg_ws(workspace, n_ct), stats, s,
+                        phase);
 }
 
 int fbm_jl_aggregate_factor(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,

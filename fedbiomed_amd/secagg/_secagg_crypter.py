@@ -114,13 +114,16 @@ class SecaggCrypter:
         return (out, sums) if want_sums else out
 
     def decrypt_factor_tensor(self, current_round: int, num_ciphertexts: int, key: int, biprime: int,
-                              ct_offset: int = 0) -> torch.Tensor:
+                              ct_offset: int = 0, phased: bool = False):
         """The server key's per-ciphertext factor H(t_k)^key mod N^2 of round `current_round`
         (int32 [num_ciphertexts, 64] in HBM).  It does not depend on the parties' ciphertexts,
-        so the researcher can compute it before they arrive and pass it to aggregate_tensor."""
+        so the researcher can compute it before they arrive and pass it to aggregate_tensor.
+        `phased`: issue constants + FDH only and return a PendingFactor (exponentiate(),
+        finish() -> tensor) so a caller can order its kernels against other work."""
         if not isinstance(key, int):
             raise TypeError("The key should be type of integer")
-        return D.jl_decrypt_factor(num_ciphertexts, biprime, key, current_round, ct_offset=ct_offset)
+        return D.jl_decrypt_factor(num_ciphertexts, biprime, key, current_round, ct_offset=ct_offset,
+                                   phased=phased)
 
     # ---- reference API -----------------------------------------------------------------------
     def encrypt(self, num_nodes: int, current_round: int, params: List[float], key: int, biprime: int,

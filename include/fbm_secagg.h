@@ -153,6 +153,11 @@ int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, 
  * Both take fbm_jl_aggregate_workspace(n_ct) bytes of workspace. */
 int fbm_jl_decrypt_factor(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau,
                           uint64_t ct_offset, uint32_t* factor, void* workspace, uint32_t* stats, void* stream);
+/* fbm_jl_decrypt_factor in phases on the same arguments and workspace: bit 1 = constants and
+ * FDH, bit 2 = the exponentiation, bit 4 = the inverse (negative key); 7 == fbm_jl_decrypt_factor. */
+int fbm_jl_decrypt_factor_phase(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative,
+                                uint64_t tau, uint64_t ct_offset, uint32_t* factor, void* workspace, uint32_t* stats,
+                                void* stream, int phase);
 int fbm_jl_aggregate_factor(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,
                             const uint32_t* biprime, const uint32_t* factor, uint64_t total_weight, double neg_clip,
                             double step, double* out, uint64_t* sums, void* workspace, uint32_t* stats, void* stream);

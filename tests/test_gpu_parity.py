@@ -435,3 +435,21 @@ def test_jl_deferred_exponentiation_equals_whole(dev):
         assert torch.equal(got, whole)
         assert pend.finish() is got  # idempotent
         del other
+
+
+def test_jl_phased_factor_equals_whole(dev):
+    """decrypt_factor_tensor(phased=True) -> exponentiate() -> finish() (fbm_jl_decrypt_factor_phase)
+    equals the one-call factor, for server keys of either sign."""
+    import torch
+
+    from fedbiomed_amd import workload as W
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    jc = SecaggCrypter()
+    for key in (-sum(W.jl_user_key(p) for p in range(3)), W.jl_user_key(5)):
+        whole = jc.decrypt_factor_tensor(4, 700, key, W.BIPRIME0, ct_offset=11)
+        pf = jc.decrypt_factor_tensor(4, 700, key, W.BIPRIME0, ct_offset=11, phased=True)
+        pf.exponentiate()
+        got = pf.finish()
+        assert torch.equal(got, whole)
+        assert pf.finish() is got
