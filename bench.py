@@ -344,16 +344,30 @@ def main():
         def step_e2e():
             # as the device-resident step: one stream per party (H2D -> encrypt -> D2H), the
             # decryption factor on its own stream, then H2D of the ciphertexts -> combine -> D2H
+            # kernel order as in the device-resident step: H2D + prologues, then the
+            # exponentiations (+ D2H of each party's ciphertexts), then the factor's inverse
             with D.deferred_checks():
-                factor_stream.wait_stream(main)
-                with torch.cuda.stream(factor_stream):
-                    factor = jc.decrypt_factor_tensor(tau, n_ct, sk0, W.BIPRIME0)
+                pend = [None] * P
                 for p in range(P):
                     streams[p].wait_stream(main)
                     with torch.cuda.stream(streams[p]):
                         x_d = xs_h[p].to(dev, non_blocking=True)
-                        ct_h[p].copy_(jc.encrypt_tensor(P, tau, x_d, keys[p], W.BIPRIME0, weight=weights[p]),
-                                      non_blocking=True)
+                        pend[p] = jc.encrypt_tensor(P, tau, x_d, keys[p], W.BIPRIME0, weight=weights[p],
+                                                    defer_exp=True)
+                factor_stream.wait_stream(main)
+                with torch.cuda.stream(factor_stream):
+                    pf = jc.decrypt_factor_tensor(tau, n_ct, sk0, W.BIPRIME0, phased=True)
+                for st in pool + [factor_stream]:
+                    main.wait_stream(st)
+                for st in pool + [factor_stream]:
+                    st.wait_stream(main)
+                with torch.cuda.stream(factor_stream):
+                    pf.exponentiate()
+                for p in range(P):
+                    with torch.cuda.stream(streams[p]):
+                        ct_h[p].copy_(pend[p].finish(), non_blocking=True)
+                with torch.cuda.stream(factor_stream):
+                    factor = pf.finish()
             for st in pool + [factor_stream]:
                 main.wait_stream(st)
             factor.record_stream(main)
