@@ -1,4 +1,5 @@
-"""Builds the in-tree gfx950 HIP library `fedbiomed_amd/_lib/libfbm_secagg.so`.
+"""Builds the in-tree gfx950 HIP library `fedbiomed_amd/_lib/libfbm_secagg.so` (and the
+list API's host conversion module `_fbm_pyconv`, csrc/fbm_pyconv.c).
 
     python -m fedbiomed_amd._build            # incremental (rebuilds when a source is newer)
     python -m fedbiomed_amd._build --force
@@ -10,12 +11,16 @@ quantise / average / dequantise FP64 sequences must round exactly like CPython +
 import os
 import subprocess
 import sys
+import sysconfig
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_lib", "libfbm_secagg.so")
 SOURCES = ["fbm_lom.hip", "fbm_jl.hip", "fbm_ass.hip", "fbm_capi.hip"]
+# host-side list <-> buffer conversions of the list API (a CPython extension, plain gcc)
+PYCONV_SRC = os.path.join(CSRC, "fbm_pyconv.c")
+PYCONV_OUT = os.path.join(HERE, "_lib", "_fbm_pyconv" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
 ARCH = os.environ.get("FBM_OFFLOAD_ARCH", "gfx950")
 
 
@@ -36,8 +41,24 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def build_pyconv(force: bool = False, verbose: bool = False) -> str:
+    if not force and os.path.exists(PYCONV_OUT) and os.path.getmtime(PYCONV_OUT) >= os.path.getmtime(PYCONV_SRC):
+        return PYCONV_OUT
+    os.makedirs(os.path.dirname(PYCONV_OUT), exist_ok=True)
+    tmp = PYCONV_OUT + ".tmp"
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-Wall", "-Werror",
+           "-I" + sysconfig.get_paths()["include"], PYCONV_SRC, "-o", tmp]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, PYCONV_OUT)
+    return PYCONV_OUT
+
+
 def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
     """`out` / `defines`: variant builds for A/B measurement (tools/ab.sh); the product is OUT."""
+    if out == OUT and not defines:
+        build_pyconv(force, verbose)
     if out == OUT and not defines and not force and not needs_build():
         return OUT
     os.makedirs(os.path.dirname(out), exist_ok=True)

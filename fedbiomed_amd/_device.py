@@ -182,47 +182,97 @@ def int_limbs(v: int, n_limbs: int) -> np.ndarray:
 # ------------------------------------------------------------------------------------------
 # list <-> tensor conversions (the host-memory boundary, measured in DESIGN.md)
 # ------------------------------------------------------------------------------------------
+def _pyconv():
+    """The list API's C conversion loops (csrc/fbm_pyconv.c), built in-tree by _build."""
+    global _PYCONV
+    if _PYCONV is None:
+        import importlib.util
+
+        from ._build import PYCONV_OUT
+
+        if not os.path.exists(PYCONV_OUT):
+            raise N.NativeUnavailable(f"{PYCONV_OUT} is not built (python -m fedbiomed_amd._build)")
+        spec = importlib.util.spec_from_file_location("_fbm_pyconv", PYCONV_OUT)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _PYCONV = mod
+    return _PYCONV
+
+
+_PYCONV = None
+
+
+def host_empty(shape, dtype: torch.dtype) -> torch.Tensor:
+    """Host staging buffer for the list API: pinned (torch's caching host allocator hands the
+    same pages back call after call -- no first-touch page faults, DMA-direct copies) when a
+    HIP device is visible, plain memory otherwise (the argument checks run without one)."""
+    return torch.empty(shape, dtype=dtype, pin_memory=torch.cuda.is_available())
+
+
+def to_host(t: torch.Tensor) -> torch.Tensor:
+    """Device tensor -> host copy through a (cached) pinned staging buffer."""
+    host = host_empty(t.shape, t.dtype)
+    host.copy_(t)
+    return host
+
+
+def floats_to_host(params: list) -> Optional[torch.Tensor]:
+    """List of floats -> float64 host tensor in one C pass; None if an item is not a float
+    (isinstance(v, float), subclasses included -- the reference's check)."""
+    host = host_empty(len(params), torch.float64)
+    return host if _pyconv().floats_to_f64(params, host.numpy()) < 0 else None
+
+
 def floats_to_device(params: Sequence[float], dev=None) -> torch.Tensor:
-    """Validated list of floats -> float64 device tensor (array('d') builds the host buffer
-    ~1.7x faster than np.asarray on a list)."""
+    """Validated list of floats -> float64 device tensor."""
     dev = dev or device()
-    host = np.frombuffer(array.array("d", params), dtype=np.float64) if isinstance(params, list) else \
-        np.asarray(params, dtype=np.float64)
-    return torch.from_numpy(host).to(dev)
+    host = floats_to_host(params) if isinstance(params, list) else None
+    if host is None:  # not a list, or not all floats: numpy's conversion (raises the TypeError)
+        host = torch.from_numpy(np.frombuffer(array.array("d", params), dtype=np.float64))
+    return host.to(dev)
 
 
 def u64_to_device(rows, dev=None) -> torch.Tensor:
     """list[int] or list[list[int]] -> int64 tensor holding the uint64 bit patterns.
     np.array(..., dtype=uint64) raises exactly where the reference's conversion raises."""
     dev = dev or device()
-    arr = np.array(rows, dtype=np.uint64)
+    if isinstance(rows, list) and rows and all(isinstance(r, list) for r in rows) and \
+            len(set(map(len, rows))) == 1:  # fast path: equal-length rows of in-range ints
+        host = host_empty((len(rows), len(rows[0])), torch.int64)
+        buf = host.numpy()
+        if all(_pyconv().ints_to_bytes(r, 8, buf[u]) < 0 for u, r in enumerate(rows)):
+            return host.to(dev)
+    arr = np.array(rows, dtype=np.uint64)  # anything else, with numpy's exact errors
     return torch.from_numpy(arr.view(np.int64)).to(dev)
 
 
 def u64_from_device(t: torch.Tensor) -> List[int]:
-    return t.cpu().numpy().view(np.uint64).tolist()
+    return to_host(t).numpy().view(np.uint64).tolist()
 
 
-def ints_to_limbs(cts: Sequence[int], modulus: Optional[int] = None) -> np.ndarray:
-    """JL ciphertext ints -> [n, 64] uint32 little-endian limbs.  Values outside
-    [0, 2^2048) are reduced mod N^2 first (same residue, as the reference reduces in its
-    product); in-range values go through unchanged."""
-    try:  # common case: every value is in range (to_bytes raises OverflowError otherwise)
-        blob = b"".join([int(c).to_bytes(256, "little") for c in cts])
-    except OverflowError:
-        out = bytearray(256 * len(cts))
-        for i, c in enumerate(cts):
-            c = int(c)
-            if c < 0 or c.bit_length() > 2048:
-                c %= modulus
-            out[256 * i:256 * (i + 1)] = c.to_bytes(256, "little")
-        blob = bytes(out)
-    return np.frombuffer(blob, dtype=np.uint32).reshape(len(cts), 64)
+def ints_to_limbs(cts: Sequence[int], modulus: Optional[int] = None, out: Optional[np.ndarray] = None) -> np.ndarray:
+    """JL ciphertext ints -> [n, 64] uint32 little-endian limbs (into `out` if given, e.g. a
+    party's row of the aggregate's input).  Values outside [0, 2^2048) are reduced mod N^2
+    first (same residue, as the reference reduces in its product); in-range values go
+    through unchanged."""
+    if out is None:
+        out = np.empty((len(cts), 64), dtype=np.uint32)
+    cts = cts if isinstance(cts, list) else list(cts)
+    bad = _pyconv().ints_to_bytes(cts, 256, out)  # common case: one C pass, -1
+    while bad >= 0:  # an out-of-range (or non-int) value: reduce it, continue after it
+        c = int(cts[bad])
+        if c < 0 or c.bit_length() > 2048:
+            if modulus is None:
+                raise OverflowError("ciphertext outside [0, 2^2048) and no modulus to reduce it by")
+            c %= modulus
+        out[bad] = np.frombuffer(c.to_bytes(256, "little"), dtype=np.uint32)
+        rest = _pyconv().ints_to_bytes(cts[bad + 1:], 256, out[bad + 1:])
+        bad = -1 if rest < 0 else bad + 1 + rest
+    return out
 
 
 def limbs_to_ints(arr: np.ndarray) -> List[int]:
-    b = np.ascontiguousarray(arr, dtype=np.uint32).tobytes()
-    return [int.from_bytes(b[256 * i:256 * (i + 1)], "little") for i in range(len(b) // 256)]
+    return _pyconv().bytes_to_ints(np.ascontiguousarray(arr, dtype=np.uint32), 256)
 
 
 # ------------------------------------------------------------------------------------------

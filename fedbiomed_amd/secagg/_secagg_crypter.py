@@ -52,14 +52,17 @@ def _all_instances(values, cls) -> bool:
     return all(issubclass(t, cls) for t in set(map(type, values)))
 
 
-def _check_float_list(params) -> None:
+def _check_float_list(params) -> torch.Tensor:
+    """The reference's list/float checks; returns the float64 host copy made in the same pass."""
     if not isinstance(params, list):
         raise FedbiomedSecaggCrypterError(
             f"{ErrorNumbers.FB624.value}: Expected argument `params` type list but got {type(params)}")
-    if not _all_instances(params, float):
+    host = D.floats_to_host(params)
+    if host is None:
         raise FedbiomedSecaggCrypterError(
             f"{ErrorNumbers.FB624.value}: The parameters to encrypt should list of floats. "
             f"There are one or more than a value that is not type of float.")
+    return host
 
 
 def _check_int_lists(params) -> None:
@@ -131,16 +134,16 @@ class SecaggCrypter:
                 target_range: Optional[int] = None) -> List[int]:
         """Encrypts model parameters (reference `_secagg_crypter.py:45-137`)."""
         start = time.process_time()
-        _check_float_list(params)
+        host = _check_float_list(params)
         if not isinstance(key, int):
             raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: The argument `key` must be integer")
         target_range = target_range or SAParameters.TARGET_RANGE
         D.quant_params(clipping_range, target_range)  # OverflowError / range checks as the reference
         if not params:
             return []
-        x = D.floats_to_device(params)
+        x = host.to(D.device())
         ct = self.encrypt_tensor(num_nodes, current_round, x, key, biprime, clipping_range, weight, target_range)
-        packed = ct.cpu().numpy().view(np.uint32)
+        packed = D.to_host(ct).numpy().view(np.uint32)
         out = D.limbs_to_ints(packed)
         if wire.enabled():
             out = wire.EncryptedParams(out, "jl", packed)
@@ -171,13 +174,16 @@ class SecaggCrypter:
             return []
         limbs = wire.packed_rows(params, "jl", n_ct)
         if limbs is None:
-            limbs = np.stack([D.ints_to_limbs(p[:n_ct], n2) for p in params])
+            staged = D.host_empty((len(params), n_ct, 64), torch.int32)
+            limbs = staged.numpy().view(np.uint32)
+            for u, p in enumerate(params):
+                D.ints_to_limbs(p if len(p) == n_ct else p[:n_ct], n2, out=limbs[u])
         dev = D.device()
         cts = torch.from_numpy(limbs.view(np.int32)).to(dev)
         out = self.aggregate_tensor(current_round, cts, key, biprime, total_sample_size, clipping_range,
                                     num_expected_params, target_range)
         logger.info(f"Aggregating {len(params)} parameters from {num_nodes} nodes.")
-        res = out.cpu().numpy().tolist()
+        res = D.to_host(out).numpy().tolist()
         logger.debug(f"Aggregation is completed in {round(time.process_time() - start, ndigits=2)} seconds.")
         return res
 
@@ -246,16 +252,16 @@ class SecaggLomCrypter(SecaggCrypter):
                 node_ids: List[str], clipping_range: Union[int, None] = None, weight: Optional[int] = None,
                 target_range: Optional[int] = None) -> List[int]:
         start = time.process_time()
-        _check_float_list(params)
+        host = _check_float_list(params)
         target_range = target_range or SAParameters.TARGET_RANGE
         D.quant_params(clipping_range, target_range)
         if not params:
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value} Error during parameter encryption. max() arg is an empty sequence")
-        x = D.floats_to_device(params)
+        x = host.to(D.device())
         y = self.encrypt_tensor(current_round, node_id, x, pairwise_secrets, node_ids, clipping_range, weight,
                                 target_range)
-        packed = y.cpu().numpy().view(np.uint64)
+        packed = D.to_host(y).numpy().view(np.uint64)
         out = packed.tolist()
         if wire.enabled():
             out = wire.EncryptedParams(out, "lom", packed)
@@ -279,6 +285,6 @@ class SecaggLomCrypter(SecaggCrypter):
             return []
         out = self.aggregate_tensor(Y, total_sample_size, clipping_range, target_range)
         logger.info(f"Aggregating {len(params)} parameters from {num_nodes} nodes.")
-        res = out.cpu().numpy().tolist()
+        res = D.to_host(out).numpy().tolist()
         logger.debug(f"Aggregation is completed in {round(time.process_time() - start, ndigits=2)} seconds.")
         return res

@@ -1,0 +1,94 @@
+"""List-API host conversions (csrc/fbm_pyconv.c) against Python's own conversions.
+
+The reference crypters take and return Python lists (`_secagg_crypter.py:45-230`); the C
+loops must give exactly what `array('d', ...)`, `int.to_bytes` / `int.from_bytes` and
+`np.array(..., dtype=uint64)` give, and hand every value they cannot convert back to the
+Python path (reduction mod N^2, numpy's errors).  CPU only.
+"""
+
+import array
+import random
+
+import numpy as np
+import pytest
+
+from fedbiomed_amd import _device as D
+from fedbiomed_amd.secagg._secagg_crypter import _check_float_list
+from fedbiomed_amd.exceptions import FedbiomedSecaggCrypterError
+
+
+class F(float):
+    pass
+
+
+def test_floats_match_array_d():
+    rng = random.Random(3)
+    vals = [rng.uniform(-1e6, 1e6) for _ in range(5000)] + [0.0, -0.0, float("inf"), float("-inf"),
+                                                           float("nan"), 5e-324, 1.7976931348623157e308, F(2.5)]
+    got = _check_float_list(vals).numpy()
+    ref = np.frombuffer(array.array("d", vals), dtype=np.float64)
+    assert got.tobytes() == ref.tobytes()  # bit patterns, NaN and -0.0 included
+    assert _check_float_list([]).numel() == 0
+
+
+@pytest.mark.parametrize("bad", [[1.0, 2, 3.0], [1.0, "x"], [None], [np.float32(1.0)], [True]])
+def test_float_check_rejects_what_isinstance_rejects(bad):
+    assert not all(isinstance(v, float) for v in bad)
+    with pytest.raises(FedbiomedSecaggCrypterError):
+        _check_float_list(bad)
+
+
+def test_float_subclasses_pass():
+    vals = [np.float64(0.25), F(1.5), 3.0]
+    assert all(isinstance(v, float) for v in vals)
+    assert _check_float_list(vals).tolist() == [0.25, 1.5, 3.0]
+
+
+def test_ints_to_limbs_matches_to_bytes():
+    rng = random.Random(5)
+    vals = [0, 1, 2**30 - 1, 2**30, 2**32, 2**60, 2**64 - 1, 2**2047, 2**2048 - 1, True]
+    vals += [rng.getrandbits(rng.randint(1, 2048)) for _ in range(3000)]
+    got = D.ints_to_limbs(vals)
+    ref = np.frombuffer(b"".join(int(v).to_bytes(256, "little") for v in vals), dtype=np.uint32).reshape(-1, 64)
+    assert np.array_equal(got, ref)
+    assert D.limbs_to_ints(got) == [int(v) for v in vals]
+
+
+def test_ints_to_limbs_out_of_range_values_reduced():
+    n2 = (2**1023 + 1155) ** 2
+    vals = [7, -5, 2**2048, 2**2100 + 9, np.int64(11), 3, -(2**3000)]
+    got = D.limbs_to_ints(D.ints_to_limbs(vals, n2))
+    assert got == [7, (-5) % n2, 2**2048 % n2, (2**2100 + 9) % n2, 11, 3, (-(2**3000)) % n2]
+    with pytest.raises(OverflowError):
+        D.ints_to_limbs([1, -1])  # no modulus to reduce by
+
+
+def test_ints_to_limbs_into_row_views():
+    rng = random.Random(9)
+    rows = [[rng.getrandbits(2048) for _ in range(17)] for _ in range(3)]
+    out = np.zeros((3, 17, 64), dtype=np.uint32)
+    for u, r in enumerate(rows):
+        D.ints_to_limbs(r, None, out=out[u])
+    assert [D.limbs_to_ints(out[u]) for u in range(3)] == rows
+
+
+def test_u64_rows_match_numpy_and_its_errors():
+    rng = random.Random(11)
+    rows = [[rng.getrandbits(64) for _ in range(1000)] for _ in range(4)]
+    rows[1][3] = 2**64 - 1
+    m = D._pyconv()
+    buf = np.empty((4, 1000), dtype=np.int64)
+    assert all(m.ints_to_bytes(r, 8, buf[u]) < 0 for u, r in enumerate(rows))
+    assert np.array_equal(buf.view(np.uint64), np.array(rows, dtype=np.uint64))
+    for bad in (-1, 2**64, 1.5, "7"):
+        assert m.ints_to_bytes([1, 2, bad], 8, np.empty(3, np.int64)) == 2
+
+
+def test_buffer_size_checked():
+    m = D._pyconv()
+    with pytest.raises(ValueError):
+        m.ints_to_bytes([1, 2], 8, np.empty(3, np.int64))
+    with pytest.raises(ValueError):
+        m.floats_to_f64([1.0], np.empty(2, np.float64))
+    with pytest.raises(ValueError):
+        m.bytes_to_ints(b"\0" * 10, 4)
