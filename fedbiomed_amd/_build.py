@@ -47,7 +47,7 @@ def build_pyconv(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(os.path.dirname(PYCONV_OUT), exist_ok=True)
     tmp = PYCONV_OUT + ".tmp"
     cmd = [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-Wall", "-Werror",
-           "-I" + sysconfig.get_paths()["include"], PYCONV_SRC, "-o", tmp]
+           "-pthread", "-I" + sysconfig.get_paths()["include"], PYCONV_SRC, "-o", tmp]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

@@ -20,6 +20,8 @@
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 #include <longintrepr.h>
+#include <pthread.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -82,6 +84,73 @@ static PyObject* floats_to_f64(PyObject* self, PyObject* args) {
     return PyLong_FromSsize_t(bad);
 }
 
+/* Ciphertext-sized conversions run on several host threads with the GIL released: the
+ * items are pinned first (a reference each, taken under the GIL), so a list mutated by
+ * another Python thread meanwhile cannot free them; PyLong digits are immutable and
+ * long_to_words touches no interpreter state.  FBM_CONV_THREADS overrides the thread count
+ * (default 8, the GPU box's CPU share is 16). */
+#define PAR_MIN_BYTES (1 << 20)
+
+typedef struct {
+    PyObject** items;
+    unsigned char* dst;
+    Py_ssize_t lo, hi, nb, bad;
+} conv_job;
+
+static void* conv_range(void* arg) {
+    conv_job* j = (conv_job*)arg;
+    j->bad = -1;
+    for (Py_ssize_t i = j->lo; i < j->hi; ++i) {
+        PyObject* v = j->items[i];
+        if (!PyLong_Check(v) || long_to_words((PyLongObject*)v, j->dst + i * j->nb, j->nb) < 0) {
+            j->bad = i;
+            break;
+        }
+    }
+    return NULL;
+}
+
+static int conv_threads(Py_ssize_t n) {
+    const char* e = getenv("FBM_CONV_THREADS");
+    long t = e ? strtol(e, NULL, 10) : 8;
+    if (t < 1) t = 1;
+    if (t > 64) t = 64;
+    if (t > n / 1024) t = n / 1024 > 0 ? (long)(n / 1024) : 1;
+    return (int)t;
+}
+
+/* -1, or the first bad index over all ranges (each range stops at its own first bad item). */
+static Py_ssize_t ints_to_words_parallel(PyObject* seq, Py_ssize_t n, Py_ssize_t nb, unsigned char* dst,
+                                         int nt) {
+    PyObject** items = (PyObject**)PyMem_Malloc((size_t)n * sizeof(PyObject*));
+    if (!items) return -2;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        items[i] = PyList_GET_ITEM(seq, i);
+        Py_INCREF(items[i]);
+    }
+    conv_job jobs[64];
+    pthread_t tid[64];
+    int started[64] = {0};
+    Py_BEGIN_ALLOW_THREADS
+    for (int t = 0; t < nt; ++t) {
+        jobs[t] = (conv_job){items, dst, n * t / nt, n * (t + 1) / nt, nb, -1};
+        if (t > 0) started[t] = pthread_create(&tid[t], NULL, conv_range, &jobs[t]) == 0;
+    }
+    conv_range(&jobs[0]);
+    for (int t = 1; t < nt; ++t) {
+        if (started[t])
+            pthread_join(tid[t], NULL);
+        else
+            conv_range(&jobs[t]); /* thread creation failed: do its range here */
+    }
+    Py_END_ALLOW_THREADS
+    Py_ssize_t bad = -1;
+    for (int t = 0; t < nt && bad < 0; ++t) bad = jobs[t].bad;
+    for (Py_ssize_t i = 0; i < n; ++i) Py_DECREF(items[i]);
+    PyMem_Free(items);
+    return bad;
+}
+
 static PyObject* ints_to_bytes(PyObject* self, PyObject* args) {
     PyObject *seq, *out;
     Py_ssize_t nb;
@@ -96,19 +165,53 @@ static PyObject* ints_to_bytes(PyObject* self, PyObject* args) {
     unsigned char* dst = (unsigned char*)view.buf;
     int words = nb % 4 == 0 && ((uintptr_t)dst & 3) == 0;
     Py_ssize_t bad = -1;
-    for (Py_ssize_t i = 0; i < n; ++i) {
-        PyObject* v = PyList_GET_ITEM(seq, i);
-        int rc = !PyLong_Check(v) ? -1
-                 : words ? long_to_words((PyLongObject*)v, dst + i * nb, nb)
-                         : _PyLong_AsByteArray((PyLongObject*)v, dst + i * nb, (size_t)nb, 1, 0);
-        if (rc < 0) {
-            PyErr_Clear(); /* OverflowError (negative or too wide): the caller's slow path */
-            bad = i;
-            break;
+    int nt = words && n * nb >= PAR_MIN_BYTES ? conv_threads(n) : 1;
+    if (nt > 1) {
+        bad = ints_to_words_parallel(seq, n, nb, dst, nt);
+        if (bad == -2) {
+            PyBuffer_Release(&view);
+            return PyErr_NoMemory();
+        }
+    } else {
+        for (Py_ssize_t i = 0; i < n; ++i) {
+            PyObject* v = PyList_GET_ITEM(seq, i);
+            int rc = !PyLong_Check(v) ? -1
+                     : words ? long_to_words((PyLongObject*)v, dst + i * nb, nb)
+                             : _PyLong_AsByteArray((PyLongObject*)v, dst + i * nb, (size_t)nb, 1, 0);
+            if (rc < 0) {
+                PyErr_Clear(); /* OverflowError (negative or too wide): the caller's slow path */
+                bad = i;
+                break;
+            }
         }
     }
     PyBuffer_Release(&view);
     return PyLong_FromSsize_t(bad);
+}
+
+/* nw little-endian 32-bit words -> int, built straight in CPython's 30-bit digits
+ * (_PyLong_FromByteArray goes byte by byte). */
+static PyObject* words_to_long(const uint32_t* w, Py_ssize_t nw) {
+    while (nw > 0 && w[nw - 1] == 0) --nw;
+    if (nw <= 1) return PyLong_FromUnsignedLong(nw ? w[0] : 0); /* small-int cache for 0..256 */
+    uint32_t top = w[nw - 1];
+    Py_ssize_t nbits = 32 * (nw - 1) + (32 - __builtin_clz(top));
+    Py_ssize_t nd = (nbits + PyLong_SHIFT - 1) / PyLong_SHIFT;
+    PyLongObject* v = _PyLong_New(nd);
+    if (!v) return NULL;
+    uint64_t acc = 0;
+    int bits = 0;
+    Py_ssize_t k = 0, d = 0;
+    while (d < nd) {
+        if (bits < PyLong_SHIFT && k < nw) {
+            acc |= (uint64_t)w[k++] << bits;
+            bits += 32;
+        }
+        v->ob_digit[d++] = (digit)(acc & PyLong_MASK);
+        acc >>= PyLong_SHIFT;
+        bits -= PyLong_SHIFT;
+    }
+    return (PyObject*)v;
 }
 
 static PyObject* bytes_to_ints(PyObject* self, PyObject* args) {
@@ -124,8 +227,10 @@ static PyObject* bytes_to_ints(PyObject* self, PyObject* args) {
     PyObject* lst = PyList_New(n);
     if (lst) {
         const unsigned char* src = (const unsigned char*)view.buf;
+        int words = nb % 4 == 0 && ((uintptr_t)src & 3) == 0;
         for (Py_ssize_t i = 0; i < n; ++i) {
-            PyObject* v = _PyLong_FromByteArray(src + i * nb, (size_t)nb, 1, 0);
+            PyObject* v = words ? words_to_long((const uint32_t*)(src + i * nb), nb / 4)
+                                : _PyLong_FromByteArray(src + i * nb, (size_t)nb, 1, 0);
             if (!v) {
                 Py_CLEAR(lst);
                 break;

@@ -161,27 +161,40 @@ class SecaggCrypter:
                 f"does not match the number of nodes has been set for the encrypter. There might "
                 f"be some nodes did not answered to training request or num of clients of "
                 "`ParameterEncrypter` has not been set properly before train request.")
-        _check_int_lists(params)
-        if not isinstance(key, int):
-            raise TypeError("The key should be type of integer")
-        if not params:
-            raise FedbiomedSecaggCrypterError(
-                f"{ErrorNumbers.FB624.value}: The aggregation of encrypted parameters "
-                f"is not successful: list_y_u_tau should be a non-empty list.")
-        n2 = biprime * biprime
-        n_ct = min(len(p) for p in params)  # zip(*list_y_u_tau) truncates (_jls.py:691-693)
-        if n_ct == 0:
-            return []
-        limbs = wire.packed_rows(params, "jl", n_ct)
-        if limbs is None:
-            staged = D.host_empty((len(params), n_ct, 64), torch.int32)
-            limbs = staged.numpy().view(np.uint32)
-            for u, p in enumerate(params):
-                D.ints_to_limbs(p if len(p) == n_ct else p[:n_ct], n2, out=limbs[u])
-        dev = D.device()
-        cts = torch.from_numpy(limbs.view(np.int32)).to(dev)
-        out = self.aggregate_tensor(current_round, cts, key, biprime, total_sample_size, clipping_range,
-                                    num_expected_params, target_range)
+        with D.deferred_checks():
+            # The decryption factor H(t_k)^key needs no ciphertext: issue it first, so the GPU
+            # exponentiates while the host validates and converts the parties' lists.  Only
+            # when the arguments are well-formed; any error is raised below, in the order
+            # the reference raises it.
+            factor = None
+            if params and isinstance(key, int) and isinstance(biprime, int) and all(type(p) is list for p in params):
+                n_ct0 = min(len(p) for p in params)
+                if n_ct0:
+                    try:
+                        factor = self.decrypt_factor_tensor(current_round, n_ct0, key, biprime)
+                    except Exception:  # noqa: BLE001 -- re-raised by the regular path below
+                        factor = None
+            _check_int_lists(params)
+            if not isinstance(key, int):
+                raise TypeError("The key should be type of integer")
+            if not params:
+                raise FedbiomedSecaggCrypterError(
+                    f"{ErrorNumbers.FB624.value}: The aggregation of encrypted parameters "
+                    f"is not successful: list_y_u_tau should be a non-empty list.")
+            n2 = biprime * biprime
+            n_ct = min(len(p) for p in params)  # zip(*list_y_u_tau) truncates (_jls.py:691-693)
+            if n_ct == 0:
+                return []
+            limbs = wire.packed_rows(params, "jl", n_ct)
+            if limbs is None:
+                staged = D.host_empty((len(params), n_ct, 64), torch.int32)
+                limbs = staged.numpy().view(np.uint32)
+                for u, p in enumerate(params):
+                    D.ints_to_limbs(p if len(p) == n_ct else p[:n_ct], n2, out=limbs[u])
+            dev = D.device()
+            cts = torch.from_numpy(limbs.view(np.int32)).to(dev)
+            out = self.aggregate_tensor(current_round, cts, key, biprime, total_sample_size, clipping_range,
+                                        num_expected_params, target_range, decrypt_factor=factor)
         logger.info(f"Aggregating {len(params)} parameters from {num_nodes} nodes.")
         res = D.to_host(out).numpy().tolist()
         logger.debug(f"Aggregation is completed in {round(time.process_time() - start, ndigits=2)} seconds.")

@@ -92,3 +92,32 @@ def test_buffer_size_checked():
         m.floats_to_f64([1.0], np.empty(2, np.float64))
     with pytest.raises(ValueError):
         m.bytes_to_ints(b"\0" * 10, 4)
+
+
+@pytest.mark.parametrize("threads", ["1", "3", "8"])
+def test_threaded_ints_to_bytes_first_bad_index(monkeypatch, threads):
+    """Ciphertext-sized lists (>= 1 MB of output) convert on several threads with the GIL
+    released; the answer (bytes and first bad index) must not depend on the thread count."""
+    monkeypatch.setenv("FBM_CONV_THREADS", threads)
+    m = D._pyconv()
+    rng = random.Random(12)
+    vals = [rng.getrandbits(2048) for _ in range(6000)]
+    vals[:6] = [0, 1, 2**30 - 1, 2**30, 2**32, 2**2048 - 1]
+    out = np.empty((len(vals), 64), dtype=np.uint32)
+    assert m.ints_to_bytes(vals, 256, out) == -1
+    assert out.tobytes() == b"".join(v.to_bytes(256, "little") for v in vals)
+    for bad_at, bad in ((5999, -3), (4500, 2**2048), (2100, 1.0), (3, "x")):
+        v2 = list(vals)
+        v2[bad_at] = bad
+        v2[5998] = -1  # a later bad item in another range: the first one is reported
+        assert m.ints_to_bytes(v2, 256, out) == min(bad_at, 5998)
+
+
+def test_bytes_to_ints_word_path_edges():
+    m = D._pyconv()
+    vals = [0, 1, 255, 256, 2**30 - 1, 2**30, 2**31, 2**32 - 1, 2**32, 2**60, 2**2047, 2**2048 - 1]
+    vals += [random.Random(13).getrandbits(b) for b in range(1, 2049, 37)]
+    blob = np.frombuffer(b"".join(v.to_bytes(256, "little") for v in vals), dtype=np.uint32)
+    got = m.bytes_to_ints(blob, 256)
+    assert got == vals and all(type(v) is int for v in got)
+    assert m.bytes_to_ints(b"\x05\0\0", 3) == [5]  # byte path (width not a word multiple)
