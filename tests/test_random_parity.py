@@ -147,3 +147,30 @@ def test_jl_random_moduli(dev, bits):
         v = prod * O.powmod(O.fdh((k << 512) | tau, n2), sk0, n2) % n2
         want.append(((v - 1) // N) % N)
     assert got == want, bits
+
+
+@pytest.mark.parametrize("P", [16, 17, 31, 33])
+def test_jl_many_parties(dev, P):
+    """Party counts past the bench's 8: the slot width grows with ceil(log2(P + 1))
+    (es = 35 at P = 16, 17 and 31; 36 at P = 33 -- `_jls.py:104-116`), so the ciphertext
+    count per vector changes; encrypt and the P-way ciphertext product bit-exact."""
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    rng = np.random.default_rng(300 + P)
+    es, cr_ = O.jl_slot(None, P)
+    assert es == 30 + int(np.ceil(np.log2(P + 1)))
+    n = 2 * cr_ + 3
+    tau = int(rng.integers(0, 2**40))
+    ws = [int(rng.integers(1, 2**16)) for _ in range(P)]
+    keys = [W.jl_user_key(900 + p) for p in range(P)]
+    xs = [_params(rng, n, None) for _ in range(P)]
+    jc = SecaggCrypter()
+    cts = []
+    for p in range(P):
+        got = jc.encrypt(P, tau, xs[p], keys[p], W.BIPRIME0, weight=ws[p])
+        if p in (0, P - 1):
+            assert got == O.jl_encrypt(xs[p], tau, keys[p], W.BIPRIME0, P, weight=ws[p]), p
+        cts.append(got)
+    out = jc.aggregate(tau, P, cts, -sum(keys), W.BIPRIME0, sum(ws), num_expected_params=n)
+    ref = O.jl_crypter_aggregate(cts, tau, -sum(keys), W.BIPRIME0, sum(ws), n)
+    assert _bits(out) == _bits(ref)
