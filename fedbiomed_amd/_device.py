@@ -13,9 +13,10 @@ from __future__ import annotations
 
 import array
 import ctypes
-import os
 import logging
 import math
+import os
+import threading
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -87,14 +88,21 @@ class deferred_checks:
                     cts[p] = D.jl_encrypt(...)
     """
 
-    _active: List[list] = []
+    _tls = threading.local()  # per thread: another thread's calls keep their own checks
+
+    @staticmethod
+    def _stack() -> List[list]:
+        st = getattr(deferred_checks._tls, "stack", None)
+        if st is None:
+            st = deferred_checks._tls.stack = []
+        return st
 
     def __enter__(self):
-        deferred_checks._active.append([])
+        deferred_checks._stack().append([])
         return self
 
     def __exit__(self, exc_type, exc, tb):
-        pending = deferred_checks._active.pop()
+        pending = deferred_checks._stack().pop()
         if exc_type is None and pending:
             torch.cuda.synchronize()  # the status words were written on other streams
             host = torch.stack([st for st, _ in pending]).cpu().numpy()  # one copy for all of them
@@ -104,8 +112,9 @@ class deferred_checks:
 
 
 def _check_stats_or_defer(stats: torch.Tensor, lom_nodes: int = 0) -> None:
-    if deferred_checks._active:
-        deferred_checks._active[-1].append((stats, lom_nodes))
+    active = deferred_checks._stack()
+    if active:
+        active[-1].append((stats, lom_nodes))
     else:
         _check_stats(stats, lom_nodes)
 

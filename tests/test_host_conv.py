@@ -121,3 +121,23 @@ def test_bytes_to_ints_word_path_edges():
     got = m.bytes_to_ints(blob, 256)
     assert got == vals and all(type(v) is int for v in got)
     assert m.bytes_to_ints(b"\x05\0\0", 3) == [5]  # byte path (width not a word multiple)
+
+
+def test_deferred_checks_are_per_thread():
+    """A status word deferred inside one thread's `deferred_checks` (the list aggregate issues
+    its decryption factor that way) never lands in another thread's context."""
+    import threading
+
+    seen = {}
+    with D.deferred_checks():
+        D.deferred_checks._stack()[-1].append(("main", 0))
+
+        def other():
+            seen["other"] = list(D.deferred_checks._stack())
+
+        t = threading.Thread(target=other)
+        t.start()
+        t.join()
+        assert len(D.deferred_checks._stack()[-1]) == 1
+        D.deferred_checks._stack()[-1].clear()  # nothing to check at exit (no device here)
+    assert seen["other"] == [] and D.deferred_checks._stack() == []
