@@ -4,6 +4,8 @@
 // (16 independent 64-bit accumulators per lane), carry-out to
 //   mode 0: vcc for every multiply (as the engine)
 //   mode 1: 16 distinct SGPR pairs, one per accumulator
+//   mode 2: as mode 1, every other multiply taking its multiplicand from an SGPR (the
+//           engine's q*N_k rows read N_k from SGPRs)
 // Prints cycles per wave-instruction (s_memtime) per mode and waves per SIMD.
 //   hipcc --offload-arch=gfx950 -O3 tools/microbench/madsdst.hip -o tools/microbench/madsdst
 #include <hip/hip_runtime.h>
@@ -22,6 +24,9 @@
     }                                                                       \
   } while (0)
 
+#define MAD_SS(c, LO, HI)                                                                   \
+  asm volatile("v_mad_u64_u32 %0, s[" #LO ":" #HI "], %1, %2, %0" : "+v"(acc[c]) : "v"(a + c), "s"(sb) \
+               : "s" #LO, "s" #HI)
 #define MAD_S(c, LO, HI)                                                                    \
   asm volatile("v_mad_u64_u32 %0, s[" #LO ":" #HI "], %1, %2, %0" : "+v"(acc[c]) : "v"(a + c), "v"(b) \
                : "s" #LO, "s" #HI)
@@ -29,6 +34,7 @@
 template <int MODE>
 __global__ void k_mad(uint64_t* out, uint64_t* cyc, uint32_t s, int iters) {
   uint32_t a = threadIdx.x + s, b = blockIdx.x * 7 + s;
+  const uint32_t sb = __builtin_amdgcn_readfirstlane(b) + 3u;
   uint64_t acc[NACC];
 #pragma unroll
   for (int c = 0; c < NACC; ++c) acc[c] = c + a;
@@ -40,6 +46,11 @@ __global__ void k_mad(uint64_t* out, uint64_t* cyc, uint32_t s, int iters) {
 #pragma unroll
         for (int c = 0; c < NACC; ++c)
           asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc[c]) : "v"(a + c), "v"(b) : "vcc");
+      } else if (MODE == 2) {
+        MAD_S(0, 40, 41); MAD_SS(1, 42, 43); MAD_S(2, 44, 45); MAD_SS(3, 46, 47);
+        MAD_S(4, 48, 49); MAD_SS(5, 50, 51); MAD_S(6, 52, 53); MAD_SS(7, 54, 55);
+        MAD_S(8, 56, 57); MAD_SS(9, 58, 59); MAD_S(10, 60, 61); MAD_SS(11, 62, 63);
+        MAD_S(12, 64, 65); MAD_SS(13, 66, 67); MAD_S(14, 68, 69); MAD_SS(15, 70, 71);
       } else {
         MAD_S(0, 40, 41); MAD_S(1, 42, 43); MAD_S(2, 44, 45); MAD_S(3, 46, 47);
         MAD_S(4, 48, 49); MAD_S(5, 50, 51); MAD_S(6, 52, 53); MAD_S(7, 54, 55);
@@ -84,7 +95,7 @@ void run(int cus, int iters) {
     const double lane_ops = (double)blocks * threads * instr;
     printf("{\"mode\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.3f, \"cyc_per_wave_instr\": %.3f, "
            "\"clock_GHz\": %.3f, \"T_lane_mad_s\": %.2f}\n",
-           MODE == 0 ? "vcc" : "sgpr-pairs", waves, ms, avg / instr, avg / (ms * 1e-3) / 1e9,
+           MODE == 0 ? "vcc" : MODE == 1 ? "sgpr-pairs" : "sgpr-pairs+sgpr-src", waves, ms, avg / instr, avg / (ms * 1e-3) / 1e9,
            lane_ops / (ms * 1e-3) / 1e12);
     CHK(hipFree(d));
     CHK(hipFree(c));
@@ -100,5 +111,6 @@ int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 20000;
   run<0>(p.multiProcessorCount, iters);
   run<1>(p.multiProcessorCount, iters);
+  run<2>(p.multiProcessorCount, iters);
   return 0;
 }
