@@ -440,6 +440,7 @@ __device__ __forceinline__ void fbm_na_mm_glb(uint32_t a_off, const uint32_t* bb
       : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
 }}
 
+#ifndef FBM_NA_PLAIN_SQUARE
 // a <- a^2 R^-1 (mod N^2): triangular x0^2 (computed-jump row suffixes), full x0 * 2 x1.
 __device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK, uint32_t np) {{
   asm volatile(
@@ -448,6 +449,17 @@ __device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK
       : [a] "v"(a_off), [NK] "s"(NK), [np] "s"(np)
       : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
 }}
+#else
+// A/B variant (-DFBM_NA_PLAIN_SQUARE): the general product with B = A from LDS -- no computed
+// jumps, {L * count_mads(row(False, True))} multiplies instead of {sq_mads()}.
+__device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK, uint32_t np) {{
+  asm volatile(
+{c_string(product(True))}
+      :
+      : [a] "v"(a_off), [NK] "s"(NK), [np] "s"(np)
+      : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
+}}
+#endif
 """
     with open(OUT, "w") as f:
         f.write(hdr)
