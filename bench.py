@@ -7,11 +7,17 @@ vector @1/8 GPU".  One step = every party encrypts its device-resident parameter
 aggregate (ciphertext product, server-key exponentiation, inverse, unmask, decode, average,
 dequantise).  value = params processed by all ranks / wall time of K steps (max over ranks).
 
-Scaling: element-range sharding with no data-path collective (fedbiomed_amd/distributed.py):
-each rank owns one 10M-element stripe (global offsets), so per-GPU work is fixed -> "weak".
-`--strong` splits a fixed total instead.
+Scaling: element-range sharding with no data-path collective (fedbiomed_amd/distributed.py).
+Default "strong": ONE 10M-element vector (config 4) is split into N stripes, one per GPU, each
+processed with its global offsets -- the total work is fixed as N grows.  `--weak` gives every
+rank its own --elements stripe instead.  `stages` reports T_enc (all P parties' encrypts),
+T_agg (the aggregate alone: decryption factor + combine), P*N/T_enc and N/T_agg.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--scheme jl|lom] [--elements 10000000] [--parties 8]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scheme jl|lom] [--elements 10000000]
+                    [--parties 8] [--weak]
+
+With --gpus N > 1 and no torch.distributed.run environment, bench.py starts the N rank
+processes itself (before anything touches a GPU) and relays rank 0's line.
 """
 
 import argparse
@@ -96,9 +102,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scheme", choices=["jl", "lom"], default="jl")
     ap.add_argument("--elements", "--n", dest="n", type=int, default=10_000_000,
-                    help="elements per GPU (weak) or total (--strong)")
+                    help="elements in total (strong, the default) or per GPU (--weak)")
     ap.add_argument("--parties", type=int, default=8)
-    ap.add_argument("--strong", action="store_true")
+    ap.add_argument("--weak", action="store_true", help="every rank owns its own --elements stripe")
+    ap.add_argument("--strong", action="store_true", help="(the default) split --elements over the ranks")
+    ap.add_argument("--no-stages", action="store_true", help="skip the per-stage T_enc / T_agg timing")
     ap.add_argument("--cpu-sample", type=int, default=None, help="elements in the timed CPU-oracle sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-lom-extra", action="store_true")
@@ -116,8 +124,40 @@ def parse():
     return ap.parse_args()
 
 
+def spawn_ranks(n: int) -> int:
+    """--gpus N without a torch.distributed.run environment: start the N rank processes here,
+    before this process touches a GPU (it never initialises HIP), and wait for them.  A rank
+    that fails ends the others (by PID) so no rank waits forever in a collective."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in procs:
+                    q.kill()
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     import torch
 
     from fedbiomed_amd import _device as D, _native, distributed, workload as W
@@ -138,7 +178,8 @@ def main():
     es, cr = D.jl_slot(None, P)
 
     # ---- this rank's stripe (global element offset) ----
-    if args.strong:
+    strong = not args.weak
+    if strong:
         align = cr if args.scheme == "jl" else 8
         lo, hi = distributed.shard_range(args.n, world, rank, align)
         n_total = args.n
@@ -165,10 +206,18 @@ def main():
     factor_stream = torch.cuda.Stream(device=dev)
     overlap_factor = not args.no_factor_overlap
 
+    def engine_ctx(mode):
+        """JL exponentiation engine for the launches issued inside (library policy otherwise):
+        the step's P + 1 concurrent exponentiations fill the chip together, so they take the
+        throughput engine (one lane per ciphertext) even when each alone would be small."""
+        import contextlib
+
+        return D.jl_engine(mode) if hasattr(D, "jl_engine") else contextlib.nullcontext()
+
     def step_jl(serial=False):
         cts = [None] * P
         factor = None
-        with D.deferred_checks():
+        with D.deferred_checks(), engine_ctx("single"):
             if args.no_prologue_first:
                 if overlap_factor:
                     f_s = main if serial else factor_stream
@@ -296,7 +345,7 @@ def main():
     line = {
         "metric": "params/s secagg encrypt+aggregate (device-resident), 10M-elem vector @1/8 GPU",
         "value": value, "unit": "params/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong" if args.strong else "weak",
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong" if strong else "weak",
         "vs_baseline": None, "dtype": "u32-limb bigint (JL) / u64 (LOM); f32 in, f64 out",
         "data": "synthetic (float32 N(0,0.05^2) + 0.1% +/-4.0 outliers per party; biprime0; random 2040-bit keys)",
         "config": {"workload": f"{'Joye-Libert' if args.scheme == 'jl' else 'LOM'} encrypt (all {P} parties) + "
@@ -318,6 +367,85 @@ def main():
                                          "above); "
                                          "achieved/frac: serialised jl_exp launches (HIP events); step_*: the "
                                          "timed step (parties on concurrent streams, all kernels)"}
+
+    # ---- per-stage times: T_enc = all P parties' encrypts as the step issues
+    #      them, T_agg = the aggregate alone (decryption factor + combine, nothing overlapped);
+    #      each the median of a few runs, max over ranks ----
+    if not args.no_stages:
+        def t_stage(fn, reps=3):
+            fn()
+            ts = []
+            for _ in range(reps):
+                if world > 1:
+                    torch.distributed.barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            t = torch.tensor([sorted(ts)[len(ts) // 2]], dtype=torch.float64, device=dev)
+            if world > 1:
+                torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            return t.item()
+
+        if args.scheme == "jl":
+            def enc_all():
+                cts = [None] * P
+                with D.deferred_checks(), engine_ctx("single"):
+                    pend = [None] * P
+                    for p in range(P):
+                        streams[p].wait_stream(main)
+                        with torch.cuda.stream(streams[p]):
+                            pend[p] = jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=weights[p],
+                                                        ct_offset=lo // cr, defer_exp=True)
+                    for st in pool:
+                        main.wait_stream(st)
+                    for st in pool:
+                        st.wait_stream(main)
+                    for p in range(P):
+                        with torch.cuda.stream(streams[p]):
+                            cts[p] = pend[p].finish()
+                for st in pool:
+                    main.wait_stream(st)
+                for c in cts:
+                    c.record_stream(main)
+                return torch.stack(cts)
+
+            cts_all = enc_all()
+
+            def agg_alone(k=n_ct, ne=n):
+                part = cts_all if k == n_ct else cts_all[:, :k].contiguous()
+                return jc.aggregate_tensor(tau, part, sk0, W.BIPRIME0, total_w, num_expected_params=ne,
+                                           ct_offset=lo // cr)
+
+            t_enc, t_agg = t_stage(enc_all), t_stage(agg_alone)
+        else:
+            def enc_all():
+                with D.deferred_checks():
+                    for p, u in enumerate(ids):
+                        lc.encrypt_tensor(tau, u, xs[p], secrets_[p], ids, weight=weights[p], elem_offset=lo,
+                                          out=Y[p])
+
+            t_enc = t_stage(enc_all)
+            t_agg = t_stage(lambda: lc.aggregate_tensor(Y, total_w))
+        line["stages"] = {"T_enc_ms": 1000 * t_enc, "T_agg_ms": 1000 * t_agg,
+                          "enc_party_params_per_s": P * n_total / t_enc, "agg_params_per_s": n_total / t_agg,
+                          "note": "T_enc: all parties' encrypts (one stream each), T_agg: one aggregate alone "
+                                  "(decryption factor + combine); max over ranks; rates over elements_total"}
+        if args.scheme == "jl" and world == 1:
+            # strong-scaling probe of the aggregate step on this GPU: T_agg of the stripe rank 0
+            # of an 8-GPU split owns (the first ceil(n/8/cr) ciphertexts: ciphertext k depends
+            # only on its global index) against T_agg of the whole vector
+            hi8 = distributed.shard_range(n, 8, 0, cr)[1]
+            k8 = (hi8 + cr - 1) // cr
+            t8 = t_stage(lambda: agg_alone(k8, hi8))
+            line["stages"]["agg_scaling_probe"] = {
+                "stripe_elements": hi8, "stripe_ciphertexts": k8, "T_agg_stripe_ms": 1000 * t8,
+                "ratio_whole_over_stripe": t_agg / t8,
+                "note": "T_agg(whole vector) / T_agg(1/8 stripe) on one GPU: the aggregate step's 8-GPU "
+                        "strong-scaling bound (north star: >= 6x)"}
+        if args.scheme == "jl":
+            del cts_all
 
     # ---- secondary: LOM at the same size (cheap), so both schemes are on record ----
     if args.scheme == "jl" and not args.no_lom_extra:

@@ -103,18 +103,29 @@ class deferred_checks:
 
     def __exit__(self, exc_type, exc, tb):
         pending = deferred_checks._stack().pop()
-        if exc_type is None and pending:
-            torch.cuda.synchronize()  # the status words were written on other streams
-            host = torch.stack([st for st, _ in pending]).cpu().numpy()  # one copy for all of them
-            for (_, nodes), row in zip(pending, host):
+        if not pending:
+            return False
+        # wait for the streams that wrote the status words only (an event recorded after
+        # each), not the whole device: other threads' work keeps running
+        for _, _, ev in pending:
+            ev.synchronize()
+        host = torch.stack([st for st, _, _ in pending]).cpu().numpy()  # one copy for all of them
+        try:
+            for (_, nodes, _), row in zip(pending, host):
                 _check_stats_host(row, nodes)
+        except Exception as dev_err:
+            if exc is not None:  # the device condition came first: surface it, chained
+                raise dev_err from exc
+            raise
         return False
 
 
 def _check_stats_or_defer(stats: torch.Tensor, lom_nodes: int = 0) -> None:
     active = deferred_checks._stack()
     if active:
-        active[-1].append((stats, lom_nodes))
+        ev = torch.cuda.Event()
+        ev.record()  # on the current stream, right after the kernels that write `stats`
+        active[-1].append((stats, lom_nodes, ev))
     else:
         _check_stats(stats, lom_nodes)
 
@@ -191,16 +202,55 @@ def int_limbs(v: int, n_limbs: int) -> np.ndarray:
 # ------------------------------------------------------------------------------------------
 # list <-> tensor conversions (the host-memory boundary, measured in DESIGN.md)
 # ------------------------------------------------------------------------------------------
+class _PyConvFallback:
+    """Pure-Python versions of csrc/fbm_pyconv.c's three loops (same contracts), used when
+    the C module is not built for this interpreter.  Host list <-> buffer conversions only:
+    no secagg arithmetic happens here."""
+
+    @staticmethod
+    def floats_to_f64(seq: list, out: np.ndarray) -> int:
+        if out.nbytes != 8 * len(seq):
+            raise ValueError(f"output buffer holds {out.nbytes} bytes, {8 * len(seq)} needed")
+        for i, v in enumerate(seq):
+            if not isinstance(v, float):
+                return i
+        out[:] = np.asarray(seq, dtype=np.float64) if seq else out[:0]
+        return -1
+
+    @staticmethod
+    def ints_to_bytes(seq: list, nb: int, out: np.ndarray) -> int:
+        if nb <= 0:
+            raise ValueError("width must be positive")
+        if out.nbytes != nb * len(seq):
+            raise ValueError(f"output buffer holds {out.nbytes} bytes, {nb * len(seq)} needed")
+        dst = out.reshape(-1).view(np.uint8)
+        for i, v in enumerate(seq):
+            if not isinstance(v, int) or v < 0 or v.bit_length() > 8 * nb:
+                return i
+            dst[i * nb:(i + 1) * nb] = np.frombuffer(v.to_bytes(nb, "little"), dtype=np.uint8)
+        return -1
+
+    @staticmethod
+    def bytes_to_ints(buf, nb: int) -> list:
+        b = memoryview(buf).cast("B").tobytes()
+        if nb <= 0 or len(b) % nb:
+            raise ValueError("buffer is not a whole number of values")
+        return [int.from_bytes(b[i:i + nb], "little") for i in range(0, len(b), nb)]
+
+
 def _pyconv():
-    """The list API's C conversion loops (csrc/fbm_pyconv.c), built in-tree by _build."""
+    """The list API's C conversion loops (csrc/fbm_pyconv.c), built in-tree by _build; the
+    pure-Python equivalents when the module is absent (not built for this interpreter)."""
     global _PYCONV
     if _PYCONV is None:
         import importlib.util
 
         from ._build import PYCONV_OUT
 
-        if not os.path.exists(PYCONV_OUT):
-            raise N.NativeUnavailable(f"{PYCONV_OUT} is not built (python -m fedbiomed_amd._build)")
+        if not os.path.exists(PYCONV_OUT) or os.environ.get("FBM_NO_PYCONV"):
+            logger.info("fedbiomed_amd: %s not built; list conversions run in Python", PYCONV_OUT)
+            _PYCONV = _PyConvFallback
+            return _PYCONV
         spec = importlib.util.spec_from_file_location("_fbm_pyconv", PYCONV_OUT)
         mod = importlib.util.module_from_spec(spec)
         spec.loader.exec_module(mod)
@@ -306,9 +356,10 @@ def _nonce_block(nonce: bytes) -> np.ndarray:
 
 def lom_protect(x: torch.Tensor, secrets: Sequence[bytes], signs: Sequence[int], nonce: bytes, tau: int,
                 n_nodes: int, clip=None, target=None, weight: int = 1, raw_seeds: bool = False,
-                elem_offset: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                elem_offset: int = 0, out: Optional[torch.Tensor] = None, check_now: bool = False) -> torch.Tensor:
     """One party's masked vector (u64 bit patterns in an int64 tensor); raises the
-    reference's LOM overflow error when max(bit_length(q*w)) >= 64 - ceil(log2(n_nodes))."""
+    reference's LOM overflow error when max(bit_length(q*w)) >= 64 - ceil(log2(n_nodes)).
+    check_now: check the status word before returning even inside `deferred_checks`."""
     dev = x.device
     lib = N.load()
     target = target or SAParameters.TARGET_RANGE
@@ -330,7 +381,10 @@ def lom_protect(x: torch.Tensor, secrets: Sequence[bytes], signs: Sequence[int],
     _call(lib.fbm_lom_protect, _ptr(x), _x_dtype(x), n, c, c2, tf, tm1, int(weight), _np_ptr(sec), _np_ptr(sg),
           len(secrets), 1 if raw_seeds else 0, _np_ptr(nb), int(tau), int(elem_offset), _ptr(y), _ptr(st),
           _stream())
-    _check_stats_or_defer(st, lom_nodes=n_nodes)
+    if check_now:
+        _check_stats(st, n_nodes)
+    else:
+        _check_stats_or_defer(st, lom_nodes=n_nodes)
     return y
 
 
@@ -447,7 +501,7 @@ def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, 
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value}: a deferred encrypt takes at most {chunk} ciphertexts")
         st = _stats(dev)
-        args = (_ptr(x), _x_dtype(x), n, c, c2, tf, tm1, int(weight), es, cr, _np_ptr(bp), _np_ptr(kl), kneg,
+        args = (_ptr(x), _x_dtype(x), n, c, c2, tf, tm1, int(weight) & U64_MAX, es, cr, _np_ptr(bp), _np_ptr(kl), kneg,
                 int(tau), int(ct_offset), _ptr(ct), _ptr(ws), _ptr(st))
         _call(lib.fbm_jl_encrypt_phase, *args, _stream(), 1)
         return PendingEncrypt(args, ct, (ws, x, bp, kl), st)
@@ -455,7 +509,7 @@ def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, 
         k1 = min(n_ct, k0 + chunk)
         xs = x[k0 * cr:min(n, k1 * cr)]
         st = _stats(dev)  # one status word per call (each call zeroes its own)
-        _call(lib.fbm_jl_encrypt, _ptr(xs), _x_dtype(x), xs.numel(), c, c2, tf, tm1, int(weight), es, cr,
+        _call(lib.fbm_jl_encrypt, _ptr(xs), _x_dtype(x), xs.numel(), c, c2, tf, tm1, int(weight) & U64_MAX, es, cr,
               _np_ptr(bp), _np_ptr(kl), kneg, int(tau), int(ct_offset) + k0, _ptr(ct[k0:k1]), _ptr(ws), _ptr(st),
               _stream())
         _check_stats_or_defer(st)

@@ -242,6 +242,20 @@ static int build_jl_params(const uint32_t* biprime, int es, int cr, uint64_t tau
     memcpy(jp.Ninv32, y, sizeof(y));
   }
   jp.n_bits = nb;
+  {  // M = N << (1036 - nb): 0 mod N, in [2^1035, 2^1036) (negative-weight nude digit)
+    Big m(N.begin(), N.end());
+    m.resize(34, 0u);
+    const int sh = FBM_NLN * FBM_LB - nb;
+    for (int i = 0; i < sh; ++i) {
+      uint32_t c = 0;
+      for (size_t k = 0; k < m.size(); ++k) {
+        const uint32_t nc = m[k] >> 31;
+        m[k] = (m[k] << 1) | c;
+        c = nc;
+      }
+    }
+    to28_host(m, jp.mneg, FBM_NLN);
+  }
   fbm_n30_setup(jp.N32, jp.n30);
   jp.es = es;
   jp.cr = cr;
@@ -549,6 +563,10 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
     set_error("null pointer argument");
     return FBM_E_ARG;
   }
+  if ((int64_t)weight <= -(int64_t)(1 << 17)) {  // negative: the two's complement of a weight > -2^17
+    set_error("negative weight %lld outside (-2^17, 0)", (long long)(int64_t)weight);
+    return FBM_E_ARG;
+  }
   JlParams jp;
   if ((rc = build_jl_params(biprime, es, cr, tau, ct_offset, jp))) return rc;
   JlSched sc;
@@ -579,7 +597,8 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
   if (phase & 1) {
     if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s); }))) return rc;
     if ((rc = timed("jl_pack", s, [&] { return launch_jl_pack(x, x_dtype, n, qp, weight, es, cr, n_ct, pt, stats, s); }))) return rc;
-    if ((rc = timed("jl_nude", s, [&] { return launch_jl_nude(pt, n_ct, jp, nude, s); }))) return rc;
+    const int negw = (int64_t)weight < 0 ? 1 : 0;
+    if ((rc = timed("jl_nude", s, [&] { return launch_jl_nude(pt, n_ct, jp, negw, nude, s); }))) return rc;
     if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, H, stats, s); }))) return rc;
     if (inverse) {
       // gmpy2.powmod with a negative exponent (_jls.py:60-73): invert H(t_k) mod N^2 first,

@@ -108,11 +108,14 @@ struct JlParams {
   FbmN30 n30;                    // N in signed-30 limbs + N^-1 mod 2^30 (modular inverse)
   int key_is_zero;
   int pad;
+  uint32_t mneg[FBM_NLN];        // N * 2^(1036 - bits(N)) in 28-bit limbs (negative-weight packing)
+  uint32_t pad2[3];
 };
 
 int launch_jl_pack(const void* x, int x_dtype, uint64_t n, const QuantParams& qp, uint64_t weight, int es, int cr,
                    uint64_t n_ct, uint32_t* pt, uint32_t* stats, hipStream_t s);
-int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, uint32_t* nude, hipStream_t s);
+int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, int negative, uint32_t* nude,
+                   hipStream_t s);
 int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s);
 int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32_t* cst, hipStream_t s);
 int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const JlSched& sc, int mode,
@@ -144,5 +147,7 @@ int launch_ass_reconstruct_wide(const uint32_t* shares, int n_shares, int l, uin
 
 // table slots the encrypt/aggregate kernels need for a given grid
 uint64_t jl_table_slots();
+// compute units of the calling thread's current device (cached per device)
+int device_num_cu();
 
 }  // namespace fbm

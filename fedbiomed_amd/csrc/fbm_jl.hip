@@ -18,6 +18,8 @@
 // HBM layouts: 32-bit-limb integers are row-major [ct][words] (pt: 32 words, H / E / inv /
 // ciphertexts: 64 words = int.to_bytes(256,'little')); 28-bit-limb residues (nude, X) and
 // the per-lane exponent tables are limb-major [limb][lane] so a wave's accesses coalesce.
+#include <atomic>
+
 #include "fbm_internal.hpp"
 #include "fbm_mont_asm.hpp"
 #include "fbm_nadic_asm.hpp"
@@ -57,14 +59,37 @@ __global__ void __launch_bounds__(256) jl_pack_kernel(const XT* __restrict__ x, 
   const uint64_t first = ct * (uint64_t)cr;
   const int cnt = (n - first) >= (uint64_t)cr ? cr : (int)(n - first);
   const int lo_bit = 32 * L;
-  int j0 = lo_bit / es, j1 = (lo_bit + 31) / es;
-  if (j1 > cnt - 1) j1 = cnt - 1;
   uint32_t w = 0;
-  for (int j = j0; j <= j1; ++j) {
-    const uint64_t q = jl_input<XT>(x, first + j, qp, clipped);
-    const unsigned __int128 v = (unsigned __int128)q * weight;
-    const int sh = es * j - lo_bit;
-    w |= sh >= 0 ? (uint32_t)(v << sh) : (uint32_t)(v >> (-sh));
+  if ((int64_t)weight >= 0) {
+    int j0 = lo_bit / es, j1 = (lo_bit + 31) / es;
+    if (j1 > cnt - 1) j1 = cnt - 1;
+    for (int j = j0; j <= j1; ++j) {
+      const uint64_t q = jl_input<XT>(x, first + j, qp, clipped);
+      const unsigned __int128 v = (unsigned __int128)q * weight;
+      const int sh = es * j - lo_bit;
+      w |= sh >= 0 ? (uint32_t)(v << sh) : (uint32_t)(v >> (-sh));
+    }
+  } else {
+    // Negative weight (the reference accepts it: _secagg_crypter.py:106-112 only bounds its bit
+    // length).  VES._batch ORs the slots (_jls.py:169-176): in two's complement the first
+    // non-zero slot v_j* = q_j* w < 0 has all bits above its own set, so the packing is exactly
+    // v_j* << (es j*) (0 if every q is 0).  Here pt = |v_j*| << (es j*); jl_nude_kernel makes the
+    // digit of N*pt + 1 from it with the sign (kernel argument).
+    const uint64_t aw = 0ull - weight;
+    uint64_t qs = 0;
+    int js = -1;
+    for (int j = 0; j < cnt; ++j) {
+      const uint64_t q = jl_input<XT>(x, first + j, qp, clipped);
+      if (js < 0 && q != 0) {
+        js = j;
+        qs = q;
+      }
+    }
+    if (js >= 0) {
+      const unsigned __int128 v = (unsigned __int128)qs * aw;
+      const int sh = es * js - lo_bit;
+      w = sh >= 0 ? (sh < 32 ? (uint32_t)(v << sh) : 0u) : (-sh < 128 ? (uint32_t)(v >> (-sh)) : 0u);
+    }
   }
   pt[ct * 32 + L] = w;
   flag_if_any(clipped, stats, FBM_WARN_CLIPPED);
@@ -74,8 +99,11 @@ __global__ void __launch_bounds__(256) jl_pack_kernel(const XT* __restrict__ x, 
 // nude = N*pt + 1 as the N-adic digit pair (1, pt)  ->  [limb][ct] 28-bit limbs (the last
 // operand of jl_exp_kernel's encrypt; pt < 2^1024 < R is a valid one-off digit)
 // ------------------------------------------------------------------------------------
+// negative != 0 (a negative weight, see jl_pack_kernel): pt holds |pt| and N*pt + 1 is
+// (1, M - |pt|) with M = N * 2^(1036 - bits(N)) = 0 (mod N): 2^1035 <= M < R, so the digit is
+// non-negative and below R for every |pt| < 2^1024.
 __global__ void __launch_bounds__(256) jl_nude_kernel(const uint32_t* __restrict__ pt, uint64_t n_ct, JlParams jp,
-                                                      uint32_t* __restrict__ nude) {
+                                                      int negative, uint32_t* __restrict__ nude) {
   const uint64_t ct = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (ct >= n_ct) return;
   uint32_t p32[32];
@@ -87,6 +115,15 @@ __global__ void __launch_bounds__(256) jl_nude_kernel(const uint32_t* __restrict
   }
   uint32_t p28[FBM_NLN];
   to28<32, FBM_NLN>(p32, p28);
+  if (negative) {
+    int32_t br = 0;
+#pragma unroll
+    for (int k = 0; k < FBM_NLN; ++k) {
+      const int32_t v = (int32_t)jp.mneg[k] - (int32_t)p28[k] + br;
+      p28[k] = (uint32_t)v & FBM_LMASK;
+      br = v >> FBM_LB;
+    }
+  }
   // N*pt + 1 in N-adic digits is (1, pt): no arithmetic, only the layout of the
   // exponentiation's B operand (blocked column, digit 0 in limbs 0..36, digit 1 in 37..73)
   uint32_t* dst = launder_v(nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255));
@@ -1015,19 +1052,29 @@ __global__ void __launch_bounds__(256) jl_decode_kernel(const uint32_t* __restri
 // ------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------
-static int g_num_cu = 0;
+// CU count of the calling thread's current device, cached per device (a process may drive
+// several devices from several threads; 0 = not yet queried, written once per device).
+#define FBM_MAX_DEVICES 64
+static std::atomic<int> g_num_cu[FBM_MAX_DEVICES];
+
+int device_num_cu() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  if (dev >= FBM_MAX_DEVICES) dev = FBM_MAX_DEVICES - 1;
+  int n = g_num_cu[dev].load(std::memory_order_relaxed);
+  if (n <= 0) {
+    hipDeviceProp_t prop;
+    n = (hipGetDeviceProperties(&prop, dev) == hipSuccess) ? prop.multiProcessorCount : 0;
+    if (n <= 0) n = 256;
+    g_num_cu[dev].store(n, std::memory_order_relaxed);
+  }
+  return n;
+}
 
 uint64_t jl_table_slots() {
-  if (!g_num_cu) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-      g_num_cu = prop.multiProcessorCount;
-    if (g_num_cu <= 0) g_num_cu = 256;
-  }
   // two workgroups of FBM_BLOCK lanes per CU: 2 waves/SIMD (244 VGPRs per lane in the
   // assembly product; 2 x 75 KB LDS columns per CU)
-  return (uint64_t)g_num_cu * 2 * FBM_BLOCK;
+  return (uint64_t)device_num_cu() * 2 * FBM_BLOCK;
 }
 
 static inline dim3 grid1(uint64_t items, unsigned block) { return dim3((unsigned)((items + block - 1) / block)); }
@@ -1047,9 +1094,10 @@ int launch_jl_pack(const void* x, int x_dtype, uint64_t n, const QuantParams& qp
   return check_launch("jl_pack_kernel");
 }
 
-int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, uint32_t* nude, hipStream_t s) {
+int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, int negative, uint32_t* nude,
+                   hipStream_t s) {
   if (n_ct == 0) return FBM_OK;
-  hipLaunchKernelGGL(jl_nude_kernel, grid1(n_ct, 256), dim3(256), 0, s, pt, n_ct, jp, nude);
+  hipLaunchKernelGGL(jl_nude_kernel, grid1(n_ct, 256), dim3(256), 0, s, pt, n_ct, jp, negative, nude);
   return check_launch("jl_nude_kernel");
 }
 

@@ -19,12 +19,26 @@
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
-#include <longintrepr.h>
+#if PY_VERSION_HEX < 0x030B0000
+#include <longintrepr.h> /* 3.11 moved it to cpython/longintrepr.h, which Python.h includes */
+#endif
 #include <pthread.h>
 #include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
 
+/* The digit-level fast paths read CPython's PyLongObject layout (ob_digit, Py_SIZE as the
+ * signed digit count), which holds up to 3.11; 3.12 changed it (long_value.ob_digit, lv_tag).
+ * From 3.12 on the conversions go through the byte-array API instead, on one thread. */
+#ifndef FBM_DIGITS_FAST /* -DFBM_DIGITS_FAST=0 builds the portable path on any version (tested) */
+#if PY_VERSION_HEX < 0x030C0000
+#define FBM_DIGITS_FAST 1
+#else
+#define FBM_DIGITS_FAST 0
+#endif
+#endif
+
+#if FBM_DIGITS_FAST
 /* Non-negative int -> nb little-endian bytes (nb a multiple of 4) straight from CPython's
  * 30-bit digits; 0 on success, -1 if negative or too wide.  _PyLong_AsByteArray gives the
  * same bytes but goes byte by byte (~4x slower on 2048-bit values). */
@@ -52,6 +66,25 @@ static int long_to_words(PyLongObject* v, unsigned char* dst, Py_ssize_t nb) {
     if (k == nw && acc >> 32) return -1;
     memset(w + k, 0, (size_t)(nw - k) * 4);
     return 0;
+}
+#endif
+
+/* Non-negative int -> nb little-endian bytes through the public/stable byte API (any
+ * version; the GIL must be held: it may set an exception, which is cleared). */
+static int long_to_bytes_api(PyObject* v, unsigned char* dst, Py_ssize_t nb) {
+    if (_PyLong_Sign(v) < 0) return -1;
+#if PY_VERSION_HEX >= 0x030D0000
+    Py_ssize_t need = PyLong_AsNativeBytes(v, dst, nb, Py_ASNATIVEBYTES_LITTLE_ENDIAN | Py_ASNATIVEBYTES_UNSIGNED_BUFFER);
+    if (need < 0) {
+        PyErr_Clear();
+        return -1;
+    }
+    return need <= nb ? 0 : -1;
+#else
+    int rc = _PyLong_AsByteArray((PyLongObject*)v, dst, (size_t)nb, 1, 0);
+    if (rc < 0) PyErr_Clear();
+    return rc;
+#endif
 }
 
 static int get_out(PyObject* obj, Py_buffer* view, Py_ssize_t need) {
@@ -97,6 +130,7 @@ typedef struct {
     Py_ssize_t lo, hi, nb, bad;
 } conv_job;
 
+#if FBM_DIGITS_FAST
 static void* conv_range(void* arg) {
     conv_job* j = (conv_job*)arg;
     j->bad = -1;
@@ -150,6 +184,7 @@ static Py_ssize_t ints_to_words_parallel(PyObject* seq, Py_ssize_t n, Py_ssize_t
     PyMem_Free(items);
     return bad;
 }
+#endif
 
 static PyObject* ints_to_bytes(PyObject* self, PyObject* args) {
     PyObject *seq, *out;
@@ -163,11 +198,17 @@ static PyObject* ints_to_bytes(PyObject* self, PyObject* args) {
     Py_buffer view;
     if (get_out(out, &view, n * nb) < 0) return NULL;
     unsigned char* dst = (unsigned char*)view.buf;
-    int words = nb % 4 == 0 && ((uintptr_t)dst & 3) == 0;
     Py_ssize_t bad = -1;
+#if FBM_DIGITS_FAST
+    int words = nb % 4 == 0 && ((uintptr_t)dst & 3) == 0;
     int nt = words && n * nb >= PAR_MIN_BYTES ? conv_threads(n) : 1;
+#else
+    int words = 0, nt = 1;
+#endif
     if (nt > 1) {
+#if FBM_DIGITS_FAST
         bad = ints_to_words_parallel(seq, n, nb, dst, nt);
+#endif
         if (bad == -2) {
             PyBuffer_Release(&view);
             return PyErr_NoMemory();
@@ -175,11 +216,16 @@ static PyObject* ints_to_bytes(PyObject* self, PyObject* args) {
     } else {
         for (Py_ssize_t i = 0; i < n; ++i) {
             PyObject* v = PyList_GET_ITEM(seq, i);
-            int rc = !PyLong_Check(v) ? -1
-                     : words ? long_to_words((PyLongObject*)v, dst + i * nb, nb)
-                             : _PyLong_AsByteArray((PyLongObject*)v, dst + i * nb, (size_t)nb, 1, 0);
-            if (rc < 0) {
-                PyErr_Clear(); /* OverflowError (negative or too wide): the caller's slow path */
+            int rc = -1;
+            if (PyLong_Check(v)) {
+#if FBM_DIGITS_FAST
+                rc = words ? long_to_words((PyLongObject*)v, dst + i * nb, nb) : long_to_bytes_api(v, dst + i * nb, nb);
+#else
+                (void)words;
+                rc = long_to_bytes_api(v, dst + i * nb, nb);
+#endif
+            }
+            if (rc < 0) { /* negative, too wide or not an int: the caller's slow path */
                 bad = i;
                 break;
             }
@@ -189,6 +235,15 @@ static PyObject* ints_to_bytes(PyObject* self, PyObject* args) {
     return PyLong_FromSsize_t(bad);
 }
 
+static PyObject* long_from_bytes_api(const unsigned char* src, Py_ssize_t nb) {
+#if PY_VERSION_HEX >= 0x030D0000
+    return PyLong_FromUnsignedNativeBytes(src, (size_t)nb, Py_ASNATIVEBYTES_LITTLE_ENDIAN);
+#else
+    return _PyLong_FromByteArray(src, (size_t)nb, 1, 0);
+#endif
+}
+
+#if FBM_DIGITS_FAST
 /* nw little-endian 32-bit words -> int, built straight in CPython's 30-bit digits
  * (_PyLong_FromByteArray goes byte by byte). */
 static PyObject* words_to_long(const uint32_t* w, Py_ssize_t nw) {
@@ -213,6 +268,7 @@ static PyObject* words_to_long(const uint32_t* w, Py_ssize_t nw) {
     }
     return (PyObject*)v;
 }
+#endif
 
 static PyObject* bytes_to_ints(PyObject* self, PyObject* args) {
     Py_buffer view;
@@ -227,10 +283,14 @@ static PyObject* bytes_to_ints(PyObject* self, PyObject* args) {
     PyObject* lst = PyList_New(n);
     if (lst) {
         const unsigned char* src = (const unsigned char*)view.buf;
-        int words = nb % 4 == 0 && ((uintptr_t)src & 3) == 0;
         for (Py_ssize_t i = 0; i < n; ++i) {
+#if FBM_DIGITS_FAST
+            const int words = nb % 4 == 0 && ((uintptr_t)src & 3) == 0;
             PyObject* v = words ? words_to_long((const uint32_t*)(src + i * nb), nb / 4)
-                                : _PyLong_FromByteArray(src + i * nb, (size_t)nb, 1, 0);
+                                : long_from_bytes_api(src + i * nb, nb);
+#else
+            PyObject* v = long_from_bytes_api(src + i * nb, nb);
+#endif
             if (!v) {
                 Py_CLEAR(lst);
                 break;

@@ -30,6 +30,10 @@ logger = logging.getLogger("fedbiomed_amd")
 
 
 def _check_weight(weight: Optional[int], jl: bool) -> None:
+    """The reference's only weight check (`_secagg_crypter.py:106-111` JL, `:367-372` LOM): the
+    bit length.  A negative weight passes it, as in the reference: JL then encrypts the
+    negative packing (`_jls.py:169-176`, reproduced on the device), LOM raises numpy's
+    OverflowError from its uint64 conversion (`_lom.py:153`, see SecaggLomCrypter)."""
     if weight is None:
         return
     if 2 ** weight.bit_length() > SAParameters.WEIGHT_RANGE:
@@ -40,9 +44,6 @@ def _check_weight(weight: Optional[int], jl: bool) -> None:
         raise FedbiomedSecaggCrypterError(
             f"{ErrorNumbers.FB624.value}: The weight is too large. The weight should be less than "
             f"{SAParameters.WEIGHT_RANGE}.")
-    if weight < 0:
-        raise FedbiomedSecaggCrypterError(
-            f"{ErrorNumbers.FB624.value}: Cannot apply weight to parameters, values outside of bounds")
 
 
 def _all_instances(values, cls) -> bool:
@@ -138,7 +139,9 @@ class SecaggCrypter:
         if not isinstance(key, int):
             raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: The argument `key` must be integer")
         target_range = target_range or SAParameters.TARGET_RANGE
-        D.quant_params(clipping_range, target_range)  # OverflowError / range checks as the reference
+        if params:  # quantize() evaluates nothing on an empty list, so it raises nothing there
+            D.quant_params(clipping_range, target_range)  # OverflowError / range checks as the reference
+        _check_weight(weight, jl=True)  # after quantize, before the (empty) protect: the reference's order
         if not params:
             return []
         x = host.to(D.device())
@@ -250,9 +253,24 @@ class SecaggLomCrypter(SecaggCrypter):
         if len(node_ids) == 0:
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value} Error during parameter encryption. math domain error")
-        return D.lom_protect(params, secrets_, signs, self._nonce, current_round, len(node_ids),
-                             clip=clipping_range, target=target_range, weight=1 if weight is None else weight,
-                             elem_offset=elem_offset, out=out)
+        if weight is None or weight >= 0:
+            return D.lom_protect(params, secrets_, signs, self._nonce, current_round, len(node_ids),
+                                 clip=clipping_range, target=target_range, weight=1 if weight is None else weight,
+                                 elem_offset=elem_offset, out=out)
+        # Negative weight: LOM.protect's overflow guard sees bit_length(q*w) == bit_length(q*|w|)
+        # (_lom.py:133-150), then np.array(x_u_tau, dtype=uint64) raises OverflowError at the
+        # first negative product (_lom.py:153; not wrapped by the crypter, which only catches
+        # TypeError / ValueError).  All-zero products pass and mask nothing but zeros.
+        y = D.lom_protect(params, secrets_, signs, self._nonce, current_round, len(node_ids),
+                          clip=clipping_range, target=target_range, weight=-weight, elem_offset=elem_offset,
+                          out=out, check_now=True)
+        q = D.lom_protect(params, [], [], bytes(16), 0, 0, clip=clipping_range, target=target_range, weight=1,
+                          check_now=True)
+        nz = torch.nonzero(q)
+        if nz.numel():
+            qv = int(q[int(nz[0, 0])].item()) & D.U64_MAX
+            raise OverflowError(f"Python integer {qv * weight} out of bounds for uint64")
+        return y
 
     def aggregate_tensor(self, Y: torch.Tensor, total_sample_size: int, clipping_range: Union[int, None] = None,
                          target_range: Optional[int] = None, want_sums: bool = False):
@@ -267,7 +285,9 @@ class SecaggLomCrypter(SecaggCrypter):
         start = time.process_time()
         host = _check_float_list(params)
         target_range = target_range or SAParameters.TARGET_RANGE
-        D.quant_params(clipping_range, target_range)
+        if params:  # quantize() evaluates nothing on an empty list
+            D.quant_params(clipping_range, target_range)
+        _check_weight(weight, jl=False)  # before LOM.protect's empty-input error, as the reference
         if not params:
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value} Error during parameter encryption. max() arg is an empty sequence")

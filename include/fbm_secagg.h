@@ -116,6 +116,9 @@ uint64_t fbm_jl_aggregate_workspace(uint64_t n_ct);
 /* JL encrypt of one party: quantise, weight, VES-pack, c_k = (N*pt_k+1) * H(t_k)^sk mod N^2.
  * Replaces SecaggCrypter.encrypt (_secagg_crypter.py:45-137) = quantize + _apply_weighting +
  * JoyeLibert.protect (_jls.py:593-644) + UserKey.encrypt (:473-505) + FDH.H (:727-762).
+ *   weight: the int64 two's complement of the multiplier; a negative weight in (-2^17, 0)
+ *           reproduces the reference's packing of negative products (VES._batch ORs the
+ *           slots, _jls.py:169-176: pt = the first non-zero q*w shifted to its slot)
  *   ct_out: device, n_ct x 64 uint32 limbs                                                */
 int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
                    uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,

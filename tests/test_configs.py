@@ -5,10 +5,16 @@
                                                                   oracle + exact decoded sums (all elements)
   cfg 3  LOM round of the 101 notebook's MNIST net, 4 nodes    -> one party bit-exact, mask cancellation
          (1,199,882 parameters)                     exact over all elements
+  cfg 4  JL encrypt+aggregate, 10M elements, 8 parties,       -> the 8 ct_offset stripes of an 8-GPU
+         element-range sharded across 8 GPUs                     split concatenate bit-exactly to the
+                                                                  whole vector, sampled ciphertexts bit-
+                                                                  exact vs the oracle, decoded sums exact
+                                                                  over all 10M elements, stripe aggregates
+                                                                  == whole aggregate, sampled float64
+                                                                  outputs bit-exact
   cfg 5  LOM masking + additive secret sharing, 100M elements, -> mask cancellation exact, sampled
          16 parties                                               windows bit-exact, split/reconstruct exact
-cfg 4 (JL 10M x 8 parties) is the bench workload; its element-range sharding is covered by
-tests/test_distributed.py.  Oracle = oracle/secagg_oracle.py (pinned to the reference's own
+Oracle = oracle/secagg_oracle.py (pinned to the reference's own
 vectors in tests/test_oracle_golden.py).  Tolerance: 0 -- integers compared exactly, float64
 outputs compared as bit patterns.
 """
@@ -127,6 +133,58 @@ def test_cfg3_lom_mnist_round_4_nodes(dev):
     idx = np.random.default_rng(3).choice(n, 5000, replace=False)
     refo = O.reverse_quantize(O.apply_average([int(v) for v in want[idx]], sum(ws)))
     assert np.array_equal(out.cpu().numpy()[idx].view(np.uint64), refo.view(np.uint64))
+
+
+def test_cfg4_jl_10m_8_parties_8_stripes(dev):
+    """Config 4 on one GPU: the whole 10M-element vector and the 8 stripes each rank of an
+    8-GPU element-range split owns (distributed.jl_shard, global ct_offset; reference
+    _jls.py:473-505 encrypt, :646-699 aggregate)."""
+    from fedbiomed_amd import distributed as Dd
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    n, P, tau, world = 10_000_000, 8, 1, 8
+    ws = [W.party_weight(p) for p in range(P)]
+    keys = [W.jl_user_key(p) for p in range(P)]
+    sk0 = -sum(keys)
+    es, cr_ = O.jl_slot(None, P)
+    n_ct = (n + cr_ - 1) // cr_
+    jc = SecaggCrypter()
+    xs = [W.party_params(p, n) for p in range(P)]
+    xd = [torch.from_numpy(x).to(dev) for x in xs]
+    whole = torch.stack([jc.encrypt_tensor(P, tau, xd[p], keys[p], W.BIPRIME0, weight=ws[p]) for p in range(P)])
+    assert tuple(whole.shape) == (P, n_ct, 64)
+    out_whole, sums = jc.aggregate_tensor(tau, whole, sk0, W.BIPRIME0, sum(ws), num_expected_params=n,
+                                          want_sums=True)
+    # the 8 stripes: ciphertexts and aggregates bit-identical to the whole vector's
+    outs = []
+    for r in range(world):
+        lo, hi = Dd.jl_shard(n, world, r, cr_)
+        k0, k1 = lo // cr_, (hi + cr_ - 1) // cr_
+        cts = torch.stack([jc.encrypt_tensor(P, tau, xd[p][lo:hi], keys[p], W.BIPRIME0, weight=ws[p],
+                                             ct_offset=k0) for p in range(P)])
+        assert torch.equal(cts, whole[:, k0:k1]), r
+        outs.append(jc.aggregate_tensor(tau, cts, sk0, W.BIPRIME0, sum(ws), num_expected_params=hi - lo,
+                                        ct_offset=k0))
+        del cts
+    assert torch.equal(torch.cat(outs), out_whole)
+    # sampled ciphertexts (first, last/partial, stripe boundaries, random) vs the oracle
+    rng = np.random.default_rng(4)
+    bounds = [Dd.jl_shard(n, world, r, cr_)[0] // cr_ for r in range(1, world)]
+    ks = sorted({0, n_ct - 1, *bounds, *rng.choice(n_ct, 22, replace=False).tolist()})
+    for p in range(P):
+        got = D.limbs_to_ints(whole[p, ks].cpu().numpy())
+        for k, g in zip(ks, got):
+            qw = [int(v) for v in _qw(xs[p][k * cr_:(k + 1) * cr_], ws[p])]
+            assert g == O.jl_encrypt_ints(qw, tau, keys[p], W.BIPRIME0, P, k0=k)[0], (p, k)
+    # decoded integer sums exact over all 10M elements: sum_p q_p w_p
+    sums = sums.cpu().numpy().view(np.uint64).reshape(n, 2)
+    want = np.zeros(n, dtype=np.uint64)
+    for p in range(P):
+        want += _qw(xs[p], ws[p])
+    assert (sums[:, 1] == 0).all() and np.array_equal(sums[:, 0], want)
+    idx = rng.choice(n, 5000, replace=False)
+    ref = O.reverse_quantize(O.apply_average([int(v) for v in want[idx]], sum(ws)))
+    assert np.array_equal(out_whole.cpu().numpy()[idx].view(np.uint64), ref.view(np.uint64))
 
 
 def test_cfg5_lom_ass_100m_16_parties(dev):

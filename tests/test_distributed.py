@@ -3,8 +3,10 @@
 CPU (gloo, world_size 2, 127.0.0.1): the party-per-rank exchange -- LOM reduce-scatter of
 masked u64 sums, JL all-to-all of ciphertext stripes, all-gather of float64 stripes --
 composed with the CPU oracle as the per-rank compute, must reproduce the single-process
-oracle result bit for bit.  GPU: element-range shards computed with global offsets
-(elem_offset / ct_offset) concatenate to the unsharded device result.
+oracle result bit for bit.  GPU: the same exchange with the HIP kernels as every rank's
+compute (2 gloo ranks sharing cuda:0, spawned before any GPU initialisation), and
+element-range shards computed with global offsets (elem_offset / ct_offset) concatenate to
+the unsharded device result.
 """
 
 import os
@@ -100,6 +102,55 @@ def _jl_party_per_rank(rank, world):
     return Dd.all_gather_stripes(out, N_JL, cr).numpy(), (e_lo, e_hi)
 
 
+# ---- per-rank bodies with the HIP path as each rank's compute (cuda:0 shared by the ranks) ----
+N_LOM_HIP = 100_003  # ragged: not a multiple of 8 * world
+N_JL_HIP = 3_001
+
+
+def _lom_party_per_rank_hip(rank, world):
+    """LOM: HIP protect of this rank's parties -> HIP column sum (mod 2^64) -> reduce-scatter
+    of the masked sums -> HIP average + dequantise of the rank's stripe -> all-gather
+    (reference LOM.aggregate _lom.py:177-192 + _secagg_crypter.py:394-455)."""
+    from fedbiomed_amd import _device as D
+    from fedbiomed_amd.secagg import SecaggLomCrypter
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    ids = W.node_ids(P)
+    lc = SecaggLomCrypter(W.LOM_NONCE)
+    mine = [p for p in range(P) if p % world == rank]
+    Y = torch.stack([lc.encrypt_tensor(TAU, ids[p], torch.from_numpy(W.party_params(p, N_LOM_HIP)).to(dev),
+                                       W.pairwise_secrets_for(ids[p], ids), ids, weight=W.party_weight(p))
+                     for p in mine])
+    _, local = D.lom_aggregate(Y, 1, want_out=False, want_sums=True)
+    stripe = Dd.reduce_scatter_u64(local.cpu(), N_LOM_HIP)  # gloo: host tensors
+    total_w = sum(W.party_weight(p) for p in range(P))
+    out = lc.aggregate_tensor(stripe.view(1, -1).to(dev), total_w)
+    return Dd.all_gather_stripes(out.cpu(), N_LOM_HIP, 8).numpy()
+
+
+def _jl_party_per_rank_hip(rank, world):
+    """JL: HIP encrypt of this rank's parties -> all-to-all of ciphertext stripes -> HIP
+    aggregate of the rank's stripe with its global ct_offset -> all-gather (reference
+    _jls.py:646-699, product :691-693)."""
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    keys = [W.jl_user_key(p) for p in range(P)]
+    jc = SecaggCrypter()
+    mine = [p for p in range(P) if (p // (P // world)) == rank]
+    cts = torch.stack([jc.encrypt_tensor(P, TAU, torch.from_numpy(W.party_params(p, N_JL_HIP)).to(dev), keys[p],
+                                         W.BIPRIME0, weight=W.party_weight(p)) for p in mine]).cpu()
+    stripe, k0 = Dd.all_to_all_ciphertexts(cts, P // world)
+    es, cr = O.jl_slot(None, P)
+    e_lo, e_hi = min(k0 * cr, N_JL_HIP), min((k0 + stripe.shape[1]) * cr, N_JL_HIP)
+    total_w = sum(W.party_weight(p) for p in range(P))
+    out = jc.aggregate_tensor(TAU, stripe.to(dev), -sum(keys), W.BIPRIME0, total_w, num_expected_params=e_hi - e_lo,
+                              ct_offset=k0)
+    return Dd.all_gather_stripes(out.cpu(), N_JL_HIP, cr).numpy(), (e_lo, e_hi)
+
+
 # ---- tests ---------------------------------------------------------------------------------
 @pytest.mark.parametrize("n,world,align", [(0, 2, 8), (7, 2, 8), (1003, 2, 8), (10_000_000, 8, 8),
                                            (10_000_000, 8, 30), (100, 3, 31)])
@@ -187,3 +238,28 @@ def test_jl_ct_offset_shards_gpu():
         outs.append(jc.aggregate_tensor(TAU, cts, -sum(keys), W.BIPRIME0, 33, num_expected_params=hi - lo,
                                         ct_offset=lo // cr))
     assert torch.equal(torch.cat(outs), out_whole)
+
+
+@pytest.mark.gpu
+def test_lom_party_per_rank_hip_gloo():
+    res = _spawn("_lom_party_per_rank_hip")
+    ids = W.node_ids(P)
+    nonce = O.lom_nonce(W.LOM_NONCE)
+    ys = [O.lom_encrypt(W.party_params(p, N_LOM_HIP).astype(np.float64), TAU, ids[p],
+                        W.pairwise_secrets_for(ids[p], ids), ids, nonce, weight=W.party_weight(p)) for p in range(P)]
+    ref = O.lom_crypter_aggregate(ys, sum(W.party_weight(p) for p in range(P)))
+    for r in range(2):
+        assert res[r].view(np.uint64).tolist() == np.asarray(ref, dtype=np.float64).view(np.uint64).tolist()
+
+
+@pytest.mark.gpu
+def test_jl_party_per_rank_hip_gloo():
+    res = _spawn("_jl_party_per_rank_hip")
+    keys = [W.jl_user_key(p) for p in range(P)]
+    cts = [O.jl_encrypt([float(v) for v in W.party_params(p, N_JL_HIP)], TAU, keys[p], W.BIPRIME0, P,
+                        weight=W.party_weight(p)) for p in range(P)]
+    ref = O.jl_crypter_aggregate(cts, TAU, -sum(keys), W.BIPRIME0, sum(W.party_weight(p) for p in range(P)),
+                                 N_JL_HIP)
+    assert res[0][1][0] == 0 and res[1][1][1] == N_JL_HIP and res[0][1][1] == res[1][1][0]
+    for r in range(2):
+        assert res[r][0].view(np.uint64).tolist() == np.asarray(ref, dtype=np.float64).view(np.uint64).tolist()

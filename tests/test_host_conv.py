@@ -141,3 +141,59 @@ def test_deferred_checks_are_per_thread():
         assert len(D.deferred_checks._stack()[-1]) == 1
         D.deferred_checks._stack()[-1].clear()  # nothing to check at exit (no device here)
     assert seen["other"] == [] and D.deferred_checks._stack() == []
+
+
+# ---- the three implementations of the conversion contract ---------------------------------
+# the in-tree C module, the same source built with the version-portable byte-API path
+# (-DFBM_DIGITS_FAST=0: what CPython >= 3.12 compiles), and the pure-Python fallback the list
+# API uses when the module is not built for the running interpreter.
+@pytest.fixture(scope="module", params=["c", "portable_c", "python"])
+def conv(request, tmp_path_factory):
+    if request.param == "python":
+        return D._PyConvFallback
+    if request.param == "c":
+        m = D._pyconv()
+        if m is D._PyConvFallback:
+            pytest.skip("C conversion module not built")
+        return m
+    import importlib.util
+    import shutil
+    import subprocess
+    import sysconfig
+
+    from fedbiomed_amd import _build
+
+    if not shutil.which("gcc"):
+        pytest.skip("no gcc")
+    out = tmp_path_factory.mktemp("pyconv") / ("_fbm_pyconv" + sysconfig.get_config_var("EXT_SUFFIX"))
+    subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-Wall", "-Werror", "-pthread", "-DFBM_DIGITS_FAST=0",
+                    "-I" + sysconfig.get_paths()["include"], _build.PYCONV_SRC, "-o", str(out)], check=True)
+    spec = importlib.util.spec_from_file_location("_fbm_pyconv", str(out))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_conv_contract_ints(conv):
+    rng = random.Random(21)
+    vals = [0, 1, 2**30 - 1, 2**30, 2**32, 2**2047, 2**2048 - 1] + [rng.getrandbits(2040) for _ in range(500)]
+    out = np.empty((len(vals), 64), dtype=np.uint32)
+    assert conv.ints_to_bytes(vals, 256, out) == -1
+    assert out.tobytes() == b"".join(v.to_bytes(256, "little") for v in vals)
+    assert conv.bytes_to_ints(out, 256) == vals
+    for bad in (-1, 2**2048, 1.0, "x"):
+        assert conv.ints_to_bytes([5, 6, bad, 7], 256, np.empty((4, 64), np.uint32)) == 2
+    u = np.empty(3, np.int64)
+    assert conv.ints_to_bytes([1, 2**64 - 1, 0], 8, u) == -1 and u.view(np.uint64).tolist() == [1, 2**64 - 1, 0]
+    with pytest.raises(ValueError):
+        conv.ints_to_bytes([1, 2], 8, np.empty(3, np.int64))
+
+
+def test_conv_contract_floats(conv):
+    vals = [0.5, -0.0, float("nan"), float("inf"), F(2.5), np.float64(3.25)]
+    out = np.empty(len(vals), np.float64)
+    assert conv.floats_to_f64(vals, out) == -1
+    assert out.tobytes() == np.frombuffer(array.array("d", vals), dtype=np.float64).tobytes()
+    assert conv.floats_to_f64([1.0, 2, 3.0], np.empty(3, np.float64)) == 1
+    with pytest.raises(ValueError):
+        conv.floats_to_f64([1.0], np.empty(2, np.float64))

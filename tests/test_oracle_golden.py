@@ -130,3 +130,37 @@ def test_ass_golden(golden):
         rec = O.ass_reconstruct(sh)
         exp = case["reconstruct"]
         assert rec == (I(exp) if isinstance(exp, str) else [I(x) for x in exp])
+
+
+def test_edge_weights_oracle(golden):
+    """Negative / zero weights (tests/golden/edge.json, from the reference): the oracle's JL
+    packing ORs negative products like VES._batch, and its LOM conversion raises numpy's
+    OverflowError at the first negative product."""
+    from fedbiomed_amd import workload as W
+
+    edge = golden["edge"]
+    for case in edge["jl"]:
+        r = case["result"]
+        x = [F(v) for v in case["x"]]
+        if "ok" not in r or not x:
+            continue
+        got = O.jl_encrypt(x, case["tau"], I(case["key"]), W.BIPRIME0, case["num_nodes"], weight=case["weight"])
+        assert got == [I(c) for c in r["ok"]], case["name"]
+    for case in edge["lom"]:
+        r = case["result"]
+        x = [F(v) for v in case["x"]]
+        if not x:
+            continue
+        ids = case["ids"]
+        run = lambda: O.lom_encrypt(x, case["tau"], case["node"], W.pairwise_secrets_for(case["node"], ids),  # noqa
+                                    ids, O.lom_nonce(case["nonce_str"]), weight=case["weight"])
+        if "ok" in r:
+            assert [int(v) for v in run()] == [I(v) for v in r["ok"]], case["name"]
+        else:
+            with pytest.raises(OverflowError, match=r["msg"].replace("(", r"\(").replace(")", r"\)")):
+                run()
+    m = edge["jl_aggregate_mixed"]
+    encs = [[I(c) for c in e] for e in m["enc"]]
+    keys = [I(k) for k in m["keys"]]
+    agg = O.jl_crypter_aggregate(encs, m["tau"], -sum(keys), W.BIPRIME0, 2, len(m["x"]))
+    assert [fbits(v) for v in agg] == [s[2:] for s in m["agg"]["ok"]]

@@ -271,12 +271,59 @@ def gen_ass(R):
     dump("ass.json", {"cases": out})
 
 
+def _outcome(fn):
+    """{"ok": value} or {"error": type, "msg": str} of one reference call."""
+    try:
+        return {"ok": fn()}
+    except Exception as e:  # noqa: BLE001 - the exception IS the golden output
+        return {"error": type(e).__name__, "msg": str(e)}
+
+
+def gen_edge(R):
+    """Weight edge cases of the crypters: validation order on empty input,
+    and negative weights (JL encrypts the OR-packed negative products, _jls.py:169-176; LOM
+    raises numpy's OverflowError from its uint64 conversion, _lom.py:153)."""
+    JC, LC = R.crypter.SecaggCrypter, R.crypter.SecaggLomCrypter
+    bp = W.BIPRIME0
+    out = {"jl": [], "lom": []}
+    x = [float(v) for v in W.party_params(0, 40)]
+    x_lowfirst = [-4.0] * 35 + [0.1, -0.2] + [-5.0] * 10 + [0.3] * 20  # q = 0 in the leading slots
+    x_allzero = [-4.0, -3.0, -100.0]  # q = 0 everywhere
+    keys = [W.jl_user_key(p) for p in range(2)]
+    for name, params, weight in [("empty_w_big", [], 2 ** 17), ("empty_none", [], None), ("empty_w_neg", [], -5),
+                                 ("neg3", x, -3), ("neg1", x, -1), ("neg_max", x, -(2 ** 17 - 1)),
+                                 ("w0", x, 0), ("neg_lowfirst", x_lowfirst, -7), ("neg_allzero", x_allzero, -9),
+                                 ("big_neg", x, -(2 ** 17))]:
+        r = _outcome(lambda: [hex(int(c)) for c in JC().encrypt(num_nodes=2, current_round=3, params=params,
+                                                               key=keys[0], biprime=bp, weight=weight)])
+        out["jl"].append({"name": name, "x": [fhex(v) for v in params], "weight": weight, "key": ihex(keys[0]),
+                          "num_nodes": 2, "tau": 3, "result": r})
+    # aggregate of a negative-weight party with a positive one (deterministic, pins decode)
+    e0 = JC().encrypt(num_nodes=2, current_round=3, params=x, key=keys[0], biprime=bp, weight=-3)
+    e1 = JC().encrypt(num_nodes=2, current_round=3, params=x, key=keys[1], biprime=bp, weight=5)
+    agg = _outcome(lambda: [fhex(v) for v in JC().aggregate(current_round=3, num_nodes=2, params=[e0, e1],
+                                                             key=-sum(keys), biprime=bp, total_sample_size=2,
+                                                             num_expected_params=len(x))])
+    out["jl_aggregate_mixed"] = {"x": [fhex(v) for v in x], "weights": [-3, 5], "keys": [ihex(k) for k in keys],
+                                 "tau": 3, "enc": [[ihex(c) for c in e0], [ihex(c) for c in e1]], "agg": agg}
+    ids = W.node_ids(3)
+    for name, params, weight in [("empty_w_big", [], 2 ** 17), ("empty_none", [], None), ("neg3", x, -3),
+                                 ("neg_lowfirst", x_lowfirst, -7), ("neg_allzero", x_allzero, -9), ("w0", x, 0)]:
+        r = _outcome(lambda: [hex(int(v)) for v in LC(nonce="abc").encrypt(
+            current_round=2, node_id=ids[1], params=params, pairwise_secrets=W.pairwise_secrets_for(ids[1], ids),
+            node_ids=ids, weight=weight)])
+        out["lom"].append({"name": name, "x": [fhex(v) for v in params], "weight": weight, "ids": ids,
+                           "node": ids[1], "nonce_str": "abc", "tau": 2, "result": r})
+    dump("edge.json", out)
+
+
 def main():
     R = load_reference.load()
     gen_quantize(R)
     gen_lom(R)
     gen_jl(R)
     gen_ass(R)
+    gen_edge(R)
     meta = {"generator": "tools/gen_golden.py", "reference": load_reference.REF,
             "note": "outputs of the reference Fed-BioMed crypter (Python), imported via tools/refshim"}
     dump("meta.json", meta)
