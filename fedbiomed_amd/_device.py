@@ -449,6 +449,38 @@ def _key_limbs(key: int) -> Tuple[np.ndarray, int]:
 
 JL_MAX_CT = 14_000_000  # include/fbm_secagg.h FBM_JL_MAX_CT: ciphertexts per library call
 
+_ENGINES = {"auto": 0, "single": 1, "quad": 4}
+
+
+class jl_engine:
+    """Exponentiation engine for the JL calls issued inside (process-wide policy,
+    fbm_jl_set_engine): "auto" (the library's choice by launch size), "single" (one lane per
+    ciphertext: several concurrent launches that fill the chip together) or "quad" (four
+    lanes per ciphertext: latency of a launch below the chip's lane count).  Results are
+    bit-identical under every engine.
+
+        with D.jl_engine("single"):
+            ...  # the parties' concurrent encrypts
+    """
+
+    def __init__(self, mode: str):
+        if mode not in _ENGINES:
+            raise ValueError(f"engine must be one of {sorted(_ENGINES)}")
+        self._mode, self._prev = _ENGINES[mode], None
+
+    def __enter__(self):
+        self._prev = N.load().fbm_jl_set_engine(self._mode)
+        return self
+
+    def __exit__(self, *exc):
+        N.load().fbm_jl_set_engine(self._prev)
+        return False
+
+
+def jl_engine_for(n_ct: int) -> str:
+    """The engine a launch of n_ct ciphertexts takes under the current policy."""
+    return "quad" if N.load().fbm_jl_engine_for(int(n_ct)) == 4 else "single"
+
 
 def jl_chunk_ct() -> int:
     """Ciphertexts per library call (FBM_JL_CHUNK_CT lowers it, for tests of the striping)."""

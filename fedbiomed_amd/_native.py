@@ -48,6 +48,9 @@ SIGNATURES = {
     "fbm_abi_version": (c_int, []),
     "fbm_jl_window": (c_int, []),
     "fbm_jl_mads": (c_int, [c_int]),
+    "fbm_jl_quad_mads": (c_int, [c_int]),
+    "fbm_jl_set_engine": (c_int, [c_int]),
+    "fbm_jl_engine_for": (c_int, [c_u64]),
     "fbm_last_error": (ctypes.c_char_p, []),
     "fbm_check_stats": (c_int, [c_vp, c_int, c_vp]),
     "fbm_lom_protect": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_vp, c_vp, c_int, c_int,

@@ -13,6 +13,7 @@
 
 #include "fbm_internal.hpp"
 #include "fbm_nadic_asm.hpp"
+#include "fbm_quad_asm.hpp"
 #include "fbm_safegcd.hpp"
 
 namespace fbm {
@@ -119,14 +120,16 @@ static Big big_pow2_mod(int e, const Big& m) {
   return x;
 }
 
-static void to28_host(const Big& a, uint32_t* o, int nl) {
+static void to_limbs_host(const Big& a, uint32_t* o, int nl, int lb) {
   for (int k = 0; k < nl; ++k) {
-    const int bit = k * FBM_LB, wi = bit >> 5, sh = bit & 31;
+    const int bit = k * lb, wi = bit >> 5, sh = bit & 31;
     const uint64_t lo = wi < (int)a.size() ? a[wi] : 0u;
     const uint64_t hi = wi + 1 < (int)a.size() ? a[wi + 1] : 0u;
-    o[k] = (uint32_t)(((hi << 32) | lo) >> sh) & FBM_LMASK;
+    o[k] = (uint32_t)(((hi << 32) | lo) >> sh) & ((1u << lb) - 1u);
   }
 }
+
+static void to28_host(const Big& a, uint32_t* o, int nl) { to_limbs_host(a, o, nl, FBM_LB); }
 
 template <int NL>
 static void build_mont(const Big& m, MontCtxT<NL>& c) {
@@ -195,6 +198,44 @@ static void build_nadic(const Big& N, const Big& M, const MontCtxN& mn, NadicCtx
   }
 }
 
+// Constants of the quad engine (tools/gen_quad_asm.py): 29-bit limbs, R = 2^(36*29) = 2^1044.
+static void build_quad(const Big& N, const Big& M, QuadCtx& qa) {
+  memset(&qa, 0, sizeof(qa));
+  const int LB = FBM_QA_LB, L = FBM_QA_L;
+  Big Rm = big_pow2_mod(L * LB, N);  // R mod N
+  Big K(N.size() + 1, 0u);
+  K[0] = 1u;
+  if (big_cmp(Rm, K) > 0) {  // K = N + 1 - Rm
+    Big t(N.begin(), N.end());
+    t.push_back(0u);
+    uint64_t c = 1;
+    for (size_t k = 0; k < t.size(); ++k) {
+      c += t[k];
+      t[k] = (uint32_t)c;
+      c >>= 32;
+    }
+    big_sub_inplace(t, Rm);
+    K = t;
+  } else {
+    K.assign(1, 0u);
+  }
+  uint32_t k29[FBM_QA_L];
+  to_limbs_host(K, k29, L, LB);
+  for (int j = 0; j < L; ++j) qa.kp[j] = ((1u << LB) - 1u) + k29[j];
+  to_limbs_host(N, qa.n, L, LB);
+  for (int e = 2; e <= 3; ++e) {
+    const Big u = big_pow2_mod(e * L * LB, M);
+    Big q, r;
+    big_divmod(u, N, q, r);
+    uint32_t* dst = e == 2 ? qa.r2 : qa.r3;
+    to_limbs_host(r, dst, L, LB);
+    to_limbs_host(q, dst + L, L, LB);
+  }
+  uint32_t inv = N[0];  // Newton: N^-1 mod 2^32
+  for (int i = 0; i < 5; ++i) inv *= 2u - N[0] * inv;
+  qa.np = (0u - inv) & ((1u << LB) - 1u);
+}
+
 static int build_jl_params(const uint32_t* biprime, int es, int cr, uint64_t tau, uint64_t ct_offset, JlParams& jp) {
   memset(&jp, 0, sizeof(jp));
   Big N(biprime, biprime + 32);
@@ -213,6 +254,7 @@ static int build_jl_params(const uint32_t* biprime, int es, int cr, uint64_t tau
   build_mont<FBM_NL>(M, jp.mc);
   build_mont<FBM_NLN>(N, jp.mn);
   build_nadic(N, M, jp.mn, jp.na);
+  build_quad(N, M, jp.qa);
   for (int i = 0; i < 32; ++i) jp.N32[i] = biprime[i];
   {  // N^-1 mod 2^1024 by Newton: y <- y (2 - N y); y = N is correct to 3 bits for odd N
     uint32_t y[32], t[32];
@@ -392,6 +434,17 @@ int fbm_abi_version(void) { return FBM_ABI_VERSION; }
 
 int fbm_jl_window(void) { return FBM_WIN; }
 int fbm_jl_mads(int square) { return square ? FBM_NA_MADS_SQR : FBM_NA_MADS_MUL; }
+int fbm_jl_quad_mads(int square) { return 4 * (square ? FBM_QA_MADS_SQR : FBM_QA_MADS_MUL); }
+
+int fbm_jl_set_engine(int mode) {
+  if (mode != FBM_ENGINE_AUTO && mode != FBM_ENGINE_SINGLE && mode != FBM_ENGINE_QUAD) {
+    set_error("fbm_jl_set_engine: mode must be 0 (auto), 1 (one lane per ciphertext) or 4 (four lanes)");
+    return FBM_E_ARG;
+  }
+  return jl_engine_set(mode);
+}
+
+int fbm_jl_engine_for(uint64_t n_ct) { return jl_use_quad(n_ct) ? FBM_ENGINE_QUAD : FBM_ENGINE_SINGLE; }
 
 const char* fbm_last_error(void) { return g_err; }
 
@@ -517,15 +570,17 @@ int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t tot
 //                    H^-1 [n_ct][64] + y [n_ct][32] (negative keys)
 uint64_t fbm_jl_encrypt_workspace(uint64_t n_ct) {
   const uint64_t slots = table_slots_for(n_ct);
+  (void)slots;
   return align256(FBM_MAX_OPS * 4) + align256(FBM_CST_WORDS * 4) + align256(n_ct * 32 * 4) +
          align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4) + 2 * align256(n_ct * 64 * 4) + align256(n_ct * 32 * 4) +
-         align256(slots * FBM_TENTRIES * FBM_NL * 4);
+         align256(jl_table_bytes(n_ct));
 }
 
 uint64_t fbm_jl_aggregate_workspace(uint64_t n_ct) {
   const uint64_t slots = table_slots_for(n_ct);
+  (void)slots;
   return align256(FBM_MAX_OPS * 4) + align256(FBM_CST_WORDS * 4) + align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4) +
-         3 * align256(n_ct * 64 * 4) + align256(n_ct * 32 * 4) + align256(slots * FBM_TENTRIES * FBM_NL * 4);
+         3 * align256(n_ct * 64 * 4) + align256(n_ct * 32 * 4) + align256(jl_table_bytes(n_ct));
 }
 
 // phase bit 1: the prologue (status word, constants, pack, nude, FDH, and the inverse of H
@@ -589,7 +644,7 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
   uint32_t* H = (uint32_t*)(ws + off);
   off += align256(n_ct * 64 * 4);
   uint32_t* table = (uint32_t*)(ws + off);
-  off += align256(slots * FBM_TENTRIES * FBM_NL * 4);
+  off += align256(jl_table_bytes(n_ct));
   uint32_t* Hinv = (uint32_t*)(ws + off);  // negative keys only (after the table: keeps its placement)
   off += align256(n_ct * 64 * 4);
   uint32_t* Y = (uint32_t*)(ws + off);

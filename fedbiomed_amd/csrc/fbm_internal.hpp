@@ -74,7 +74,13 @@ int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t 
 #define FBM_CST_NK (256 + 2 * FBM_NL * 256)
 #define FBM_CST_R2NA (FBM_CST_NK + 128)
 #define FBM_CST_R3NA (FBM_CST_R2NA + 128)  // R^3 mod N^2 (digits): the high part of a wide h
-#define FBM_CST_WORDS (FBM_CST_R3NA + 128)
+// quad engine (fbm_quad_asm.hpp, 29-bit limbs, R = 2^1044): K'_i (36 words), the lanes' N
+// limbs (limb 9 l + r at word 4 r + l), R^2 and R^3 mod N^2 as digit pairs (72 limbs each)
+#define FBM_CST_QK (FBM_CST_R3NA + 128)
+#define FBM_CST_QN (FBM_CST_QK + 64)
+#define FBM_CST_QR2 (FBM_CST_QN + 64)
+#define FBM_CST_QR3 (FBM_CST_QR2 + 128)
+#define FBM_CST_WORDS (FBM_CST_QR3 + 128)
 
 // sliding-window schedule, passed by value (kernarg segment -> scalar loads).
 // op k (u16): (squarings before the multiply) << FBM_OP_SHIFT | (table index + 1, 0 = none)
@@ -94,6 +100,16 @@ struct NadicCtx {
   uint32_t pad[4];
 };
 
+// quad-engine constants (tools/gen_quad_asm.py): 29-bit limbs, R = 2^1044
+struct QuadCtx {
+  uint32_t kp[36];   // K'_i = 2^29 - 1 + K_i, K = (1 - R) mod N
+  uint32_t n[36];    // N
+  uint32_t r2[72];   // R^2 mod N^2 = u0 + u1 N: u0 limbs, then u1 limbs
+  uint32_t r3[72];   // R^3 mod N^2 likewise
+  uint32_t np;       // -N^-1 mod 2^29
+  uint32_t pad[3];
+};
+
 struct JlParams {
   MontCtx mc;                    // modulus M = N^2 (74 limbs)
   MontCtxN mn;                   // modulus N (37 limbs) -- inverse mod N, N*pt, N-adic np
@@ -110,6 +126,7 @@ struct JlParams {
   int pad;
   uint32_t mneg[FBM_NLN];        // N * 2^(1036 - bits(N)) in 28-bit limbs (negative-weight packing)
   uint32_t pad2[3];
+  QuadCtx qa;                    // quad exponentiation engine constants
 };
 
 int launch_jl_pack(const void* x, int x_dtype, uint64_t n, const QuantParams& qp, uint64_t weight, int es, int cr,
@@ -147,6 +164,14 @@ int launch_ass_reconstruct_wide(const uint32_t* shares, int n_shares, int l, uin
 
 // table slots the encrypt/aggregate kernels need for a given grid
 uint64_t jl_table_slots();
+// exponentiation engine policy (fbm_jl_set_engine) and the table bytes both engines fit in
+#define FBM_ENGINE_AUTO 0
+#define FBM_ENGINE_SINGLE 1
+#define FBM_ENGINE_QUAD 4
+int jl_engine_policy();
+int jl_engine_set(int mode);
+bool jl_use_quad(uint64_t n_ct);
+uint64_t jl_table_bytes(uint64_t n_ct);
 // compute units of the calling thread's current device (cached per device)
 int device_num_cu();
 

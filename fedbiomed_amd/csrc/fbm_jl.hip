@@ -18,11 +18,15 @@
 // HBM layouts: 32-bit-limb integers are row-major [ct][words] (pt: 32 words, H / E / inv /
 // ciphertexts: 64 words = int.to_bytes(256,'little')); 28-bit-limb residues (nude, X) and
 // the per-lane exponent tables are limb-major [limb][lane] so a wave's accesses coalesce.
+#include <stdlib.h>
+#include <string.h>
+
 #include <atomic>
 
 #include "fbm_internal.hpp"
 #include "fbm_mont_asm.hpp"
 #include "fbm_nadic_asm.hpp"
+#include "fbm_quad_asm.hpp"
 #include "fbm_safegcd.hpp"
 
 namespace fbm {
@@ -418,16 +422,12 @@ __device__ __forceinline__ uint32_t csub28(uint32_t (&x)[L], const uint32_t (&n)
 // N-adic result (t, s) in the lane's LDS column (t < N + 1, s < 2N: the last product of
 // the exponentiation has a (1, .) operand) -> the canonical residue V = t + s N < N^2,
 // 64 words.  NK: the engine's constants block (N limbs at words 0..9, 16..42).
-__device__ __forceinline__ void na_final(const uint32_t* lds, const uint32_t* NK, uint32_t (&w)[64]) {
+__device__ __forceinline__ void na_final_digits(uint32_t (&t)[FBM_NLN], uint32_t (&sd)[FBM_NLN], const uint32_t* NK,
+                                                uint32_t (&w)[64]) {
   const uint32_t* nk = launder_s(NK);
-  uint32_t n[FBM_NLN], t[FBM_NLN], sd[FBM_NLN];
+  uint32_t n[FBM_NLN];
 #pragma unroll
   for (int j = 0; j < FBM_NLN; ++j) n[j] = j < 10 ? nk[j] : nk[6 + j];
-#pragma unroll
-  for (int k = 0; k < FBM_NLN; ++k) {
-    t[k] = lds[k * FBM_BLOCK];
-    sd[k] = lds[(FBM_NLN + k) * FBM_BLOCK];
-  }
   // t + s N = (t mod N) + N (s + [t >= N])  ->  reduce s + carry mod N
   uint32_t cy = csub28(t, n);
   cy += csub28(t, n);  // (a second one only matters for digits >= 2N: none here, kept cheap)
@@ -453,6 +453,16 @@ __device__ __forceinline__ void na_final(const uint32_t* lds, const uint32_t* NK
     carry = acc >> FBM_LB;
   }
   from28<FBM_NL, 64>(v28, w);
+}
+
+__device__ __forceinline__ void na_final(const uint32_t* lds, const uint32_t* NK, uint32_t (&w)[64]) {
+  uint32_t t[FBM_NLN], sd[FBM_NLN];
+#pragma unroll
+  for (int k = 0; k < FBM_NLN; ++k) {
+    t[k] = lds[k * FBM_BLOCK];
+    sd[k] = lds[(FBM_NLN + k) * FBM_BLOCK];
+  }
+  na_final_digits(t, sd, NK, w);
 }
 
 // mode 0 (ENC): out[ct] = nude[ct] * H[ct]^key  mod N^2          (ciphertext)
@@ -600,6 +610,239 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
     uint32_t w[64];
     na_final(lds, NK, w);
     if (valid) store_row64(out + ct * 64, w);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// The same exponentiation on the QUAD engine (fbm_quad_asm.hpp, tools/gen_quad_asm.py):
+// four lanes per ciphertext, 29-bit limbs (36 per digit, R = 2^1044), lane l owning limbs
+// 9 l .. 9 l + 8 of both digits, for launches that hold fewer ciphertexts than the chip has
+// resident lanes (one party's 1M elements, the aggregate of a 1/8 stripe): the 4x lanes fill
+// the chip and a ciphertext's exponentiation takes about a quarter of a lane's time.  Same
+// residues at every step (the Montgomery form uses R = 2^1044 instead of 2^1036), the same
+// canonical results (tests/test_quad_asm.py; the -m gpu tests through both engines).
+//   workgroup: 256 lanes = 64 ciphertexts; LDS column of ciphertext c: limb k of digit d at
+//   word (36 d + k) * 72 + c (2 spare rows: the last row's prefetch);  per-lane tables in the
+//   QUAD layout: entry e, limb row j (b0: j = r, b1: j = 9 + r) at word
+//   (slot * FBM_TENTRIES + e) * 4608 + j * 256 + tid.
+// ------------------------------------------------------------------------------------
+#define FBM_QBLOCK 256
+#define FBM_QCT (FBM_QBLOCK / 4)
+#define FBM_QROWW FBM_QA_ROWW                 // LDS words between limb rows (72)
+#define FBM_QENTRY (2 * FBM_QA_LIMBS * 256)   // words of one quad-layout table entry (4608)
+#define FBM_QMASK ((1u << FBM_QA_LB) - 1u)
+
+// limb k (lb bits at bit lb k) of a little-endian number of `nw` words in global memory
+__device__ __forceinline__ uint32_t glb_limb(const uint32_t* p, int nw, int k, int lb) {
+  const int bit = k * lb, wi = bit >> 5, sh = bit & 31;
+  const uint64_t lo = wi < nw ? p[wi] : 0u;
+  const uint64_t hi = wi + 1 < nw ? p[wi + 1] : 0u;
+  return (uint32_t)(((hi << 32) | lo) >> sh) & ((1u << lb) - 1u);
+}
+
+// the lane's slice of a digit pair held as 72 uniform 29-bit limbs (R^2, R^3 digits) -> LDS
+__device__ __forceinline__ void qa_lds_store_uniform(uint32_t* col, int l, const uint32_t* u) {
+  u = launder_s(u);
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < FBM_QA_LIMBS; ++r) {
+      const int k = FBM_QA_LIMBS * l + r;
+      col[(d * FBM_QA_D1 + k) * FBM_QROWW] = u[d * FBM_QA_L + k];
+    }
+}
+// lane slice LDS <-> quad-layout table entry (p = entry base + tid)
+__device__ __forceinline__ void qa_lds_to_tbl(const uint32_t* col, int l, uint32_t* p) {
+  uint32_t v[2 * FBM_QA_LIMBS];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < FBM_QA_LIMBS; ++r)
+      v[d * FBM_QA_LIMBS + r] = col[(d * FBM_QA_D1 + FBM_QA_LIMBS * l + r) * FBM_QROWW];
+  col_store<2 * FBM_QA_LIMBS>(p, v);
+}
+__device__ __forceinline__ void qa_tbl_to_lds(const uint32_t* p, uint32_t* col, int l) {
+  uint32_t v[2 * FBM_QA_LIMBS];
+  col_load<2 * FBM_QA_LIMBS>(p, v);
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < FBM_QA_LIMBS; ++r)
+      col[(d * FBM_QA_D1 + FBM_QA_LIMBS * l + r) * FBM_QROWW] = v[d * FBM_QA_LIMBS + r];
+}
+// lane 0 of the quad: carry-normalise both digits of the column in place (lazy limbs from
+// a digit-wise sum; the engine's own outputs need no pass)
+__device__ __forceinline__ void qa_normalise_column(uint32_t* col) {
+#pragma unroll 1
+  for (int d = 0; d < 2; ++d) {
+    uint32_t c = 0;
+#pragma unroll 1
+    for (int k = 0; k < FBM_QA_L; ++k) {
+      const uint32_t v = col[(d * FBM_QA_D1 + k) * FBM_QROWW] + c;
+      col[(d * FBM_QA_D1 + k) * FBM_QROWW] = v & FBM_QMASK;
+      c = v >> FBM_QA_LB;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(FBM_QBLOCK, 3) jl_expq_kernel(const uint32_t* __restrict__ H, uint64_t n_ct,
+                                                               uint32_t* __restrict__ cst, uint32_t np29,
+                                                               const uint32_t* __restrict__ ops, int n_ops,
+                                                               int first, int mode, int key_is_zero,
+                                                               const uint32_t* __restrict__ nude,
+                                                               uint32_t* __restrict__ table,
+                                                               uint32_t* __restrict__ out) {
+  __shared__ uint32_t lds_q[(2 * FBM_QA_D1 + 2) * FBM_QROWW];
+  __shared__ uint32_t chunk_s;
+  const int tid = threadIdx.x, l = tid & 3, c = tid >> 2;
+  uint32_t* col = lds_q + c;
+  const uint32_t ac = lds_addr(col);
+  const uint32_t al = ac + (uint32_t)(FBM_QA_LIMBS * l * FBM_QA_ROWB);
+  const uint32_t* QK = cst + FBM_CST_QK;
+  uint32_t n[FBM_QA_LIMBS];
+#pragma unroll
+  for (int r = 0; r < FBM_QA_LIMBS; ++r) n[r] = cst[FBM_CST_QN + 4 * r + l];
+  const uint32_t e0 = l == 0 ? 1u : 0u;
+  // byte offset of this lane's word in table entry 0 of this workgroup's slot
+  const uint32_t tb0 = (uint32_t)(((uint64_t)blockIdx.x * FBM_TENTRIES * FBM_QENTRY + tid) * 4);
+  const uint32_t tstride = FBM_QENTRY * 4;
+  const uint32_t n_chunks = (uint32_t)((n_ct + FBM_QCT - 1) / FBM_QCT);
+#pragma unroll 1
+  for (;;) {
+    if (tid == 0) chunk_s = atomicAdd(cst + FBM_CST_CTR, 1u);
+    __syncthreads();
+    const uint32_t chunk = __builtin_amdgcn_readfirstlane(chunk_s);
+    __syncthreads();
+    if (chunk >= n_chunks) break;
+    const uint64_t ct_raw = (uint64_t)chunk * FBM_QCT + c;
+    const bool valid = ct_raw < n_ct;
+    const uint64_t ct = valid ? ct_raw : n_ct - 1;
+    uint32_t* scratch = table + (tb0 + FBM_TSCRATCH * tstride) / 4;
+    bool wide = false;
+    {  // h -> the lane's 29-bit limbs of (h mod R, h div R) (or the N-adic digits) -> scratch
+      uint32_t h18[2 * FBM_QA_LIMBS];
+      const uint32_t* hr = H + ct * 64;
+#pragma unroll
+      for (int r = 0; r < FBM_QA_LIMBS; ++r) {
+        const int k = FBM_QA_LIMBS * l + r;
+        uint32_t lo = 0, hi = 0;
+        if (key_is_zero) {
+          lo = k == 0 ? 1u : 0u;
+        } else if (mode & FBM_EXP_H_NADIC) {  // (h mod N, h div N) as two 1024-bit rows
+          lo = glb_limb(hr, 32, k, FBM_QA_LB);
+          hi = glb_limb(hr + 32, 32, k, FBM_QA_LB);
+        } else {
+          lo = glb_limb(hr, 64, k, FBM_QA_LB);
+          hi = glb_limb(hr, 64, FBM_QA_L + k, FBM_QA_LB);
+        }
+        h18[r] = lo;
+        h18[FBM_QA_LIMBS + r] = hi;
+      }
+      if (!(mode & FBM_EXP_H_NADIC)) {
+        uint32_t any = 0;
+#pragma unroll
+        for (int r = 0; r < FBM_QA_LIMBS; ++r) any |= h18[FBM_QA_LIMBS + r];
+        // wide is a property of the ciphertext, not of the lane's slice: OR over the quad
+        const uint64_t bal = __ballot(any != 0u);
+        wide = ((bal >> ((tid & 63) & ~3)) & 0xFull) != 0ull;
+        if (__any(wide)) {  // FDH retries (small moduli): h_hi R^2 = (h_hi, 0) * R^3 R^-1 -> entry 1
+          uint32_t w18[2 * FBM_QA_LIMBS];
+#pragma unroll
+          for (int r = 0; r < FBM_QA_LIMBS; ++r) {
+            w18[r] = h18[FBM_QA_LIMBS + r];
+            w18[FBM_QA_LIMBS + r] = 0u;
+            h18[FBM_QA_LIMBS + r] = 0u;  // (h_lo, 0) for the main product below
+          }
+          col_store<2 * FBM_QA_LIMBS>(scratch, w18);
+          qa_lds_store_uniform(col, l, cst + FBM_CST_QR3);
+          fbm_qa_mm_glb(ac, al, table, tb0 + FBM_TSCRATCH * tstride, QK, np29, n, e0);
+          qa_lds_to_tbl(col, l, table + (tb0 + tstride) / 4);
+        }
+      }
+      col_store<2 * FBM_QA_LIMBS>(scratch, h18);
+    }
+    qa_lds_store_uniform(col, l, cst + FBM_CST_QR2);
+    fbm_qa_mm_glb(ac, al, table, tb0 + FBM_TSCRATCH * tstride, QK, np29, n, e0);  // h R | h_lo R
+    if (!(mode & FBM_EXP_H_NADIC) && __any(wide)) {  // h R = h_lo R + h_hi R^2 (digit-wise, then carries)
+      uint32_t b18[2 * FBM_QA_LIMBS];
+      col_load<2 * FBM_QA_LIMBS>(table + (tb0 + tstride) / 4, b18);
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int r = 0; r < FBM_QA_LIMBS; ++r)
+          col[(d * FBM_QA_D1 + FBM_QA_LIMBS * l + r) * FBM_QROWW] += wide ? b18[d * FBM_QA_LIMBS + r] : 0u;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (l == 0) qa_normalise_column(col);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (!key_is_zero) {
+      qa_lds_to_tbl(col, l, table + tb0 / 4);
+      fbm_qa_sq_lds(ac, al, QK, np29, n, e0);  // h^2 R
+      qa_lds_to_tbl(col, l, scratch);
+      qa_tbl_to_lds(table + tb0 / 4, col, l);
+#pragma unroll 1
+      for (int t = 1; t < FBM_TABLE; ++t) {
+        fbm_qa_mm_glb(ac, al, table, tb0 + FBM_TSCRATCH * tstride, QK, np29, n, e0);
+        qa_lds_to_tbl(col, l, table + (tb0 + (uint32_t)t * tstride) / 4);
+      }
+      qa_tbl_to_lds(table + (tb0 + (uint32_t)first * tstride) / 4, col, l);
+#pragma unroll 1
+      for (int k = 0; k < n_ops; ++k) {
+        const uint32_t op = __builtin_amdgcn_readfirstlane(ops[k]);
+        const int nsq = (int)(op >> FBM_OP_SHIFT);
+        const int idx = (int)(op & ((1u << FBM_OP_SHIFT) - 1u)) - 1;
+#pragma unroll 1
+        for (int q = 0; q < nsq; ++q) fbm_qa_sq_lds(ac, al, QK, np29, n, e0);
+        if (idx >= 0) fbm_qa_mm_glb(ac, al, table, tb0 + (uint32_t)idx * tstride, QK, np29, n, e0);
+      }
+    }
+    {  // last operand: nude = (1, pt) (encrypt; 28-bit blocked column -> 29-bit slice) or 1
+      uint32_t b18[2 * FBM_QA_LIMBS];
+      const uint32_t* nb = nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255);
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int r = 0; r < FBM_QA_LIMBS; ++r) {
+          const int k = FBM_QA_LIMBS * l + r;
+          uint32_t v = 0;
+          if ((mode & FBM_EXP_DEC) == 0) {
+            const int bit = k * FBM_QA_LB, j = bit / FBM_LB, off = bit % FBM_LB;
+            const uint32_t a0 = j < FBM_NLN ? nb[(d * FBM_NLN + j) * 256] : 0u;
+            const uint32_t a1 = j + 1 < FBM_NLN ? nb[(d * FBM_NLN + j + 1) * 256] : 0u;
+            v = (uint32_t)((((uint64_t)a1 << FBM_LB) | a0) >> off) & FBM_QMASK;
+          } else {
+            v = (d == 0 && k == 0) ? 1u : 0u;
+          }
+          b18[d * FBM_QA_LIMBS + r] = v;
+        }
+      col_store<2 * FBM_QA_LIMBS>(scratch, b18);
+    }
+    fbm_qa_mm_glb(ac, al, table, tb0 + FBM_TSCRATCH * tstride, QK, np29, n, e0);
+    if (l == 0) {  // t + s N -> the canonical residue (lane 0 of the quad, from the LDS column)
+      uint32_t t29[FBM_QA_L], s29[FBM_QA_L];
+      uint32_t ct0 = 0, cs0 = 0;
+#pragma unroll
+      for (int k = 0; k < FBM_QA_L; ++k) {  // the engine's lazy limbs -> normalised 29-bit limbs
+        const uint32_t vt = col[k * FBM_QROWW] + ct0;
+        const uint32_t vs = col[(FBM_QA_D1 + k) * FBM_QROWW] + cs0;
+        t29[k] = vt & FBM_QMASK;
+        s29[k] = vs & FBM_QMASK;
+        ct0 = vt >> FBM_QA_LB;
+        cs0 = vs >> FBM_QA_LB;
+      }
+      uint32_t t[FBM_NLN], sd[FBM_NLN];  // re-limbed to 28 bits for the shared final step
+#pragma unroll
+      for (int j = 0; j < FBM_NLN; ++j) {
+        const int bit = j * FBM_LB, k = bit / FBM_QA_LB, off = bit % FBM_QA_LB;
+        const uint64_t tw = ((uint64_t)(k + 1 < FBM_QA_L ? t29[k + 1] : 0u) << FBM_QA_LB) | (k < FBM_QA_L ? t29[k] : 0u);
+        const uint64_t sw = ((uint64_t)(k + 1 < FBM_QA_L ? s29[k + 1] : 0u) << FBM_QA_LB) | (k < FBM_QA_L ? s29[k] : 0u);
+        t[j] = (uint32_t)(tw >> off) & FBM_LMASK;
+        sd[j] = (uint32_t)(sw >> off) & FBM_LMASK;
+      }
+      uint32_t w[64];
+      na_final_digits(t, sd, cst + FBM_CST_NK, w);
+      if (valid) store_row64(out + ct * 64, w);
+    }
   }
 }
 
@@ -1112,7 +1355,7 @@ int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stat
 // memory for the exp kernel, which indexes it dynamically; M and R^2 for the scalar
 // loads of the assembly product; broadcast columns of 1 and R^2 (limb k at word k*256,
 // read by every lane at offset 0).
-__global__ void jl_setup_kernel(JlSched sc, MontCtx mc, NadicCtx na, uint32_t* __restrict__ ops,
+__global__ void jl_setup_kernel(JlSched sc, MontCtx mc, NadicCtx na, QuadCtx qa, uint32_t* __restrict__ ops,
                                 uint32_t* __restrict__ cst) {
   const int t = threadIdx.x;
   for (int i = t; i < sc.n_ops; i += blockDim.x) ops[i] = sc.op[i];
@@ -1123,6 +1366,15 @@ __global__ void jl_setup_kernel(JlSched sc, MontCtx mc, NadicCtx na, uint32_t* _
     cst[FBM_CST_R2NA + t] = t < FBM_NL ? na.r2na[t] : 0u;
     cst[FBM_CST_R3NA + t] = t < FBM_NL ? na.r3na[t] : 0u;
   }
+  if (t < 64) {  // quad engine: K'_i, the lanes' N limbs (limb 9 l + r at word 4 r + l)
+    cst[FBM_CST_QK + t] = t < FBM_QA_L ? qa.kp[t] : 0u;
+    const int r = t >> 2, l = t & 3;
+    cst[FBM_CST_QN + t] = t < 4 * FBM_QA_LIMBS ? qa.n[FBM_QA_LIMBS * l + r] : 0u;
+  }
+  if (t < 128) {
+    cst[FBM_CST_QR2 + t] = t < 2 * FBM_QA_L ? qa.r2[t] : 0u;
+    cst[FBM_CST_QR3 + t] = t < 2 * FBM_QA_L ? qa.r3[t] : 0u;
+  }
   for (int i = t; i < FBM_NL * 256; i += blockDim.x) {
     const int k = i >> 8, l = i & 255;
     cst[FBM_CST_ONE + i] = (l == 0 && k == 0) ? 1u : 0u;
@@ -1131,14 +1383,68 @@ __global__ void jl_setup_kernel(JlSched sc, MontCtx mc, NadicCtx na, uint32_t* _
 }
 
 int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32_t* cst, hipStream_t s) {
-  hipLaunchKernelGGL(jl_setup_kernel, dim3(1), dim3(256), 0, s, sc, jp.mc, jp.na, ops, cst);
+  hipLaunchKernelGGL(jl_setup_kernel, dim3(1), dim3(256), 0, s, sc, jp.mc, jp.na, jp.qa, ops, cst);
   return check_launch("jl_setup_kernel");
+}
+
+// ---- exponentiation engine choice ------------------------------------------------------
+// FBM_ENGINE_SINGLE: one lane per ciphertext (throughput: every lane busy, 2 waves/SIMD);
+// FBM_ENGINE_QUAD: four lanes per ciphertext (latency: launches below the chip's lane count);
+// FBM_ENGINE_AUTO: QUAD when every quad wave of the launch is resident at once (at most 3 per
+// SIMD: 3/8 of a one-lane round, 49 152 ciphertexts on 256 CUs); above that the one-lane
+// engine's lone-lane latency is the cheaper bound (measured: DESIGN.md section 5).
+static std::atomic<int> g_engine{-1};
+
+int jl_engine_policy() {
+  int e = g_engine.load(std::memory_order_relaxed);
+  if (e < 0) {  // first use: FBM_JL_ENGINE=auto|single|quad (A/B runs), default auto
+    const char* v = getenv("FBM_JL_ENGINE");
+    e = FBM_ENGINE_AUTO;
+    if (v && !strcmp(v, "single")) e = FBM_ENGINE_SINGLE;
+    if (v && !strcmp(v, "quad")) e = FBM_ENGINE_QUAD;
+    int expect = -1;
+    g_engine.compare_exchange_strong(expect, e);
+    e = g_engine.load(std::memory_order_relaxed);
+  }
+  return e;
+}
+
+int jl_engine_set(int mode) {
+  const int prev = jl_engine_policy();
+  g_engine.store(mode, std::memory_order_relaxed);
+  return prev;
+}
+
+static uint64_t quad_wgs_max() { return (uint64_t)device_num_cu() * 3; }  // 3 workgroups (12 waves) per CU
+
+bool jl_use_quad(uint64_t n_ct) {
+  const int e = jl_engine_policy();
+  if (e == FBM_ENGINE_QUAD) return true;
+  if (e == FBM_ENGINE_SINGLE) return false;
+  return n_ct * 8 <= jl_table_slots() * 3;
+}
+
+uint64_t jl_table_bytes(uint64_t n_ct) {
+  const uint64_t cap = jl_table_slots();
+  uint64_t g = ((n_ct + 255) / 256) * 256;
+  const uint64_t single = (g < cap ? g : cap) * FBM_TENTRIES * FBM_NL * 4;
+  uint64_t wq = (n_ct + FBM_QCT - 1) / FBM_QCT;
+  if (wq > quad_wgs_max()) wq = quad_wgs_max();
+  const uint64_t quad = wq * FBM_TENTRIES * FBM_QENTRY * 4;
+  return single > quad ? single : quad;
 }
 
 int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const JlSched& sc, int mode,
                   const uint32_t* nude, uint32_t* table, uint64_t table_slots, const uint32_t* ops,
                   const uint32_t* cst, uint32_t* out, hipStream_t s) {
   if (n_ct == 0) return FBM_OK;
+  if (jl_use_quad(n_ct)) {
+    uint64_t g = (n_ct + FBM_QCT - 1) / FBM_QCT;
+    if (g > quad_wgs_max()) g = quad_wgs_max();
+    hipLaunchKernelGGL(jl_expq_kernel, dim3((unsigned)g), dim3(FBM_QBLOCK), 0, s, H, n_ct, (uint32_t*)cst, jp.qa.np,
+                       ops, sc.n_ops, sc.first, mode, jp.key_is_zero, nude, table, out);
+    return check_launch("jl_expq_kernel");
+  }
   uint64_t g = (n_ct + FBM_BLOCK - 1) / FBM_BLOCK;
   const uint64_t gmax = table_slots / FBM_BLOCK;
   if (g > gmax) g = gmax;

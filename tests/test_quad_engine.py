@@ -1,0 +1,124 @@
+"""The quad exponentiation engine (four lanes per ciphertext, jl_expq_kernel) against the
+one-lane engine and the oracle, through the C-ABI: every JL entry point that exponentiates
+(encrypt, decryption factor, aggregate) must give bit-identical results under both engines,
+on the default biprime, small moduli (FDH retries: the wide-digest path), negative keys
+(H^-1 as N-adic digits), a zero key and negative weights.  The engine choice itself
+(fbm_jl_set_engine / auto by launch size) is checked on the host without a GPU."""
+
+import numpy as np
+import pytest
+import torch
+
+from fedbiomed_amd import _device as D, workload as W
+from oracle import secagg_oracle as O
+
+
+def test_engine_policy_host():
+    from fedbiomed_amd import _build, _native
+
+    _build.build()
+    lib = _native.load()
+    prev = lib.fbm_jl_set_engine(1)
+    try:
+        assert lib.fbm_jl_engine_for(10) == 1
+        assert lib.fbm_jl_set_engine(4) == 1 and lib.fbm_jl_engine_for(10**7) == 4
+        assert lib.fbm_jl_set_engine(7) == _native.FBM_E_ARG
+        lib.fbm_jl_set_engine(0)  # auto: small launches quad, chip-filling ones single
+        assert lib.fbm_jl_engine_for(1000) == 4 and lib.fbm_jl_engine_for(333_334) == 1
+    finally:
+        lib.fbm_jl_set_engine(prev)
+    import importlib.util
+    import os
+
+    spec = importlib.util.spec_from_file_location(
+        "gen_quad_asm", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools",
+                                     "gen_quad_asm.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    assert lib.fbm_jl_quad_mads(1) == 4 * g.product_mads(True) and lib.fbm_jl_quad_mads(0) == 4 * g.product_mads(False)
+
+
+def _both(fn):
+    outs = []
+    for eng in ("single", "quad"):
+        with D.jl_engine(eng):
+            outs.append(fn())
+    return outs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["bench", "negkey", "zerokey", "negweight"])
+def test_quad_equals_single_encrypt_aggregate(case):
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    dev = D.device()
+    n, P, tau = 3_001, 3, 5
+    keys = [W.jl_user_key(p) for p in range(P)]
+    ws = [W.party_weight(p) for p in range(P)]
+    if case == "negkey":
+        keys[1] = -keys[1]
+    if case == "zerokey":
+        keys[2] = 0
+    if case == "negweight":
+        ws[0] = -ws[0]
+    jc = SecaggCrypter()
+    xs = [torch.from_numpy(W.party_params(p, n)).to(dev) for p in range(P)]
+
+    def enc():
+        return torch.stack([jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=ws[p]) for p in range(P)])
+
+    c1, c4 = _both(enc)
+    assert torch.equal(c1, c4)
+    es, cr = O.jl_slot(None, P)
+    for p in range(P):  # first, last and one middle ciphertext vs the oracle
+        qw = [int(v) * ws[p] for v in O.quantize(W.party_params(p, n).astype(np.float64))]
+        for k in (0, 50, c1.shape[1] - 1):
+            got = D.limbs_to_ints(c1[p, k:k + 1].cpu().numpy())[0]
+            assert got == O.jl_encrypt_ints(qw[k * cr:(k + 1) * cr], tau, keys[p], W.BIPRIME0, P, k0=k)[0]
+    sk0 = -sum(keys)
+    a1, a4 = _both(lambda: jc.aggregate_tensor(tau, c1, sk0, W.BIPRIME0, 77, num_expected_params=n,
+                                               want_sums=True))
+    assert torch.equal(a1[0], a4[0]) and torch.equal(a1[1], a4[1])
+
+
+_N297 = 105 * (__import__("random").Random(5).getrandbits(290) | 1 | (1 << 289))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nmod", [0xC9F2B5, 123457, 3000009, 15015, _N297])
+def test_quad_equals_single_small_moduli(nmod):
+    """Small odd moduli: FDH digests wider than R (gcd retries, 3000009 = 3 * 1000003 and
+    15015 = 3 * 5 * 7 * 11 * 13 retry often) take the wide path on both engines.  The launch
+    stops before the first ciphertext whose digests overflow (the reference's OverflowError)."""
+    dev = D.device()
+    n2 = nmod * nmod
+    n_ct, retries = 300, 0
+    for k in range(300):
+        try:
+            h = O.fdh((k << 512) | 3, n2)
+        except OverflowError:
+            n_ct = k
+            break
+        retries += h.bit_length() > 256
+    f1, f4 = _both(lambda: D.jl_decrypt_factor(n_ct, nmod, 123456789, 3, dev=dev))
+    assert torch.equal(f1, f4)
+    got = D.limbs_to_ints(f1.cpu().numpy())
+    for k in range(0, n_ct, max(1, n_ct // 40)):
+        h = O.fdh((k << 512) | 3, n2)
+        assert got[k] == O.powmod(h, 123456789, n2), k
+    if nmod in (3000009, 15015, _N297):
+        assert retries > 0 and n_ct >= 10
+    if nmod == _N297:  # digests past R = 2^1036 whose high part spans several lanes' limbs
+        assert any(O.fdh((k << 512) | 3, n2).bit_length() > 1100 for k in range(n_ct))
+
+
+@pytest.mark.gpu
+def test_quad_factor_stripe_config4():
+    """The 1/8 stripe of config 4 (41 667 ciphertexts: the auto policy's quad case) and an
+    offset stripe: identical factors under both engines."""
+    dev = D.device()
+    sk0 = W.jl_server_key(8)
+    for n_ct, off in ((41_667, 0), (5_000, 41_667 * 3)):
+        f1, f4 = _both(lambda: D.jl_decrypt_factor(n_ct, W.BIPRIME0, sk0, 1, ct_offset=off, dev=dev))
+        assert torch.equal(f1, f4)
+    assert D.jl_engine_for(41_667) == "quad"

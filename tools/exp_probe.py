@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Drives the JL exponentiation alone for profiling: the decryption factor H(t_k)^sk0 of
+`--ct` ciphertexts under each engine (rocprofv3 --kernel-trace / --pmc attribute the
+dispatches to jl_exp_kernel / jl_expq_kernel).  Prints per-engine wall times.
+
+    python tools/exp_probe.py [--ct 41667] [--engines single,quad] [--reps 2]
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ct", type=int, default=41_667)
+    ap.add_argument("--engines", default="single,quad")
+    ap.add_argument("--reps", type=int, default=2)
+    args = ap.parse_args()
+    import torch
+
+    from fedbiomed_amd import _device as D, workload as W
+
+    dev = D.device()
+    sk0 = W.jl_server_key(8)
+    out = {"ct": args.ct}
+    for eng in args.engines.split(","):
+        with D.jl_engine(eng):
+            D.jl_decrypt_factor(args.ct, W.BIPRIME0, sk0, 1, dev=dev)
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(args.reps):
+                t0 = time.perf_counter()
+                D.jl_decrypt_factor(args.ct, W.BIPRIME0, sk0, 1, dev=dev)
+                torch.cuda.synchronize()
+                ts.append(1000 * (time.perf_counter() - t0))
+        out[eng + "_ms"] = ts
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
