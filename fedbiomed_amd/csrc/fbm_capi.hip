@@ -120,6 +120,69 @@ static Big big_pow2_mod(int e, const Big& m) {
   return x;
 }
 
+// a b 2^-32n mod m (CIOS over n = m.size() 32-bit words; m odd, a, b < m)
+static Big host_mont(const Big& a, const Big& b, const Big& m, uint32_t mi) {
+  const size_t n = m.size();
+  std::vector<uint32_t> t(n + 2, 0u);
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t c = 0;
+    for (size_t j = 0; j < n; ++j) {
+      const uint64_t v = (uint64_t)a[j] * b[i] + t[j] + c;
+      t[j] = (uint32_t)v;
+      c = v >> 32;
+    }
+    uint64_t v = (uint64_t)t[n] + c;
+    t[n] = (uint32_t)v;
+    t[n + 1] = (uint32_t)(v >> 32);
+    const uint32_t q = t[0] * mi;
+    c = ((uint64_t)q * m[0] + t[0]) >> 32;
+    for (size_t j = 1; j < n; ++j) {
+      const uint64_t w = (uint64_t)q * m[j] + t[j] + c;
+      t[j - 1] = (uint32_t)w;
+      c = w >> 32;
+    }
+    v = (uint64_t)t[n] + c;
+    t[n - 1] = (uint32_t)v;
+    t[n] = t[n + 1] + (uint32_t)(v >> 32);
+  }
+  Big r(t.begin(), t.begin() + n + 1);
+  if (big_cmp(r, m) >= 0) big_sub_inplace(r, m);
+  r.resize(n);
+  return r;
+}
+
+// 2^e mod m (m odd, > 1, top word nonzero or not): left-to-right, Montgomery squarings and
+// plain modular doublings -- log2(e) products instead of e doublings (big_pow2_mod)
+static Big big_pow2_mod_mont(uint64_t e, Big m) {
+  while (m.size() > 1 && m.back() == 0u) m.pop_back();
+  const size_t n = m.size();
+  uint32_t inv = m[0];  // Newton: m^-1 mod 2^32
+  for (int i = 0; i < 5; ++i) inv *= 2u - m[0] * inv;
+  const uint32_t mi = 0u - inv;
+  Big x = big_pow2_mod((int)(32 * n), m);  // 1 in Montgomery form
+  x.resize(n);
+  auto dbl = [&](Big& y) {
+    Big z(y.begin(), y.end());
+    z.push_back(0u);
+    uint32_t c = 0;
+    for (size_t k = 0; k < z.size(); ++k) {
+      const uint32_t nc = z[k] >> 31;
+      z[k] = (z[k] << 1) | c;
+      c = nc;
+    }
+    if (big_cmp(z, m) >= 0) big_sub_inplace(z, m);
+    z.resize(n);
+    y = z;
+  };
+  for (int b = 63; b >= 0; --b) {
+    x = host_mont(x, x, m, mi);
+    if ((e >> b) & 1u) dbl(x);
+  }
+  Big one(n, 0u);
+  one[0] = 1u;
+  return host_mont(x, one, m, mi);
+}
+
 static void to_limbs_host(const Big& a, uint32_t* o, int nl, int lb) {
   for (int k = 0; k < nl; ++k) {
     const int bit = k * lb, wi = bit >> 5, sh = bit & 31;
@@ -645,7 +708,7 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
   off += align256(n_ct * 64 * 4);
   uint32_t* table = (uint32_t*)(ws + off);
   off += align256(jl_table_bytes(n_ct));
-  uint32_t* Hinv = (uint32_t*)(ws + off);  // negative keys only (after the table: keeps its placement)
+  uint32_t* Hinv = (uint32_t*)(ws + off);  // negative keys only: H^|key| digits (after the table)
   off += align256(n_ct * 64 * 4);
   uint32_t* Y = (uint32_t*)(ws + off);
   const bool inverse = key_negative && !is_zero;
@@ -655,18 +718,20 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
     const int negw = (int64_t)weight < 0 ? 1 : 0;
     if ((rc = timed("jl_nude", s, [&] { return launch_jl_nude(pt, n_ct, jp, negw, nude, s); }))) return rc;
     if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, H, stats, s); }))) return rc;
-    if (inverse) {
-      // gmpy2.powmod with a negative exponent (_jls.py:60-73): invert H(t_k) mod N^2 first,
-      // then raise the inverse to |key|
-      if ((rc = timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, H, Y, Hinv, stats, s); }))) return rc;
-      // the inverse is a full-width residue: hand it to the exponentiation as N-adic digits
-      if ((rc = timed("jl_split", s, [&] { return launch_jl_nadic_split(n_ct, jp, Hinv, Y, Hinv, s); }))) return rc;
-    }
   }
   if (!(phase & 2)) return FBM_OK;
-  const uint32_t* base = inverse ? Hinv : H;
-  const int mode = inverse ? FBM_EXP_H_NADIC : 0;
-  return timed("jl_exp", s, [&] { return launch_jl_exp(base, n_ct, jp, sc, mode, nude, table, slots, ops, cst, ct_out, s); });
+  if (inverse) {
+    // gmpy2.powmod with a negative exponent (_jls.py:60-73) is (H^-1)^|key| = (H^|key|)^-1:
+    // the power's N-adic digits (any H < 2^2048), then the lift inverts it and multiplies
+    // by nude in the same pass
+    if ((rc = timed("jl_exp", s, [&] {
+           return launch_jl_exp(H, n_ct, jp, sc, FBM_EXP_DEC | FBM_EXP_OUT_NADIC, nullptr, table, slots, ops, cst, Hinv,
+                                s);
+         })))
+      return rc;
+    return timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, cst, Hinv, Y, nude, ct_out, stats, s); });
+  }
+  return timed("jl_exp", s, [&] { return launch_jl_exp(H, n_ct, jp, sc, 0, nude, table, slots, ops, cst, ct_out, s); });
 }
 
 int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
@@ -741,10 +806,14 @@ static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t
     if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, w.H, stats, s); }))) return rc;
   }
   if ((phase & 2) &&
-      (rc = timed("jl_exp", s, [&] { return launch_jl_exp(w.H, n_ct, jp, sc, FBM_EXP_DEC, nullptr, w.table, w.slots, w.ops, w.cst, E, s); })))
+      (rc = timed("jl_exp", s, [&] {
+         // the inverse starts from the power's N-adic digits (no division by N needed)
+         return launch_jl_exp(w.H, n_ct, jp, sc, FBM_EXP_DEC | (inv ? FBM_EXP_OUT_NADIC : 0), nullptr, w.table, w.slots,
+                              w.ops, w.cst, E, s);
+       })))
     return rc;
   if ((phase & 4) && inv &&
-      (rc = timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, E, w.xs, factor, stats, s); })))  // xs: y scratch
+      (rc = timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, w.cst, E, w.xs, nullptr, factor, stats, s); })))  // xs: y scratch
     return rc;
   return FBM_OK;
 }
@@ -759,8 +828,18 @@ static int jl_combine_impl(const uint32_t* cts, int n_parties, uint64_t n_ct, in
   JlSched none;
   memset(&none, 0, sizeof(none));
   if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, none, w.ops, w.cst, s); }))) return rc;
-  if ((rc = timed("jl_prod", s, [&] { return launch_jl_prod(cts, n_parties, n_ct, jp, w.cst, w.X, s); }))) return rc;
-  if ((rc = timed("jl_fin", s, [&] { return launch_jl_fin(n_ct, jp, w.X, factor, w.xs, s); }))) return rc;
+  {  // R^(P+1) mod N^2: the product's uniform first operand (P + 1 products each drop one R)
+    Big M(jp.N32, jp.N32 + 32);
+    M = big_mul(M, M);
+    M.resize(64);
+    const Big rk = big_pow2_mod_mont((uint64_t)(n_parties + 1) * FBM_NL * FBM_LB, M);
+    JlRk r;
+    memset(&r, 0, sizeof(r));
+    to28_host(rk, r.w, FBM_NL);
+    if ((rc = timed("jl_rk", s, [&] { return launch_jl_rk(r, w.cst, s); }))) return rc;
+  }
+  if ((rc = timed("jl_prod", s, [&] { return launch_jl_prod(cts, n_parties, n_ct, jp, w.cst, factor, w.X, w.xs, s); })))
+    return rc;
   return timed("jl_decode", s, [&] {
     return launch_jl_decode(w.xs, es, cr, n_out, total_weight, neg_clip, step, out, sums, stats, s);
   });

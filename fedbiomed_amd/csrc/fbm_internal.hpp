@@ -61,17 +61,18 @@ int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t 
 #define FBM_TENTRIES (FBM_TABLE + 1)    // + one scratch column (h, then h^2)
 #define FBM_TSCRATCH FBM_TABLE
 
-// per-call device constants (words): M, R^2 (74 limbs, padded to 128) and the broadcast
-// columns 1 and R^2 (limb k at word k*256)
+// per-call device constants (words): M, R^2 (74 limbs, padded to 128), the broadcast
+// column 1 (limb k at word k*256) and R^(P+1) mod M (the aggregate's uniform first operand,
+// written by jl_rk_kernel: P parties + the factor leave the product at the plain value)
 #define FBM_CST_M 0
 #define FBM_CST_CTR 120  // exp-kernel chunk counter (in M's padding; zeroed by jl_setup_kernel)
 #define FBM_CST_R2 128
 #define FBM_CST_ONE 256
-#define FBM_CST_R2COL (256 + FBM_NL * 256)
+#define FBM_CST_RK (256 + FBM_NL * 256)
 // N-adic exponentiation engine (fbm_nadic_asm.hpp): its 80-word constants block (N limbs
 // and K'_i, the layout the assembly's scalar loads expect) and R^2 mod N^2 as two N-adic
 // digits (74 limbs, the uniform A operand that brings h into Montgomery form)
-#define FBM_CST_NK (256 + 2 * FBM_NL * 256)
+#define FBM_CST_NK (FBM_CST_RK + 128)
 #define FBM_CST_R2NA (FBM_CST_NK + 128)
 #define FBM_CST_R3NA (FBM_CST_R2NA + 128)  // R^3 mod N^2 (digits): the high part of a wide h
 // quad engine (fbm_quad_asm.hpp, 29-bit limbs, R = 2^1044): K'_i (36 words), the lanes' N
@@ -80,7 +81,11 @@ int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t 
 #define FBM_CST_QN (FBM_CST_QK + 64)
 #define FBM_CST_QR2 (FBM_CST_QN + 64)
 #define FBM_CST_QR3 (FBM_CST_QR2 + 128)
-#define FBM_CST_WORDS (FBM_CST_QR3 + 128)
+// the MontCtxN image (M, R^2 mod N, mp: 76 words) for the mod-N products of jl_emodn /
+// jl_lift, read through device memory (a laundered pointer into the by-value JlParams
+// kernel argument would make the compiler copy all 3.3 KB of it to scratch per lane)
+#define FBM_CST_MN (FBM_CST_QR3 + 128)
+#define FBM_CST_WORDS (FBM_CST_MN + 128)
 
 // sliding-window schedule, passed by value (kernarg segment -> scalar loads).
 // op k (u16): (squarings before the multiply) << FBM_OP_SHIFT | (table index + 1, 0 = none)
@@ -115,7 +120,7 @@ struct JlParams {
   MontCtxN mn;                   // modulus N (37 limbs) -- inverse mod N, N*pt, N-adic np
   NadicCtx na;                   // N-adic engine constants (jl_exp_kernel)
   uint32_t N32[32];              // N, 32-bit limbs (<= 1024 bits)
-  uint32_t Ninv32[32];           // N^-1 mod 2^1024 (exact division (v-1)/N in jl_fin_kernel)
+  uint32_t Ninv32[32];           // N^-1 mod 2^1024 (exact divisions by N: jl_prod, jl_lift, jl_split)
   int n_bits;                    // bit length of N
   int es, cr;                    // VES slot size / slots per ciphertext
   uint64_t tau;
@@ -138,17 +143,21 @@ int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32
 int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const JlSched& sc, int mode,
                   const uint32_t* nude, uint32_t* table, uint64_t table_slots, const uint32_t* ops,
                   const uint32_t* cst, uint32_t* out, hipStream_t s);
+struct JlRk {  // R^(P+1) mod N^2, 28-bit limbs (jl_rk_kernel -> cst[FBM_CST_RK])
+  uint32_t w[FBM_NL];
+  uint32_t pad[2];
+};
+int launch_jl_rk(const JlRk& rk, uint32_t* cst, hipStream_t s);
+// x_k = (prod_u c_u * F_k mod N^2 - 1) div N   (cst[FBM_CST_RK] = R^(P+1) mod N^2)
 int launch_jl_prod(const uint32_t* cts, int n_parties, uint64_t n_ct, const JlParams& jp, const uint32_t* cst,
-                   uint32_t* X, hipStream_t s);
-#define FBM_EXP_DEC 1      // jl_exp mode bits: plain power (no nude product)
-#define FBM_EXP_H_NADIC 2  // H rows are N-adic digit pairs (jl_split_kernel)
+                   const uint32_t* factor, uint32_t* X, uint32_t* xout, hipStream_t s);
+#define FBM_EXP_DEC 1        // jl_exp mode bits: plain power (no nude product)
+#define FBM_EXP_OUT_NADIC 4  // out rows are the result's N-adic digits (v mod N, v div N)
 int host_gcd_is_one_r8(const uint32_t* r8, const uint32_t* n32, uint32_t* err);
-int launch_jl_nadic_split(uint64_t n_ct, const JlParams& jp, const uint32_t* E, uint32_t* Y, uint32_t* out,
-                          hipStream_t s);
-int launch_jl_inv(uint64_t n_ct, const JlParams& jp, const uint32_t* E, uint32_t* Y, uint32_t* inv, uint32_t* stats,
-                  hipStream_t s);
-int launch_jl_fin(uint64_t n_ct, const JlParams& jp, const uint32_t* X, const uint32_t* inv, uint32_t* xout,
-                  hipStream_t s);
+// E^-1 mod N^2 (times nude when given: a negative-key encrypt) from E's N-adic digit rows
+// Ed [ct][64] (e0 | e1): y = e0^-1 mod N into Y [ct][32], then the lift -> out [ct][64]
+int launch_jl_inv(uint64_t n_ct, const JlParams& jp, const uint32_t* cst, const uint32_t* Ed, uint32_t* Y,
+                  const uint32_t* nude, uint32_t* out, uint32_t* stats, hipStream_t s);
 int launch_jl_decode(const uint32_t* xs, int es, int cr, uint64_t n_out, uint64_t total_weight, double neg_c,
                      double step, double* out, uint64_t* sums, uint32_t* stats, hipStream_t s);
 

@@ -7,11 +7,12 @@
 //   jl_fdh_kernel    FDH.H(t_k), t_k = (k<<512)|tau       (_jls.py:451-467,727-762)
 //   jl_exp_kernel    H^sk mod N^2 (GMP mpz_powm via gmpy2, _jls.py:60-73,500-501) and
 //                    the final product with nude           (_jls.py:502)
-// Aggregate:  prod -> fdh -> exp(DEC) -> inv -> fin -> decode
-//   jl_prod_kernel   prod_u c_u mod N^2                    (_jls.py:353-374,691-693)
-//   jl_exp_kernel    H^|sk0| mod N^2                       (_jls.py:550-551)
-//   jl_inv_kernel    (H^|sk0|)^-1 mod N^2 (gmpy2.powmod with b<0 inverts; _jls.py:550-551)
-//   jl_fin_kernel    v = prod * inv mod N^2, x = ((v-1)//N) mod N   (_jls.py:553-558)
+// Aggregate:  fdh -> exp(DEC, digits out) -> inv -> lift -> prod -> decode
+//   jl_exp_kernel    H^|sk0| mod N^2 as N-adic digits     (_jls.py:550-551)
+//   jl_inv_modn_kernel, jl_lift_kernel
+//                    (H^|sk0|)^-1 mod N^2 (gmpy2.powmod with b<0 inverts; _jls.py:550-551)
+//   jl_prod_kernel   v = prod_u c_u * factor mod N^2, x = (v-1)//N   (_jls.py:353-374,
+//                    691-693, 553-558)
 //   jl_decode_kernel VES.decode + _apply_average + reverse_quantize
 //                    (_jls.py:146-192, _secagg_crypter.py:233-249, _secagg_utils.py:152-187)
 //
@@ -421,9 +422,10 @@ __device__ __forceinline__ uint32_t csub28(uint32_t (&x)[L], const uint32_t (&n)
 
 // N-adic result (t, s) in the lane's LDS column (t < N + 1, s < 2N: the last product of
 // the exponentiation has a (1, .) operand) -> the canonical residue V = t + s N < N^2,
-// 64 words.  NK: the engine's constants block (N limbs at words 0..9, 16..42).
+// 64 words, or (nadic_out) its reduced digits (V mod N | V div N), 32 words each.
+// NK: the engine's constants block (N limbs at words 0..9, 16..42).
 __device__ __forceinline__ void na_final_digits(uint32_t (&t)[FBM_NLN], uint32_t (&sd)[FBM_NLN], const uint32_t* NK,
-                                                uint32_t (&w)[64]) {
+                                                uint32_t (&w)[64], int nadic_out = 0) {
   const uint32_t* nk = launder_s(NK);
   uint32_t n[FBM_NLN];
 #pragma unroll
@@ -440,6 +442,17 @@ __device__ __forceinline__ void na_final_digits(uint32_t (&t)[FBM_NLN], uint32_t
   csub28(sd, n);
   csub28(sd, n);
   csub28(sd, n);
+  if (nadic_out) {  // the digits themselves (the inverse's input: no division by N needed)
+    uint32_t d0[32], d1[32];
+    from28<FBM_NLN, 32>(t, d0);
+    from28<FBM_NLN, 32>(sd, d1);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      w[i] = d0[i];
+      w[32 + i] = d1[i];
+    }
+    return;
+  }
   // V = t + s N by columns (each < 37 products < 2^56 + t limb + carry)
   uint32_t v28[FBM_NL];
   uint64_t carry = 0;
@@ -455,20 +468,19 @@ __device__ __forceinline__ void na_final_digits(uint32_t (&t)[FBM_NLN], uint32_t
   from28<FBM_NL, 64>(v28, w);
 }
 
-__device__ __forceinline__ void na_final(const uint32_t* lds, const uint32_t* NK, uint32_t (&w)[64]) {
+__device__ __forceinline__ void na_final(const uint32_t* lds, const uint32_t* NK, uint32_t (&w)[64], int nadic_out) {
   uint32_t t[FBM_NLN], sd[FBM_NLN];
 #pragma unroll
   for (int k = 0; k < FBM_NLN; ++k) {
     t[k] = lds[k * FBM_BLOCK];
     sd[k] = lds[(FBM_NLN + k) * FBM_BLOCK];
   }
-  na_final_digits(t, sd, NK, w);
+  na_final_digits(t, sd, NK, w, nadic_out);
 }
 
 // mode 0 (ENC): out[ct] = nude[ct] * H[ct]^key  mod N^2          (ciphertext)
 // mode 1 (DEC): out[ct] = H[ct]^key mod N^2 (plain)                (for the inverse)
-// | FBM_EXP_H_NADIC: H rows hold the N-adic digits (h mod N, h div N) of any h < N^2
-//   (jl_split_kernel; the inverse H^-1 of a negative-key encrypt)
+// | FBM_EXP_OUT_NADIC: out rows hold the result's digits (v mod N, v div N) (jl_lift_kernel)
 // N-adic engine (fbm_nadic_asm.hpp): a residue is the digit pair (x0, x1), X = x0 + x1 N,
 // 74 limbs = 2 x 37 in the same blocked columns.  Sliding window (width FBM_WIN,
 // FBM_TABLE odd powers) over the device copy of the host-built schedule.  Per-lane table:
@@ -522,21 +534,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
         load_row64(H + ct * 64, h);
       }
       uint32_t h28[FBM_NL];
-      if (mode & FBM_EXP_H_NADIC) {  // (h mod N, h div N) as two 1024-bit rows
-        uint32_t d0[32], d1[32], l0[FBM_NLN], l1[FBM_NLN];
-#pragma unroll
-        for (int i = 0; i < 32; ++i) {
-          d0[i] = h[i];
-          d1[i] = h[32 + i];
-        }
-        to28<32, FBM_NLN>(d0, l0);
-        to28<32, FBM_NLN>(d1, l1);
-#pragma unroll
-        for (int k = 0; k < FBM_NLN; ++k) {
-          h28[k] = l0[k];
-          h28[FBM_NLN + k] = l1[k];
-        }
-      } else {  // h = h_lo + h_hi R (R = 2^1036): the 74-limb decomposition is (h_lo, h_hi)
+      {  // h = h_lo + h_hi R (R = 2^1036): the 74-limb decomposition is (h_lo, h_hi)
         to28<64, FBM_NL>(h, h28);
         uint32_t hi = 0;
 #pragma unroll
@@ -608,7 +606,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
     else
       fbm_na_mm_glb(aoff, cst + FBM_CST_ONE, 0u, NK, np);
     uint32_t w[64];
-    na_final(lds, NK, w);
+    na_final(lds, NK, w, mode & FBM_EXP_OUT_NADIC);
     if (valid) store_row64(out + ct * 64, w);
   }
 }
@@ -719,7 +717,7 @@ __global__ void __launch_bounds__(FBM_QBLOCK, 3) jl_expq_kernel(const uint32_t* 
     const uint64_t ct = valid ? ct_raw : n_ct - 1;
     uint32_t* scratch = table + (tb0 + FBM_TSCRATCH * tstride) / 4;
     bool wide = false;
-    {  // h -> the lane's 29-bit limbs of (h mod R, h div R) (or the N-adic digits) -> scratch
+    {  // h -> the lane's 29-bit limbs of (h mod R, h div R) -> scratch
       uint32_t h18[2 * FBM_QA_LIMBS];
       const uint32_t* hr = H + ct * 64;
 #pragma unroll
@@ -728,9 +726,6 @@ __global__ void __launch_bounds__(FBM_QBLOCK, 3) jl_expq_kernel(const uint32_t* 
         uint32_t lo = 0, hi = 0;
         if (key_is_zero) {
           lo = k == 0 ? 1u : 0u;
-        } else if (mode & FBM_EXP_H_NADIC) {  // (h mod N, h div N) as two 1024-bit rows
-          lo = glb_limb(hr, 32, k, FBM_QA_LB);
-          hi = glb_limb(hr + 32, 32, k, FBM_QA_LB);
         } else {
           lo = glb_limb(hr, 64, k, FBM_QA_LB);
           hi = glb_limb(hr, 64, FBM_QA_L + k, FBM_QA_LB);
@@ -738,7 +733,7 @@ __global__ void __launch_bounds__(FBM_QBLOCK, 3) jl_expq_kernel(const uint32_t* 
         h18[r] = lo;
         h18[FBM_QA_LIMBS + r] = hi;
       }
-      if (!(mode & FBM_EXP_H_NADIC)) {
+      {
         uint32_t any = 0;
 #pragma unroll
         for (int r = 0; r < FBM_QA_LIMBS; ++r) any |= h18[FBM_QA_LIMBS + r];
@@ -763,7 +758,7 @@ __global__ void __launch_bounds__(FBM_QBLOCK, 3) jl_expq_kernel(const uint32_t* 
     }
     qa_lds_store_uniform(col, l, cst + FBM_CST_QR2);
     fbm_qa_mm_glb(ac, al, table, tb0 + FBM_TSCRATCH * tstride, QK, np29, n, e0);  // h R | h_lo R
-    if (!(mode & FBM_EXP_H_NADIC) && __any(wide)) {  // h R = h_lo R + h_hi R^2 (digit-wise, then carries)
+    if (__any(wide)) {  // h R = h_lo R + h_hi R^2 (digit-wise, then carries)
       uint32_t b18[2 * FBM_QA_LIMBS];
       col_load<2 * FBM_QA_LIMBS>(table + (tb0 + tstride) / 4, b18);
 #pragma unroll
@@ -840,166 +835,27 @@ __global__ void __launch_bounds__(FBM_QBLOCK, 3) jl_expq_kernel(const uint32_t* 
         sd[j] = (uint32_t)(sw >> off) & FBM_LMASK;
       }
       uint32_t w[64];
-      na_final_digits(t, sd, cst + FBM_CST_NK, w);
+      na_final_digits(t, sd, cst + FBM_CST_NK, w, mode & FBM_EXP_OUT_NADIC);
       if (valid) store_row64(out + ct * 64, w);
     }
   }
 }
 
 // ------------------------------------------------------------------------------------
-// aggregate: product of the P ciphertexts, X = prod_u c_u * R  (Montgomery form, lazy)
-//   a = R^2, b = c_0 -> c_0*R;  then per u >= 1:  *c_u (drops R), *R^2 (restores R)
-// c_u (any value < 2^2048) is staged as a 28-bit column in X's slot, which finally
-// receives the product.
+// (v - 1) div N for v < N^2 (64 words, v >= 1 for any unit: D = v - 1 on entry) -> x (32
+// words).  Exact whenever the keys are consistent (v = 1 + N x mod N^2): x = D N^-1 mod
+// 2^1024, accepted iff x N == D.  Otherwise (a wrong server key: the reference still returns
+// floor((v-1)/N), _jls.py:553-558) binary long division.
 // ------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(FBM_BLOCK, 2) jl_prod_kernel(const uint32_t* __restrict__ cts, int n_parties,
-                                                              uint64_t n_ct, const uint32_t* __restrict__ cst,
-                                                              uint32_t mp, uint32_t* __restrict__ X) {
-  __shared__ uint32_t lds_a[(FBM_NL + 1) * FBM_BLOCK];
-  const int tid = threadIdx.x;
-  uint32_t* lds = lds_a + tid;
-  const uint32_t aoff = lds_addr(lds);
-  const uint32_t* M = cst + FBM_CST_M;
-  const uint64_t ct_raw = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
-  const bool valid = ct_raw < n_ct;  // no early return: X is padded to whole blocks
-  const uint64_t ct = valid ? ct_raw : n_ct - 1;
-  const uint32_t xoff = (uint32_t)(((ct_raw >> 8) * (FBM_NL * 256) + (ct_raw & 255)) * 4);
-  lds_store_uniform<FBM_NL>(lds, FBM_BLOCK, cst + FBM_CST_R2);
-#pragma unroll 1
-  for (int u = 0; u < n_parties; ++u) {
-    {
-      uint32_t c32[64], c28[FBM_NL];
-      load_row64(cts + ((uint64_t)u * n_ct + ct) * 64, c32);
-      to28<64, FBM_NL>(c32, c28);
-      col_store(X + xoff / 4, c28);
-    }
-    fbm_mm_glb(aoff, X, xoff, M, mp);
-    if (u > 0) fbm_mm_glb(aoff, cst + FBM_CST_R2COL, 0u, M, mp);
-  }
-  lds_to_glb(lds, X + xoff / 4);
-}
-
-// ------------------------------------------------------------------------------------
-// inverse mod N^2 by Hensel lifting: y = e^-1 mod N (1024-bit binary extended Euclid),
-// inv = y * (2 - e*y) mod N^2.   e = H^|sk0| mod N^2 (plain).
-// ------------------------------------------------------------------------------------
-template <int W>
-__device__ __forceinline__ void shr1(uint32_t (&a)[W], uint32_t top) {
-#pragma unroll
-  for (int i = 0; i < W - 1; ++i) a[i] = (a[i] >> 1) | (a[i + 1] << 31);
-  a[W - 1] = (a[W - 1] >> 1) | (top << 31);
-}
-template <int W>
-__device__ __forceinline__ uint32_t add_into(uint32_t (&a)[W], const uint32_t* b) {
-  uint32_t c = 0;
-#pragma unroll
-  for (int i = 0; i < W; ++i) {
-    const uint64_t s = (uint64_t)a[i] + b[i] + c;
-    a[i] = (uint32_t)s;
-    c = (uint32_t)(s >> 32);
-  }
-  return c;
-}
-template <int W>
-__device__ __forceinline__ uint32_t sub_from(uint32_t (&a)[W], const uint32_t (&b)[W]) {
-  uint32_t br = 0;
-#pragma unroll
-  for (int i = 0; i < W; ++i) {
-    const uint64_t d = (uint64_t)a[i] - b[i] - br;
-    a[i] = (uint32_t)d;
-    br = (uint32_t)(d >> 63);
-  }
-  return br;
-}
-
-// stage 1a: E mod N -> Y [ct][32]
-__global__ void __launch_bounds__(FBM_BLOCK, 1) jl_emodn_kernel(uint64_t n_ct, JlParams jp,
-                                                               const uint32_t* __restrict__ E,
-                                                               uint32_t* __restrict__ Y) {
-  __shared__ uint32_t lds_a[FBM_NL * FBM_BLOCK];
-  const int tid = threadIdx.x;
-  uint32_t* lds = lds_a + tid;
-  const int ls = FBM_BLOCK;
-  const uint64_t ct = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
-  if (ct >= n_ct) return;
-
-  // --- e mod N = (e_hi * R_N + e_lo) mod N  with R_N = 2^1036 --------------------------
-  //   t1 = mont(R2N, hi) = hi*R_N mod N            (lazy, < 2N)
-  //   t2 = mont(1, mont(R2N, lo)) = lo mod N        (lazy, < 2N; lo may be >= N)
-  //   y  = t1 + t2 < 4N, then three conditional subtractions -> e mod N
-  uint32_t y28[FBM_NLN];
-  {
-    uint32_t e32[64];
-    load_row64(E + ct * 64, e32);
-    uint32_t e28[FBM_NL];
-    to28<64, FBM_NL>(e32, e28);
-    uint32_t lo[FBM_NLN];
-#pragma unroll
-    for (int k = 0; k < FBM_NLN; ++k) {
-      lo[k] = e28[k];
-      y28[k] = e28[k + FBM_NLN];
-    }
-    lds_store_uniform<FBM_NLN>(lds, ls, jp.mn.R2);
-    mont_mul(y28, lds, ls, jp.mn);  // hi * R_N mod N
-    mont_mul(lo, lds, ls, jp.mn);   // lo * R_N mod N
-    lds_store_one<FBM_NLN>(lds, ls);
-    mont_mul(lo, lds, ls, jp.mn);   // lo mod N
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < FBM_NLN; ++k) {
-      const uint32_t v = y28[k] + lo[k] + c;
-      y28[k] = v & FBM_LMASK;
-      c = v >> FBM_LB;
-    }
-    mont_csub(y28, jp.mn.M);
-    mont_csub(y28, jp.mn.M);
-    mont_csub(y28, jp.mn.M);
-  }
-  uint32_t u[32];
-  from28<FBM_NLN, 32>(y28, u);
-  uint4* yo = reinterpret_cast<uint4*>(Y + ct * 32);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) yo[i] = make_uint4(u[4 * i], u[4 * i + 1], u[4 * i + 2], u[4 * i + 3]);
-}
-
-// N-adic digits of e < N^2 (negative-key encrypt: the inverse H^-1 mod N^2 enters the
-// exponentiation as (e mod N, e div N)); r = Y = e mod N from jl_emodn_kernel, and
-// q = (e - r) / N exactly, as (e - r) * N^-1 mod 2^1024 (q < N).  out [ct][64]: words
-// 0..31 = r, 32..63 = q  (out may alias E: each lane reads its row before writing it).
-__global__ void __launch_bounds__(FBM_BLOCK) jl_split_kernel(uint64_t n_ct, JlParams jp,
-                                                            const uint32_t* E, const uint32_t* __restrict__ Y,
-                                                            uint32_t* out) {
-  const uint64_t ct = (uint64_t)blockIdx.x * FBM_BLOCK + threadIdx.x;
-  if (ct >= n_ct) return;
-  uint32_t e[64], r[32];
-  load_row64(E + ct * 64, e);
-  {
-    const uint4* yi = reinterpret_cast<const uint4*>(Y + ct * 32);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint4 v = yi[i];
-      r[4 * i] = v.x; r[4 * i + 1] = v.y; r[4 * i + 2] = v.z; r[4 * i + 3] = v.w;
-    }
-  }
-  // d = (e - r) mod 2^1024 (only the low half matters for the product mod 2^1024)
-  uint32_t d[32];
-  uint32_t br = 0;
-#pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    const uint64_t v = (uint64_t)e[i] - r[i] - br;
-    d[i] = (uint32_t)v;
-    br = (uint32_t)(v >> 63);
-  }
-  // q = d * N^-1 mod 2^1024, product scanning over 32-bit words (3-word column sums)
-  uint32_t q[32];
+__device__ __forceinline__ void mullo1024(const uint32_t (&d)[32], const uint32_t* m, uint32_t (&q)[32]) {
+  // q = d * m mod 2^1024, product scanning over 32-bit words (3-word column sums)
   uint64_t lo = 0, hi = 0;
-#pragma unroll
+#pragma clang loop unroll(full)
   for (int k = 0; k < 32; ++k) {
-#pragma unroll
+#pragma clang loop unroll(full)
     for (int i = 0; i <= k; ++i) {
-      const uint64_t p = (uint64_t)d[i] * jp.Ninv32[k - i];
-      const uint64_t t = lo + (uint32_t)p;
-      lo = t;
+      const uint64_t p = (uint64_t)d[i] * m[k - i];
+      lo += (uint32_t)p;
       hi += (p >> 32);
     }
     q[k] = (uint32_t)lo;
@@ -1007,204 +863,42 @@ __global__ void __launch_bounds__(FBM_BLOCK) jl_split_kernel(uint64_t n_ct, JlPa
     lo = c & 0xffffffffull;
     hi = c >> 32;
   }
-  uint4* o = reinterpret_cast<uint4*>(out + ct * 64);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) o[i] = make_uint4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) o[8 + i] = make_uint4(q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]);
 }
 
-// stage 1b: y = (e mod N)^-1 mod N in place in Y, by Bernstein-Yang divsteps
-// (fbm_safegcd.hpp): branch-free batches of 30 divsteps; the loop leaves when every lane
-// of the wave is done (a finished lane is a fixed point of further batches).
-__global__ void __launch_bounds__(FBM_BLOCK) jl_inv_modn_kernel(uint64_t n_ct, JlParams jp,
-                                                               uint32_t* __restrict__ Y,
-                                                               uint32_t* __restrict__ stats) {
-  const uint64_t ct_raw = (uint64_t)blockIdx.x * FBM_BLOCK + threadIdx.x;
-  const uint64_t ct = ct_raw < n_ct ? ct_raw : n_ct - 1;  // all lanes take part in the vote
-  uint32_t err = 0;
-  uint32_t x1[32];
-  {
-    uint32_t u[32];
-    const uint4* yi = reinterpret_cast<const uint4*>(Y + ct * 32);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint4 v = yi[i];
-      u[4 * i] = v.x; u[4 * i + 1] = v.y; u[4 * i + 2] = v.z; u[4 * i + 3] = v.w;
+// r = a * b (32 x 32 words -> 64), product scanning like mullo1024 (fully unrolled: a
+// row-by-row form gets re-rolled by the optimiser into a loop over a scratch array)
+__device__ __forceinline__ void mul1024(const uint32_t (&a)[32], const uint32_t* b, uint32_t (&r)[64]) {
+  uint64_t lo = 0, hi = 0;
+#pragma clang loop unroll(full)
+  for (int k = 0; k < 63; ++k) {
+#pragma clang loop unroll(full)
+    for (int i = (k < 32 ? 0 : k - 31); i <= (k < 32 ? k : 31); ++i) {
+      const uint64_t p = (uint64_t)a[i] * b[k - i];
+      lo += (uint32_t)p;
+      hi += (p >> 32);
     }
-    FbmInvState st;
-    fbm_modinv_init(st, u, jp.n30);
-    for (int b = 0; b < FBM_INV_MAX_BATCHES; ++b) {
-      if (__all(fbm_s30_is_zero(st.g))) break;
-      fbm_modinv_batch(st, jp.n30);
-    }
-    if (!fbm_s30_is_zero(st.g)) {
-      err |= FBM_ERR_ITER_CAP;
-    } else if (!fbm_modinv_finish(st, jp.n30, x1)) {
-      err |= FBM_ERR_NOT_INVERTIBLE;
-    }
+    r[k] = (uint32_t)lo;
+    const uint64_t c = (lo >> 32) + hi;
+    lo = c & 0xffffffffull;
+    hi = c >> 32;
   }
-  if (ct_raw < n_ct) {
-    uint4* yo = reinterpret_cast<uint4*>(Y + ct * 32);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) yo[i] = make_uint4(x1[4 * i], x1[4 * i + 1], x1[4 * i + 2], x1[4 * i + 3]);
-    if (err) atomicOr(stats + FBM_STAT_ERRFLAGS, err);
-  }
+  r[63] = (uint32_t)lo;
 }
 
-// stage 2 (Hensel lift): inv = y * (2 - E*y) mod N^2   -> inv [ct][64]
-__global__ void __launch_bounds__(FBM_BLOCK, 1) jl_inv_lift_kernel(uint64_t n_ct, JlParams jp,
-                                                                  const uint32_t* __restrict__ E,
-                                                                  const uint32_t* __restrict__ Y,
-                                                                  uint32_t* __restrict__ inv) {
-  __shared__ uint32_t lds_a[FBM_NL * FBM_BLOCK];
-  const int tid = threadIdx.x;
-  uint32_t* lds = lds_a + tid;
-  const int ls = FBM_BLOCK;
-  const uint64_t ct = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
-  if (ct >= n_ct) return;
-  uint32_t x1[32];
+__device__ __forceinline__ void div_by_n(uint32_t (&D)[64], const JlParams& jp, uint32_t (&q)[32]) {
   {
-    const uint4* yi = reinterpret_cast<const uint4*>(Y + ct * 32);
+    uint32_t dl[32];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint4 v = yi[i];
-      x1[4 * i] = v.x; x1[4 * i + 1] = v.y; x1[4 * i + 2] = v.z; x1[4 * i + 3] = v.w;
-    }
-  }
-  // --- Hensel: inv = y * (2 - e*y) mod N^2 ------------------------------------------------
-  //   s0: a = y,  b = e  -> e*y/R      s1: a = R^2, b -> z = e*y      (w = 2 - z mod M)
-  //   s2: a = y,  b = w  -> y*w/R      s3: a = R^2, b -> y*w = inv
-  uint32_t acc[FBM_NL];
-  {
-    uint32_t e32[64];
-    load_row64(E + ct * 64, e32);
-    to28<64, FBM_NL>(e32, acc);
-  }
-  {
-    uint32_t x64[64];
-#pragma unroll
-    for (int i = 0; i < 64; ++i) x64[i] = i < 32 ? x1[i] : 0u;
-    uint32_t y[FBM_NL];
-    to28<64, FBM_NL>(x64, y);
-    lds_store_col(lds, ls, y);
-  }
-#pragma unroll 1
-  for (int st = 0; st < 4; ++st) {
-    mont_mul(acc, lds, ls, jp.mc);
-    if (st == 0 || st == 2) {
-      lds_store_uniform<FBM_NL>(lds, ls, jp.mc.R2);
-    } else if (st == 1) {
-      mont_csub(acc, jp.mc.M);  // z < M
-      int32_t br = 0;           // w = 2 - z mod M   (M > 2)
-#pragma unroll
-      for (int k = 0; k < FBM_NL; ++k) {
-        const int32_t v = (int32_t)(k == 0 ? 2u : 0u) - (int32_t)acc[k] + br;
-        acc[k] = (uint32_t)v & FBM_LMASK;
-        br = v >> FBM_LB;
-      }
-      if (br) {
-        uint32_t c = 0;
-#pragma unroll
-        for (int k = 0; k < FBM_NL; ++k) {
-          const uint32_t v = acc[k] + jp.mc.M[k] + c;
-          acc[k] = v & FBM_LMASK;
-          c = v >> FBM_LB;
-        }
-      }
-      uint32_t x64[64];
-#pragma unroll
-      for (int i = 0; i < 64; ++i) x64[i] = i < 32 ? x1[i] : 0u;
-      uint32_t y[FBM_NL];
-      to28<64, FBM_NL>(x64, y);
-      lds_store_col(lds, ls, y);
-    }
-  }
-  mont_csub(acc, jp.mc.M);
-  uint32_t w[64];
-  from28<FBM_NL, 64>(acc, w);
-  store_row64(inv + ct * 64, w);
-}
-
-// ------------------------------------------------------------------------------------
-// v = X * inv (plain) ; x = floor((v-1)/N)   (x < N, 32 words)
-// ------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(FBM_BLOCK, 1) jl_fin_kernel(uint64_t n_ct, JlParams jp,
-                                                             const uint32_t* __restrict__ X,
-                                                             const uint32_t* __restrict__ inv,
-                                                             uint32_t* __restrict__ xout) {
-  __shared__ uint32_t lds_a[FBM_NL * FBM_BLOCK];
-  const int tid = threadIdx.x;
-  const uint64_t ct = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
-  if (ct >= n_ct) return;
-  uint32_t* lds = lds_a + tid;
-  {
-    uint32_t xv[FBM_NL];
-    col_load(X + (ct >> 8) * (FBM_NL * 256) + (ct & 255), xv);
-    lds_store_col(lds, FBM_BLOCK, xv);
-  }
-  uint32_t acc[FBM_NL];
-  {
-    uint32_t i32[64];
-    load_row64(inv + ct * 64, i32);
-    to28<64, FBM_NL>(i32, acc);
-  }
-  mont_mul(acc, lds, FBM_BLOCK, jp.mc);  // (prod*R) * inv * R^-1 = prod * inv mod M
-  mont_csub(acc, jp.mc.M);
-  uint32_t D[64];
-  from28<FBM_NL, 64>(acc, D);
-  {  // D = v - 1  (v >= 1 for any unit)
-    uint32_t br = 1;
-#pragma unroll
-    for (int i = 0; i < 64; ++i) {
-      const uint64_t d = (uint64_t)D[i] - br;
-      D[i] = (uint32_t)d;
-      br = (uint32_t)(d >> 63);
-    }
-  }
-  // (v-1)/N is exact whenever the keys are consistent (v = 1 + N x mod N^2): x = (v-1) N^-1
-  // mod 2^1024, accepted iff x N == v - 1.  Otherwise (a wrong server key: the reference
-  // still returns floor((v-1)/N) mod N) fall back to binary long division.
-  {
-    uint32_t x[32];
-#pragma unroll
-    for (int i = 0; i < 32; ++i) x[i] = 0u;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      uint64_t c = 0;
-#pragma unroll
-      for (int j = 0; i + j < 32; ++j) {
-        const uint64_t v = (uint64_t)D[i] * jp.Ninv32[j] + x[i + j] + c;
-        x[i + j] = (uint32_t)v;
-        c = v >> 32;
-      }
-    }
-    uint32_t diff = 0;  // x*N (2048 bits) vs D
+    for (int i = 0; i < 32; ++i) dl[i] = D[i];
+    mullo1024(dl, jp.Ninv32, q);
     uint32_t pr[64];
-#pragma unroll
-    for (int i = 0; i < 64; ++i) pr[i] = 0u;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      uint64_t c = 0;
-#pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        const uint64_t v = (uint64_t)x[i] * jp.N32[j] + pr[i + j] + c;
-        pr[i + j] = (uint32_t)v;
-        c = v >> 32;
-      }
-      pr[i + 32] = (uint32_t)c;
-    }
+    mul1024(q, jp.N32, pr);
+    uint32_t diff = 0;
 #pragma unroll
     for (int i = 0; i < 64; ++i) diff |= pr[i] ^ D[i];
-    if (diff == 0) {
-      uint4* o = reinterpret_cast<uint4*>(xout + ct * 32);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = make_uint4(x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]);
-      return;
-    }
+    if (diff == 0) return;
   }
-  // binary long division by N; quotient q (< N), remainder r
-  uint32_t q[32], r[33];
+  uint32_t r[33];
 #pragma unroll
   for (int i = 0; i < 32; ++i) q[i] = 0u;
 #pragma unroll
@@ -1246,9 +940,257 @@ __global__ void __launch_bounds__(FBM_BLOCK, 1) jl_fin_kernel(uint64_t n_ct, JlP
       q[0] |= 1u;
     }
   }
-  uint4* o = reinterpret_cast<uint4*>(xout + ct * 32);
+}
+
+// ------------------------------------------------------------------------------------
+// aggregate (_jls.py:353-374 product, :547-558 decrypt), one lane per ciphertext:
+//   v = prod_u c_u * F mod N^2,  x = (v - 1) div N   -> xout [ct][32]
+// Montgomery products mod M = N^2 on the assembly engine (fbm_mont_asm.hpp), a = the running
+// product in LDS, b = the next operand staged as a 28-bit column in X's slot:
+//   a = R^(P+1) mod M (uniform, cst[FBM_CST_RK]),  b = c_0   -> c_0 R^P
+//   b = c_u, u = 1 .. P-1, then b = F                        -> each drops one R -> v (lazy)
+// P + 1 products, no Montgomery-form round trips; any c_u < 2^2048 qualifies (a b < R M).
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(FBM_BLOCK, 2) jl_prod_kernel(const uint32_t* __restrict__ cts, int n_parties,
+                                                              uint64_t n_ct, const uint32_t* __restrict__ cst,
+                                                              JlParams jp, const uint32_t* __restrict__ factor,
+                                                              uint32_t* __restrict__ X, uint32_t* __restrict__ xout) {
+  __shared__ uint32_t lds_a[(FBM_NL + 1) * FBM_BLOCK];
+  const int tid = threadIdx.x;
+  uint32_t* lds = lds_a + tid;
+  const uint32_t aoff = lds_addr(lds);
+  const uint32_t* M = cst + FBM_CST_M;
+  const uint64_t ct_raw = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
+  const bool valid = ct_raw < n_ct;  // no early return: X is padded to whole blocks
+  const uint64_t ct = valid ? ct_raw : n_ct - 1;
+  const uint32_t xoff = (uint32_t)(((ct_raw >> 8) * (FBM_NL * 256) + (ct_raw & 255)) * 4);
+  lds_store_uniform<FBM_NL>(lds, FBM_BLOCK, cst + FBM_CST_RK);
+#pragma unroll 1
+  for (int u = 0; u <= n_parties; ++u) {
+    {
+      const uint32_t* row = u < n_parties ? cts + ((uint64_t)u * n_ct + ct) * 64 : factor + ct * 64;
+      uint32_t c32[64], c28[FBM_NL];
+      load_row64(row, c32);
+      to28<64, FBM_NL>(c32, c28);
+      col_store(X + xoff / 4, c28);
+    }
+    fbm_mm_glb(aoff, X, xoff, M, jp.mc.mp);
+  }
+  uint32_t D[64];
+  {
+    uint32_t v[FBM_NL];
+    lds_load_col(lds, FBM_BLOCK, v);
+    mont_csub(v, jp.mc.M);
+    from28<FBM_NL, 64>(v, D);
+  }
+  uint32_t br = 1;  // D = v - 1
 #pragma unroll
-  for (int i = 0; i < 8; ++i) o[i] = make_uint4(q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]);
+  for (int i = 0; i < 64; ++i) {
+    const uint64_t d = (uint64_t)D[i] - br;
+    D[i] = (uint32_t)d;
+    br = (uint32_t)(d >> 63);
+  }
+  uint32_t x[32];
+  div_by_n(D, jp, x);
+  if (valid) {
+    uint4* o = reinterpret_cast<uint4*>(xout + ct * 32);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = make_uint4(x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// inverse mod N^2 from N-adic digits: y = e0^-1 mod N (Bernstein-Yang divsteps), then
+// one N-adic lift step (jl_lift_kernel).  e = H^|sk0| mod N^2 (the factor) or H (a
+// negative-key encrypt).
+// ------------------------------------------------------------------------------------
+template <int W>
+__device__ __forceinline__ void shr1(uint32_t (&a)[W], uint32_t top) {
+#pragma unroll
+  for (int i = 0; i < W - 1; ++i) a[i] = (a[i] >> 1) | (a[i + 1] << 31);
+  a[W - 1] = (a[W - 1] >> 1) | (top << 31);
+}
+template <int W>
+__device__ __forceinline__ uint32_t add_into(uint32_t (&a)[W], const uint32_t* b) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const uint64_t s = (uint64_t)a[i] + b[i] + c;
+    a[i] = (uint32_t)s;
+    c = (uint32_t)(s >> 32);
+  }
+  return c;
+}
+template <int W>
+__device__ __forceinline__ uint32_t sub_from(uint32_t (&a)[W], const uint32_t (&b)[W]) {
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const uint64_t d = (uint64_t)a[i] - b[i] - br;
+    a[i] = (uint32_t)d;
+    br = (uint32_t)(d >> 63);
+  }
+  return br;
+}
+
+// y = e0^-1 mod N -> Y [ct][32], e0 = words 0..31 of src row ct (stride src_stride words),
+// by Bernstein-Yang divsteps (fbm_safegcd.hpp): branch-free batches of 30 divsteps; the loop
+// leaves when every lane of the wave is done (a finished lane is a fixed point of further
+// batches).
+__global__ void __launch_bounds__(FBM_BLOCK) jl_inv_modn_kernel(uint64_t n_ct, JlParams jp,
+                                                               const uint32_t* __restrict__ src, int src_stride,
+                                                               uint32_t* __restrict__ Y,
+                                                               uint32_t* __restrict__ stats) {
+  const uint64_t ct_raw = (uint64_t)blockIdx.x * FBM_BLOCK + threadIdx.x;
+  const uint64_t ct = ct_raw < n_ct ? ct_raw : n_ct - 1;  // all lanes take part in the vote
+  uint32_t err = 0;
+  uint32_t x1[32];
+  {
+    uint32_t u[32];
+    const uint4* yi = reinterpret_cast<const uint4*>(src + ct * (uint64_t)src_stride);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint4 v = yi[i];
+      u[4 * i] = v.x; u[4 * i + 1] = v.y; u[4 * i + 2] = v.z; u[4 * i + 3] = v.w;
+    }
+    FbmInvState st;
+    fbm_modinv_init(st, u, jp.n30);
+    for (int b = 0; b < FBM_INV_MAX_BATCHES; ++b) {
+      if (__all(fbm_s30_is_zero(st.g))) break;
+      fbm_modinv_batch(st, jp.n30);
+    }
+    if (!fbm_s30_is_zero(st.g)) {
+      err |= FBM_ERR_ITER_CAP;
+    } else if (!fbm_modinv_finish(st, jp.n30, x1)) {
+      err |= FBM_ERR_NOT_INVERTIBLE;
+    }
+  }
+  if (ct_raw < n_ct) {
+    uint4* yo = reinterpret_cast<uint4*>(Y + ct * 32);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) yo[i] = make_uint4(x1[4 * i], x1[4 * i + 1], x1[4 * i + 2], x1[4 * i + 3]);
+    if (err) atomicOr(stats + FBM_STAT_ERRFLAGS, err);
+  }
+}
+
+// E^-1 mod N^2 from E = e0 + e1 N (digits < N, Ed [ct][64] = e0 | e1) and y = e0^-1 mod N:
+// e0 y = 1 + a N with a < N, so E y = 1 + N (a + e1 y) mod N^2 and
+//   E^-1 = y (1 - N (a + e1 y)) = y + N v,   v = -y (a + e1 y) mod N.
+// a = (e0 y - 1) N^-1 mod 2^1024 from the low halves alone (a < N); v by three Montgomery
+// products mod N (37 limbs, R_N = 2^1036): Y' = y R_N, u = e1 y, w = (a + u) y.
+// With nude (a negative-key encrypt: c = (N pt + 1) H^key = nude * (H^|key|)^-1, nude = the
+// digits (1, p) of jl_nude_kernel): c = y + N ((v + p y) mod N), one more product.
+// out [ct][64] canonical.  out may alias Ed: each lane reads its row before writing it.
+__global__ void __launch_bounds__(FBM_BLOCK, 2) jl_lift_kernel(uint64_t n_ct, JlParams jp,
+                                                              const uint32_t* __restrict__ cst, const uint32_t* Ed,
+                                                              const uint32_t* __restrict__ Y,
+                                                              const uint32_t* __restrict__ nude, uint32_t* out) {
+  const MontCtxN& mn = *reinterpret_cast<const MontCtxN*>(cst + FBM_CST_MN);
+  __shared__ uint32_t lds_a[FBM_NLN * FBM_BLOCK];
+  const int tid = threadIdx.x;
+  uint32_t* lds = lds_a + tid;
+  const int ls = FBM_BLOCK;
+  const uint64_t ct = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
+  if (ct >= n_ct) return;
+  uint32_t y[32], a[32], acc[FBM_NLN];
+  {
+    uint32_t e0[32];
+    const uint4* ei = reinterpret_cast<const uint4*>(Ed + ct * 64);
+    const uint4* yi = reinterpret_cast<const uint4*>(Y + ct * 32);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint4 v = ei[i], w = yi[i];
+      e0[4 * i] = v.x; e0[4 * i + 1] = v.y; e0[4 * i + 2] = v.z; e0[4 * i + 3] = v.w;
+      y[4 * i] = w.x; y[4 * i + 1] = w.y; y[4 * i + 2] = w.z; y[4 * i + 3] = w.w;
+    }
+    uint32_t p[32];
+    mullo1024(e0, y, p);
+    uint32_t br = 1;  // p = e0 y - 1 (mod 2^1024)
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const uint64_t d = (uint64_t)p[i] - br;
+      p[i] = (uint32_t)d;
+      br = (uint32_t)(d >> 63);
+    }
+    mullo1024(p, jp.Ninv32, a);
+  }
+  {
+    uint32_t y28[FBM_NLN];
+    to28<32, FBM_NLN>(y, y28);
+    lds_store_col(lds, ls, y28);
+  }
+#pragma unroll
+  for (int k = 0; k < FBM_NLN; ++k) acc[k] = mn.R2[k];
+  mont_mul(acc, lds, ls, mn);  // Y' = y R_N (lazy < 2N)
+  lds_store_col(lds, ls, acc);
+  {
+    uint32_t e1[32];
+    const uint4* ei = reinterpret_cast<const uint4*>(Ed + ct * 64 + 32);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint4 v = ei[i];
+      e1[4 * i] = v.x; e1[4 * i + 1] = v.y; e1[4 * i + 2] = v.z; e1[4 * i + 3] = v.w;
+    }
+    to28<32, FBM_NLN>(e1, acc);
+  }
+  mont_mul(acc, lds, ls, mn);  // u = e1 y (lazy < 2N)
+  {
+    uint32_t a28[FBM_NLN];
+    to28<32, FBM_NLN>(a, a28);
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < FBM_NLN; ++k) {  // a + u < 3N
+      const uint32_t v = acc[k] + a28[k] + c;
+      acc[k] = v & FBM_LMASK;
+      c = v >> FBM_LB;
+    }
+  }
+  mont_mul(acc, lds, ls, mn);  // w = (a + u) y (lazy < 2N)
+  mont_csub(acc, mn.M);
+  {  // v = N - w, then N -> 0
+    int32_t br = 0;
+#pragma unroll
+    for (int k = 0; k < FBM_NLN; ++k) {
+      const int32_t d = (int32_t)mn.M[k] - (int32_t)acc[k] + br;
+      acc[k] = (uint32_t)d & FBM_LMASK;
+      br = d >> FBM_LB;
+    }
+    mont_csub(acc, mn.M);
+  }
+  if (nude) {  // v <- (v + p y) mod N; p < 2^1036 = R_N, Y' < 2N: p Y' R_N^-1 < 3N
+    uint32_t p28[FBM_NLN];
+    const uint32_t* nb = nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255);
+#pragma unroll
+    for (int k = 0; k < FBM_NLN; ++k) p28[k] = nb[(FBM_NLN + k) * 256];
+    mont_mul(p28, lds, ls, mn);  // p y
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < FBM_NLN; ++k) {  // < 4N
+      const uint32_t t = acc[k] + p28[k] + c;
+      acc[k] = t & FBM_LMASK;
+      c = t >> FBM_LB;
+    }
+    uint32_t n[FBM_NLN];
+#pragma unroll
+    for (int k = 0; k < FBM_NLN; ++k) n[k] = mn.M[k];
+    csub28(acc, n);
+    csub28(acc, n);
+    csub28(acc, n);
+  }
+  uint32_t v[32];
+  from28<FBM_NLN, 32>(acc, v);
+  uint4* o = reinterpret_cast<uint4*>(out + ct * 64);
+  uint32_t f[64];  // y + N v < N^2
+  mul1024(v, jp.N32, f);
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    const uint64_t t = (uint64_t)f[i] + (i < 32 ? y[i] : 0u) + c;
+    f[i] = (uint32_t)t;
+    c = (uint32_t)(t >> 32);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) o[i] = make_uint4(f[4 * i], f[4 * i + 1], f[4 * i + 2], f[4 * i + 3]);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1355,9 +1297,11 @@ int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stat
 // memory for the exp kernel, which indexes it dynamically; M and R^2 for the scalar
 // loads of the assembly product; broadcast columns of 1 and R^2 (limb k at word k*256,
 // read by every lane at offset 0).
-__global__ void jl_setup_kernel(JlSched sc, MontCtx mc, NadicCtx na, QuadCtx qa, uint32_t* __restrict__ ops,
-                                uint32_t* __restrict__ cst) {
+__global__ void jl_setup_kernel(JlSched sc, MontCtx mc, MontCtxN mn, NadicCtx na, QuadCtx qa,
+                                uint32_t* __restrict__ ops, uint32_t* __restrict__ cst) {
   const int t = threadIdx.x;
+  if (t < 128)  // MontCtxN image: M[37] R2[37] mp pad
+    cst[FBM_CST_MN + t] = t < FBM_NLN ? mn.M[t] : t < 2 * FBM_NLN ? mn.R2[t - FBM_NLN] : t == 2 * FBM_NLN ? mn.mp : 0u;
   for (int i = t; i < sc.n_ops; i += blockDim.x) ops[i] = sc.op[i];
   if (t < 128) {
     cst[FBM_CST_M + t] = t < FBM_NL ? mc.M[t] : 0u;
@@ -1378,12 +1322,11 @@ __global__ void jl_setup_kernel(JlSched sc, MontCtx mc, NadicCtx na, QuadCtx qa,
   for (int i = t; i < FBM_NL * 256; i += blockDim.x) {
     const int k = i >> 8, l = i & 255;
     cst[FBM_CST_ONE + i] = (l == 0 && k == 0) ? 1u : 0u;
-    cst[FBM_CST_R2COL + i] = l == 0 ? mc.R2[k] : 0u;
   }
 }
 
 int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32_t* cst, hipStream_t s) {
-  hipLaunchKernelGGL(jl_setup_kernel, dim3(1), dim3(256), 0, s, sc, jp.mc, jp.na, jp.qa, ops, cst);
+  hipLaunchKernelGGL(jl_setup_kernel, dim3(1), dim3(256), 0, s, sc, jp.mc, jp.mn, jp.na, jp.qa, ops, cst);
   return check_launch("jl_setup_kernel");
 }
 
@@ -1454,24 +1397,31 @@ int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const Jl
 }
 
 int launch_jl_prod(const uint32_t* cts, int n_parties, uint64_t n_ct, const JlParams& jp, const uint32_t* cst,
-                   uint32_t* X, hipStream_t s) {
+                   const uint32_t* factor, uint32_t* X, uint32_t* xout, hipStream_t s) {
   if (n_ct == 0) return FBM_OK;
-  hipLaunchKernelGGL(jl_prod_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, cts, n_parties, n_ct, cst,
-                     jp.mc.mp, X);
+  hipLaunchKernelGGL(jl_prod_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, cts, n_parties, n_ct, cst, jp,
+                     factor, X, xout);
   return check_launch("jl_prod_kernel");
 }
 
-int launch_jl_inv(uint64_t n_ct, const JlParams& jp, const uint32_t* E, uint32_t* Y, uint32_t* inv, uint32_t* stats,
-                  hipStream_t s) {
+__global__ void jl_rk_kernel(JlRk rk, uint32_t* __restrict__ cst) {
+  const int t = threadIdx.x;
+  if (t < 128) cst[FBM_CST_RK + t] = t < FBM_NL ? rk.w[t] : 0u;
+}
+
+int launch_jl_rk(const JlRk& rk, uint32_t* cst, hipStream_t s) {
+  hipLaunchKernelGGL(jl_rk_kernel, dim3(1), dim3(128), 0, s, rk, cst);
+  return check_launch("jl_rk_kernel");
+}
+
+int launch_jl_inv(uint64_t n_ct, const JlParams& jp, const uint32_t* cst, const uint32_t* Ed, uint32_t* Y,
+                  const uint32_t* nude, uint32_t* out, uint32_t* stats, hipStream_t s) {
   if (n_ct == 0) return FBM_OK;
-  hipLaunchKernelGGL(jl_emodn_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, E, Y);
-  int rc = check_launch("jl_emodn_kernel");
+  hipLaunchKernelGGL(jl_inv_modn_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, Ed, 64, Y, stats);
+  int rc = check_launch("jl_inv_modn_kernel");
   if (rc) return rc;
-  hipLaunchKernelGGL(jl_inv_modn_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, Y, stats);
-  rc = check_launch("jl_inv_modn_kernel");
-  if (rc) return rc;
-  hipLaunchKernelGGL(jl_inv_lift_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, E, Y, inv);
-  return check_launch("jl_inv_lift_kernel");
+  hipLaunchKernelGGL(jl_lift_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, cst, Ed, Y, nude, out);
+  return check_launch("jl_lift_kernel");
 }
 
 // host test hook (fbm_test_fdh_gcd, include/fbm_secagg.h): the device's one-digest gcd test
@@ -1482,23 +1432,6 @@ int host_gcd_is_one_r8(const uint32_t* r8, const uint32_t* n32, uint32_t* err) {
   const bool ok = gcd_is_one_r8(r, n32, e);
   *err = e;
   return ok ? 1 : 0;
-}
-
-int launch_jl_nadic_split(uint64_t n_ct, const JlParams& jp, const uint32_t* E, uint32_t* Y, uint32_t* out,
-                          hipStream_t s) {
-  if (n_ct == 0) return FBM_OK;
-  hipLaunchKernelGGL(jl_emodn_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, E, Y);
-  int rc = check_launch("jl_emodn_kernel");
-  if (rc) return rc;
-  hipLaunchKernelGGL(jl_split_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, E, Y, out);
-  return check_launch("jl_split_kernel");
-}
-
-int launch_jl_fin(uint64_t n_ct, const JlParams& jp, const uint32_t* X, const uint32_t* inv, uint32_t* xout,
-                  hipStream_t s) {
-  if (n_ct == 0) return FBM_OK;
-  hipLaunchKernelGGL(jl_fin_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, n_ct, jp, X, inv, xout);
-  return check_launch("jl_fin_kernel");
 }
 
 int launch_jl_decode(const uint32_t* xs, int es, int cr, uint64_t n_out, uint64_t total_weight, double neg_c,
