@@ -449,15 +449,15 @@ def _key_limbs(key: int) -> Tuple[np.ndarray, int]:
 
 JL_MAX_CT = 14_000_000  # include/fbm_secagg.h FBM_JL_MAX_CT: ciphertexts per library call
 
-_ENGINES = {"auto": 0, "single": 1, "quad": 4}
+_ENGINES = {"auto": 0, "single": 1, "triple": 3, "quad": 4}
 
 
 class jl_engine:
     """Exponentiation engine for the JL calls issued inside (process-wide policy,
     fbm_jl_set_engine): "auto" (the library's choice by launch size), "single" (one lane per
-    ciphertext: several concurrent launches that fill the chip together) or "quad" (four
-    lanes per ciphertext: latency of a launch below the chip's lane count).  Results are
-    bit-identical under every engine.
+    ciphertext: several concurrent launches that fill the chip together), "quad" / "triple"
+    (four / three lanes per ciphertext: latency of a launch below the chip's lane count).
+    Results are bit-identical under every engine.
 
         with D.jl_engine("single"):
             ...  # the parties' concurrent encrypts
@@ -479,7 +479,7 @@ class jl_engine:
 
 def jl_engine_for(n_ct: int) -> str:
     """The engine a launch of n_ct ciphertexts takes under the current policy."""
-    return "quad" if N.load().fbm_jl_engine_for(int(n_ct)) == 4 else "single"
+    return {1: "single", 3: "triple", 4: "quad"}[N.load().fbm_jl_engine_for(int(n_ct))]
 
 
 def jl_chunk_ct() -> int:

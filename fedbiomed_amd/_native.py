@@ -49,6 +49,7 @@ SIGNATURES = {
     "fbm_jl_window": (c_int, []),
     "fbm_jl_mads": (c_int, [c_int]),
     "fbm_jl_quad_mads": (c_int, [c_int]),
+    "fbm_jl_triple_mads": (c_int, [c_int]),
     "fbm_jl_set_engine": (c_int, [c_int]),
     "fbm_jl_engine_for": (c_int, [c_u64]),
     "fbm_last_error": (ctypes.c_char_p, []),

@@ -14,6 +14,7 @@
 #include "fbm_internal.hpp"
 #include "fbm_nadic_asm.hpp"
 #include "fbm_quad_asm.hpp"
+#include "fbm_tri_asm.hpp"
 #include "fbm_safegcd.hpp"
 
 namespace fbm {
@@ -498,16 +499,17 @@ int fbm_abi_version(void) { return FBM_ABI_VERSION; }
 int fbm_jl_window(void) { return FBM_WIN; }
 int fbm_jl_mads(int square) { return square ? FBM_NA_MADS_SQR : FBM_NA_MADS_MUL; }
 int fbm_jl_quad_mads(int square) { return 4 * (square ? FBM_QA_MADS_SQR : FBM_QA_MADS_MUL); }
+int fbm_jl_triple_mads(int square) { return 3 * (square ? FBM_TA_MADS_SQR : FBM_TA_MADS_MUL); }
 
 int fbm_jl_set_engine(int mode) {
-  if (mode != FBM_ENGINE_AUTO && mode != FBM_ENGINE_SINGLE && mode != FBM_ENGINE_QUAD) {
-    set_error("fbm_jl_set_engine: mode must be 0 (auto), 1 (one lane per ciphertext) or 4 (four lanes)");
+  if (mode != FBM_ENGINE_AUTO && mode != FBM_ENGINE_SINGLE && mode != FBM_ENGINE_QUAD && mode != FBM_ENGINE_TRIPLE) {
+    set_error("fbm_jl_set_engine: mode must be 0 (auto), 1 (one lane per ciphertext), 3 (three lanes) or 4 (four)");
     return FBM_E_ARG;
   }
   return jl_engine_set(mode);
 }
 
-int fbm_jl_engine_for(uint64_t n_ct) { return jl_use_quad(n_ct) ? FBM_ENGINE_QUAD : FBM_ENGINE_SINGLE; }
+int fbm_jl_engine_for(uint64_t n_ct) { return jl_engine_for(n_ct); }
 
 const char* fbm_last_error(void) { return g_err; }
 

@@ -75,11 +75,11 @@ int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t 
 #define FBM_CST_NK (FBM_CST_RK + 128)
 #define FBM_CST_R2NA (FBM_CST_NK + 128)
 #define FBM_CST_R3NA (FBM_CST_R2NA + 128)  // R^3 mod N^2 (digits): the high part of a wide h
-// quad engine (fbm_quad_asm.hpp, 29-bit limbs, R = 2^1044): K'_i (36 words), the lanes' N
-// limbs (limb 9 l + r at word 4 r + l), R^2 and R^3 mod N^2 as digit pairs (72 limbs each)
+// lane-group engines (fbm_quad_asm.hpp / fbm_tri_asm.hpp, 29-bit limbs, R = 2^1044): K'_i
+// (36 words), N's limbs (limb k at word k), R^2 and R^3 mod N^2 as digit pairs (72 limbs each)
 #define FBM_CST_QK (FBM_CST_R3NA + 128)
-#define FBM_CST_QN (FBM_CST_QK + 64)
-#define FBM_CST_QR2 (FBM_CST_QN + 64)
+#define FBM_CST_QNP (FBM_CST_QK + 64)
+#define FBM_CST_QR2 (FBM_CST_QNP + 64)
 #define FBM_CST_QR3 (FBM_CST_QR2 + 128)
 // the MontCtxN image (M, R^2 mod N, mp: 76 words) for the mod-N products of jl_emodn /
 // jl_lift, read through device memory (a laundered pointer into the by-value JlParams
@@ -105,7 +105,7 @@ struct NadicCtx {
   uint32_t pad[4];
 };
 
-// quad-engine constants (tools/gen_quad_asm.py): 29-bit limbs, R = 2^1044
+// lane-group engine constants (tools/gen_quad_asm.py): 29-bit limbs, R = 2^1044
 struct QuadCtx {
   uint32_t kp[36];   // K'_i = 2^29 - 1 + K_i, K = (1 - R) mod N
   uint32_t n[36];    // N
@@ -176,10 +176,11 @@ uint64_t jl_table_slots();
 // exponentiation engine policy (fbm_jl_set_engine) and the table bytes both engines fit in
 #define FBM_ENGINE_AUTO 0
 #define FBM_ENGINE_SINGLE 1
+#define FBM_ENGINE_TRIPLE 3
 #define FBM_ENGINE_QUAD 4
 int jl_engine_policy();
 int jl_engine_set(int mode);
-bool jl_use_quad(uint64_t n_ct);
+int jl_engine_for(uint64_t n_ct);
 uint64_t jl_table_bytes(uint64_t n_ct);
 // compute units of the calling thread's current device (cached per device)
 int device_num_cu();

@@ -28,6 +28,7 @@
 #include "fbm_mont_asm.hpp"
 #include "fbm_nadic_asm.hpp"
 #include "fbm_quad_asm.hpp"
+#include "fbm_tri_asm.hpp"
 #include "fbm_safegcd.hpp"
 
 namespace fbm {
@@ -612,22 +613,21 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
 }
 
 // ------------------------------------------------------------------------------------
-// The same exponentiation on the QUAD engine (fbm_quad_asm.hpp, tools/gen_quad_asm.py):
-// four lanes per ciphertext, 29-bit limbs (36 per digit, R = 2^1044), lane l owning limbs
-// 9 l .. 9 l + 8 of both digits, for launches that hold fewer ciphertexts than the chip has
-// resident lanes (one party's 1M elements, the aggregate of a 1/8 stripe): the 4x lanes fill
-// the chip and a ciphertext's exponentiation takes about a quarter of a lane's time.  Same
-// residues at every step (the Montgomery form uses R = 2^1044 instead of 2^1036), the same
-// canonical results (tests/test_quad_asm.py; the -m gpu tests through both engines).
-//   workgroup: 256 lanes = 64 ciphertexts; LDS column of ciphertext c: limb k of digit d at
-//   word (36 d + k) * 72 + c (2 spare rows: the last row's prefetch);  per-lane tables in the
-//   QUAD layout: entry e, limb row j (b0: j = r, b1: j = 9 + r) at word
-//   (slot * FBM_TENTRIES + e) * 4608 + j * 256 + tid.
+// The same exponentiation on the lane-GROUP engines (tools/gen_quad_asm.py): G lanes per
+// ciphertext, 29-bit limbs (36 per digit, R = 2^1044), lane l owning limbs M l .. M l + M - 1
+// of both digits (M = 36 / G), for launches that hold fewer ciphertexts than the chip has
+// resident lanes (one party's 1M elements, the aggregate of a 1/8 stripe): the G x lanes fill
+// the chip and a ciphertext's exponentiation takes a fraction of a lane's time.  Same residues
+// at every step (the Montgomery form uses R = 2^1044 instead of 2^1036), the same canonical
+// results (tests/test_quad_asm.py; the -m gpu tests through every engine).
+//   QUAD   (G = 4, fbm_quad_asm.hpp): 16 ciphertexts per wave, DPP quad_perm exchanges.
+//   TRIPLE (G = 3, fbm_tri_asm.hpp): 21 ciphertexts per wave (lanes 0..62) + a dummy lane 63
+//          with an all-zero column (the wave-shift neighbour of lane 62), ds_bpermute broadcasts.
+//   workgroup: 256 lanes = 4 waves; LDS column of ciphertext c: limb k of digit d at word
+//   (36 d + k) * ROWW + c (2 spare rows: the last row's prefetch); per-lane tables: entry e,
+//   limb row j (b0: j = r, b1: j = M + r) at word (slot * FBM_TENTRIES + e) * ENTRY + j * 256 + tid.
 // ------------------------------------------------------------------------------------
 #define FBM_QBLOCK 256
-#define FBM_QCT (FBM_QBLOCK / 4)
-#define FBM_QROWW FBM_QA_ROWW                 // LDS words between limb rows (72)
-#define FBM_QENTRY (2 * FBM_QA_LIMBS * 256)   // words of one quad-layout table entry (4608)
 #define FBM_QMASK ((1u << FBM_QA_LB) - 1u)
 
 // limb k (lb bits at bit lb k) of a little-endian number of `nw` words in global memory
@@ -638,73 +638,131 @@ __device__ __forceinline__ uint32_t glb_limb(const uint32_t* p, int nw, int k, i
   return (uint32_t)(((hi << 32) | lo) >> sh) & ((1u << lb) - 1u);
 }
 
+template <int G>
+struct GroupEng;
+template <>
+struct GroupEng<4> {
+  static constexpr int M = FBM_QA_LIMBS, ROWW = FBM_QA_ROWW, CT_WAVE = 16, CT_WG = 64;
+  __device__ static void lane_map(int tid, int& c, int& l, bool& dummy) {
+    c = tid >> 2;
+    l = tid & 3;
+    dummy = false;
+  }
+  __device__ static uint32_t group_mask(uint64_t bal, int tid) { return (uint32_t)((bal >> ((tid & 63) & ~3)) & 0xFull); }
+  __device__ static void mm(uint32_t ac, uint32_t al, const uint32_t* bb, uint32_t boff, const uint32_t* QK, uint32_t np,
+                            const uint32_t (&n)[M], uint32_t e0, uint32_t) {
+    fbm_qa_mm_glb(ac, al, bb, boff, QK, np, n, e0);
+  }
+  __device__ static void sq(uint32_t ac, uint32_t al, const uint32_t* QK, uint32_t np, const uint32_t (&n)[M],
+                            uint32_t e0, uint32_t) {
+    fbm_qa_sq_lds(ac, al, QK, np, n, e0);
+  }
+};
+template <>
+struct GroupEng<3> {
+  static constexpr int M = FBM_TA_LIMBS, ROWW = FBM_TA_ROWW, CT_WAVE = 21, CT_WG = 84;
+  __device__ static void lane_map(int tid, int& c, int& l, bool& dummy) {
+    const int w = tid >> 6, j = tid & 63;
+    dummy = j == 63;
+    c = dummy ? CT_WG : CT_WAVE * w + j / 3;  // the 4 dummy lanes share the zero column CT_WG
+    l = dummy ? 0 : j % 3;
+  }
+  __device__ static uint32_t group_mask(uint64_t bal, int tid) {
+    const int j = tid & 63;
+    return (uint32_t)((bal >> (3 * (j / 3))) & 0x7ull);
+  }
+  __device__ static void mm(uint32_t ac, uint32_t al, const uint32_t* bb, uint32_t boff, const uint32_t* QK, uint32_t np,
+                            const uint32_t (&n)[M], uint32_t e0, uint32_t bp) {
+    fbm_ta_mm_glb(ac, al, bb, boff, QK, np, n, e0, bp);
+  }
+  __device__ static void sq(uint32_t ac, uint32_t al, const uint32_t* QK, uint32_t np, const uint32_t (&n)[M],
+                            uint32_t e0, uint32_t bp) {
+    fbm_ta_sq_lds(ac, al, QK, np, n, e0, bp);
+  }
+};
+
 // the lane's slice of a digit pair held as 72 uniform 29-bit limbs (R^2, R^3 digits) -> LDS
+template <int M, int ROWW>
 __device__ __forceinline__ void qa_lds_store_uniform(uint32_t* col, int l, const uint32_t* u) {
   u = launder_s(u);
 #pragma unroll
   for (int d = 0; d < 2; ++d)
 #pragma unroll
-    for (int r = 0; r < FBM_QA_LIMBS; ++r) {
-      const int k = FBM_QA_LIMBS * l + r;
-      col[(d * FBM_QA_D1 + k) * FBM_QROWW] = u[d * FBM_QA_L + k];
+    for (int r = 0; r < M; ++r) {
+      const int k = M * l + r;
+      col[(d * FBM_QA_D1 + k) * ROWW] = u[d * FBM_QA_L + k];
     }
 }
-// lane slice LDS <-> quad-layout table entry (p = entry base + tid)
+// lane slice LDS <-> table entry (p = entry base + tid)
+template <int M, int ROWW>
 __device__ __forceinline__ void qa_lds_to_tbl(const uint32_t* col, int l, uint32_t* p) {
-  uint32_t v[2 * FBM_QA_LIMBS];
+  uint32_t v[2 * M];
 #pragma unroll
   for (int d = 0; d < 2; ++d)
 #pragma unroll
-    for (int r = 0; r < FBM_QA_LIMBS; ++r)
-      v[d * FBM_QA_LIMBS + r] = col[(d * FBM_QA_D1 + FBM_QA_LIMBS * l + r) * FBM_QROWW];
-  col_store<2 * FBM_QA_LIMBS>(p, v);
+    for (int r = 0; r < M; ++r) v[d * M + r] = col[(d * FBM_QA_D1 + M * l + r) * ROWW];
+  col_store<2 * M>(p, v);
 }
+template <int M, int ROWW>
 __device__ __forceinline__ void qa_tbl_to_lds(const uint32_t* p, uint32_t* col, int l) {
-  uint32_t v[2 * FBM_QA_LIMBS];
-  col_load<2 * FBM_QA_LIMBS>(p, v);
+  uint32_t v[2 * M];
+  col_load<2 * M>(p, v);
 #pragma unroll
   for (int d = 0; d < 2; ++d)
 #pragma unroll
-    for (int r = 0; r < FBM_QA_LIMBS; ++r)
-      col[(d * FBM_QA_D1 + FBM_QA_LIMBS * l + r) * FBM_QROWW] = v[d * FBM_QA_LIMBS + r];
+    for (int r = 0; r < M; ++r) col[(d * FBM_QA_D1 + M * l + r) * ROWW] = v[d * M + r];
 }
-// lane 0 of the quad: carry-normalise both digits of the column in place (lazy limbs from
+// lane 0 of the group: carry-normalise both digits of the column in place (lazy limbs from
 // a digit-wise sum; the engine's own outputs need no pass)
+template <int ROWW>
 __device__ __forceinline__ void qa_normalise_column(uint32_t* col) {
 #pragma unroll 1
   for (int d = 0; d < 2; ++d) {
     uint32_t c = 0;
 #pragma unroll 1
     for (int k = 0; k < FBM_QA_L; ++k) {
-      const uint32_t v = col[(d * FBM_QA_D1 + k) * FBM_QROWW] + c;
-      col[(d * FBM_QA_D1 + k) * FBM_QROWW] = v & FBM_QMASK;
+      const uint32_t v = col[(d * FBM_QA_D1 + k) * ROWW] + c;
+      col[(d * FBM_QA_D1 + k) * ROWW] = v & FBM_QMASK;
       c = v >> FBM_QA_LB;
     }
   }
 }
 
-__global__ void __launch_bounds__(FBM_QBLOCK, 3) jl_expq_kernel(const uint32_t* __restrict__ H, uint64_t n_ct,
+template <int G>
+__global__ void __launch_bounds__(FBM_QBLOCK, 3) jl_expg_kernel(const uint32_t* __restrict__ H, uint64_t n_ct,
                                                                uint32_t* __restrict__ cst, uint32_t np29,
                                                                const uint32_t* __restrict__ ops, int n_ops,
                                                                int first, int mode, int key_is_zero,
                                                                const uint32_t* __restrict__ nude,
                                                                uint32_t* __restrict__ table,
                                                                uint32_t* __restrict__ out) {
-  __shared__ uint32_t lds_q[(2 * FBM_QA_D1 + 2) * FBM_QROWW];
+  using E = GroupEng<G>;
+  constexpr int M = E::M, ROWW = E::ROWW;
+  constexpr uint32_t ENTRY = 2 * M * 256;  // words of one table entry
+  __shared__ uint32_t lds_q[(2 * FBM_QA_D1 + 2) * ROWW];
   __shared__ uint32_t chunk_s;
-  const int tid = threadIdx.x, l = tid & 3, c = tid >> 2;
+  const int tid = threadIdx.x;
+  int c, l;
+  bool dummy;
+  E::lane_map(tid, c, l, dummy);
   uint32_t* col = lds_q + c;
   const uint32_t ac = lds_addr(col);
-  const uint32_t al = ac + (uint32_t)(FBM_QA_LIMBS * l * FBM_QA_ROWB);
+  const uint32_t al = ac + (uint32_t)(M * l * ROWW * 4);
   const uint32_t* QK = cst + FBM_CST_QK;
-  uint32_t n[FBM_QA_LIMBS];
+  uint32_t n[M];
 #pragma unroll
-  for (int r = 0; r < FBM_QA_LIMBS; ++r) n[r] = cst[FBM_CST_QN + 4 * r + l];
-  const uint32_t e0 = l == 0 ? 1u : 0u;
+  for (int r = 0; r < M; ++r) n[r] = dummy ? 0u : cst[FBM_CST_QNP + M * l + r];
+  const uint32_t e0 = (l == 0 && !dummy) ? 1u : 0u;
+  // ds_bpermute source of the quotient digits: the group's lane 0 (the dummy: itself)
+  const uint32_t bp = (uint32_t)(4 * (dummy ? (tid & 63) : (tid & 63) - l));
+  if (dummy) {  // the dummy column stays all-zero: its lanes multiply nothing but zeros
+#pragma unroll 1
+    for (int k = 0; k < 2 * FBM_QA_D1 + 2; ++k) col[k * ROWW] = 0u;
+  }
   // byte offset of this lane's word in table entry 0 of this workgroup's slot
-  const uint32_t tb0 = (uint32_t)(((uint64_t)blockIdx.x * FBM_TENTRIES * FBM_QENTRY + tid) * 4);
-  const uint32_t tstride = FBM_QENTRY * 4;
-  const uint32_t n_chunks = (uint32_t)((n_ct + FBM_QCT - 1) / FBM_QCT);
+  const uint32_t tb0 = (uint32_t)(((uint64_t)blockIdx.x * FBM_TENTRIES * ENTRY + tid) * 4);
+  const uint32_t tstride = ENTRY * 4;
+  const uint32_t n_chunks = (uint32_t)((n_ct + E::CT_WG - 1) / E::CT_WG);
 #pragma unroll 1
   for (;;) {
     if (tid == 0) chunk_s = atomicAdd(cst + FBM_CST_CTR, 1u);
@@ -712,95 +770,95 @@ __global__ void __launch_bounds__(FBM_QBLOCK, 3) jl_expq_kernel(const uint32_t* 
     const uint32_t chunk = __builtin_amdgcn_readfirstlane(chunk_s);
     __syncthreads();
     if (chunk >= n_chunks) break;
-    const uint64_t ct_raw = (uint64_t)chunk * FBM_QCT + c;
-    const bool valid = ct_raw < n_ct;
-    const uint64_t ct = valid ? ct_raw : n_ct - 1;
+    const uint64_t ct_raw = (uint64_t)chunk * E::CT_WG + c;
+    const bool valid = !dummy && ct_raw < n_ct;
+    const uint64_t ct = ct_raw < n_ct ? ct_raw : n_ct - 1;
     uint32_t* scratch = table + (tb0 + FBM_TSCRATCH * tstride) / 4;
     bool wide = false;
     {  // h -> the lane's 29-bit limbs of (h mod R, h div R) -> scratch
-      uint32_t h18[2 * FBM_QA_LIMBS];
+      uint32_t h18[2 * M];
       const uint32_t* hr = H + ct * 64;
 #pragma unroll
-      for (int r = 0; r < FBM_QA_LIMBS; ++r) {
-        const int k = FBM_QA_LIMBS * l + r;
+      for (int r = 0; r < M; ++r) {
+        const int k = M * l + r;
         uint32_t lo = 0, hi = 0;
-        if (key_is_zero) {
+        if (dummy) {
+        } else if (key_is_zero) {
           lo = k == 0 ? 1u : 0u;
         } else {
           lo = glb_limb(hr, 64, k, FBM_QA_LB);
           hi = glb_limb(hr, 64, FBM_QA_L + k, FBM_QA_LB);
         }
         h18[r] = lo;
-        h18[FBM_QA_LIMBS + r] = hi;
+        h18[M + r] = hi;
       }
       {
         uint32_t any = 0;
 #pragma unroll
-        for (int r = 0; r < FBM_QA_LIMBS; ++r) any |= h18[FBM_QA_LIMBS + r];
-        // wide is a property of the ciphertext, not of the lane's slice: OR over the quad
-        const uint64_t bal = __ballot(any != 0u);
-        wide = ((bal >> ((tid & 63) & ~3)) & 0xFull) != 0ull;
+        for (int r = 0; r < M; ++r) any |= h18[M + r];
+        // wide is a property of the ciphertext, not of the lane's slice: OR over the group
+        wide = E::group_mask(__ballot(any != 0u), tid) != 0u;
         if (__any(wide)) {  // FDH retries (small moduli): h_hi R^2 = (h_hi, 0) * R^3 R^-1 -> entry 1
-          uint32_t w18[2 * FBM_QA_LIMBS];
+          uint32_t w18[2 * M];
 #pragma unroll
-          for (int r = 0; r < FBM_QA_LIMBS; ++r) {
-            w18[r] = h18[FBM_QA_LIMBS + r];
-            w18[FBM_QA_LIMBS + r] = 0u;
-            h18[FBM_QA_LIMBS + r] = 0u;  // (h_lo, 0) for the main product below
+          for (int r = 0; r < M; ++r) {
+            w18[r] = h18[M + r];
+            w18[M + r] = 0u;
+            h18[M + r] = 0u;  // (h_lo, 0) for the main product below
           }
-          col_store<2 * FBM_QA_LIMBS>(scratch, w18);
-          qa_lds_store_uniform(col, l, cst + FBM_CST_QR3);
-          fbm_qa_mm_glb(ac, al, table, tb0 + FBM_TSCRATCH * tstride, QK, np29, n, e0);
-          qa_lds_to_tbl(col, l, table + (tb0 + tstride) / 4);
+          col_store<2 * M>(scratch, w18);
+          if (!dummy) qa_lds_store_uniform<M, ROWW>(col, l, cst + FBM_CST_QR3);
+          E::mm(ac, al, table, tb0 + FBM_TSCRATCH * tstride, QK, np29, n, e0, bp);
+          qa_lds_to_tbl<M, ROWW>(col, l, table + (tb0 + tstride) / 4);
         }
       }
-      col_store<2 * FBM_QA_LIMBS>(scratch, h18);
+      col_store<2 * M>(scratch, h18);
     }
-    qa_lds_store_uniform(col, l, cst + FBM_CST_QR2);
-    fbm_qa_mm_glb(ac, al, table, tb0 + FBM_TSCRATCH * tstride, QK, np29, n, e0);  // h R | h_lo R
+    if (!dummy) qa_lds_store_uniform<M, ROWW>(col, l, cst + FBM_CST_QR2);
+    E::mm(ac, al, table, tb0 + FBM_TSCRATCH * tstride, QK, np29, n, e0, bp);  // h R | h_lo R
     if (__any(wide)) {  // h R = h_lo R + h_hi R^2 (digit-wise, then carries)
-      uint32_t b18[2 * FBM_QA_LIMBS];
-      col_load<2 * FBM_QA_LIMBS>(table + (tb0 + tstride) / 4, b18);
+      uint32_t b18[2 * M];
+      col_load<2 * M>(table + (tb0 + tstride) / 4, b18);
 #pragma unroll
       for (int d = 0; d < 2; ++d)
 #pragma unroll
-        for (int r = 0; r < FBM_QA_LIMBS; ++r)
-          col[(d * FBM_QA_D1 + FBM_QA_LIMBS * l + r) * FBM_QROWW] += wide ? b18[d * FBM_QA_LIMBS + r] : 0u;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (l == 0) qa_normalise_column(col);
+        for (int r = 0; r < M; ++r) col[(d * FBM_QA_D1 + M * l + r) * ROWW] += wide ? b18[d * M + r] : 0u;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // a group never straddles two waves
+      if (l == 0 && !dummy) qa_normalise_column<ROWW>(col);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     if (!key_is_zero) {
-      qa_lds_to_tbl(col, l, table + tb0 / 4);
-      fbm_qa_sq_lds(ac, al, QK, np29, n, e0);  // h^2 R
-      qa_lds_to_tbl(col, l, scratch);
-      qa_tbl_to_lds(table + tb0 / 4, col, l);
+      qa_lds_to_tbl<M, ROWW>(col, l, table + tb0 / 4);
+      E::sq(ac, al, QK, np29, n, e0, bp);  // h^2 R
+      qa_lds_to_tbl<M, ROWW>(col, l, scratch);
+      qa_tbl_to_lds<M, ROWW>(table + tb0 / 4, col, l);
 #pragma unroll 1
       for (int t = 1; t < FBM_TABLE; ++t) {
-        fbm_qa_mm_glb(ac, al, table, tb0 + FBM_TSCRATCH * tstride, QK, np29, n, e0);
-        qa_lds_to_tbl(col, l, table + (tb0 + (uint32_t)t * tstride) / 4);
+        E::mm(ac, al, table, tb0 + FBM_TSCRATCH * tstride, QK, np29, n, e0, bp);
+        qa_lds_to_tbl<M, ROWW>(col, l, table + (tb0 + (uint32_t)t * tstride) / 4);
       }
-      qa_tbl_to_lds(table + (tb0 + (uint32_t)first * tstride) / 4, col, l);
+      qa_tbl_to_lds<M, ROWW>(table + (tb0 + (uint32_t)first * tstride) / 4, col, l);
 #pragma unroll 1
       for (int k = 0; k < n_ops; ++k) {
         const uint32_t op = __builtin_amdgcn_readfirstlane(ops[k]);
         const int nsq = (int)(op >> FBM_OP_SHIFT);
         const int idx = (int)(op & ((1u << FBM_OP_SHIFT) - 1u)) - 1;
 #pragma unroll 1
-        for (int q = 0; q < nsq; ++q) fbm_qa_sq_lds(ac, al, QK, np29, n, e0);
-        if (idx >= 0) fbm_qa_mm_glb(ac, al, table, tb0 + (uint32_t)idx * tstride, QK, np29, n, e0);
+        for (int q = 0; q < nsq; ++q) E::sq(ac, al, QK, np29, n, e0, bp);
+        if (idx >= 0) E::mm(ac, al, table, tb0 + (uint32_t)idx * tstride, QK, np29, n, e0, bp);
       }
     }
     {  // last operand: nude = (1, pt) (encrypt; 28-bit blocked column -> 29-bit slice) or 1
-      uint32_t b18[2 * FBM_QA_LIMBS];
+      uint32_t b18[2 * M];
       const uint32_t* nb = nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255);
 #pragma unroll
       for (int d = 0; d < 2; ++d)
 #pragma unroll
-        for (int r = 0; r < FBM_QA_LIMBS; ++r) {
-          const int k = FBM_QA_LIMBS * l + r;
+        for (int r = 0; r < M; ++r) {
+          const int k = M * l + r;
           uint32_t v = 0;
-          if ((mode & FBM_EXP_DEC) == 0) {
+          if (dummy) {
+          } else if ((mode & FBM_EXP_DEC) == 0) {
             const int bit = k * FBM_QA_LB, j = bit / FBM_LB, off = bit % FBM_LB;
             const uint32_t a0 = j < FBM_NLN ? nb[(d * FBM_NLN + j) * 256] : 0u;
             const uint32_t a1 = j + 1 < FBM_NLN ? nb[(d * FBM_NLN + j + 1) * 256] : 0u;
@@ -808,18 +866,18 @@ __global__ void __launch_bounds__(FBM_QBLOCK, 3) jl_expq_kernel(const uint32_t* 
           } else {
             v = (d == 0 && k == 0) ? 1u : 0u;
           }
-          b18[d * FBM_QA_LIMBS + r] = v;
+          b18[d * M + r] = v;
         }
-      col_store<2 * FBM_QA_LIMBS>(scratch, b18);
+      col_store<2 * M>(scratch, b18);
     }
-    fbm_qa_mm_glb(ac, al, table, tb0 + FBM_TSCRATCH * tstride, QK, np29, n, e0);
-    if (l == 0) {  // t + s N -> the canonical residue (lane 0 of the quad, from the LDS column)
+    E::mm(ac, al, table, tb0 + FBM_TSCRATCH * tstride, QK, np29, n, e0, bp);
+    if (l == 0 && !dummy) {  // t + s N -> the canonical residue (lane 0 of the group, from the LDS column)
       uint32_t t29[FBM_QA_L], s29[FBM_QA_L];
       uint32_t ct0 = 0, cs0 = 0;
 #pragma unroll
       for (int k = 0; k < FBM_QA_L; ++k) {  // the engine's lazy limbs -> normalised 29-bit limbs
-        const uint32_t vt = col[k * FBM_QROWW] + ct0;
-        const uint32_t vs = col[(FBM_QA_D1 + k) * FBM_QROWW] + cs0;
+        const uint32_t vt = col[k * ROWW] + ct0;
+        const uint32_t vs = col[(FBM_QA_D1 + k) * ROWW] + cs0;
         t29[k] = vt & FBM_QMASK;
         s29[k] = vs & FBM_QMASK;
         ct0 = vt >> FBM_QA_LB;
@@ -1310,10 +1368,9 @@ __global__ void jl_setup_kernel(JlSched sc, MontCtx mc, MontCtxN mn, NadicCtx na
     cst[FBM_CST_R2NA + t] = t < FBM_NL ? na.r2na[t] : 0u;
     cst[FBM_CST_R3NA + t] = t < FBM_NL ? na.r3na[t] : 0u;
   }
-  if (t < 64) {  // quad engine: K'_i, the lanes' N limbs (limb 9 l + r at word 4 r + l)
+  if (t < 64) {  // group engines: K'_i and N's 29-bit limbs
     cst[FBM_CST_QK + t] = t < FBM_QA_L ? qa.kp[t] : 0u;
-    const int r = t >> 2, l = t & 3;
-    cst[FBM_CST_QN + t] = t < 4 * FBM_QA_LIMBS ? qa.n[FBM_QA_LIMBS * l + r] : 0u;
+    cst[FBM_CST_QNP + t] = t < FBM_QA_L ? qa.n[t] : 0u;
   }
   if (t < 128) {
     cst[FBM_CST_QR2 + t] = t < 2 * FBM_QA_L ? qa.r2[t] : 0u;
@@ -1332,19 +1389,26 @@ int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32
 
 // ---- exponentiation engine choice ------------------------------------------------------
 // FBM_ENGINE_SINGLE: one lane per ciphertext (throughput: every lane busy, 2 waves/SIMD);
-// FBM_ENGINE_QUAD: four lanes per ciphertext (latency: launches below the chip's lane count);
-// FBM_ENGINE_AUTO: QUAD when every quad wave of the launch is resident at once (at most 3 per
-// SIMD: 3/8 of a one-lane round, 49 152 ciphertexts on 256 CUs); above that the one-lane
-// engine's lone-lane latency is the cheaper bound (measured: DESIGN.md section 5).
+// FBM_ENGINE_QUAD / FBM_ENGINE_TRIPLE: four / three lanes per ciphertext (latency: launches
+// below the chip's lane count).  FBM_ENGINE_AUTO picks the engine of least modelled time.  A
+// group engine's launch time is set by its busiest SIMD: with w waves on it (w = workgroups per
+// CU, each workgroup's 4 waves on the CU's 4 SIMDs) it takes about A + B w -- A the part of a
+// lone wave's time another wave cannot fill, B a wave's issue time.  Measured on MI355X
+// (tools/exp_probe.py over 1k..65k ciphertexts, 2040-bit exponent, profiles/r2_engine_sweep.jsonl):
+// quad 12.0 / 19.7 / 28.5 ms at 1 / 2 / 3 waves (A = 4, B = 8.1), triple 15.0 / 24.9 / 36.3
+// (A = 5.1, B = 9.9).  The one-lane engine's lone wave takes 33.6 ms (up to one wave per SIMD),
+// 50 ms per round of two.  The group engines hold at most 3 workgroups per CU and are only modelled (and
+// chosen) for launches that fit in one residency.
 static std::atomic<int> g_engine{-1};
 
 int jl_engine_policy() {
   int e = g_engine.load(std::memory_order_relaxed);
-  if (e < 0) {  // first use: FBM_JL_ENGINE=auto|single|quad (A/B runs), default auto
+  if (e < 0) {  // first use: FBM_JL_ENGINE=auto|single|quad|triple (A/B runs), default auto
     const char* v = getenv("FBM_JL_ENGINE");
     e = FBM_ENGINE_AUTO;
     if (v && !strcmp(v, "single")) e = FBM_ENGINE_SINGLE;
     if (v && !strcmp(v, "quad")) e = FBM_ENGINE_QUAD;
+    if (v && !strcmp(v, "triple")) e = FBM_ENGINE_TRIPLE;
     int expect = -1;
     g_engine.compare_exchange_strong(expect, e);
     e = g_engine.load(std::memory_order_relaxed);
@@ -1358,35 +1422,72 @@ int jl_engine_set(int mode) {
   return prev;
 }
 
-static uint64_t quad_wgs_max() { return (uint64_t)device_num_cu() * 3; }  // 3 workgroups (12 waves) per CU
+#define FBM_GROUP_WGS_PER_CU 3
+static uint64_t group_wgs_max() { return (uint64_t)device_num_cu() * FBM_GROUP_WGS_PER_CU; }
+static int group_ct_per_wg(int engine) { return engine == FBM_ENGINE_TRIPLE ? 84 : 64; }
 
-bool jl_use_quad(uint64_t n_ct) {
+// modelled launch time (ms) of n_ct ciphertexts on one engine (relative ranking only)
+static double engine_model_ms(int engine, uint64_t n_ct) {
+  const uint64_t ncu = (uint64_t)device_num_cu();
+  if (engine == FBM_ENGINE_SINGLE) {
+    const uint64_t lanes = ncu * 2 * FBM_BLOCK;
+    if (n_ct <= lanes / 2) return 33.6;
+    return 50.0 * (double)((n_ct + lanes - 1) / lanes) - (n_ct % lanes && n_ct % lanes <= lanes / 2 ? 16.4 : 0.0);
+  }
+  const uint64_t wgs = (n_ct + group_ct_per_wg(engine) - 1) / group_ct_per_wg(engine);
+  const uint64_t w = (wgs + ncu - 1) / ncu;
+  const double A = engine == FBM_ENGINE_TRIPLE ? 5.1 : 4.0, B = engine == FBM_ENGINE_TRIPLE ? 9.9 : 8.1;
+  // only launches whose workgroups are all resident at once (beyond that the one-lane engine's
+  // higher throughput per SIMD wins: 64 ciphertexts per 25 ms wave against 16 per 8.1 / 21 per 9.9)
+  if (w <= FBM_GROUP_WGS_PER_CU) return A + B * (double)w;
+  return 1e30;
+}
+
+int jl_engine_for(uint64_t n_ct) {
   const int e = jl_engine_policy();
-  if (e == FBM_ENGINE_QUAD) return true;
-  if (e == FBM_ENGINE_SINGLE) return false;
-  return n_ct * 8 <= jl_table_slots() * 3;
+  if (e != FBM_ENGINE_AUTO) return e;
+  int best = FBM_ENGINE_SINGLE;
+  double tb = engine_model_ms(FBM_ENGINE_SINGLE, n_ct);
+  for (int g : {FBM_ENGINE_QUAD, FBM_ENGINE_TRIPLE}) {
+    const double t = engine_model_ms(g, n_ct);
+    if (t < tb) {
+      tb = t;
+      best = g;
+    }
+  }
+  return best;
 }
 
 uint64_t jl_table_bytes(uint64_t n_ct) {
   const uint64_t cap = jl_table_slots();
   uint64_t g = ((n_ct + 255) / 256) * 256;
-  const uint64_t single = (g < cap ? g : cap) * FBM_TENTRIES * FBM_NL * 4;
-  uint64_t wq = (n_ct + FBM_QCT - 1) / FBM_QCT;
-  if (wq > quad_wgs_max()) wq = quad_wgs_max();
-  const uint64_t quad = wq * FBM_TENTRIES * FBM_QENTRY * 4;
-  return single > quad ? single : quad;
+  uint64_t need = (g < cap ? g : cap) * FBM_TENTRIES * FBM_NL * 4;
+  for (int e : {FBM_ENGINE_QUAD, FBM_ENGINE_TRIPLE}) {
+    uint64_t w = (n_ct + group_ct_per_wg(e) - 1) / group_ct_per_wg(e);
+    if (w > group_wgs_max()) w = group_wgs_max();
+    const uint64_t m = e == FBM_ENGINE_TRIPLE ? FBM_TA_LIMBS : FBM_QA_LIMBS;
+    const uint64_t b = w * FBM_TENTRIES * 2 * m * 256 * 4;
+    if (b > need) need = b;
+  }
+  return need;
 }
 
 int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const JlSched& sc, int mode,
                   const uint32_t* nude, uint32_t* table, uint64_t table_slots, const uint32_t* ops,
                   const uint32_t* cst, uint32_t* out, hipStream_t s) {
   if (n_ct == 0) return FBM_OK;
-  if (jl_use_quad(n_ct)) {
-    uint64_t g = (n_ct + FBM_QCT - 1) / FBM_QCT;
-    if (g > quad_wgs_max()) g = quad_wgs_max();
-    hipLaunchKernelGGL(jl_expq_kernel, dim3((unsigned)g), dim3(FBM_QBLOCK), 0, s, H, n_ct, (uint32_t*)cst, jp.qa.np,
-                       ops, sc.n_ops, sc.first, mode, jp.key_is_zero, nude, table, out);
-    return check_launch("jl_expq_kernel");
+  const int eng = jl_engine_for(n_ct);
+  if (eng == FBM_ENGINE_QUAD || eng == FBM_ENGINE_TRIPLE) {
+    uint64_t g = (n_ct + group_ct_per_wg(eng) - 1) / group_ct_per_wg(eng);
+    if (g > group_wgs_max()) g = group_wgs_max();
+    if (eng == FBM_ENGINE_QUAD) {
+      hipLaunchKernelGGL(jl_expg_kernel<4>, dim3((unsigned)g), dim3(FBM_QBLOCK), 0, s, H, n_ct, (uint32_t*)cst,
+                         jp.qa.np, ops, sc.n_ops, sc.first, mode, jp.key_is_zero, nude, table, out);
+      return check_launch("jl_expq_kernel");
+    }
+    hipLaunchKernelGGL(jl_expg_kernel<3>, dim3((unsigned)g), dim3(FBM_QBLOCK), 0, s, H, n_ct, (uint32_t*)cst,
+                       jp.qa.np, ops, sc.n_ops, sc.first, mode, jp.key_is_zero, nude, table, out);
+    return check_launch("jl_expt_kernel");
   }
   uint64_t g = (n_ct + FBM_BLOCK - 1) / FBM_BLOCK;
   const uint64_t gmax = table_slots / FBM_BLOCK;

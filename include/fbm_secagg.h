@@ -201,18 +201,19 @@ int fbm_jl_window(void);
 /* v_mad_u64_u32 per lane of one product of the JL exponentiation engine (N-adic Montgomery
  * product modulo N^2, fedbiomed_amd/csrc/fbm_nadic_asm.hpp): square != 0 -> a squaring. */
 int fbm_jl_mads(int square);
-/* The same count for the quad engine (4 lanes per ciphertext): v_mad_u64_u32 lane-ops per
- * product summed over the 4 lanes (fedbiomed_amd/csrc/fbm_quad_asm.hpp). */
+/* The same count for the quad / triple engines (4 / 3 lanes per ciphertext): v_mad_u64_u32
+ * lane-ops per product summed over the lanes (fedbiomed_amd/csrc/fbm_quad_asm.hpp, fbm_tri_asm.hpp). */
 int fbm_jl_quad_mads(int square);
+int fbm_jl_triple_mads(int square);
 
 /* Exponentiation engine policy of this process for the JL entry points (encrypt, decryption
- * factor, aggregate): 0 = auto (the default: four lanes per ciphertext when a launch holds
- * at most 3/8 of the chip's one-lane round, i.e. every quad wave resident at once; one lane
- * otherwise), 1 = one lane
- * per ciphertext (throughput: several concurrent launches that fill the chip together),
- * 4 = four lanes per ciphertext (latency).  Results are bit-identical either way.  Returns
- * the previous policy (or FBM_E_ARG).  FBM_JL_ENGINE=auto|single|quad sets the initial one.
- * fbm_jl_engine_for: the engine a launch of n_ct ciphertexts takes under the policy (1 or 4). */
+ * factor, aggregate): 0 = auto (the default: the engine of least modelled launch time for the
+ * launch's ciphertext count -- lane groups of 4 or 3 below the chip's one-lane round, one lane
+ * otherwise; fedbiomed_amd/csrc/fbm_jl.hip engine_model_ms), 1 = one lane per ciphertext
+ * (throughput: several concurrent launches that fill the chip together), 3 / 4 = three / four
+ * lanes per ciphertext (latency).  Results are bit-identical either way.  Returns the previous
+ * policy (or FBM_E_ARG).  FBM_JL_ENGINE=auto|single|triple|quad sets the initial one.
+ * fbm_jl_engine_for: the engine a launch of n_ct ciphertexts takes under the policy (1, 3 or 4). */
 int fbm_jl_set_engine(int mode);
 int fbm_jl_engine_for(uint64_t n_ct);
 

@@ -1,8 +1,9 @@
 """Lockstep interpreter for the generated gfx950 assembly products (test infrastructure).
 
 Runs the instruction list a generator (tools/gen_nadic_asm.py: one lane per ciphertext,
-tools/gen_quad_asm.py: four) emits for ONE lane (`Lane.run`) or for a group of lanes in
-lockstep (`Wave.run`: DPP quad_perm reads another lane's register, scalar state is
+tools/gen_quad_asm.py: four or three) emits for ONE lane (`Lane.run`) or for lanes in
+lockstep (`Wave.run`: DPP quad_perm / wave_shl:1 / wave_shr:1 and ds_bpermute_b32 read another
+lane's register -- wave shifts with bound_ctrl read 0 past either end --, scalar state is
 per-lane but identical), with LDS / global memory / the scalar constants block as shared
 dictionaries, so the register plan, offsets, loop control, cross-lane steps and arithmetic
 of the assembly are checked on the CPU against Python integers before they run on a GPU.
@@ -17,6 +18,7 @@ M64 = (1 << 64) - 1
 _PAIR = re.compile(r"^([vs])\[(\d+):(\d+)\]$")
 _ONE = re.compile(r"^([vs])(\d+)$")
 _QPERM = re.compile(r"quad_perm:\[(\d),(\d),(\d),(\d)\]")
+_WSHIFT = re.compile(r"wave_(shl|shr):1")
 
 
 def _size(ln):
@@ -35,13 +37,20 @@ def _size(ln):
 
 
 def _parse(ln):
-    """(op, operands, offset, quad_perm or None)"""
+    """(op, operands, offset, cross-lane source: quad_perm tuple, +1 (wave_shl:1: lane i reads
+    lane i + 1), -1 (wave_shr:1) or None)"""
     perm = None
     m = _QPERM.search(ln)
     if m:
         perm = tuple(int(m.group(i)) for i in range(1, 5))
         ln = ln[:m.start()].rstrip()
-    ln = re.sub(r"\s+(row_mask|bank_mask):\S+", "", ln)
+    m = _WSHIFT.search(ln)
+    if m:
+        if "bound_ctrl:0" not in ln:
+            raise NotImplementedError("wave shifts are only modelled with bound_ctrl:0 (0 past the ends)")
+        perm = 1 if m.group(1) == "shl" else -1
+        ln = ln[:m.start()].rstrip()
+    ln = re.sub(r"\s+(row_mask|bank_mask|bound_ctrl):\S+", "", ln)
     op, _, rest = ln.partition(" ")
     ops = [t.strip() for t in rest.split(",")] if rest else []
     off = 0
@@ -233,11 +242,24 @@ class Wave:
             op, ops, off, perm = prog[pc]
             pc += 1
             counts[op] = counts.get(op, 0) + 1
+            if op == "ds_bpermute_b32":  # dst <- data of lane addr / 4 (every lane reads, then writes)
+                vals = []
+                for lane in self.lanes:
+                    a = lane.get(ops[1]) + off
+                    assert a % 4 == 0 and 0 <= a // 4 < n, f"ds_bpermute address {a}"
+                    vals.append(a)
+                vals = [self.lanes[a // 4].get(ops[2]) for a in vals]
+                for i, lane in enumerate(self.lanes):
+                    lane.put(ops[0], vals[i])
+                continue
             if perm is not None:
-                # every lane reads src0 from its source lane (within its quad) before any
-                # lane writes; a VOP2 takes src1 from its own lane
-                src = [self.lanes[(i & ~3) + perm[i & 3]].get(ops[1]) if (i & ~3) + perm[i & 3] < n else 0
-                       for i in range(n)]
+                # every lane reads src0 from its source lane (within its quad, or the next /
+                # previous lane of the wave) before any lane writes; a VOP2 takes src1 from its own lane
+                if isinstance(perm, tuple):
+                    src = [self.lanes[(i & ~3) + perm[i & 3]].get(ops[1]) if (i & ~3) + perm[i & 3] < n else 0
+                           for i in range(n)]
+                else:
+                    src = [self.lanes[i + perm].get(ops[1]) if 0 <= i + perm < n else 0 for i in range(n)]
                 if op == "v_mov_b32_dpp":
                     vals = src
                 elif op == "v_and_b32_dpp":

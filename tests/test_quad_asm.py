@@ -1,6 +1,7 @@
-"""The generated QUAD N-adic assembly product (fedbiomed_amd/csrc/fbm_quad_asm.hpp, from
-tools/gen_quad_asm.py: four lanes per ciphertext, 29-bit limbs, DPP quad_perm exchanges),
-run in lockstep for whole quads on the CPU (tests/asm_sim.py Wave) against Python integers:
+"""The generated QUAD and TRIPLE N-adic assembly products (fedbiomed_amd/csrc/fbm_quad_asm.hpp /
+fbm_tri_asm.hpp, from tools/gen_quad_asm.py: four / three lanes per ciphertext, 29-bit limbs;
+DPP quad_perm exchanges / ds_bpermute broadcasts and DPP wave shifts), run in lockstep for
+whole groups (the triple with a trailing all-zero dummy lane, as lane 63 of a wave) on the CPU (tests/asm_sim.py Wave) against Python integers:
 X*Y*R^-1 mod N^2 with R = 2^1044, digits < 2N, lazy limbs within the documented bound, and
 no 64-bit column overflow (asserted by the simulator on every v_mad_u64_u32 -- the point of
 the mid-product reduction).  The residues are the one-lane engine's (tests/test_nadic_asm.py);
@@ -25,10 +26,11 @@ def _load(name):
 
 
 Q = _load("gen_quad_asm")
-LB, L, ML, ROWB, D1 = Q.LB, Q.L, Q.M, Q.ROWB, Q.D1
+LB, L = Q.LB, Q.L
 MASK = (1 << LB) - 1
 R = 1 << (LB * L)
-QMM, QSQ = Q.product(False), Q.product(True)
+GEOS = {"quad": Q.QUAD, "triple": Q.TRI}
+PROGS = {k: (Q.product(False, g), Q.product(True, g)) for k, g in GEOS.items()}
 
 
 def limbs(x, n=L):
@@ -42,9 +44,15 @@ def qconsts(N):
     return [MASK + v for v in limbs(K)], (-pow(N, -1, 1 << LB)) % (1 << LB)
 
 
-def run_quad(N, As, Bs=None, lazy_in=False):
-    """As / Bs: lists (one per ciphertext = quad) of digit pairs; Bs None = square.
-    Returns per ciphertext the result digit integers (t, s), the max limb and the counts."""
+def run_quad(N, As, Bs=None, lazy_in=False, geo="quad", in_bounds=True):
+    """As / Bs: lists (one per ciphertext = lane group) of digit pairs; Bs None = square.
+    Returns per ciphertext the result digit integers (t, s), the max limb and the counts.
+    geo "triple": groups of 3 lanes and a trailing dummy lane (zero column, e0 = 0, N = 0,
+    permute source itself), as lane 63 of a triple-engine wave.  in_bounds: the operands are
+    within the engine's documented bounds, so the top lane hands nothing up (checked: the
+    dummy column stays zero)."""
+    g = GEOS[geo]
+    G, ML, ROWB, D1 = g.G, g.M, g.ROWB, g.D1
     kp, np_ = qconsts(N)
     QK, BB = 0x4000, 0x100000
     smem = {QK + 4 * i: w for i, w in enumerate(kp)}
@@ -61,19 +69,30 @@ def run_quad(N, As, Bs=None, lazy_in=False):
                     col[d + 9] += 1 << LB
         for k, v in enumerate(col):
             lds[ac + k * ROWB] = v
-        for l in range(4):
-            tid = 4 * c + l
+        for l in range(G):
+            tid = G * c + l
             if Bs is not None:
                 bl, bh = limbs(Bs[c][0]), limbs(Bs[c][1])
                 for r in range(ML):
                     glb[BB + tid * 4 + r * 1024] = bl[ML * l + r]
                     glb[BB + tid * 4 + (ML + r) * 1024] = bh[ML * l + r]
             args = {"ac": ac, "al": ac + ML * l * ROWB, "b": tid * 4, "bb": BB, "QK": QK, "np": np_,
-                    "e0": 1 if l == 0 else 0}
+                    "e0": 1 if l == 0 else 0, "bp": 4 * G * c}
             for r in range(ML):
                 args[f"n{r}"] = nl[ML * l + r]
             lanes.append(Lane(args, lds=lds, glb=glb, smem=smem))
-    counts = Wave(lanes).run(QMM if Bs is not None else QSQ)
+    if G == 3:  # the wave's dummy lane: its own all-zero column, contributes nothing
+        tid, ac = G * len(As), 4 * len(As)
+        if Bs is not None:
+            for j in range(2 * ML):
+                glb[BB + tid * 4 + j * 1024] = 0
+        args = {"ac": ac, "al": ac, "b": tid * 4, "bb": BB, "QK": QK, "np": np_, "e0": 0, "bp": 4 * tid}
+        args.update({f"n{r}": 0 for r in range(ML)})
+        lanes.append(Lane(args, lds=lds, glb=glb, smem=smem))
+    mm, sq = PROGS[geo]
+    counts = Wave(lanes).run(mm if Bs is not None else sq)
+    if G == 3 and in_bounds:
+        assert all(lds.get(4 * len(As) + k * ROWB, 0) == 0 for k in range(2 * L)), "dummy column disturbed"
     out, top = [], 0
     for c in range(len(As)):
         col = [lds[4 * c + k * ROWB] for k in range(2 * L)]
@@ -88,41 +107,44 @@ def _rand_n(rng, bits):
     return rng.getrandbits(bits) | (1 << (bits - 1)) | 1
 
 
+@pytest.mark.parametrize("geo", ["quad", "triple"])
 @pytest.mark.parametrize("bits", [2, 24, 1024])
-def test_quad_product_and_square(bits):
+def test_quad_product_and_square(bits, geo):
     rng = random.Random(100 + bits)
     N = _rand_n(rng, bits)
     M = N * N
     rinv = pow(R, -1, M)
     As = [(2 * N - 1, 2 * N - 1)] + [(rng.randrange(2 * N), rng.randrange(2 * N)) for _ in range(2)]
     Bs = [(2 * N - 1, 2 * N - 1)] + [(rng.randrange(2 * N), rng.randrange(2 * N)) for _ in range(2)]
-    got, top, counts = run_quad(N, As, Bs)
+    got, top, counts = run_quad(N, As, Bs, geo=geo)
     assert top < (1 << LB) + (1 << 11)
-    assert counts["v_mad_u64_u32"] == Q.product_mads(False)
+    assert counts["v_mad_u64_u32"] == Q.product_mads(False, GEOS[geo])
     for a, b, (t, s) in zip(As, Bs, got):
         A, B = (a[0] + a[1] * N) % M, (b[0] + b[1] * N) % M
         assert (t + s * N) % M == A * B * rinv % M
         assert t < 2 * N and s < 2 * N
-    got, top, counts = run_quad(N, As)
-    assert counts["v_mad_u64_u32"] == Q.product_mads(True)
+    got, top, counts = run_quad(N, As, geo=geo)
+    assert counts["v_mad_u64_u32"] == Q.product_mads(True, GEOS[geo])
     for a, (t, s) in zip(As, got):
         A = (a[0] + a[1] * N) % M
         assert (t + s * N) % M == A * A * rinv % M
         assert t < 2 * N and s < 2 * N
 
 
-def test_quad_worst_case_columns():
+@pytest.mark.parametrize("geo", ["quad", "triple"])
+def test_quad_worst_case_columns(geo):
     """All-ones limbs (every operand limb 2^29 - 1, and lazy ones above it): the largest column
     sums the bound allows; the simulator's overflow asserts are the check."""
     N = (1 << 1024) - 1  # odd, every limb of N at its maximum
     top = (1 << (LB * L)) - 1
     for a, b in (((top, top), (top, top)), ((2 * N - 1, 2 * N - 1), (top, top))):
-        run_quad(N, [a], [b])
-        run_quad(N, [a])
-        run_quad(N, [a], lazy_in=True)
+        run_quad(N, [a], [b], geo=geo, in_bounds=False)
+        run_quad(N, [a], geo=geo, in_bounds=False)
+        run_quad(N, [a], lazy_in=True, geo=geo, in_bounds=False)
 
 
-def test_quad_operand_shapes_and_lazy_limbs():
+@pytest.mark.parametrize("geo", ["quad", "triple"])
+def test_quad_operand_shapes_and_lazy_limbs(geo):
     """(h, 0) with h < R, (1, pt) with pt < 2^1036, and lazy input limbs: exact."""
     rng = random.Random(9)
     for bits in (24, 1024):
@@ -131,18 +153,19 @@ def test_quad_operand_shapes_and_lazy_limbs():
         rinv = pow(R, -1, M)
         h = rng.getrandbits(LB * L)
         r2 = (R * R) % M
-        (t, s), = run_quad(N, [(r2 % N, r2 // N)], [(h, 0)])[0]
+        (t, s), = run_quad(N, [(r2 % N, r2 // N)], [(h, 0)], geo=geo)[0]
         assert (t + s * N) % M == h * R % M and t < 3 * N + 1 and s < 3 * N + 1
         pt = rng.getrandbits(1036)
         x = (rng.randrange(2 * N), rng.randrange(2 * N))
-        (t, s), = run_quad(N, [x], [(1, pt)])[0]
+        (t, s), = run_quad(N, [x], [(1, pt)], geo=geo)[0]
         assert (t + s * N) % M == (x[0] + x[1] * N) * (1 + N * pt) * rinv % M
-        (t, s), = run_quad(N, [x], lazy_in=True)[0]
+        (t, s), = run_quad(N, [x], lazy_in=True, geo=geo)[0]
         X = (x[0] + x[1] * N) % M
         assert (t + s * N) % M == X * X * rinv % M
 
 
-def test_quad_chain_power():
+@pytest.mark.parametrize("geo", ["quad", "triple"])
+def test_quad_chain_power(geo):
     """A short square-and-multiply chain through the simulated quad engine (results fed back
     as the next operands, lazy limbs and all): h^e mod N^2."""
     from fedbiomed_amd import workload as W
@@ -152,21 +175,22 @@ def test_quad_chain_power():
     rng = random.Random(11)
     h, e = rng.getrandbits(256), rng.getrandbits(10) | (1 << 9)
     u = (R * R) % M
-    (x,), _, _ = run_quad(N, [(u % N, u // N)], [(h, 0)])
+    (x,), _, _ = run_quad(N, [(u % N, u // N)], [(h, 0)], geo=geo)
     hr = x
     for bit in bin(e)[3:]:
-        (x,), _, _ = run_quad(N, [x])
+        (x,), _, _ = run_quad(N, [x], geo=geo)
         if bit == "1":
-            (x,), _, _ = run_quad(N, [x], [hr])
-    (t, s), = run_quad(N, [x], [(1, 0)])[0]  # * 1 (drops R)
+            (x,), _, _ = run_quad(N, [x], [hr], geo=geo)
+    (t, s), = run_quad(N, [x], [(1, 0)], geo=geo)[0]  # * 1 (drops R)
     assert (t + s * N) % M == pow(h, e, M)
 
 
-def test_quad_dpp_wait_states():
+@pytest.mark.parametrize("geo", ["quad", "triple"])
+def test_quad_dpp_wait_states(geo):
     """Every DPP read of a VGPR is at least 2 wait states after the VALU write of it."""
-    for prog in (QMM, QSQ):
+    for prog in PROGS[geo]:
         for i, ln in enumerate(prog):
-            if "quad_perm" not in ln:
+            if not Q.is_dpp(ln):
                 continue
             src = ln.split(",")[1].split()[0]
             dist = 0
@@ -182,3 +206,47 @@ def test_quad_dpp_wait_states():
                 if dist >= 2:
                     break
             assert dist >= 2, (i, ln)
+
+
+def _lds_waits_ok(prog, g):
+    """Every read of a ds_bpermute / ds_read destination comes after an s_waitcnt that has
+    retired that LDS op (LDS ops return in order; lgkmcnt(k) = at most k still in flight).
+    Loop back-edges are followed once (the row pairs are the steady state)."""
+    lab = {ln[:-1]: i for i, ln in enumerate(prog) if ln.endswith(":")}
+    pending = []  # destinations of in-flight LDS ops, oldest first
+
+    def reads(ln):
+        op, _, rest = ln.partition(" ")
+        toks = [t.strip().split()[0] for t in rest.split(",")[1:]] if rest else []
+        if op.startswith("ds_write"):
+            toks = [t.strip().split()[0] for t in rest.split(",")]
+        return {t for t in toks if t.startswith("v") and not t.startswith("v[")} | \
+            {f"v{k}" for t in toks if t.startswith("v[") for k in range(int(t[2:-1].split(":")[0]),
+                                                                       int(t[2:-1].split(":")[1]) + 1)}
+
+    seen_back = set()
+    i = 0
+    while i < len(prog):
+        ln = prog[i]
+        op = ln.split(" ")[0]
+        if op == "s_waitcnt" and "lgkmcnt" in ln:
+            k = int(ln.split("lgkmcnt(")[1].split(")")[0])
+            pending = pending[len(pending) - k:] if k else []
+        else:
+            r = reads(ln)
+            for d in pending:
+                assert d not in r, f"read of {d} before its LDS op retired: {i}: {ln}"
+            if op in ("ds_read_b32", "ds_bpermute_b32"):
+                pending.append(ln.split(" ")[1].rstrip(","))
+        if op == "s_cbranch_scc1" and i not in seen_back:
+            seen_back.add(i)
+            i = lab[ln.split(" ")[1].rstrip("bf")]
+            continue
+        i += 1
+    return True
+
+
+@pytest.mark.parametrize("geo", ["quad", "triple"])
+def test_lds_results_waited_for(geo):
+    for prog in PROGS[geo]:
+        assert _lds_waits_ok(prog, GEOS[geo])

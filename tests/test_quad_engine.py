@@ -1,9 +1,11 @@
-"""The quad exponentiation engine (four lanes per ciphertext, jl_expq_kernel) against the
-one-lane engine and the oracle, through the C-ABI: every JL entry point that exponentiates
-(encrypt, decryption factor, aggregate) must give bit-identical results under both engines,
+"""The lane-group exponentiation engines (four / three lanes per ciphertext, jl_expg_kernel<4>
+/ <3>) against the one-lane engine and the oracle, through the C-ABI: every JL entry point that
+exponentiates (encrypt, decryption factor, aggregate) must give bit-identical results under
+every engine,
 on the default biprime, small moduli (FDH retries: the wide-digest path), negative keys
-(H^-1 as N-adic digits), a zero key and negative weights.  The engine choice itself
-(fbm_jl_set_engine / auto by launch size) is checked on the host without a GPU."""
+(H^-1 as N-adic digits), a zero key and negative weights, and launches that span several
+triple waves and workgroups (the wave-shift neighbours and the dummy lane 63).  The engine
+choice itself (fbm_jl_set_engine / auto by launch size) is checked on the host without a GPU."""
 
 import numpy as np
 import pytest
@@ -23,8 +25,11 @@ def test_engine_policy_host():
         assert lib.fbm_jl_engine_for(10) == 1
         assert lib.fbm_jl_set_engine(4) == 1 and lib.fbm_jl_engine_for(10**7) == 4
         assert lib.fbm_jl_set_engine(7) == _native.FBM_E_ARG
-        lib.fbm_jl_set_engine(0)  # auto: small launches quad, chip-filling ones single
+        assert lib.fbm_jl_set_engine(3) == 4 and lib.fbm_jl_engine_for(10) == 3
+        lib.fbm_jl_set_engine(0)  # auto: the engine of least modelled time (256 CUs here: no GPU)
         assert lib.fbm_jl_engine_for(1000) == 4 and lib.fbm_jl_engine_for(333_334) == 1
+        assert lib.fbm_jl_engine_for(41_667) == 3  # a config-4 stripe: 2 triple waves per SIMD, 3 quad
+        assert lib.fbm_jl_engine_for(30_000) == 4 and lib.fbm_jl_engine_for(200_000) == 1
     finally:
         lib.fbm_jl_set_engine(prev)
     import importlib.util
@@ -36,11 +41,17 @@ def test_engine_policy_host():
     g = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(g)
     assert lib.fbm_jl_quad_mads(1) == 4 * g.product_mads(True) and lib.fbm_jl_quad_mads(0) == 4 * g.product_mads(False)
+    assert lib.fbm_jl_triple_mads(1) == 3 * g.product_mads(True, g.TRI)
+    assert lib.fbm_jl_triple_mads(0) == 3 * g.product_mads(False, g.TRI)
+
+
+ENGINES = ("single", "quad", "triple")
 
 
 def _both(fn):
+    """fn() under every engine: [single, quad, triple]"""
     outs = []
-    for eng in ("single", "quad"):
+    for eng in ENGINES:
         with D.jl_engine(eng):
             outs.append(fn())
     return outs
@@ -67,8 +78,8 @@ def test_quad_equals_single_encrypt_aggregate(case):
     def enc():
         return torch.stack([jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=ws[p]) for p in range(P)])
 
-    c1, c4 = _both(enc)
-    assert torch.equal(c1, c4)
+    c1, c4, c3 = _both(enc)
+    assert torch.equal(c1, c4) and torch.equal(c1, c3)
     es, cr = O.jl_slot(None, P)
     for p in range(P):  # first, last and one middle ciphertext vs the oracle
         qw = [int(v) * ws[p] for v in O.quantize(W.party_params(p, n).astype(np.float64))]
@@ -76,9 +87,10 @@ def test_quad_equals_single_encrypt_aggregate(case):
             got = D.limbs_to_ints(c1[p, k:k + 1].cpu().numpy())[0]
             assert got == O.jl_encrypt_ints(qw[k * cr:(k + 1) * cr], tau, keys[p], W.BIPRIME0, P, k0=k)[0]
     sk0 = -sum(keys)
-    a1, a4 = _both(lambda: jc.aggregate_tensor(tau, c1, sk0, W.BIPRIME0, 77, num_expected_params=n,
-                                               want_sums=True))
-    assert torch.equal(a1[0], a4[0]) and torch.equal(a1[1], a4[1])
+    a1, a4, a3 = _both(lambda: jc.aggregate_tensor(tau, c1, sk0, W.BIPRIME0, 77, num_expected_params=n,
+                                                   want_sums=True))
+    for a in (a4, a3):
+        assert torch.equal(a1[0], a[0]) and torch.equal(a1[1], a[1])
 
 
 _N297 = 105 * (__import__("random").Random(5).getrandbits(290) | 1 | (1 << 289))
@@ -100,8 +112,8 @@ def test_quad_equals_single_small_moduli(nmod):
             n_ct = k
             break
         retries += h.bit_length() > 256
-    f1, f4 = _both(lambda: D.jl_decrypt_factor(n_ct, nmod, 123456789, 3, dev=dev))
-    assert torch.equal(f1, f4)
+    f1, f4, f3 = _both(lambda: D.jl_decrypt_factor(n_ct, nmod, 123456789, 3, dev=dev))
+    assert torch.equal(f1, f4) and torch.equal(f1, f3)
     got = D.limbs_to_ints(f1.cpu().numpy())
     for k in range(0, n_ct, max(1, n_ct // 40)):
         h = O.fdh((k << 512) | 3, n2)
@@ -114,11 +126,16 @@ def test_quad_equals_single_small_moduli(nmod):
 
 @pytest.mark.gpu
 def test_quad_factor_stripe_config4():
-    """The 1/8 stripe of config 4 (41 667 ciphertexts: the auto policy's quad case) and an
-    offset stripe: identical factors under both engines."""
+    """The 1/8 stripe of config 4 (41 667 ciphertexts: the auto policy's triple case), an
+    offset stripe and a size past the group engines' resident capacity (chunks pulled in
+    rounds): identical factors under every engine, spot-checked against the oracle."""
     dev = D.device()
     sk0 = W.jl_server_key(8)
-    for n_ct, off in ((41_667, 0), (5_000, 41_667 * 3)):
-        f1, f4 = _both(lambda: D.jl_decrypt_factor(n_ct, W.BIPRIME0, sk0, 1, ct_offset=off, dev=dev))
-        assert torch.equal(f1, f4)
-    assert D.jl_engine_for(41_667) == "quad"
+    n2 = W.BIPRIME0 ** 2
+    for n_ct, off in ((41_667, 0), (5_000, 41_667 * 3), (70_001, 11)):
+        f1, f4, f3 = _both(lambda: D.jl_decrypt_factor(n_ct, W.BIPRIME0, sk0, 1, ct_offset=off, dev=dev))
+        assert torch.equal(f1, f4) and torch.equal(f1, f3)
+        got = D.limbs_to_ints(f3[::n_ct // 7].cpu().numpy())
+        for i, k in enumerate(range(0, n_ct, n_ct // 7)):
+            assert got[i] == O.powmod(O.fdh(((k + off) << 512) | 1, n2), sk0, n2), (n_ct, k)
+    assert D.jl_engine_for(41_667) == "triple"

@@ -3,7 +3,7 @@
 `--ct` ciphertexts under each engine (rocprofv3 --kernel-trace / --pmc attribute the
 dispatches to jl_exp_kernel / jl_expq_kernel).  Prints per-engine wall times.
 
-    python tools/exp_probe.py [--ct 41667] [--engines single,quad] [--reps 2]
+    python tools/exp_probe.py [--ct 41667[,16384,...]] [--engines single,quad] [--reps 2]
 """
 
 import argparse
@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--ct", type=int, default=41_667)
+    ap.add_argument("--ct", default="41667", help="comma-separated ciphertext counts")
     ap.add_argument("--engines", default="single,quad")
     ap.add_argument("--reps", type=int, default=2)
     args = ap.parse_args()
@@ -28,19 +28,20 @@ def main():
 
     dev = D.device()
     sk0 = W.jl_server_key(8)
-    out = {"ct": args.ct}
-    for eng in args.engines.split(","):
-        with D.jl_engine(eng):
-            D.jl_decrypt_factor(args.ct, W.BIPRIME0, sk0, 1, dev=dev)
-            torch.cuda.synchronize()
-            ts = []
-            for _ in range(args.reps):
-                t0 = time.perf_counter()
-                D.jl_decrypt_factor(args.ct, W.BIPRIME0, sk0, 1, dev=dev)
+    for ct in [int(c) for c in args.ct.split(",")]:
+        out = {"ct": ct}
+        for eng in args.engines.split(","):
+            with D.jl_engine(eng):
+                D.jl_decrypt_factor(ct, W.BIPRIME0, sk0, 1, dev=dev)
                 torch.cuda.synchronize()
-                ts.append(1000 * (time.perf_counter() - t0))
-        out[eng + "_ms"] = ts
-    print(json.dumps(out))
+                ts = []
+                for _ in range(args.reps):
+                    t0 = time.perf_counter()
+                    D.jl_decrypt_factor(ct, W.BIPRIME0, sk0, 1, dev=dev)
+                    torch.cuda.synchronize()
+                    ts.append(round(1000 * (time.perf_counter() - t0), 3))
+            out[eng + "_ms"] = ts
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

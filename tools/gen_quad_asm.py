@@ -62,69 +62,108 @@ Register plan (per lane):
 LDS column: limb k of digit d at byte ac + (36 d + k) * ROW, ROW = 72 words * 4 (64 ciphertexts
 per workgroup + 8 words of padding: the slice writes of a 32-lane half hit 32 distinct banks).
 
-Usage:  python tools/gen_quad_asm.py   (rewrites the header; the build does not run this)
+TRIPLE variant (G = 3 lanes per ciphertext, 12 limbs per lane, fbm_tri_asm.hpp): 21
+ciphertexts per wave (lanes 0..62) + one dummy lane (63, all-zero data).  Same arithmetic and
+register roles; the cross-lane steps cannot use quad_perm (groups of 3 straddle the 4-lane DPP
+quads), so
+  * the quotient digits are masked in place (v_and_b32) and broadcast from the group's lane 0
+    by ds_bpermute_b32 (an LDS-pipe op: no VALU cycle; its latency hides behind the row's
+    multiplies -- s_waitcnt lgkmcnt before the first use), lane 0 itself using its own copy;
+  * the retire rotation (lane -> lane below) is v_and_b32_dpp wave_shl:1 bound_ctrl:0 (the
+    group's top lane receives the next group's lane 0, whose masked value is 0; lane 62
+    receives the dummy's 0), the carry hand-ups are v_mov_b32_dpp wave_shr:1 bound_ctrl:0.
+Why: a launch of n ciphertexts needs ceil(n / 16) quad waves but ceil(n / 21) triple waves;
+at a config-4 stripe (41 667) that is 2.54 vs 1.94 waves per SIMD, i.e. 3 vs 2 on the
+busiest SIMD, and one triple wave costs ~1.16 quad waves.
+
+Usage:  python tools/gen_quad_asm.py   (rewrites both headers; the build does not run this)
 """
 
 import os
 
 LB = 29         # bits per limb
 L = 36          # limbs per digit
-M = 9           # limbs per lane
-ROWW = 72       # LDS words between limb rows
-ROWB = ROWW * 4
-D1 = L          # limb index of digit 1 in the LDS column
 MID = 18        # rows before the mid-product reduction
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "fedbiomed_amd", "csrc", "fbm_quad_asm.hpp")
 MASK = hex((1 << LB) - 1)
 
 
-def At(k):
-    return f"v[{2 * k}:{2 * k + 1}]"
+class Geo:
+    """Register plan and cross-lane primitives of one engine: G lanes per ciphertext,
+    M = 36 / G limbs per lane."""
+
+    def __init__(self, G, rows_w):
+        self.G, self.M = G, L // G
+        self.ROWW, self.ROWB, self.D1 = rows_w, rows_w * 4, L
+        M = self.M
+        self.TT0 = 2 * (M - 1)          # t window: slots 0..M-2 at v[0:2M-3], TT, RT
+        self.RT0 = self.TT0 + 2
+        self.AS0 = self.RT0 + 2         # s window
+        self.TS0 = self.AS0 + 2 * (M - 1)
+        self.RS0 = self.TS0 + 2
+        self.B00 = self.RS0 + 2         # b0[0..M-1], b1[0..M-1]
+        self.B10 = self.B00 + M
+        x = self.B10 + M
+        self.XA, self.XB = (f"v{x}", f"v{x + 1}"), (f"v{x + 2}", f"v{x + 3}")
+        names = ["Q", "Q2", "CQ", "AADR", "TMP", "TMP2", "MASKV"]
+        for i, nm in enumerate(names):
+            setattr(self, nm, f"v{x + 4 + i}")
+        c = x + 4 + len(names) + 1      # (quad: one spare register before the carry pairs)
+        self.CY, self.CYLO, self.CYHI = f"v[{c}:{c + 1}]", f"v{c}", f"v{c + 1}"
+        self.CS, self.CSLO, self.CSHI = f"v[{c + 2}:{c + 3}]", f"v{c + 2}", f"v{c + 3}"
+        self.T3, self.T4 = f"v{c + 4}", f"v{c + 5}"
+        nreg = c + 6
+        if G == 3:                      # broadcast copies of the quotient digits
+            self.QB, self.Q2B = f"v{nreg}", f"v{nreg + 1}"
+            nreg += 2
+        else:
+            self.QB, self.Q2B = self.Q, self.Q2
+        self.NREG = nreg
+        self.TT, self.TTLO = f"v[{self.TT0}:{self.TT0 + 1}]", f"v{self.TT0}"
+        self.RT, self.RTLO, self.RTHI = f"v[{self.RT0}:{self.RT0 + 1}]", f"v{self.RT0}", f"v{self.RT0 + 1}"
+        self.TS, self.TSLO = f"v[{self.TS0}:{self.TS0 + 1}]", f"v{self.TS0}"
+        self.RS, self.RSLO, self.RSHI = f"v[{self.RS0}:{self.RS0 + 1}]", f"v{self.RS0}", f"v{self.RS0 + 1}"
+
+    def At(self, k):
+        return f"v[{2 * k}:{2 * k + 1}]"
+
+    def AtLo(self, k):
+        return f"v{2 * k}"
+
+    def AtHi(self, k):
+        return f"v{2 * k + 1}"
+
+    def As(self, k):
+        return f"v[{self.AS0 + 2 * k}:{self.AS0 + 2 * k + 1}]"
+
+    def AsLo(self, k):
+        return f"v{self.AS0 + 2 * k}"
+
+    def AsHi(self, k):
+        return f"v{self.AS0 + 2 * k + 1}"
+
+    def B0(self, r):
+        return f"v{self.B00 + r}"
+
+    def B1(self, r):
+        return f"v{self.B10 + r}"
+
+    # ---- cross-lane steps ----
+    def down(self, op, dst, src, extra=""):
+        """dst <- src of the lane above (the lane below receives): retire rotation"""
+        if self.G == 4:
+            return f"{op} {dst}, {src}{extra} {dpp((1, 2, 3, 0))}"
+        return f"{op} {dst}, {src}{extra} wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+
+    def up(self, dst, src):
+        """dst <- src of the lane below (carry hand-up; the group's lane 0 receives 0)"""
+        if self.G == 4:
+            return f"v_mov_b32_dpp {dst}, {src} {dpp((3, 0, 1, 2))}"
+        return f"v_mov_b32_dpp {dst}, {src} wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
 
 
-def AtLo(k):
-    return f"v{2 * k}"
-
-
-def AtHi(k):
-    return f"v{2 * k + 1}"
-
-
-def As(k):
-    return f"v[{20 + 2 * k}:{21 + 2 * k}]"
-
-
-def AsLo(k):
-    return f"v{20 + 2 * k}"
-
-
-def AsHi(k):
-    return f"v{21 + 2 * k}"
-
-
-TT, TTLO = "v[16:17]", "v16"
-RT, RTLO, RTHI = "v[18:19]", "v18", "v19"
-TS, TSLO = "v[36:37]", "v36"
-RS, RSLO, RSHI = "v[38:39]", "v38", "v39"
-
-
-def B0(r):
-    return f"v{40 + r}"
-
-
-def B1(r):
-    return f"v{49 + r}"
-
-
-XA, XB = ("v58", "v59"), ("v60", "v61")
-Q, Q2, CQ, AADR, TMP, TMP2, MASKV = "v62", "v63", "v64", "v65", "v66", "v67", "v68"
-CY, CYLO, CYHI = "v[70:71]", "v70", "v71"
-CS, CSLO, CSHI = "v[72:73]", "v72", "v73"
-T3, T4 = "v74", "v75"
-NREG = 76
-KBASE = 64      # K'_i in s(64 + i)
-M0_SAVE = "s19"
+QUAD = Geo(4, 72)   # 64 ciphertexts per workgroup + 8 words of padding
+TRI = Geo(3, 89)    # 84 ciphertexts + the dummy column + 4 words of padding
 
 
 def N(r):
@@ -133,6 +172,10 @@ def N(r):
 
 def dpp(perm):
     return f"quad_perm:[{','.join(str(p) for p in perm)}] row_mask:0xf bank_mask:0xf"
+
+
+def is_dpp(ln):
+    return "quad_perm" in ln or "wave_sh" in ln
 
 
 class Emitter:
@@ -154,7 +197,7 @@ class Emitter:
         return {d} if d.startswith("v") else set()
 
     def emit(self, ln):
-        if "quad_perm" in ln:
+        if is_dpp(ln):
             src = ln.split(",")[1].split()[0].strip()
             dist = 0
             for prev in reversed(self.out):
@@ -184,68 +227,98 @@ def load_consts():
             "s_load_dwordx4 s[96:99], %[QK], 0x80"]
 
 
-def load_b_global():
-    """b0[r] = limb row r, b1[r] = limb row 9 + r of the lane's quad-layout column: word
-    (row * 256 + lane) of the 64-ciphertext block, rows 1 KB apart (%[b] = the lane's byte
-    offset from the uniform %[bb])."""
-    out = ["s_waitcnt vmcnt(0)", f"v_mov_b32 {TMP}, %[b]"]
-    for j in range(2 * M):
+def load_b_global(g):
+    """b0[r] = limb row r, b1[r] = limb row M + r of the lane's table column: word
+    (row * 256 + lane) of the block, rows 1 KB apart (%[b] = the lane's byte offset from the
+    uniform %[bb])."""
+    out = ["s_waitcnt vmcnt(0)", f"v_mov_b32 {g.TMP}, %[b]"]
+    for j in range(2 * g.M):
         if j and j % 4 == 0:
-            out.append(f"v_add_u32 {TMP}, 0x1000, {TMP}")
-        reg = B0(j) if j < M else B1(j - M)
-        out.append(f"global_load_dword {reg}, {TMP}, %[bb] offset:{(j % 4) * 1024}")
+            out.append(f"v_add_u32 {g.TMP}, 0x1000, {g.TMP}")
+        reg = g.B0(j) if j < g.M else g.B1(j - g.M)
+        out.append(f"global_load_dword {reg}, {g.TMP}, %[bb] offset:{(j % 4) * 1024}")
     return out
 
 
-def load_b_lds(double_b1):
+def load_b_lds(g, double_b1):
     out = []
-    for r in range(M):
-        out.append(f"ds_read_b32 {B0(r)}, %[al] offset:{r * ROWB}")
-        out.append(f"ds_read_b32 {B1(r)}, %[al] offset:{(D1 + r) * ROWB}")
+    for r in range(g.M):
+        out.append(f"ds_read_b32 {g.B0(r)}, %[al] offset:{r * g.ROWB}")
+        out.append(f"ds_read_b32 {g.B1(r)}, %[al] offset:{(g.D1 + r) * g.ROWB}")
     out.append("s_waitcnt lgkmcnt(0)")
     if double_b1:  # square: the s part is x0 * (2 x1)
-        out += [f"v_lshlrev_b32 {B1(r)}, 1, {B1(r)}" for r in range(M)]
+        out += [f"v_lshlrev_b32 {g.B1(r)}, 1, {g.B1(r)}" for r in range(g.M)]
     return out
 
 
-def row(first, sq, kreg, xs, xn, pre_off):
+def row(g, first, sq, kreg, xs, xn, pre_off):
     """One row with an explicit schedule (every dependent instruction 3+ instructions after
     its producer).  xs = this row's (x0, x1); xn = where the prefetch of the next row's
     operands goes, read at byte offset pre_off from AADR; kreg = K'_i."""
+    M = g.M
     x0, x1 = xs
-    out = [f"ds_read_b32 {xn[0]}, {AADR} offset:{pre_off}"]
+    out = [f"ds_read_b32 {xn[0]}, {g.AADR} offset:{pre_off}"]
     if not sq:
-        out.append(f"ds_read_b32 {xn[1]}, {AADR} offset:{pre_off + D1 * ROWB}")
+        out.append(f"ds_read_b32 {xn[1]}, {g.AADR} offset:{pre_off + g.D1 * g.ROWB}")
 
     def addend(acc, r):
         if first:
             return "0"
         if r == M - 1:
-            return RT if acc is At else RS
+            return g.RT if acc == g.At else g.RS
         return acc(r)
 
     def tm(r):  # t pass 1: x0 * b0[r]
-        dst = TT if r == 0 else At(r - 1)
-        return f"v_mad_u64_u32 {dst}, vcc, {x0}, {B0(r)}, {addend(At, r)}"
+        dst = g.TT if r == 0 else g.At(r - 1)
+        return f"v_mad_u64_u32 {dst}, vcc, {x0}, {g.B0(r)}, {addend(g.At, r)}"
 
     def sm(r):  # s pass 1: x0 * b1[r]
-        dst = TS if r == 0 else As(r - 1)
-        return f"v_mad_u64_u32 {dst}, vcc, {x0}, {B1(r)}, {addend(As, r)}"
+        dst = g.TS if r == 0 else g.As(r - 1)
+        return f"v_mad_u64_u32 {dst}, vcc, {x0}, {g.B1(r)}, {addend(g.As, r)}"
 
     # ---- pass 1: x0_i * b0 (t) and x0_i * b1 (s), the quotient chains threaded through ----
-    p1 = [tm(0), sm(0), tm(1)]
-    if not sq:
-        p1.append(f"v_mad_u64_u32 {TS}, vcc, {x1}, {B0(0)}, {TS}")
-    p1 += [tm(2), f"v_mul_lo_u32 {Q}, {TTLO}, %[np]", sm(1), tm(3), sm(2),
-           f"v_and_b32_dpp {Q}, {Q}, {MASKV} {dpp((0, 0, 0, 0))}", sm(3), tm(4),
-           f"v_sub_u32 {CQ}, {kreg}, {Q}", sm(4), tm(5),      # K'_i - q (>= 0: K'_i >= 2^29 - 1)
-           f"v_mad_u64_u32 {TS}, vcc, {CQ}, %[e0], {TS}", sm(5), tm(6),
-           f"v_mul_lo_u32 {Q2}, {TSLO}, %[np]", sm(6), tm(7), sm(7),
-           f"v_and_b32_dpp {Q2}, {Q2}, {MASKV} {dpp((0, 0, 0, 0))}", tm(8), sm(8)]
+    if g.G == 4:
+        Q, Q2, CQ, MASKV, TSLO, TTLO, TS = g.Q, g.Q2, g.CQ, g.MASKV, g.TSLO, g.TTLO, g.TS
+        p1 = [tm(0), sm(0), tm(1)]
+        if not sq:
+            p1.append(f"v_mad_u64_u32 {TS}, vcc, {x1}, {g.B0(0)}, {TS}")
+        p1 += [tm(2), f"v_mul_lo_u32 {Q}, {TTLO}, %[np]", sm(1), tm(3), sm(2),
+               f"v_and_b32_dpp {Q}, {Q}, {MASKV} {dpp((0, 0, 0, 0))}", sm(3), tm(4),
+               f"v_sub_u32 {CQ}, {kreg}, {Q}", sm(4), tm(5),      # K'_i - q (>= 0: K'_i >= 2^29 - 1)
+               f"v_mad_u64_u32 {TS}, vcc, {CQ}, %[e0], {TS}", sm(5), tm(6),
+               f"v_mul_lo_u32 {Q2}, {TSLO}, %[np]", sm(6), tm(7), sm(7),
+               f"v_and_b32_dpp {Q2}, {Q2}, {MASKV} {dpp((0, 0, 0, 0))}", tm(8), sm(8)]
+    else:
+        # the same chain with the broadcasts on the LDS pipe: lane 0 subtracts its own masked q;
+        # the others take the group's q from lane 0 by ds_bpermute (QB / Q2B, waited for below)
+        mads = [tm(0), sm(0), tm(1)] + ([] if sq else [f"v_mad_u64_u32 {g.TS}, vcc, {x1}, {g.B0(0)}, {g.TS}"])
+        rest = []
+        for r in range(2, M):
+            rest += [tm(r), sm(r - 1)]
+        rest.append(sm(M - 1))
+        chain = [f"v_mul_lo_u32 {g.Q}, {g.TTLO}, %[np]",
+                 f"v_and_b32 {g.Q}, {MASK}, {g.Q}",
+                 f"ds_bpermute_b32 {g.QB}, %[bp], {g.Q}",
+                 f"v_sub_u32 {g.CQ}, {kreg}, {g.Q}",
+                 f"v_mad_u64_u32 {g.TS}, vcc, {g.CQ}, %[e0], {g.TS}",
+                 f"v_mul_lo_u32 {g.Q2}, {g.TSLO}, %[np]",
+                 f"v_and_b32 {g.Q2}, {MASK}, {g.Q2}",
+                 f"ds_bpermute_b32 {g.Q2B}, %[bp], {g.Q2}"]
+        # chain step k after 3 (the first) / 2 .. 3 independent multiplies
+        gaps = [1, 2, 0, 2, 2, 3, 2, 0]
+        p1 = list(mads)
+        ri = 0
+        for k, ins in enumerate(chain):
+            take = gaps[k] if k else max(0, 3 - (len(mads) - 1))
+            p1 += rest[ri:ri + take]
+            ri += take
+            p1.append(ins)
+        p1 += rest[ri:]
+        p1.append("s_waitcnt lgkmcnt(1)")  # QB (the Q2B permute may still be in flight)
     # ---- pass 2: q * N (t), interleaved with x1_i * b0 (s, general product) ----
-    tq = [f"v_mad_u64_u32 {TT}, vcc, {Q}, {N(0)}, {TT}"] + \
-        [f"v_mad_u64_u32 {At(r - 1)}, vcc, {Q}, {N(r)}, {At(r - 1)}" for r in range(1, M)]
-    sx = [] if sq else [f"v_mad_u64_u32 {As(r - 1)}, vcc, {x1}, {B0(r)}, {As(r - 1)}" for r in range(1, M)]
+    tq = [f"v_mad_u64_u32 {g.TT}, vcc, {g.QB}, {N(0)}, {g.TT}"] + \
+        [f"v_mad_u64_u32 {g.At(r - 1)}, vcc, {g.QB}, {N(r)}, {g.At(r - 1)}" for r in range(1, M)]
+    sx = [] if sq else [f"v_mad_u64_u32 {g.As(r - 1)}, vcc, {x1}, {g.B0(r)}, {g.As(r - 1)}" for r in range(1, M)]
     p2 = []
     for k in range(max(len(tq), len(sx))):
         if k < len(tq):
@@ -254,30 +327,32 @@ def row(first, sq, kreg, xs, xn, pre_off):
             p2.append(sx[k])
     # ---- pass 3: q' * N (s), both retires threaded in:
     #      T = lo + c 2^29 -> lo (masked) to the lane below's top slot, c into the new slot 0 ----
-    sq3 = [f"v_mad_u64_u32 {TS}, vcc, {Q2}, {N(0)}, {TS}"] + \
-        [f"v_mad_u64_u32 {As(r - 1)}, vcc, {Q2}, {N(r)}, {As(r - 1)}" for r in range(1, M)]
-    ret_t = [f"v_and_b32_dpp {RTLO}, {TTLO}, {MASKV} {dpp((1, 2, 3, 0))}",
-             f"v_lshrrev_b64 {TT}, {LB}, {TT}",
-             f"v_lshl_add_u64 {At(0)}, {TT}, 0, {At(0)}"]
-    ret_s = [f"v_and_b32_dpp {RSLO}, {TSLO}, {MASKV} {dpp((1, 2, 3, 0))}",
-             f"v_lshrrev_b64 {TS}, {LB}, {TS}",
-             f"v_lshl_add_u64 {As(0)}, {TS}, 0, {As(0)}"]
-    p3 = [sq3[0], ret_t[0], sq3[1], ret_t[1], sq3[2], ret_t[2], sq3[3], ret_s[0], sq3[4], ret_s[1], sq3[5],
-          ret_s[2]] + sq3[6:]
+    sq3 = [f"v_mad_u64_u32 {g.TS}, vcc, {g.Q2B}, {N(0)}, {g.TS}"] + \
+        [f"v_mad_u64_u32 {g.As(r - 1)}, vcc, {g.Q2B}, {N(r)}, {g.As(r - 1)}" for r in range(1, M)]
+    ret_t = [g.down("v_and_b32_dpp", g.RTLO, g.TTLO, f", {g.MASKV}"),
+             f"v_lshrrev_b64 {g.TT}, {LB}, {g.TT}",
+             f"v_lshl_add_u64 {g.At(0)}, {g.TT}, 0, {g.At(0)}"]
+    ret_s = [g.down("v_and_b32_dpp", g.RSLO, g.TSLO, f", {g.MASKV}"),
+             f"v_lshrrev_b64 {g.TS}, {LB}, {g.TS}",
+             f"v_lshl_add_u64 {g.As(0)}, {g.TS}, 0, {g.As(0)}"]
+    p3 = [] if g.G == 4 else ["s_waitcnt lgkmcnt(0)"]
+    p3 += [sq3[0], ret_t[0], sq3[1], ret_t[1], sq3[2], ret_t[2], sq3[3], ret_s[0], sq3[4], ret_s[1], sq3[5],
+           ret_s[2]] + sq3[6:]
     return out + p1 + p2 + p3
 
 
-def mid_reduce():
+def mid_reduce(g):
     """After row 17: every slot keeps its low dword and hands the high one to the slot above
     (x 8 = 2^32 / 2^29); the top slot's (R) high dword goes to the lane above's slot 0
-    (lane 3's is 0: the window's value is below 2^1026).  Values drop below 2^36."""
+    (the top lane's is 0: the window's value is below 2^1026).  Values drop below 2^36."""
+    M = g.M
     chains = []
-    for acc, hi, rr, rhi, t in ((At, AtHi, RT, RTHI, T3), (As, AsHi, RS, RSHI, T4)):
+    for acc, hi, rr, rhi, t in ((g.At, g.AtHi, g.RT, g.RTHI, g.T3), (g.As, g.AsHi, g.RS, g.RSHI, g.T4)):
         ch = []
         for k in range(M - 2):
             ch += [f"v_mad_u64_u32 {acc(k + 1)}, vcc, {hi(k)}, 8, {acc(k + 1)}", f"v_mov_b32 {hi(k)}, 0"]
         ch += [f"v_mad_u64_u32 {rr}, vcc, {hi(M - 2)}, 8, {rr}", f"v_mov_b32 {hi(M - 2)}, 0",
-               f"v_mov_b32_dpp {t}, {rhi} {dpp((3, 0, 1, 2))}",
+               g.up(t, rhi),
                f"v_mov_b32 {rhi}, 0",
                f"v_mad_u64_u32 {acc(0)}, vcc, {t}, 8, {acc(0)}"]
         chains.append(ch)
@@ -287,14 +362,15 @@ def mid_reduce():
     return out
 
 
-def normalise_store():
-    """Window (slots 0..7 + R) -> 9 lazy 29-bit limbs per digit part, into the b registers
+def normalise_store(g):
+    """Window (slots 0..M-2 + R) -> M lazy 29-bit limbs per digit part, into the b registers
     (t -> b0, s -> b1), and the lane's slice of the LDS column.  The t and s carry chains are
     independent: interleaved instruction by instruction (a vcc add/addc pair kept together)."""
+    M = g.M
     chains = []
     for acc, lo, rr, rlo, breg, cy, cylo, cyhi, t1, t2 in (
-            (At, AtLo, RT, RTLO, B0, CY, CYLO, CYHI, TMP, TMP2),
-            (As, AsLo, RS, RSLO, B1, CS, CSLO, CSHI, T3, T4)):
+            (g.At, g.AtLo, g.RT, g.RTLO, g.B0, g.CY, g.CYLO, g.CYHI, g.TMP, g.TMP2),
+            (g.As, g.AsLo, g.RS, g.RSLO, g.B1, g.CS, g.CSLO, g.CSHI, g.T3, g.T4)):
         ch = [f"v_and_b32 {breg(0)}, {MASK}, {lo(0)}", f"v_lshrrev_b64 {cy}, {LB}, {acc(0)}"]
         for r in range(1, M - 1):
             ch += [f"v_lshl_add_u64 {acc(r)}, {cy}, 0, {acc(r)}",
@@ -303,9 +379,9 @@ def normalise_store():
         ch += [f"v_lshl_add_u64 {rr}, {cy}, 0, {rr}",
                f"v_and_b32 {breg(M - 1)}, {MASK}, {rlo}",
                f"v_lshrrev_b64 {cy}, {LB}, {rr}",
-               # carry-out -> the lane above (lane 0 receives lane 3's, which is 0)
-               f"v_mov_b32_dpp {t1}, {cylo} {dpp((3, 0, 1, 2))}",
-               f"v_mov_b32_dpp {t2}, {cyhi} {dpp((3, 0, 1, 2))}",
+               # carry-out -> the lane above (the group's lane 0 receives the top lane's, which is 0)
+               g.up(t1, cylo),
+               g.up(t2, cyhi),
                f"v_add_co_u32 {t1}, vcc, {t1}, {breg(0)}|v_addc_co_u32 {t2}, vcc, 0, {t2}, vcc",
                f"v_and_b32 {breg(0)}, {MASK}, {t1}",
                f"v_alignbit_b32 {t1}, {t2}, {t1}, {LB}",  # (t2:t1) >> 29 (< 2^10: fits)
@@ -316,10 +392,14 @@ def normalise_store():
         for ch in chains:
             if k < len(ch):
                 out += ch[k].split("|")
-    for d, breg in ((0, B0), (1, B1)):
-        out += [f"ds_write_b32 %[al], {breg(r)} offset:{(d * D1 + r) * ROWB}" for r in range(M)]
+    for d, breg in ((0, g.B0), (1, g.B1)):
+        out += [f"ds_write_b32 %[al], {breg(r)} offset:{(d * g.D1 + r) * g.ROWB}" for r in range(M)]
     out.append("s_waitcnt lgkmcnt(0)")
     return out
+
+
+KBASE = 64      # K'_i in s(64 + i)
+M0_SAVE = "s19"
 
 
 def krow(dst, m0_expr):
@@ -327,54 +407,55 @@ def krow(dst, m0_expr):
     return [m0_expr, "s_nop 1", f"s_movrels_b32 {dst}, s{KBASE}"]
 
 
-def pair(sq, first_x, second_x):
+def pair(g, sq, first_x, second_x):
     """Rows (i, i+1) with i = s34; operands of row i in first_x, of row i+1 in second_x."""
     body = krow("s35", "s_mov_b32 m0, s34") + krow("s36", "s_add_u32 m0, s34, 1")
-    body += row(False, sq, "s35", first_x, second_x, ROWB)
+    body += row(g, False, sq, "s35", first_x, second_x, g.ROWB)
     body += ["s_waitcnt lgkmcnt(0)"]
-    body += row(False, sq, "s36", second_x, first_x, 2 * ROWB)
-    body += [f"v_add_u32 {AADR}, {2 * ROWB}, {AADR}", "s_waitcnt lgkmcnt(0)"]
+    body += row(g, False, sq, "s36", second_x, first_x, 2 * g.ROWB)
+    body += [f"v_add_u32 {g.AADR}, {2 * g.ROWB}, {g.AADR}", "s_waitcnt lgkmcnt(0)"]
     return body
 
 
-def product(sq):
+def product(sq, g=QUAD):
     e = Emitter()
+    XA, XB = g.XA, g.XB
     e.extend([f"s_mov_b32 {M0_SAVE}, m0"] + load_consts())
-    e.extend(load_b_lds(True) if sq else load_b_global())
-    e.extend([f"v_mov_b32 {RTHI}, 0", f"v_mov_b32 {RSHI}, 0", f"v_mov_b32 {MASKV}, {MASK}",
-              f"v_mov_b32 {AADR}, %[ac]", f"ds_read_b32 {XA[0]}, {AADR}"])
+    e.extend(load_b_lds(g, True) if sq else load_b_global(g))
+    e.extend([f"v_mov_b32 {g.RTHI}, 0", f"v_mov_b32 {g.RSHI}, 0", f"v_mov_b32 {g.MASKV}, {MASK}",
+              f"v_mov_b32 {g.AADR}, %[ac]", f"ds_read_b32 {XA[0]}, {g.AADR}"])
     if not sq:
-        e.emit(f"ds_read_b32 {XA[1]}, {AADR} offset:{D1 * ROWB}")
+        e.emit(f"ds_read_b32 {XA[1]}, {g.AADR} offset:{g.D1 * g.ROWB}")
     e.emit("s_waitcnt vmcnt(0) lgkmcnt(0)")
     # row 0 (even: XA), prefetch row 1 into XB
-    e.extend(row(True, sq, f"s{KBASE}", XA, XB, ROWB))
-    e.extend([f"v_add_u32 {AADR}, {ROWB}, {AADR}", "s_waitcnt lgkmcnt(0)"])
+    e.extend(row(g, True, sq, f"s{KBASE}", XA, XB, g.ROWB))
+    e.extend([f"v_add_u32 {g.AADR}, {g.ROWB}, {g.AADR}", "s_waitcnt lgkmcnt(0)"])
     # rows 1..16: pairs (odd XB, even XA)
-    e.extend(["s_mov_b32 s34, 1", "1:"] + pair(sq, XB, XA) +
+    e.extend(["s_mov_b32 s34, 1", "1:"] + pair(g, sq, XB, XA) +
              ["s_add_u32 s34, s34, 2", f"s_cmp_lg_u32 s34, {MID - 1}", "s_cbranch_scc1 1b"])
     # row 17 (odd: XB), prefetch row 18 into XA
-    e.extend(row(False, sq, f"s{KBASE + MID - 1}", XB, XA, ROWB))
-    e.extend([f"v_add_u32 {AADR}, {ROWB}, {AADR}"])
-    e.extend(mid_reduce())
+    e.extend(row(g, False, sq, f"s{KBASE + MID - 1}", XB, XA, g.ROWB))
+    e.extend([f"v_add_u32 {g.AADR}, {g.ROWB}, {g.AADR}"])
+    e.extend(mid_reduce(g))
     e.emit("s_waitcnt lgkmcnt(0)")
     # rows 18..35: pairs (even XA, odd XB)
-    e.extend([f"s_mov_b32 s34, {MID}", "2:"] + pair(sq, XA, XB) +
+    e.extend([f"s_mov_b32 s34, {MID}", "2:"] + pair(g, sq, XA, XB) +
              ["s_add_u32 s34, s34, 2", f"s_cmp_lg_u32 s34, {L}", "s_cbranch_scc1 2b"])
-    e.extend(normalise_store())
+    e.extend(normalise_store(g))
     e.extend([f"s_mov_b32 m0, {M0_SAVE}", "s_nop 1"])
     return e.out
 
 
-def row_mads(sq):
-    return sum(1 for ln in row(False, sq, "s35", XA, XB, ROWB) if ln.startswith("v_mad_u64_u32"))
+def row_mads(sq, g=QUAD):
+    return sum(1 for ln in row(g, False, sq, "s35", g.XA, g.XB, g.ROWB) if ln.startswith("v_mad_u64_u32"))
 
 
-def product_mads(sq):
-    return L * row_mads(sq) + sum(1 for ln in mid_reduce() if ln.startswith("v_mad_u64_u32"))
+def product_mads(sq, g=QUAD):
+    return L * row_mads(sq, g) + sum(1 for ln in mid_reduce(g) if ln.startswith("v_mad_u64_u32"))
 
 
-def clobbers():
-    regs = [f'"v{i}"' for i in range(NREG)]
+def clobbers(g):
+    regs = [f'"v{i}"' for i in range(g.NREG)]
     regs += [f'"s{i}"' for i in [19, 34, 35, 36] + list(range(KBASE, KBASE + L))]
     out = [", ".join(regs[i:i + 16]) for i in range(0, len(regs), 16)]
     return " \\\n  ".join(x + "," for x in out[:-1]) + " \\\n  " + out[-1]
@@ -384,66 +465,83 @@ def c_string(lines):
     return "\n".join(f'  "{ln}\\n"' for ln in lines)
 
 
-OPERANDS = ", ".join([f'[n{r}] "v"(n[{r}])' for r in range(M)])
-
-
-def main():
-    mm, sq = product(False), product(True)
-    hdr = f"""// GENERATED by tools/gen_quad_asm.py -- do not edit by hand.
+def header(g, pfx, PFX, name):
+    M = g.M
+    mm, sq = product(False, g), product(True, g)
+    operands = ", ".join([f'[n{r}] "v"(n[{r}])' for r in range(M)])
+    bp_doc, bp_arg, bp_op = "", "", ""
+    if g.G == 3:
+        bp_doc = ("\n// bp: ds_bpermute byte address of the group's lane 0 (4 * (3 * (lane / 3)), the dummy lane 63\n"
+                  "// its own).")
+        bp_arg = ", uint32_t bp"
+        bp_op = ', [bp] "v"(bp)'
+    dpp_word = "DPP quad_perm" if g.G == 4 else "ds_bpermute broadcasts, DPP wave shifts"
+    return f"""// GENERATED by tools/gen_quad_asm.py -- do not edit by hand.
 //
-// gfx950 assembly N-adic Montgomery product modulo N^2 over a QUAD of lanes (4 lanes per
-// ciphertext, lane l owns limbs 9 l .. 9 l + 8 of both 36-limb digits, radix 2^29,
-// R = 2^1044): the LDS column a <- a * b * R^-1 (mod N^2), digits lazily < 2N.
+// gfx950 assembly N-adic Montgomery product modulo N^2 over a {name} of lanes ({g.G} lanes per
+// ciphertext, lane l owns limbs {M} l .. {M} l + {M - 1} of both 36-limb digits, radix 2^29,
+// R = 2^1044; {dpp_word}): the LDS column a <- a * b * R^-1 (mod N^2), digits lazily < 2N.
 // See tools/gen_quad_asm.py for the layout, the cross-lane steps and the bounds.
 // {len(mm)} instructions (general, B from global), {len(sq)} (square); per lane and row
-// {row_mads(False)} / {row_mads(True)} v_mad_u64_u32 -> {product_mads(False)} / {product_mads(True)} per product.
+// {row_mads(False, g)} / {row_mads(True, g)} v_mad_u64_u32 -> {product_mads(False, g)} / {product_mads(True, g)} per product.
 #pragma once
 #include <stdint.h>
 
-#define FBM_QA_LB {LB}
-#define FBM_QA_L {L}
-#define FBM_QA_LIMBS {M}
-#define FBM_QA_ROWW {ROWW}
-#define FBM_QA_ROWB {ROWB}
-#define FBM_QA_D1 {D1}
-#define FBM_QA_MADS_MUL {product_mads(False)}
-#define FBM_QA_MADS_SQR {product_mads(True)}
+#define FBM_{PFX}_LB {LB}
+#define FBM_{PFX}_L {L}
+#define FBM_{PFX}_LIMBS {M}
+#define FBM_{PFX}_ROWW {g.ROWW}
+#define FBM_{PFX}_ROWB {g.ROWB}
+#define FBM_{PFX}_D1 {g.D1}
+#define FBM_{PFX}_MADS_MUL {product_mads(False, g)}
+#define FBM_{PFX}_MADS_SQR {product_mads(True, g)}
 
-#define FBM_QA_CLOBBERS \\
-  {clobbers()}
+#define FBM_{PFX}_CLOBBERS \\
+  {clobbers(g)}
 
-// n: the lane's 9 limbs of N (N_(9 l + r)); e0 = (lane % 4 == 0); ac: LDS byte address of the
-// ciphertext column (limb 0 of digit 0), al = ac + 9 l * ROWB; QK: the quad constants block
-// (K'_i = 2^29 - 1 + K_i, K = (1 - R) mod N, at words 0..35); np = -N^-1 mod 2^29.
+// n: the lane's {M} limbs of N (N_({M} l + r)); e0 = (lane is the group's lane 0); ac: LDS byte address
+// of the ciphertext column (limb 0 of digit 0), al = ac + {M} l * ROWB; QK: the quad constants block
+// (K'_i = 2^29 - 1 + K_i, K = (1 - R) mod N, at words 0..35); np = -N^-1 mod 2^29.{bp_doc}
 
-// B from global memory, quad layout: limb row j (b0: j = r, b1: j = 9 + r) at
+// B from global memory, table layout: limb row j (b0: j = r, b1: j = {M} + r) at
 // bb + b_off + j * 1024 (bytes; bb uniform, b_off the lane's offset).
-__device__ __forceinline__ void fbm_qa_mm_glb(uint32_t ac, uint32_t al, const uint32_t* bb, uint32_t b_off,
+__device__ __forceinline__ void fbm_{pfx}_mm_glb(uint32_t ac, uint32_t al, const uint32_t* bb, uint32_t b_off,
                                               const uint32_t* QK, uint32_t np, const uint32_t (&n)[{M}],
-                                              uint32_t e0) {{
+                                              uint32_t e0{bp_arg}) {{
   asm volatile(
 {c_string(mm)}
       :
-      : [ac] "v"(ac), [al] "v"(al), [b] "v"(b_off), [bb] "s"(bb), [QK] "s"(QK), [np] "s"(np), [e0] "v"(e0),
-        {OPERANDS}
-      : "memory", "vcc", "scc", FBM_QA_CLOBBERS);
+      : [ac] "v"(ac), [al] "v"(al), [b] "v"(b_off), [bb] "s"(bb), [QK] "s"(QK), [np] "s"(np), [e0] "v"(e0){bp_op},
+        {operands}
+      : "memory", "vcc", "scc", FBM_{PFX}_CLOBBERS);
 }}
 
 // a <- a^2 R^-1 (mod N^2): B = A from the LDS column (the s part as x0 * (2 x1)).
-__device__ __forceinline__ void fbm_qa_sq_lds(uint32_t ac, uint32_t al, const uint32_t* QK, uint32_t np,
-                                              const uint32_t (&n)[{M}], uint32_t e0) {{
+__device__ __forceinline__ void fbm_{pfx}_sq_lds(uint32_t ac, uint32_t al, const uint32_t* QK, uint32_t np,
+                                              const uint32_t (&n)[{M}], uint32_t e0{bp_arg}) {{
   asm volatile(
 {c_string(sq)}
       :
-      : [ac] "v"(ac), [al] "v"(al), [QK] "s"(QK), [np] "s"(np), [e0] "v"(e0),
-        {OPERANDS}
-      : "memory", "vcc", "scc", FBM_QA_CLOBBERS);
+      : [ac] "v"(ac), [al] "v"(al), [QK] "s"(QK), [np] "s"(np), [e0] "v"(e0){bp_op},
+        {operands}
+      : "memory", "vcc", "scc", FBM_{PFX}_CLOBBERS);
 }}
-"""
-    with open(OUT, "w") as f:
-        f.write(hdr)
-    print(f"wrote {OUT}: general {len(mm)} / square {len(sq)} instructions; mads/row {row_mads(False)} / "
-          f"{row_mads(True)}")
+""", mm, sq
+
+
+# module-level names kept for tests/test_quad_asm.py (the quad geometry)
+M, ROWW, ROWB, D1 = QUAD.M, QUAD.ROWW, QUAD.ROWB, QUAD.D1
+
+
+def main():
+    for g, pfx, PFX, name, fn in ((QUAD, "qa", "QA", "QUAD", "fbm_quad_asm.hpp"),
+                                  (TRI, "ta", "TA", "TRIPLE", "fbm_tri_asm.hpp")):
+        hdr, mm, sq = header(g, pfx, PFX, name)
+        out = os.path.join(ROOT, "fedbiomed_amd", "csrc", fn)
+        with open(out, "w") as f:
+            f.write(hdr)
+        print(f"wrote {out}: general {len(mm)} / square {len(sq)} instructions; mads/row {row_mads(False, g)} / "
+              f"{row_mads(True, g)}; {g.NREG} VGPRs")
 
 
 if __name__ == "__main__":
