@@ -31,6 +31,12 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# The step runs the P + 1 exponentiations on P + 1 HIP streams; HIP maps streams onto FIFO
+# hardware queues (4 per process by default), so with 4 queues at most 4 launches run at once
+# and the rest wait behind them.  16 queues (set before the runtime starts; the pool allows up
+# to 32): 1/8-stripe step 183-186 -> 168-175 ms, 10M step 1174-1176 -> 1155-1158 ms (A/B on one
+# box, tools/ab_hwq.sh, profiles/r2_hwq_ab.txt).  An explicit setting in the environment wins.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MAD_PEAK_TOPS = 36.48        # measured v_mad_u64_u32 peak, whole chip, best occupancy (tools/microbench/madpeak.hip,

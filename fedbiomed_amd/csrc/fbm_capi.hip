@@ -300,7 +300,12 @@ static void build_quad(const Big& N, const Big& M, QuadCtx& qa) {
   qa.np = (0u - inv) & ((1u << LB) - 1u);
 }
 
-static int build_jl_params(const uint32_t* biprime, int es, int cr, uint64_t tau, uint64_t ct_offset, JlParams& jp) {
+// The modulus-dependent part of JlParams (Montgomery / N-adic / group-engine constants, N^-1
+// mod 2^1024, the FDH midstate): ~0.3 ms of host big-integer work per call, so it is built once
+// per biprime and kept in a small process-wide cache (a round's encrypts and aggregate, and
+// every round of an experiment, share one biprime).
+static int build_jl_params_uncached(const uint32_t* biprime, int es, int cr, uint64_t tau, uint64_t ct_offset,
+                                    JlParams& jp) {
   memset(&jp, 0, sizeof(jp));
   Big N(biprime, biprime + 32);
   const int nb = big_bits(N);
@@ -374,6 +379,78 @@ static int build_jl_params(const uint32_t* biprime, int es, int cr, uint64_t tau
   for (int b = 0; b < 14; ++b) fbm_sha256_compress(st, W);
   memcpy(jp.mid, st, sizeof(st));
   return FBM_OK;
+}
+
+struct JlParamsCacheEntry {
+  uint32_t n32[32];
+  JlParams jp;
+};
+static std::mutex g_jp_mu;
+static std::vector<JlParamsCacheEntry> g_jp_cache;  // most recently used last, at most 8
+
+static int build_jl_params(const uint32_t* biprime, int es, int cr, uint64_t tau, uint64_t ct_offset, JlParams& jp) {
+  if (es < 1 || cr < 1 || es > 100 || (int64_t)es * cr > 1024) {
+    set_error("invalid VES parameters es=%d cr=%d", es, cr);
+    return FBM_E_ARG;
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_jp_mu);
+    for (size_t i = 0; i < g_jp_cache.size(); ++i) {
+      if (memcmp(g_jp_cache[i].n32, biprime, sizeof(g_jp_cache[i].n32)) == 0) {
+        JlParamsCacheEntry e = g_jp_cache[i];
+        g_jp_cache.erase(g_jp_cache.begin() + i);
+        g_jp_cache.push_back(e);
+        jp = e.jp;
+        jp.es = es;
+        jp.cr = cr;
+        jp.tau = tau;
+        jp.ct_offset = ct_offset;
+        jp.key_is_zero = 0;
+        return FBM_OK;
+      }
+    }
+  }
+  const int rc = build_jl_params_uncached(biprime, es, cr, tau, ct_offset, jp);
+  if (rc) return rc;
+  JlParamsCacheEntry e;
+  memcpy(e.n32, biprime, sizeof(e.n32));
+  e.jp = jp;
+  std::lock_guard<std::mutex> lk(g_jp_mu);
+  if (g_jp_cache.size() >= 8) g_jp_cache.erase(g_jp_cache.begin());
+  g_jp_cache.push_back(e);
+  return FBM_OK;
+}
+
+// R^(P+1) mod N^2 in 28-bit limbs (the ciphertext product's first operand), cached per (N, P)
+struct JlRkCacheEntry {
+  uint32_t n32[32];
+  int parties;
+  JlRk rk;
+};
+static std::vector<JlRkCacheEntry> g_rk_cache;  // guarded by g_jp_mu, at most 16
+
+static void jl_rk_for(const uint32_t* n32, int n_parties, JlRk& r) {
+  {
+    std::lock_guard<std::mutex> lk(g_jp_mu);
+    for (const JlRkCacheEntry& e : g_rk_cache)
+      if (e.parties == n_parties && memcmp(e.n32, n32, sizeof(e.n32)) == 0) {
+        r = e.rk;
+        return;
+      }
+  }
+  Big M(n32, n32 + 32);
+  M = big_mul(M, M);
+  M.resize(64);
+  const Big rk = big_pow2_mod_mont((uint64_t)(n_parties + 1) * FBM_NL * FBM_LB, M);
+  memset(&r, 0, sizeof(r));
+  to28_host(rk, r.w, FBM_NL);
+  JlRkCacheEntry e;
+  memcpy(e.n32, n32, sizeof(e.n32));
+  e.parties = n_parties;
+  e.rk = r;
+  std::lock_guard<std::mutex> lk(g_jp_mu);
+  if (g_rk_cache.size() >= 16) g_rk_cache.erase(g_rk_cache.begin());
+  g_rk_cache.push_back(e);
 }
 
 // Left-to-right sliding window (width FBM_WIN) over |key|, odd-power table.
@@ -831,13 +908,8 @@ static int jl_combine_impl(const uint32_t* cts, int n_parties, uint64_t n_ct, in
   memset(&none, 0, sizeof(none));
   if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, none, w.ops, w.cst, s); }))) return rc;
   {  // R^(P+1) mod N^2: the product's uniform first operand (P + 1 products each drop one R)
-    Big M(jp.N32, jp.N32 + 32);
-    M = big_mul(M, M);
-    M.resize(64);
-    const Big rk = big_pow2_mod_mont((uint64_t)(n_parties + 1) * FBM_NL * FBM_LB, M);
     JlRk r;
-    memset(&r, 0, sizeof(r));
-    to28_host(rk, r.w, FBM_NL);
+    jl_rk_for(jp.N32, n_parties, r);
     if ((rc = timed("jl_rk", s, [&] { return launch_jl_rk(r, w.cst, s); }))) return rc;
   }
   if ((rc = timed("jl_prod", s, [&] { return launch_jl_prod(cts, n_parties, n_ct, jp, w.cst, factor, w.X, w.xs, s); })))
