@@ -125,6 +125,9 @@ def parse():
                     help="JL: issue each party's encrypt whole (prologue and exponentiation back to back)")
     ap.add_argument("--streams", type=int, default=0,
                     help="HIP streams for the parties' encrypts (0 = one per party); the decryption factor has its own")
+    ap.add_argument("--no-batch-exp", action="store_true",
+                    help="JL: one exponentiation launch per party (+ the factor's) on its own stream instead of "
+                         "one batched launch over all of them (D.jl_exp_batch)")
     ap.add_argument("--serial", action="store_true",
                     help="no per-party streams in the timed steps (rocprof passes: per-kernel times unconfounded)")
     return ap.parse_args()
@@ -211,6 +214,7 @@ def main():
 
     factor_stream = torch.cuda.Stream(device=dev)
     overlap_factor = not args.no_factor_overlap
+    batch_exp = not args.no_batch_exp and not args.no_prologue_first
 
     def engine_ctx(mode):
         """JL exponentiation engine for the launches issued inside (library policy otherwise):
@@ -260,15 +264,25 @@ def main():
                         main.wait_stream(st)
                     for st in pool + [factor_stream]:
                         st.wait_stream(main)
-                if overlap_factor:
-                    with torch.cuda.stream(f_s):
-                        pf.exponentiate()
-                for p in range(P):
-                    with torch.cuda.stream(main if serial else streams[p]):
-                        cts[p] = pend[p].finish()
-                if overlap_factor:
-                    with torch.cuda.stream(f_s):
+                if batch_exp and not serial:
+                    # one launch over every party's ciphertexts and the factor's, on `main`
+                    with D.jl_exp_batch(dev):
+                        if overlap_factor:
+                            pf.exponentiate()
+                        for p in range(P):
+                            cts[p] = pend[p].finish()
+                    if overlap_factor:
                         factor = pf.finish()
+                else:
+                    if overlap_factor:
+                        with torch.cuda.stream(f_s):
+                            pf.exponentiate()
+                    for p in range(P):
+                        with torch.cuda.stream(main if serial else streams[p]):
+                            cts[p] = pend[p].finish()
+                    if overlap_factor:
+                        with torch.cuda.stream(f_s):
+                            factor = pf.finish()
         if not serial:
             for st in pool + [factor_stream]:
                 main.wait_stream(st)
@@ -408,9 +422,14 @@ def main():
                         main.wait_stream(st)
                     for st in pool:
                         st.wait_stream(main)
-                    for p in range(P):
-                        with torch.cuda.stream(streams[p]):
-                            cts[p] = pend[p].finish()
+                    if batch_exp:
+                        with D.jl_exp_batch(dev):
+                            for p in range(P):
+                                cts[p] = pend[p].finish()
+                    else:
+                        for p in range(P):
+                            with torch.cuda.stream(streams[p]):
+                                cts[p] = pend[p].finish()
                 for st in pool:
                     main.wait_stream(st)
                 for c in cts:

@@ -488,10 +488,63 @@ def jl_chunk_ct() -> int:
     return max(1, min(v, JL_MAX_CT))
 
 
+class jl_exp_batch:
+    """Within this context the JL exponentiations of PendingEncrypt.finish() (non-negative key)
+    and PendingFactor.exponentiate() are recorded, not launched; at exit ONE launch runs them all
+    on the current stream (fbm_jl_batch_begin / fbm_jl_batch_flush): one chunk counter over every
+    party's ciphertexts, so the chip's rounds pack whatever the parts' sizes and however the
+    streams map onto the hardware queues.  The recorded calls' prologues must be complete on the
+    current stream at exit (wait on their streams first) and their outputs are valid after it;
+    the same biprime throughout; at most 24 calls.  A factor's inverse (PendingFactor.finish)
+    goes after the context.
+
+        with D.jl_exp_batch():
+            cts = [pend[p].finish() for p in range(P)]
+            pf.exponentiate()
+        factor = pf.finish()
+    """
+
+    _tls = threading.local()
+
+    def __init__(self, dev=None):
+        self._dev, self._keep = dev, []
+
+    @staticmethod
+    def active() -> Optional["jl_exp_batch"]:
+        return getattr(jl_exp_batch._tls, "cur", None)
+
+    def keep(self, tensors) -> None:
+        """device tensors a recorded call reads or writes (kept alive until the launch, then
+        marked as used on the launch stream for the caching allocator)"""
+        self._keep += [t for t in tensors if isinstance(t, torch.Tensor) and t.is_cuda]
+
+    def __enter__(self):
+        if jl_exp_batch.active() is not None:
+            raise RuntimeError("jl_exp_batch contexts do not nest")
+        _call(N.load().fbm_jl_batch_begin)
+        jl_exp_batch._tls.cur = self
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        jl_exp_batch._tls.cur = None
+        lib = N.load()
+        if exc_type is not None:
+            lib.fbm_jl_batch_abort()
+            return False
+        ws = torch.empty(int(lib.fbm_jl_batch_workspace()), dtype=torch.uint8, device=self._dev or device())
+        _call(lib.fbm_jl_batch_flush, _ptr(ws), ws.numel(), _stream())
+        cur = torch.cuda.current_stream(ws.device)
+        for t in self._keep:
+            t.record_stream(cur)
+        self._keep = []
+        return False
+
+
 class PendingEncrypt:
     """A JL encrypt whose prologue kernels are issued and whose exponentiation is not yet
     (jl_encrypt(..., defer_exp=True)); finish() issues it on the current stream and returns
-    the ciphertext tensor.  Holds the workspace and the status word until then."""
+    the ciphertext tensor (inside a jl_exp_batch: records it for the batch's launch).  Holds
+    the workspace and the status word until then."""
 
     def __init__(self, args, ct, ws, st):
         self._args, self._ct, self._ws, self._st = args, ct, ws, st
@@ -499,6 +552,9 @@ class PendingEncrypt:
     def finish(self) -> torch.Tensor:
         if self._args is not None:
             _call(N.load().fbm_jl_encrypt_phase, *self._args, _stream(), 2)
+            b = jl_exp_batch.active()
+            if b is not None:
+                b.keep([self._ct, *self._ws])
             _check_stats_or_defer(self._st)
             self._args = None
         return self._ct
@@ -560,6 +616,9 @@ class PendingFactor:
         if not self._done & bit:
             _call(N.load().fbm_jl_decrypt_factor_phase, *self._args, _stream(), bit)
             self._done |= bit
+            b = jl_exp_batch.active()
+            if b is not None:
+                b.keep([self._f, *self._keep])
 
     def exponentiate(self) -> "PendingFactor":
         self._phase(2)

@@ -52,6 +52,10 @@ SIGNATURES = {
     "fbm_jl_triple_mads": (c_int, [c_int]),
     "fbm_jl_set_engine": (c_int, [c_int]),
     "fbm_jl_engine_for": (c_int, [c_u64]),
+    "fbm_jl_batch_begin": (c_int, []),
+    "fbm_jl_batch_abort": (None, []),
+    "fbm_jl_batch_workspace": (c_u64, []),
+    "fbm_jl_batch_flush": (c_int, [c_vp, c_u64, c_vp]),
     "fbm_last_error": (ctypes.c_char_p, []),
     "fbm_check_stats": (c_int, [c_vp, c_int, c_vp]),
     "fbm_lom_protect": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_vp, c_vp, c_int, c_int,

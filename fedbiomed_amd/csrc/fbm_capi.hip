@@ -810,7 +810,11 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
       return rc;
     return timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, cst, Hinv, Y, nude, ct_out, stats, s); });
   }
-  return timed("jl_exp", s, [&] { return launch_jl_exp(H, n_ct, jp, sc, 0, nude, table, slots, ops, cst, ct_out, s); });
+  // a phase-2-only call inside an open batch (fbm_jl_batch_begin) is recorded, not launched
+  const bool acc = jl_batch_accept(phase == 2);
+  rc = timed("jl_exp", s, [&] { return launch_jl_exp(H, n_ct, jp, sc, 0, nude, table, slots, ops, cst, ct_out, s); });
+  jl_batch_accept(acc);
+  return rc;
 }
 
 int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
@@ -884,13 +888,20 @@ static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t
     if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, w.ops, w.cst, s); }))) return rc;
     if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, w.H, stats, s); }))) return rc;
   }
-  if ((phase & 2) &&
-      (rc = timed("jl_exp", s, [&] {
-         // the inverse starts from the power's N-adic digits (no division by N needed)
-         return launch_jl_exp(w.H, n_ct, jp, sc, FBM_EXP_DEC | (inv ? FBM_EXP_OUT_NADIC : 0), nullptr, w.table, w.slots,
-                              w.ops, w.cst, E, s);
-       })))
-    return rc;
+  if (phase & 2) {
+    const bool acc = jl_batch_accept(phase == 2);  // recorded inside an open batch
+    rc = timed("jl_exp", s, [&] {
+      // the inverse starts from the power's N-adic digits (no division by N needed)
+      return launch_jl_exp(w.H, n_ct, jp, sc, FBM_EXP_DEC | (inv ? FBM_EXP_OUT_NADIC : 0), nullptr, w.table, w.slots,
+                           w.ops, w.cst, E, s);
+    });
+    jl_batch_accept(acc);
+    if (rc) return rc;
+  }
+  if ((phase & 4) && inv && jl_batch_active()) {
+    set_error("the decryption factor's inverse needs its exponentiation: flush the open batch first");
+    return FBM_E_ARG;
+  }
   if ((phase & 4) && inv &&
       (rc = timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, w.cst, E, w.xs, nullptr, factor, stats, s); })))  // xs: y scratch
     return rc;
@@ -1005,6 +1016,17 @@ int fbm_jl_aggregate_factor(const uint32_t* cts, int n_parties, uint64_t n_ct, i
   }
   return jl_combine_impl(cts, n_parties, n_ct, es, cr, n_out, biprime, factor, total_weight, neg_clip, step, out, sums,
                          agg_ws(workspace, n_ct), stats, s);
+}
+
+int fbm_jl_batch_begin(void) { return jl_batch_begin(); }
+
+void fbm_jl_batch_abort(void) { jl_batch_abort(); }
+
+uint64_t fbm_jl_batch_workspace(void) { return jl_batch_workspace(); }
+
+int fbm_jl_batch_flush(void* workspace, uint64_t workspace_bytes, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  return timed("jl_exp", s, [&] { return jl_batch_flush(workspace, workspace_bytes, s); });
 }
 
 int fbm_test_fdh_gcd(const uint32_t* r8, const uint32_t* n32, uint32_t* err) {

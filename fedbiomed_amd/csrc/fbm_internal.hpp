@@ -140,6 +140,30 @@ int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, int ne
                    hipStream_t s);
 int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s);
 int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32_t* cst, hipStream_t s);
+// one exponentiation launch over several calls' ciphertexts (jl_exp_kernel<true> segments)
+#define FBM_EXP_MAXSEG 24
+struct JlExpSeg {
+  const uint32_t* H;
+  const uint32_t* nude;
+  uint32_t* out;
+  const uint32_t* ops;
+  uint64_t n_ct;
+  uint32_t chunk0;  // first chunk of this segment in the launch's chunk sequence
+  int n_ops, first, mode, key_is_zero;
+};
+struct JlExpBatch {
+  int nseg;
+  uint32_t total_chunks;
+  JlExpSeg seg[FBM_EXP_MAXSEG];
+};
+// batch mode (per thread): while a batch is open, the exponentiation of a phase-2-only call
+// (jl_batch_accept(true) around it) is recorded instead of launched; flush launches them all
+int jl_batch_begin();
+void jl_batch_abort();
+bool jl_batch_accept(bool on);
+bool jl_batch_active();
+uint64_t jl_batch_workspace();
+int jl_batch_flush(void* workspace, uint64_t ws_bytes, hipStream_t s);
 int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const JlSched& sc, int mode,
                   const uint32_t* nude, uint32_t* table, uint64_t table_slots, const uint32_t* ops,
                   const uint32_t* cst, uint32_t* out, hipStream_t s);

@@ -494,13 +494,38 @@ __device__ __forceinline__ void na_final(const uint32_t* lds, const uint32_t* NK
 // h < 2^1036 (one FDH digest: always, for a 1024-bit N) IS the digit pair (h, 0); a wider h
 // (FDH retries, small moduli) enters as h_lo R + h_hi R^2 (one more product, that wave only).
 // Lanes past n_ct (last chunk) redo the last ciphertext and store nothing.
-__global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __restrict__ H, uint64_t n_ct,
+//
+// BATCH: one launch over several SEGMENTS (the exponentiations of several parties' encrypts and
+// the decryption factor, same biprime; JlExpSeg table in device memory): the chunks of all
+// segments are pulled from one counter, so the launch packs the chip's rounds whatever the
+// segments' sizes.  A chunk never spans two segments.  A segment's fields are re-read from the
+// table (scalar values) where they are used rather than held across the products, as the plain
+// kernel's arguments are.
+template <typename T>
+__device__ __forceinline__ T uniform_val(T v) {  // a wave-uniform value as a scalar (SGPR) value
+  if constexpr (sizeof(T) == 8) {
+    uint64_t u;
+    __builtin_memcpy(&u, &v, 8);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32));
+    u = ((uint64_t)hi << 32) | (uint64_t)lo;  // (readfirstlane returns int: no sign extension)
+    __builtin_memcpy(&v, &u, 8);
+    return v;
+  } else {
+    return (T)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  }
+}
+
+template <bool BATCH>
+__global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __restrict__ H_a, uint64_t n_ct_a,
                                                              uint32_t* __restrict__ cst, uint32_t np,
-                                                             const uint32_t* __restrict__ ops, int n_ops,
-                                                             int first, int mode, int key_is_zero,
-                                                             const uint32_t* __restrict__ nude,
+                                                             const uint32_t* __restrict__ ops_a, int n_ops_a,
+                                                             int first_a, int mode_a, int key_is_zero_a,
+                                                             const uint32_t* __restrict__ nude_a,
                                                              uint32_t* __restrict__ table,
-                                                             uint32_t* __restrict__ out) {
+                                                             uint32_t* __restrict__ out_a,
+                                                             const JlExpSeg* __restrict__ segs, int nseg,
+                                                             uint32_t total_chunks, uint32_t* __restrict__ ctr) {
   __shared__ uint32_t lds_a[(FBM_NL + 1) * FBM_BLOCK];
   __shared__ uint32_t chunk_s;
   const int tid = threadIdx.x;
@@ -510,29 +535,39 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
   // byte offset of this lane's table entry 0 (entries FBM_NL*256 words apart)
   const uint32_t tb0 = (uint32_t)(((uint64_t)blockIdx.x * FBM_TENTRIES * FBM_NL * FBM_BLOCK + tid) * 4);
   const uint32_t tstride = FBM_NL * FBM_BLOCK * 4;
-  const uint32_t n_chunks = (uint32_t)((n_ct + FBM_BLOCK - 1) / FBM_BLOCK);
+  const uint32_t n_chunks = BATCH ? total_chunks : (uint32_t)((n_ct_a + FBM_BLOCK - 1) / FBM_BLOCK);
+  uint32_t* counter = BATCH ? ctr : cst + FBM_CST_CTR;
   // Persistent workgroups pull 256-ciphertext chunks from a counter (zeroed by
-  // jl_setup_kernel): a workgroup leaves as soon as the chunks run out, so the tail of
-  // one launch leaves CUs free for a concurrent launch on another stream (the parties'
-  // encrypts), instead of every workgroup idling through a partial last round.
+  // jl_setup_kernel / before the batch launch): a workgroup leaves as soon as the chunks run
+  // out, so the tail of one launch leaves CUs free for a concurrent launch on another stream
+  // (the parties' encrypts), instead of every workgroup idling through a partial last round.
 #pragma unroll 1
   for (;;) {
-    if (tid == 0) chunk_s = atomicAdd(cst + FBM_CST_CTR, 1u);
+    if (tid == 0) chunk_s = atomicAdd(counter, 1u);
     __syncthreads();
     const uint32_t chunk = __builtin_amdgcn_readfirstlane(chunk_s);
     __syncthreads();
     if (chunk >= n_chunks) break;
-    const uint64_t ct_raw = (uint64_t)chunk * FBM_BLOCK + tid;
+    int si = 0;
+    if (BATCH) {
+#pragma unroll 1
+      for (int i = 1; i < nseg; ++i)
+        if (chunk >= uniform_val(segs[i].chunk0)) si = i;
+      si = __builtin_amdgcn_readfirstlane(si);
+    }
+#define SEG(f, a) (BATCH ? uniform_val(launder_s(segs)[si].f) : a)
+    const uint64_t n_ct = SEG(n_ct, n_ct_a);
+    const uint64_t ct_raw = (uint64_t)(chunk - (BATCH ? uniform_val(segs[si].chunk0) : 0u)) * FBM_BLOCK + tid;
     const bool valid = ct_raw < n_ct;
     const uint64_t ct = valid ? ct_raw : n_ct - 1;
     bool wide = false;
     {  // h -> 28-bit limbs -> scratch entry 16
       uint32_t h[64];
-      if (key_is_zero) {
+      if (SEG(key_is_zero, key_is_zero_a)) {
 #pragma unroll
         for (int i = 0; i < 64; ++i) h[i] = i == 0 ? 1u : 0u;
       } else {
-        load_row64(H + ct * 64, h);
+        load_row64(SEG(H, H_a) + ct * 64, h);
       }
       uint32_t h28[FBM_NL];
       {  // h = h_lo + h_hi R (R = 2^1036): the 74-limb decomposition is (h_lo, h_hi)
@@ -556,7 +591,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
       fbm_na_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, NK, np);  // h_hi*R^2 (wide lanes)
       lds_to_glb(lds, table + (tb0 + tstride) / 4);
       uint32_t h[64];
-      load_row64(H + ct * 64, h);
+      load_row64(SEG(H, H_a) + ct * 64, h);
       uint32_t h28[FBM_NL];
       to28<64, FBM_NL>(h, h28);
 #pragma unroll
@@ -581,7 +616,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
       }
       lds_store_col(lds, FBM_BLOCK, a);
     }
-    if (!key_is_zero) {
+    if (!SEG(key_is_zero, key_is_zero_a)) {
       lds_to_glb(lds, table + tb0 / 4);
       fbm_na_sq_lds(aoff, NK, np);  // h^2*R
       lds_to_glb(lds, table + (tb0 + FBM_TSCRATCH * tstride) / 4);
@@ -591,10 +626,11 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
         fbm_na_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, NK, np);
         lds_to_glb(lds, table + (tb0 + (uint32_t)t * tstride) / 4);
       }
-      glb_to_lds(table + (tb0 + (uint32_t)first * tstride) / 4, lds);
+      glb_to_lds(table + (tb0 + (uint32_t)SEG(first, first_a) * tstride) / 4, lds);
+      const int n_ops = SEG(n_ops, n_ops_a);
 #pragma unroll 1
       for (int k = 0; k < n_ops; ++k) {
-        const uint32_t op = __builtin_amdgcn_readfirstlane(ops[k]);
+        const uint32_t op = __builtin_amdgcn_readfirstlane(SEG(ops, ops_a)[k]);
         const int nsq = (int)(op >> FBM_OP_SHIFT);
         const int idx = (int)(op & ((1u << FBM_OP_SHIFT) - 1u)) - 1;
 #pragma unroll 1
@@ -602,13 +638,15 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
         if (idx >= 0) fbm_na_mm_glb(aoff, table, tb0 + (uint32_t)idx * tstride, NK, np);
       }
     }
+    const int mode = SEG(mode, mode_a);
     if ((mode & FBM_EXP_DEC) == 0)
-      fbm_na_mm_glb(aoff, nude, (uint32_t)((((ct >> 8) * (FBM_NL * 256)) + (ct & 255)) * 4), NK, np);
+      fbm_na_mm_glb(aoff, SEG(nude, nude_a), (uint32_t)((((ct >> 8) * (FBM_NL * 256)) + (ct & 255)) * 4), NK, np);
     else
       fbm_na_mm_glb(aoff, cst + FBM_CST_ONE, 0u, NK, np);
     uint32_t w[64];
     na_final(lds, NK, w, mode & FBM_EXP_OUT_NADIC);
-    if (valid) store_row64(out + ct * 64, w);
+    if (valid) store_row64(SEG(out, out_a) + ct * 64, w);
+#undef SEG
   }
 }
 
@@ -1472,10 +1510,79 @@ uint64_t jl_table_bytes(uint64_t n_ct) {
   return need;
 }
 
+// ---- batched one-lane exponentiations (fbm_jl_batch_begin / _flush, include/fbm_secagg.h) ----
+struct JlBatchState {
+  bool active = false;
+  bool accept = false;  // set by the phase-2 entry points only (jl_batch_accept): other calls launch
+  JlExpBatch bt;
+  const uint32_t* cst = nullptr;  // the first segment's constants block (all segments: same N)
+  uint32_t n32[32];
+  uint32_t np = 0;
+};
+static thread_local JlBatchState g_batch;
+
+bool jl_batch_active() { return g_batch.active; }
+
+int jl_batch_begin() {
+  if (g_batch.active) {
+    set_error("fbm_jl_batch_begin: a batch is already open on this thread");
+    return FBM_E_ARG;
+  }
+  memset(&g_batch.bt, 0, sizeof(g_batch.bt));
+  g_batch.cst = nullptr;
+  g_batch.active = true;
+  return FBM_OK;
+}
+
+void jl_batch_abort() { g_batch.active = false; }
+
+bool jl_batch_accept(bool on) {
+  const bool prev = g_batch.accept;
+  g_batch.accept = on;
+  return prev;
+}
+
+static int jl_batch_record(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const JlSched& sc, int mode,
+                           const uint32_t* nude, const uint32_t* ops, const uint32_t* cst, uint32_t* out) {
+  JlExpBatch& bt = g_batch.bt;
+  if (n_ct == 0) return FBM_OK;
+  if (bt.nseg >= FBM_EXP_MAXSEG) {
+    set_error("a JL exponentiation batch holds at most %d calls", FBM_EXP_MAXSEG);
+    return FBM_E_UNSUPPORTED;
+  }
+  if (bt.nseg == 0) {
+    g_batch.cst = cst;
+    memcpy(g_batch.n32, jp.N32, sizeof(g_batch.n32));
+    g_batch.np = jp.mn.mp;
+  } else if (memcmp(g_batch.n32, jp.N32, sizeof(g_batch.n32)) != 0) {
+    set_error("every call of a JL exponentiation batch must use the same biprime");
+    return FBM_E_ARG;
+  }
+  const uint64_t chunks = (n_ct + FBM_BLOCK - 1) / FBM_BLOCK;
+  if ((uint64_t)bt.total_chunks + chunks > 0xFFFFFFFFull) {
+    set_error("JL exponentiation batch too large");
+    return FBM_E_UNSUPPORTED;
+  }
+  bt.seg[bt.nseg++] = JlExpSeg{H, nude, out, ops, n_ct, bt.total_chunks, sc.n_ops, sc.first, mode, jp.key_is_zero};
+  bt.total_chunks += (uint32_t)chunks;
+  return FBM_OK;
+}
+
+uint64_t jl_batch_workspace() { return 256 + 4096 + jl_table_slots() * (uint64_t)FBM_TENTRIES * FBM_NL * 4; }
+
+// the batch's segment table into device memory (a kernel argument -> the batch workspace) and
+// the chunk counter zeroed
+__global__ void jl_batch_desc_kernel(JlExpBatch bt, JlExpSeg* __restrict__ segs, uint32_t* __restrict__ ctr) {
+  const int t = threadIdx.x;
+  if (t < bt.nseg) segs[t] = bt.seg[t];
+  if (t == 0) ctr[0] = 0u;
+}
+
 int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const JlSched& sc, int mode,
                   const uint32_t* nude, uint32_t* table, uint64_t table_slots, const uint32_t* ops,
                   const uint32_t* cst, uint32_t* out, hipStream_t s) {
   if (n_ct == 0) return FBM_OK;
+  if (g_batch.active && g_batch.accept) return jl_batch_record(H, n_ct, jp, sc, mode, nude, ops, cst, out);
   const int eng = jl_engine_for(n_ct);
   if (eng == FBM_ENGINE_QUAD || eng == FBM_ENGINE_TRIPLE) {
     uint64_t g = (n_ct + group_ct_per_wg(eng) - 1) / group_ct_per_wg(eng);
@@ -1492,9 +1599,38 @@ int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const Jl
   uint64_t g = (n_ct + FBM_BLOCK - 1) / FBM_BLOCK;
   const uint64_t gmax = table_slots / FBM_BLOCK;
   if (g > gmax) g = gmax;
-  hipLaunchKernelGGL(jl_exp_kernel, dim3((unsigned)g), dim3(FBM_BLOCK), 0, s, H, n_ct, (uint32_t*)cst, jp.mn.mp, ops, sc.n_ops,
-                     sc.first, mode, jp.key_is_zero, nude, table, out);
+  hipLaunchKernelGGL(jl_exp_kernel<false>, dim3((unsigned)g), dim3(FBM_BLOCK), 0, s, H, n_ct, (uint32_t*)cst, jp.mn.mp,
+                     ops, sc.n_ops, sc.first, mode, jp.key_is_zero, nude, table, out, (const JlExpSeg*)nullptr, 0, 0u,
+                     (uint32_t*)nullptr);
   return check_launch("jl_exp_kernel");
+}
+
+int jl_batch_flush(void* workspace, uint64_t ws_bytes, hipStream_t s) {
+  if (!g_batch.active) {
+    set_error("fbm_jl_batch_flush: no open batch on this thread");
+    return FBM_E_ARG;
+  }
+  g_batch.active = false;
+  const JlExpBatch& bt = g_batch.bt;
+  if (bt.nseg == 0) return FBM_OK;
+  if (!workspace || ws_bytes < jl_batch_workspace()) {
+    set_error("fbm_jl_batch_flush: workspace of %llu bytes needed", (unsigned long long)jl_batch_workspace());
+    return FBM_E_ARG;
+  }
+  // workspace: counter (word 0) | segment table (at 256) | exponent tables (at 256 + 4 KB)
+  uint32_t* ctr = (uint32_t*)workspace;
+  JlExpSeg* segs = (JlExpSeg*)((uint8_t*)workspace + 256);
+  uint32_t* table = (uint32_t*)((uint8_t*)workspace + 256 + 4096);
+  hipLaunchKernelGGL(jl_batch_desc_kernel, dim3(1), dim3(64), 0, s, bt, segs, ctr);
+  int rc = check_launch("jl_batch_desc_kernel");
+  if (rc) return rc;
+  uint64_t g = bt.total_chunks;
+  const uint64_t gmax = jl_table_slots() / FBM_BLOCK;
+  if (g > gmax) g = gmax;
+  hipLaunchKernelGGL(jl_exp_kernel<true>, dim3((unsigned)g), dim3(FBM_BLOCK), 0, s, (const uint32_t*)nullptr, (uint64_t)0,
+                     (uint32_t*)g_batch.cst, g_batch.np, (const uint32_t*)nullptr, 0, 0, 0, 0, (const uint32_t*)nullptr,
+                     table, (uint32_t*)nullptr, (const JlExpSeg*)segs, bt.nseg, bt.total_chunks, ctr);
+  return check_launch("jl_exp_kernel (batch)");
 }
 
 int launch_jl_prod(const uint32_t* cts, int n_parties, uint64_t n_ct, const JlParams& jp, const uint32_t* cst,

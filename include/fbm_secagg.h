@@ -217,6 +217,22 @@ int fbm_jl_triple_mads(int square);
 int fbm_jl_set_engine(int mode);
 int fbm_jl_engine_for(uint64_t n_ct);
 
+/* Batched exponentiation (one-lane engine), for callers that run several parties' encrypts and
+ * the decryption factor on one device (simulation, the benchmark): between fbm_jl_batch_begin
+ * and fbm_jl_batch_flush the calling thread's phase-2-only calls -- fbm_jl_encrypt_phase(..., 2)
+ * with a non-negative key, fbm_jl_decrypt_factor_phase(..., 2) -- record their exponentiation
+ * instead of launching it; the flush launches ONE kernel over all of them on `stream` (one chunk
+ * counter: the chip's rounds pack whatever the parts' sizes and however streams map onto hardware
+ * queues).  Every recorded call must use the same biprime; at most 24 calls; their prologues must
+ * be complete on `stream` at the flush, and their outputs are valid after it.  Other calls made
+ * while a batch is open launch as usual; a factor's inverse (phase 4) is refused until the flush.
+ * workspace: fbm_jl_batch_workspace() bytes of device memory.  No reference counterpart: the
+ * reference encrypts one party per call (fedbiomed/common/secagg/_secagg_crypter.py:45-137). */
+int fbm_jl_batch_begin(void);
+void fbm_jl_batch_abort(void);
+uint64_t fbm_jl_batch_workspace(void);
+int fbm_jl_batch_flush(void* workspace, uint64_t workspace_bytes, void* stream);
+
 /* ---- host test hook (no GPU): the device modular-inverse routine (Bernstein-Yang divsteps,
  * fedbiomed_amd/csrc/fbm_safegcd.hpp) run on the host, for unit tests.
  * x, n, out: 32 little-endian words (n odd);  batches: number of 30-divstep batches used. */
