@@ -1,4 +1,4 @@
-"""Constants mirrored from the reference (fedbiomed/common/constants.py:350-362, :412, :437)."""
+"""Constants mirrored from the reference (fedbiomed/common/constants.py:350-362, :412, :437, :442)."""
 
 from enum import Enum
 
@@ -15,3 +15,4 @@ class SAParameters:
 class ErrorNumbers(Enum):
     FB417 = "FB417: secure aggregation error"
     FB624 = "FB624: Secure aggregation crypter error"
+    FB629 = "FB629: Diffie-Hellman KA error"

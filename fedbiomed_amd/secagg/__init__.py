@@ -1,5 +1,7 @@
 from ._additive_ss import AdditiveSecret, AdditiveShare, AdditiveShares
+from ._dh import DHKey, DHKeyAgreement
 from ._lom import LOM, PRF
 from ._secagg_crypter import SecaggCrypter, SecaggLomCrypter
 
-__all__ = ["AdditiveSecret", "AdditiveShare", "AdditiveShares", "LOM", "PRF", "SecaggCrypter", "SecaggLomCrypter"]
+__all__ = ["AdditiveSecret", "AdditiveShare", "AdditiveShares", "DHKey", "DHKeyAgreement", "LOM", "PRF",
+           "SecaggCrypter", "SecaggLomCrypter"]

@@ -317,6 +317,42 @@ def gen_edge(R):
     dump("edge.json", out)
 
 
+def gen_dh(R):
+    """Setup-time key agreement (reference fedbiomed/common/secagg/_dh.py): P-256
+    key pairs generated and exported by the reference DHKey (PKCS#8 / SubjectPublicKeyInfo PEM),
+    the pairwise keys its DHKeyAgreement derives (ECDH + ConcatKDF-SHA256 over salt || ordered
+    ids), _kdf on fixed secrets, and the error outcomes of its tests (tests/test_dh.py)."""
+    import importlib
+
+    dh = importlib.import_module("fedbiomed.common.secagg._dh")
+    ids = ["node_u", "node_v", "node-01", "node-10", "Zeta", "alpha"]
+    keys = [dh.DHKey() for _ in ids]
+    priv = [k.export_private_key() for k in keys]
+    pub = [k.export_public_key() for k in keys]
+    pairs = []
+    for salt in (b"this_is_a_salt", b"secagg_0f1e2d3c4b5a", b""):
+        for u in range(len(ids)):
+            for v in range(len(ids)):
+                if u == v:
+                    continue
+                ka = dh.DHKeyAgreement(ids[u], dh.DHKey(private_key_pem=priv[u]), salt)
+                pairs.append({"u": u, "v": v, "salt": salt.hex(), "key": ka.agree(ids[v], pub[v]).hex()})
+    kdf = []
+    for secret, u, v, salt in ((b"secret_key", "node_u", "node_v", b"this_is_a_salt"),
+                               (b"secret_key", "node_v", "node_u", b"this_is_a_salt"),
+                               (bytes(range(32)), "a", "b", b""), (b"\x00" * 32, "n1", "n10", b"s" * 70)):
+        ka = dh.DHKeyAgreement(u, keys[0], salt)
+        kdf.append({"secret": secret.hex(), "u": u, "v": v, "salt": salt.hex(), "key": ka._kdf(secret, v).hex()})
+    errors = {
+        "bad_private": _outcome(lambda: dh.DHKey(private_key_pem=b"invalid_key_data") and None),
+        "bad_public": _outcome(lambda: dh.DHKey(public_key_pem=b"invalid_key_data") and None),
+        "private_as_public": _outcome(lambda: dh.DHKeyAgreement(ids[0], keys[0], b"s").agree(ids[1], priv[1])),
+        "public_only_export_private": _outcome(lambda: dh.DHKey(public_key_pem=pub[0]).export_private_key()),
+    }
+    dump("dh.json", {"ids": ids, "private_pem": [p.decode() for p in priv], "public_pem": [p.decode() for p in pub],
+                     "pairs": pairs, "kdf": kdf, "errors": errors})
+
+
 def main():
     R = load_reference.load()
     gen_quantize(R)
@@ -324,6 +360,7 @@ def main():
     gen_jl(R)
     gen_ass(R)
     gen_edge(R)
+    gen_dh(R)
     meta = {"generator": "tools/gen_golden.py", "reference": load_reference.REF,
             "note": "outputs of the reference Fed-BioMed crypter (Python), imported via tools/refshim"}
     dump("meta.json", meta)
