@@ -95,8 +95,8 @@ def committed_traffic(kernel: str, scheme: str, n_ct: int):
             continue
         cfg = d.get("meta", {}).get("bench_config") or {}
         if cfg.get("scheme") == scheme and (scheme != "jl" or cfg.get("ciphertexts_per_party_per_gpu") == n_ct):
-            for name, k in d.get("kernels", {}).items():  # template arguments stripped
-                if name.split("<")[0] == "fbm::" + kernel:
+            for name, k in d.get("kernels", {}).items():  # exact, or template arguments stripped
+                if name == "fbm::" + kernel or ("<" not in kernel and name.split("<")[0] == "fbm::" + kernel):
                     return k["hbm_bytes_per_launch"]
     return None
 
@@ -264,8 +264,9 @@ def main():
                         main.wait_stream(st)
                     for st in pool + [factor_stream]:
                         st.wait_stream(main)
-                if batch_exp and not serial:
-                    # one launch over every party's ciphertexts and the factor's, on `main`
+                if batch_exp:
+                    # one launch over every party's ciphertexts and the factor's, on `main` (the
+                    # serialised profiling step too: it times the step's own kernel)
                     with D.jl_exp_batch(dev):
                         if overlap_factor:
                             pf.exponentiate()
@@ -347,7 +348,9 @@ def main():
         mads_step = n_ct * (sum(mads_per_exp(k, win, mads_mul, mads_sq) for k in keys)
                             + mads_per_exp(sk0, win, mads_mul, mads_sq))
         mads = prof_steps * mads_step
-        kname = "jl_exp_kernel"
+        # the step's exponentiation kernel: one batched launch over every party and the factor
+        # (jl_exp_kernel<true>), or one launch each (<false>, --no-batch-exp)
+        kname = "jl_exp_kernel<true>" if batch_exp else "jl_exp_kernel<false>"
     else:
         cnt, ms = kprof.get("lom_aggregate", (0, 0.0))
         alg_bytes = prof_steps * 8 * (P + 1) * n
@@ -361,7 +364,8 @@ def main():
     if args.scheme == "jl":
         roof["note"] = ("jl_exp_kernel moves ~1e-4 of the HBM roofline's bytes by construction: it is bound by "
                         "integer multiply issue (v_mad_u64_u32), reported in roofline_valu; traffic = the "
-                        "sliding-window table reads (DESIGN.md section 4)")
+                        "sliding-window table reads (DESIGN.md section 4); one launch = every party's and "
+                        "the decryption factor's exponentiations (batched)")
     line = {
         "metric": "params/s secagg encrypt+aggregate (device-resident), 10M-elem vector @1/8 GPU",
         "value": value, "unit": "params/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -385,8 +389,8 @@ def main():
                                  "mads_per_square": mads_sq, "mads_per_product": mads_mul,
                                  "note": "executed v_mad_u64_u32 of the N-adic engine (per square / product "
                                          "above); "
-                                         "achieved/frac: serialised jl_exp launches (HIP events); step_*: the "
-                                         "timed step (parties on concurrent streams, all kernels)"}
+                                         "achieved/frac: the step's jl_exp launch(es) in a serialised step (HIP "
+                                         "events on the launch stream); step_*: the timed step (all kernels)"}
 
     # ---- per-stage times: T_enc = all P parties' encrypts as the step issues
     #      them, T_agg = the aggregate alone (decryption factor + combine, nothing overlapped);

@@ -811,8 +811,11 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
     return timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, cst, Hinv, Y, nude, ct_out, stats, s); });
   }
   // a phase-2-only call inside an open batch (fbm_jl_batch_begin) is recorded, not launched
-  const bool acc = jl_batch_accept(phase == 2);
-  rc = timed("jl_exp", s, [&] { return launch_jl_exp(H, n_ct, jp, sc, 0, nude, table, slots, ops, cst, ct_out, s); });
+  // (and not timed: the batch's one launch is, at the flush)
+  auto go = [&] { return launch_jl_exp(H, n_ct, jp, sc, 0, nude, table, slots, ops, cst, ct_out, s); };
+  const bool rec = phase == 2 && jl_batch_active();
+  const bool acc = jl_batch_accept(rec);
+  rc = rec ? go() : timed("jl_exp", s, go);
   jl_batch_accept(acc);
   return rc;
 }
@@ -889,12 +892,14 @@ static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t
     if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, w.H, stats, s); }))) return rc;
   }
   if (phase & 2) {
-    const bool acc = jl_batch_accept(phase == 2);  // recorded inside an open batch
-    rc = timed("jl_exp", s, [&] {
-      // the inverse starts from the power's N-adic digits (no division by N needed)
+    // the inverse starts from the power's N-adic digits (no division by N needed)
+    auto go = [&] {
       return launch_jl_exp(w.H, n_ct, jp, sc, FBM_EXP_DEC | (inv ? FBM_EXP_OUT_NADIC : 0), nullptr, w.table, w.slots,
                            w.ops, w.cst, E, s);
-    });
+    };
+    const bool rec = phase == 2 && jl_batch_active();  // recorded (not launched, not timed) in an open batch
+    const bool acc = jl_batch_accept(rec);
+    rc = rec ? go() : timed("jl_exp", s, go);
     jl_batch_accept(acc);
     if (rc) return rc;
   }

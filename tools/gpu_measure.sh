@@ -11,9 +11,9 @@ cd $R
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1 &&
 timeout -k 10 300 python bench.py --steps 2 --warmup 1 > $O/bench.json 2> $O/bench.err &&
 cd /tmp && export TMPDIR=/tmp &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 1 --warmup 0 --serial --no-cpu-baseline --no-lom-extra --no-e2e > $O/prof_bench.json 2> $O/prof.err &&
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 1 --warmup 0 --serial --no-cpu-baseline --no-lom-extra --no-e2e > /dev/null 2> $O/pmc_fetch.err &&
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 $R/bench.py --steps 1 --warmup 0 --serial --no-cpu-baseline --no-lom-extra --no-e2e > /dev/null 2> $O/pmc_write.err &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 1 --warmup 0 --serial --no-cpu-baseline --no-lom-extra --no-e2e --no-stages > $O/prof_bench.json 2> $O/prof.err &&
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 1 --warmup 0 --serial --no-cpu-baseline --no-lom-extra --no-e2e --no-stages > /dev/null 2> $O/pmc_fetch.err &&
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 $R/bench.py --steps 1 --warmup 0 --serial --no-cpu-baseline --no-lom-extra --no-e2e --no-stages > /dev/null 2> $O/pmc_write.err &&
 cd $R && timeout -k 10 300 python -u bench.py --elements 1250010 --steps 5 --warmup 1 --no-cpu-baseline --no-lom-extra --no-e2e > $O/bench_stripe8.json 2> $O/bench_stripe8.err &&
 if [ -x ./tools/microbench/madpeak ]; then timeout -k 10 120 ./tools/microbench/madpeak 400000 > $O/madpeak.txt 2>&1; fi
 rc=$?
