@@ -499,10 +499,10 @@ def main():
         out_h = torch.empty(n, dtype=torch.float64).pin_memory()
 
         def step_e2e():
-            # as the device-resident step: one stream per party (H2D -> encrypt -> D2H), the
-            # decryption factor on its own stream, then H2D of the ciphertexts -> combine -> D2H
-            # kernel order as in the device-resident step: H2D + prologues, then the
-            # exponentiations (+ D2H of each party's ciphertexts), then the factor's inverse
+            # as the device-resident step: one stream per party (H2D -> prologue), the decryption
+            # factor's prologue on its own stream, then the exponentiations (one batched launch),
+            # each party's D2H of its ciphertexts, the factor's inverse; then H2D of the
+            # ciphertexts -> combine -> D2H
             with D.deferred_checks():
                 pend = [None] * P
                 for p in range(P):
@@ -518,13 +518,24 @@ def main():
                     main.wait_stream(st)
                 for st in pool + [factor_stream]:
                     st.wait_stream(main)
-                with torch.cuda.stream(factor_stream):
-                    pf.exponentiate()
-                for p in range(P):
-                    with torch.cuda.stream(streams[p]):
-                        ct_h[p].copy_(pend[p].finish(), non_blocking=True)
-                with torch.cuda.stream(factor_stream):
+                if batch_exp:  # one exponentiation launch on `main`, then each party's D2H on its stream
+                    with D.jl_exp_batch(dev):
+                        pf.exponentiate()
+                        cts_d = [pend[p].finish() for p in range(P)]
                     factor = pf.finish()
+                    for p in range(P):
+                        streams[p].wait_stream(main)
+                        with torch.cuda.stream(streams[p]):
+                            ct_h[p].copy_(cts_d[p], non_blocking=True)
+                            cts_d[p].record_stream(streams[p])
+                else:
+                    with torch.cuda.stream(factor_stream):
+                        pf.exponentiate()
+                    for p in range(P):
+                        with torch.cuda.stream(streams[p]):
+                            ct_h[p].copy_(pend[p].finish(), non_blocking=True)
+                    with torch.cuda.stream(factor_stream):
+                        factor = pf.finish()
             for st in pool + [factor_stream]:
                 main.wait_stream(st)
             factor.record_stream(main)
