@@ -155,6 +155,20 @@ def test_cfg4_jl_10m_8_parties_8_stripes(dev):
     assert tuple(whole.shape) == (P, n_ct, 64)
     out_whole, sums = jc.aggregate_tensor(tau, whole, sk0, W.BIPRIME0, sum(ws), num_expected_params=n,
                                           want_sums=True)
+    # the benchmark's path: every party's exponentiation and the decryption factor in ONE batched
+    # launch (D.jl_exp_batch) -- bit-identical ciphertexts and aggregate
+    with D.deferred_checks():
+        pend = [jc.encrypt_tensor(P, tau, xd[p], keys[p], W.BIPRIME0, weight=ws[p], defer_exp=True) for p in range(P)]
+        pf = jc.decrypt_factor_tensor(tau, n_ct, sk0, W.BIPRIME0, phased=True)
+        with D.jl_exp_batch(dev):
+            pf.exponentiate()
+            cts = [q.finish() for q in pend]  # (valid after the batch's launch, at exit)
+        factor = pf.finish()
+    batched = torch.stack(cts)
+    assert torch.equal(batched, whole)
+    out_b = jc.aggregate_tensor(tau, batched, sk0, W.BIPRIME0, sum(ws), num_expected_params=n, decrypt_factor=factor)
+    assert torch.equal(out_b, out_whole)
+    del batched, cts, pend, pf, factor, out_b
     # the 8 stripes: ciphertexts and aggregates bit-identical to the whole vector's
     outs = []
     for r in range(world):
