@@ -103,3 +103,41 @@ def test_batch_mixed_and_refused_calls():
             p1.finish()
             p2.finish()
     torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [5, 300, 1000, 1024])
+def test_batch_random_moduli(bits):
+    """The batched launch on random odd moduli (small ones: FDH retries, i.e. wide digests
+    entering as h_lo R + h_hi R^2 inside the batch), keys of several lengths incl. 0, and the
+    decryption factor of a negative sum: bit-identical to per-call launches and the oracle."""
+    import random
+
+    dev = D.device()
+    rng = random.Random(3000 + bits)
+    N = max(3, rng.getrandbits(bits) | (1 << (bits - 1)) | 1)
+    n2, P, tau = N * N, 3, rng.getrandbits(64)
+    sizes = [37, 300, 1]
+    keys = [rng.getrandbits(rng.choice([40, 700, 2040])) for _ in range(P)]
+    keys[2] = 0
+    xs = [torch.tensor([rng.getrandbits(63) for _ in range(s)], dtype=torch.int64, device=dev) for s in sizes]
+    ref = [D.jl_encrypt(xs[p], N, keys[p], tau, P, slot=(100, 1)) for p in range(P)]
+    sk0 = -sum(keys) - 1
+    fref = D.jl_decrypt_factor(50, N, sk0, tau, ct_offset=4)
+    with D.deferred_checks():
+        pend = [D.jl_encrypt(xs[p], N, keys[p], tau, P, slot=(100, 1), defer_exp=True) for p in range(P)]
+        pf = D.jl_decrypt_factor(50, N, sk0, tau, ct_offset=4, phased=True)
+        with D.jl_exp_batch(dev):
+            pf.exponentiate()
+            cts = [q.finish() for q in pend]
+        f = pf.finish()
+    for p in range(P):
+        assert torch.equal(cts[p], ref[p]), p
+        k = sizes[p] - 1
+        pt = int(xs[p][k])
+        want = ((N * pt + 1) % n2) * O.powmod(O.fdh((k << 512) | tau, n2), keys[p], n2) % n2
+        assert D.limbs_to_ints(cts[p][k:k + 1].cpu().numpy())[0] == want, p
+    assert torch.equal(f, fref)
+    got = D.limbs_to_ints(f[[0, 49]].cpu().numpy())
+    for g, k in zip(got, (4, 53)):
+        assert g == O.powmod(O.fdh((k << 512) | tau, n2), sk0, n2)
