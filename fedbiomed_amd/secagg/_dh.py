@@ -82,6 +82,8 @@ class _PKey:
     def _pem(self, private: bool) -> bytes:
         lib = _ssl()
         bio = lib.BIO_new(lib.BIO_s_mem())
+        if not bio:
+            raise MemoryError("OpenSSL: no memory BIO")
         try:
             ok = (lib.PEM_write_bio_PKCS8PrivateKey(bio, self._p, None, None, 0, None, None) if private
                   else lib.PEM_write_bio_PUBKEY(bio, self._p))
@@ -119,7 +121,10 @@ def _load(data: bytes, private: bool) -> _PKey:
     if not isinstance(data, (bytes, bytearray)):
         raise TypeError("data must be bytes")
     lib = _ssl()
-    bio = lib.BIO_new_mem_buf(bytes(data), len(data))
+    buf = bytes(data)  # held until the BIO is freed: a memory BIO reads the caller's buffer in place
+    bio = lib.BIO_new_mem_buf(buf, len(buf))
+    if not bio:
+        raise MemoryError("OpenSSL: no memory BIO")
     try:
         fn = lib.PEM_read_bio_PrivateKey if private else lib.PEM_read_bio_PUBKEY
         p = fn(bio, None, None, None)
@@ -138,6 +143,8 @@ def _ecdh(priv: _PKey, peer: _PKey) -> bytes:
     if lib.EVP_PKEY_get_base_id(priv._p) != _EVP_PKEY_EC or lib.EVP_PKEY_get_base_id(peer._p) != _EVP_PKEY_EC:
         raise TypeError("ECDH needs elliptic-curve keys")
     ctx = lib.EVP_PKEY_CTX_new(priv._p, None)
+    if not ctx:
+        raise ValueError("Error computing shared key.")
     try:
         n = ctypes.c_size_t(0)
         if (lib.EVP_PKEY_derive_init(ctx) != 1 or lib.EVP_PKEY_derive_set_peer(ctx, peer._p) != 1

@@ -78,3 +78,15 @@ def test_concat_kdf_multi_block():
     out = concat_kdf_sha256(z, 70, info)
     want = b"".join(hashlib.sha256(c.to_bytes(4, "big") + z + info).digest() for c in (1, 2, 3))[:70]
     assert out == want
+
+
+def test_bytearray_pem_input(dh):
+    """PEM handed over as a bytearray (a temporary bytes copy must outlive OpenSSL's memory BIO)."""
+    import gc
+
+    priv, pub = dh["private_pem"][1].encode(), dh["public_pem"][1].encode()
+    for _ in range(20):
+        k = DHKey(private_key_pem=bytearray(priv))
+        gc.collect()
+        assert k.export_public_key() == pub
+        assert DHKey(public_key_pem=bytearray(pub)).export_public_key() == pub
