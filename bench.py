@@ -82,9 +82,10 @@ def mads_per_exp(key: int, win: int, mads_mul: int, mads_sq: int) -> int:
     return sq * mads_sq + gen * mads_mul
 
 
-def committed_traffic(kernel: str, scheme: str, n_ct: int):
+def committed_traffic(kernel: str, scheme: str, elements: int, n_ct=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
-    workload (profiles/*_hbm_traffic.json, written by tools/prof_summary.py), else None."""
+    workload -- same scheme and elements per GPU (JL: same ciphertexts per party) --
+    (profiles/*_hbm_traffic.json, written by tools/prof_summary.py), else None."""
     import glob
 
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic.json")), reverse=True):
@@ -94,7 +95,8 @@ def committed_traffic(kernel: str, scheme: str, n_ct: int):
         except (OSError, ValueError):
             continue
         cfg = d.get("meta", {}).get("bench_config") or {}
-        if cfg.get("scheme") == scheme and (scheme != "jl" or cfg.get("ciphertexts_per_party_per_gpu") == n_ct):
+        if (cfg.get("scheme") == scheme and cfg.get("elements_per_gpu") == elements
+                and (scheme != "jl" or cfg.get("ciphertexts_per_party_per_gpu") == n_ct)):
             for name, k in d.get("kernels", {}).items():  # exact, or template arguments stripped
                 if name == "fbm::" + kernel or ("<" not in kernel and name.split("<")[0] == "fbm::" + kernel):
                     return k["hbm_bytes_per_launch"]
@@ -294,12 +296,20 @@ def main():
         return jc.aggregate_tensor(tau, torch.stack(cts), sk0, W.BIPRIME0, total_w, num_expected_params=n,
                                    ct_offset=lo // cr, decrypt_factor=factor)
 
-    Y = torch.empty((P, n), dtype=torch.int64, device=dev) if args.scheme == "lom" or not args.no_lom_extra else None
+    # LOM stripes are ChaCha20-block (8-element) aligned: with the JL stripe (ciphertext aligned)
+    # as the main workload, the LOM leg takes its own 8-aligned split of the same vector
+    if args.scheme == "jl" and strong and world > 1:
+        lo_l, hi_l = distributed.shard_range(args.n, world, rank, 8)
+        xs_l = [torch.from_numpy(W.party_params(p + 1000 * rank, hi_l - lo_l)).to(dev) for p in range(P)]
+    else:
+        lo_l, hi_l, xs_l = lo, hi, xs
+    Y = (torch.empty((P, hi_l - lo_l), dtype=torch.int64, device=dev)
+         if args.scheme == "lom" or not args.no_lom_extra else None)
 
     def step_lom(serial=False):
         with D.deferred_checks():  # overflow-guard status checked once per step, no per-party sync
             for p, u in enumerate(ids):  # each party's masked vector straight into its row
-                lc.encrypt_tensor(tau, u, xs[p], secrets_[p], ids, weight=weights[p], elem_offset=lo, out=Y[p])
+                lc.encrypt_tensor(tau, u, xs_l[p], secrets_[p], ids, weight=weights[p], elem_offset=lo_l, out=Y[p])
         return lc.aggregate_tensor(Y, total_w)
 
     def timed(step, steps, warmup, prof=False):
@@ -359,7 +369,7 @@ def main():
     achieved = alg_bytes / sec / 1e9 if ms > 0 else None
     roof = {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-            "traffic": committed_traffic(kname, args.scheme, n_ct),
+            "traffic": committed_traffic(kname, args.scheme, n, n_ct),
             "avg_launch_ms": (ms / cnt) if cnt else None, "launches": cnt}
     if args.scheme == "jl":
         roof["note"] = ("jl_exp_kernel moves ~1e-4 of the HBM roofline's bytes by construction: it is bound by "
@@ -482,10 +492,10 @@ def main():
         el2, _ = timed(step_lom, k2, 2)  # the step as it runs
         _, kp2 = timed(step_lom, 1, 0, prof=True)  # one instrumented step: per-kernel durations
         c2, m2 = kp2.get("lom_aggregate", (0, 0.0))
-        ab = c2 * 8 * (P + 1) * n
+        ab = c2 * 8 * (P + 1) * (hi_l - lo_l)
         line["lom"] = {"value": n_total * k2 / el2, "unit": "params/s",
                        "ms_per_step": 1000 * el2 / k2,
-                       "aggregate_traffic": committed_traffic("lom_aggregate_kernel", "lom", n_ct),
+                       "aggregate_traffic": committed_traffic("lom_aggregate_kernel", "lom", hi_l - lo_l),
                        "aggregate_hbm_GBps": ab / (m2 / 1000) / 1e9 if m2 else None,
                        "aggregate_hbm_frac": (ab / (m2 / 1000) / 1e9) / HBM_PEAK_GBS if m2 else None,
                        "kernels_ms": {k: {"launches": c, "total_ms": round(t, 3)} for k, (c, t) in sorted(kp2.items())}}
