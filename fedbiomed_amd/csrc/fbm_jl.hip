@@ -666,6 +666,9 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
 //   limb row j (b0: j = r, b1: j = M + r) at word (slot * FBM_TENTRIES + e) * ENTRY + j * 256 + tid.
 // ------------------------------------------------------------------------------------
 #define FBM_QBLOCK 256
+#ifndef FBM_GROUP_WAVES  // resident group-engine waves per SIMD (= workgroups per CU): the VGPR budget
+#define FBM_GROUP_WAVES 3
+#endif
 #define FBM_QMASK ((1u << FBM_QA_LB) - 1u)
 
 // limb k (lb bits at bit lb k) of a little-endian number of `nw` words in global memory
@@ -767,7 +770,7 @@ __device__ __forceinline__ void qa_normalise_column(uint32_t* col) {
 }
 
 template <int G>
-__global__ void __launch_bounds__(FBM_QBLOCK, 3) jl_expg_kernel(const uint32_t* __restrict__ H, uint64_t n_ct,
+__global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(const uint32_t* __restrict__ H, uint64_t n_ct,
                                                                uint32_t* __restrict__ cst, uint32_t np29,
                                                                const uint32_t* __restrict__ ops, int n_ops,
                                                                int first, int mode, int key_is_zero,
@@ -1428,15 +1431,17 @@ int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32
 // ---- exponentiation engine choice ------------------------------------------------------
 // FBM_ENGINE_SINGLE: one lane per ciphertext (throughput: every lane busy, 2 waves/SIMD);
 // FBM_ENGINE_QUAD / FBM_ENGINE_TRIPLE: four / three lanes per ciphertext (latency: launches
-// below the chip's lane count).  FBM_ENGINE_AUTO picks the engine of least modelled time.  A
-// group engine's launch time is set by its busiest SIMD: with w waves on it (w = workgroups per
-// CU, each workgroup's 4 waves on the CU's 4 SIMDs) it takes about A + B w -- A the part of a
-// lone wave's time another wave cannot fill, B a wave's issue time.  Measured on MI355X
-// (tools/exp_probe.py over 1k..65k ciphertexts, 2040-bit exponent, profiles/r2_engine_sweep.jsonl):
-// quad 12.0 / 19.7 / 28.5 ms at 1 / 2 / 3 waves (A = 4, B = 8.1), triple 15.0 / 24.9 / 36.3
-// (A = 5.1, B = 9.9).  The one-lane engine's lone wave takes 33.6 ms (up to one wave per SIMD),
-// 50 ms per round of two.  The group engines hold at most 3 workgroups per CU and are only modelled (and
-// chosen) for launches that fit in one residency.
+// below about two thirds of the chip's lane count).  FBM_ENGINE_AUTO picks the engine of least
+// modelled time.  A group engine's launch time is set by its busiest SIMD: with w waves' worth
+// of work on it (w = workgroups per CU, each workgroup's 4 waves on the CU's 4 SIMDs; beyond
+// FBM_GROUP_WAVES resident workgroups the persistent ones loop) it takes about A + B w -- A the
+// part of a lone wave's time another wave cannot fill, B a wave's issue time.  Measured on
+// MI355X (tools/exp_probe.py, 2040-bit exponent, profiles/r2_engine_sweep.jsonl): triple
+// 26.3 / 37.0 / 48.3 / 58.7 ms at w = 2 / 3 / 4 / 5 (A = 4.5, B = 10.8), quad 29.5 / 37.3 / 51.9 /
+// 60.3 at w = 3 / 4 / 6 / 7 (A = 4, B = 8.1).  The one-lane engine: 33.6 ms up to one wave per SIMD,
+// 57 ms for a launch of one round of two, 50 ms per round of longer launches.  (A build with 4
+// resident group waves per SIMD, -DFBM_GROUP_WAVES=4, measured no faster at w = 4: the issue is
+// already saturated at 3.)
 static std::atomic<int> g_engine{-1};
 
 int jl_engine_policy() {
@@ -1460,7 +1465,7 @@ int jl_engine_set(int mode) {
   return prev;
 }
 
-#define FBM_GROUP_WGS_PER_CU 3
+#define FBM_GROUP_WGS_PER_CU FBM_GROUP_WAVES
 static uint64_t group_wgs_max() { return (uint64_t)device_num_cu() * FBM_GROUP_WGS_PER_CU; }
 static int group_ct_per_wg(int engine) { return engine == FBM_ENGINE_TRIPLE ? 84 : 64; }
 
@@ -1470,15 +1475,13 @@ static double engine_model_ms(int engine, uint64_t n_ct) {
   if (engine == FBM_ENGINE_SINGLE) {
     const uint64_t lanes = ncu * 2 * FBM_BLOCK;
     if (n_ct <= lanes / 2) return 33.6;
+    if (n_ct <= lanes) return 57.0;
     return 50.0 * (double)((n_ct + lanes - 1) / lanes) - (n_ct % lanes && n_ct % lanes <= lanes / 2 ? 16.4 : 0.0);
   }
   const uint64_t wgs = (n_ct + group_ct_per_wg(engine) - 1) / group_ct_per_wg(engine);
   const uint64_t w = (wgs + ncu - 1) / ncu;
-  const double A = engine == FBM_ENGINE_TRIPLE ? 5.1 : 4.0, B = engine == FBM_ENGINE_TRIPLE ? 9.9 : 8.1;
-  // only launches whose workgroups are all resident at once (beyond that the one-lane engine's
-  // higher throughput per SIMD wins: 64 ciphertexts per 25 ms wave against 16 per 8.1 / 21 per 9.9)
-  if (w <= FBM_GROUP_WGS_PER_CU) return A + B * (double)w;
-  return 1e30;
+  const double A = engine == FBM_ENGINE_TRIPLE ? 4.5 : 4.0, B = engine == FBM_ENGINE_TRIPLE ? 10.8 : 8.1;
+  return A + B * (double)w;
 }
 
 int jl_engine_for(uint64_t n_ct) {

@@ -30,6 +30,9 @@ def test_engine_policy_host():
         assert lib.fbm_jl_engine_for(1000) == 4 and lib.fbm_jl_engine_for(333_334) == 1
         assert lib.fbm_jl_engine_for(41_667) == 3  # a config-4 stripe: 2 triple waves per SIMD, 3 quad
         assert lib.fbm_jl_engine_for(30_000) == 4 and lib.fbm_jl_engine_for(200_000) == 1
+        # past the group engines' residency (persistent workgroups loop): a config-4 N = 4 stripe's
+        # 83 334 ciphertexts take the triple (48 ms measured against the one-lane engine's 57)
+        assert lib.fbm_jl_engine_for(83_334) == 3 and lib.fbm_jl_engine_for(100_000) == 1
     finally:
         lib.fbm_jl_set_engine(prev)
     import importlib.util
