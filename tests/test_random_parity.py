@@ -174,3 +174,59 @@ def test_jl_many_parties(dev, P):
     out = jc.aggregate(tau, P, cts, -sum(keys), W.BIPRIME0, sum(ws), num_expected_params=n)
     ref = O.jl_crypter_aggregate(cts, tau, -sum(keys), W.BIPRIME0, sum(ws), n)
     assert _bits(out) == _bits(ref)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_jl_random_tensor_engines(dev, seed):
+    """The device-tensor path on random configurations under each exponentiation engine (one
+    lane, quad, triple, auto policy), half of them with the parties' exponentiations in one
+    batched launch: sampled ciphertexts against the oracle's UserKey.encrypt, the decoded
+    integer sums exact for every element, and the float64 outputs bit-exact."""
+    import torch
+
+    from fedbiomed_amd import _device as D
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    rng = np.random.default_rng(500 + seed)
+    P = int(rng.integers(2, 13))
+    clip, target = _ranges(rng)
+    es, cr_ = O.jl_slot(target, P)
+    n = int(rng.choice([1, cr_, cr_ + 1, int(rng.integers(2, 40_000))]))
+    tau = int(rng.integers(0, 2**63)) * 2 + 1 if seed % 3 == 0 else int(rng.integers(0, 100))
+    ws = [int(rng.integers(1, 2**16)) for _ in range(P)]
+    keys = [int(rng.choice([-1, 1])) * W.jl_user_key(300 + 20 * seed + p) for p in range(P)]
+    if seed % 5 == 0:
+        keys[0] = 0
+    engine = ("single", "quad", "triple", "auto")[seed % 4]
+    batch = seed % 2 == 1
+    xs = [np.asarray(_params(rng, n, clip), dtype=np.float64) for _ in range(P)]
+    xd = [torch.tensor(x, dtype=torch.float64, device=dev) for x in xs]
+    jc = SecaggCrypter()
+    sk0 = -sum(keys)
+    kw = dict(clipping_range=clip, target_range=target)
+    with D.jl_engine(engine):
+        if batch:
+            with D.deferred_checks():
+                pend = [jc.encrypt_tensor(P, tau, xd[p], keys[p], W.BIPRIME0, weight=ws[p], defer_exp=True, **kw)
+                        for p in range(P)]
+                with D.jl_exp_batch(dev):
+                    cts = [q.finish() for q in pend]
+        else:
+            cts = [jc.encrypt_tensor(P, tau, xd[p], keys[p], W.BIPRIME0, weight=ws[p], **kw) for p in range(P)]
+        C = torch.stack(cts)
+        out, sums = jc.aggregate_tensor(tau, C, sk0, W.BIPRIME0, sum(ws), num_expected_params=n, want_sums=True,
+                                        **kw)
+    n_ct = C.shape[1]
+    tr = target or O.TARGET_RANGE
+    qw = [[int(v) * ws[p] for v in O.quantize(xs[p], clip, tr)] for p in range(P)]
+    ks = sorted({0, n_ct - 1, *rng.choice(n_ct, min(n_ct, 4), replace=False).tolist()})
+    for p in range(P):
+        got = D.limbs_to_ints(C[p, ks].cpu().numpy())
+        for k, g in zip(ks, got):
+            assert g == O.jl_encrypt_ints(qw[p][k * cr_:(k + 1) * cr_], tau, keys[p], W.BIPRIME0, P,
+                                          target=target, k0=k)[0], (seed, p, k)
+    want = [sum(col) for col in zip(*qw)]
+    s = sums.cpu().numpy().view(np.uint64)
+    assert [int(a) | (int(b) << 64) for a, b in s] == want, seed
+    ref = O.reverse_quantize(O.apply_average(want, sum(ws)), clip, tr)
+    assert _bits(out.cpu().numpy()) == _bits(ref)
