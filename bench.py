@@ -667,7 +667,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import secagg_oracle as O
 
-        ns = args.cpu_sample or (20_000 if args.scheme == "jl" else 500_000)
+        ns = args.cpu_sample or (30_000 if args.scheme == "jl" else 500_000)  # JL: ~12.5 s on one core
         xs_c = [[float(v) for v in W.party_params(p, ns)] for p in range(P)]
         t0 = time.perf_counter()
         if args.scheme == "jl":
