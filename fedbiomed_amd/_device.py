@@ -15,6 +15,7 @@ import array
 import ctypes
 import logging
 import math
+import operator
 import os
 import threading
 from typing import List, Optional, Sequence, Tuple
@@ -334,6 +335,12 @@ def limbs_to_ints(arr: np.ndarray) -> List[int]:
     return _pyconv().bytes_to_ints(np.ascontiguousarray(arr, dtype=np.uint32), 256)
 
 
+def limbs_to_ints_w(t: torch.Tensor, words: int) -> List[int]:
+    """[n, words] 32-bit limbs (device or host tensor) -> list of Python ints."""
+    a = (to_host(t) if t.is_cuda else t).numpy().view(np.uint32)
+    return _pyconv().bytes_to_ints(np.ascontiguousarray(a.reshape(-1, words)), 4 * words)
+
+
 # ------------------------------------------------------------------------------------------
 # LOM
 # ------------------------------------------------------------------------------------------
@@ -562,20 +569,30 @@ class PendingEncrypt:
 
 def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, clip=None, target=None,
                weight: int = 1, slot: Optional[Tuple[int, int]] = None, ct_offset: int = 0,
-               defer_exp: bool = False):
+               defer_exp: bool = False, kind: Optional[str] = None):
     """One party's JL ciphertexts as an int32 [n_ct, 64] tensor of 32-bit limbs.
-    `slot` overrides the (element_size, comp_ratio) packing (UserKey.encrypt on raw
-    plaintexts = slot (es, 1) with an int64 input).  defer_exp: issue only the prologue and
-    return a PendingEncrypt (one library call's worth of ciphertexts at most)."""
+    `slot` overrides the (element_size, comp_ratio) packing.  `kind` selects a raw input:
+    "u128" = int64 [n, 2] (lo, hi) integers packed into the VES slots (JoyeLibert.protect),
+    "pt" = int32 [n, 32] plaintext limbs encrypted as they are (UserKey.encrypt; slot (1, 1)).
+    defer_exp: issue only the prologue and return a PendingEncrypt (one library call's worth of
+    ciphertexts at most)."""
     dev = x.device
     lib = N.load()
     target = target or SAParameters.TARGET_RANGE
     es, cr = slot if slot else jl_slot(target, n_users)
-    c, c2, tf, tm1 = quant_params(clip, target) if x.dtype != torch.int64 else (1.0, 2.0, 1.0, 0)
+    raw = kind is not None or x.dtype == torch.int64
+    c, c2, tf, tm1 = (1.0, 2.0, 1.0, 0) if raw else quant_params(clip, target)
     if tau < 0 or tau > U64_MAX:
         raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: round must be in [0, 2^64)")
     x = x.contiguous()
-    n = x.numel()
+    if kind == "u128":
+        xdt, n = N.FBM_U128, x.shape[0]
+    elif kind == "pt":
+        xdt, n, es, cr = N.FBM_PT, x.shape[0], 1, 1
+    elif kind is None:
+        xdt, n = _x_dtype(x), x.numel()
+    else:
+        raise ValueError(f"unknown input kind {kind!r}")
     n_ct = (n + cr - 1) // cr
     ct = torch.empty((n_ct, 64), dtype=torch.int32, device=dev)
     if n_ct == 0:
@@ -589,7 +606,7 @@ def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, 
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value}: a deferred encrypt takes at most {chunk} ciphertexts")
         st = _stats(dev)
-        args = (_ptr(x), _x_dtype(x), n, c, c2, tf, tm1, int(weight) & U64_MAX, es, cr, _np_ptr(bp), _np_ptr(kl), kneg,
+        args = (_ptr(x), xdt, n, c, c2, tf, tm1, int(weight) & U64_MAX, es, cr, _np_ptr(bp), _np_ptr(kl), kneg,
                 int(tau), int(ct_offset), _ptr(ct), _ptr(ws), _ptr(st))
         _call(lib.fbm_jl_encrypt_phase, *args, _stream(), 1)
         return PendingEncrypt(args, ct, (ws, x, bp, kl), st)
@@ -597,7 +614,8 @@ def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, 
         k1 = min(n_ct, k0 + chunk)
         xs = x[k0 * cr:min(n, k1 * cr)]
         st = _stats(dev)  # one status word per call (each call zeroes its own)
-        _call(lib.fbm_jl_encrypt, _ptr(xs), _x_dtype(x), xs.numel(), c, c2, tf, tm1, int(weight) & U64_MAX, es, cr,
+        _call(lib.fbm_jl_encrypt, _ptr(xs), xdt, xs.shape[0] if kind else xs.numel(), c, c2, tf, tm1,
+              int(weight) & U64_MAX, es, cr,
               _np_ptr(bp), _np_ptr(kl), kneg, int(tau), int(ct_offset) + k0, _ptr(ct[k0:k1]), _ptr(ws), _ptr(st),
               _stream())
         _check_stats_or_defer(st)
@@ -713,6 +731,133 @@ def jl_aggregate(cts: torch.Tensor, biprime: int, key: int, tau: int, n_expected
                   _ptr(factor[k0:k1]), int(total_weight), negc, step, o, sm, _ptr(ws), _ptr(st), _stream())
         _check_stats(st)
     return out, sums
+
+
+# ------------------------------------------------------------------------------------------
+# the JoyeLibert object API (secagg/_jls.py): VES, FDH, ciphertext products, raw decryption
+# ------------------------------------------------------------------------------------------
+def ints_to_u128(values: Sequence[int], dev=None) -> torch.Tensor:
+    """list of ints in [0, 2^128) -> int64 [n, 2] (lo, hi) device tensor; FB624 outside."""
+    vals = values if isinstance(values, list) else list(values)
+    host = host_empty((len(vals), 2), torch.int64)
+    bad = _pyconv().ints_to_bytes(vals, 16, host.numpy()) if vals else -1
+    if bad >= 0:
+        v = vals[bad]
+        if not isinstance(v, int):
+            try:
+                v = v.__index__()
+            except (AttributeError, TypeError):
+                raise TypeError(f"unsupported operand type for VES packing: {type(vals[bad])}") from None
+        raise FedbiomedSecaggCrypterError(
+            f"{ErrorNumbers.FB624.value}: VES value {v} outside [0, 2^128), the device path's domain")
+    return host.to(dev or device())
+
+
+def u128_to_ints(t: torch.Tensor) -> List[int]:
+    a = to_host(t).numpy().view(np.uint64)
+    return [int(lo) | (int(hi) << 64) for lo, hi in a.tolist()]
+
+
+def ints_to_pt(values: Sequence[int], modulus: int, dev=None) -> torch.Tensor:
+    """Plaintext ints -> int32 [n, 32] limbs; values outside [0, 2^1024) are replaced by their
+    residue mod N (N*pt + 1 mod N^2 depends on pt mod N only)."""
+    vals = values if isinstance(values, list) else list(values)
+    host = host_empty((len(vals), 32), torch.int32)
+    buf = host.numpy()
+    bad = _pyconv().ints_to_bytes(vals, 128, buf) if vals else -1
+    while bad >= 0:
+        v = operator.index(vals[bad]) % modulus
+        buf[bad] = np.frombuffer(v.to_bytes(128, "little"), dtype=np.int32)
+        rest = _pyconv().ints_to_bytes(vals[bad + 1:], 128, buf[bad + 1:])
+        bad = -1 if rest < 0 else bad + 1 + rest
+    return host.to(dev or device())
+
+
+def jl_pack(vals: torch.Tensor, es: int, cr: int) -> torch.Tensor:
+    """VES.encode on the device: int64 [n, 2] (lo, hi) values -> int32 [ceil(n/cr), 32] limbs."""
+    n = vals.shape[0]
+    pt = torch.empty(((n + cr - 1) // cr, 32), dtype=torch.int32, device=vals.device)
+    st = _stats(vals.device)
+    _call(N.load().fbm_jl_pack, _ptr(vals.contiguous()), N.FBM_U128, n, int(es), int(cr), _ptr(pt), _ptr(st),
+          _stream())
+    _check_stats(st)
+    return pt
+
+
+def jl_unpack(pt: torch.Tensor, es: int, cr: int, n_out: int) -> torch.Tensor:
+    """VES.decode on the device: int32 [n_ct, 32] limbs -> int64 [n_out, 2] (lo, hi) slot values."""
+    n_ct = pt.shape[0]
+    n_out = max(0, min(int(n_out), n_ct * cr))
+    vals = torch.empty((n_out, 2), dtype=torch.int64, device=pt.device)
+    if n_out:
+        _call(N.load().fbm_jl_unpack, _ptr(pt.contiguous()), n_ct, int(es), int(cr), n_out, _ptr(vals), _stream())
+    return vals
+
+
+def fdh_modulus(m: int) -> Tuple[int, bool]:
+    """FDH gcd modulus M -> (odd part of M or of its square root, M even): gcd(r, M) == 1 iff r
+    is coprime to that odd part (and odd, for an even M).  FB624 outside the device domain."""
+    m = operator.index(m)
+    if m > 0:
+        root = math.isqrt(m)
+        base = root if root * root == m else m
+        even = base % 2 == 0
+        while base and base % 2 == 0:
+            base //= 2
+        if 3 <= base < 2**1024:
+            return base, even
+    raise FedbiomedSecaggCrypterError(
+        f"{ErrorNumbers.FB624.value}: FDH modulus outside the device path's domain (odd part of M or of its "
+        "square root in [3, 2^1024))")
+
+
+def jl_fdh(n_ct: int, modulus: int, tau: int, ct_offset: int = 0, dev=None) -> torch.Tensor:
+    """FDH.H(t_k) of t_k = ((k + ct_offset) << 512) | tau, bits_size 2048, gcd against `modulus`
+    (any M: its odd part, or its square root's) -> int32 [n_ct, 64] limbs."""
+    dev = dev or device()
+    if not (0 <= tau <= U64_MAX and 0 <= ct_offset and ct_offset + max(n_ct, 1) - 1 <= U64_MAX):
+        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: FDH input outside the device path's domain")
+    odd, even = fdh_modulus(modulus)
+    h = torch.empty((n_ct, 64), dtype=torch.int32, device=dev)
+    st = _stats(dev)
+    _call(N.load().fbm_jl_fdh, n_ct, _np_ptr(int_limbs(odd, 32)), 1 if even else 0, int(tau), int(ct_offset),
+          _ptr(h), _ptr(st), _stream())
+    _check_stats(st)
+    return h
+
+
+def jl_product(cts: torch.Tensor, biprime: int) -> torch.Tensor:
+    """prod_u cts[u] mod N^2 (EncryptedNumber sums): int32 [P, n_ct, 64] -> [n_ct, 64], canonical."""
+    P, n_ct, _ = cts.shape
+    out = torch.empty((n_ct, 64), dtype=torch.int32, device=cts.device)
+    if n_ct == 0:
+        return out
+    lib = N.load()
+    bp = _biprime_limbs(biprime)
+    ws = torch.empty(int(lib.fbm_jl_aggregate_workspace(n_ct)), dtype=torch.uint8, device=cts.device)
+    _call(lib.fbm_jl_product, _ptr(cts.contiguous()), P, n_ct, _np_ptr(bp), _ptr(out), _ptr(ws), _stream())
+    return out
+
+
+def jl_decrypt(cts: torch.Tensor, biprime: int, key: int, tau: int, ct_offset: int = 0) -> torch.Tensor:
+    """ServerKey.decrypt (delta = 1) of the product of P ciphertext rows: int32 [P, n_ct, 64] ->
+    x = ((prod * H(t_k)^key mod N^2) - 1) // N mod N as int32 [n_ct, 32] limbs."""
+    P, n_ct, _ = cts.shape
+    dev = cts.device
+    x = torch.empty((n_ct, 32), dtype=torch.int32, device=dev)
+    if n_ct == 0:
+        return x
+    if tau < 0 or tau > U64_MAX:
+        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: round must be in [0, 2^64)")
+    lib = N.load()
+    bp = _biprime_limbs(biprime)
+    kl, kneg = _key_limbs(key)
+    ws = torch.empty(int(lib.fbm_jl_aggregate_workspace(n_ct)), dtype=torch.uint8, device=dev)
+    st = _stats(dev)
+    _call(lib.fbm_jl_decrypt, _ptr(cts.contiguous()), P, n_ct, _np_ptr(bp), _np_ptr(kl), kneg, int(tau),
+          int(ct_offset), _ptr(x), _ptr(ws), _ptr(st), _stream())
+    _check_stats(st)
+    return x
 
 
 # ------------------------------------------------------------------------------------------

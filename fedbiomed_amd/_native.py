@@ -33,6 +33,8 @@ FBM_F32 = 0
 FBM_F64 = 1
 FBM_U64 = 2
 FBM_I64 = 3
+FBM_U128 = 4
+FBM_PT = 5
 STATS_WORDS = 4
 
 _lock = threading.Lock()
@@ -75,6 +77,11 @@ SIGNATURES = {
     "fbm_jl_decrypt_factor_phase": (c_int, [c_u64, c_vp, c_vp, c_int, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp, c_int]),
     "fbm_jl_aggregate_factor": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_u64, c_vp, c_vp, c_u64, c_dbl, c_dbl,
                                         c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "fbm_jl_pack": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_vp, c_vp, c_vp]),
+    "fbm_jl_unpack": (c_int, [c_vp, c_u64, c_int, c_int, c_u64, c_vp, c_vp]),
+    "fbm_jl_fdh": (c_int, [c_u64, c_vp, c_int, c_u64, c_u64, c_vp, c_vp, c_vp]),
+    "fbm_jl_product": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp, c_vp, c_vp]),
+    "fbm_jl_decrypt": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp, c_int, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),
     "fbm_ass_split": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_vp, c_vp, c_u64, c_vp, c_vp]),
     "fbm_ass_reconstruct": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp]),
     "fbm_ass_split_wide": (c_int, [c_vp, c_u64, c_int, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_vp, c_vp]),

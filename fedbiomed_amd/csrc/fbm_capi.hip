@@ -595,7 +595,7 @@ int fbm_check_stats(const uint32_t* st, int lom_nodes, uint32_t* max_bits_out) {
   if (max_bits_out) *max_bits_out = st[FBM_STAT_MAXBITS];
   const uint32_t f = st[FBM_STAT_ERRFLAGS];
   if (f & FBM_ERR_FDH_OVERFLOW) {
-    set_error("FDH: more than 8 digests without gcd(r, N^2) == 1 (reference: OverflowError)");
+    set_error("FDH: no r of 1..7 digests with gcd(r, N^2) == 1 (reference: OverflowError)");
     return FBM_E_FDH;
   }
   if (f & FBM_ERR_NOT_INVERTIBLE) {
@@ -605,6 +605,11 @@ int fbm_check_stats(const uint32_t* st, int lom_nodes, uint32_t* max_bits_out) {
   if (f & FBM_ERR_ITER_CAP) {
     set_error("bounded device loop hit its iteration cap");
     return FBM_E_ITER;
+  }
+  if (f & FBM_ERR_PT_WIDE) {
+    set_error("VES: a packed value spills past the 1024-bit plaintext (a value wider than its slot); "
+              "outside the device path's domain");
+    return FBM_E_UNSUPPORTED;
   }
   if (f & FBM_ERR_DEQUANT_RANGE) {
     set_error("Cannot reverse quantize, received values exceed maximum number");
@@ -737,8 +742,16 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
   if ((phase & 1) && (rc = zero_stats(stats, s))) return rc;
   QuantParams qp;
   if ((rc = quant_params(clip, two_clip, target_f, target_m1, qp))) return rc;
-  if (x_dtype != FBM_F32 && x_dtype != FBM_F64 && x_dtype != FBM_U64) {
-    set_error("x_dtype must be FBM_F32, FBM_F64 or FBM_U64");
+  if (x_dtype != FBM_F32 && x_dtype != FBM_F64 && x_dtype != FBM_U64 && x_dtype != FBM_U128 && x_dtype != FBM_PT) {
+    set_error("x_dtype must be FBM_F32, FBM_F64, FBM_U64, FBM_U128 or FBM_PT");
+    return FBM_E_ARG;
+  }
+  if ((x_dtype == FBM_U128 || x_dtype == FBM_PT) && weight != 1) {
+    set_error("raw-integer / plaintext inputs take weight 1");
+    return FBM_E_ARG;
+  }
+  if (x_dtype == FBM_PT && cr != 1) {
+    set_error("plaintext input (FBM_PT) takes cr = 1");
     return FBM_E_ARG;
   }
   if (!biprime || !key) {
@@ -793,9 +806,12 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
   const bool inverse = key_negative && !is_zero;
   if (phase & 1) {
     if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s); }))) return rc;
-    if ((rc = timed("jl_pack", s, [&] { return launch_jl_pack(x, x_dtype, n, qp, weight, es, cr, n_ct, pt, stats, s); }))) return rc;
+    if (x_dtype != FBM_PT &&
+        (rc = timed("jl_pack", s, [&] { return launch_jl_pack(x, x_dtype, n, qp, weight, es, cr, n_ct, pt, stats, s); })))
+      return rc;
+    const uint32_t* ptp = x_dtype == FBM_PT ? (const uint32_t*)x : pt;  // UserKey.encrypt: packed already
     const int negw = (int64_t)weight < 0 ? 1 : 0;
-    if ((rc = timed("jl_nude", s, [&] { return launch_jl_nude(pt, n_ct, jp, negw, nude, s); }))) return rc;
+    if ((rc = timed("jl_nude", s, [&] { return launch_jl_nude(ptp, n_ct, jp, negw, nude, s); }))) return rc;
     if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, H, stats, s); }))) return rc;
   }
   if (!(phase & 2)) return FBM_OK;
@@ -914,9 +930,11 @@ static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t
 }
 
 // v = prod_u c_u * factor mod N^2, x = (v-1)/N, decode + average + dequantise
+// x_raw != NULL: ServerKey.decrypt's x to x_raw [n_ct][32] instead of decode/average/dequantise
 static int jl_combine_impl(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,
                            const uint32_t* biprime, const uint32_t* factor, uint64_t total_weight, double neg_clip,
-                           double step, double* out, uint64_t* sums, const JlAggWs& w, uint32_t* stats, hipStream_t s) {
+                           double step, double* out, uint64_t* sums, const JlAggWs& w, uint32_t* stats, hipStream_t s,
+                           uint32_t* x_raw = nullptr) {
   JlParams jp;
   int rc;
   if ((rc = build_jl_params(biprime, es, cr, 0, 0, jp))) return rc;
@@ -928,8 +946,10 @@ static int jl_combine_impl(const uint32_t* cts, int n_parties, uint64_t n_ct, in
     jl_rk_for(jp.N32, n_parties, r);
     if ((rc = timed("jl_rk", s, [&] { return launch_jl_rk(r, w.cst, s); }))) return rc;
   }
-  if ((rc = timed("jl_prod", s, [&] { return launch_jl_prod(cts, n_parties, n_ct, jp, w.cst, factor, w.X, w.xs, s); })))
+  uint32_t* xs = x_raw ? x_raw : w.xs;
+  if ((rc = timed("jl_prod", s, [&] { return launch_jl_prod(cts, n_parties, n_ct, jp, w.cst, factor, w.X, xs, s); })))
     return rc;
+  if (x_raw) return FBM_OK;
   return timed("jl_decode", s, [&] {
     return launch_jl_decode(w.xs, es, cr, n_out, total_weight, neg_clip, step, out, sums, stats, s);
   });
@@ -1021,6 +1041,109 @@ int fbm_jl_aggregate_factor(const uint32_t* cts, int n_parties, uint64_t n_ct, i
   }
   return jl_combine_impl(cts, n_parties, n_ct, es, cr, n_out, biprime, factor, total_weight, neg_clip, step, out, sums,
                          agg_ws(workspace, n_ct), stats, s);
+}
+
+// ---- the JoyeLibert object API (fedbiomed_amd/secagg/_jls.py) ----
+int fbm_jl_pack(const void* x, int x_dtype, uint64_t n, int es, int cr, uint32_t* pt, uint32_t* stats, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc = zero_stats(stats, s);
+  if (rc) return rc;
+  if (x_dtype != FBM_U128) {
+    set_error("fbm_jl_pack takes FBM_U128 values");
+    return FBM_E_ARG;
+  }
+  if (es < 1 || cr < 1 || (int64_t)es * cr > 1024) {
+    set_error("invalid VES parameters es=%d cr=%d", es, cr);
+    return FBM_E_ARG;
+  }
+  if (n == 0) return FBM_OK;
+  if (!x || !pt) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  const uint64_t n_ct = (n + (uint64_t)cr - 1) / (uint64_t)cr;
+  QuantParams qp{};
+  return timed("jl_pack", s, [&] { return launch_jl_pack(x, x_dtype, n, qp, 1, es, cr, n_ct, pt, stats, s); });
+}
+
+int fbm_jl_unpack(const uint32_t* pt, uint64_t n_ct, int es, int cr, uint64_t n_out, uint64_t* vals, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (es < 1 || es > 128 || cr < 1 || (int64_t)es * cr > 1024) {
+    set_error("invalid VES parameters es=%d cr=%d (device decode: es <= 128)", es, cr);
+    return FBM_E_ARG;
+  }
+  if (n_out > n_ct * (uint64_t)cr) n_out = n_ct * (uint64_t)cr;
+  if (n_out == 0) return FBM_OK;
+  if (!pt || !vals) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  return timed("jl_decode", s, [&] { return launch_jl_decode(pt, es, cr, n_out, 1, 0.0, 1.0, nullptr, vals, nullptr, s); });
+}
+
+int fbm_jl_fdh(uint64_t n_ct, const uint32_t* modulus_odd, int modulus_even, uint64_t tau, uint64_t ct_offset,
+               uint32_t* h, uint32_t* stats, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc = zero_stats(stats, s);
+  if (rc) return rc;
+  if (!modulus_odd) {
+    set_error("null modulus");
+    return FBM_E_ARG;
+  }
+  JlParams jp;
+  if ((rc = build_jl_params(modulus_odd, 1, 1, tau, ct_offset, jp))) return rc;
+  jp.fdh_even = modulus_even ? 1 : 0;
+  if (n_ct == 0) return FBM_OK;
+  if (!h) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  return timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, h, stats, s); });
+}
+
+int fbm_jl_product(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* biprime, uint32_t* out,
+                   void* workspace, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc;
+  if ((rc = jl_agg_checks(n_parties, n_ct, biprime, 1))) return rc;
+  if (n_ct == 0) return FBM_OK;
+  if (!cts || !out || !workspace) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  const JlAggWs w = agg_ws(workspace, n_ct);
+  JlParams jp;
+  if ((rc = build_jl_params(biprime, 1, 1, 0, 0, jp))) return rc;
+  JlSched none;
+  memset(&none, 0, sizeof(none));
+  if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, none, w.ops, w.cst, s); }))) return rc;
+  {  // R^P: P products, each dropping one R
+    JlRk r;
+    jl_rk_for(jp.N32, n_parties - 1, r);
+    if ((rc = timed("jl_rk", s, [&] { return launch_jl_rk(r, w.cst, s); }))) return rc;
+  }
+  return timed("jl_prod", s, [&] { return launch_jl_prod(cts, n_parties, n_ct, jp, w.cst, nullptr, w.X, out, s); });
+}
+
+int fbm_jl_decrypt(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* biprime, const uint32_t* key,
+                   int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* x, void* workspace, uint32_t* stats,
+                   void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc = zero_stats(stats, s);
+  if (rc) return rc;
+  if ((rc = jl_agg_checks(n_parties, n_ct, biprime, 1))) return rc;
+  if (!key) {
+    set_error("null key");
+    return FBM_E_ARG;
+  }
+  if (n_ct == 0) return FBM_OK;
+  if (!cts || !x || !workspace) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  const JlAggWs w = agg_ws(workspace, n_ct);
+  if ((rc = jl_factor_impl(n_ct, biprime, key, key_negative, tau, ct_offset, w.F, w, stats, s))) return rc;
+  return jl_combine_impl(cts, n_parties, n_ct, 1, 1, 0, biprime, w.F, 1, 0.0, 1.0, nullptr, nullptr, w, stats, s, x);
 }
 
 int fbm_jl_batch_begin(void) { return jl_batch_begin(); }

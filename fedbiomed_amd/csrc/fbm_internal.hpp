@@ -13,9 +13,10 @@
 #define FBM_STAT_COUNT 4
 
 #define FBM_ERR_DEQUANT_RANGE 1u   // averaged value > 2^64-1 (reverse_quantize FB624)
-#define FBM_ERR_FDH_OVERFLOW 2u    // > 8 non-coprime FDH digests (reference: OverflowError)
+#define FBM_ERR_FDH_OVERFLOW 2u    // no coprime r of 1..7 FDH digests (reference: OverflowError)
 #define FBM_ERR_NOT_INVERTIBLE 4u  // server-key power not invertible mod N^2
 #define FBM_ERR_ITER_CAP 8u        // a bounded data-dependent loop hit its cap
+#define FBM_ERR_PT_WIDE 32u        // VES: a packed value spills past the 1024-bit plaintext
 #define FBM_WARN_CLIPPED 16u       // not an error: some |x| > clipping range (the reference's
                                    // _check_clipping_range warning, _secagg_utils.py:189-204)
 
@@ -128,7 +129,7 @@ struct JlParams {
   uint32_t mid[8];               // SHA-256 state after the 14 all-zero message blocks
   FbmN30 n30;                    // N in signed-30 limbs + N^-1 mod 2^30 (modular inverse)
   int key_is_zero;
-  int pad;
+  int fdh_even;                  // FDH.H standalone: the modulus is even (r must be odd as well)
   uint32_t mneg[FBM_NLN];        // N * 2^(1036 - bits(N)) in 28-bit limbs (negative-weight packing)
   uint32_t pad2[3];
   QuadCtx qa;                    // quad exponentiation engine constants

@@ -101,6 +101,44 @@ __global__ void __launch_bounds__(256) jl_pack_kernel(const XT* __restrict__ x, 
   flag_if_any(clipped, stats, FBM_WARN_CLIPPED);
 }
 
+// VES.encode of raw integers (JoyeLibert.protect / VES.encode on int lists, _jls.py:118-144,
+// 169-176): values are (lo, hi) uint64 pairs, v < 2^128, ORed into slot j at bit es*j with the
+// reference's OR semantics also for a value wider than its slot (its high bits land in the
+// next slots).  Slot j reaches limb L (bits [32L, 32L+32)) iff es*j < 32L + 32 and
+// es*j + 128 > 32L.  A bit at or above 2^1024 (only possible for a value wider than its slot
+// in the last slots) flags FBM_ERR_PT_WIDE: outside the 1024-bit plaintext the device keeps.
+__global__ void __launch_bounds__(256) jl_pack_wide_kernel(const uint64_t* __restrict__ x, uint64_t n, int es,
+                                                           int cr, uint64_t n_ct, uint32_t* __restrict__ pt,
+                                                           uint32_t* __restrict__ stats) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t ct = gid >> 5;
+  const int L = (int)(gid & 31);
+  if (ct >= n_ct) return;
+  const uint64_t first = ct * (uint64_t)cr;
+  const int cnt = (n - first) >= (uint64_t)cr ? cr : (int)(n - first);
+  const int lo_bit = 32 * L;
+  int j0 = lo_bit >= 128 ? (lo_bit - 128) / es + 1 : 0;
+  int j1 = (lo_bit + 31) / es;
+  if (j1 > cnt - 1) j1 = cnt - 1;
+  uint32_t w = 0;
+  for (int j = j0; j <= j1; ++j) {
+    const unsigned __int128 v = ((unsigned __int128)x[2 * (first + j) + 1] << 64) | x[2 * (first + j)];
+    const int sh = es * j - lo_bit;
+    w |= sh >= 0 ? (uint32_t)(v << sh) : (uint32_t)(v >> (-sh));
+  }
+  pt[ct * 32 + L] = w;
+  if (L == 31) {  // bits past 2^1024: slots with es*j + 128 > 1024
+    bool wide = false;
+    for (int j = 0; j < cnt; ++j) {
+      if (es * j + 128 <= 1024) continue;
+      const unsigned __int128 v = ((unsigned __int128)x[2 * (first + j) + 1] << 64) | x[2 * (first + j)];
+      const int room = 1024 - es * j;  // bits of v that stay below 2^1024
+      wide |= room <= 0 ? v != 0 : (v >> room) != 0;
+    }
+    if (wide) atomicOr(stats + FBM_STAT_ERRFLAGS, FBM_ERR_PT_WIDE);
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // nude = N*pt + 1 as the N-adic digit pair (1, pt)  ->  [limb][ct] 28-bit limbs (the last
 // operand of jl_exp_kernel's encrypt; pt < 2^1024 < R is a valid one-off digit)
@@ -303,8 +341,10 @@ __host__ __device__ inline bool gcd_is_one_r8(const uint32_t (&r)[8], const uint
 // FDH.H(t_k): message = t.to_bytes(1024,'big') || counter (1 byte).  Blocks 0..13 are
 // all zero for k < 2^64 (midstate from the host), block 14 carries k, block 15 tau,
 // block 16 the counter byte + padding (length 8200 bits).  While gcd(r, N^2) != 1 the
-// counter is bumped and r grows by one digest (r = D1 || D2 || ...); more than 8 digests
-// is the reference's OverflowError.
+// counter is bumped and r grows by one digest (r = D1 || D2 || ...).  r is tested with 1..7
+// digests only: once 8 digests (256 bytes = bits_size // 8) are in, the reference's inner
+// loop (_jls.py:746-755) never breaks again and counter.to_bytes(1) overflows at 256 -- its
+// OverflowError, whatever gcd the 8-digest r would have.
 __global__ void __launch_bounds__(256) jl_fdh_kernel(uint64_t n_ct, JlParams jp, uint32_t* __restrict__ H,
                                                      uint32_t* __restrict__ stats) {
   const uint64_t kl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -326,7 +366,7 @@ __global__ void __launch_bounds__(256) jl_fdh_kernel(uint64_t n_ct, JlParams jp,
 #pragma unroll
   for (int i = 0; i < 64; ++i) r[i] = 0u;
   bool ok = false;
-  for (uint32_t c = 1; c <= 8 && !ok; ++c) {
+  for (uint32_t c = 1; c <= 7 && !ok; ++c) {
     uint32_t d[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) d[i] = st[i];
@@ -339,7 +379,9 @@ __global__ void __launch_bounds__(256) jl_fdh_kernel(uint64_t n_ct, JlParams jp,
     for (int i = 63; i >= 8; --i) r[i] = r[i - 8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) r[i] = d[7 - i];
-    if (c == 1) {  // one digest: r = d (8 limbs)
+    if (jp.fdh_even && !(r[0] & 1u)) {  // an even modulus 2^s N: gcd = 1 needs r odd too
+      ok = false;
+    } else if (c == 1) {  // one digest: r = d (8 limbs)
       uint32_t r8[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) r8[i] = r[i];
@@ -1050,6 +1092,8 @@ __device__ __forceinline__ void div_by_n(uint32_t (&D)[64], const JlParams& jp, 
 //   b = c_u, u = 1 .. P-1, then b = F                        -> each drops one R -> v (lazy)
 // P + 1 products, no Montgomery-form round trips; any c_u < 2^2048 qualifies (a b < R M).
 // ------------------------------------------------------------------------------------
+// factor == nullptr: the bare product (EncryptedNumber sums, _jls.py:353-374): a starts from
+// R^P, P products, and the canonical v goes to xout [ct][64] (no decryption).
 __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_prod_kernel(const uint32_t* __restrict__ cts, int n_parties,
                                                               uint64_t n_ct, const uint32_t* __restrict__ cst,
                                                               JlParams jp, const uint32_t* __restrict__ factor,
@@ -1064,8 +1108,9 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_prod_kernel(const uint32_t* _
   const uint64_t ct = valid ? ct_raw : n_ct - 1;
   const uint32_t xoff = (uint32_t)(((ct_raw >> 8) * (FBM_NL * 256) + (ct_raw & 255)) * 4);
   lds_store_uniform<FBM_NL>(lds, FBM_BLOCK, cst + FBM_CST_RK);
+  const int n_ops = n_parties + (factor ? 1 : 0);
 #pragma unroll 1
-  for (int u = 0; u <= n_parties; ++u) {
+  for (int u = 0; u < n_ops; ++u) {
     {
       const uint32_t* row = u < n_parties ? cts + ((uint64_t)u * n_ct + ct) * 64 : factor + ct * 64;
       uint32_t c32[64], c28[FBM_NL];
@@ -1081,6 +1126,10 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_prod_kernel(const uint32_t* _
     lds_load_col(lds, FBM_BLOCK, v);
     mont_csub(v, jp.mc.M);
     from28<FBM_NL, 64>(v, D);
+  }
+  if (!factor) {
+    if (valid) store_row64(xout + ct * 64, D);
+    return;
   }
   uint32_t br = 1;  // D = v - 1
 #pragma unroll
@@ -1372,6 +1421,9 @@ int launch_jl_pack(const void* x, int x_dtype, uint64_t n, const QuantParams& qp
   else if (x_dtype == FBM_F64)
     hipLaunchKernelGGL(jl_pack_kernel<double>, grid1(n_ct * 32, 256), dim3(256), 0, s, (const double*)x, n, qp,
                        weight, es, cr, n_ct, pt, stats);
+  else if (x_dtype == FBM_U128)
+    hipLaunchKernelGGL(jl_pack_wide_kernel, grid1(n_ct * 32, 256), dim3(256), 0, s, (const uint64_t*)x, n, es, cr,
+                       n_ct, pt, stats);
   else
     hipLaunchKernelGGL(jl_pack_kernel<uint64_t>, grid1(n_ct * 32, 256), dim3(256), 0, s, (const uint64_t*)x, n, qp,
                        weight, es, cr, n_ct, pt, stats);

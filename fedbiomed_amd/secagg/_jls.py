@@ -1,0 +1,408 @@
+"""Joye-Libert objects mirroring the reference class API (fedbiomed/common/secagg/_jls.py):
+VES, PublicParam, EncryptedNumber, BaseKey, UserKey, ServerKey, JoyeLibert and FDH, for
+callers and tests that use them directly (SecaggCrypter itself runs the fused tensor path).
+
+Every vector operation runs in the gfx950 kernels through the C-ABI (include/fbm_secagg.h):
+
+    VES.encode / VES.decode           fbm_jl_pack / fbm_jl_unpack        _jls.py:118-192
+    FDH.H, BaseKey._populate_tau      fbm_jl_fdh                         _jls.py:451-467, 727-762
+    UserKey.encrypt                   fbm_jl_encrypt (FBM_PT)            _jls.py:473-505
+    EncryptedNumber sums              fbm_jl_product                     _jls.py:308-374
+    ServerKey.decrypt                 fbm_jl_decrypt                     _jls.py:520-562
+    JoyeLibert.protect                fbm_jl_encrypt (FBM_U128)          _jls.py:593-644
+    JoyeLibert.aggregate              fbm_jl_aggregate (decoded sums)    _jls.py:646-699
+
+A sum of EncryptedNumbers keeps its operands until its ciphertext is read (then one device
+product), so `[sum(ep) for ep in zip(*parties)]` followed by ServerKey.decrypt is one device
+call, as JoyeLibert.aggregate is.
+
+Domain of the device path (FB624 outside it): N odd, 3 <= N < 2^1024; a
+PublicParam with bits = 1024 whose hashing function is FDH(2048, N^2).H (what
+SecaggCrypter._setup_public_param builds); tau in [0, 2^64); VES values in [0, 2^128) with
+es <= 100; ServerKey.decrypt with delta^2 = 1 (mod N).  Integers are Python ints (gmpy2 is
+not a dependency): where the reference returns gmpy2.mpz this returns int, and FDH takes an
+int modulus.
+"""
+
+import math
+import operator
+from typing import Callable, List, Optional, Tuple, Union
+
+import numpy as np
+import torch
+
+from .. import _device as D
+from ..constants import ErrorNumbers, SAParameters
+from ..exceptions import FedbiomedSecaggCrypterError
+
+_TAU_SHIFT_BITS = SAParameters.KEY_SIZE // 2  # PublicParam.bits of SecaggCrypter._setup_public_param
+
+
+def _unsupported(what: str) -> FedbiomedSecaggCrypterError:
+    return FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: {what} is outside the device path's domain")
+
+
+def _is_integer(v) -> bool:
+    return (isinstance(v, int) and not isinstance(v, bool)) or type(v).__name__ == "mpz"
+
+
+class VES:
+    """The vector encoding class (reference _jls.py:76-192): packs `comp_ratio` values of
+    `element_size` bits into one plaintext, on the device."""
+
+    def __init__(self, ptsize: int, valuesize: int) -> None:
+        self._ptsize: int = ptsize
+        self._valuesize: int = valuesize
+
+    def _get_elements_size_and_compression_ratio(self, add_ops: int) -> Tuple[int, int]:
+        """reference _jls.py:104-116"""
+        element_size = self._valuesize + math.ceil(math.log2(add_ops + 1))
+        comp_ratio = math.floor(self._ptsize / element_size)
+        return element_size, comp_ratio
+
+    def _slot(self, add_ops: int) -> Tuple[int, int]:
+        es, cr = self._get_elements_size_and_compression_ratio(add_ops)
+        if cr < 1 or es > 100 or es * cr > 1024:
+            raise _unsupported(f"VES slot of {es} bits x {cr} (ptsize {self._ptsize})")
+        return es, cr
+
+    def encode(self, V: List[int], add_ops: int) -> List[int]:
+        """reference _jls.py:118-144 (OR packing, _batch :169-176) -- fbm_jl_pack."""
+        es, cr = self._slot(add_ops)
+        if not V:
+            return []
+        pt = D.jl_pack(D.ints_to_u128(V), es, cr)
+        return D.limbs_to_ints_w(pt, 32)
+
+    def decode(self, E: List[int], add_ops: int, v_expected: int) -> List[int]:
+        """reference _jls.py:146-167 (_debatch :179-192): slot j = (e >> es*j) & (2^es - 1),
+        min(remaining, comp_ratio) values per plaintext -- fbm_jl_unpack."""
+        es, cr = self._slot(add_ops)
+        if es > 128:
+            raise _unsupported(f"VES decode of {es}-bit slots")
+        if not E or v_expected <= 0:
+            return []
+        # only the low es*cr <= 1024 bits of a plaintext are read: two's-complement truncation
+        pts = D.ints_to_pt([int(e) & ((1 << 1024) - 1) for e in E], 1 << 1024)
+        return D.u128_to_ints(D.jl_unpack(pts, es, cr, v_expected))
+
+
+class PublicParam:
+    """The public parameters for Joye-Libert Scheme (reference _jls.py:195-286)."""
+
+    def __init__(self, n_modulus: int, bits: int, hashing_function: Callable) -> None:
+        self._n_modulus = n_modulus
+        self._n_square = n_modulus * n_modulus
+        self._bits = bits
+        self._hashing_function = hashing_function
+
+    @property
+    def bits(self) -> int:
+        return self._bits
+
+    @property
+    def n_modulus(self) -> int:
+        return self._n_modulus
+
+    @property
+    def n_square(self) -> int:
+        return self._n_square
+
+    def hashing_function(self, val: int):
+        return self._hashing_function(val)
+
+    def __eq__(self, other: "PublicParam") -> bool:
+        return self._n_modulus == other.n_modulus
+
+    __hash__ = None  # as the reference: __eq__ without __hash__
+
+    def __repr__(self) -> str:
+        hashcode = hex(hash(self._hashing_function))
+        n_str = str(int(self._n_modulus))
+        return "<PublicParam (N={}...{}, H(x)={})>".format(n_str[:5], n_str[-5:], hashcode[:10])
+
+
+def _device_n(pp: PublicParam) -> int:
+    """N of a PublicParam the device path can encrypt/decrypt under (its FDH, bits 1024)."""
+    fdh = getattr(pp._hashing_function, "__self__", None)
+    n = int(pp.n_modulus)
+    if not (isinstance(fdh, FDH) and getattr(pp._hashing_function, "__func__", None) is FDH.H
+            and fdh.bits_size == SAParameters.KEY_SIZE and int(fdh._n_modules) == n * n
+            and pp.bits == _TAU_SHIFT_BITS):
+        raise _unsupported("a PublicParam whose hashing function is not FDH(2048, N^2).H with bits 1024")
+    if n < 3 or n % 2 == 0 or n.bit_length() > 1024:
+        raise _unsupported("a modulus N that is not odd in [3, 2^1024)")
+    return n
+
+
+def _check_tau(tau) -> int:
+    t = operator.index(tau)
+    if not 0 <= t < 2**64:
+        raise _unsupported(f"round tau={t} (device path: 0 <= tau < 2^64)")
+    return t
+
+
+class EncryptedNumber(object):
+    """An encrypted number by one of the user keys (reference _jls.py:289-374).  A sum keeps
+    its operands until `ciphertext` is read: the product mod N^2 then runs on the device."""
+
+    def __init__(self, param: PublicParam, ciphertext: int):
+        self.public_param = param
+        self.ciphertext = ciphertext
+
+    @classmethod
+    def _of_terms(cls, param: PublicParam, terms: Tuple[int, ...]) -> "EncryptedNumber":
+        e = cls.__new__(cls)
+        e.public_param = param
+        e._terms, e._value = terms, None
+        return e
+
+    @property
+    def ciphertext(self) -> int:
+        if self._value is None:
+            self._value = _materialize([self])[0]
+            self._terms = (self._value,)
+        return self._value
+
+    @ciphertext.setter
+    def ciphertext(self, value) -> None:
+        v = int(value)  # gmpy2.mpz(value) in the reference
+        self._terms, self._value = (v,), v
+
+    def __add__(self, other: "EncryptedNumber") -> "EncryptedNumber":
+        if not isinstance(other, EncryptedNumber):
+            raise TypeError(
+                "Encrypted number can be only summed with another Encrypted num."
+                f"Can not sum Encrypted number with type {type(other)}"
+            )
+        return self._add_encrypted(other)
+
+    def __iadd__(self, other):
+        return self.__add__(other)
+
+    def __radd__(self, other: Union["EncryptedNumber", int]) -> "EncryptedNumber":
+        if other == 0:
+            return self
+        return self.__add__(other)
+
+    def __repr__(self) -> str:
+        r = str(self.ciphertext)
+        return "<EncryptedNumber {}...{}>".format(r[:5], r[-5:])
+
+    def _add_encrypted(self, other: "EncryptedNumber") -> "EncryptedNumber":
+        if self.public_param != other.public_param:
+            raise ValueError("Attempted to add numbers encrypted against different parameters!")
+        return EncryptedNumber._of_terms(self.public_param, self._terms + other._terms)
+
+
+def _term_rows(nums: List[EncryptedNumber], n: int) -> torch.Tensor:
+    """int32 [P, len(nums), 64] limbs of the numbers' product operands, shorter products
+    padded with the identity 1 (P = the most operands of any number)."""
+    P = max((len(e._terms) for e in nums), default=1)
+    host = D.host_empty((P, len(nums), 64), torch.int32)
+    buf = host.numpy().view(np.uint32)
+    for u in range(P):
+        col = [e._terms[u] if u < len(e._terms) else 1 for e in nums]
+        D.ints_to_limbs(col, n * n, out=buf[u])
+    return host.to(D.device())
+
+
+def _sum_column(col) -> Union[EncryptedNumber, int]:
+    """sum(col) with the reference's operand and parameter checks (_jls.py:308-374, 691-693);
+    no arithmetic: the sum carries every operand to the device product."""
+    if col and all(type(e) is EncryptedNumber for e in col):
+        p0 = col[0].public_param
+        if all(e.public_param is p0 for e in col) or all(p0 == e.public_param for e in col[1:]):
+            if len(col) == 1:
+                return col[0]
+            return EncryptedNumber._of_terms(p0, tuple(t for e in col for t in e._terms))
+    acc = 0
+    for e in col:  # the general case, raising where sum() raises
+        acc = acc + e
+    return acc
+
+
+def _materialize(nums: List[EncryptedNumber]) -> List[int]:
+    """Ciphertexts of (lazy) sums: one device product over all of them."""
+    n = _modulus_of(nums[0].public_param)
+    return D.limbs_to_ints(D.to_host(D.jl_product(_term_rows(nums, n), n)).numpy())
+
+
+def _modulus_of(pp: PublicParam) -> int:
+    n = int(pp.n_modulus)
+    if n < 3 or n % 2 == 0 or n.bit_length() > 1024:
+        raise _unsupported("a modulus N that is not odd in [3, 2^1024)")
+    return n
+
+
+class BaseKey:
+    """A base key class for Joye-Libert Scheme (reference _jls.py:377-467)."""
+
+    def __init__(self, public_param: PublicParam, key: int):
+        if not isinstance(key, int):
+            raise TypeError("The key should be type of integer")
+        self._public_param = public_param
+        self._key = int(key)
+
+    @property
+    def public_param(self) -> PublicParam:
+        return self._public_param
+
+    @property
+    def key(self) -> int:
+        return self._key
+
+    def __repr__(self):
+        hashcode = hex(hash(self))
+        return "<ServerKey {}>".format(hashcode[:10])
+
+    def __eq__(self, other: Union["BaseKey", "ServerKey", "UserKey"]) -> bool:
+        if not isinstance(other, type(self)):
+            raise TypeError(f"The key can not be compared with type {type(other)}")
+        return self._public_param == other.public_param and self._key == other.key
+
+    def __hash__(self) -> int:
+        return hash(self._key)
+
+    def _populate_tau(self, tau: int, len_: int):
+        """reference _jls.py:451-467: [H((k << bits/2) | tau) for k < len_] -- one fbm_jl_fdh
+        launch when the hashing function is an FDH of bits_size 2048 and bits is 1024; any
+        other hashing function is the caller's own callable and is called per t."""
+        pp = self._public_param
+        fdh = getattr(pp._hashing_function, "__self__", None)
+        if (isinstance(fdh, FDH) and getattr(pp._hashing_function, "__func__", None) is FDH.H
+                and pp.bits == _TAU_SHIFT_BITS):
+            return fdh._hash_range(tau, len_)
+        return [pp.hashing_function((k << (pp.bits // 2)) | tau) for k in range(len_)]
+
+
+class UserKey(BaseKey):
+    """A user key for Joye-Libert Scheme (reference _jls.py:470-505)."""
+
+    def encrypt(self, plaintext: List[int], tau: int) -> List[int]:
+        """c_k = (N pt_k + 1) H(t_k)^key mod N^2 -- fbm_jl_encrypt on plaintext limbs."""
+        if not isinstance(plaintext, list):
+            raise TypeError(f"Expected plaintext type list but got {type(plaintext)}")
+        n = _device_n(self._public_param)
+        tau = _check_tau(tau)
+        if not plaintext:
+            return []
+        pts = D.ints_to_pt(plaintext, n)
+        ct = D.jl_encrypt(pts, n, self._key, tau, 1, kind="pt")
+        return D.limbs_to_ints(D.to_host(ct).numpy())
+
+
+class ServerKey(BaseKey):
+    """A server key for Joye-Libert Scheme (reference _jls.py:508-562)."""
+
+    def __init__(self, public_param: PublicParam, key: int) -> None:
+        super().__init__(public_param, key)
+
+    def decrypt(self, cipher: List[EncryptedNumber], tau: int, delta: int = 1) -> List[int]:
+        """x_k = ((c_k H(t_k)^(delta^2 key) mod N^2) - 1) // N mod N, times delta^-2 mod N --
+        fbm_jl_decrypt (the product of a lazy sum's operands runs in the same call)."""
+        if not isinstance(cipher, list):
+            raise TypeError(f"Expected `cipher` is list of encrypter numbers but got {type(cipher)}")
+        if not all([isinstance(c, EncryptedNumber) for c in cipher]):
+            raise TypeError("Cipher text should be list of EncryptedNumbers")
+        n = _device_n(self._public_param)
+        d2 = delta ** 2
+        if math.gcd(d2 % (n * n), n * n) != 1:
+            raise ZeroDivisionError("invert() no inverse exists")
+        if d2 % n != 1:
+            raise _unsupported("ServerKey.decrypt with delta^2 != 1 (mod N)")
+        tau = _check_tau(tau)
+        if not cipher:
+            return []
+        x = D.jl_decrypt(_term_rows(cipher, n), n, d2 * self._key, tau)
+        return D.limbs_to_ints_w(x, 32)
+
+
+class JoyeLibert:
+    """The Joye-Libert scheme (reference _jls.py:565-699): Protect and Agg."""
+
+    def __init__(self, target_range: Optional[int] = None):
+        target_range = target_range or SAParameters.TARGET_RANGE
+        self._vector_encoder = VES(
+            ptsize=SAParameters.KEY_SIZE // 2,
+            valuesize=math.ceil(math.log2(target_range) + math.log2(SAParameters.WEIGHT_RANGE)),
+        )
+
+    def protect(self, public_param: PublicParam, user_key: UserKey, tau: int, x_u_tau: List[int],
+                n_users: int) -> List[int]:
+        """y = (1 + x N) H(tau)^sk_u mod N^2 of the VES-packed input -- one fbm_jl_encrypt."""
+        if not isinstance(user_key, UserKey):
+            raise TypeError(f"Expected key for encryption type is UserKey. but got {type(user_key)}")
+        if user_key.public_param != public_param:
+            raise ValueError(
+                "Bad public parameter. The public parameter of user key does not match the "
+                "one given for encryption"
+            )
+        if not isinstance(x_u_tau, list):
+            raise TypeError(
+                f"Bad vector for encryption. Excepted argument `x_u_tau` type list but "
+                f"got {type(x_u_tau)}"
+            )
+        es, cr = self._vector_encoder._slot(n_users)
+        n = _device_n(user_key.public_param)
+        tau = _check_tau(tau)
+        if not x_u_tau:
+            return []
+        ct = D.jl_encrypt(D.ints_to_u128(x_u_tau), n, user_key.key, tau, n_users, slot=(es, cr), kind="u128")
+        return D.limbs_to_ints(D.to_host(ct).numpy())
+
+    def aggregate(self, sk_0: ServerKey, tau: int, list_y_u_tau: List[List[EncryptedNumber]],
+                  num_expected_params: int) -> List[int]:
+        """X = ((prod_u y_u * H(tau)^sk_0 mod N^2) - 1) // N mod N, VES-decoded -- one
+        fbm_jl_aggregate (product, server-key factor, decryption and decode on the device)."""
+        if not isinstance(sk_0, ServerKey):
+            raise ValueError("Key must be an instance of `ServerKey`")
+        if not isinstance(list_y_u_tau, list) or not list_y_u_tau:
+            raise ValueError("list_y_u_tau should be a non-empty list.")
+        if not isinstance(list_y_u_tau[0], list):
+            raise ValueError("list_y_u_tau should be a list that contains list of encrypted numbers")
+        n_user = len(list_y_u_tau)
+        summed = [_sum_column(col) for col in zip(*list_y_u_tau)]  # strict=False: shortest length
+        # ServerKey.decrypt's checks, then the decode's slot
+        if not all([isinstance(c, EncryptedNumber) for c in summed]):
+            raise TypeError("Cipher text should be list of EncryptedNumbers")
+        n = _device_n(sk_0.public_param)
+        tau = _check_tau(tau)
+        es, cr = self._vector_encoder._slot(n_user)
+        if es > 128:
+            raise _unsupported(f"VES decode of {es}-bit slots")
+        if not summed:
+            return []
+        _, sums = D.jl_aggregate(_term_rows(summed, n), n, sk_0.key, tau, num_expected_params, 1,
+                                 want_out=False, want_sums=True, slot=(es, cr))
+        return D.u128_to_ints(sums)
+
+
+class FDH:
+    """The Full-Domain Hash scheme (reference _jls.py:702-762), on the device."""
+
+    def __init__(self, bits_size: int, n_modulus: int) -> None:
+        if not isinstance(bits_size, int):
+            raise TypeError(f"Bits size should be an integer not {type(bits_size)}")
+        if not _is_integer(n_modulus):
+            raise TypeError(f"n_modules should be of type `gmpy2.mpz` not {type(n_modulus)}")
+        self.bits_size = bits_size
+        self._n_modules = n_modulus
+
+    def _hash_range(self, tau: int, len_: int, k0: int = 0) -> List[int]:
+        if self.bits_size != SAParameters.KEY_SIZE:
+            raise _unsupported(f"FDH of bits_size {self.bits_size} (device path: {SAParameters.KEY_SIZE})")
+        tau = _check_tau(tau)
+        if len_ <= 0:
+            return []
+        h = D.jl_fdh(len_, int(self._n_modules), tau, k0)
+        return D.limbs_to_ints(D.to_host(h).numpy())
+
+    def H(self, t: int) -> int:
+        """SHA256(t || 1) || SHA256(t || 2) || ... until gcd(r, n_modulus) == 1, t as 1024
+        big-endian bytes -- fbm_jl_fdh with t = (k << 512) | tau (k, tau < 2^64)."""
+        t = operator.index(t)
+        k, tau = t >> 512, t & ((1 << 512) - 1)
+        if t < 0 or k >= 2**64 or tau >= 2**64:
+            raise _unsupported("FDH input t outside {(k << 512) | tau : k, tau < 2^64}")
+        return self._hash_range(tau, 1, k)[0]

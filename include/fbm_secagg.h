@@ -34,7 +34,7 @@ extern "C" {
 #define FBM_E_HIP (-2)         /* HIP runtime / launch failure                             */
 #define FBM_E_RANGE (-3)       /* averaged value > 2^64-1 (reverse_quantize)  -> FB624      */
 #define FBM_E_OVERFLOW (-4)    /* LOM overflow guard (_lom.py:133-150)        -> FB417      */
-#define FBM_E_FDH (-5)         /* > 8 non-coprime FDH digests (_jls.py:742-760: OverflowError) */
+#define FBM_E_FDH (-5)         /* no coprime r of 1..7 FDH digests (_jls.py:742-760: OverflowError) */
 #define FBM_E_INVERSE (-6)     /* H^|sk0| not invertible mod N^2 (gmpy2: ZeroDivisionError) */
 #define FBM_E_ITER (-7)        /* a bounded data-dependent device loop hit its cap          */
 #define FBM_E_UNSUPPORTED (-8) /* parameters outside the device path's domain (documented)  */
@@ -43,6 +43,8 @@ extern "C" {
 #define FBM_F64 1
 #define FBM_U64 2 /* raw integer input (LOM.protect / JoyeLibert.protect on ints); no quantisation */
 #define FBM_I64 3 /* signed 64-bit integers (additive secret sharing)                           */
+#define FBM_U128 4 /* raw integers < 2^128 as (lo, hi) uint64 pairs: JoyeLibert.protect / VES.encode */
+#define FBM_PT 5   /* packed JL plaintexts, n x 32 uint32 limbs (UserKey.encrypt; cr = 1)          */
 
 #define FBM_STATS_WORDS 4
 
@@ -164,6 +166,35 @@ int fbm_jl_decrypt_factor_phase(uint64_t n_ct, const uint32_t* biprime, const ui
 int fbm_jl_aggregate_factor(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,
                             const uint32_t* biprime, const uint32_t* factor, uint64_t total_weight, double neg_clip,
                             double step, double* out, uint64_t* sums, void* workspace, uint32_t* stats, void* stream);
+
+/* ---- the JoyeLibert object API (reference _jls.py classes, fedbiomed_amd/secagg/_jls.py) ----
+ * fbm_jl_encrypt also takes x_dtype FBM_U128 (JoyeLibert.protect: VES-packed raw integers,
+ * weight 1) and FBM_PT (UserKey.encrypt, _jls.py:473-505: x = n plaintexts of 32 limbs, each
+ * < 2^1024, cr = 1, n_ct = n).
+ *
+ * fbm_jl_pack: VES.encode (_jls.py:118-144,169-176) of n raw integers (FBM_U128: (lo, hi)
+ *   pairs, < 2^128), slot j at bit es*j, cr slots per plaintext, the reference's OR packing
+ *   (a value wider than its slot spills into the next slots).  pt: device, ceil(n/cr) x 32
+ *   limbs.  A bit past 2^1024 is FBM_E_UNSUPPORTED at fbm_check_stats (the reference keeps it).
+ * fbm_jl_unpack: VES.decode (_jls.py:146-192): value o = slot o % cr of plaintext o / cr,
+ *   masked to es bits (es <= 128), as (lo, hi) uint64 pairs in vals [n_out x 2] (device).
+ * fbm_jl_fdh: FBM's FDH.H (_jls.py:727-762) of t_k = ((k + ct_offset) << 512) | tau, k < n_ct,
+ *   bits_size 2048, against a modulus M given as its odd part (32 limbs, odd, >= 3) and whether
+ *   M is even (gcd(r, M) == 1 then also needs r odd); for M = N^2 pass N.  h: n_ct x 64 limbs.
+ * fbm_jl_product: EncryptedNumber sums (_jls.py:308-374): out[k] = prod_u cts[u][k] mod N^2,
+ *   canonical, n_ct x 64 limbs; workspace fbm_jl_aggregate_workspace(n_ct).
+ * fbm_jl_decrypt: JoyeLibert.aggregate's product + ServerKey.decrypt (_jls.py:520-562) with
+ *   delta = 1: x[k] = ((prod_u cts[u][k] * H(t_k)^key mod N^2) - 1) // N mod N, n_ct x 32
+ *   limbs (no VES decode); workspace fbm_jl_aggregate_workspace(n_ct).                    */
+int fbm_jl_pack(const void* x, int x_dtype, uint64_t n, int es, int cr, uint32_t* pt, uint32_t* stats, void* stream);
+int fbm_jl_unpack(const uint32_t* pt, uint64_t n_ct, int es, int cr, uint64_t n_out, uint64_t* vals, void* stream);
+int fbm_jl_fdh(uint64_t n_ct, const uint32_t* modulus_odd, int modulus_even, uint64_t tau, uint64_t ct_offset,
+               uint32_t* h, uint32_t* stats, void* stream);
+int fbm_jl_product(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* biprime, uint32_t* out,
+                   void* workspace, void* stream);
+int fbm_jl_decrypt(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* biprime, const uint32_t* key,
+                   int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* x, void* workspace, uint32_t* stats,
+                   void* stream);
 
 /* ---- additive secret sharing of vectors (reference fedbiomed/common/secagg/_additive_ss.py) ----
  * fbm_ass_split replaces AdditiveSecret.split / _shares_int (:40-98) for a list secret:

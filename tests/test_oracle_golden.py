@@ -164,3 +164,48 @@ def test_edge_weights_oracle(golden):
     keys = [I(k) for k in m["keys"]]
     agg = O.jl_crypter_aggregate(encs, m["tau"], -sum(keys), W.BIPRIME0, 2, len(m["x"]))
     assert [fbits(v) for v in agg] == [s[2:] for s in m["agg"]["ok"]]
+
+
+# ---- the JoyeLibert object API fixture (tools/gen_golden.py gen_jls_api) ----
+def test_jls_api_oracle(golden):
+    g = golden["jls_api"]
+    for case in g["fdh"]:
+        m = I(case["m"])
+        for t, h in zip(case["t"], case["h"]):
+            if "ok" in h:
+                assert O.fdh(I(t), m) == I(h["ok"])
+            else:
+                with pytest.raises(OverflowError):
+                    O.fdh(I(t), m)
+    for case in g["populate_tau"]:
+        n = I(case["n"])
+        if "ok" in case["h"]:
+            assert [O.fdh((k << 512) | case["tau"], n * n) for k in range(case["len"])] == \
+                [I(h) for h in case["h"]["ok"]]
+    for case in g["user_encrypt"]:
+        got = O.jl_user_encrypt([I(v) for v in case["pt"]], case["tau"], I(case["key"]), I(case["n"]))
+        assert got == [I(c) for c in case["ct"]]
+    for case in g["sums"]:
+        n2 = I(case["n"]) ** 2
+        assert math.prod(I(c) for c in case["cts"]) % n2 == I(case["sum"])
+    for case in g["decrypt"]:
+        n = I(case["n"])
+        summed = [math.prod(col) % (n * n) for col in zip(*[[I(c) for c in row] for row in case["cts"]])]
+        keys = [I(k) for k in case["keys"]]
+        assert O.jl_server_decrypt(summed, case["tau"], -sum(keys), n, case["delta"]) == [I(v) for v in case["dec"]]
+        assert O.jl_server_decrypt(summed, case["tau"], -sum(keys) + 1, n) == [I(v) for v in case["dec_badkey"]]
+    for case, agg in zip(g["protect"], g["aggregate"]):
+        n, keys = I(case["n"]), [I(k) for k in case["keys"]]
+        target = I(case["target"]) if case["target"] else None
+        x = [I(v) for v in case["x"]]
+        for key, row in zip(keys, case["ct"]):
+            assert O.jl_encrypt_ints(x, case["tau"], key, n, len(keys), target) == [I(c) for c in row]
+        cts = [[I(c) for c in row] for row in case["ct"]]
+        for ne, res in zip(agg["n_expected"], agg["out"]):
+            assert O.jl_aggregate_ints(cts, case["tau"], -sum(keys), n, ne, target) == [I(v) for v in res["ok"]]
+    for case in g["ves"]:
+        es = case["valuesize"] + math.ceil(math.log2(case["add_ops"] + 1))
+        cr = case["ptsize"] // es
+        V = [I(v) for v in case["V"]]
+        assert O.ves_encode(V, es, cr) == [I(e) for e in case["E"]]
+        assert O.ves_decode([I(e) for e in case["E"]], es, cr, case["v_expected"]) == [I(v) for v in case["D"]]

@@ -353,14 +353,126 @@ def gen_dh(R):
                      "pairs": pairs, "kdf": kdf, "errors": errors})
 
 
+def gen_jls_api(R):
+    """The JoyeLibert object API (reference _jls.py classes, mirrored by fedbiomed_amd/secagg/_jls.py):
+    FDH.H over odd/even/non-square moduli, BaseKey._populate_tau, UserKey.encrypt on raw plaintexts
+    (incl. values >= N, >= 2^1024 and negative), EncryptedNumber sums, ServerKey.decrypt (delta 1 / -1),
+    JoyeLibert.protect / aggregate (the reference test's inputs, FA-width slots, values wider than their
+    slot), VES.encode / decode, and the error outcomes of the reference's tests."""
+    jls = R.jls
+    mpz = sys.modules["gmpy2"].mpz
+    bp = W.BIPRIME0
+    p = int("7801876574383880214548650574033350741129913580793719706746361606042541080141291132224899113047934760"
+            "791108387050756752894517232516965892712015132079112571")
+    q = int("7755946847853454424709929267431997195175500554762787715247111385596652741022399320865688002114973453"
+            "057088521173384791077635017567166681500095602864712097")
+    out = {"fdh": [], "populate_tau": [], "user_encrypt": [], "sums": [], "decrypt": [], "protect": [],
+           "aggregate": [], "ves": [], "errors": {}}
+    for m in [12345, 12123, 123456 * 123456, 123457 * 123457, 2 * 3 * 5 * 7 * 11 * 13, bp * bp, 4 * 15 * 15]:
+        fdh = jls.FDH(2048, mpz(m))
+        ts = [10, 0, 1, 7, (1 << 512) | 3, (5 << 512) | (2 ** 64 - 1), (2 ** 64 - 1) << 512]
+        out["fdh"].append({"m": ihex(m), "t": [ihex(t) for t in ts],
+                           "h": [_outcome(lambda t=t: ihex(int(fdh.H(t)))) for t in ts]})
+    for n_mod, tau, ln in [(123457, 1, 10), (p * q, 5, 7), (123456, 2, 6), (123455, 3, 12)]:
+        pp = jls.PublicParam(mpz(n_mod), 1024, jls.FDH(2048, mpz(n_mod) * mpz(n_mod)).H)
+        r = _outcome(lambda: [ihex(int(v)) for v in jls.BaseKey(pp, 191919191919191)._populate_tau(tau=tau, len_=ln)])
+        out["populate_tau"].append({"n": ihex(n_mod), "tau": tau, "len": ln, "h": r})
+    rng = random.Random(11)
+    for n_mod, key, pts, tau in [
+        (123457, 191919191919191, [10, 10, 10], 1),
+        (p * q, W.jl_user_key(0), [0, 1, 2 ** 1023 + 5, p * q - 1, p * q, p * q + 7, 2 ** 1024 + 3, -5, -(p * q) - 1], 3),
+        (p * q, -W.jl_user_key(1), [rng.getrandbits(1000) for _ in range(5)], 2 ** 64 - 1),
+        (bp, 0, [4, 5], 9),
+        (3000009, 12345, list(range(20)), 2),
+    ]:
+        pp = jls.PublicParam(mpz(n_mod), 1024, jls.FDH(2048, mpz(n_mod) * mpz(n_mod)).H)
+        ct = jls.UserKey(pp, key).encrypt([mpz(v) for v in pts], tau)
+        out["user_encrypt"].append({"n": ihex(n_mod), "key": ihex(key), "pt": [ihex(v) for v in pts], "tau": tau,
+                                    "ct": [ihex(int(c)) for c in ct]})
+    # EncryptedNumber sums (the reference's test values, and 3- and 4-term products)
+    for n_mod, cts in [(123457, [10, 10]), (123457, [10, 10, 10, 10]), (p * q, [rng.getrandbits(2040) for _ in range(3)]),
+                       (p * q, [(p * q) ** 2 + 5, 3])]:
+        pp = jls.PublicParam(mpz(n_mod), 1024, jls.FDH(2048, mpz(n_mod) * mpz(n_mod)).H)
+        total = sum(jls.EncryptedNumber(pp, c) for c in cts)
+        out["sums"].append({"n": ihex(n_mod), "cts": [ihex(c) for c in cts], "sum": ihex(int(total.ciphertext))})
+    # ServerKey.decrypt of summed ciphertexts, delta 1 and -1
+    for n_mod, keys, pts, tau, delta in [(123457, [10, 10], [10, 10, 10], 1, 1), (p * q, [10, 10], [0, 5, 20, 0], 1, -1),
+                                         (bp, [W.jl_user_key(u) for u in range(3)], [1, 2, 3, 2 ** 500], 4, 1)]:
+        pp = jls.PublicParam(mpz(n_mod), 1024, jls.FDH(2048, mpz(n_mod) * mpz(n_mod)).H)
+        encs = [[jls.EncryptedNumber(pp, c) for c in jls.UserKey(pp, k).encrypt([mpz(v) for v in pts], tau)]
+                for k in keys]
+        summed = [sum(ep) for ep in zip(*encs)]
+        dec = jls.ServerKey(pp, -sum(keys)).decrypt(summed, tau, delta=delta)
+        bad = jls.ServerKey(pp, -sum(keys) + 1).decrypt(summed, tau)
+        out["decrypt"].append({"n": ihex(n_mod), "keys": [ihex(k) for k in keys], "tau": tau, "delta": delta,
+                               "cts": [[ihex(int(e.ciphertext)) for e in row] for row in encs],
+                               "dec": [ihex(int(v)) for v in dec], "dec_badkey": [ihex(int(v)) for v in bad]})
+    # JoyeLibert.protect / aggregate
+    ref_pt = list(range(11, 28)) * 5
+    for n_mod, keys, plaintexts, tau, target in [
+        (p * q, [10, 10], [10, 10, 10], 1, None),
+        (p * q, [10, 10], ref_pt, 1, None),
+        (p * q, [10, 10], [0, 5, 20, 0], 1, None),
+        (bp, [W.jl_user_key(u) for u in range(3)], [rng.getrandbits(30) for _ in range(70)], 6, None),
+        (bp, [W.jl_user_key(u) for u in range(2)], [rng.getrandbits(72) for _ in range(30)], 2, 2 ** 55),
+        (bp, [W.jl_user_key(u) for u in range(2)], [2 ** 40 + 3, 7, 2 ** 33, 1] * 9, 3, None),
+    ]:
+        jl = jls.JoyeLibert(target_range=target)
+        pp = jls.PublicParam(mpz(n_mod), 1024, jls.FDH(2048, mpz(n_mod) * mpz(n_mod)).H)
+        prot = [jl.protect(pp, jls.UserKey(pp, k), tau, list(plaintexts), len(keys)) for k in keys]
+        encs = [[jls.EncryptedNumber(pp, int(c)) for c in row] for row in prot]
+        agg = [_outcome(lambda ne=ne: [ihex(v) for v in jl.aggregate(jls.ServerKey(pp, -sum(keys)), tau, encs, ne)])
+               for ne in (len(plaintexts), len(plaintexts) - 1, 0)]
+        out["protect"].append({"n": ihex(n_mod), "keys": [ihex(k) for k in keys], "x": [ihex(v) for v in plaintexts],
+                               "tau": tau, "target": None if target is None else ihex(target),
+                               "ct": [[ihex(int(c)) for c in row] for row in prot]})
+        out["aggregate"].append({"n_expected": [len(plaintexts), len(plaintexts) - 1, 0], "out": agg})
+    for ptsize, valuesize, add_ops, V, v_exp in [(1024, 30, 2, [1, 2, 3, 2 ** 31 + 1] * 10, 40),
+                                                  (1024, 72, 16, [2 ** 72 - 1, 0, 5] * 7, 19),
+                                                  (1024, 30, 8, [2 ** 100, 3] * 40, 80),
+                                                  (512, 20, 1, list(range(60)), 70)]:
+        ves = jls.VES(ptsize, valuesize)
+        E = ves.encode(list(V), add_ops)
+        out["ves"].append({"ptsize": ptsize, "valuesize": valuesize, "add_ops": add_ops, "V": [ihex(v) for v in V],
+                           "E": [ihex(int(e)) for e in E], "v_expected": v_exp,
+                           "D": [ihex(v) for v in ves.decode(E, add_ops, v_exp)]})
+    pp = jls.PublicParam(mpz(p * q), 1024, jls.FDH(2048, mpz(p * q) ** 2).H)
+    uk = jls.UserKey(pp, 10)
+    jl = jls.JoyeLibert()
+    out["errors"] = {
+        "protect_bad_key": _outcome(lambda: jl.protect(pp, "in-valid-user-key", 1, [1], 2)),
+        "protect_bad_param": _outcome(lambda: jl.protect(jls.PublicParam(mpz(1111), 1024, jls.FDH(2048, mpz(1111) ** 2).H),
+                                                         uk, 1, [1], 2)),
+        "protect_bad_x": _outcome(lambda: jl.protect(pp, uk, 1, "invalid-plaintext", 2)),
+        "aggregate_bad_key": _outcome(lambda: jl.aggregate(uk, 1, [[1]], 1)),
+        "aggregate_empty": _outcome(lambda: jl.aggregate(jls.ServerKey(pp, -10), 1, [], 1)),
+        "aggregate_not_nested": _outcome(lambda: jl.aggregate(jls.ServerKey(pp, -10), 1, [1, 2], 1)),
+        "encrypt_not_list": _outcome(lambda: uk.encrypt("not-a-list", 1)),
+        "decrypt_not_list": _outcome(lambda: jls.ServerKey(pp, -10).decrypt("x", 1)),
+        "decrypt_not_en": _outcome(lambda: jls.ServerKey(pp, -10).decrypt([1, 2], 1)),
+        "key_not_int": _outcome(lambda: jls.UserKey(pp, 1.5) and None),
+        "en_plus_int": _outcome(lambda: jls.EncryptedNumber(pp, 10) + 15),
+        "en_param_mismatch": _outcome(lambda: jls.EncryptedNumber(pp, 10) + jls.EncryptedNumber(
+            jls.PublicParam(mpz(987654123), 1024, jls.FDH(2048, mpz(987654123) ** 2).H), 10)),
+        "key_compare_type": _outcome(lambda: uk == jls.ServerKey(pp, 10)),
+        "fdh_bits_str": _outcome(lambda: jls.FDH("not-int", mpz(12123)) and None),
+        "fdh_mod_str": _outcome(lambda: jls.FDH(2048, "1234") and None),
+    }
+    dump("jls_api.json", out)
+
+
 def main():
     R = load_reference.load()
+    if sys.argv[1:] == ["jls_api"]:  # only the object-API fixture
+        gen_jls_api(R)
+        return
     gen_quantize(R)
     gen_lom(R)
     gen_jl(R)
     gen_ass(R)
     gen_edge(R)
     gen_dh(R)
+    gen_jls_api(R)
     meta = {"generator": "tools/gen_golden.py", "reference": load_reference.REF,
             "note": "outputs of the reference Fed-BioMed crypter (Python), imported via tools/refshim"}
     dump("meta.json", meta)
