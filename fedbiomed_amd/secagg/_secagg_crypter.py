@@ -25,6 +25,7 @@ import torch
 from .. import _device as D, wire
 from ..constants import ErrorNumbers, SAParameters
 from ..exceptions import FedbiomedSecaggCrypterError
+from ._jls import FDH, EncryptedNumber, PublicParam
 
 logger = logging.getLogger("fedbiomed_amd")
 
@@ -79,6 +80,20 @@ def _check_int_lists(params) -> None:
 
 class SecaggCrypter:
     """Joye-Libert secure aggregation (encrypt on nodes, aggregate on the researcher)."""
+
+    @staticmethod
+    def _setup_public_param(biprime: int) -> PublicParam:
+        """reference _secagg_crypter.py:28-43: N = biprime, bits 1024, FDH(2048, N^2).H (the
+        object API's PublicParam; encrypt/aggregate themselves take the biprime directly)."""
+        key_size = SAParameters.KEY_SIZE
+        biprime = int(biprime)
+        fdh = FDH(bits_size=key_size, n_modulus=biprime * biprime)
+        return PublicParam(n_modulus=biprime, bits=key_size // 2, hashing_function=fdh.H)
+
+    @staticmethod
+    def _convert_to_encrypted_number(params: List[List[int]], public_param: PublicParam) -> List[List[EncryptedNumber]]:
+        """reference _secagg_crypter.py:279-297"""
+        return [[EncryptedNumber(public_param, int(param)) for param in parameters] for parameters in params]
 
     # ---- device fast path ------------------------------------------------------------------
     def encrypt_tensor(self, num_nodes: int, current_round: int, params: torch.Tensor, key: int, biprime: int,

@@ -283,3 +283,14 @@ def test_random_protect_aggregate_vs_oracle():
         assert [prot[u][k] for k in ks] == [ref[k] for k in ks]
     encs = [[EncryptedNumber(pp, c) for c in row] for row in prot]
     assert jl.aggregate(ServerKey(pp, -sum(keys)), 9, encs, 2000) == [sum(v) for v in zip(*xs)]
+
+
+def test_crypter_public_param_helpers():
+    """reference test_secagg_crypter.py:23-47"""
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    pp = SecaggCrypter._setup_public_param(biprime=12345)
+    assert isinstance(pp, PublicParam) and pp.n_modulus == 12345 and pp.bits == 1024
+    enc = SecaggCrypter._convert_to_encrypted_number([[1, 2, 3, 4], [1, 2, 3, 4], [1, 2, 3, 4]], pp)
+    assert isinstance(enc[0][0], EncryptedNumber) and isinstance(enc[2][3], EncryptedNumber)
+    assert enc[0][0].ciphertext == 1 and enc[2][3].ciphertext == 4
