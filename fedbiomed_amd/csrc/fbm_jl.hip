@@ -1139,7 +1139,17 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_prod_kernel(const uint32_t* _
     br = (uint32_t)(d >> 63);
   }
   uint32_t x[32];
-  div_by_n(D, jp, x);
+  if (br) {  // v == 0 (a ciphertext = 0 mod N^2): ((0 - 1) // N) mod N = N - 1 in Python
+    uint32_t b = 1;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const uint64_t d = (uint64_t)jp.N32[i] - b;
+      x[i] = (uint32_t)d;
+      b = (uint32_t)(d >> 63);
+    }
+  } else {
+    div_by_n(D, jp, x);
+  }
   if (valid) {
     uint4* o = reinterpret_cast<uint4*>(xout + ct * 32);
 #pragma unroll

@@ -294,3 +294,22 @@ def test_crypter_public_param_helpers():
     enc = SecaggCrypter._convert_to_encrypted_number([[1, 2, 3, 4], [1, 2, 3, 4], [1, 2, 3, 4]], pp)
     assert isinstance(enc[0][0], EncryptedNumber) and isinstance(enc[2][3], EncryptedNumber)
     assert enc[0][0].ciphertext == 1 and enc[2][3].ciphertext == 4
+
+
+@pytest.mark.gpu
+def test_decrypt_of_zero_product():
+    """A product = 0 mod N^2 (a zero ciphertext): ((0 - 1) // N) % N = N - 1, as Python computes it
+    in ServerKey.decrypt (_jls.py:553-554) -- through the object API and the crypter's combine."""
+    from fedbiomed_amd import workload as W
+    from oracle import secagg_oracle as O
+
+    for n in (123457, W.BIPRIME0):
+        pp = pp_of(n)
+        cts = [0, n * n, 5, 0]
+        got = ServerKey(pp, -20).decrypt([EncryptedNumber(pp, c) for c in cts], tau=3)
+        assert got == O.jl_server_decrypt(cts, 3, -20, n) and got[0] == n - 1
+        en = [[EncryptedNumber(pp, c) for c in cts], [EncryptedNumber(pp, 7)] * 4]
+        jl = JoyeLibert()
+        es, cr = jl._vector_encoder._get_elements_size_and_compression_ratio(2)
+        xs = O.jl_server_decrypt([c * 7 % (n * n) for c in cts], 3, -20, n)
+        assert jl.aggregate(ServerKey(pp, -20), 3, en, 4 * cr) == O.ves_decode(xs, es, cr, 4 * cr)
