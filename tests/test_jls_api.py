@@ -6,6 +6,7 @@ plaintexts, EncryptedNumber sums, ServerKey.decrypt, JoyeLibert.protect / aggreg
 Every integer output is compared bit-exactly.  The argument checks that precede any device
 call run on the CPU; everything else runs the HIP path (`gpu`)."""
 
+import math
 import random
 
 import pytest
@@ -313,3 +314,41 @@ def test_decrypt_of_zero_product():
         es, cr = jl._vector_encoder._get_elements_size_and_compression_ratio(2)
         xs = O.jl_server_decrypt([c * 7 % (n * n) for c in cts], 3, -20, n)
         assert jl.aggregate(ServerKey(pp, -20), 3, en, 4 * cr) == O.ves_decode(xs, es, cr, 4 * cr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [2, 5, 17, 64, 129, 511, 1000, 1024])
+def test_random_moduli_object_api_vs_oracle(bits):
+    """UserKey.encrypt / EncryptedNumber sums / ServerKey.decrypt on random odd moduli (FDH
+    retries on the small ones) with keys of both signs and plaintexts at the edges (0, N - 1,
+    N, 2^1024 - 1, negative), against the oracle."""
+    from oracle import secagg_oracle as O
+
+    rng = random.Random(1000 + bits)
+    n = rng.getrandbits(bits) | 1 | (1 << (bits - 1))
+    if n < 3:
+        n = 3
+    pp = pp_of(n)
+    keys = [rng.getrandbits(rng.choice([1, 64, 2040])) * rng.choice([1, -1]) for _ in range(3)]
+    pts = [0, n - 1, n, 2**1024 - 1, -7, 1] + [rng.getrandbits(1024) for _ in range(10)]
+    tau = rng.getrandbits(64)
+    try:
+        ref = [O.jl_user_encrypt(pts, tau, k, n) for k in keys]
+    except (OverflowError, ValueError) as e:  # FDH exhausted / H not invertible for a negative key
+        with pytest.raises(type(e) if isinstance(e, OverflowError) else (ZeroDivisionError, ValueError)):
+            for k in keys:
+                UserKey(pp, k).encrypt(pts, tau)
+        return
+    got = [UserKey(pp, k).encrypt(list(pts), tau) for k in keys]
+    assert got == ref
+    summed = [sum(ep) for ep in zip(*[[EncryptedNumber(pp, c) for c in row] for row in got])]
+    products = [math.prod(col) % (n * n) for col in zip(*ref)]
+    assert [s.ciphertext for s in summed[:4]] == products[:4]  # materialised one by one on the device
+    sk = -sum(keys)
+    try:
+        want = O.jl_server_decrypt(products, tau, sk, n)
+    except ValueError:  # the server power is not invertible mod N^2
+        with pytest.raises(ZeroDivisionError):
+            ServerKey(pp, sk).decrypt(summed, tau)
+        return
+    assert ServerKey(pp, sk).decrypt(summed, tau) == want
