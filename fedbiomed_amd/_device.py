@@ -747,9 +747,9 @@ def ints_to_u128(values: Sequence[int], dev=None) -> torch.Tensor:
             try:
                 v = v.__index__()
             except (AttributeError, TypeError):
-                raise TypeError(f"unsupported operand type for VES packing: {type(vals[bad])}") from None
+                raise TypeError(f"expected integers, got {type(vals[bad])}") from None
         raise FedbiomedSecaggCrypterError(
-            f"{ErrorNumbers.FB624.value}: VES value {v} outside [0, 2^128), the device path's domain")
+            f"{ErrorNumbers.FB624.value}: integer {v} outside [0, 2^128), the device path's domain")
     return host.to(dev or device())
 
 
@@ -771,6 +771,28 @@ def ints_to_pt(values: Sequence[int], modulus: int, dev=None) -> torch.Tensor:
         rest = _pyconv().ints_to_bytes(vals[bad + 1:], 128, buf[bad + 1:])
         bad = -1 if rest < 0 else bad + 1 + rest
     return host.to(dev or device())
+
+
+def int_multiply(vals: torch.Tensor, k: int) -> List[int]:
+    """[v * k] on the device for int64 [n, 2] (lo, hi) values, 0 <= k < 2^64; FB624 when a
+    product reaches 2^128."""
+    if not 0 <= k <= U64_MAX:
+        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: factor {k} outside [0, 2^64)")
+    out = torch.empty_like(vals)
+    st = _stats(vals.device)
+    _call(N.load().fbm_int_ops, _ptr(vals.contiguous()), vals.shape[0], int(k), 0, _ptr(out), _ptr(st), _stream())
+    _check_stats(st)
+    return u128_to_ints(out)
+
+
+def int_true_divide(vals: torch.Tensor, k: int) -> List[float]:
+    """[v / k] (Python int/int true division, correctly rounded) on the device, 1 <= k < 2^64."""
+    if not 1 <= k <= U64_MAX:
+        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: divisor {k} outside [1, 2^64)")
+    out = torch.empty(vals.shape[0], dtype=torch.float64, device=vals.device)
+    st = _stats(vals.device)
+    _call(N.load().fbm_int_ops, _ptr(vals.contiguous()), vals.shape[0], int(k), 1, _ptr(out), _ptr(st), _stream())
+    return to_host(out).numpy().tolist()
 
 
 def jl_pack(vals: torch.Tensor, es: int, cr: int) -> torch.Tensor:

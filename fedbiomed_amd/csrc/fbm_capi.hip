@@ -606,6 +606,10 @@ int fbm_check_stats(const uint32_t* st, int lom_nodes, uint32_t* max_bits_out) {
     set_error("bounded device loop hit its iteration cap");
     return FBM_E_ITER;
   }
+  if (f & FBM_ERR_INT_RANGE) {
+    set_error("multiply: a product reaches 2^128, outside the device path's domain");
+    return FBM_E_UNSUPPORTED;
+  }
   if (f & FBM_ERR_PT_WIDE) {
     set_error("VES: a packed value spills past the 1024-bit plaintext (a value wider than its slot); "
               "outside the device path's domain");
@@ -1144,6 +1148,24 @@ int fbm_jl_decrypt(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint
   const JlAggWs w = agg_ws(workspace, n_ct);
   if ((rc = jl_factor_impl(n_ct, biprime, key, key_negative, tau, ct_offset, w.F, w, stats, s))) return rc;
   return jl_combine_impl(cts, n_parties, n_ct, 1, 1, 0, biprime, w.F, 1, 0.0, 1.0, nullptr, nullptr, w, stats, s, x);
+}
+
+int fbm_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, void* out, uint32_t* stats, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc = zero_stats(stats, s);
+  if (rc) return rc;
+  if ((op != 0 && op != 1) || (op == 1 && k == 0)) {
+    set_error("fbm_int_ops: op must be 0 (multiply) or 1 (divide, k >= 1)");
+    return FBM_E_ARG;
+  }
+  if (n == 0) return FBM_OK;
+  if (!x || !out) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  return timed("int_ops", s, [&] {
+    return launch_int_ops(x, n, k, op, op == 0 ? (uint64_t*)out : nullptr, op == 1 ? (double*)out : nullptr, stats, s);
+  });
 }
 
 int fbm_jl_batch_begin(void) { return jl_batch_begin(); }

@@ -16,6 +16,7 @@
 #define FBM_ERR_FDH_OVERFLOW 2u    // no coprime r of 1..7 FDH digests (reference: OverflowError)
 #define FBM_ERR_NOT_INVERTIBLE 4u  // server-key power not invertible mod N^2
 #define FBM_ERR_ITER_CAP 8u        // a bounded data-dependent loop hit its cap
+#define FBM_ERR_INT_RANGE 64u       // utils.multiply: a product reaches 2^128 (device domain)
 #define FBM_ERR_PT_WIDE 32u        // VES: a packed value spills past the 1024-bit plaintext
 #define FBM_WARN_CLIPPED 16u       // not an error: some |x| > clipping range (the reference's
                                    // _check_clipping_range warning, _secagg_utils.py:189-204)
@@ -137,6 +138,8 @@ struct JlParams {
 
 int launch_jl_pack(const void* x, int x_dtype, uint64_t n, const QuantParams& qp, uint64_t weight, int es, int cr,
                    uint64_t n_ct, uint32_t* pt, uint32_t* stats, hipStream_t s);
+int launch_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, uint64_t* prod, double* quot, uint32_t* stats,
+                   hipStream_t s);
 int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, int negative, uint32_t* nude,
                    hipStream_t s);
 int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s);

@@ -1744,4 +1744,31 @@ int launch_jl_decode(const uint32_t* xs, int es, int cr, uint64_t n_out, uint64_
   return check_launch("jl_decode_kernel");
 }
 
+// multiply / divide of the reference's secagg utils (_secagg_utils.py:122-149: [e * k], [e / k]) on
+// (lo, hi) uint64 pairs: op 0 = v * k (u128; FBM_ERR_INT_RANGE if the product reaches 2^128),
+// op 1 = v / k as Python's int/int true division (correctly rounded float64), k >= 1.
+__global__ void __launch_bounds__(256) int_ops_kernel(const uint64_t* __restrict__ x, uint64_t n, uint64_t k, int op,
+                                                      uint64_t* __restrict__ prod, double* __restrict__ quot,
+                                                      uint32_t* __restrict__ stats) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t lo = x[2 * i], hi = x[2 * i + 1];
+  if (op == 1) {
+    quot[i] = fbm_true_div_u128(((unsigned __int128)hi << 64) | lo, k);
+    return;
+  }
+  const unsigned __int128 pl = (unsigned __int128)lo * k, ph = (unsigned __int128)hi * k;
+  const unsigned __int128 r = pl + (ph << 64);
+  if ((ph >> 64) != 0 || r < pl) atomicOr(stats + FBM_STAT_ERRFLAGS, FBM_ERR_INT_RANGE);
+  prod[2 * i] = (uint64_t)r;
+  prod[2 * i + 1] = (uint64_t)(r >> 64);
+}
+
+int launch_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, uint64_t* prod, double* quot, uint32_t* stats,
+                   hipStream_t s) {
+  if (n == 0) return FBM_OK;
+  hipLaunchKernelGGL(int_ops_kernel, grid1(n, 256), dim3(256), 0, s, x, n, k, op, prod, quot, stats);
+  return check_launch("int_ops_kernel");
+}
+
 }  // namespace fbm

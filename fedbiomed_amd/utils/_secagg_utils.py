@@ -1,8 +1,10 @@
-"""Device-backed mirrors of the reference's secagg utilities
-(fedbiomed/common/utils/_secagg_utils.py:82-187): `quantize`, `reverse_quantize`,
-`multiply`, `divide`.  quantize / reverse_quantize run on the GPU (the LOM protect kernel
-with no peers is exactly quantize; `fbm_dequantize` is reverse_quantize); multiply /
-divide are the reference's Python list comprehensions (integer host semantics).
+"""Mirrors of the reference's secagg utilities (fedbiomed/common/utils/_secagg_utils.py:82-187):
+`quantize` and `reverse_quantize` run on the GPU (the LOM protect kernel with no peers is exactly
+quantize; `fbm_dequantize` is reverse_quantize).  `multiply` / `divide` are generic arithmetic
+helpers on any Python numbers (the reference's own tests call them on floats), kept as the
+reference's list comprehensions: no secagg path calls them -- the crypters' weighting and averaging
+are fused into their kernels, and `SecaggCrypter._apply_weighting` / `_apply_average` run on the
+device (`fbm_int_ops`).
 """
 
 from typing import List, Union
@@ -27,10 +29,12 @@ def quantize(weights: List[float], clipping_range: Union[int, None] = None,
 
 
 def multiply(xs: List[int], k: int) -> List[int]:
+    """reference _secagg_utils.py:122-134"""
     return [e * k for e in xs]
 
 
 def divide(xs: List[int], k: int) -> List[float]:
+    """reference _secagg_utils.py:137-149"""
     return [e / k for e in xs]
 
 

@@ -196,6 +196,13 @@ int fbm_jl_decrypt(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint
                    int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* x, void* workspace, uint32_t* stats,
                    void* stream);
 
+/* multiply / divide of the reference's secagg utils (fedbiomed/common/utils/_secagg_utils.py:122-149,
+ * used by SecaggCrypter._apply_weighting / _apply_average, :233-276) on n integers given as (lo, hi)
+ * uint64 pairs in x (device): op 0 = x * k into out as (lo, hi) pairs (a product >= 2^128 is
+ * FBM_E_UNSUPPORTED at fbm_check_stats), op 1 = x / k (k >= 1) into out as float64, Python's
+ * correctly rounded int/int true division.                                                   */
+int fbm_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, void* out, uint32_t* stats, void* stream);
+
 /* ---- additive secret sharing of vectors (reference fedbiomed/common/secagg/_additive_ss.py) ----
  * fbm_ass_split replaces AdditiveSecret.split / _shares_int (:40-98) for a list secret:
  * every element v (secret_dtype FBM_U64 or FBM_I64) gets n_shares-1 shares uniform in
