@@ -4,7 +4,8 @@
 the additive-sharing pair (split of the 100M summed vector into 16 int128 shares, exact
 reconstruct), each timed with HIP events on the launch stream (median of --reps), with the
 HBM rates of the two HBM-bound kernels against the 8 TB/s peak:
-  lom_aggregate:   8 (P + 1) bytes per element (P u64 rows in, one f64 out)
+  lom_aggregate:   8 (P + 2) bytes per element (P u64 rows in, one f64 out, the u64 sum the
+                   additive sharing splits)
   ass_reconstruct: 16 P + 16 bytes per element (P int128 shares in, one int128 sum out)
   ass_split:       8 + 16 P bytes per element (u64 in, P int128 shares out; ChaCha20 for the
                    P - 1 random shares).
@@ -91,7 +92,7 @@ def main():
     def gbs(nbytes, ms):
         return nbytes / (ms / 1000) / 1e9
 
-    agg_b, rec_b, split_b = 8 * (P + 1) * n, (16 * P + 16) * n, (8 + 16 * P) * n
+    agg_b, rec_b, split_b = 8 * (P + 2) * n, (16 * P + 16) * n, (8 + 16 * P) * n
     line = {
         "workload": f"config 5: LOM + additive secret sharing, {n:,} elements, {P} parties, 1 GPU",
         "lom_step": {"value": n / ((t_prot + t_agg) / 1000), "unit": "params/s", "ms": t_prot + t_agg,
