@@ -307,10 +307,12 @@ def main():
          if args.scheme == "lom" or not args.no_lom_extra else None)
 
     def step_lom(serial=False):
-        with D.deferred_checks():  # overflow-guard status checked once per step, no per-party sync
+        # the parties' overflow-guard status words are checked once per step, after the aggregate
+        # is queued behind the protects (no per-party sync, no idle GPU while the host reads them)
+        with D.deferred_checks():
             for p, u in enumerate(ids):  # each party's masked vector straight into its row
                 lc.encrypt_tensor(tau, u, xs_l[p], secrets_[p], ids, weight=weights[p], elem_offset=lo_l, out=Y[p])
-        return lc.aggregate_tensor(Y, total_w)
+            return lc.aggregate_tensor(Y, total_w)
 
     def timed(step, steps, warmup, prof=False):
         """prof=True: serialised launches (one stream) with per-kernel HIP events, so each
