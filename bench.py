@@ -7,9 +7,10 @@ vector @1/8 GPU".  One step = every party encrypts its device-resident parameter
 aggregate (ciphertext product, server-key exponentiation, inverse, unmask, decode, average,
 dequantise).  value = params processed by all ranks / wall time of K steps (max over ranks).
 
-Scaling: element-range sharding with no data-path collective (fedbiomed_amd/distributed.py).
-Default "strong": ONE 10M-element vector (config 4) is split into N stripes, one per GPU, each
-processed with its global offsets -- the total work is fixed as N grows.  `--weak` gives every
+Scaling: element-range sharding (fedbiomed_amd/distributed.py).  Default "strong": ONE 10M-element
+vector (config 4) is split into N stripes, one per GPU, each processed with its global offsets -- the
+total work is fixed as N grows -- and the step ends with the split's final gather (an RCCL all-gather
+of the float64 output stripes: every rank holds the whole averaged vector).  `--weak` gives every
 rank its own --elements stripe instead.  `stages` reports T_enc (all P parties' encrypts),
 T_agg (the aggregate alone: decryption factor + combine), P*N/T_enc and N/T_agg.
 
@@ -214,6 +215,9 @@ def main():
     streams = [pool[p % n_streams] for p in range(P)]
     main = torch.cuda.current_stream(dev)
 
+    # strong scaling over N > 1 ranks: the step ends with the element-range split's final gather
+    # (SURVEY 8(e)), so every rank -- the researcher -- holds the whole averaged vector
+    gather = strong and world > 1
     factor_stream = torch.cuda.Stream(device=dev)
     overlap_factor = not args.no_factor_overlap
     batch_exp = not args.no_batch_exp and not args.no_prologue_first
@@ -293,8 +297,11 @@ def main():
                 cts[p].record_stream(main)
             if factor is not None:
                 factor.record_stream(main)
-        return jc.aggregate_tensor(tau, torch.stack(cts), sk0, W.BIPRIME0, total_w, num_expected_params=n,
-                                   ct_offset=lo // cr, decrypt_factor=factor)
+        out = jc.aggregate_tensor(tau, torch.stack(cts), sk0, W.BIPRIME0, total_w, num_expected_params=n,
+                                  ct_offset=lo // cr, decrypt_factor=factor)
+        if gather:  # the split's final gather: the whole averaged vector on every rank (RCCL all-gather)
+            out = distributed.all_gather_shards(out, n_total, cr)
+        return out
 
     # LOM stripes are ChaCha20-block (8-element) aligned: with the JL stripe (ciphertext aligned)
     # as the main workload, the LOM leg takes its own 8-aligned split of the same vector
@@ -312,7 +319,8 @@ def main():
         with D.deferred_checks():
             for p, u in enumerate(ids):  # each party's masked vector straight into its row
                 lc.encrypt_tensor(tau, u, xs_l[p], secrets_[p], ids, weight=weights[p], elem_offset=lo_l, out=Y[p])
-            return lc.aggregate_tensor(Y, total_w)
+            out = lc.aggregate_tensor(Y, total_w)
+        return distributed.all_gather_shards(out, n_total, 8) if gather else out
 
     def timed(step, steps, warmup, prof=False):
         """prof=True: serialised launches (one stream) with per-kernel HIP events, so each
@@ -473,6 +481,11 @@ def main():
                           "enc_party_params_per_s": P * n_total / t_enc, "agg_params_per_s": n_total / t_agg,
                           "note": "T_enc: all parties' encrypts (one stream each), T_agg: one aggregate alone "
                                   "(decryption factor + combine); max over ranks; rates over elements_total"}
+        if gather:  # the step's final all-gather of the float64 output stripes, alone
+            stripe = torch.zeros(n, dtype=torch.float64, device=dev)
+            align = cr if args.scheme == "jl" else 8
+            line["stages"]["T_gather_ms"] = 1000 * t_stage(
+                lambda: distributed.all_gather_shards(stripe, n_total, align))
         if args.scheme == "jl" and world == 1:
             # strong-scaling probe of the aggregate step on this GPU: T_agg of the stripe rank 0
             # of an 8-GPU split owns (the first ceil(n/8/cr) ciphertexts: ciphertext k depends

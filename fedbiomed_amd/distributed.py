@@ -118,6 +118,26 @@ def all_gather_stripes(stripe, n_total: int, align: int):
     return torch.cat([out[r * per: r * per + (hi - lo)] for r, (lo, hi) in enumerate(bounds)])
 
 
+def all_gather_shards(stripe, n_total: int, align: int):
+    """The element-range split's final gather: every rank's output stripe (its
+    shard_range(n_total, world, rank, align) elements) -> the whole [n_total] vector on every
+    rank, one all-gather (RCCL over xGMI with "nccl"; host tensors with gloo)."""
+    import torch
+
+    dist = _dist()
+    world = dist.get_world_size()
+    bounds = [shard_range(n_total, world, r, align) for r in range(world)]
+    per = max(hi - lo for lo, hi in bounds)
+    dev = stripe.device
+    host = dist.get_backend() != "nccl"
+    buf = torch.zeros(per, dtype=stripe.dtype, device="cpu" if host else dev)
+    buf[: stripe.numel()] = stripe.cpu() if host else stripe
+    out = torch.empty(per * world, dtype=stripe.dtype, device=buf.device)
+    dist.all_gather_into_tensor(out, buf)
+    full = torch.cat([out[r * per: r * per + (hi - lo)] for r, (lo, hi) in enumerate(bounds)])
+    return full.to(dev) if host else full
+
+
 def all_to_all_ciphertexts(cts_local, parties_per_rank: int):
     """cts_local: [P_local, n_ct, 64] int32 limbs of this rank's parties (whole vector).
     Returns ([P_total, stripe_ct, 64] int32, ct_offset) = every party's ciphertexts for this

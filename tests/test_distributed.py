@@ -151,7 +151,26 @@ def _jl_party_per_rank_hip(rank, world):
     return Dd.all_gather_stripes(out.cpu(), N_JL_HIP, cr).numpy(), (e_lo, e_hi)
 
 
+def _gather_shards(rank, world):
+    """Each rank holds its shard_range stripe of a known vector; the gather rebuilds it whole."""
+    res = []
+    for n, align in ((1003, 8), (10_001, 30), (5, 8)):
+        lo, hi = Dd.shard_range(n, world, rank, align)
+        full = torch.arange(n, dtype=torch.float64) * 0.5 - 3.0
+        res.append(Dd.all_gather_shards(full[lo:hi].clone(), n, align).numpy())
+    return res
+
+
 # ---- tests ---------------------------------------------------------------------------------
+@pytest.mark.parametrize("world", [2, 3])
+def test_all_gather_shards_gloo(world):
+    """The bench's final gather of the element-range output stripes (uneven shard_range stripes)."""
+    res = _spawn("_gather_shards", world)
+    for r in range(world):
+        for n, got in zip((1003, 10_001, 5), res[r]):
+            assert got.tolist() == (np.arange(n, dtype=np.float64) * 0.5 - 3.0).tolist()
+
+
 @pytest.mark.parametrize("n,world,align", [(0, 2, 8), (7, 2, 8), (1003, 2, 8), (10_000_000, 8, 8),
                                            (10_000_000, 8, 30), (100, 3, 31)])
 def test_shard_range_tiles(n, world, align):
