@@ -515,6 +515,38 @@ def main():
                        "aggregate_hbm_frac": (ab / (m2 / 1000) / 1e9) / HBM_PEAK_GBS if m2 else None,
                        "kernels_ms": {k: {"launches": c, "total_ms": round(t, 3)} for k, (c, t) in sorted(kp2.items())}}
 
+    # ---- secondary, N > 1: party-per-rank LOM -- the north star's RCCL reduce of the masked sum.
+    #      Rank r protects parties r, r + N, ... over the WHOLE vector (the concatenation of every
+    #      rank's element-range stripe of them, so the result is comparable), sums them, and one
+    #      reduce-scatter of the u64 sums over xGMI leaves it the masked total of its stripe; it
+    #      averages + dequantises that stripe and all-gathers the float64 stripes.  The output is
+    #      checked bit for bit against the element-range LOM leg's gathered vector. ----
+    if args.scheme == "jl" and strong and world > 1 and not args.no_lom_extra and P % world == 0:
+        mine = [p for p in range(P) if p % world == rank]
+        bnd = [distributed.shard_range(args.n, world, r, 8) for r in range(world)]
+        xs_pp = [torch.from_numpy(np.concatenate([W.party_params(p + 1000 * r, b - a) for r, (a, b) in
+                                                  enumerate(bnd)])).to(dev) for p in mine]
+        Ypp = torch.empty((len(mine), args.n), dtype=torch.int64, device=dev)
+
+        def step_pp(serial=False):
+            with D.deferred_checks():
+                for i, p in enumerate(mine):
+                    lc.encrypt_tensor(tau, ids[p], xs_pp[i], secrets_[p], ids, weight=weights[p], out=Ypp[i])
+                _, local = D.lom_aggregate(Ypp, 1, want_out=False, want_sums=True)
+            stripe = distributed.reduce_scatter_u64(local, args.n)
+            return distributed.all_gather_stripes(lc.aggregate_tensor(stripe.view(1, -1), total_w), args.n, 8)
+
+        k3 = max(args.steps, 10)
+        el3, _ = timed(step_pp, k3, 2)
+        same = torch.tensor([int(torch.equal(step_pp(), step_lom()))], device=dev)
+        torch.distributed.all_reduce(same, op=torch.distributed.ReduceOp.MIN)
+        line["lom_party_per_rank"] = {
+            "value": n_total * k3 / el3, "unit": "params/s", "ms_per_step": 1000 * el3 / k3,
+            "parties_per_rank": len(mine), "equals_element_range": bool(same.item()), "backend": args.dist_backend,
+            "note": "each rank protects its parties over the whole vector, local u64 sum, reduce-scatter "
+                    "(RCCL over xGMI) of the masked sums, per-stripe average + dequantise, all-gather; "
+                    "bit-exact vs the element-range LOM leg's gathered vector"}
+
     # ---- end-to-end legs (host memory in, host memory out): never `value` ----
     if rank == 0 and world == 1 and args.scheme == "jl" and not args.no_e2e:
         # (a) pinned host float32 vectors -> H2D -> encrypt -> D2H ciphertext limbs (each party),

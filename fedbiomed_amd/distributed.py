@@ -93,15 +93,17 @@ def reduce_scatter_u64(local_sum, n_total: int):
     dist = _dist()
     world, rank = dist.get_world_size(), dist.get_rank()
     per, bounds = stripe_bounds(n_total, world, 8)
-    buf = torch.zeros(per * world, dtype=torch.int64, device=local_sum.device)
-    buf[:n_total] = local_sum
     lo, hi = bounds[rank]
     if dist.get_backend() == "nccl":
+        buf = torch.zeros(per * world, dtype=torch.int64, device=local_sum.device)
+        buf[:n_total] = local_sum
         out = torch.empty(per, dtype=torch.int64, device=local_sum.device)
         dist.reduce_scatter_tensor(out, buf, op=dist.ReduceOp.SUM)
         return out[: hi - lo]
+    buf = torch.zeros(per * world, dtype=torch.int64)  # gloo: host tensors, all-reduce + slice
+    buf[:n_total] = local_sum.cpu()
     dist.all_reduce(buf, op=dist.ReduceOp.SUM)
-    return buf[lo:hi].clone()
+    return buf[lo:hi].clone().to(local_sum.device)
 
 
 def all_gather_stripes(stripe, n_total: int, align: int):
@@ -111,11 +113,13 @@ def all_gather_stripes(stripe, n_total: int, align: int):
     dist = _dist()
     world, rank = dist.get_world_size(), dist.get_rank()
     per, bounds = stripe_bounds(n_total, world, align)
-    buf = torch.zeros(per, dtype=stripe.dtype, device=stripe.device)
-    buf[: stripe.numel()] = stripe
-    out = torch.empty(per * world, dtype=stripe.dtype, device=stripe.device)
+    host = dist.get_backend() != "nccl"  # gloo: host tensors
+    buf = torch.zeros(per, dtype=stripe.dtype, device="cpu" if host else stripe.device)
+    buf[: stripe.numel()] = stripe.cpu() if host else stripe
+    out = torch.empty(per * world, dtype=stripe.dtype, device=buf.device)
     dist.all_gather_into_tensor(out, buf)
-    return torch.cat([out[r * per: r * per + (hi - lo)] for r, (lo, hi) in enumerate(bounds)])
+    full = torch.cat([out[r * per: r * per + (hi - lo)] for r, (lo, hi) in enumerate(bounds)])
+    return full.to(stripe.device) if host else full
 
 
 def all_gather_shards(stripe, n_total: int, align: int):
