@@ -547,6 +547,41 @@ def main():
                     "(RCCL over xGMI) of the masked sums, per-stripe average + dequantise, all-gather; "
                     "bit-exact vs the element-range LOM leg's gathered vector"}
 
+    # ---- secondary, N > 1: party-per-rank JL -- rank r encrypts parties r*P/N .. (r+1)*P/N - 1 over
+    #      the WHOLE vector (the concatenation of every rank's element-range stripe of them), one
+    #      all-to-all of ciphertext stripes (RCCL over xGMI; the modular product is no RCCL reduction),
+    #      the aggregate of its ciphertext stripe at its ct_offset, all-gather of the float64 stripes;
+    #      checked bit for bit against the element-range JL step's gathered vector ----
+    if args.scheme == "jl" and strong and world > 1 and not args.no_lom_extra and P % world == 0:
+        ppr = P // world
+        mine = list(range(rank * ppr, (rank + 1) * ppr))  # rank-major party blocks
+        bnd = [distributed.shard_range(args.n, world, r, cr) for r in range(world)]
+        xs_pj = [torch.from_numpy(np.concatenate([W.party_params(p + 1000 * r, b - a) for r, (a, b) in
+                                                  enumerate(bnd)])).to(dev) for p in mine]
+        n_ct_all = (args.n + cr - 1) // cr
+
+        def step_pj(serial=False):
+            with D.deferred_checks(), engine_ctx("single"):
+                cts_mine = torch.stack([jc.encrypt_tensor(P, tau, xs_pj[i], keys[p], W.BIPRIME0, weight=weights[p])
+                                        for i, p in enumerate(mine)])
+            stripe, k0 = distributed.all_to_all_ciphertexts(cts_mine, ppr)
+            e_lo, e_hi = min(k0 * cr, args.n), min((k0 + stripe.shape[1]) * cr, args.n)
+            out = jc.aggregate_tensor(tau, stripe, sk0, W.BIPRIME0, total_w, num_expected_params=e_hi - e_lo,
+                                      ct_offset=k0)
+            return distributed.all_gather_stripes(out, args.n, cr)
+
+        kj = max(2, min(args.steps, 3))
+        elj, _ = timed(step_pj, kj, 1)
+        same = torch.tensor([int(torch.equal(step_pj(), step_jl()))], device=dev)
+        torch.distributed.all_reduce(same, op=torch.distributed.ReduceOp.MIN)
+        line["jl_party_per_rank"] = {
+            "value": n_total * kj / elj, "unit": "params/s", "ms_per_step": 1000 * elj / kj,
+            "parties_per_rank": ppr, "ciphertexts_per_rank_encrypted": ppr * n_ct_all,
+            "equals_element_range": bool(same.item()), "backend": args.dist_backend,
+            "note": "each rank encrypts its parties over the whole vector, all-to-all of ciphertext stripes "
+                    "(RCCL over xGMI), aggregate of its stripe, all-gather; bit-exact vs the element-range "
+                    "JL step's gathered vector"}
+
     # ---- end-to-end legs (host memory in, host memory out): never `value` ----
     if rank == 0 and world == 1 and args.scheme == "jl" and not args.no_e2e:
         # (a) pinned host float32 vectors -> H2D -> encrypt -> D2H ciphertext limbs (each party),

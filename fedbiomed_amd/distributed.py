@@ -154,12 +154,14 @@ def all_to_all_ciphertexts(cts_local, parties_per_rank: int):
     if P_local != parties_per_rank:
         raise ValueError("every rank must hold the same number of parties")
     per, bounds = stripe_bounds(n_ct, world, 1)
+    host = dist.get_backend() != "nccl"  # gloo: host tensors
     # ct-major, padded to equal stripes: rows [r*per, (r+1)*per) go to rank r
-    send = torch.zeros((per * world, P_local, W), dtype=cts_local.dtype, device=cts_local.device)
-    send[:n_ct] = cts_local.permute(1, 0, 2)
+    send = torch.zeros((per * world, P_local, W), dtype=cts_local.dtype, device="cpu" if host else cts_local.device)
+    send[:n_ct] = (cts_local.cpu() if host else cts_local).permute(1, 0, 2)
     recv = torch.empty_like(send)
     dist.all_to_all_single(recv, send)
     lo, hi = bounds[rank]
     # recv block s = source rank s's parties for my stripe: [per, P_local, W]
     recv = recv.view(world, per, P_local, W)[:, : hi - lo]
-    return recv.permute(0, 2, 1, 3).reshape(world * P_local, hi - lo, W).contiguous(), lo
+    out = recv.permute(0, 2, 1, 3).reshape(world * P_local, hi - lo, W).contiguous()
+    return (out.to(cts_local.device) if host else out), lo
