@@ -66,6 +66,8 @@ def _raise(rc: int) -> None:
         raise OverflowError("int too big to convert")  # the reference's FDH counter.to_bytes(1)
     if rc == N.FBM_E_INVERSE:
         raise ZeroDivisionError("invert() no inverse exists")
+    if rc == N.FBM_E_ROUND:
+        raise OverflowError("int too big to convert")  # the reference's (i + tau).to_bytes(8, 'big')
     if rc in (N.FBM_E_ARG, N.FBM_E_UNSUPPORTED):
         raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: {msg}")
     raise RuntimeError(f"fedbiomed_amd HIP error {rc}: {msg}")
@@ -112,8 +114,10 @@ class deferred_checks:
             ev.synchronize()
         host = torch.stack([st for st, _, _ in pending]).cpu().numpy()  # one copy for all of them
         try:
-            for (_, nodes, _), row in zip(pending, host):
+            for (_, (nodes, post), _), row in zip(pending, host):
                 _check_stats_host(row, nodes)
+                if post is not None:
+                    raise post
         except Exception as dev_err:
             if exc is not None:  # the device condition came first: surface it, chained
                 raise dev_err from exc
@@ -121,14 +125,18 @@ class deferred_checks:
         return False
 
 
-def _check_stats_or_defer(stats: torch.Tensor, lom_nodes: int = 0) -> None:
+def _check_stats_or_defer(stats: torch.Tensor, lom_nodes: int = 0, post: Optional[Exception] = None) -> None:
+    """`post`: a host-known error of the same call, raised after the device conditions (the
+    reference's order, e.g. LOM's round-counter overflow after its overflow guard)."""
     active = deferred_checks._stack()
     if active:
         ev = torch.cuda.Event()
         ev.record()  # on the current stream, right after the kernels that write `stats`
-        active[-1].append((stats, lom_nodes, ev))
+        active[-1].append((stats, (lom_nodes, post), ev))
     else:
         _check_stats(stats, lom_nodes)
+        if post is not None:
+            raise post
 
 
 def _check_stats(stats: torch.Tensor, lom_nodes: int = 0) -> int:
@@ -142,9 +150,27 @@ def _check_stats_host(host: np.ndarray, lom_nodes: int = 0) -> int:
                        "Please increase the clipping range to account for value")
     mb = ctypes.c_uint32(0)
     rc = N.load().fbm_check_stats(_np_ptr(host), lom_nodes, ctypes.byref(mb))
+    if rc == N.FBM_E_OVERFLOW:
+        raise FedbiomedSecaggError(_lom_overflow_message(int(mb.value), lom_nodes))
     if rc != N.FBM_OK:
         _raise(rc)
     return int(mb.value)
+
+
+def _lom_overflow_message(max_bits: int, num_nodes: int) -> str:
+    """LOM.protect's overflow-guard message (secagg/_lom.py:133-149), word for word."""
+    node_bits = math.ceil(math.log2(num_nodes))
+    avail = 64 - node_bits
+    missing = max_bits + node_bits - 64
+    return (f"{ErrorNumbers.FB417.value}: Secure aggregation overflow detected.\n\n"
+            f"Your value requires {max_bits} bits, but only {avail} bits "
+            f"are available (64-bit dtype minus {node_bits} bits reserved for {num_nodes} nodes).\n\n"
+            f"To fix this, choose one of the following:\n"
+            f"  1) Reduce the number of nodes to at most {2 ** (64 - max_bits)} (currently {num_nodes}).\n"
+            f"  2) Reduce your values by at least {missing} bit(s) "
+            f"(i.e. divide them by at least {2 ** missing}).\n"
+            f"  3) If you are quantizing model weights, use a lower quantization range "
+            f"so that individual values fit within {avail} bits.")
 
 
 def _stats(dev) -> torch.Tensor:
@@ -371,13 +397,20 @@ def lom_protect(x: torch.Tensor, secrets: Sequence[bytes], signs: Sequence[int],
     lib = N.load()
     target = target or SAParameters.TARGET_RANGE
     c, c2, tf, tm1 = quant_params(clip, target) if x.dtype != torch.int64 else (1.0, 2.0, 1.0, 0)
-    if tau < 0 or tau > U64_MAX:
-        raise OverflowError("int too big to convert")
     sec = _secret_block(secrets)
     sg = np.asarray([1 if s > 0 else -1 for s in signs] or [0], dtype=np.int8)
     nb = _nonce_block(nonce)
     x = x.contiguous()
     n = x.numel()
+    # PRF.eval_key / eval_vector (_lom.py:43-45, 81) serialise tau and i + tau to 16 / 8 big-endian
+    # bytes: a negative tau, or some i + tau >= 2^64, is the reference's OverflowError, raised (like
+    # it) after the overflow guard and only when there are peers to mask with.  The C-ABI reports
+    # i + tau past 2^64 for a 64-bit tau (FBM_E_ROUND); a tau outside [0, 2^64) is known here.
+    post = None
+    if secrets and n > 0 and not 0 <= tau <= U64_MAX:
+        post = OverflowError("can't convert negative int to unsigned" if tau < 0 else "int too big to convert")
+        tau = 0
+    tau &= U64_MAX
     if out is not None:  # caller-owned destination, e.g. row p of the aggregate's [P, n] matrix
         if out.dtype != torch.int64 or out.numel() != n or not out.is_contiguous() or out.device != dev:
             raise ValueError("out must be a contiguous int64 tensor of x.numel() elements on x's device")
@@ -390,8 +423,10 @@ def lom_protect(x: torch.Tensor, secrets: Sequence[bytes], signs: Sequence[int],
           _stream())
     if check_now:
         _check_stats(st, n_nodes)
+        if post is not None:
+            raise post
     else:
-        _check_stats_or_defer(st, lom_nodes=n_nodes)
+        _check_stats_or_defer(st, lom_nodes=n_nodes, post=post)
     return y
 
 
@@ -399,8 +434,11 @@ def prf_key(secret: bytes, nonce: bytes, tau: int, dev=None) -> bytes:
     dev = dev or device()
     sec = _secret_block([secret])
     nb = _nonce_block(nonce)
-    if tau < 0 or tau >= 2**64:
-        raise OverflowError("int too big to convert")
+    if tau < 0:  # tau.to_bytes(16, 'big') (_lom.py:43-45)
+        raise OverflowError("can't convert negative int to unsigned")
+    if tau > U64_MAX:  # valid up to 2^128 in the reference; the device round counter is 64-bit
+        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: round counter {tau} >= 2^64 is outside "
+                                          "the device path's domain")
     out = torch.empty(32, dtype=torch.uint8, device=dev)
     _call(N.load().fbm_prf_key, _np_ptr(sec), _np_ptr(nb), int(tau), _ptr(out), _stream())
     return out.cpu().numpy().tobytes()

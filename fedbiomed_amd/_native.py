@@ -28,6 +28,7 @@ FBM_E_FDH = -5
 FBM_E_INVERSE = -6
 FBM_E_ITER = -7
 FBM_E_UNSUPPORTED = -8
+FBM_E_ROUND = -9
 
 FBM_F32 = 0
 FBM_F64 = 1

@@ -628,6 +628,10 @@ int fbm_check_stats(const uint32_t* st, int lom_nodes, uint32_t* max_bits_out) {
       return FBM_E_OVERFLOW;
     }
   }
+  if (f & FBM_ERR_ROUND_RANGE) {
+    set_error("int too big to convert");
+    return FBM_E_ROUND;
+  }
   return FBM_OK;
 }
 
@@ -652,16 +656,20 @@ int fbm_lom_protect(const void* x, int x_dtype, uint64_t n, double clip, double 
     set_error("null pointer argument");
     return FBM_E_ARG;
   }
-  // PRF.eval_vector guard (_lom.py:74-78) and (i + tau).to_bytes(8) range, on global indices
+  // PRF.eval_vector guard (_lom.py:74-78), on global indices
   if ((elem_offset & 7ull) != 0) {
     set_error("elem_offset must be a multiple of 8 (ChaCha20 block aligned shard)");
     return FBM_E_ARG;
   }
   const uint64_t n_glob = elem_offset + n;
-  if (n_glob < n || n_glob + 1000ull > (1ull << 61) || (n > 0 && tau > ~0ull - (n_glob - 1))) {
+  if (n_glob < n || n_glob + 1000ull > (1ull << 61)) {
     set_error("Can not perform encryiton due to large input vector");
     return FBM_E_ARG;
   }
+  // (i + tau).to_bytes(8, 'big') (_lom.py:81) past 2^64 is the reference's OverflowError, raised
+  // after its overflow guard and only when there are peers (no PRF call without one): reported
+  // through the status words in that order (fbm_check_stats), the counters wrapping meanwhile
+  const int round_range = n_peers > 0 && n > 0 && tau > ~0ull - (n_glob - 1);
   // peers in groups of FBM_MAX_PEERS (the kernel-argument block): the first group with the
   // quantise/weight/overflow statistics, later groups accumulated in place
   for (int g0 = 0; g0 == 0 || g0 < n_peers; g0 += FBM_MAX_PEERS) {
@@ -671,6 +679,7 @@ int fbm_lom_protect(const void* x, int x_dtype, uint64_t n, double clip, double 
     pe.n_peers = gn < 0 ? 0 : gn;
     pe.raw_seeds = raw_seeds;
     pe.elem_offset = elem_offset;
+    pe.round_range = g0 == 0 ? round_range : 0;
     for (int p = 0; p < pe.n_peers; ++p) {
       memcpy(pe.secret[p], secrets + 32 * (g0 + p), 32);
       if (signs[g0 + p] >= 0) pe.add_bits |= 1ull << p;

@@ -17,6 +17,7 @@
 #define FBM_ERR_NOT_INVERTIBLE 4u  // server-key power not invertible mod N^2
 #define FBM_ERR_ITER_CAP 8u        // a bounded data-dependent loop hit its cap
 #define FBM_ERR_INT_RANGE 64u       // utils.multiply: a product reaches 2^128 (device domain)
+#define FBM_ERR_ROUND_RANGE 128u   // LOM: some i + tau reaches 2^64 with peers to mask with
 #define FBM_ERR_PT_WIDE 32u        // VES: a packed value spills past the 1024-bit plaintext
 #define FBM_WARN_CLIPPED 16u       // not an error: some |x| > clipping range (the reference's
                                    // _check_clipping_range warning, _secagg_utils.py:189-204)
@@ -38,6 +39,7 @@ struct LomPeers {
   uint32_t tau_be[4];            // tau.to_bytes(16, 'big') as LE words
   uint32_t secret[FBM_MAX_PEERS][8];
   uint64_t add_bits;             // bit p set: mask += vec (peer < node), clear: mask -= vec
+  uint32_t round_range;          // 1: flag FBM_ERR_ROUND_RANGE (first peer group only)
 };
 
 int check_launch(const char* what);

@@ -122,6 +122,7 @@ __global__ void __launch_bounds__(256, 8) lom_protect_kernel(const XT* __restric
   }
 
   flag_if_any(clipped, stats, FBM_WARN_CLIPPED);
+  if (peers.round_range && blockIdx.x == 0 && tid == 0) atomicOr(stats + FBM_STAT_ERRFLAGS, FBM_ERR_ROUND_RANGE);
   // wave-level max of the bit lengths, one atomic per wave
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {

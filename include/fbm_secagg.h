@@ -38,6 +38,7 @@ extern "C" {
 #define FBM_E_INVERSE (-6)     /* H^|sk0| not invertible mod N^2 (gmpy2: ZeroDivisionError) */
 #define FBM_E_ITER (-7)        /* a bounded data-dependent device loop hit its cap          */
 #define FBM_E_UNSUPPORTED (-8) /* parameters outside the device path's domain (documented)  */
+#define FBM_E_ROUND (-9)       /* LOM: some i + tau >= 2^64 (_lom.py:81: OverflowError), after FBM_E_OVERFLOW */
 
 #define FBM_F32 0
 #define FBM_F64 1

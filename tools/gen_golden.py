@@ -461,10 +461,79 @@ def gen_jls_api(R):
     dump("jls_api.json", out)
 
 
+def gen_crypter_sweep(R):
+    """A broader sweep of both crypters through the reference (crypter_sweep.json): party counts
+    1..17, ragged lengths around the VES slot counts, rounds 0 and 2^64 - 1, unweighted / weighted
+    (incl. the largest weight), clipping ranges 1 .. 1e14, target ranges 7 .. 2^64, inputs with
+    clipped values, exact halves and signed zeros; every outcome (ciphertexts / masked vectors,
+    averaged floats, or the error raised) as the reference produces it."""
+    JC, LC = R.crypter.SecaggCrypter, R.crypter.SecaggLomCrypter
+    bp = W.BIPRIME0
+    rng = random.Random(21)
+    specials = [0.0, -0.0, 1.5, -1.5, 3.0, -3.0, 2.9999999999999996, 1e-300, 4.0, -4.0, 0.5, 1 / 3]
+
+    def params(p, n, clip):
+        x = [float(v) for v in W.party_params(50 + p, n)]
+        for i in range(0, n, 7):
+            x[i] = specials[(i // 7 + p) % len(specials)]
+        scale = 1.0 if clip is None else clip / 3.0
+        return [v * scale for v in x]
+
+    out = {"jl": [], "lom": []}
+    for P, n, tau, weighted, clip, target in [
+        (1, 31, 0, False, None, None), (3, 29, 2 ** 64 - 1, True, None, None), (5, 33, 12345, True, 1, 2 ** 20 + 3),
+        (7, 93, 4, False, None, 7), (12, 61, 9, True, 10 ** 6, 2 ** 40), (17, 40, 1, True, None, None),
+        (2, 120, 3, "max", None, None), (3, 50, 5, True, 10 ** 14, 2 ** 55), (2, 35, 6, False, 5, 2 ** 64),
+    ]:
+        keys = [rng.getrandbits(2040) * (1 if u % 3 else -1) for u in range(P)]
+        sk0 = -sum(keys)
+        xs = [params(p, n, clip) for p in range(P)]
+        ws = [(2 ** 17 - 1 if weighted == "max" else W.party_weight(p)) if weighted else None for p in range(P)]
+        enc = [_outcome(lambda p=p: [ihex(int(c)) for c in JC().encrypt(
+            num_nodes=P, current_round=tau, params=xs[p], key=keys[p], biprime=bp, clipping_range=clip,
+            weight=ws[p], target_range=target)]) for p in range(P)]
+        total = sum(ws) if weighted else P
+        agg = ({"error": "skipped", "msg": "an encrypt failed"} if any("error" in e for e in enc) else
+               _outcome(lambda: [fhex(v) for v in JC().aggregate(
+                   current_round=tau, num_nodes=P, params=[[I(c) for c in e["ok"]] for e in enc], key=sk0,
+                   biprime=bp, total_sample_size=total, clipping_range=clip, num_expected_params=n,
+                   target_range=target)]))
+        out["jl"].append({"P": P, "n": n, "tau": tau, "clip": clip, "target": None if target is None else ihex(target),
+                          "keys": [ihex(k) for k in keys], "weights": ws, "total": total,
+                          "x": [[fhex(v) for v in x] for x in xs], "enc": enc, "agg": agg})
+    for P, n, tau, weighted, clip, target, nonce in [
+        (2, 1, 0, False, None, None, "n1"), (3, 9, 2 ** 64 - 1, True, None, None, "0123456789abcdefXYZ"),
+        (5, 1001, 17, True, 1, 2 ** 20 + 3, "short"), (7, 64, 4, False, None, 7, "seven"),
+        (12, 333, 9, True, 10 ** 6, 2 ** 40, "twelve"), (17, 100, 1, True, None, None, W.LOM_NONCE),
+        (3, 200, 2, "max", None, None, "maxw"), (2, 77, 6, False, 5, 2 ** 64, "t64"),
+    ]:
+        ids = [f"n{u:02d}" for u in range(P)]
+        xs = [params(p, n, clip) for p in range(P)]
+        ws = [(2 ** 17 - 1 if weighted == "max" else W.party_weight(p)) if weighted else None for p in range(P)]
+        enc = [_outcome(lambda p=p: [ihex(int(v)) for v in LC(nonce=nonce).encrypt(
+            current_round=tau, node_id=ids[p], params=xs[p], pairwise_secrets=W.pairwise_secrets_for(ids[p], ids),
+            node_ids=ids, clipping_range=clip, weight=ws[p], target_range=target)]) for p in range(P)]
+        total = sum(ws) if weighted else P
+        agg = ({"error": "skipped", "msg": "an encrypt failed"} if any("error" in e for e in enc) else
+               _outcome(lambda: [fhex(v) for v in LC(nonce=nonce).aggregate(
+                   [[I(v) for v in e["ok"]] for e in enc], total, clipping_range=clip, target_range=target)]))
+        out["lom"].append({"P": P, "n": n, "tau": tau, "clip": clip, "target": None if target is None else ihex(target),
+                           "nonce_str": nonce, "ids": ids, "weights": ws, "total": total,
+                           "x": [[fhex(v) for v in x] for x in xs], "enc": enc, "agg": agg})
+    dump("crypter_sweep.json", out)
+
+
+def I(s):  # noqa: E743 - hex string -> int (the fixtures' encoding)
+    return int(s, 16)
+
+
 def main():
     R = load_reference.load()
     if sys.argv[1:] == ["jls_api"]:  # only the object-API fixture
         gen_jls_api(R)
+        return
+    if sys.argv[1:] == ["crypter_sweep"]:
+        gen_crypter_sweep(R)
         return
     gen_quantize(R)
     gen_lom(R)
@@ -473,6 +542,7 @@ def main():
     gen_edge(R)
     gen_dh(R)
     gen_jls_api(R)
+    gen_crypter_sweep(R)
     meta = {"generator": "tools/gen_golden.py", "reference": load_reference.REF,
             "note": "outputs of the reference Fed-BioMed crypter (Python), imported via tools/refshim"}
     dump("meta.json", meta)
