@@ -960,7 +960,7 @@ static int jl_combine_impl(const uint32_t* cts, int n_parties, uint64_t n_ct, in
     if ((rc = timed("jl_rk", s, [&] { return launch_jl_rk(r, w.cst, s); }))) return rc;
   }
   uint32_t* xs = x_raw ? x_raw : w.xs;
-  if ((rc = timed("jl_prod", s, [&] { return launch_jl_prod(cts, n_parties, n_ct, jp, w.cst, factor, w.X, xs, s); })))
+  if ((rc = timed("jl_prod", s, [&] { return launch_jl_prod(cts, n_parties, n_ct, jp, w.cst, factor, xs, s); })))
     return rc;
   if (x_raw) return FBM_OK;
   return timed("jl_decode", s, [&] {
@@ -1135,7 +1135,7 @@ int fbm_jl_product(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint
     jl_rk_for(jp.N32, n_parties - 1, r);
     if ((rc = timed("jl_rk", s, [&] { return launch_jl_rk(r, w.cst, s); }))) return rc;
   }
-  return timed("jl_prod", s, [&] { return launch_jl_prod(cts, n_parties, n_ct, jp, w.cst, nullptr, w.X, out, s); });
+  return timed("jl_prod", s, [&] { return launch_jl_prod(cts, n_parties, n_ct, jp, w.cst, nullptr, out, s); });
 }
 
 int fbm_jl_decrypt(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* biprime, const uint32_t* key,

@@ -180,7 +180,7 @@ struct JlRk {  // R^(P+1) mod N^2, 28-bit limbs (jl_rk_kernel -> cst[FBM_CST_RK]
 int launch_jl_rk(const JlRk& rk, uint32_t* cst, hipStream_t s);
 // x_k = (prod_u c_u * F_k mod N^2 - 1) div N   (cst[FBM_CST_RK] = R^(P+1) mod N^2)
 int launch_jl_prod(const uint32_t* cts, int n_parties, uint64_t n_ct, const JlParams& jp, const uint32_t* cst,
-                   const uint32_t* factor, uint32_t* X, uint32_t* xout, hipStream_t s);
+                   const uint32_t* factor, uint32_t* xout, hipStream_t s);
 #define FBM_EXP_DEC 1        // jl_exp mode bits: plain power (no nude product)
 #define FBM_EXP_OUT_NADIC 4  // out rows are the result's N-adic digits (v mod N, v div N)
 int host_gcd_is_one_r8(const uint32_t* r8, const uint32_t* n32, uint32_t* err);

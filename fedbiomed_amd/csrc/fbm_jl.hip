@@ -418,6 +418,13 @@ __device__ __forceinline__ void load_row64(const uint32_t* p, uint32_t (&w)[64])
     w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
   }
 }
+__device__ __forceinline__ void load_row32(const uint4* s, uint32_t (&w)[32]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint4 v = s[i];
+    w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+  }
+}
 __device__ __forceinline__ void store_row64(uint32_t* p, const uint32_t (&w)[64]) {
   uint4* o = reinterpret_cast<uint4*>(launder_v(p));
 #pragma unroll
@@ -1094,19 +1101,24 @@ __device__ __forceinline__ void div_by_n(uint32_t (&D)[64], const JlParams& jp, 
 // ------------------------------------------------------------------------------------
 // factor == nullptr: the bare product (EncryptedNumber sums, _jls.py:353-374): a starts from
 // R^P, P products, and the canonical v goes to xout [ct][64] (no decryption).
-__global__ void __launch_bounds__(FBM_BLOCK, 2) jl_prod_kernel(const uint32_t* __restrict__ cts, int n_parties,
+// The operand's 28-bit column goes to a second LDS column (150 KB of LDS: one workgroup per
+// CU).  A global scratch column instead (two workgroups per CU) was 8 % faster over several
+// rounds of workgroups but tripled the HBM traffic (write-back of the scratch through L2) and
+// was 10 % slower on an 8-GPU split's stripe (tools/ab_prod.sh).
+__global__ void __launch_bounds__(FBM_BLOCK, 1) jl_prod_kernel(const uint32_t* __restrict__ cts, int n_parties,
                                                               uint64_t n_ct, const uint32_t* __restrict__ cst,
                                                               JlParams jp, const uint32_t* __restrict__ factor,
-                                                              uint32_t* __restrict__ X, uint32_t* __restrict__ xout) {
+                                                              uint32_t* __restrict__ xout) {
   __shared__ uint32_t lds_a[(FBM_NL + 1) * FBM_BLOCK];
+  __shared__ uint32_t lds_b[(FBM_NL + 1) * FBM_BLOCK];
   const int tid = threadIdx.x;
   uint32_t* lds = lds_a + tid;
   const uint32_t aoff = lds_addr(lds);
   const uint32_t* M = cst + FBM_CST_M;
   const uint64_t ct_raw = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
-  const bool valid = ct_raw < n_ct;  // no early return: X is padded to whole blocks
+  const bool valid = ct_raw < n_ct;  // (an early return here measured 15 % slower)
   const uint64_t ct = valid ? ct_raw : n_ct - 1;
-  const uint32_t xoff = (uint32_t)(((ct_raw >> 8) * (FBM_NL * 256) + (ct_raw & 255)) * 4);
+  const uint32_t boff = lds_addr(lds_b + tid);
   lds_store_uniform<FBM_NL>(lds, FBM_BLOCK, cst + FBM_CST_RK);
   const int n_ops = n_parties + (factor ? 1 : 0);
 #pragma unroll 1
@@ -1116,9 +1128,9 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_prod_kernel(const uint32_t* _
       uint32_t c32[64], c28[FBM_NL];
       load_row64(row, c32);
       to28<64, FBM_NL>(c32, c28);
-      col_store(X + xoff / 4, c28);
+      lds_store_col(lds_b + tid, FBM_BLOCK, c28);
     }
-    fbm_mm_glb(aoff, X, xoff, M, jp.mc.mp);
+    fbm_mm_lds(aoff, boff, M, jp.mc.mp);
   }
   uint32_t D[64];
   {
@@ -1248,32 +1260,15 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_lift_kernel(uint64_t n_ct, Jl
   const int tid = threadIdx.x;
   uint32_t* lds = lds_a + tid;
   const int ls = FBM_BLOCK;
-  const uint64_t ct = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
-  if (ct >= n_ct) return;
-  uint32_t y[32], a[32], acc[FBM_NLN];
+  const uint64_t ct0 = (uint64_t)blockIdx.x * FBM_BLOCK;
+  const uint64_t ct = ct0 + tid < n_ct ? ct0 + tid : n_ct - 1;  // no early return: barriers below
+  // y, e0 and a are (re)loaded / formed where they are used: nothing 1024-bit stays live across
+  // the Montgomery products (no scratch spills; the rows are L2-resident re-reads)
+  const uint4* yi = reinterpret_cast<const uint4*>(Y + ct * 32);
+  uint32_t acc[FBM_NLN];
   {
-    uint32_t e0[32];
-    const uint4* ei = reinterpret_cast<const uint4*>(Ed + ct * 64);
-    const uint4* yi = reinterpret_cast<const uint4*>(Y + ct * 32);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint4 v = ei[i], w = yi[i];
-      e0[4 * i] = v.x; e0[4 * i + 1] = v.y; e0[4 * i + 2] = v.z; e0[4 * i + 3] = v.w;
-      y[4 * i] = w.x; y[4 * i + 1] = w.y; y[4 * i + 2] = w.z; y[4 * i + 3] = w.w;
-    }
-    uint32_t p[32];
-    mullo1024(e0, y, p);
-    uint32_t br = 1;  // p = e0 y - 1 (mod 2^1024)
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      const uint64_t d = (uint64_t)p[i] - br;
-      p[i] = (uint32_t)d;
-      br = (uint32_t)(d >> 63);
-    }
-    mullo1024(p, jp.Ninv32, a);
-  }
-  {
-    uint32_t y28[FBM_NLN];
+    uint32_t y[32], y28[FBM_NLN];
+    load_row32(yi, y);
     to28<32, FBM_NLN>(y, y28);
     lds_store_col(lds, ls, y28);
   }
@@ -1283,16 +1278,23 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_lift_kernel(uint64_t n_ct, Jl
   lds_store_col(lds, ls, acc);
   {
     uint32_t e1[32];
-    const uint4* ei = reinterpret_cast<const uint4*>(Ed + ct * 64 + 32);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint4 v = ei[i];
-      e1[4 * i] = v.x; e1[4 * i + 1] = v.y; e1[4 * i + 2] = v.z; e1[4 * i + 3] = v.w;
-    }
+    load_row32(reinterpret_cast<const uint4*>(Ed + ct * 64 + 32), e1);
     to28<32, FBM_NLN>(e1, acc);
   }
   mont_mul(acc, lds, ls, mn);  // u = e1 y (lazy < 2N)
   {
+    uint32_t e0[32], y[32], p[32], a[32];
+    load_row32(reinterpret_cast<const uint4*>(Ed + ct * 64), e0);
+    load_row32(yi, y);
+    mullo1024(e0, y, p);
+    uint32_t br = 1;  // p = e0 y - 1 (mod 2^1024)
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const uint64_t d = (uint64_t)p[i] - br;
+      p[i] = (uint32_t)d;
+      br = (uint32_t)(d >> 63);
+    }
+    mullo1024(p, jp.Ninv32, a);
     uint32_t a28[FBM_NLN];
     to28<32, FBM_NLN>(a, a28);
     uint32_t c = 0;
@@ -1337,9 +1339,10 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_lift_kernel(uint64_t n_ct, Jl
   }
   uint32_t v[32];
   from28<FBM_NLN, 32>(acc, v);
-  uint4* o = reinterpret_cast<uint4*>(out + ct * 64);
   uint32_t f[64];  // y + N v < N^2
   mul1024(v, jp.N32, f);
+  uint32_t y[32];
+  load_row32(yi, y);
   uint32_t c = 0;
 #pragma unroll
   for (int i = 0; i < 64; ++i) {
@@ -1347,8 +1350,28 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_lift_kernel(uint64_t n_ct, Jl
     f[i] = (uint32_t)t;
     c = (uint32_t)(t >> 32);
   }
+  // The workgroup's rows are one contiguous range of out: staged through LDS in two halves
+  // (128 B of every row, padded stride 33 words), each 128-B line is written whole by eight
+  // consecutive work-items -- per-lane 16-B row stores left partial lines to the L2, written
+  // back up to 3x over at the full vector (tools/pmc_agg.sh).  Every lane has read its Ed row
+  // (out may alias it) before the first barrier.
+  const uint64_t rows = n_ct - ct0 < FBM_BLOCK ? n_ct - ct0 : FBM_BLOCK;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) o[i] = make_uint4(f[4 * i], f[4 * i + 1], f[4 * i + 2], f[4 * i + 3]);
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 32; ++i) lds_a[tid * 33 + i] = f[32 * h + i];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = k * FBM_BLOCK + tid;  // 16-B chunk q: row q / 8, chunk q % 8 of its half
+      const int r = q >> 3, c4 = (q & 7) * 4;
+      if ((uint64_t)r < rows) {
+        const uint32_t* src = lds_a + r * 33 + c4;
+        *reinterpret_cast<uint4*>(out + (ct0 + r) * 64 + 32 * h + c4) = make_uint4(src[0], src[1], src[2], src[3]);
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1699,10 +1722,10 @@ int jl_batch_flush(void* workspace, uint64_t ws_bytes, hipStream_t s) {
 }
 
 int launch_jl_prod(const uint32_t* cts, int n_parties, uint64_t n_ct, const JlParams& jp, const uint32_t* cst,
-                   const uint32_t* factor, uint32_t* X, uint32_t* xout, hipStream_t s) {
+                   const uint32_t* factor, uint32_t* xout, hipStream_t s) {
   if (n_ct == 0) return FBM_OK;
   hipLaunchKernelGGL(jl_prod_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, cts, n_parties, n_ct, cst, jp,
-                     factor, X, xout);
+                     factor, xout);
   return check_launch("jl_prod_kernel");
 }
 
