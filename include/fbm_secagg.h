@@ -76,7 +76,10 @@ int fbm_check_stats(const uint32_t* host_stats, int lom_nodes, uint32_t* max_bit
  *              (multiple of 8; 0 for a whole vector): PRF block counter and (i + tau) use
  *              global indices, so shards concatenate to the unsharded result.
  * With x_dtype == FBM_U64, x holds integers used as-is (x == NULL: zeros) and only the
- * weight multiplies them (weight 1 = LOM.protect semantics).                           */
+ * weight multiplies them (weight 1 = LOM.protect semantics).
+ * Status words (fbm_check_stats with lom_nodes = P): the overflow guard (FBM_E_OVERFLOW), then,
+ * with n_peers > 0, some global i + tau >= 2^64 (FBM_E_ROUND: the reference's OverflowError from
+ * (i + tau).to_bytes(8), _lom.py:81; the counters wrap meanwhile) -- the reference's order.    */
 int fbm_lom_protect(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
                     uint64_t target_m1, uint64_t weight, const uint8_t* secrets, const int8_t* signs, int n_peers,
                     int raw_seeds, const uint8_t* nonce, uint64_t tau, uint64_t elem_offset, uint64_t* y,
