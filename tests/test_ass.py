@@ -182,3 +182,29 @@ def test_wide_limb_roundtrip_and_draw_map():
             carry = int((x & (2**64 - 1)) + (x >> b) >= 2**64)
             r = (x >> 64) + carry
             assert r == (x * (2**b + 1)) >> (b + 64) and 0 <= r <= 2**b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["int", "list"])
+def test_share_exchange_flows(dev, kind):
+    """reference tests/test_additive_ss.py:90-180: share addition, and the key setup's exchange
+    (every user splits its key in 3, keeps one share, sends the others; the sums of what each
+    user holds reconstruct the sum of the keys)."""
+    import random
+
+    from fedbiomed_amd.exceptions import FedbiomedTypeError
+    from fedbiomed_amd.secagg import AdditiveSecret, AdditiveShares
+
+    if kind == "int":
+        assert (AdditiveSecret(10).split(2) + AdditiveSecret(15).split(2)).reconstruct() == 25
+        with pytest.raises(FedbiomedTypeError):
+            AdditiveSecret(10).split(2) + AdditiveSecret([1, 2, 3]).split(2)
+    else:
+        assert (AdditiveSecret([1, 2, 3]).split(3) + AdditiveSecret([4, 5, 6]).split(3)).reconstruct() == [5, 7, 9]
+    rnd = random.Random(11)
+    keys = [rnd.randint(0, 2**2048) if kind == "int" else [rnd.randint(0, 2**50) for _ in range(10)]
+            for _ in range(3)]
+    shares = [AdditiveSecret(k).split(3) for k in keys]
+    held = [shares[u][u] + shares[(u + 1) % 3][u] + shares[(u + 2) % 3][u] for u in range(3)]
+    got = AdditiveShares(held).reconstruct()
+    assert got == (sum(keys) if kind == "int" else [sum(c) for c in zip(*keys)])
