@@ -68,6 +68,21 @@ def test_quantize_reference_tests(dev):
     assert quantize([-5.0, 0.0, 5.0], 5, 2**64) == [0, 2**63, 2**64 - 1]
     with pytest.raises(OverflowError):
         quantize([7.0], 7, 2**64 + 1)
+    with pytest.raises(OverflowError):
+        quantize([0.0], None, 2**65)
+
+
+def test_reverse_quantize_reference_tests(dev):
+    # reference tests/test_joye_libert.py:511-561
+    from fedbiomed_amd.exceptions import FedbiomedSecaggCrypterError
+    from fedbiomed_amd.utils import reverse_quantize
+
+    for w, c, t, ref in (([0, 5, 10], 5, 11, [-5, 0, 5]), ([0, 1, 3, 8], 2, 9, [-2, -1.5, -0.5, 2]),
+                         ([0, 6], None, 7, [-3, 3]), ([0, 2**63, 2**64 - 1], 10, 2**64, [-10, 0, 10])):
+        assert reverse_quantize(w, c, t) == pytest.approx(ref, abs=1e-7)
+    for w, c, t in (([-1], None, 2**64), ([2**64], None, 2**64), ([2**64], 2, 10)):
+        with pytest.raises(FedbiomedSecaggCrypterError):
+            reverse_quantize(w, c, t)
 
 
 # ---------------------------------------------------------------- LOM
