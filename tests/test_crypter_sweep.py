@@ -152,3 +152,20 @@ def test_lom_round_counter_edges():
         with pytest.raises(FedbiomedSecaggError):  # the overflow guard first
             LOM(nonce=nonce).protect("b", sec, tau, [2 ** 62] + x, ids)
     assert LOM(nonce=nonce).protect("b", {}, top + 1, x, ["b"]) == x  # no peers: no PRF call
+
+
+def test_lom_overflow_message_word_for_word(golden):
+    """The overflow guard's message (secagg/_lom.py:137-149) as the host mirror builds it from the
+    status words, against the reference's own text in the sweep fixture (CPU: no device call)."""
+    import re
+
+    from fedbiomed_amd import _device as D
+
+    seen = 0
+    for c in golden["crypter_sweep"]["lom"]:
+        for e in c["enc"]:
+            if e.get("error") == "FedbiomedSecaggError" and "overflow detected" in e["msg"]:
+                bits = int(re.search(r"requires (\d+) bits", e["msg"]).group(1))
+                assert D._lom_overflow_message(bits, c["P"]) == e["msg"]
+                seen += 1
+    assert seen
