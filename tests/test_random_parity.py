@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 from fedbiomed_amd import workload as W
+from fedbiomed_amd.constants import SAParameters
 from oracle import secagg_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -230,3 +231,24 @@ def test_jl_random_tensor_engines(dev, seed):
     assert [int(a) | (int(b) << 64) for a, b in s] == want, seed
     ref = O.reverse_quantize(O.apply_average(want, sum(ws)), clip, tr)
     assert _bits(out.cpu().numpy()) == _bits(ref)
+
+
+@pytest.mark.parametrize("n_ct", [255, 256, 257, 512])
+def test_jl_aggregate_block_boundaries(dev, n_ct):
+    """Ciphertext counts around the 256-lane workgroups of the combine (jl_prod_kernel: operand
+    column in LDS) and of the factor's inverse lift (jl_lift_kernel: output rows staged through
+    LDS, a partial last workgroup writes only its own rows): outputs bit-exact vs the oracle."""
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    rng = np.random.default_rng(7000 + n_ct)
+    P, clip, target = 3, 3, SAParameters.TARGET_RANGE
+    es, cr_ = O.jl_slot(target, P)
+    n = n_ct * cr_ - int(rng.integers(0, cr_))
+    keys = [W.jl_user_key(900 + p) for p in range(P)]
+    xs = [_params(rng, n, clip) for _ in range(P)]
+    jc = SecaggCrypter()
+    cts = [jc.encrypt(P, 5, xs[p], keys[p], W.BIPRIME0, clipping_range=clip) for p in range(P)]
+    assert len(cts[0]) == n_ct
+    out = jc.aggregate(5, P, cts, -sum(keys), W.BIPRIME0, P, clipping_range=clip, num_expected_params=n)
+    ref = O.jl_crypter_aggregate(cts, 5, -sum(keys), W.BIPRIME0, P, n, clip=clip)
+    assert _bits(out) == _bits(ref)
