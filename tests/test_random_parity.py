@@ -252,3 +252,20 @@ def test_jl_aggregate_block_boundaries(dev, n_ct):
     out = jc.aggregate(5, P, cts, -sum(keys), W.BIPRIME0, P, clipping_range=clip, num_expected_params=n)
     ref = O.jl_crypter_aggregate(cts, 5, -sum(keys), W.BIPRIME0, P, n, clip=clip)
     assert _bits(out) == _bits(ref)
+
+
+def test_lom_more_peers_than_one_argument_block(dev):
+    """70 parties: every node has 69 peers, past the 64-peer kernel-argument block (the first group
+    with the quantise / overflow statistics, the rest accumulated in place): masked vectors
+    bit-exact vs the oracle for a few nodes, and all 70 masks cancel in the aggregate."""
+    from fedbiomed_amd.secagg import LOM
+
+    rng = np.random.default_rng(70)
+    ids = [f"n{u:03d}" for u in range(70)]
+    n, tau, nonce = 37, 12345, bytes(range(16))
+    xs = [rng.integers(0, 2**20, size=n).tolist() for _ in ids]
+    ys = [LOM(nonce=nonce).protect(u, W.pairwise_secrets_for(u, ids), tau, xs[p], ids) for p, u in enumerate(ids)]
+    for p in (0, 33, 69):
+        ref = O.lom_protect(ids[p], W.pairwise_secrets_for(ids[p], ids), tau, xs[p], ids, nonce)
+        assert ys[p] == [int(v) for v in ref]
+    assert LOM(nonce=nonce).aggregate(ys) == [sum(c) for c in zip(*xs)]
