@@ -605,6 +605,16 @@ class PendingEncrypt:
         return self._ct
 
 
+def _check_round(tau: int) -> None:
+    """The JL round's domain: FDH.H serialises t = (k << 512) | tau (_jls.py:742-760), so a negative
+    round is the reference's OverflowError; rounds of 2^64 and above are valid there (up to 2^512)
+    but outside the device path's 64-bit round (FB624)."""
+    if tau < 0:
+        raise OverflowError("can't convert negative int to unsigned")
+    if tau > U64_MAX:
+        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: round must be in [0, 2^64)")
+
+
 def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, clip=None, target=None,
                weight: int = 1, slot: Optional[Tuple[int, int]] = None, ct_offset: int = 0,
                defer_exp: bool = False, kind: Optional[str] = None):
@@ -620,8 +630,7 @@ def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, 
     es, cr = slot if slot else jl_slot(target, n_users)
     raw = kind is not None or x.dtype == torch.int64
     c, c2, tf, tm1 = (1.0, 2.0, 1.0, 0) if raw else quant_params(clip, target)
-    if tau < 0 or tau > U64_MAX:
-        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: round must be in [0, 2^64)")
+    _check_round(tau)
     x = x.contiguous()
     if kind == "u128":
         xdt, n = N.FBM_U128, x.shape[0]
@@ -695,8 +704,7 @@ def jl_decrypt_factor(n_ct: int, biprime: int, key: int, tau: int, ct_offset: in
     phased: issue only the first phase (constants + FDH) and return a PendingFactor."""
     dev = dev or device()
     lib = N.load()
-    if tau < 0 or tau > U64_MAX:
-        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: round must be in [0, 2^64)")
+    _check_round(tau)
     f = torch.empty((n_ct, 64), dtype=torch.int32, device=dev)
     if n_ct == 0:
         return f
@@ -738,8 +746,7 @@ def jl_aggregate(cts: torch.Tensor, biprime: int, key: int, tau: int, n_expected
     if total_weight < 0 or total_weight > U64_MAX:
         raise FedbiomedSecaggCrypterError(
             f"{ErrorNumbers.FB624.value}: total_sample_size must be in [1, 2^64) for the device path")
-    if tau < 0 or tau > U64_MAX:
-        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: round must be in [0, 2^64)")
+    _check_round(tau)
     out = torch.empty(n_out, dtype=torch.float64, device=dev) if want_out else None
     sums = torch.empty((n_out, 2), dtype=torch.int64, device=dev) if want_sums else None
     if n_ct == 0:
@@ -875,7 +882,8 @@ def jl_fdh(n_ct: int, modulus: int, tau: int, ct_offset: int = 0, dev=None) -> t
     """FDH.H(t_k) of t_k = ((k + ct_offset) << 512) | tau, bits_size 2048, gcd against `modulus`
     (any M: its odd part, or its square root's) -> int32 [n_ct, 64] limbs."""
     dev = dev or device()
-    if not (0 <= tau <= U64_MAX and 0 <= ct_offset and ct_offset + max(n_ct, 1) - 1 <= U64_MAX):
+    _check_round(tau)
+    if not (0 <= ct_offset and ct_offset + max(n_ct, 1) - 1 <= U64_MAX):
         raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: FDH input outside the device path's domain")
     odd, even = fdh_modulus(modulus)
     h = torch.empty((n_ct, 64), dtype=torch.int32, device=dev)
@@ -907,8 +915,7 @@ def jl_decrypt(cts: torch.Tensor, biprime: int, key: int, tau: int, ct_offset: i
     x = torch.empty((n_ct, 32), dtype=torch.int32, device=dev)
     if n_ct == 0:
         return x
-    if tau < 0 or tau > U64_MAX:
-        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: round must be in [0, 2^64)")
+    _check_round(tau)
     lib = N.load()
     bp = _biprime_limbs(biprime)
     kl, kneg = _key_limbs(key)

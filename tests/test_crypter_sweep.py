@@ -44,8 +44,10 @@ def test_jl_sweep_oracle(golden, idx):
     target = I(c["target"]) if c["target"] else None
     keys = [I(k) for k in c["keys"]]
     for p, e in enumerate(c["enc"]):
-        got = O.jl_encrypt([F(v) for v in c["x"][p]], c["tau"], keys[p], W.BIPRIME0, c["P"], clip=c["clip"],
-                           weight=c["weights"][p], target=target)
+        got = _run(e, lambda p=p: O.jl_encrypt([F(v) for v in c["x"][p]], c["tau"], keys[p], W.BIPRIME0, c["P"],
+                                               clip=c["clip"], weight=c["weights"][p], target=target))
+        if got is None:  # an expected error: the reference skipped the aggregate
+            return
         assert got == [I(v) for v in e["ok"]]
     cts = [[I(v) for v in e["ok"]] for e in c["enc"]]
     out = O.jl_crypter_aggregate(cts, c["tau"], -sum(keys), W.BIPRIME0, c["total"], c["n"], clip=c["clip"],
@@ -68,7 +70,9 @@ def test_jl_sweep_gpu(golden, idx, caplog):
                                                weight=c["weights"][p], target_range=target))
                 for p, e in enumerate(c["enc"])]
     for got, e in zip(encs, c["enc"]):
-        assert got == [I(v) for v in e["ok"]]
+        assert got == ([I(v) for v in e["ok"]] if "ok" in e else None)
+    if c["agg"].get("error") == "skipped":  # an encrypt failed (as expected): nothing to aggregate
+        return
     out = _run(c["agg"], lambda: jc.aggregate(current_round=c["tau"], num_nodes=c["P"], params=encs, key=-sum(keys),
                                               biprime=W.BIPRIME0, total_sample_size=c["total"],
                                               clipping_range=c["clip"], num_expected_params=c["n"],

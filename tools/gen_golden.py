@@ -463,7 +463,7 @@ def gen_jls_api(R):
 
 def gen_crypter_sweep(R):
     """A broader sweep of both crypters through the reference (crypter_sweep.json): party counts
-    1..17, ragged lengths around the VES slot counts, rounds 0 and 2^64 - 1, unweighted / weighted
+    1..17, ragged lengths around the VES slot counts, rounds 0, 2^64 - 1 and -1, unweighted / weighted
     (incl. the largest weight), clipping ranges 1 .. 1e14, target ranges 7 .. 2^64, inputs with
     clipped values, exact halves and signed zeros; every outcome (ciphertexts / masked vectors,
     averaged floats, or the error raised) as the reference produces it."""
@@ -484,6 +484,7 @@ def gen_crypter_sweep(R):
         (1, 31, 0, False, None, None), (3, 29, 2 ** 64 - 1, True, None, None), (5, 33, 12345, True, 1, 2 ** 20 + 3),
         (7, 93, 4, False, None, 7), (12, 61, 9, True, 10 ** 6, 2 ** 40), (17, 40, 1, True, None, None),
         (2, 120, 3, "max", None, None), (3, 50, 5, True, 10 ** 14, 2 ** 55), (2, 35, 6, False, 5, 2 ** 64),
+        (2, 5, -1, False, None, None),
     ]:
         keys = [rng.getrandbits(2040) * (1 if u % 3 else -1) for u in range(P)]
         sk0 = -sum(keys)
@@ -506,6 +507,7 @@ def gen_crypter_sweep(R):
         (5, 1001, 17, True, 1, 2 ** 20 + 3, "short"), (7, 64, 4, False, None, 7, "seven"),
         (12, 333, 9, True, 10 ** 6, 2 ** 40, "twelve"), (17, 100, 1, True, None, None, W.LOM_NONCE),
         (3, 200, 2, "max", None, None, "maxw"), (2, 77, 6, False, 5, 2 ** 64, "t64"),
+        (2, 5, -1, False, None, None, "neg"),
     ]:
         ids = [f"n{u:02d}" for u in range(P)]
         xs = [params(p, n, clip) for p in range(P)]
