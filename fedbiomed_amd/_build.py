@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_lib", "libfbm_secagg.so")
-SOURCES = ["fbm_lom.hip", "fbm_jl.hip", "fbm_ass.hip", "fbm_capi.hip"]
+SOURCES = ["fbm_lom.hip", "fbm_jl.hip", "fbm_gen.hip", "fbm_ass.hip", "fbm_capi.hip"]
 # host-side list <-> buffer conversions of the list API (a CPython extension, plain gcc)
 PYCONV_SRC = os.path.join(CSRC, "fbm_pyconv.c")
 PYCONV_OUT = os.path.join(HERE, "_lib", "_fbm_pyconv" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))

@@ -480,9 +480,11 @@ def dequantize(u: torch.Tensor, clip=None, target=None) -> torch.Tensor:
 # Joye-Libert
 # ------------------------------------------------------------------------------------------
 def _biprime_limbs(biprime: int) -> np.ndarray:
-    if biprime <= 0 or biprime.bit_length() > 1024:
+    """N as 32 limbs.  Any 2 <= N < 2^1024: an odd N runs on the Montgomery engines, an even one on
+    the generic engine (csrc/fbm_gen.hip), as the reference computes with any N (_jls.py:37-73)."""
+    if biprime < 2 or biprime.bit_length() > 1024:
         raise FedbiomedSecaggCrypterError(
-            f"{ErrorNumbers.FB624.value}: biprime must be a positive integer of at most 1024 bits")
+            f"{ErrorNumbers.FB624.value}: biprime must be an integer in [2, 2^1024) (the device path's domain)")
     return int_limbs(biprime, 32)
 
 
@@ -494,14 +496,16 @@ def _key_limbs(key: int) -> Tuple[np.ndarray, int]:
 
 JL_MAX_CT = 14_000_000  # include/fbm_secagg.h FBM_JL_MAX_CT: ciphertexts per library call
 
-_ENGINES = {"auto": 0, "single": 1, "triple": 3, "quad": 4}
+_ENGINES = {"auto": 0, "single": 1, "generic": 2, "triple": 3, "quad": 4}
 
 
 class jl_engine:
     """Exponentiation engine for the JL calls issued inside (process-wide policy,
     fbm_jl_set_engine): "auto" (the library's choice by launch size), "single" (one lane per
     ciphertext: several concurrent launches that fill the chip together), "quad" / "triple"
-    (four / three lanes per ciphertext: latency of a launch below the chip's lane count).
+    (four / three lanes per ciphertext: latency of a launch below the chip's lane count),
+    "generic" (csrc/fbm_gen.hip, Barrett products for any modulus: even biprimes always take it;
+    under this policy odd ones do too -- a cross-check of the Montgomery engines).
     Results are bit-identical under every engine.
 
         with D.jl_engine("single"):
@@ -524,7 +528,7 @@ class jl_engine:
 
 def jl_engine_for(n_ct: int) -> str:
     """The engine a launch of n_ct ciphertexts takes under the current policy."""
-    return {1: "single", 3: "triple", 4: "quad"}[N.load().fbm_jl_engine_for(int(n_ct))]
+    return {1: "single", 2: "generic", 3: "triple", 4: "quad"}[N.load().fbm_jl_engine_for(int(n_ct))]
 
 
 def jl_chunk_ct() -> int:
@@ -541,7 +545,8 @@ class jl_exp_batch:
     streams map onto the hardware queues.  The recorded calls' prologues must be complete on the
     current stream at exit (wait on their streams first) and their outputs are valid after it;
     the same biprime throughout; at most 24 calls.  A factor's inverse (PendingFactor.finish)
-    goes after the context.
+    goes after the context.  An even biprime's calls (the generic engine) are not recorded: they
+    launch when issued, on the current stream.
 
         with D.jl_exp_batch():
             cts = [pend[p].finish() for p in range(P)]
@@ -871,11 +876,11 @@ def fdh_modulus(m: int) -> Tuple[int, bool]:
         even = base % 2 == 0
         while base and base % 2 == 0:
             base //= 2
-        if 3 <= base < 2**1024:
+        if 1 <= base < 2**1024:
             return base, even
     raise FedbiomedSecaggCrypterError(
         f"{ErrorNumbers.FB624.value}: FDH modulus outside the device path's domain (odd part of M or of its "
-        "square root in [3, 2^1024))")
+        "square root in [1, 2^1024))")
 
 
 def jl_fdh(n_ct: int, modulus: int, tau: int, ct_offset: int = 0, dev=None) -> torch.Tensor:

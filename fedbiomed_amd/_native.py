@@ -91,6 +91,8 @@ SIGNATURES = {
     "fbm_test_modinv": (c_int, [c_vp, c_vp, c_vp, c_vp]),
     "fbm_test_nadic_consts": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fbm_test_fdh_gcd": (c_int, [c_vp, c_vp, c_vp]),
+    "fbm_test_gen_exp": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "fbm_test_gen_combine": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp]),
     "fbm_prof_enable": (c_int, [c_int]),
     "fbm_prof_report": (c_int, [ctypes.c_char_p, c_int]),
 }

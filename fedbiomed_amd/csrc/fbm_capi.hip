@@ -300,6 +300,140 @@ static void build_quad(const Big& N, const Big& M, QuadCtx& qa) {
   qa.np = (0u - inv) & ((1u << LB) - 1u);
 }
 
+// SHA-256 midstate over the 14 leading all-zero blocks of t.to_bytes(1024,'big') (FDH.H)
+static void fdh_midstate(uint32_t mid[8]) {
+  uint32_t st[8], W[16];
+  fbm_sha256_init(st);
+  memset(W, 0, sizeof(W));
+  for (int b = 0; b < 14; ++b) fbm_sha256_compress(st, W);
+  memcpy(mid, st, sizeof(st));
+}
+
+static void big_trim(Big& a) {
+  while (a.size() > 1 && a.back() == 0u) a.pop_back();
+}
+
+static int big_ctz(const Big& a) {
+  for (size_t i = 0; i < a.size(); ++i)
+    if (a[i]) return 32 * (int)i + __builtin_ctz(a[i]);
+  return 0;
+}
+
+static Big big_shr(const Big& a, int s) {
+  Big r(a.size(), 0u);
+  const int w = s >> 5, b = s & 31;
+  for (size_t i = 0; i + w < a.size(); ++i) {
+    const uint64_t lo = a[i + w], hi = i + w + 1 < a.size() ? a[i + w + 1] : 0u;
+    r[i] = (uint32_t)((((hi << 32) | lo) >> b));
+  }
+  big_trim(r);
+  return r;
+}
+
+// a b mod 2^(32 n)
+static Big big_mullo(const Big& a, const Big& b, size_t n) {
+  Big r(n, 0u);
+  for (size_t i = 0; i < n && i < a.size(); ++i) {
+    uint64_t c = 0;
+    for (size_t j = 0; i + j < n; ++j) {
+      const uint64_t t = (uint64_t)a[i] * (j < b.size() ? b[j] : 0u) + r[i + j] + c;
+      r[i + j] = (uint32_t)t;
+      c = t >> 32;
+    }
+  }
+  return r;
+}
+
+// FDH.H's parameters only (fbm_jl_fdh and the generic engine): the gcd modulus' odd part
+// (>= 1; 1: every odd r is coprime) and whether r must be odd as well
+static int fdh_params(const uint32_t* n_odd, int even, uint64_t tau, uint64_t ct_offset, JlParams& jp) {
+  if (!(n_odd[0] & 1u)) {
+    set_error("FDH: the gcd modulus' odd part must be odd");
+    return FBM_E_ARG;
+  }
+  memset(&jp, 0, sizeof(jp));
+  for (int i = 0; i < 32; ++i) jp.N32[i] = n_odd[i];
+  jp.fdh_even = even ? 1 : 0;
+  jp.tau = tau;
+  jp.ct_offset = ct_offset;
+  fdh_midstate(jp.mid);
+  return FBM_OK;
+}
+
+// FDH(2048, N^2): gcd(r, N^2) == 1 iff r is coprime to N's odd part (and odd, for an even N)
+static int fdh_params_for_biprime(const uint32_t* biprime, uint64_t tau, uint64_t ct_offset, JlParams& jp) {
+  Big N(biprime, biprime + 32);
+  const int s = big_ctz(N);
+  Big m = big_shr(N, s);
+  m.resize(32, 0u);
+  return fdh_params(m.data(), s > 0, tau, ct_offset, jp);
+}
+
+// the generic engine (fbm_gen.hip) takes every even N, and every N under FBM_ENGINE_GENERIC
+static bool jl_generic(const uint32_t* biprime) {
+  return (biprime[0] & 1u) == 0u || jl_engine_policy() == FBM_ENGINE_GENERIC;
+}
+
+// GenCtx of (N, key): M = N^2, Barrett constants of M and N, M = 2^e m2 with m2 odd, m2^-1 mod 2^e
+static int build_gen_ctx(const uint32_t* biprime, const uint32_t* key, int key_negative, GenCtx& g) {
+  memset(&g, 0, sizeof(g));
+  Big N(biprime, biprime + 32);
+  big_trim(N);
+  if (big_bits(N) < 2) {
+    set_error("biprime must be >= 2 (N = 1 is outside the device path's domain)");
+    return FBM_E_UNSUPPORTED;
+  }
+  Big M = big_mul(N, N);
+  big_trim(M);
+  auto mu = [](const Big& m) {  // floor(2^(64 k) / m), k = words of m
+    Big a(2 * m.size() + 1, 0u), q, r;
+    a.back() = 1u;
+    big_divmod(a, m, q, r);
+    big_trim(q);
+    return q;
+  };
+  const Big muM = mu(M), muN = mu(N);
+  g.kM = (int)M.size();
+  g.kN = (int)N.size();
+  for (size_t i = 0; i < M.size(); ++i) g.M[i] = M[i];
+  for (size_t i = 0; i < muM.size() && i < 68; ++i) g.muM[i] = muM[i];
+  for (size_t i = 0; i < N.size(); ++i) g.N[i] = N[i];
+  for (size_t i = 0; i < muN.size() && i < 36; ++i) g.muN[i] = muN[i];
+  const int s = big_ctz(N);
+  const Big m = big_shr(N, s);
+  Big m2 = big_mul(m, m);
+  big_trim(m2);
+  g.km2 = (int)m2.size();
+  g.e = 2 * s;
+  for (size_t i = 0; i < m2.size(); ++i) g.m2[i] = m2[i];
+  if (g.e > 0) {  // m2^-1 mod 2^e by Newton (m2 odd): y <- y (2 - m2 y), 32 -> 64 -> ... bits
+    const size_t W = (size_t)((g.e + 31) / 32);
+    uint32_t y0 = m2[0];
+    for (int i = 0; i < 5; ++i) y0 *= 2u - m2[0] * y0;
+    Big y(W, 0u);
+    y[0] = y0;
+    for (size_t prec = 32; prec < 32 * W; prec *= 2) {
+      Big t = big_mullo(m2, y, W);
+      uint64_t c = 3;  // 2 - t = ~t + 3 (mod 2^(32 W))
+      for (size_t i = 0; i < W; ++i) {
+        c += (uint32_t)~t[i];
+        t[i] = (uint32_t)c;
+        c >>= 32;
+      }
+      y = big_mullo(y, t, W);
+    }
+    if (g.e & 31) y[W - 1] &= (1u << (g.e & 31)) - 1u;
+    for (size_t i = 0; i < W; ++i) g.m2inv[i] = y[i];
+  }
+  if (key) {
+    Big K(key, key + 64);
+    g.key_bits = big_bits(K);
+    for (int i = 0; i < 64; ++i) g.key[i] = key[i];
+    g.key_negative = key_negative ? 1 : 0;
+  }
+  return FBM_OK;
+}
+
 // The modulus-dependent part of JlParams (Montgomery / N-adic / group-engine constants, N^-1
 // mod 2^1024, the FDH midstate): ~0.3 ms of host big-integer work per call, so it is built once
 // per biprime and kept in a small process-wide cache (a round's encrypts and aggregate, and
@@ -309,8 +443,8 @@ static int build_jl_params_uncached(const uint32_t* biprime, int es, int cr, uin
   memset(&jp, 0, sizeof(jp));
   Big N(biprime, biprime + 32);
   const int nb = big_bits(N);
-  if (nb < 2 || (N[0] & 1u) == 0u) {
-    set_error("biprime must be odd and >= 3 (device Montgomery path); got %d bits, %s", nb,
+  if (nb < 2 || (N[0] & 1u) == 0u) {  // an even N takes the generic engine before this (jl_generic)
+    set_error("biprime must be >= 2 (the Montgomery engines take an odd N >= 3); got %d bits, %s", nb,
               (N[0] & 1u) ? "odd" : "even");
     return FBM_E_UNSUPPORTED;
   }
@@ -372,12 +506,7 @@ static int build_jl_params_uncached(const uint32_t* biprime, int es, int cr, uin
   jp.cr = cr;
   jp.tau = tau;
   jp.ct_offset = ct_offset;
-  // SHA-256 midstate over the 14 leading all-zero blocks of t.to_bytes(1024,'big')
-  uint32_t st[8], W[16];
-  fbm_sha256_init(st);
-  memset(W, 0, sizeof(W));
-  for (int b = 0; b < 14; ++b) fbm_sha256_compress(st, W);
-  memcpy(jp.mid, st, sizeof(st));
+  fdh_midstate(jp.mid);
   return FBM_OK;
 }
 
@@ -579,8 +708,10 @@ int fbm_jl_quad_mads(int square) { return 4 * (square ? FBM_QA_MADS_SQR : FBM_QA
 int fbm_jl_triple_mads(int square) { return 3 * (square ? FBM_TA_MADS_SQR : FBM_TA_MADS_MUL); }
 
 int fbm_jl_set_engine(int mode) {
-  if (mode != FBM_ENGINE_AUTO && mode != FBM_ENGINE_SINGLE && mode != FBM_ENGINE_QUAD && mode != FBM_ENGINE_TRIPLE) {
-    set_error("fbm_jl_set_engine: mode must be 0 (auto), 1 (one lane per ciphertext), 3 (three lanes) or 4 (four)");
+  if (mode != FBM_ENGINE_AUTO && mode != FBM_ENGINE_SINGLE && mode != FBM_ENGINE_GENERIC && mode != FBM_ENGINE_QUAD &&
+      mode != FBM_ENGINE_TRIPLE) {
+    set_error("fbm_jl_set_engine: mode must be 0 (auto), 1 (one lane per ciphertext), 2 (generic: any modulus), "
+              "3 (three lanes) or 4 (four)");
     return FBM_E_ARG;
   }
   return jl_engine_set(mode);
@@ -790,6 +921,31 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
     set_error("negative weight %lld outside (-2^17, 0)", (long long)(int64_t)weight);
     return FBM_E_ARG;
   }
+  if (jl_generic(biprime)) {  // any N (fbm_gen.hip): pack -> FDH -> H^key (N pt + 1) mod N^2
+    if (es < 1 || es > 100 || (int64_t)es * cr > 1024) {
+      set_error("invalid VES parameters es=%d cr=%d", es, cr);
+      return FBM_E_ARG;
+    }
+    GenCtx g;
+    JlParams fp;
+    if ((rc = build_gen_ctx(biprime, key, key_negative, g)) || (rc = fdh_params_for_biprime(biprime, tau, ct_offset, fp)))
+      return rc;
+    uint8_t* ws = (uint8_t*)workspace;  // the encrypt workspace's cst | pt | (nude) | H
+    uint32_t* cst = (uint32_t*)(ws + align256(FBM_MAX_OPS * 4));
+    uint32_t* pt = (uint32_t*)(ws + align256(FBM_MAX_OPS * 4) + align256(FBM_CST_WORDS * 4));
+    uint32_t* H = (uint32_t*)((uint8_t*)pt + align256(n_ct * 32 * 4) + align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4));
+    const uint32_t* ptp = x_dtype == FBM_PT ? (const uint32_t*)x : pt;
+    if (phase & 1) {
+      if ((rc = launch_jl_gen_setup(g, cst, s))) return rc;
+      if (x_dtype != FBM_PT &&
+          (rc = timed("jl_pack", s, [&] { return launch_jl_pack(x, x_dtype, n, qp, weight, es, cr, n_ct, pt, stats, s); })))
+        return rc;
+      if ((rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, fp, H, stats, s); }))) return rc;
+    }
+    if (!(phase & 2)) return FBM_OK;
+    const int negw = (int64_t)weight < 0 ? 1 : 0;
+    return timed("jl_gen_exp", s, [&] { return launch_jl_gen_exp(H, ptp, negw, n_ct, cst, ct_out, stats, s); });
+  }
   JlParams jp;
   if ((rc = build_jl_params(biprime, es, cr, tau, ct_offset, jp))) return rc;
   JlSched sc;
@@ -906,6 +1062,18 @@ static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t
                           int phase = 7) {
   JlParams jp;
   int rc;
+  if (jl_generic(biprime)) {  // any N: FDH, then H^key mod N^2 with the inverse in the same kernel
+    GenCtx g;
+    if ((rc = build_gen_ctx(biprime, key, key_negative, g)) || (rc = fdh_params_for_biprime(biprime, tau, ct_offset, jp)))
+      return rc;
+    if (phase & 1) {
+      if ((rc = launch_jl_gen_setup(g, w.cst, s))) return rc;
+      if ((rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, w.H, stats, s); }))) return rc;
+    }
+    if (phase & 2)
+      return timed("jl_gen_exp", s, [&] { return launch_jl_gen_exp(w.H, nullptr, 0, n_ct, w.cst, factor, stats, s); });
+    return FBM_OK;
+  }
   if ((rc = build_jl_params(biprime, 1, 1, tau, ct_offset, jp))) return rc;
   JlSched sc;
   int is_zero = 0;
@@ -950,6 +1118,23 @@ static int jl_combine_impl(const uint32_t* cts, int n_parties, uint64_t n_ct, in
                            uint32_t* x_raw = nullptr) {
   JlParams jp;
   int rc;
+  if (jl_generic(biprime)) {  // any N: product, factor, ((v - 1) // N) mod N, then the decode
+    if (es < 1 || cr < 1 || es > 100 || (int64_t)es * cr > 1024) {
+      set_error("invalid VES parameters es=%d cr=%d", es, cr);
+      return FBM_E_ARG;
+    }
+    GenCtx g;
+    if ((rc = build_gen_ctx(biprime, nullptr, 0, g)) || (rc = launch_jl_gen_setup(g, w.cst, s))) return rc;
+    uint32_t* xs = x_raw ? x_raw : w.xs;
+    if ((rc = timed("jl_gen_combine", s, [&] {
+           return launch_jl_gen_combine(cts, n_parties, n_ct, factor, w.cst, FBM_GEN_DECRYPT, xs, stats, s);
+         })))
+      return rc;
+    if (x_raw) return FBM_OK;
+    return timed("jl_decode", s, [&] {
+      return launch_jl_decode(w.xs, es, cr, n_out, total_weight, neg_clip, step, out, sums, stats, s);
+    });
+  }
   if ((rc = build_jl_params(biprime, es, cr, 0, 0, jp))) return rc;
   JlSched none;
   memset(&none, 0, sizeof(none));
@@ -1104,8 +1289,7 @@ int fbm_jl_fdh(uint64_t n_ct, const uint32_t* modulus_odd, int modulus_even, uin
     return FBM_E_ARG;
   }
   JlParams jp;
-  if ((rc = build_jl_params(modulus_odd, 1, 1, tau, ct_offset, jp))) return rc;
-  jp.fdh_even = modulus_even ? 1 : 0;
+  if ((rc = fdh_params(modulus_odd, modulus_even, tau, ct_offset, jp))) return rc;
   if (n_ct == 0) return FBM_OK;
   if (!h) {
     set_error("null pointer argument");
@@ -1125,6 +1309,13 @@ int fbm_jl_product(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint
     return FBM_E_ARG;
   }
   const JlAggWs w = agg_ws(workspace, n_ct);
+  if (jl_generic(biprime)) {
+    GenCtx g;
+    if ((rc = build_gen_ctx(biprime, nullptr, 0, g)) || (rc = launch_jl_gen_setup(g, w.cst, s))) return rc;
+    return timed("jl_gen_combine", s, [&] {
+      return launch_jl_gen_combine(cts, n_parties, n_ct, nullptr, w.cst, FBM_GEN_PRODUCT, out, nullptr, s);
+    });
+  }
   JlParams jp;
   if ((rc = build_jl_params(biprime, 1, 1, 0, 0, jp))) return rc;
   JlSched none;
@@ -1194,6 +1385,32 @@ int fbm_test_fdh_gcd(const uint32_t* r8, const uint32_t* n32, uint32_t* err) {
     return FBM_E_ARG;
   }
   return host_gcd_is_one_r8(r8, n32, err);
+}
+
+int fbm_test_gen_exp(const uint32_t* h, const uint32_t* pt, int negative, const uint32_t* biprime, const uint32_t* key,
+                     int key_negative, uint32_t* out, uint32_t* err) {
+  if (!h || !biprime || !key || !out || !err) {
+    set_error("fbm_test_gen_exp: null pointer");
+    return FBM_E_ARG;
+  }
+  GenCtx g;
+  const int rc = build_gen_ctx(biprime, key, key_negative, g);
+  if (rc) return rc;
+  *err = host_gen_exp(h, pt, negative, g, out);
+  return FBM_OK;
+}
+
+int fbm_test_gen_combine(const uint32_t* cts, int n_parties, const uint32_t* factor, const uint32_t* biprime,
+                         int mode, uint32_t* out, uint32_t* err) {
+  if (!cts || n_parties < 1 || !biprime || !out || !err || (mode != FBM_GEN_PRODUCT && mode != FBM_GEN_DECRYPT)) {
+    set_error("fbm_test_gen_combine: bad arguments");
+    return FBM_E_ARG;
+  }
+  GenCtx g;
+  const int rc = build_gen_ctx(biprime, nullptr, 0, g);
+  if (rc) return rc;
+  *err = host_gen_combine(cts, n_parties, factor, g, mode, out);
+  return FBM_OK;
 }
 
 int fbm_test_nadic_consts(const uint32_t* n32, uint32_t* nk, uint32_t* r2na, uint32_t* r3na, uint32_t* np) {

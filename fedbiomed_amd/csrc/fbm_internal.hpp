@@ -191,6 +191,38 @@ int launch_jl_inv(uint64_t n_ct, const JlParams& jp, const uint32_t* cst, const 
 int launch_jl_decode(const uint32_t* xs, int es, int cr, uint64_t n_out, uint64_t total_weight, double neg_c,
                      double step, double* out, uint64_t* sums, uint32_t* stats, hipStream_t s);
 
+// ---- the generic JL engine (fbm_gen.hip): any biprime N, even ones included ------------
+// Constants of one (N, key), host-built (fbm_capi.hip build_gen_ctx), copied into the call's
+// constants block by jl_gen_setup_kernel.  32-bit limbs, little-endian; M = N^2 = 2^e m2 with
+// m2 odd; muX = floor(2^(64 kX) / X) (Barrett: kX + 1 words, or kX + 2 when X = 2^(32(kX-1)),
+// zero-padded); m2inv = m2^-1 mod 2^e.
+struct GenCtx {
+  int kM, kN, km2, e;  // words of M, N, m2; e = 2 * (trailing zero bits of N)
+  int key_bits, key_negative, pad0, pad1;
+  uint32_t M[64];
+  uint32_t muM[68];
+  uint32_t N[32];
+  uint32_t muN[36];
+  uint32_t m2[64];
+  uint32_t m2inv[64];
+  uint32_t key[64];  // |key|
+};
+#define FBM_GEN_ENC 1       // jl_gen_exp: times (N pt + 1) mod N^2 (an encrypt)
+#define FBM_GEN_PRODUCT 0   // jl_gen_combine: out = prod mod N^2 [ct][64]
+#define FBM_GEN_DECRYPT 1   // jl_gen_combine: out = ((v - 1) // N) mod N [ct][32]
+int launch_jl_gen_setup(const GenCtx& g, uint32_t* cst, hipStream_t s);
+// out = H^key mod N^2 (the inverse of H^|key| for a negative key), times (N pt + 1) mod N^2
+// when pt != NULL (pt [ct][32]: |pt| and the sign `negative` of a negative-weight packing)
+int launch_jl_gen_exp(const uint32_t* H, const uint32_t* pt, int negative, uint64_t n_ct, const uint32_t* cst,
+                      uint32_t* out, uint32_t* stats, hipStream_t s);
+// v = prod_u cts[u] (* factor) mod N^2 -> out (FBM_GEN_PRODUCT) or ((v - 1) // N) mod N (FBM_GEN_DECRYPT)
+int launch_jl_gen_combine(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* factor,
+                          const uint32_t* cst, int mode, uint32_t* out, uint32_t* stats, hipStream_t s);
+// the same per-ciphertext work on the host, one ciphertext (test hooks; cts: n_parties rows of 64)
+uint32_t host_gen_exp(const uint32_t* Hrow, const uint32_t* ptrow, int negative, const GenCtx& g, uint32_t* out);
+uint32_t host_gen_combine(const uint32_t* cts, int n_parties, const uint32_t* frow, const GenCtx& g, int mode,
+                          uint32_t* out);
+
 int launch_ass_split(const uint64_t* secret, uint64_t n, const uint32_t* key, uint32_t n14, uint32_t n15,
                      uint64_t elem_offset, int n_shares, int bit_length, int is_signed, int64_t* shares,
                      hipStream_t s);
@@ -206,6 +238,7 @@ uint64_t jl_table_slots();
 // exponentiation engine policy (fbm_jl_set_engine) and the table bytes both engines fit in
 #define FBM_ENGINE_AUTO 0
 #define FBM_ENGINE_SINGLE 1
+#define FBM_ENGINE_GENERIC 2  // every modulus on the generic engine (fbm_gen.hip; odd N: a cross-check)
 #define FBM_ENGINE_TRIPLE 3
 #define FBM_ENGINE_QUAD 4
 int jl_engine_policy();

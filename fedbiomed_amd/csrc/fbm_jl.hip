@@ -1537,6 +1537,7 @@ int jl_engine_policy() {
     if (v && !strcmp(v, "single")) e = FBM_ENGINE_SINGLE;
     if (v && !strcmp(v, "quad")) e = FBM_ENGINE_QUAD;
     if (v && !strcmp(v, "triple")) e = FBM_ENGINE_TRIPLE;
+    if (v && !strcmp(v, "generic")) e = FBM_ENGINE_GENERIC;
     int expect = -1;
     g_engine.compare_exchange_strong(expect, e);
     e = g_engine.load(std::memory_order_relaxed);

@@ -16,7 +16,8 @@ A sum of EncryptedNumbers keeps its operands until its ciphertext is read (then 
 product), so `[sum(ep) for ep in zip(*parties)]` followed by ServerKey.decrypt is one device
 call, as JoyeLibert.aggregate is.
 
-Domain of the device path (FB624 outside it): N odd, 3 <= N < 2^1024; a
+Domain of the device path (FB624 outside it): 2 <= N < 2^1024 (an even N
+runs on the generic engine, fedbiomed_amd/csrc/fbm_gen.hip, an odd one on the Montgomery engines); a
 PublicParam with bits = 1024 whose hashing function is FDH(2048, N^2).H (what
 SecaggCrypter._setup_public_param builds); tau in [0, 2^64); VES values in [0, 2^128) with
 es <= 100; ServerKey.decrypt with delta^2 = 1 (mod N).  Integers are Python ints (gmpy2 is
@@ -130,8 +131,8 @@ def _device_n(pp: PublicParam) -> int:
             and fdh.bits_size == SAParameters.KEY_SIZE and int(fdh._n_modules) == n * n
             and pp.bits == _TAU_SHIFT_BITS):
         raise _unsupported("a PublicParam whose hashing function is not FDH(2048, N^2).H with bits 1024")
-    if n < 3 or n % 2 == 0 or n.bit_length() > 1024:
-        raise _unsupported("a modulus N that is not odd in [3, 2^1024)")
+    if n < 2 or n.bit_length() > 1024:
+        raise _unsupported("a modulus N outside [2, 2^1024)")
     return n
 
 
@@ -230,8 +231,8 @@ def _materialize(nums: List[EncryptedNumber]) -> List[int]:
 
 def _modulus_of(pp: PublicParam) -> int:
     n = int(pp.n_modulus)
-    if n < 3 or n % 2 == 0 or n.bit_length() > 1024:
-        raise _unsupported("a modulus N that is not odd in [3, 2^1024)")
+    if n < 2 or n.bit_length() > 1024:
+        raise _unsupported("a modulus N outside [2, 2^1024)")
     return n
 
 

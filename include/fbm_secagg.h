@@ -103,7 +103,8 @@ int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t tot
                       double step, double* out, uint64_t* sums, uint32_t* stats, void* stream);
 
 /* ---- Joye-Libert (reference fedbiomed/common/secagg/_jls.py) -------------------------
- * biprime: HOST, 32 limbs (N, odd, 3 <= N < 2^1024)
+ * biprime: HOST, 32 limbs (N, 2 <= N < 2^1024; an odd N runs on the Montgomery engines, an
+ *          even one on the generic engine, fedbiomed_amd/csrc/fbm_gen.hip -- same results)
  * key:     HOST, 64 limbs |sk| (< 2^2048);  key_negative: sign of sk
  * es, cr:  VES slot bits / slots per ciphertext (JoyeLibert vector encoder, _jls.py:104-116)
  * tau:     round (< 2^64); n_ct = ceil(n / cr)
@@ -183,7 +184,7 @@ int fbm_jl_aggregate_factor(const uint32_t* cts, int n_parties, uint64_t n_ct, i
  * fbm_jl_unpack: VES.decode (_jls.py:146-192): value o = slot o % cr of plaintext o / cr,
  *   masked to es bits (es <= 128), as (lo, hi) uint64 pairs in vals [n_out x 2] (device).
  * fbm_jl_fdh: FBM's FDH.H (_jls.py:727-762) of t_k = ((k + ct_offset) << 512) | tau, k < n_ct,
- *   bits_size 2048, against a modulus M given as its odd part (32 limbs, odd, >= 3) and whether
+ *   bits_size 2048, against a modulus M given as its odd part (32 limbs, odd, >= 1) and whether
  *   M is even (gcd(r, M) == 1 then also needs r odd); for M = N^2 pass N.  h: n_ct x 64 limbs.
  * fbm_jl_product: EncryptedNumber sums (_jls.py:308-374): out[k] = prod_u cts[u][k] mod N^2,
  *   canonical, n_ct x 64 limbs; workspace fbm_jl_aggregate_workspace(n_ct).
@@ -253,9 +254,11 @@ int fbm_jl_triple_mads(int square);
  * launch's ciphertext count -- lane groups of 4 or 3 below the chip's one-lane round, one lane
  * otherwise; fedbiomed_amd/csrc/fbm_jl.hip engine_model_ms), 1 = one lane per ciphertext
  * (throughput: several concurrent launches that fill the chip together), 3 / 4 = three / four
- * lanes per ciphertext (latency).  Results are bit-identical either way.  Returns the previous
- * policy (or FBM_E_ARG).  FBM_JL_ENGINE=auto|single|triple|quad sets the initial one.
- * fbm_jl_engine_for: the engine a launch of n_ct ciphertexts takes under the policy (1, 3 or 4). */
+ * lanes per ciphertext (latency), 2 = the generic engine for every modulus (fbm_gen.hip: Barrett
+ * products, any N; even N always take it -- under this policy odd N do too, a cross-check of the
+ * Montgomery engines).  Results are bit-identical either way.  Returns the previous policy (or
+ * FBM_E_ARG).  FBM_JL_ENGINE=auto|single|triple|quad|generic sets the initial one.
+ * fbm_jl_engine_for: the engine a launch of n_ct ciphertexts takes under the policy (1-4). */
 int fbm_jl_set_engine(int mode);
 int fbm_jl_engine_for(uint64_t n_ct);
 
@@ -265,7 +268,8 @@ int fbm_jl_engine_for(uint64_t n_ct);
  * with a non-negative key, fbm_jl_decrypt_factor_phase(..., 2) -- record their exponentiation
  * instead of launching it; the flush launches ONE kernel over all of them on `stream` (one chunk
  * counter: the chip's rounds pack whatever the parts' sizes and however streams map onto hardware
- * queues).  Every recorded call must use the same biprime; at most 24 calls; their prologues must
+ * queues).  Calls on the generic engine (an even biprime) are not recorded: they launch at once,
+ * on their own stream.  Every recorded call must use the same biprime; at most 24 calls; their prologues must
  * be complete on `stream` at the flush, and their outputs are valid after it.  Other calls made
  * while a batch is open launch as usual; a factor's inverse (phase 4) is refused until the flush.
  * workspace: fbm_jl_batch_workspace() bytes of device memory.  No reference counterpart: the
@@ -283,6 +287,17 @@ int fbm_test_modinv(const uint32_t* x, const uint32_t* n, uint32_t* out, int* ba
  * r8: 8 words (a 256-bit digest), n32: 32 words (odd N).  Returns 1 if gcd(r, N) == 1, 0 if
  * not, a negative FBM_E_* code on bad arguments; *err receives device error flags. */
 int fbm_test_fdh_gcd(const uint32_t* r8, const uint32_t* n32, uint32_t* err);
+/* host test hooks (no GPU): one ciphertext of the generic engine (fedbiomed_amd/csrc/fbm_gen.hip)
+ * run on the host, any N (2 <= N < 2^1024).  fbm_test_gen_exp: out (64 words) = h^key mod N^2 (the
+ * inverse of h^|key| for key_negative), times (N pt + 1) mod N^2 when pt (32 words; `negative`:
+ * pt holds |pt| of a negative packing) is not NULL; h: 64 words.  fbm_test_gen_combine: v =
+ * prod of n_parties 64-word rows (cts, row-major) times factor (64 words, may be NULL) mod N^2;
+ * mode 0: out = v (64 words), mode 1: out = ((v - 1) // N) mod N (32 words).  *err receives the
+ * device error flags. */
+int fbm_test_gen_exp(const uint32_t* h, const uint32_t* pt, int negative, const uint32_t* biprime, const uint32_t* key,
+                     int key_negative, uint32_t* out, uint32_t* err);
+int fbm_test_gen_combine(const uint32_t* cts, int n_parties, const uint32_t* factor, const uint32_t* biprime,
+                         int mode, uint32_t* out, uint32_t* err);
 /* host test hook (no GPU): the N-adic engine's per-modulus constants as the library builds
  * them -- nk: 80 words (N limbs, K'_i), r2na / r3na: 74 limbs (digits of R^2 / R^3 mod N^2,
  * R = 2^1036), np = -N^-1 mod 2^28. */

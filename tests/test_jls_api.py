@@ -125,7 +125,7 @@ def test_domain_restrictions_raise_fb624():
     with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):  # not the FDH of SecaggCrypter's PublicParam
         UserKey(PublicParam(123457, 1024, lambda t: 5), 3).encrypt([1], 1)
     with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
-        UserKey(pp_of(123456), 3).encrypt([1], 1)  # even N
+        UserKey(pp_of(1), 3).encrypt([1], 1)  # N = 1 (every N >= 2 is in the domain, even ones included)
     with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
         UserKey(pp, 3).encrypt([1], 2**64)  # tau beyond the device's 64 bits
     with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
@@ -139,6 +139,13 @@ def test_domain_restrictions_raise_fb624():
 
 
 # ------------------------------------------------------------------ device parity (GPU)
+@pytest.mark.gpu
+def test_even_modulus_user_encrypt(golden):
+    """An even N (123456) is encrypted as the reference does (the generic engine, csrc/fbm_gen.hip);
+    rounds 2 and earlier refused it with FB624."""
+    assert UserKey(pp_of(123456), 3).encrypt([1], 1) == [I(v) for v in golden["even"]["user_encrypt_123456"]]
+
+
 @pytest.mark.gpu
 def test_fdh_golden(golden):
     for case in golden["jls_api"]["fdh"]:

@@ -525,6 +525,83 @@ def gen_crypter_sweep(R):
     dump("crypter_sweep.json", out)
 
 
+def gen_even(R):
+    """Even (and other non-Montgomery) biprimes, which the reference computes with like any other
+    (gmpy2 powmod / invert and Python ints): the exact inputs of its two caller tests that pass
+    even biprimes -- tests/test_node_secagg.py:207-221 (_JLSRound.encrypt: 3 parties, round 1,
+    [1.0, 1.0], weight 20, key 12345, biprime 1156, clipping range 3) and
+    tests/test_secure_aggregation.py:193-233 (researcher aggregate of [[1..5], [1..5]] and the
+    validation's [[1], [1]], key 1234, biprime 1234, total 100) -- then a seeded sweep of even moduli
+    of 2..1024 bits (powers of two among them) through both crypter calls and the object API
+    (UserKey.encrypt, EncryptedNumber sums, ServerKey.decrypt incl. a wrong key and a zero product)."""
+    jls = R.jls
+    Crypter = R.crypter.SecaggCrypter
+    mpz = sys.modules["gmpy2"].mpz
+    out = {}
+    cr = Crypter()
+    out["node_round"] = {"num_nodes": 3, "round": 1, "params": [fhex(1.0), fhex(1.0)], "key": 12345, "biprime": 1156,
+                         "clip": 3, "weight": 20,
+                         "enc": _outcome(lambda: [ihex(c) for c in cr.encrypt(
+                             num_nodes=3, current_round=1, params=[1.0, 1.0], key=12345, biprime=1156,
+                             clipping_range=3, weight=20)])}
+    res = []
+    for params, n_exp in [([[1, 2, 3, 4, 5], [1, 2, 3, 4, 5]], 5), ([[1], [1]], 1)]:
+        res.append({"params": params, "n_expected": n_exp, "agg": _outcome(lambda params=params, n_exp=n_exp: [
+            fhex(v) for v in cr.aggregate(current_round=1, num_nodes=2, params=params, key=1234, biprime=1234,
+                                          total_sample_size=100, clipping_range=None, num_expected_params=n_exp)])})
+    out["researcher"] = {"key": 1234, "biprime": 1234, "round": 1, "total": 100, "cases": res}
+    rng = random.Random(2024)
+    sweep = []
+    moduli = [1156, 1234, 2, 4, 6, 2 ** 32, 2 ** 64, 2 ** 100, 2 ** 1023, 3 * 2 ** 40]
+    moduli += [rng.getrandbits(b) | (1 << (b - 1)) & ~1 for b in (20, 33, 64, 65, 100, 256, 513, 1000, 1024)]
+    moduli = [m & ~1 if m > 2 else m for m in moduli]
+    for i, n_mod in enumerate(moduli):
+        n_parties = [1, 2, 3][i % 3]
+        keys = [rng.getrandbits(rng.choice([8, 64, 2040])) for _ in range(n_parties)]
+        n = rng.choice([1, 29, 61])
+        tau = rng.choice([0, 1, 7, 2 ** 64 - 1])
+        xs = [[float(v) for v in np.random.default_rng(1000 * i + p).standard_normal(n) * 1.5] for p in range(n_parties)]
+        ws = [rng.choice([None, 1, 37, 2 ** 17 - 1, -3]) for _ in range(n_parties)]
+        enc = [_outcome(lambda x=x, k=k, w=w: [ihex(c) for c in cr.encrypt(
+            num_nodes=n_parties, current_round=tau, params=x, key=k, biprime=n_mod, weight=w)])
+            for x, k, w in zip(xs, keys, ws)]
+        case = {"n": ihex(n_mod), "tau": ihex(tau), "keys": [ihex(k) for k in keys], "weights": ws,
+                "x": [[fhex(v) for v in x] for x in xs], "enc": enc}
+        if all("ok" in e for e in enc):
+            cts = [[int(c, 16) for c in e["ok"]] for e in enc]
+            total = max(1, sum(w if w is not None else 1 for w in ws))
+            for tag, sk0 in (("agg", -sum(keys)), ("agg_badkey", -sum(keys) + 1)):
+                case[tag] = _outcome(lambda sk0=sk0: [fhex(v) for v in cr.aggregate(
+                    current_round=tau, num_nodes=n_parties, params=cts, key=sk0, biprime=n_mod,
+                    total_sample_size=total, num_expected_params=n)])
+            case["total"] = total
+        sweep.append(case)
+    out["crypter"] = sweep
+    obj = []
+    for i, n_mod in enumerate(moduli[:12]):
+        pp = jls.PublicParam(mpz(n_mod), 1024, jls.FDH(2048, mpz(n_mod) * mpz(n_mod)).H)
+        keys = [rng.getrandbits(rng.choice([16, 2040])) for _ in range(2)]
+        keys[1] = -keys[1]  # a negative user key: the inverse of H first (gmpy2 powmod)
+        tau = rng.choice([1, 9])
+        pts = [0, 1, n_mod - 1, n_mod, n_mod + 5, rng.getrandbits(1000), 2 ** 1024 + 3, -5]
+        cts = [[int(c) for c in jls.UserKey(pp, k).encrypt([mpz(v) for v in pts], tau)] for k in keys]
+        encs = [[jls.EncryptedNumber(pp, c) for c in row] for row in cts]
+        summed = [sum(ep) for ep in zip(*encs)]
+        sk = -sum(keys)
+        dec = _outcome(lambda: [ihex(int(v)) for v in jls.ServerKey(pp, sk).decrypt(summed, tau)])
+        bad = _outcome(lambda: [ihex(int(v)) for v in jls.ServerKey(pp, sk + 3).decrypt(summed, tau)])
+        zero = _outcome(lambda: [ihex(int(v)) for v in jls.ServerKey(pp, sk).decrypt(
+            [jls.EncryptedNumber(pp, 0), jls.EncryptedNumber(pp, n_mod * n_mod)], tau)])
+        obj.append({"n": ihex(n_mod), "keys": [ihex(k) for k in keys], "tau": tau, "pt": [ihex(v) for v in pts],
+                    "ct": [[ihex(c) for c in row] for row in cts], "sum": [ihex(int(s.ciphertext)) for s in summed],
+                    "dec": dec, "dec_badkey": bad, "dec_zero": zero})
+    out["object"] = obj
+    # tests/test_jls_api.py's former refusal: UserKey(PublicParam(123456, ...), 3).encrypt([1], 1)
+    pp = jls.PublicParam(mpz(123456), 1024, jls.FDH(2048, mpz(123456) * mpz(123456)).H)
+    out["user_encrypt_123456"] = [ihex(int(c)) for c in jls.UserKey(pp, 3).encrypt([mpz(1)], 1)]
+    dump("even.json", out)
+
+
 def I(s):  # noqa: E743 - hex string -> int (the fixtures' encoding)
     return int(s, 16)
 
@@ -537,6 +614,9 @@ def main():
     if sys.argv[1:] == ["crypter_sweep"]:
         gen_crypter_sweep(R)
         return
+    if sys.argv[1:] == ["even"]:
+        gen_even(R)
+        return
     gen_quantize(R)
     gen_lom(R)
     gen_jl(R)
@@ -545,6 +625,7 @@ def main():
     gen_dh(R)
     gen_jls_api(R)
     gen_crypter_sweep(R)
+    gen_even(R)
     meta = {"generator": "tools/gen_golden.py", "reference": load_reference.REF,
             "note": "outputs of the reference Fed-BioMed crypter (Python), imported via tools/refshim"}
     dump("meta.json", meta)
