@@ -40,6 +40,7 @@ sys.path.insert(0, ROOT)
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+ISA_MAD_TOPS_2400 = 256 * 4 * 16 * 2.4e9 / 1e12  # 39.3 T: quarter-rate v_mad_u64_u32 at 2.4 GHz
 MAD_PEAK_TOPS = 36.48        # measured v_mad_u64_u32 peak, whole chip, best occupancy (tools/microbench/madpeak.hip,
                              # profiles/r1_madpeak.txt: 35.3 T at 2 waves/SIMD, 36.5 T at 4)
 # v_mad_u64_u32 per lane of one N-adic product modulo N^2 (tools/gen_nadic_asm.py: 37 rows x
@@ -84,9 +85,10 @@ def mads_per_exp(key: int, win: int, mads_mul: int, mads_sq: int) -> int:
 
 
 def committed_traffic(kernel: str, scheme: str, elements: int, n_ct=None):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
-    workload -- same scheme and elements per GPU (JL: same ciphertexts per party) --
-    (profiles/*_hbm_traffic.json, written by tools/prof_summary.py), else None."""
+    """(HBM bytes per launch of `kernel`, the profile file) from the committed rocprofv3 PMC summary
+    of this workload -- same scheme and elements per GPU (JL: same ciphertexts per party) --
+    (profiles/*_hbm_traffic.json, written by tools/prof_summary.py), else (None, None).  Not
+    measured in the run: a PMC pass needs its own rocprofv3 process."""
     import glob
 
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic.json")), reverse=True):
@@ -100,8 +102,80 @@ def committed_traffic(kernel: str, scheme: str, elements: int, n_ct=None):
                 and (scheme != "jl" or cfg.get("ciphertexts_per_party_per_gpu") == n_ct)):
             for name, k in d.get("kernels", {}).items():  # exact, or template arguments stripped
                 if name == "fbm::" + kernel or ("<" not in kernel and name.split("<")[0] == "fbm::" + kernel):
-                    return k["hbm_bytes_per_launch"]
-    return None
+                    return k["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+    return None, None
+
+
+class GfxClockSampler:
+    """Samples the GPU's graphics clock (amdsmi, read-only) on a thread while a region runs: the
+    clock the VALU peak is quoted against.  Every failure leaves `mhz` empty (the line says so)."""
+
+    def __init__(self, index: int, period_s: float = 0.02):
+        self.index, self.period, self.mhz, self._stop, self._t, self.error = index, period_s, [], None, None, None
+
+    def __enter__(self):
+        import threading
+
+        try:
+            import amdsmi
+
+            amdsmi.amdsmi_init()
+            handle = amdsmi.amdsmi_get_processor_handles()[self.index]
+            self._stop = threading.Event()
+
+            def run():
+                while not self._stop.is_set():
+                    try:
+                        self.mhz.append(float(amdsmi.amdsmi_get_clock_info(handle, amdsmi.AmdSmiClkType.GFX)["clk"]))
+                    except Exception as e:  # noqa: BLE001
+                        self.error = repr(e)
+                        return
+                    self._stop.wait(self.period)
+
+            self._t = threading.Thread(target=run, daemon=True)
+            self._t.start()
+        except Exception as e:  # noqa: BLE001
+            self.error = repr(e)
+        return self
+
+    def __exit__(self, *exc):
+        if self._t is not None:
+            self._stop.set()
+            self._t.join(timeout=5)
+        try:
+            import amdsmi
+
+            amdsmi.amdsmi_shut_down()
+        except Exception:  # noqa: BLE001
+            pass
+        return False
+
+    def summary(self):
+        if not self.mhz:
+            return {"samples": 0, "error": self.error}
+        v = sorted(self.mhz)
+        return {"samples": len(v), "median_mhz": v[len(v) // 2], "min_mhz": v[0], "max_mhz": v[-1]}
+
+
+def quiet_clipping_warnings():
+    """bench.py only: the product logs the reference's clipping warning on every encrypt that clips
+    (_secagg_utils.py:189-204); the synthetic inputs clip on purpose, so after the first one the
+    bench drops the repeats, keeping the driver's stderr tail readable.  Other records pass."""
+    import logging
+
+    class Once(logging.Filter):
+        seen = False
+
+        def filter(self, rec):
+            if "exceeds clipping range" not in rec.getMessage():
+                return True
+            if Once.seen:
+                return False
+            Once.seen = True
+            rec.msg = str(rec.msg) + " (bench.py: further clipping warnings of this process suppressed)"
+            return True
+
+    logging.getLogger("fedbiomed_amd").addFilter(Once())
 
 
 def parse():
@@ -133,6 +207,11 @@ def parse():
                          "one batched launch over all of them (D.jl_exp_batch)")
     ap.add_argument("--serial", action="store_true",
                     help="no per-party streams in the timed steps (rocprof passes: per-kernel times unconfounded)")
+    ap.add_argument("--rccl-world1", action="store_true",
+                    help="at --gpus 1: form a world-1 RCCL process group, so the step ends with the strong-scaling "
+                         "gather over RCCL (all_gather_shards) as every rank of an N-GPU run does")
+    ap.add_argument("--node-list-n", type=int, nargs="*", default=[1_000_000, 10_000_000],
+                    help="elements of the per-node list-API encrypt legs (one party's SecaggCrypter.encrypt)")
     return ap.parse_args()
 
 
@@ -175,12 +254,21 @@ def main():
     from fedbiomed_amd import _device as D, _native, distributed, workload as W
     from fedbiomed_amd.secagg import SecaggCrypter, SecaggLomCrypter
 
+    quiet_clipping_warnings()
     rank, world, local = distributed.env_rank()
     # more ranks than visible GPUs only happens in a rehearsal (--dist-backend gloo on a
     # one-GPU box): ranks then share devices round-robin
     local = local % max(1, torch.cuda.device_count())
     if world > 1:
         distributed.init(args.dist_backend, device=local)
+    elif args.rccl_world1:  # one rank, an RCCL group all the same: the gather leg runs over RCCL
+        import socket
+
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     P, tau = args.parties, 1
@@ -217,7 +305,7 @@ def main():
 
     # strong scaling over N > 1 ranks: the step ends with the element-range split's final gather
     # (SURVEY 8(e)), so every rank -- the researcher -- holds the whole averaged vector
-    gather = strong and world > 1
+    gather = strong and (world > 1 or args.rccl_world1)
     factor_stream = torch.cuda.Stream(device=dev)
     overlap_factor = not args.no_factor_overlap
     batch_exp = not args.no_batch_exp and not args.no_prologue_first
@@ -354,14 +442,19 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     # one extra serialised step for the per-kernel durations (not part of `value`)
     prof_steps = 1
-    _, kprof = timed(step, prof_steps, 0, prof=True)
+    with GfxClockSampler(local) as clk_s:
+        _, kprof = timed(step, prof_steps, 0, prof=True)
+    clk = clk_s.summary()
 
     # ---- roofline of the dominant kernel, from the live per-kernel HIP events ----
     n_ct = (n + cr - 1) // cr
     if args.scheme == "jl":
         cnt, ms = kprof.get("jl_exp", (0, 0.0))
-        # algorithmic bytes: encrypt/party 4N + 256*#ct, aggregate 256*P*#ct + 8N
-        alg_bytes = prof_steps * (P * (4 * n + 256 * n_ct) + (256 * P * n_ct + 8 * n))
+        # algorithmic bytes of the launch(es) timed: the P parties' encrypts (4N +
+        # 256*#ct each) and the decryption factor's output (256*#ct) -- the exponentiation launch
+        # carries every party's and the factor's ciphertexts; the aggregate's own bytes belong to
+        # the combine kernel, not to this launch
+        alg_bytes = prof_steps * (P * (4 * n + 256 * n_ct) + 256 * n_ct)
         win = _native.load().fbm_jl_window()
         mm = sum(sum(products_per_exp(k, win)) for k in keys) + sum(products_per_exp(sk0, win))
         mads_mul, mads_sq = _native.load().fbm_jl_mads(0), _native.load().fbm_jl_mads(1)
@@ -377,9 +470,14 @@ def main():
         mads, kname = 0, "lom_aggregate_kernel"
     sec = ms / 1000.0 if ms > 0 else float("nan")
     achieved = alg_bytes / sec / 1e9 if ms > 0 else None
+    traffic, traffic_src = committed_traffic(kname, args.scheme, n, n_ct)
     roof = {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-            "traffic": committed_traffic(kname, args.scheme, n, n_ct),
+            "algorithmic_bytes_per_launch": alg_bytes / cnt if cnt else None,
+            "traffic": traffic,
+            "traffic_source": (f"{traffic_src}: rocprofv3 PMC pass of this workload (2*FETCH_SIZE + WRITE_SIZE per "
+                               "launch, committed; a PMC pass needs its own profiler process, so it is looked up, "
+                               "not measured in this run)") if traffic_src else None,
             "avg_launch_ms": (ms / cnt) if cnt else None, "launches": cnt}
     if args.scheme == "jl":
         roof["note"] = ("jl_exp_kernel moves ~1e-4 of the HBM roofline's bytes by construction: it is bound by "
@@ -403,6 +501,17 @@ def main():
         ach = mads / sec / 1e12
         line["roofline_valu"] = {"bound": "int-valu (v_mad_u64_u32)", "achieved": ach, "peak": MAD_PEAK_TOPS,
                                  "unit": "T lane-mad/s", "frac": ach / MAD_PEAK_TOPS,
+                                 "peak_provenance": {
+                                     "measured_T": MAD_PEAK_TOPS,
+                                     "measured_note": "tools/microbench/madpeak.hip, profiles/r1_madpeak.txt: best "
+                                                      "occupancy (4 waves/SIMD) ran at 1.78 GHz -- power-limited",
+                                     "isa_quarter_rate_T_at_2400MHz": ISA_MAD_TOPS_2400,
+                                     "frac_of_isa_2400": ach / ISA_MAD_TOPS_2400,
+                                     "isa_note": "256 CU x 4 SIMD x 16 lanes x 2.4 GHz (v_mad_u64_u32 at a quarter of "
+                                                 "the 64-lane issue rate)",
+                                     "gfx_clock_during_launch": clk,
+                                     "isa_T_at_observed_clock": (ISA_MAD_TOPS_2400 * clk["median_mhz"] / 2400.0
+                                                                 if clk.get("median_mhz") else None)},
                                  "products_per_ct_step": mm, "window": win,
                                  "step_achieved": mads_step / (ms_per_step / 1000) / 1e12,
                                  "step_frac": mads_step / (ms_per_step / 1000) / 1e12 / MAD_PEAK_TOPS,
@@ -487,17 +596,19 @@ def main():
             line["stages"]["T_gather_ms"] = 1000 * t_stage(
                 lambda: distributed.all_gather_shards(stripe, n_total, align))
         if args.scheme == "jl" and world == 1:
-            # strong-scaling probe of the aggregate step on this GPU: T_agg of the stripe rank 0
-            # of an 8-GPU split owns (the first ceil(n/8/cr) ciphertexts: ciphertext k depends
-            # only on its global index) against T_agg of the whole vector
-            hi8 = distributed.shard_range(n, 8, 0, cr)[1]
-            k8 = (hi8 + cr - 1) // cr
-            t8 = t_stage(lambda: agg_alone(k8, hi8))
-            line["stages"]["agg_scaling_probe"] = {
-                "stripe_elements": hi8, "stripe_ciphertexts": k8, "T_agg_stripe_ms": 1000 * t8,
-                "ratio_whole_over_stripe": t_agg / t8,
-                "note": "T_agg(whole vector) / T_agg(1/8 stripe) on one GPU: the aggregate step's 8-GPU "
-                        "strong-scaling bound (north star: >= 6x)"}
+            # strong-scaling probe of the aggregate step on this GPU: T_agg of the stripe rank 0 of a
+            # 2-, 4- and 8-GPU split owns (its first ciphertexts: ciphertext k depends only on its
+            # global index, and rank 0's stripe is the largest) against T_agg of the whole vector
+            probe = {}
+            for g in (2, 4, 8):
+                hig = distributed.shard_range(n, g, 0, cr)[1]
+                kg = (hig + cr - 1) // cr
+                tg = t_stage(lambda kg=kg, hig=hig: agg_alone(kg, hig))
+                probe[f"n{g}"] = {"stripe_elements": hig, "stripe_ciphertexts": kg, "T_agg_stripe_ms": 1000 * tg,
+                                  "engine": D.jl_engine_for(kg), "ratio_whole_over_stripe": t_agg / tg}
+            line["stages"]["agg_scaling_probe"] = dict(probe["n8"], curve=probe, note=(
+                "T_agg(whole vector) / T_agg(rank 0's stripe of an N-GPU split) on one GPU, N = 2 / 4 / 8: the "
+                "aggregate step's strong-scaling bound (north star: >= 6x at N = 8); top-level fields = N = 8"))
         if args.scheme == "jl":
             del cts_all
 
@@ -655,6 +766,50 @@ def main():
         cl = [jc.encrypt(P, tau, xl[p], keys[p], W.BIPRIME0, weight=weights[p]) for p in range(P)]
         jc.aggregate(tau, P, cl, sk0, W.BIPRIME0, total_w, num_expected_params=nl)
         tl = time.perf_counter() - t0
+
+        # (b2) the per-node numbers a deployment sees: ONE party's SecaggCrypter.encrypt(List[float])
+        #      -- the node's call (node/secagg/_secagg_round.py:142-157) -- at 1M and 10M elements, and
+        #      the researcher's aggregate(List[List[int]]) of the P parties' lists at nl elements
+        #      (researcher/secagg/_secure_aggregation.py:644-655), wall time split into the host
+        #      conversions and the GPU
+        def node_encrypt(ne):
+            xl0 = xs_h[0][:ne].tolist()
+            jc.encrypt(P, tau, xl0[:cr * 64], keys[0], W.BIPRIME0, weight=weights[0])  # warm the staging
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            jc.encrypt(P, tau, xl0, keys[0], W.BIPRIME0, weight=weights[0])
+            t_tot = time.perf_counter() - t0
+            # the same call in its parts: list -> pinned f64 -> device | encrypt kernels | D2H -> ints
+            t0 = time.perf_counter()
+            x_d = D.floats_to_host(xl0).to(dev)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            ct_d = jc.encrypt_tensor(P, tau, x_d, keys[0], W.BIPRIME0, weight=weights[0])
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            D.limbs_to_ints(D.to_host(ct_d).numpy().view(np.uint32))
+            t3 = time.perf_counter()
+            return {"elements": ne, "ciphertexts": (ne + cr - 1) // cr, "ms": 1000 * t_tot, "params_per_s": ne / t_tot,
+                    "host_in_ms": 1000 * (t1 - t0), "gpu_ms": 1000 * (t2 - t1), "host_out_ms": 1000 * (t3 - t2),
+                    "engine": D.jl_engine_for((ne + cr - 1) // cr)}
+
+        node_legs = {str(ne): node_encrypt(ne) for ne in args.node_list_n if ne <= n}
+        n2 = W.BIPRIME0 * W.BIPRIME0
+        nct_l = len(cl[0])
+        t0 = time.perf_counter()
+        staged = D.host_empty((P, nct_l, 64), torch.int32)
+        limbs = staged.numpy().view(np.uint32)
+        for u in range(P):
+            D.ints_to_limbs(cl[u], n2, out=limbs[u])
+        cts_l = staged.to(dev)
+        torch.cuda.synchronize()
+        t_conv = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        D.to_host(jc.aggregate_tensor(tau, cts_l, sk0, W.BIPRIME0, total_w, num_expected_params=nl)).numpy().tolist()
+        t_gpu = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        jc.aggregate(tau, P, cl, sk0, W.BIPRIME0, total_w, num_expected_params=nl)
+        t_agg_l = time.perf_counter() - t0
         # (c) over the wire: the same updates through a msgpack Serializer configured as the
         #     reference's (strict_types, one {"__type__": "int"} map per big int) vs the
         #     EncryptedParams hook (one bin per update), encrypt -> dumps -> loads -> aggregate
@@ -711,7 +866,17 @@ def main():
                                                            "stream, then H2D + combine + D2H"},
             "list_api": {"value": nl / tl, "unit": "params/s", "ms_per_step": 1000 * tl, "elements": nl,
                          "note": "SecaggCrypter.encrypt (List[float] -> List[int]) x P + aggregate "
-                                 "(List[List[int]] -> List[float])"}}
+                                 "(List[List[int]] -> List[float]), the P parties issued one after another in "
+                                 "one process (a simulation artefact: each node encrypts on its own GPU)"},
+            "node_encrypt_list_api": dict(node_legs, note=(
+                "one party's SecaggCrypter.encrypt(List[float]) -> List[int] (the node's call); host_in = list -> "
+                "pinned float64 -> H2D, gpu = the encrypt kernels, host_out = D2H + limbs -> Python ints")),
+            "researcher_aggregate_list_api": {
+                "elements": nl, "parties": P, "ms": 1000 * t_agg_l, "params_per_s": nl / t_agg_l,
+                "host_conversion_ms": 1000 * t_conv, "gpu_ms": 1000 * t_gpu,
+                "note": "SecaggCrypter.aggregate(List[List[int]]) of the P parties' ciphertext lists; host_conversion "
+                        "= ints -> pinned limbs -> H2D alone, gpu = aggregate_tensor + D2H + float list alone; the "
+                        "call itself issues the decryption factor before converting, so ms < the sum"}}
 
         # (d) LOM from and to host memory: pinned float32 -> H2D -> protect -> D2H u64 rows (one
         #     stream per party), then H2D of the rows -> aggregate -> D2H float64; and the
@@ -783,9 +948,11 @@ def main():
                     "note": f"the reference crypter itself ran {r:.3f}x the oracle's time on this sample in the "
                             "build container (profiles/cpu_calibration.json); it cannot run on the GPU box"}
         line["gpu_over_cpu"] = value / (ns / tc)
+    if args.rccl_world1:
+        line["config"]["gather"] = "all_gather_shards over a world-1 RCCL group (--rccl-world1)"
     if rank == 0:
         print(json.dumps(line))
-    if world > 1:
+    if world > 1 or args.rccl_world1:
         torch.distributed.destroy_process_group()
 
 

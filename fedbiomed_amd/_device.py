@@ -544,7 +544,9 @@ class jl_exp_batch:
     party's ciphertexts, so the chip's rounds pack whatever the parts' sizes and however the
     streams map onto the hardware queues.  The recorded calls' prologues must be complete on the
     current stream at exit (wait on their streams first) and their outputs are valid after it;
-    the same biprime throughout; at most 24 calls.  A factor's inverse (PendingFactor.finish)
+    the same biprime throughout; at most 24 calls.  If the block raises, the batch is dropped: the
+    recorded exponentiations never run, and finish() on any of their Pending objects raises
+    instead of returning unwritten memory.  A factor's inverse (PendingFactor.finish)
     goes after the context.  An even biprime's calls (the generic engine) are not recorded: they
     launch when issued, on the current stream.
 
@@ -557,7 +559,7 @@ class jl_exp_batch:
     _tls = threading.local()
 
     def __init__(self, dev=None):
-        self._dev, self._keep = dev, []
+        self._dev, self._keep, self._recorded = dev, [], []
 
     @staticmethod
     def active() -> Optional["jl_exp_batch"]:
@@ -567,6 +569,10 @@ class jl_exp_batch:
         """device tensors a recorded call reads or writes (kept alive until the launch, then
         marked as used on the launch stream for the caching allocator)"""
         self._keep += [t for t in tensors if isinstance(t, torch.Tensor) and t.is_cuda]
+
+    def record(self, pending) -> None:
+        """a Pending object whose exponentiation this batch recorded (invalidated on abort)"""
+        self._recorded.append(pending)
 
     def __enter__(self):
         if jl_exp_batch.active() is not None:
@@ -580,6 +586,9 @@ class jl_exp_batch:
         lib = N.load()
         if exc_type is not None:
             lib.fbm_jl_batch_abort()
+            for p in self._recorded:  # their exponentiations never ran
+                p._aborted = True
+            self._recorded, self._keep = [], []
             return False
         ws = torch.empty(int(lib.fbm_jl_batch_workspace()), dtype=torch.uint8, device=self._dev or device())
         _call(lib.fbm_jl_batch_flush, _ptr(ws), ws.numel(), _stream())
@@ -597,27 +606,40 @@ class PendingEncrypt:
     the workspace and the status word until then."""
 
     def __init__(self, args, ct, ws, st):
-        self._args, self._ct, self._ws, self._st = args, ct, ws, st
+        self._args, self._ct, self._ws, self._st, self._aborted = args, ct, ws, st, False
 
     def finish(self) -> torch.Tensor:
+        if self._aborted:
+            raise RuntimeError("this encrypt's exponentiation was recorded in a jl_exp_batch that was aborted: "
+                               "its ciphertexts were never computed")
         if self._args is not None:
-            _call(N.load().fbm_jl_encrypt_phase, *self._args, _stream(), 2)
+            lib = N.load()
+            n0 = lib.fbm_jl_batch_count()
+            _call(lib.fbm_jl_encrypt_phase, *self._args, _stream(), 2)
             b = jl_exp_batch.active()
             if b is not None:
                 b.keep([self._ct, *self._ws])
+                if lib.fbm_jl_batch_count() > n0:
+                    b.record(self)
             _check_stats_or_defer(self._st)
             self._args = None
         return self._ct
 
 
-def _check_round(tau: int) -> None:
-    """The JL round's domain: FDH.H serialises t = (k << 512) | tau (_jls.py:742-760), so a negative
-    round is the reference's OverflowError; rounds of 2^64 and above are valid there (up to 2^512)
-    but outside the device path's 64-bit round (FB624)."""
+JL_ROUND_BITS = 512  # t_k = (k << 512) | tau: a round below 2^512 keeps to FDH's last message block
+
+
+def _check_round(tau: int) -> np.ndarray:
+    """The JL round's domain -> its 16 limbs for the C-ABI.  FDH.H serialises t = (k << 512) | tau
+    (_jls.py:742-760), so a negative round is the reference's OverflowError; a round of 2^512 or more
+    ORs into k's bits there (valid up to 2^8192) and is outside the device path (FB624, DESIGN.md
+    section 8)."""
+    tau = operator.index(tau)
     if tau < 0:
         raise OverflowError("can't convert negative int to unsigned")
-    if tau > U64_MAX:
-        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: round must be in [0, 2^64)")
+    if tau >> JL_ROUND_BITS:
+        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: round must be in [0, 2^512)")
+    return int_limbs(tau, 16)
 
 
 def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, clip=None, target=None,
@@ -635,7 +657,7 @@ def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, 
     es, cr = slot if slot else jl_slot(target, n_users)
     raw = kind is not None or x.dtype == torch.int64
     c, c2, tf, tm1 = (1.0, 2.0, 1.0, 0) if raw else quant_params(clip, target)
-    _check_round(tau)
+    tl = _check_round(tau)
     x = x.contiguous()
     if kind == "u128":
         xdt, n = N.FBM_U128, x.shape[0]
@@ -659,16 +681,16 @@ def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, 
                 f"{ErrorNumbers.FB624.value}: a deferred encrypt takes at most {chunk} ciphertexts")
         st = _stats(dev)
         args = (_ptr(x), xdt, n, c, c2, tf, tm1, int(weight) & U64_MAX, es, cr, _np_ptr(bp), _np_ptr(kl), kneg,
-                int(tau), int(ct_offset), _ptr(ct), _ptr(ws), _ptr(st))
+                _np_ptr(tl), int(ct_offset), _ptr(ct), _ptr(ws), _ptr(st))
         _call(lib.fbm_jl_encrypt_phase, *args, _stream(), 1)
-        return PendingEncrypt(args, ct, (ws, x, bp, kl), st)
+        return PendingEncrypt(args, ct, (ws, x, bp, kl, tl), st)
     for k0 in range(0, n_ct, chunk):
         k1 = min(n_ct, k0 + chunk)
         xs = x[k0 * cr:min(n, k1 * cr)]
         st = _stats(dev)  # one status word per call (each call zeroes its own)
         _call(lib.fbm_jl_encrypt, _ptr(xs), xdt, xs.shape[0] if kind else xs.numel(), c, c2, tf, tm1,
               int(weight) & U64_MAX, es, cr,
-              _np_ptr(bp), _np_ptr(kl), kneg, int(tau), int(ct_offset) + k0, _ptr(ct[k0:k1]), _ptr(ws), _ptr(st),
+              _np_ptr(bp), _np_ptr(kl), kneg, _np_ptr(tl), int(ct_offset) + k0, _ptr(ct[k0:k1]), _ptr(ws), _ptr(st),
               _stream())
         _check_stats_or_defer(st)
     return ct
@@ -680,15 +702,22 @@ class PendingFactor:
     rest on the current stream; finish() returns the factor tensor."""
 
     def __init__(self, args, f, keep, st):
-        self._args, self._f, self._keep, self._st, self._done = args, f, keep, st, 1
+        self._args, self._f, self._keep, self._st, self._done, self._aborted = args, f, keep, st, 1, False
 
     def _phase(self, bit):
+        if self._aborted:
+            raise RuntimeError("this decryption factor's exponentiation was recorded in a jl_exp_batch that was "
+                               "aborted: the factor was never computed")
         if not self._done & bit:
-            _call(N.load().fbm_jl_decrypt_factor_phase, *self._args, _stream(), bit)
+            lib = N.load()
+            n0 = lib.fbm_jl_batch_count()
+            _call(lib.fbm_jl_decrypt_factor_phase, *self._args, _stream(), bit)
             self._done |= bit
             b = jl_exp_batch.active()
             if b is not None:
                 b.keep([self._f, *self._keep])
+                if lib.fbm_jl_batch_count() > n0:
+                    b.record(self)
 
     def exponentiate(self) -> "PendingFactor":
         self._phase(2)
@@ -709,7 +738,7 @@ def jl_decrypt_factor(n_ct: int, biprime: int, key: int, tau: int, ct_offset: in
     phased: issue only the first phase (constants + FDH) and return a PendingFactor."""
     dev = dev or device()
     lib = N.load()
-    _check_round(tau)
+    tl = _check_round(tau)
     f = torch.empty((n_ct, 64), dtype=torch.int32, device=dev)
     if n_ct == 0:
         return f
@@ -722,13 +751,13 @@ def jl_decrypt_factor(n_ct: int, biprime: int, key: int, tau: int, ct_offset: in
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value}: a phased decryption factor takes at most {chunk} ciphertexts")
         st = _stats(dev)
-        args = (n_ct, _np_ptr(bp), _np_ptr(kl), kneg, int(tau), int(ct_offset), _ptr(f), _ptr(ws), _ptr(st))
+        args = (n_ct, _np_ptr(bp), _np_ptr(kl), kneg, _np_ptr(tl), int(ct_offset), _ptr(f), _ptr(ws), _ptr(st))
         _call(lib.fbm_jl_decrypt_factor_phase, *args, _stream(), 1)
-        return PendingFactor(args, f, (ws, bp, kl), st)
+        return PendingFactor(args, f, (ws, bp, kl, tl), st)
     for k0 in range(0, n_ct, chunk):
         k1 = min(n_ct, k0 + chunk)
         st = _stats(dev)
-        _call(lib.fbm_jl_decrypt_factor, k1 - k0, _np_ptr(bp), _np_ptr(kl), kneg, int(tau), int(ct_offset) + k0,
+        _call(lib.fbm_jl_decrypt_factor, k1 - k0, _np_ptr(bp), _np_ptr(kl), kneg, _np_ptr(tl), int(ct_offset) + k0,
               _ptr(f[k0:k1]), _ptr(ws), _ptr(st), _stream())
         _check_stats_or_defer(st)
     return f
@@ -751,7 +780,7 @@ def jl_aggregate(cts: torch.Tensor, biprime: int, key: int, tau: int, n_expected
     if total_weight < 0 or total_weight > U64_MAX:
         raise FedbiomedSecaggCrypterError(
             f"{ErrorNumbers.FB624.value}: total_sample_size must be in [1, 2^64) for the device path")
-    _check_round(tau)
+    tl = _check_round(tau)
     out = torch.empty(n_out, dtype=torch.float64, device=dev) if want_out else None
     sums = torch.empty((n_out, 2), dtype=torch.int64, device=dev) if want_sums else None
     if n_ct == 0:
@@ -775,7 +804,7 @@ def jl_aggregate(cts: torch.Tensor, biprime: int, key: int, tau: int, n_expected
         o, sm = _ptr(out[e0:e1] if want_out else None), _ptr(sums[e0:e1] if want_sums else None)
         if factor is None:
             _call(lib.fbm_jl_aggregate, _ptr(part), P, k1 - k0, es, cr, e1 - e0, _np_ptr(bp), _np_ptr(kl), kneg,
-                  int(tau), int(ct_offset) + k0, int(total_weight), negc, step, o, sm, _ptr(ws), _ptr(st), _stream())
+                  _np_ptr(tl), int(ct_offset) + k0, int(total_weight), negc, step, o, sm, _ptr(ws), _ptr(st), _stream())
         else:
             _call(lib.fbm_jl_aggregate_factor, _ptr(part), P, k1 - k0, es, cr, e1 - e0, _np_ptr(bp),
                   _ptr(factor[k0:k1]), int(total_weight), negc, step, o, sm, _ptr(ws), _ptr(st), _stream())
@@ -824,24 +853,46 @@ def ints_to_pt(values: Sequence[int], modulus: int, dev=None) -> torch.Tensor:
 
 
 def int_multiply(vals: torch.Tensor, k: int) -> List[int]:
-    """[v * k] on the device for int64 [n, 2] (lo, hi) values, 0 <= k < 2^64; FB624 when a
-    product reaches 2^128."""
-    if not 0 <= k <= U64_MAX:
-        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: factor {k} outside [0, 2^64)")
-    out = torch.empty_like(vals)
+    """[v * k] (utils.multiply, _secagg_utils.py:122-134) on the device for int64 [n, 2] (lo, hi) values
+    v < 2^128 and an integer k with |k| < 2^64: the exact products (< 2^192), negative for k < 0 as in
+    the reference; FB624 for a wider k."""
+    k = operator.index(k)
+    if abs(k) > U64_MAX:
+        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: factor {k} outside (-2^64, 2^64), "
+                                          "the device path's domain")
+    out = torch.empty((vals.shape[0], 3), dtype=torch.int64, device=vals.device)
     st = _stats(vals.device)
-    _call(N.load().fbm_int_ops, _ptr(vals.contiguous()), vals.shape[0], int(k), 0, _ptr(out), _ptr(st), _stream())
-    _check_stats(st)
-    return u128_to_ints(out)
+    _call(N.load().fbm_int_ops, _ptr(vals.contiguous()), vals.shape[0], abs(k), 0, _ptr(out), _ptr(st), _stream())
+    w = to_host(out).numpy().view(np.uint64)
+    sign = -1 if k < 0 else 1
+    return [sign * (int(a) | (int(b) << 64) | (int(c) << 128)) for a, b, c in w.tolist()]
 
 
-def int_true_divide(vals: torch.Tensor, k: int) -> List[float]:
-    """[v / k] (Python int/int true division, correctly rounded) on the device, 1 <= k < 2^64."""
-    if not 1 <= k <= U64_MAX:
-        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: divisor {k} outside [1, 2^64)")
+def int_true_divide(vals: torch.Tensor, k) -> List[float]:
+    """[v / k] (utils.divide, _secagg_utils.py:137-149) on the device for v < 2^128: an integer k
+    (0 < |k| < 2^64) with Python's correctly rounded int/int true division, a real k with Python's
+    int / float (float(v), then the IEEE division); the divisor is never truncated.  k == 0 raises
+    the reference's ZeroDivisionError; an integer |k| >= 2^64 is FB624 (the device path's domain)."""
+    import numbers
+
+    if isinstance(k, numbers.Integral):
+        k = operator.index(k)
+        if k == 0:
+            raise ZeroDivisionError("division by zero")
+        if abs(k) > U64_MAX:
+            raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: divisor {k} outside (-2^64, 2^64), "
+                                              "the device path's domain")
+        op, karg = (1 if k > 0 else 3), abs(k)
+    elif isinstance(k, numbers.Real):
+        kd = float(k)
+        if kd == 0.0:
+            raise ZeroDivisionError("float division by zero")
+        op, karg = 2, int(np.frombuffer(np.float64(kd).tobytes(), dtype=np.uint64)[0])
+    else:
+        raise TypeError(f"unsupported operand type(s) for /: 'int' and '{type(k).__name__}'")
     out = torch.empty(vals.shape[0], dtype=torch.float64, device=vals.device)
     st = _stats(vals.device)
-    _call(N.load().fbm_int_ops, _ptr(vals.contiguous()), vals.shape[0], int(k), 1, _ptr(out), _ptr(st), _stream())
+    _call(N.load().fbm_int_ops, _ptr(vals.contiguous()), vals.shape[0], karg, op, _ptr(out), _ptr(st), _stream())
     return to_host(out).numpy().tolist()
 
 
@@ -887,13 +938,14 @@ def jl_fdh(n_ct: int, modulus: int, tau: int, ct_offset: int = 0, dev=None) -> t
     """FDH.H(t_k) of t_k = ((k + ct_offset) << 512) | tau, bits_size 2048, gcd against `modulus`
     (any M: its odd part, or its square root's) -> int32 [n_ct, 64] limbs."""
     dev = dev or device()
-    _check_round(tau)
+    tl = _check_round(tau)
     if not (0 <= ct_offset and ct_offset + max(n_ct, 1) - 1 <= U64_MAX):
         raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: FDH input outside the device path's domain")
     odd, even = fdh_modulus(modulus)
     h = torch.empty((n_ct, 64), dtype=torch.int32, device=dev)
     st = _stats(dev)
-    _call(N.load().fbm_jl_fdh, n_ct, _np_ptr(int_limbs(odd, 32)), 1 if even else 0, int(tau), int(ct_offset),
+    ol = int_limbs(odd, 32)
+    _call(N.load().fbm_jl_fdh, n_ct, _np_ptr(ol), 1 if even else 0, _np_ptr(tl), int(ct_offset),
           _ptr(h), _ptr(st), _stream())
     _check_stats(st)
     return h
@@ -920,13 +972,13 @@ def jl_decrypt(cts: torch.Tensor, biprime: int, key: int, tau: int, ct_offset: i
     x = torch.empty((n_ct, 32), dtype=torch.int32, device=dev)
     if n_ct == 0:
         return x
-    _check_round(tau)
+    tl = _check_round(tau)
     lib = N.load()
     bp = _biprime_limbs(biprime)
     kl, kneg = _key_limbs(key)
     ws = torch.empty(int(lib.fbm_jl_aggregate_workspace(n_ct)), dtype=torch.uint8, device=dev)
     st = _stats(dev)
-    _call(lib.fbm_jl_decrypt, _ptr(cts.contiguous()), P, n_ct, _np_ptr(bp), _np_ptr(kl), kneg, int(tau),
+    _call(lib.fbm_jl_decrypt, _ptr(cts.contiguous()), P, n_ct, _np_ptr(bp), _np_ptr(kl), kneg, _np_ptr(tl),
           int(ct_offset), _ptr(x), _ptr(ws), _ptr(st), _stream())
     _check_stats(st)
     return x

@@ -19,6 +19,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "lib
 # A/B measurement of kernel variants (tools/ab.sh): load another build of the same library
 LIB_PATH = os.environ.get("FBM_LIB_PATH", LIB_PATH)
 
+ABI_VERSION = 2  # include/fbm_secagg.h FBM_ABI_VERSION
 FBM_OK = 0
 FBM_E_ARG = -1
 FBM_E_HIP = -2
@@ -57,6 +58,7 @@ SIGNATURES = {
     "fbm_jl_engine_for": (c_int, [c_u64]),
     "fbm_jl_batch_begin": (c_int, []),
     "fbm_jl_batch_abort": (None, []),
+    "fbm_jl_batch_count": (c_int, []),
     "fbm_jl_batch_workspace": (c_u64, []),
     "fbm_jl_batch_flush": (c_int, [c_vp, c_u64, c_vp]),
     "fbm_last_error": (ctypes.c_char_p, []),
@@ -68,21 +70,22 @@ SIGNATURES = {
     "fbm_lom_aggregate": (c_int, [c_vp, c_int, c_u64, c_u64, c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_encrypt_workspace": (c_u64, [c_u64]),
     "fbm_jl_aggregate_workspace": (c_u64, [c_u64]),
+    # the JL round (tau) is a HOST pointer to 16 limbs (< 2^512, ABI 2)
     "fbm_jl_encrypt": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_int, c_int, c_vp, c_vp,
-                               c_int, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),
+                               c_int, c_vp, c_u64, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_encrypt_phase": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_int, c_int, c_vp,
-                                     c_vp, c_int, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp, c_int]),
-    "fbm_jl_aggregate": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_u64, c_vp, c_vp, c_int, c_u64, c_u64, c_u64,
+                                     c_vp, c_int, c_vp, c_u64, c_vp, c_vp, c_vp, c_vp, c_int]),
+    "fbm_jl_aggregate": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_u64, c_vp, c_vp, c_int, c_vp, c_u64, c_u64,
                                  c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    "fbm_jl_decrypt_factor": (c_int, [c_u64, c_vp, c_vp, c_int, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),
-    "fbm_jl_decrypt_factor_phase": (c_int, [c_u64, c_vp, c_vp, c_int, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp, c_int]),
+    "fbm_jl_decrypt_factor": (c_int, [c_u64, c_vp, c_vp, c_int, c_vp, c_u64, c_vp, c_vp, c_vp, c_vp]),
+    "fbm_jl_decrypt_factor_phase": (c_int, [c_u64, c_vp, c_vp, c_int, c_vp, c_u64, c_vp, c_vp, c_vp, c_vp, c_int]),
     "fbm_jl_aggregate_factor": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_u64, c_vp, c_vp, c_u64, c_dbl, c_dbl,
                                         c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_pack": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_vp, c_vp, c_vp]),
     "fbm_jl_unpack": (c_int, [c_vp, c_u64, c_int, c_int, c_u64, c_vp, c_vp]),
-    "fbm_jl_fdh": (c_int, [c_u64, c_vp, c_int, c_u64, c_u64, c_vp, c_vp, c_vp]),
+    "fbm_jl_fdh": (c_int, [c_u64, c_vp, c_int, c_vp, c_u64, c_vp, c_vp, c_vp]),
     "fbm_jl_product": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp, c_vp, c_vp]),
-    "fbm_jl_decrypt": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp, c_int, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),
+    "fbm_jl_decrypt": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp, c_int, c_vp, c_u64, c_vp, c_vp, c_vp, c_vp]),
     "fbm_int_ops": (c_int, [c_vp, c_u64, c_u64, c_int, c_vp, c_vp, c_vp]),
     "fbm_ass_split": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_vp, c_vp, c_u64, c_vp, c_vp]),
     "fbm_ass_reconstruct": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp]),
@@ -119,7 +122,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.fbm_abi_version() != 1:
+        if lib.fbm_abi_version() != ABI_VERSION:
             raise NativeUnavailable("ABI version mismatch")
         _lib = lib
         return lib

@@ -309,6 +309,11 @@ static void fdh_midstate(uint32_t mid[8]) {
   memcpy(mid, st, sizeof(st));
 }
 
+// tau (16 LE words, < 2^512) -> FDH block 15 in SHA-256 word order
+static void set_tau(JlParams& jp, const uint32_t* tau) {
+  for (int i = 0; i < 16; ++i) jp.tau_w[i] = tau ? tau[15 - i] : 0u;
+}
+
 static void big_trim(Big& a) {
   while (a.size() > 1 && a.back() == 0u) a.pop_back();
 }
@@ -346,7 +351,7 @@ static Big big_mullo(const Big& a, const Big& b, size_t n) {
 
 // FDH.H's parameters only (fbm_jl_fdh and the generic engine): the gcd modulus' odd part
 // (>= 1; 1: every odd r is coprime) and whether r must be odd as well
-static int fdh_params(const uint32_t* n_odd, int even, uint64_t tau, uint64_t ct_offset, JlParams& jp) {
+static int fdh_params(const uint32_t* n_odd, int even, const uint32_t* tau, uint64_t ct_offset, JlParams& jp) {
   if (!(n_odd[0] & 1u)) {
     set_error("FDH: the gcd modulus' odd part must be odd");
     return FBM_E_ARG;
@@ -354,14 +359,14 @@ static int fdh_params(const uint32_t* n_odd, int even, uint64_t tau, uint64_t ct
   memset(&jp, 0, sizeof(jp));
   for (int i = 0; i < 32; ++i) jp.N32[i] = n_odd[i];
   jp.fdh_even = even ? 1 : 0;
-  jp.tau = tau;
+  set_tau(jp, tau);
   jp.ct_offset = ct_offset;
   fdh_midstate(jp.mid);
   return FBM_OK;
 }
 
 // FDH(2048, N^2): gcd(r, N^2) == 1 iff r is coprime to N's odd part (and odd, for an even N)
-static int fdh_params_for_biprime(const uint32_t* biprime, uint64_t tau, uint64_t ct_offset, JlParams& jp) {
+static int fdh_params_for_biprime(const uint32_t* biprime, const uint32_t* tau, uint64_t ct_offset, JlParams& jp) {
   Big N(biprime, biprime + 32);
   const int s = big_ctz(N);
   Big m = big_shr(N, s);
@@ -438,7 +443,7 @@ static int build_gen_ctx(const uint32_t* biprime, const uint32_t* key, int key_n
 // mod 2^1024, the FDH midstate): ~0.3 ms of host big-integer work per call, so it is built once
 // per biprime and kept in a small process-wide cache (a round's encrypts and aggregate, and
 // every round of an experiment, share one biprime).
-static int build_jl_params_uncached(const uint32_t* biprime, int es, int cr, uint64_t tau, uint64_t ct_offset,
+static int build_jl_params_uncached(const uint32_t* biprime, int es, int cr, const uint32_t* tau, uint64_t ct_offset,
                                     JlParams& jp) {
   memset(&jp, 0, sizeof(jp));
   Big N(biprime, biprime + 32);
@@ -504,7 +509,7 @@ static int build_jl_params_uncached(const uint32_t* biprime, int es, int cr, uin
   fbm_n30_setup(jp.N32, jp.n30);
   jp.es = es;
   jp.cr = cr;
-  jp.tau = tau;
+  set_tau(jp, tau);
   jp.ct_offset = ct_offset;
   fdh_midstate(jp.mid);
   return FBM_OK;
@@ -517,7 +522,8 @@ struct JlParamsCacheEntry {
 static std::mutex g_jp_mu;
 static std::vector<JlParamsCacheEntry> g_jp_cache;  // most recently used last, at most 8
 
-static int build_jl_params(const uint32_t* biprime, int es, int cr, uint64_t tau, uint64_t ct_offset, JlParams& jp) {
+static int build_jl_params(const uint32_t* biprime, int es, int cr, const uint32_t* tau, uint64_t ct_offset,
+                           JlParams& jp) {
   if (es < 1 || cr < 1 || es > 100 || (int64_t)es * cr > 1024) {
     set_error("invalid VES parameters es=%d cr=%d", es, cr);
     return FBM_E_ARG;
@@ -532,7 +538,7 @@ static int build_jl_params(const uint32_t* biprime, int es, int cr, uint64_t tau
         jp = e.jp;
         jp.es = es;
         jp.cr = cr;
-        jp.tau = tau;
+        set_tau(jp, tau);
         jp.ct_offset = ct_offset;
         jp.key_is_zero = 0;
         return FBM_OK;
@@ -737,10 +743,6 @@ int fbm_check_stats(const uint32_t* st, int lom_nodes, uint32_t* max_bits_out) {
     set_error("bounded device loop hit its iteration cap");
     return FBM_E_ITER;
   }
-  if (f & FBM_ERR_INT_RANGE) {
-    set_error("multiply: a product reaches 2^128, outside the device path's domain");
-    return FBM_E_UNSUPPORTED;
-  }
   if (f & FBM_ERR_PT_WIDE) {
     set_error("VES: a packed value spills past the 1024-bit plaintext (a value wider than its slot); "
               "outside the device path's domain");
@@ -879,7 +881,7 @@ uint64_t fbm_jl_aggregate_workspace(uint64_t n_ct) {
 // parameters from the same arguments and use the same workspace, so (1 then 2) == 3.
 static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
                            uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,
-                           const uint32_t* key, int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* ct_out,
+                           const uint32_t* key, int key_negative, const uint32_t* tau, uint64_t ct_offset, uint32_t* ct_out,
                            void* workspace, uint32_t* stats, void* stream, int phase) {
   hipStream_t s = (hipStream_t)stream;
   int rc;
@@ -1007,7 +1009,7 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
 
 int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
                    uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime, const uint32_t* key,
-                   int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* ct_out, void* workspace,
+                   int key_negative, const uint32_t* tau, uint64_t ct_offset, uint32_t* ct_out, void* workspace,
                    uint32_t* stats, void* stream) {
   return jl_encrypt_impl(x, x_dtype, n, clip, two_clip, target_f, target_m1, weight, es, cr, biprime, key,
                          key_negative, tau, ct_offset, ct_out, workspace, stats, stream, 3);
@@ -1015,7 +1017,7 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
 
 int fbm_jl_encrypt_phase(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
                          uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,
-                         const uint32_t* key, int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* ct_out,
+                         const uint32_t* key, int key_negative, const uint32_t* tau, uint64_t ct_offset, uint32_t* ct_out,
                          void* workspace, uint32_t* stats, void* stream, int phase) {
   if (phase < 1 || phase > 3) {
     set_error("fbm_jl_encrypt_phase: phase must be 1, 2 or 3");
@@ -1057,7 +1059,7 @@ static JlAggWs agg_ws(void* workspace, uint64_t n_ct) {
 // ServerKey's factor H(t_k)^sk0 mod N^2 (inverse first for sk0 < 0): depends on the round,
 // the ciphertext index and the key only -- not on the parties' ciphertexts.
 // phase bits: 1 = constants + FDH, 2 = the exponentiation, 4 = the inverse (negative key)
-static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau,
+static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative, const uint32_t* tau,
                           uint64_t ct_offset, uint32_t* factor, const JlAggWs& w, uint32_t* stats, hipStream_t s,
                           int phase = 7) {
   JlParams jp;
@@ -1135,7 +1137,7 @@ static int jl_combine_impl(const uint32_t* cts, int n_parties, uint64_t n_ct, in
       return launch_jl_decode(w.xs, es, cr, n_out, total_weight, neg_clip, step, out, sums, stats, s);
     });
   }
-  if ((rc = build_jl_params(biprime, es, cr, 0, 0, jp))) return rc;
+  if ((rc = build_jl_params(biprime, es, cr, nullptr, 0, jp))) return rc;
   JlSched none;
   memset(&none, 0, sizeof(none));
   if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, none, w.ops, w.cst, s); }))) return rc;
@@ -1167,7 +1169,7 @@ static int jl_agg_checks(int n_parties, uint64_t n_ct, const uint32_t* biprime, 
 }
 
 int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,
-                     const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau, uint64_t ct_offset,
+                     const uint32_t* biprime, const uint32_t* key, int key_negative, const uint32_t* tau, uint64_t ct_offset,
                      uint64_t total_weight, double neg_clip, double step, double* out, uint64_t* sums,
                      void* workspace, uint32_t* stats, void* stream) {
   hipStream_t s = (hipStream_t)stream;
@@ -1190,7 +1192,7 @@ int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, 
                          stats, s);
 }
 
-int fbm_jl_decrypt_factor(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau,
+int fbm_jl_decrypt_factor(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative, const uint32_t* tau,
                           uint64_t ct_offset, uint32_t* factor, void* workspace, uint32_t* stats, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   int rc = zero_stats(stats, s);
@@ -1205,7 +1207,7 @@ int fbm_jl_decrypt_factor(uint64_t n_ct, const uint32_t* biprime, const uint32_t
 }
 
 int fbm_jl_decrypt_factor_phase(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative,
-                                uint64_t tau, uint64_t ct_offset, uint32_t* factor, void* workspace, uint32_t* stats,
+                                const uint32_t* tau, uint64_t ct_offset, uint32_t* factor, void* workspace, uint32_t* stats,
                                 void* stream, int phase) {
   hipStream_t s = (hipStream_t)stream;
   int rc;
@@ -1279,7 +1281,7 @@ int fbm_jl_unpack(const uint32_t* pt, uint64_t n_ct, int es, int cr, uint64_t n_
   return timed("jl_decode", s, [&] { return launch_jl_decode(pt, es, cr, n_out, 1, 0.0, 1.0, nullptr, vals, nullptr, s); });
 }
 
-int fbm_jl_fdh(uint64_t n_ct, const uint32_t* modulus_odd, int modulus_even, uint64_t tau, uint64_t ct_offset,
+int fbm_jl_fdh(uint64_t n_ct, const uint32_t* modulus_odd, int modulus_even, const uint32_t* tau, uint64_t ct_offset,
                uint32_t* h, uint32_t* stats, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   int rc = zero_stats(stats, s);
@@ -1317,7 +1319,7 @@ int fbm_jl_product(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint
     });
   }
   JlParams jp;
-  if ((rc = build_jl_params(biprime, 1, 1, 0, 0, jp))) return rc;
+  if ((rc = build_jl_params(biprime, 1, 1, nullptr, 0, jp))) return rc;
   JlSched none;
   memset(&none, 0, sizeof(none));
   if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, none, w.ops, w.cst, s); }))) return rc;
@@ -1330,7 +1332,7 @@ int fbm_jl_product(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint
 }
 
 int fbm_jl_decrypt(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* biprime, const uint32_t* key,
-                   int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* x, void* workspace, uint32_t* stats,
+                   int key_negative, const uint32_t* tau, uint64_t ct_offset, uint32_t* x, void* workspace, uint32_t* stats,
                    void* stream) {
   hipStream_t s = (hipStream_t)stream;
   int rc = zero_stats(stats, s);
@@ -1354,8 +1356,8 @@ int fbm_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, void* out, ui
   hipStream_t s = (hipStream_t)stream;
   int rc = zero_stats(stats, s);
   if (rc) return rc;
-  if ((op != 0 && op != 1) || (op == 1 && k == 0)) {
-    set_error("fbm_int_ops: op must be 0 (multiply) or 1 (divide, k >= 1)");
+  if (op < 0 || op > 3 || ((op == 1 || op == 3) && k == 0)) {
+    set_error("fbm_int_ops: op must be 0 (multiply), 1 / 3 (divide by k / -k, k >= 1) or 2 (divide by a float64)");
     return FBM_E_ARG;
   }
   if (n == 0) return FBM_OK;
@@ -1364,13 +1366,15 @@ int fbm_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, void* out, ui
     return FBM_E_ARG;
   }
   return timed("int_ops", s, [&] {
-    return launch_int_ops(x, n, k, op, op == 0 ? (uint64_t*)out : nullptr, op == 1 ? (double*)out : nullptr, stats, s);
+    return launch_int_ops(x, n, k, op, op == 0 ? (uint64_t*)out : nullptr, op != 0 ? (double*)out : nullptr, stats, s);
   });
 }
 
 int fbm_jl_batch_begin(void) { return jl_batch_begin(); }
 
 void fbm_jl_batch_abort(void) { jl_batch_abort(); }
+
+int fbm_jl_batch_count(void) { return jl_batch_count(); }
 
 uint64_t fbm_jl_batch_workspace(void) { return jl_batch_workspace(); }
 
@@ -1419,7 +1423,8 @@ int fbm_test_nadic_consts(const uint32_t* n32, uint32_t* nk, uint32_t* r2na, uin
     return FBM_E_ARG;
   }
   JlParams jp;
-  int rc = build_jl_params(n32, 34, 30, 1, 0, jp);
+  const uint32_t tau1[16] = {1u};
+  int rc = build_jl_params(n32, 34, 30, tau1, 0, jp);
   if (rc) return rc;
   memcpy(nk, jp.na.nk, sizeof(jp.na.nk));
   memcpy(r2na, jp.na.r2na, sizeof(jp.na.r2na));

@@ -16,7 +16,6 @@
 #define FBM_ERR_FDH_OVERFLOW 2u    // no coprime r of 1..7 FDH digests (reference: OverflowError)
 #define FBM_ERR_NOT_INVERTIBLE 4u  // server-key power not invertible mod N^2
 #define FBM_ERR_ITER_CAP 8u        // a bounded data-dependent loop hit its cap
-#define FBM_ERR_INT_RANGE 64u       // utils.multiply: a product reaches 2^128 (device domain)
 #define FBM_ERR_ROUND_RANGE 128u   // LOM: some i + tau reaches 2^64 with peers to mask with
 #define FBM_ERR_PT_WIDE 32u        // VES: a packed value spills past the 1024-bit plaintext
 #define FBM_WARN_CLIPPED 16u       // not an error: some |x| > clipping range (the reference's
@@ -127,7 +126,8 @@ struct JlParams {
   uint32_t Ninv32[32];           // N^-1 mod 2^1024 (exact divisions by N: jl_prod, jl_lift, jl_split)
   int n_bits;                    // bit length of N
   int es, cr;                    // VES slot size / slots per ciphertext
-  uint64_t tau;
+  uint32_t tau_w[16];            // the round tau < 2^512 as FDH's message block 15 (t's low 512 bits,
+                                 // big-endian words: tau_w[15] = tau mod 2^32)
   uint64_t ct_offset;            // global index of ciphertext 0 (element-range shard)
   uint32_t mid[8];               // SHA-256 state after the 14 all-zero message blocks
   FbmN30 n30;                    // N in signed-30 limbs + N^-1 mod 2^30 (modular inverse)
@@ -168,6 +168,7 @@ int jl_batch_begin();
 void jl_batch_abort();
 bool jl_batch_accept(bool on);
 bool jl_batch_active();
+int jl_batch_count();  // segments recorded in this thread's open batch (0 when none is open)
 uint64_t jl_batch_workspace();
 int jl_batch_flush(void* workspace, uint64_t ws_bytes, hipStream_t s);
 int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const JlSched& sc, int mode,

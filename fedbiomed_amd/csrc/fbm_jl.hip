@@ -339,7 +339,7 @@ __host__ __device__ inline bool gcd_is_one_r8(const uint32_t (&r)[8], const uint
 }
 
 // FDH.H(t_k): message = t.to_bytes(1024,'big') || counter (1 byte).  Blocks 0..13 are
-// all zero for k < 2^64 (midstate from the host), block 14 carries k, block 15 tau,
+// all zero for k < 2^64 (midstate from the host), block 14 carries k, block 15 tau (< 2^512),
 // block 16 the counter byte + padding (length 8200 bits).  While gcd(r, N^2) != 1 the
 // counter is bumped and r grows by one digest (r = D1 || D2 || ...).  r is tested with 1..7
 // digests only: once 8 digests (256 bytes = bits_size // 8) are in, the reference's inner
@@ -359,8 +359,8 @@ __global__ void __launch_bounds__(256) jl_fdh_kernel(uint64_t n_ct, JlParams jp,
   W[14] = (uint32_t)(k >> 32);
   W[15] = (uint32_t)k;
   fbm_sha256_compress(st, W);
-  W[14] = (uint32_t)(jp.tau >> 32);
-  W[15] = (uint32_t)jp.tau;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) W[i] = jp.tau_w[i];  // block 15: the round (any tau < 2^512)
   fbm_sha256_compress(st, W);
   uint32_t r[64];
 #pragma unroll
@@ -1625,6 +1625,8 @@ int jl_batch_begin() {
 
 void jl_batch_abort() { g_batch.active = false; }
 
+int jl_batch_count() { return g_batch.active ? g_batch.bt.nseg : 0; }
+
 bool jl_batch_accept(bool on) {
   const bool prev = g_batch.accept;
   g_batch.accept = on;
@@ -1769,23 +1771,36 @@ int launch_jl_decode(const uint32_t* xs, int es, int cr, uint64_t n_out, uint64_
 }
 
 // multiply / divide of the reference's secagg utils (_secagg_utils.py:122-149: [e * k], [e / k]) on
-// (lo, hi) uint64 pairs: op 0 = v * k (u128; FBM_ERR_INT_RANGE if the product reaches 2^128),
-// op 1 = v / k as Python's int/int true division (correctly rounded float64), k >= 1.
+// (lo, hi) uint64 pairs v < 2^128:
+//   op 0: v * k, k < 2^64 -> (w0, w1, w2) uint64 words of the exact product (< 2^192; the host
+//         applies the sign of a negative weight)
+//   op 1: v / k, 1 <= k < 2^64, Python's int/int true division (correctly rounded float64)
+//   op 2: v / kd, kd = the float64 whose bits k holds: Python's int / float (float(v), correctly
+//         rounded, then the IEEE division)
+//   op 3: -(v / k), the int/int division by a negative divisor -k
 __global__ void __launch_bounds__(256) int_ops_kernel(const uint64_t* __restrict__ x, uint64_t n, uint64_t k, int op,
                                                       uint64_t* __restrict__ prod, double* __restrict__ quot,
                                                       uint32_t* __restrict__ stats) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t lo = x[2 * i], hi = x[2 * i + 1];
-  if (op == 1) {
-    quot[i] = fbm_true_div_u128(((unsigned __int128)hi << 64) | lo, k);
+  const unsigned __int128 v = ((unsigned __int128)hi << 64) | lo;
+  if (op == 1 || op == 3) {
+    const double q = fbm_true_div_u128(v, k);
+    quot[i] = op == 3 ? -q : q;
+    return;
+  }
+  if (op == 2) {
+    double kd;
+    memcpy(&kd, &k, sizeof(kd));
+    quot[i] = fbm_true_div_u128(v, 1) / kd;  // float(v) (round to nearest even), then one division
     return;
   }
   const unsigned __int128 pl = (unsigned __int128)lo * k, ph = (unsigned __int128)hi * k;
-  const unsigned __int128 r = pl + (ph << 64);
-  if ((ph >> 64) != 0 || r < pl) atomicOr(stats + FBM_STAT_ERRFLAGS, FBM_ERR_INT_RANGE);
-  prod[2 * i] = (uint64_t)r;
-  prod[2 * i + 1] = (uint64_t)(r >> 64);
+  const unsigned __int128 mid = (pl >> 64) + (uint64_t)ph;
+  prod[3 * i] = (uint64_t)pl;
+  prod[3 * i + 1] = (uint64_t)mid;
+  prod[3 * i + 2] = (uint64_t)(ph >> 64) + (uint64_t)(mid >> 64);
 }
 
 int launch_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, uint64_t* prod, double* quot, uint32_t* stats,

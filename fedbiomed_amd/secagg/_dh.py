@@ -64,6 +64,9 @@ def _ssl():
 
 
 _EVP_PKEY_EC = 408  # NID_X9_62_id_ecPublicKey
+# pem_password_cb(char *buf, int size, int rwflag, void *u): OpenSSL asks for a pass phrase through
+# it; with a NULL callback it would fall back to PEM_def_callback, which prompts on the terminal
+_PEM_PASSWORD_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p)
 _BIO_CTRL_INFO = 3  # BIO_get_mem_data
 
 
@@ -117,7 +120,9 @@ def _generate_p256() -> _PKey:
 
 def _load(data: bytes, private: bool) -> _PKey:
     """PEM bytes -> key; ValueError on anything OpenSSL does not parse (as cryptography's
-    load_pem_private_key / load_pem_public_key)."""
+    load_pem_private_key / load_pem_public_key).  An encrypted private key is refused with
+    cryptography's TypeError for load_pem_private_key(password=None): the pass-phrase callback
+    only records that OpenSSL asked and returns -1, so nothing ever prompts."""
     if not isinstance(data, (bytes, bytearray)):
         raise TypeError("data must be bytes")
     lib = _ssl()
@@ -125,13 +130,22 @@ def _load(data: bytes, private: bool) -> _PKey:
     bio = lib.BIO_new_mem_buf(buf, len(buf))
     if not bio:
         raise MemoryError("OpenSSL: no memory BIO")
+    asked = []
+
+    def no_password(_buf, _size, _rwflag, _u):
+        asked.append(True)
+        return -1
+
+    cb = _PEM_PASSWORD_CB(no_password)  # alive until the read returns
     try:
         fn = lib.PEM_read_bio_PrivateKey if private else lib.PEM_read_bio_PUBKEY
-        p = fn(bio, None, None, None)
+        p = fn(bio, None, ctypes.cast(cb, ctypes.c_void_p), None)
     finally:
         lib.BIO_free(bio)
         lib.ERR_clear_error()
     if not p:
+        if asked:
+            raise TypeError("Password was not given but private key is encrypted")
         raise ValueError("Could not deserialize key data.")
     return _PKey(p, private=private)
 

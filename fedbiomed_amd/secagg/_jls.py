@@ -19,7 +19,7 @@ call, as JoyeLibert.aggregate is.
 Domain of the device path (FB624 outside it): 2 <= N < 2^1024 (an even N
 runs on the generic engine, fedbiomed_amd/csrc/fbm_gen.hip, an odd one on the Montgomery engines); a
 PublicParam with bits = 1024 whose hashing function is FDH(2048, N^2).H (what
-SecaggCrypter._setup_public_param builds); tau in [0, 2^64); VES values in [0, 2^128) with
+SecaggCrypter._setup_public_param builds); tau in [0, 2^512); VES values in [0, 2^128) with
 es <= 100; ServerKey.decrypt with delta^2 = 1 (mod N).  Integers are Python ints (gmpy2 is
 not a dependency): where the reference returns gmpy2.mpz this returns int, and FDH takes an
 int modulus.
@@ -137,9 +137,13 @@ def _device_n(pp: PublicParam) -> int:
 
 
 def _check_tau(tau) -> int:
+    """A round the device takes: 0 <= tau < 2^512.  A negative one is the reference's OverflowError
+    (FDH.H's int(t).to_bytes, _jls.py:747); 2^512 and above OR into t's k bits there (FB624 here)."""
     t = operator.index(tau)
-    if not 0 <= t < 2**64:
-        raise _unsupported(f"round tau={t} (device path: 0 <= tau < 2^64)")
+    if t < 0:
+        raise OverflowError("can't convert negative int to unsigned")
+    if t >> 512:
+        raise _unsupported(f"round tau={t} (device path: 0 <= tau < 2^512)")
     return t
 
 
@@ -284,10 +288,10 @@ class UserKey(BaseKey):
         """c_k = (N pt_k + 1) H(t_k)^key mod N^2 -- fbm_jl_encrypt on plaintext limbs."""
         if not isinstance(plaintext, list):
             raise TypeError(f"Expected plaintext type list but got {type(plaintext)}")
+        if not plaintext:  # the reference hashes no round for an empty list
+            return []
         n = _device_n(self._public_param)
         tau = _check_tau(tau)
-        if not plaintext:
-            return []
         pts = D.ints_to_pt(plaintext, n)
         ct = D.jl_encrypt(pts, n, self._key, tau, 1, kind="pt")
         return D.limbs_to_ints(D.to_host(ct).numpy())
@@ -308,13 +312,13 @@ class ServerKey(BaseKey):
             raise TypeError("Cipher text should be list of EncryptedNumbers")
         n = _device_n(self._public_param)
         d2 = delta ** 2
-        if math.gcd(d2 % (n * n), n * n) != 1:
+        if math.gcd(d2 % (n * n), n * n) != 1:  # invert(delta^2, N^2) runs even on an empty list
             raise ZeroDivisionError("invert() no inverse exists")
+        if not cipher:
+            return []
         if d2 % n != 1:
             raise _unsupported("ServerKey.decrypt with delta^2 != 1 (mod N)")
         tau = _check_tau(tau)
-        if not cipher:
-            return []
         x = D.jl_decrypt(_term_rows(cipher, n), n, d2 * self._key, tau)
         return D.limbs_to_ints_w(x, 32)
 
@@ -345,10 +349,10 @@ class JoyeLibert:
                 f"got {type(x_u_tau)}"
             )
         es, cr = self._vector_encoder._slot(n_users)
-        n = _device_n(user_key.public_param)
-        tau = _check_tau(tau)
         if not x_u_tau:
             return []
+        n = _device_n(user_key.public_param)
+        tau = _check_tau(tau)
         ct = D.jl_encrypt(D.ints_to_u128(x_u_tau), n, user_key.key, tau, n_users, slot=(es, cr), kind="u128")
         return D.limbs_to_ints(D.to_host(ct).numpy())
 
@@ -367,13 +371,13 @@ class JoyeLibert:
         # ServerKey.decrypt's checks, then the decode's slot
         if not all([isinstance(c, EncryptedNumber) for c in summed]):
             raise TypeError("Cipher text should be list of EncryptedNumbers")
+        if not summed:
+            return []
         n = _device_n(sk_0.public_param)
         tau = _check_tau(tau)
         es, cr = self._vector_encoder._slot(n_user)
         if es > 128:
             raise _unsupported(f"VES decode of {es}-bit slots")
-        if not summed:
-            return []
         _, sums = D.jl_aggregate(_term_rows(summed, n), n, sk_0.key, tau, num_expected_params, 1,
                                  want_out=False, want_sums=True, slot=(es, cr))
         return D.u128_to_ints(sums)
@@ -391,19 +395,21 @@ class FDH:
         self._n_modules = n_modulus
 
     def _hash_range(self, tau: int, len_: int, k0: int = 0) -> List[int]:
+        if len_ <= 0:
+            return []
         if self.bits_size != SAParameters.KEY_SIZE:
             raise _unsupported(f"FDH of bits_size {self.bits_size} (device path: {SAParameters.KEY_SIZE})")
         tau = _check_tau(tau)
-        if len_ <= 0:
-            return []
         h = D.jl_fdh(len_, int(self._n_modules), tau, k0)
         return D.limbs_to_ints(D.to_host(h).numpy())
 
     def H(self, t: int) -> int:
         """SHA256(t || 1) || SHA256(t || 2) || ... until gcd(r, n_modulus) == 1, t as 1024
-        big-endian bytes -- fbm_jl_fdh with t = (k << 512) | tau (k, tau < 2^64)."""
+        big-endian bytes -- fbm_jl_fdh with t = (k << 512) | tau (k < 2^64, tau < 2^512)."""
         t = operator.index(t)
+        if t < 0:  # int(t).to_bytes(...) (_jls.py:747)
+            raise OverflowError("can't convert negative int to unsigned")
         k, tau = t >> 512, t & ((1 << 512) - 1)
-        if t < 0 or k >= 2**64 or tau >= 2**64:
-            raise _unsupported("FDH input t outside {(k << 512) | tau : k, tau < 2^64}")
+        if k >= 2**64:
+            raise _unsupported("FDH input t outside {(k << 512) | tau : k < 2^64, tau < 2^512}")
         return self._hash_range(tau, 1, k)[0]

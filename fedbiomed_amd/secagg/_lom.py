@@ -11,7 +11,7 @@ import torch
 
 from .. import _device as D
 from ..constants import ErrorNumbers
-from ..exceptions import FedbiomedSecaggError
+from ..exceptions import FedbiomedSecaggError  # noqa: F401  (raised by D's helpers; the API's error class)
 
 _MAX_ROUND = 1000
 
@@ -53,11 +53,8 @@ class LOM:
         num_nodes = len(node_ids)
         _max_param_bits = max(val.bit_length() for val in x_u_tau)
         _node_bits = math.ceil(math.log2(num_nodes))
-        if _max_param_bits >= self._values_bit - _node_bits:
-            raise FedbiomedSecaggError(
-                f"{ErrorNumbers.FB417.value}: Secure aggregation overflow detected.\n\n"
-                f"Your value requires {_max_param_bits} bits, but only {self._values_bit - _node_bits} bits "
-                f"are available ({self._values_bit}-bit dtype minus {_node_bits} bits reserved for {num_nodes} nodes).")
+        if _max_param_bits >= self._values_bit - _node_bits:  # the reference's message, word for word
+            raise FedbiomedSecaggError(D._lom_overflow_message(_max_param_bits, num_nodes))
         x = D.u64_to_device(list(x_u_tau))
         peers = [p for p in node_ids if p != node_id]
         y = D.lom_protect(x, [pairwise_secrets[p] for p in peers], [1 if p < node_id else -1 for p in peers],

@@ -221,20 +221,20 @@ class SecaggCrypter:
     @staticmethod
     def _apply_average(params: List[int], total_weight: int) -> List:
         """Reference `_secagg_crypter.py:233-249` on the device (`fbm_int_ops`: integer sums below
-        2^128, a divisor below 2^64); the crypters' own averaging is fused into their kernels."""
+        2^128; an integer divisor of either sign below 2^64 in magnitude, or a float one, never
+        truncated); the crypters' own averaging is fused into their kernels."""
         if any(v < 0 for v in params):
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value}: Cannot compute weighted average, values outside of bounds")
         if not params:
             return []
-        if total_weight == 0:
-            raise ZeroDivisionError("division by zero")
-        return D.int_true_divide(D.ints_to_u128(params), total_weight)
+        return D.int_true_divide(D.ints_to_u128(params), total_weight)  # its ZeroDivisionErrors as Python's
 
     @staticmethod
     def _apply_weighting(params: List[int], weight: int, target_range: int = SAParameters.TARGET_RANGE) -> List[int]:
         """Reference `_secagg_crypter.py:252-276` on the device (`fbm_int_ops`: values below 2^128, a
-        weight in [0, 2^64)); the crypters' own weighting is fused into their encrypt kernels."""
+        weight of either sign below 2^64 in magnitude, exact products); the crypters' own weighting
+        is fused into their encrypt kernels."""
         max_val = target_range - 1
         if any(v > max_val or v < 0 for v in params):
             raise FedbiomedSecaggCrypterError(

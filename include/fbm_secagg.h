@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FBM_ABI_VERSION 1
+#define FBM_ABI_VERSION 2 /* 2: the JL round is a 512-bit value (16 limbs), FBM_ABI 1 took a uint64 */
 
 #define FBM_OK 0
 #define FBM_E_ARG (-1)         /* bad argument (type/shape/range)            -> FB624      */
@@ -107,7 +107,8 @@ int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t tot
  *          even one on the generic engine, fedbiomed_amd/csrc/fbm_gen.hip -- same results)
  * key:     HOST, 64 limbs |sk| (< 2^2048);  key_negative: sign of sk
  * es, cr:  VES slot bits / slots per ciphertext (JoyeLibert vector encoder, _jls.py:104-116)
- * tau:     round (< 2^64); n_ct = ceil(n / cr)
+ * tau:     HOST, 16 limbs: the round, < 2^512 (t_k = (k << 512) | tau, FDH.H's input, _jls.py:451-467);
+ *          n_ct = ceil(n / cr)
  * ct_offset: global index of ciphertext 0 (t_k = ((k + ct_offset) << 512) | tau) when the
  *          element range is sharded across devices on ciphertext boundaries; 0 otherwise.   */
 
@@ -129,7 +130,7 @@ uint64_t fbm_jl_aggregate_workspace(uint64_t n_ct);
  *   ct_out: device, n_ct x 64 uint32 limbs                                                */
 int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
                    uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,
-                   const uint32_t* key, int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* ct_out,
+                   const uint32_t* key, int key_negative, const uint32_t* tau, uint64_t ct_offset, uint32_t* ct_out,
                    void* workspace, uint32_t* stats, void* stream);
 /* fbm_jl_encrypt in two phases on the same arguments and workspace: phase 1 = the prologue
  * kernels (pack, N*pt+1 digits, FDH, the inverse of H for a negative key), phase 2 = the
@@ -137,7 +138,7 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
  * device issue every prologue before the first exponentiation takes the whole chip. */
 int fbm_jl_encrypt_phase(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
                          uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,
-                         const uint32_t* key, int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* ct_out,
+                         const uint32_t* key, int key_negative, const uint32_t* tau, uint64_t ct_offset, uint32_t* ct_out,
                          void* workspace, uint32_t* stats, void* stream, int phase);
 
 /* JL aggregate: prod_u c_u * H(t_k)^sk0 mod N^2, x = ((v-1)//N) mod N, VES decode,
@@ -149,7 +150,7 @@ int fbm_jl_encrypt_phase(const void* x, int x_dtype, uint64_t n, double clip, do
  *   out:  device, n_out float64 (may be NULL)
  *   sums: device, n_out x 2 uint64 (lo, hi) decoded integer sums (may be NULL)            */
 int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,
-                     const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau,
+                     const uint32_t* biprime, const uint32_t* key, int key_negative, const uint32_t* tau,
                      uint64_t ct_offset, uint64_t total_weight, double neg_clip, double step, double* out, uint64_t* sums,
                      void* workspace, uint32_t* stats, void* stream);
 
@@ -161,12 +162,12 @@ int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, 
  * fbm_jl_aggregate_factor: the ciphertext product (_jls.py:353-374,691-693), v = prod *
  *   factor, x = (v-1)/N, VES decode, average, dequantise -- as fbm_jl_aggregate.
  * Both take fbm_jl_aggregate_workspace(n_ct) bytes of workspace. */
-int fbm_jl_decrypt_factor(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative, uint64_t tau,
+int fbm_jl_decrypt_factor(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative, const uint32_t* tau,
                           uint64_t ct_offset, uint32_t* factor, void* workspace, uint32_t* stats, void* stream);
 /* fbm_jl_decrypt_factor in phases on the same arguments and workspace: bit 1 = constants and
  * FDH, bit 2 = the exponentiation, bit 4 = the inverse (negative key); 7 == fbm_jl_decrypt_factor. */
 int fbm_jl_decrypt_factor_phase(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative,
-                                uint64_t tau, uint64_t ct_offset, uint32_t* factor, void* workspace, uint32_t* stats,
+                                const uint32_t* tau, uint64_t ct_offset, uint32_t* factor, void* workspace, uint32_t* stats,
                                 void* stream, int phase);
 int fbm_jl_aggregate_factor(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, int cr, uint64_t n_out,
                             const uint32_t* biprime, const uint32_t* factor, uint64_t total_weight, double neg_clip,
@@ -193,19 +194,23 @@ int fbm_jl_aggregate_factor(const uint32_t* cts, int n_parties, uint64_t n_ct, i
  *   limbs (no VES decode); workspace fbm_jl_aggregate_workspace(n_ct).                    */
 int fbm_jl_pack(const void* x, int x_dtype, uint64_t n, int es, int cr, uint32_t* pt, uint32_t* stats, void* stream);
 int fbm_jl_unpack(const uint32_t* pt, uint64_t n_ct, int es, int cr, uint64_t n_out, uint64_t* vals, void* stream);
-int fbm_jl_fdh(uint64_t n_ct, const uint32_t* modulus_odd, int modulus_even, uint64_t tau, uint64_t ct_offset,
+int fbm_jl_fdh(uint64_t n_ct, const uint32_t* modulus_odd, int modulus_even, const uint32_t* tau, uint64_t ct_offset,
                uint32_t* h, uint32_t* stats, void* stream);
 int fbm_jl_product(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* biprime, uint32_t* out,
                    void* workspace, void* stream);
 int fbm_jl_decrypt(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* biprime, const uint32_t* key,
-                   int key_negative, uint64_t tau, uint64_t ct_offset, uint32_t* x, void* workspace, uint32_t* stats,
+                   int key_negative, const uint32_t* tau, uint64_t ct_offset, uint32_t* x, void* workspace, uint32_t* stats,
                    void* stream);
 
 /* multiply / divide of the reference's secagg utils (fedbiomed/common/utils/_secagg_utils.py:122-149,
- * used by SecaggCrypter._apply_weighting / _apply_average, :233-276) on n integers given as (lo, hi)
- * uint64 pairs in x (device): op 0 = x * k into out as (lo, hi) pairs (a product >= 2^128 is
- * FBM_E_UNSUPPORTED at fbm_check_stats), op 1 = x / k (k >= 1) into out as float64, Python's
- * correctly rounded int/int true division.                                                   */
+ * used by SecaggCrypter._apply_weighting / _apply_average, :233-276) on n integers v < 2^128 given as
+ * (lo, hi) uint64 pairs in x (device):
+ *   op 0: v * k (k < 2^64) into out as n x 3 uint64 words, the exact product (< 2^192); a negative
+ *         multiplier is the caller's sign on the result;
+ *   op 1: v / k (k >= 1) into out as float64, Python's correctly rounded int/int true division;
+ *   op 2: v / kd with kd the float64 whose bit pattern k holds: Python's int / float (float(v)
+ *         correctly rounded, then the IEEE division);
+ *   op 3: v / (-k) (k >= 1): op 1 negated.                                                       */
 int fbm_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, void* out, uint32_t* stats, void* stream);
 
 /* ---- additive secret sharing of vectors (reference fedbiomed/common/secagg/_additive_ss.py) ----
@@ -275,7 +280,11 @@ int fbm_jl_engine_for(uint64_t n_ct);
  * workspace: fbm_jl_batch_workspace() bytes of device memory.  No reference counterpart: the
  * reference encrypts one party per call (fedbiomed/common/secagg/_secagg_crypter.py:45-137). */
 int fbm_jl_batch_begin(void);
+/* fbm_jl_batch_abort: drops the open batch -- the recorded exponentiations never run, so the calls'
+ * outputs stay unwritten.  fbm_jl_batch_count: calls recorded in this thread's open batch (0 when
+ * none is open; a call that launched at once, e.g. on the generic engine, is not counted). */
 void fbm_jl_batch_abort(void);
+int fbm_jl_batch_count(void);
 uint64_t fbm_jl_batch_workspace(void);
 int fbm_jl_batch_flush(void* workspace, uint64_t workspace_bytes, void* stream);
 

@@ -30,4 +30,5 @@ def load(name):
 
 
 def load_all():
-    return {k: load(k + ".json") for k in ("quantize", "lom", "jl", "ass", "edge", "dh", "jls_api", "crypter_sweep", "even")}
+    return {k: load(k + ".json") for k in ("quantize", "lom", "jl", "ass", "edge", "dh", "jls_api", "crypter_sweep", "even",
+                                           "api_edges")}

@@ -1,0 +1,151 @@
+"""API-surface edges against the reference's own outcomes (tests/golden/api_edges.json,
+tools/gen_golden.py gen_api_edges): LOM.protect's overflow message through the LOM class
+(_lom.py:133-150), SecaggCrypter._apply_average / _apply_weighting (_secagg_crypter.py:233-276)
+with float, negative and wide divisors / weights (never truncated: utils.divide / multiply,
+_secagg_utils.py:122-149), JL rounds past 2^64 (any tau < 2^512 is one FDH message block,
+_jls.py:451-467, 742-760), and the object API's negative-round outcomes.  Argument-level outcomes
+run on the CPU; device arithmetic on the GPU."""
+
+import ast
+import logging
+
+import numpy as np
+import pytest
+
+from fedbiomed_amd import workload as W
+from tests.golden_util import F, I
+
+
+def _expect(outcome, fn):
+    if "error" in outcome:
+        with pytest.raises(Exception) as ei:
+            fn()
+        assert type(ei.value).__name__ == outcome["error"], (ei.value, outcome)
+        assert str(ei.value) == outcome["msg"]
+        return None
+    return fn()
+
+
+def _bits(xs):
+    return np.asarray(xs, dtype=np.float64).view(np.uint64).tolist()
+
+
+def _k(rep: str):
+    return float(rep) if rep in ("inf", "-inf", "nan") else ast.literal_eval(rep)
+
+
+# ------------------------------------------------------------------ CPU
+def test_lom_class_overflow_message(golden):
+    """The LOM class raises the reference's overflow-guard message word for word (its guard runs on
+    the host list before any device work)."""
+    from fedbiomed_amd.secagg._lom import LOM
+
+    for r in golden["api_edges"]["lom_overflow"]:
+        if "error" not in r["out"]:
+            continue
+        ids = W.node_ids(r["nodes"])
+        x = [I(v) for v in r["x"]]
+        _expect(r["out"], lambda ids=ids, x=x: LOM(b"0" * 16).protect(ids[0], W.pairwise_secrets_for(ids[0], ids), 1,
+                                                                        x, ids))
+
+
+def test_negative_round_object_api(golden):
+    """A negative round is FDH's OverflowError (int(t).to_bytes) in every object-API entry point,
+    and nothing at all for an empty list (the reference hashes no round then)."""
+    from fedbiomed_amd.secagg._jls import FDH, BaseKey, EncryptedNumber, JoyeLibert, ServerKey, UserKey
+    from tests.test_jls_api import pp_of
+
+    g = golden["api_edges"]["negative_round"]
+    pp = pp_of(123457)
+    _expect(g["user_encrypt"], lambda: UserKey(pp, 3).encrypt([1], -1))
+    assert _expect(g["user_encrypt_empty"], lambda: UserKey(pp, 3).encrypt([], -1)) == []
+    _expect(g["server_decrypt"], lambda: ServerKey(pp, -3).decrypt([EncryptedNumber(pp, 5)], -1))
+    assert _expect(g["server_decrypt_empty"], lambda: ServerKey(pp, -3).decrypt([], -1)) == []
+    _expect(g["protect"], lambda: JoyeLibert().protect(pp, UserKey(pp, 3), -1, [1, 2], 2))
+    assert _expect(g["protect_empty"], lambda: JoyeLibert().protect(pp, UserKey(pp, 3), -1, [], 2)) == []
+    _expect(g["fdh"], lambda: FDH(2048, 123457).H(-1))
+    assert _expect(g["populate_tau_empty"], lambda: BaseKey(pp, 3)._populate_tau(-1, 0)) == []
+
+
+def test_round_domain():
+    """Rounds up to 2^512 - 1 reach the C-ABI (16 limbs); 2^512 and above are FB624 (they OR into
+    the ciphertext index bits of t in the reference); a negative one is the reference's OverflowError."""
+    from fedbiomed_amd import _device as D
+    from fedbiomed_amd.exceptions import FedbiomedSecaggCrypterError
+
+    assert D._check_round(2**512 - 1).tolist() == [0xFFFFFFFF] * 16
+    assert D._check_round(2**64 + 5).tolist() == [5, 0, 1] + [0] * 13
+    with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
+        D._check_round(2**512)
+    with pytest.raises(OverflowError):
+        D._check_round(-1)
+
+
+def test_oracle_jl_rounds(golden):
+    """The oracle reproduces the reference at rounds past 2^64 (it pins the GPU test below)."""
+    from oracle import secagg_oracle as O
+
+    for r in golden["api_edges"]["jl_rounds"]:
+        tau = I(r["tau"])
+        keys = [I(k) for k in r["keys"]]
+        for x, e in zip(r["x"], r["enc"]):
+            assert O.jl_encrypt([F(v) for v in x], tau, keys[r["x"].index(x)], W.BIPRIME0, 2, weight=3) == [
+                I(c) for c in e]
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+def test_apply_average_edges(golden):
+    """_apply_average with int divisors of either sign (incl. -2^63 and 2^64 - 1), float divisors (2.5,
+    -2.5, 7.0, 1e-300, inf), zero (both ZeroDivisionErrors): the reference's floats bit for bit.  An
+    integer divisor of 2^64 or more is outside the device path (FB624)."""
+    from fedbiomed_amd.exceptions import FedbiomedSecaggCrypterError
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    g = golden["api_edges"]["apply_average"]
+    vals = [I(v) for v in g["vals"]]
+    for c in g["cases"]:
+        k = _k(c["k"])
+        if isinstance(k, int) and abs(k) >= 2**64:
+            with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
+                SecaggCrypter._apply_average(vals, k)
+            continue
+        got = _expect(c["out"], lambda k=k: SecaggCrypter._apply_average(vals, k))
+        if got is not None:
+            assert _bits(got) == _bits([F(v) for v in c["out"]["ok"]]), c["k"]
+
+
+@pytest.mark.gpu
+def test_apply_weighting_edges(golden):
+    """_apply_weighting with negative, zero and 64-bit weights and values up to 2^128 (target range
+    2^128): the reference's exact integers (products up to 2^192, negative for a negative weight)."""
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    g = golden["api_edges"]["apply_weighting"]
+    for c in g["cases"]:
+        vals = [I(v) for v in c["vals"]] if "vals" in c else g["vals"]
+        target = I(c["target"]) if "target" in c else None
+        fn = (lambda c=c, vals=vals, target=target: SecaggCrypter._apply_weighting(vals, c["w"], target)
+              if target else SecaggCrypter._apply_weighting(vals, c["w"]))
+        got = _expect(c["out"], fn)
+        if got is not None:
+            assert got == [I(v) for v in c["out"]["ok"]], c["w"]
+
+
+@pytest.mark.gpu
+def test_jl_rounds_past_2_64(golden, caplog):
+    """SecaggCrypter.encrypt / aggregate at rounds 2^64, 2^100 + 12345, 2^511 + 3 and 2^512 - 1: the
+    reference's ciphertexts and float64 outputs bit for bit (the round is FDH's last message block)."""
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    jc = SecaggCrypter()
+    for r in golden["api_edges"]["jl_rounds"]:
+        tau = I(r["tau"])
+        keys = [I(k) for k in r["keys"]]
+        with caplog.at_level(logging.WARNING):
+            encs = [jc.encrypt(num_nodes=2, current_round=tau, params=[F(v) for v in x], key=k, biprime=W.BIPRIME0,
+                               weight=3) for x, k in zip(r["x"], keys)]
+        assert encs == [[I(c) for c in e] for e in r["enc"]], r["tau"]
+        out = jc.aggregate(current_round=tau, num_nodes=2, params=encs, key=-sum(keys), biprime=W.BIPRIME0,
+                           total_sample_size=6, num_expected_params=40)
+        assert _bits(out) == _bits([F(v) for v in r["agg"]]), r["tau"]

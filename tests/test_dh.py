@@ -90,3 +90,28 @@ def test_bytearray_pem_input(dh):
         gc.collect()
         assert k.export_public_key() == pub
         assert DHKey(public_key_pem=bytearray(pub)).export_public_key() == pub
+
+
+def test_encrypted_private_pem_is_refused_without_prompting():
+    """An encrypted PKCS#8 PEM with no password: cryptography's load_pem_private_key(password=None)
+    raises TypeError (the reference's _import_key lets it through); OpenSSL must not fall back to
+    its terminal prompt (PEM_def_callback)."""
+    import ctypes
+
+    from fedbiomed_amd.secagg import _dh
+
+    lib = _dh._ssl()
+    lib.EVP_aes_256_cbc.restype = ctypes.c_void_p
+    k = DHKey()
+    bio = lib.BIO_new(lib.BIO_s_mem())
+    try:
+        assert lib.PEM_write_bio_PKCS8PrivateKey(bio, k.private_key._p, lib.EVP_aes_256_cbc(), b"pw", 2, None,
+                                                 None) == 1
+        buf = ctypes.c_void_p()
+        n = lib.BIO_ctrl(bio, 3, 0, ctypes.byref(buf))
+        pem = ctypes.string_at(buf, n)
+    finally:
+        lib.BIO_free(bio)
+    assert b"ENCRYPTED PRIVATE KEY" in pem
+    with pytest.raises(TypeError, match="Password was not given but private key is encrypted"):
+        DHKey(private_key_pem=pem)

@@ -282,3 +282,100 @@ def test_jl_party_per_rank_hip_gloo():
     assert res[0][1][0] == 0 and res[1][1][1] == N_JL_HIP and res[0][1][1] == res[1][1][0]
     for r in range(2):
         assert res[r][0].view(np.uint64).tolist() == np.asarray(ref, dtype=np.float64).view(np.uint64).tolist()
+
+
+# ---- the RCCL branches: a world-1 "nccl" group on cuda:0 (one GPU per box) -----------------
+def _collectives_world1_body():
+    """Every collective of distributed.py on device tensors (int64, float64, int32) plus the LOM
+    party-per-rank exchange with HIP compute, in a world-1 group of the spawning backend."""
+    from fedbiomed_amd import _device as D
+    from fedbiomed_amd.secagg import SecaggLomCrypter
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(7)
+    local = torch.randint(-2**62, 2**62, (1003,), dtype=torch.int64, generator=g).to(dev)
+    f64 = torch.randn(1003, dtype=torch.float64, generator=g).to(dev)
+    cts = torch.randint(-2**31, 2**31 - 1, (2, 37, 64), dtype=torch.int32, generator=g).to(dev)
+    out = {
+        "reduce_scatter_u64": Dd.reduce_scatter_u64(local, 1003).cpu(),
+        "all_gather_stripes": Dd.all_gather_stripes(f64, 1003, 8).cpu(),
+        "all_gather_shards_f64": Dd.all_gather_shards(f64, 1003, 30).cpu(),
+        "all_gather_shards_i32": Dd.all_gather_shards(cts[0, :, 0].contiguous(), 37, 1).cpu(),
+    }
+    stripe, k0 = Dd.all_to_all_ciphertexts(cts, 2)
+    out["all_to_all_ciphertexts"] = stripe.cpu()
+    out["k0"] = k0
+    out["inputs"] = (local.cpu(), f64.cpu(), cts.cpu())
+    # the LOM party-per-rank leg: HIP protect -> HIP u64 column sum -> reduce-scatter -> HIP average
+    ids = W.node_ids(P)
+    lc = SecaggLomCrypter(W.LOM_NONCE)
+    Y = torch.stack([lc.encrypt_tensor(TAU, ids[p], torch.from_numpy(W.party_params(p, N_LOM)).to(dev),
+                                       W.pairwise_secrets_for(ids[p], ids), ids, weight=W.party_weight(p))
+                     for p in range(P)])
+    _, sums = D.lom_aggregate(Y, 1, want_out=False, want_sums=True)
+    red = Dd.reduce_scatter_u64(sums, N_LOM)
+    agg = lc.aggregate_tensor(red.view(1, -1), sum(W.party_weight(p) for p in range(P)))
+    out["lom_pp"] = Dd.all_gather_stripes(agg, N_LOM, 8).cpu()
+    torch.cuda.synchronize()
+    # numpy, not tensors: torch's queue shares tensors through file descriptors that die with
+    # the child process
+    return {k: (tuple(t.numpy() for t in v) if isinstance(v, tuple) else v.numpy() if isinstance(v, torch.Tensor)
+                else v) for k, v in out.items()}
+
+
+def _world1_worker(backend, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group(backend, rank=0, world_size=1)
+        try:
+            q.put((dist.get_backend(), _collectives_world1_body()))
+        finally:
+            dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        q.put((backend, e))
+
+
+def _run_world1(backend):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_world1_worker, args=(backend, _free_port(), q))
+    p.start()
+    got_backend, res = q.get(timeout=240)
+    p.join(timeout=60)
+    if isinstance(res, Exception):
+        raise res
+    assert got_backend == backend
+    return res
+
+
+@pytest.mark.gpu
+def test_rccl_collectives_world1():
+    """The "nccl" (= RCCL) branches of distributed.py -- reduce_scatter_tensor, all_gather_into_tensor,
+    all_to_all_single -- run once on the GPU (a world-1 group in a fresh spawned process, before any
+    GPU call), equal to the gloo branches on the same inputs and to the collectives' meaning at world
+    size 1; the LOM party-per-rank exchange with HIP compute through them equals the oracle
+    (reference LOM.aggregate, _lom.py:177-192)."""
+    nccl, gloo = _run_world1("nccl"), _run_world1("gloo")
+
+    def same(a, b):
+        return a.dtype == b.dtype and a.shape == b.shape and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+    for k in ("reduce_scatter_u64", "all_gather_stripes", "all_gather_shards_f64", "all_gather_shards_i32",
+              "all_to_all_ciphertexts", "lom_pp"):
+        assert same(nccl[k], gloo[k]), k
+    local, f64, cts = nccl["inputs"]
+    assert same(nccl["reduce_scatter_u64"], local)
+    assert same(nccl["all_gather_stripes"], f64) and same(nccl["all_gather_shards_f64"], f64)
+    assert same(nccl["all_gather_shards_i32"], np.ascontiguousarray(cts[0, :, 0]))
+    assert nccl["k0"] == 0 and same(nccl["all_to_all_ciphertexts"], cts)
+    ids = W.node_ids(P)
+    nonce = O.lom_nonce(W.LOM_NONCE)
+    ys = [O.lom_encrypt(W.party_params(p, N_LOM).astype(np.float64), TAU, ids[p], W.pairwise_secrets_for(ids[p], ids),
+                        ids, nonce, weight=W.party_weight(p)) for p in range(P)]
+    ref = O.lom_crypter_aggregate(ys, sum(W.party_weight(p) for p in range(P)))
+    assert nccl["lom_pp"].view(np.uint64).tolist() == np.asarray(ref, np.float64).view(np.uint64).tolist()

@@ -141,3 +141,40 @@ def test_batch_random_moduli(bits):
     got = D.limbs_to_ints(f[[0, 49]].cpu().numpy())
     for g, k in zip(got, (4, 53)):
         assert g == O.powmod(O.fdh((k << 512) | tau, n2), sk0, n2)
+
+
+@pytest.mark.gpu
+def test_batch_abort_invalidates_recorded_calls():
+    """An exception inside jl_exp_batch drops the batch: the recorded exponentiations never run, so
+    finish() on their Pending objects raises afterwards instead of handing out unwritten memory.
+    Calls that launched at once inside the block (a negative-key encrypt, an even biprime on the
+    generic engine) were not recorded and stay valid."""
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    dev = D.device()
+    P, tau, n = 3, 1, 1_000
+    keys = [W.jl_user_key(p) for p in range(P)]
+    keys[1] = -keys[1]
+    ws = [W.party_weight(p) for p in range(P)]
+    xs = [torch.from_numpy(W.party_params(p, n)).to(dev) for p in range(P)]
+    jc = SecaggCrypter()
+    ref = [jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=ws[p]) for p in range(P)]
+    even = 1156
+    ref_even = jc.encrypt_tensor(P, tau, xs[2], keys[2], even, weight=ws[2])
+    pend = _pend_all(jc, xs, keys, ws, P, tau)
+    pe = jc.encrypt_tensor(P, tau, xs[2], keys[2], even, weight=ws[2], defer_exp=True)
+    pf = jc.decrypt_factor_tensor(tau, 100, -sum(keys), W.BIPRIME0, phased=True)
+    with pytest.raises(KeyError):
+        with D.jl_exp_batch(dev):
+            out = [pend[p].finish() for p in range(P)]
+            out_even = pe.finish()
+            pf.exponentiate()
+            raise KeyError("caller error inside the batch")
+    for p in (0, 2):
+        with pytest.raises(RuntimeError, match="aborted"):
+            pend[p].finish()
+    with pytest.raises(RuntimeError, match="aborted"):
+        pf.finish()
+    torch.cuda.synchronize()
+    assert torch.equal(pend[1].finish(), ref[1]) and torch.equal(out[1], ref[1])  # negative key: ran inline
+    assert torch.equal(pe.finish(), ref_even) and torch.equal(out_even, ref_even)  # generic engine: ran inline

@@ -127,7 +127,7 @@ def test_domain_restrictions_raise_fb624():
     with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
         UserKey(pp_of(1), 3).encrypt([1], 1)  # N = 1 (every N >= 2 is in the domain, even ones included)
     with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
-        UserKey(pp, 3).encrypt([1], 2**64)  # tau beyond the device's 64 bits
+        UserKey(pp, 3).encrypt([1], 2**512)  # tau beyond one FDH message block (the device takes < 2^512)
     with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
         FDH(2048, 123457).H(1 << 600)  # t not of the (k << 512) | tau form
     with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):

@@ -602,6 +602,66 @@ def gen_even(R):
     dump("even.json", out)
 
 
+def gen_api_edges(R):
+    """Edges of the API surface round 3 lifted or pinned (api_edges.json): LOM.protect's overflow
+    message through the LOM class, _apply_average / _apply_weighting with float / negative / wide
+    divisors and weights, JL rounds past 2^64 (the reference takes any tau below 2^512 as one FDH
+    block), and the object API's negative-round outcomes (OverflowError from FDH's to_bytes, none
+    for an empty list)."""
+    jls, lom = R.jls, R.lom
+    Crypter = R.crypter.SecaggCrypter
+    mpz = sys.modules["gmpy2"].mpz
+    out = {}
+    ids5 = W.node_ids(5)
+    rows = []
+    for nodes, bits in [(1, 63), (1, 64), (2, 63), (3, 62), (5, 61), (5, 62), (16, 60), (17, 59)]:
+        ids = W.node_ids(nodes)
+        x = [1, 2 ** (bits - 1) + 5, 7]
+        rows.append({"nodes": nodes, "bits": bits, "x": [ihex(v) for v in x], "out": _outcome(lambda ids=ids, x=x: [
+            ihex(v) for v in lom.LOM(b"0" * 16).protect(ids[0], W.pairwise_secrets_for(ids[0], ids), 1, x, ids)])})
+    out["lom_overflow"] = rows
+    del ids5
+    avg = []
+    vals = [0, 1, 5, 2 ** 53 + 1, 2 ** 64 + 3, 2 ** 127 - 1, 10 ** 30 + 7]
+    for k in [2, 7, 2.5, -3, -2.5, 7.0, 1e-300, float("inf"), 2 ** 64 - 1, -(2 ** 63), 0, 0.0, 3 ** 50]:
+        avg.append({"k": repr(k), "out": _outcome(lambda k=k: [fhex(v) for v in Crypter._apply_average(vals, k)])})
+    out["apply_average"] = {"vals": [ihex(v) for v in vals], "cases": avg}
+    wts = []
+    wvals = [0, 1, 8191, 4096]
+    for w in [2, -3, 0, -(2 ** 17 - 1), 2 ** 63 + 5, -(2 ** 64 - 1)]:
+        wts.append({"w": w, "out": _outcome(lambda w=w: [ihex(v) for v in Crypter._apply_weighting(wvals, w)])})
+    big = [2 ** 100 + 3, 2 ** 127 + 1]
+    wts.append({"w": 2 ** 60 + 7, "target": ihex(2 ** 128), "vals": [ihex(v) for v in big],
+                "out": _outcome(lambda: [ihex(v) for v in Crypter._apply_weighting(big, 2 ** 60 + 7, 2 ** 128)])})
+    out["apply_weighting"] = {"vals": wvals, "cases": wts}
+    rounds = []
+    cr = Crypter()
+    bp = W.BIPRIME0
+    for tau in [2 ** 64, 2 ** 100 + 12345, 2 ** 511 + 3, 2 ** 512 - 1]:
+        keys = [W.jl_user_key(p) for p in range(2)]
+        xs = [[float(v) for v in W.party_params(p, 40)] for p in range(2)]
+        enc = [[ihex(c) for c in cr.encrypt(num_nodes=2, current_round=tau, params=x, key=k, biprime=bp, weight=3)]
+               for x, k in zip(xs, keys)]
+        agg = cr.aggregate(current_round=tau, num_nodes=2, params=[[int(c, 16) for c in e] for e in enc],
+                           key=-sum(keys), biprime=bp, total_sample_size=6, num_expected_params=40)
+        rounds.append({"tau": ihex(tau), "keys": [ihex(k) for k in keys], "x": [[fhex(v) for v in x] for x in xs],
+                       "enc": enc, "agg": [fhex(v) for v in agg]})
+    out["jl_rounds"] = rounds
+    pp = jls.PublicParam(mpz(123457), 1024, jls.FDH(2048, mpz(123457) * mpz(123457)).H)
+    jl = jls.JoyeLibert()
+    out["negative_round"] = {
+        "user_encrypt": _outcome(lambda: jls.UserKey(pp, 3).encrypt([mpz(1)], -1)),
+        "user_encrypt_empty": _outcome(lambda: jls.UserKey(pp, 3).encrypt([], -1)),
+        "server_decrypt": _outcome(lambda: jls.ServerKey(pp, -3).decrypt([jls.EncryptedNumber(pp, mpz(5))], -1)),
+        "server_decrypt_empty": _outcome(lambda: jls.ServerKey(pp, -3).decrypt([], -1)),
+        "protect": _outcome(lambda: jl.protect(pp, jls.UserKey(pp, 3), -1, [1, 2], 2)),
+        "protect_empty": _outcome(lambda: jl.protect(pp, jls.UserKey(pp, 3), -1, [], 2)),
+        "fdh": _outcome(lambda: int(jls.FDH(2048, mpz(123457)).H(-1))),
+        "populate_tau_empty": _outcome(lambda: jls.BaseKey(pp, 3)._populate_tau(-1, 0)),
+    }
+    dump("api_edges.json", out)
+
+
 def I(s):  # noqa: E743 - hex string -> int (the fixtures' encoding)
     return int(s, 16)
 
@@ -617,6 +677,9 @@ def main():
     if sys.argv[1:] == ["even"]:
         gen_even(R)
         return
+    if sys.argv[1:] == ["api_edges"]:
+        gen_api_edges(R)
+        return
     gen_quantize(R)
     gen_lom(R)
     gen_jl(R)
@@ -626,6 +689,7 @@ def main():
     gen_jls_api(R)
     gen_crypter_sweep(R)
     gen_even(R)
+    gen_api_edges(R)
     meta = {"generator": "tools/gen_golden.py", "reference": load_reference.REF,
             "note": "outputs of the reference Fed-BioMed crypter (Python), imported via tools/refshim"}
     dump("meta.json", meta)
