@@ -780,7 +780,7 @@ def jl_aggregate(cts: torch.Tensor, biprime: int, key: int, tau: int, n_expected
     if total_weight < 0 or total_weight > U64_MAX:
         raise FedbiomedSecaggCrypterError(
             f"{ErrorNumbers.FB624.value}: total_sample_size must be in [1, 2^64) for the device path")
-    tl = _check_round(tau)
+    tl = _check_round(tau) if factor is None else None  # a given factor fixes the round already
     out = torch.empty(n_out, dtype=torch.float64, device=dev) if want_out else None
     sums = torch.empty((n_out, 2), dtype=torch.int64, device=dev) if want_sums else None
     if n_ct == 0:
@@ -980,6 +980,53 @@ def jl_decrypt(cts: torch.Tensor, biprime: int, key: int, tau: int, ct_offset: i
     st = _stats(dev)
     _call(lib.fbm_jl_decrypt, _ptr(cts.contiguous()), P, n_ct, _np_ptr(bp), _np_ptr(kl), kneg, _np_ptr(tl),
           int(ct_offset), _ptr(x), _ptr(ws), _ptr(st), _stream())
+    _check_stats(st)
+    return x
+
+
+def jl_powmod(h: torch.Tensor, biprime: int, key: int, pt: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Caller-given bases (the hashes of a PublicParam whose hashing function is not FBM's FDH):
+    (N pt[k] + 1) h[k]^key mod N^2 with pt (int32 [n_ct, 32] plaintext limbs, UserKey.encrypt), or
+    h[k]^key mod N^2 without (ServerKey.decrypt's powmod), as int32 [n_ct, 64] limbs; h: int32 [n_ct, 64]
+    limbs (< 2^2048).  A negative key inverts first: a base without an inverse is ZeroDivisionError."""
+    n_ct = h.shape[0]
+    dev = h.device
+    out = torch.empty((n_ct, 64), dtype=torch.int32, device=dev)
+    if n_ct == 0:
+        return out
+    lib = N.load()
+    bp = _biprime_limbs(biprime)
+    kl, kneg = _key_limbs(key)
+    h = h.contiguous()
+    pt = pt.contiguous() if pt is not None else None
+    chunk = jl_chunk_ct()
+    ws = torch.empty(int(lib.fbm_jl_encrypt_workspace(min(n_ct, chunk))), dtype=torch.uint8, device=dev)
+    for k0 in range(0, n_ct, chunk):
+        k1 = min(n_ct, k0 + chunk)
+        st = _stats(dev)
+        _call(lib.fbm_jl_powmod, _ptr(h[k0:k1]), _ptr(pt[k0:k1] if pt is not None else None), k1 - k0, _np_ptr(bp),
+              _np_ptr(kl), kneg, _ptr(out[k0:k1]), _ptr(ws), _ptr(st), _stream())
+        _check_stats(st)
+    return out
+
+
+def jl_decrypt_with(cts: torch.Tensor, biprime: int, factor: torch.Tensor) -> torch.Tensor:
+    """ServerKey.decrypt's x = ((prod_u cts[u] * factor mod N^2) - 1) // N mod N for a jl_powmod factor:
+    int32 [P, n_ct, 64] ciphertext limbs -> int32 [n_ct, 32]."""
+    P, n_ct, _ = cts.shape
+    dev = cts.device
+    x = torch.empty((n_ct, 32), dtype=torch.int32, device=dev)
+    if n_ct == 0:
+        return x
+    factor = factor.contiguous()
+    if factor.dtype != torch.int32 or tuple(factor.shape) != (n_ct, 64) or factor.device != dev:
+        raise ValueError("factor must be the int32 [n_ct, 64] jl_powmod power of these ciphertexts' bases")
+    lib = N.load()
+    bp = _biprime_limbs(biprime)
+    ws = torch.empty(int(lib.fbm_jl_aggregate_workspace(n_ct)), dtype=torch.uint8, device=dev)
+    st = _stats(dev)
+    _call(lib.fbm_jl_decrypt_with, _ptr(cts.contiguous()), P, n_ct, _np_ptr(bp), _ptr(factor), _ptr(x), _ptr(ws),
+          _ptr(st), _stream())
     _check_stats(st)
     return x
 

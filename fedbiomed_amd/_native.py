@@ -86,6 +86,8 @@ SIGNATURES = {
     "fbm_jl_fdh": (c_int, [c_u64, c_vp, c_int, c_vp, c_u64, c_vp, c_vp, c_vp]),
     "fbm_jl_product": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_decrypt": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp, c_int, c_vp, c_u64, c_vp, c_vp, c_vp, c_vp]),
+    "fbm_jl_powmod": (c_int, [c_vp, c_vp, c_u64, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "fbm_jl_decrypt_with": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fbm_int_ops": (c_int, [c_vp, c_u64, c_u64, c_int, c_vp, c_vp, c_vp]),
     "fbm_ass_split": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_vp, c_vp, c_u64, c_vp, c_vp]),
     "fbm_ass_reconstruct": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp]),

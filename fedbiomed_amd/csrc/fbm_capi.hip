@@ -1352,6 +1352,84 @@ int fbm_jl_decrypt(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint
   return jl_combine_impl(cts, n_parties, n_ct, 1, 1, 0, biprime, w.F, 1, 0.0, 1.0, nullptr, nullptr, w, stats, s, x);
 }
 
+// out[k] = nude_k * h[k]^key mod N^2 for caller-given bases (a PublicParam whose hashing function
+// is not FBM's FDH): the encrypt's exponentiation without its FDH (nude = N pt + 1), or with
+// pt == NULL the decryption factor's (the power alone).  Workspace: the encrypt's layout.
+int fbm_jl_powmod(const uint32_t* h, const uint32_t* pt, uint64_t n_ct, const uint32_t* biprime, const uint32_t* key,
+                  int key_negative, uint32_t* out, void* workspace, uint32_t* stats, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc = zero_stats(stats, s);
+  if (rc) return rc;
+  if ((rc = jl_agg_checks(1, n_ct, biprime, 1))) return rc;
+  if (!key) {
+    set_error("null key");
+    return FBM_E_ARG;
+  }
+  if (n_ct == 0) return FBM_OK;
+  if (!h || !out || !workspace) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  uint8_t* ws = (uint8_t*)workspace;  // fbm_jl_encrypt_workspace: ops | cst | pt | nude | H | table | H^-1 | y
+  uint32_t* ops = (uint32_t*)ws;
+  uint64_t off = align256(FBM_MAX_OPS * 4);
+  uint32_t* cst = (uint32_t*)(ws + off);
+  off += align256(FBM_CST_WORDS * 4) + align256(n_ct * 32 * 4);
+  uint32_t* nude = (uint32_t*)(ws + off);
+  off += align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4) + align256(n_ct * 64 * 4);
+  uint32_t* table = (uint32_t*)(ws + off);
+  off += align256(jl_table_bytes(n_ct));
+  uint32_t* Hinv = (uint32_t*)(ws + off);
+  off += align256(n_ct * 64 * 4);
+  uint32_t* Y = (uint32_t*)(ws + off);
+  if (jl_generic(biprime)) {
+    GenCtx g;
+    if ((rc = build_gen_ctx(biprime, key, key_negative, g)) || (rc = launch_jl_gen_setup(g, cst, s))) return rc;
+    return timed("jl_gen_exp", s, [&] { return launch_jl_gen_exp(h, pt, 0, n_ct, cst, out, stats, s); });
+  }
+  JlParams jp;
+  if ((rc = build_jl_params(biprime, 1, 1, nullptr, 0, jp))) return rc;
+  JlSched sc;
+  int is_zero = 0;
+  if ((rc = build_schedule(key, sc, is_zero))) {
+    set_error("exponent schedule overflow");
+    return rc;
+  }
+  jp.key_is_zero = is_zero;
+  const uint64_t slots = table_slots_for(n_ct);
+  if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s); }))) return rc;
+  const int mode = pt ? 0 : FBM_EXP_DEC;
+  if (pt && (rc = timed("jl_nude", s, [&] { return launch_jl_nude(pt, n_ct, jp, 0, nude, s); }))) return rc;
+  if (key_negative && !is_zero) {  // powmod with a negative exponent: (h^|key|)^-1, then * nude
+    if ((rc = timed("jl_exp", s, [&] {
+           return launch_jl_exp(h, n_ct, jp, sc, FBM_EXP_DEC | FBM_EXP_OUT_NADIC, nullptr, table, slots, ops, cst, Hinv,
+                                s);
+         })))
+      return rc;
+    return timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, cst, Hinv, Y, pt ? nude : nullptr, out, stats, s); });
+  }
+  return timed("jl_exp", s, [&] {
+    return launch_jl_exp(h, n_ct, jp, sc, mode, pt ? nude : nullptr, table, slots, ops, cst, out, s);
+  });
+}
+
+// ServerKey.decrypt's last step with a caller-computed factor (fbm_jl_powmod, pt == NULL):
+// x = ((prod_u cts[u] * factor mod N^2) - 1) // N mod N
+int fbm_jl_decrypt_with(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* biprime,
+                        const uint32_t* factor, uint32_t* x, void* workspace, uint32_t* stats, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc = zero_stats(stats, s);
+  if (rc) return rc;
+  if ((rc = jl_agg_checks(n_parties, n_ct, biprime, 1))) return rc;
+  if (n_ct == 0) return FBM_OK;
+  if (!cts || !factor || !x || !workspace) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  return jl_combine_impl(cts, n_parties, n_ct, 1, 1, 0, biprime, factor, 1, 0.0, 1.0, nullptr, nullptr,
+                         agg_ws(workspace, n_ct), stats, s, x);
+}
+
 int fbm_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, void* out, uint32_t* stats, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   int rc = zero_stats(stats, s);

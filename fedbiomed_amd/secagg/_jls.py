@@ -16,10 +16,14 @@ A sum of EncryptedNumbers keeps its operands until its ciphertext is read (then 
 product), so `[sum(ep) for ep in zip(*parties)]` followed by ServerKey.decrypt is one device
 call, as JoyeLibert.aggregate is.
 
+A PublicParam whose hashing function is anything but FDH(2048, N^2).H with bits = 1024 (what
+SecaggCrypter._setup_public_param builds) has its hashes computed as the reference computes them --
+the callable per t on the host (one fbm_jl_fdh launch for an FDH of bits_size 2048 against another
+modulus) -- and the exponentiations on the device (fbm_jl_powmod / fbm_jl_decrypt_with).
+
 Domain of the device path (FB624 outside it): 2 <= N < 2^1024 (an even N
-runs on the generic engine, fedbiomed_amd/csrc/fbm_gen.hip, an odd one on the Montgomery engines); a
-PublicParam with bits = 1024 whose hashing function is FDH(2048, N^2).H (what
-SecaggCrypter._setup_public_param builds); tau in [0, 2^512); VES values in [0, 2^128) with
+runs on the generic engine, fedbiomed_amd/csrc/fbm_gen.hip, an odd one on the Montgomery engines);
+FDH of bits_size 2048; tau in [0, 2^512) where FDH hashes it; VES values in [0, 2^128) with
 es <= 100; ServerKey.decrypt with delta^2 = 1 (mod N).  Integers are Python ints (gmpy2 is
 not a dependency): where the reference returns gmpy2.mpz this returns int, and FDH takes an
 int modulus.
@@ -123,17 +127,29 @@ class PublicParam:
         return "<PublicParam (N={}...{}, H(x)={})>".format(n_str[:5], n_str[-5:], hashcode[:10])
 
 
-def _device_n(pp: PublicParam) -> int:
-    """N of a PublicParam the device path can encrypt/decrypt under (its FDH, bits 1024)."""
+def _fdh_standard(pp: PublicParam) -> bool:
+    """Is pp's hashing function FDH(2048, N^2).H with bits 1024 (SecaggCrypter._setup_public_param's)?
+    Then the fused entry points hash on the device inside the encrypt / decrypt call."""
     fdh = getattr(pp._hashing_function, "__self__", None)
-    n = int(pp.n_modulus)
-    if not (isinstance(fdh, FDH) and getattr(pp._hashing_function, "__func__", None) is FDH.H
-            and fdh.bits_size == SAParameters.KEY_SIZE and int(fdh._n_modules) == n * n
-            and pp.bits == _TAU_SHIFT_BITS):
-        raise _unsupported("a PublicParam whose hashing function is not FDH(2048, N^2).H with bits 1024")
-    if n < 2 or n.bit_length() > 1024:
-        raise _unsupported("a modulus N outside [2, 2^1024)")
-    return n
+    return (isinstance(fdh, FDH) and getattr(pp._hashing_function, "__func__", None) is FDH.H
+            and fdh.bits_size == SAParameters.KEY_SIZE and _is_integer(fdh._n_modules)
+            and int(fdh._n_modules) == int(pp.n_modulus) ** 2 and pp.bits == _TAU_SHIFT_BITS)
+
+
+def _check_hash_domain(pp: PublicParam) -> None:
+    """FDH hashes on the device at bits_size 2048 only (FB624 before any device work otherwise)."""
+    fdh = getattr(pp._hashing_function, "__self__", None)
+    if (isinstance(fdh, FDH) and getattr(pp._hashing_function, "__func__", None) is FDH.H
+            and fdh.bits_size != SAParameters.KEY_SIZE):
+        raise _unsupported(f"FDH of bits_size {fdh.bits_size} (device path: {SAParameters.KEY_SIZE})")
+
+
+def _bases(key: "BaseKey", tau, len_: int, n: int) -> torch.Tensor:
+    """Any other hashing function: BaseKey._populate_tau's values (the callable per t on the host, as
+    the reference calls it, or one fbm_jl_fdh launch for an FDH of another modulus) as device limbs of
+    the powmod bases; a base outside [0, 2^2048) is reduced mod N^2 (gmpy2.powmod reduces its base)."""
+    vals = [operator.index(h) for h in key._populate_tau(tau, len_)]  # a non-integer: TypeError
+    return torch.from_numpy(D.ints_to_limbs(vals, n * n).view(np.int32)).to(D.device())
 
 
 def _check_tau(tau) -> int:
@@ -290,7 +306,12 @@ class UserKey(BaseKey):
             raise TypeError(f"Expected plaintext type list but got {type(plaintext)}")
         if not plaintext:  # the reference hashes no round for an empty list
             return []
-        n = _device_n(self._public_param)
+        n = _modulus_of(self._public_param)
+        if not _fdh_standard(self._public_param):  # the caller's hashing function, then fbm_jl_powmod
+            _check_hash_domain(self._public_param)
+            pts = D.ints_to_pt(plaintext, n)
+            ct = D.jl_powmod(_bases(self, tau, len(plaintext), n), n, self._key, pts)
+            return D.limbs_to_ints(D.to_host(ct).numpy())
         tau = _check_tau(tau)
         pts = D.ints_to_pt(plaintext, n)
         ct = D.jl_encrypt(pts, n, self._key, tau, 1, kind="pt")
@@ -310,7 +331,7 @@ class ServerKey(BaseKey):
             raise TypeError(f"Expected `cipher` is list of encrypter numbers but got {type(cipher)}")
         if not all([isinstance(c, EncryptedNumber) for c in cipher]):
             raise TypeError("Cipher text should be list of EncryptedNumbers")
-        n = _device_n(self._public_param)
+        n = _modulus_of(self._public_param)
         d2 = delta ** 2
         if math.gcd(d2 % (n * n), n * n) != 1:  # invert(delta^2, N^2) runs even on an empty list
             raise ZeroDivisionError("invert() no inverse exists")
@@ -318,6 +339,11 @@ class ServerKey(BaseKey):
             return []
         if d2 % n != 1:
             raise _unsupported("ServerKey.decrypt with delta^2 != 1 (mod N)")
+        if not _fdh_standard(self._public_param):  # fbm_jl_powmod's factor, then fbm_jl_decrypt_with
+            _check_hash_domain(self._public_param)
+            rows = _term_rows(cipher, n)
+            factor = D.jl_powmod(_bases(self, tau, len(cipher), n), n, d2 * self._key)
+            return D.limbs_to_ints_w(D.jl_decrypt_with(rows, n, factor), 32)
         tau = _check_tau(tau)
         x = D.jl_decrypt(_term_rows(cipher, n), n, d2 * self._key, tau)
         return D.limbs_to_ints_w(x, 32)
@@ -351,7 +377,12 @@ class JoyeLibert:
         es, cr = self._vector_encoder._slot(n_users)
         if not x_u_tau:
             return []
-        n = _device_n(user_key.public_param)
+        n = _modulus_of(user_key.public_param)
+        if not _fdh_standard(user_key.public_param):  # VES on the device, the caller's hashes, fbm_jl_powmod
+            _check_hash_domain(user_key.public_param)
+            pt = D.jl_pack(D.ints_to_u128(x_u_tau), es, cr)
+            ct = D.jl_powmod(_bases(user_key, tau, pt.shape[0], n), n, user_key.key, pt)
+            return D.limbs_to_ints(D.to_host(ct).numpy())
         tau = _check_tau(tau)
         ct = D.jl_encrypt(D.ints_to_u128(x_u_tau), n, user_key.key, tau, n_users, slot=(es, cr), kind="u128")
         return D.limbs_to_ints(D.to_host(ct).numpy())
@@ -373,13 +404,19 @@ class JoyeLibert:
             raise TypeError("Cipher text should be list of EncryptedNumbers")
         if not summed:
             return []
-        n = _device_n(sk_0.public_param)
-        tau = _check_tau(tau)
+        n = _modulus_of(sk_0.public_param)
+        standard = _fdh_standard(sk_0.public_param)
+        if standard:
+            tau = _check_tau(tau)
+        else:
+            _check_hash_domain(sk_0.public_param)
         es, cr = self._vector_encoder._slot(n_user)
         if es > 128:
             raise _unsupported(f"VES decode of {es}-bit slots")
-        _, sums = D.jl_aggregate(_term_rows(summed, n), n, sk_0.key, tau, num_expected_params, 1,
-                                 want_out=False, want_sums=True, slot=(es, cr))
+        rows = _term_rows(summed, n)
+        factor = None if standard else D.jl_powmod(_bases(sk_0, tau, len(summed), n), n, sk_0.key)
+        _, sums = D.jl_aggregate(rows, n, sk_0.key, tau, num_expected_params, 1, want_out=False, want_sums=True,
+                                 slot=(es, cr), factor=factor)
         return D.u128_to_ints(sums)
 
 

@@ -202,6 +202,20 @@ int fbm_jl_decrypt(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint
                    int key_negative, const uint32_t* tau, uint64_t ct_offset, uint32_t* x, void* workspace, uint32_t* stats,
                    void* stream);
 
+/* Keys whose PublicParam hashes with a callable other than FBM's FDH(2048, N^2).H (BaseKey._populate_tau,
+ * _jls.py:451-467, calls it per t on the host; the exponentiations stay on the device):
+ * fbm_jl_powmod: out[k] = (N*pt[k] + 1) * h[k]^key mod N^2 (UserKey.encrypt, _jls.py:473-505), or with
+ *   pt == NULL out[k] = h[k]^key mod N^2 (ServerKey.decrypt's powmod, :541-543).  h: device, n_ct x 64
+ *   limbs (< 2^2048); pt: device, n_ct x 32 limbs (< 2^1024) or NULL; a negative key inverts first (a base
+ *   with no inverse is FBM_E_INVERSE at fbm_check_stats); workspace fbm_jl_encrypt_workspace(n_ct).
+ * fbm_jl_decrypt_with: x[k] = ((prod_u cts[u][k] * factor[k] mod N^2) - 1) // N mod N (:545-546) for a
+ *   factor from fbm_jl_powmod (pt == NULL); n_ct x 32 limbs; workspace fbm_jl_aggregate_workspace(n_ct).
+ *   (JoyeLibert.aggregate's VES decode on such a factor: fbm_jl_aggregate_factor.)                      */
+int fbm_jl_powmod(const uint32_t* h, const uint32_t* pt, uint64_t n_ct, const uint32_t* biprime, const uint32_t* key,
+                  int key_negative, uint32_t* out, void* workspace, uint32_t* stats, void* stream);
+int fbm_jl_decrypt_with(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* biprime,
+                        const uint32_t* factor, uint32_t* x, void* workspace, uint32_t* stats, void* stream);
+
 /* multiply / divide of the reference's secagg utils (fedbiomed/common/utils/_secagg_utils.py:122-149,
  * used by SecaggCrypter._apply_weighting / _apply_average, :233-276) on n integers v < 2^128 given as
  * (lo, hi) uint64 pairs in x (device):

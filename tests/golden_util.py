@@ -31,4 +31,23 @@ def load(name):
 
 def load_all():
     return {k: load(k + ".json") for k in ("quantize", "lom", "jl", "ass", "edge", "dh", "jls_api", "crypter_sweep", "even",
-                                           "api_edges")}
+                                           "api_edges", "custom_hash")}
+
+
+def custom_hashes():
+    """Hashing functions other than FBM's FDH(2048, N^2).H, the same callables for the reference run
+    that made tests/golden/custom_hash.json (tools/gen_golden.py gen_custom_hash) and for the tests:
+    a small affine map, one past 2^2048 (reduced mod N^2 by powmod), a negative one, a SHA-256 based
+    2048-bit one and the constant 1 (powmod's shortcut)."""
+    import hashlib
+
+    def sha(t):
+        return int.from_bytes(hashlib.sha256(int(t).to_bytes(128, "big")).digest() * 8, "big")
+
+    return {
+        "affine": lambda t: 5 * int(t) + 3,
+        "wide": lambda t: (int(t) * 0x9E3779B97F4A7C15 + 1) ** 4 + 11,
+        "negative": lambda t: -(int(t) + 2),
+        "sha": sha,
+        "one": lambda t: 1,
+    }

@@ -122,8 +122,8 @@ def test_encrypted_number_sums_are_lazy():
 
 def test_domain_restrictions_raise_fb624():
     pp = pp_of(123457)
-    with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):  # not the FDH of SecaggCrypter's PublicParam
-        UserKey(PublicParam(123457, 1024, lambda t: 5), 3).encrypt([1], 1)
+    with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):  # FDH hashes on the device at 2048 bits only
+        UserKey(PublicParam(123457, 1024, FDH(1024, 123457 ** 2).H), 3).encrypt([1], 1)
     with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
         UserKey(pp_of(1), 3).encrypt([1], 1)  # N = 1 (every N >= 2 is in the domain, even ones included)
     with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):

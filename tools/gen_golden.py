@@ -662,6 +662,53 @@ def gen_api_edges(R):
     dump("api_edges.json", out)
 
 
+def gen_custom_hash(R):
+    """The JoyeLibert object API under PublicParams whose hashing function is not FDH(2048, N^2).H
+    (custom_hash.json): UserKey.encrypt, ServerKey.decrypt of two users' sums and JoyeLibert.protect /
+    aggregate for the callables of tests/golden_util.custom_hashes() and an FDH against N instead of
+    N^2, over an odd biprime (the reference test's P * Q), a small odd and an even modulus, rounds
+    inside and outside FDH's [0, 2^512) (a callable takes any t), positive and negative keys."""
+    from tests.golden_util import custom_hashes
+    from tests.test_jls_api import P_REF, Q_REF
+
+    jls = R.jls
+    mpz = sys.modules["gmpy2"].mpz
+    hashes = custom_hashes()
+    rng = random.Random(20261017)
+    cases = []
+    for n, hnames in [(P_REF * Q_REF, list(hashes) + ["fdh_n"]), (123457, ["affine", "wide", "sha", "fdh_n"]),
+                      (1156, ["affine", "one"])]:
+        for hn in hnames:
+            hf = jls.FDH(2048, mpz(n)).H if hn == "fdh_n" else hashes[hn]
+            pp = jls.PublicParam(mpz(n), 1024, hf)
+            taus = [3] if hn == "fdh_n" else [3, 2 ** 600 + 5, -7]
+            for tau in taus:
+                k1, k2 = rng.getrandbits(2040) | 1, rng.getrandbits(64)
+                keys = [k1, k2] if n % 2 == 0 else [k1, -k2]
+                pts = [rng.randrange(n) for _ in range(4)]
+                pts2 = [rng.randrange(n) for _ in range(4)]
+                c1 = _outcome(lambda: [ihex(c) for c in jls.UserKey(pp, keys[0]).encrypt([mpz(v) for v in pts], tau)])
+                c2 = _outcome(lambda: [ihex(c) for c in jls.UserKey(pp, keys[1]).encrypt([mpz(v) for v in pts2], tau)])
+                row = {"n": ihex(n), "hash": hn, "tau": tau, "keys": [k1, keys[1]], "pts": [ihex(v) for v in pts],
+                       "pts2": [ihex(v) for v in pts2], "enc1": c1, "enc2": c2}
+                if "ok" in c1 and "ok" in c2:
+                    sk0 = -(keys[0] + keys[1])
+                    ens = [jls.EncryptedNumber(pp, mpz(I(a))) + jls.EncryptedNumber(pp, mpz(I(b)))
+                           for a, b in zip(c1["ok"], c2["ok"])]
+                    row["sk0"] = sk0
+                    row["dec"] = _outcome(lambda: [ihex(v) for v in jls.ServerKey(pp, sk0).decrypt(ens, tau)])
+                    x1, x2 = [rng.randrange(1 << 20) for _ in range(9)], [rng.randrange(1 << 20) for _ in range(9)]
+                    jl = jls.JoyeLibert()
+                    y1 = jl.protect(pp, jls.UserKey(pp, keys[0]), tau, x1, 2)
+                    y2 = jl.protect(pp, jls.UserKey(pp, keys[1]), tau, x2, 2)
+                    agg = _outcome(lambda: [int(v) for v in jl.aggregate(
+                        jls.ServerKey(pp, sk0), tau, [[jls.EncryptedNumber(pp, c) for c in y] for y in (y1, y2)], 9)])
+                    row["protect"] = {"x1": x1, "x2": x2, "y1": [ihex(c) for c in y1], "y2": [ihex(c) for c in y2],
+                                      "agg": agg}
+                cases.append(row)
+    dump("custom_hash.json", {"cases": cases})
+
+
 def I(s):  # noqa: E743 - hex string -> int (the fixtures' encoding)
     return int(s, 16)
 
@@ -680,6 +727,9 @@ def main():
     if sys.argv[1:] == ["api_edges"]:
         gen_api_edges(R)
         return
+    if sys.argv[1:] == ["custom_hash"]:
+        gen_custom_hash(R)
+        return
     gen_quantize(R)
     gen_lom(R)
     gen_jl(R)
@@ -690,6 +740,7 @@ def main():
     gen_crypter_sweep(R)
     gen_even(R)
     gen_api_edges(R)
+    gen_custom_hash(R)
     meta = {"generator": "tools/gen_golden.py", "reference": load_reference.REF,
             "note": "outputs of the reference Fed-BioMed crypter (Python), imported via tools/refshim"}
     dump("meta.json", meta)
