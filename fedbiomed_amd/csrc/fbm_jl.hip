@@ -1690,7 +1690,10 @@ int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const Jl
   uint64_t g = (n_ct + FBM_BLOCK - 1) / FBM_BLOCK;
   const uint64_t gmax = table_slots / FBM_BLOCK;
   if (g > gmax) g = gmax;
-  hipLaunchKernelGGL(jl_exp_kernel<false>, dim3((unsigned)g), dim3(FBM_BLOCK), 0, s, H, n_ct, (uint32_t*)cst, jp.mn.mp,
+  // probe knob (tools/mixed_probe.py): extra dynamic LDS per workgroup, e.g. enough to hold the
+  // one-lane engine to one workgroup per CU
+  static const unsigned lds_pad = getenv("FBM_EXP_LDS_PAD") ? (unsigned)atoi(getenv("FBM_EXP_LDS_PAD")) : 0u;
+  hipLaunchKernelGGL(jl_exp_kernel<false>, dim3((unsigned)g), dim3(FBM_BLOCK), lds_pad, s, H, n_ct, (uint32_t*)cst, jp.mn.mp,
                      ops, sc.n_ops, sc.first, mode, jp.key_is_zero, nude, table, out, (const JlExpSeg*)nullptr, 0, 0u,
                      (uint32_t*)nullptr);
   return check_launch("jl_exp_kernel");

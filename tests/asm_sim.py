@@ -176,7 +176,7 @@ class Lane:
             v = a * b + self.get(ops[4])
             assert v <= M64, f"v_mad_u64_u32 overflow: {ops}"
             self.put(ops[0], v)
-            self.vcc = 0
+            self.put(ops[1], 0)  # the carry-out (vcc or a rotated SGPR pair): 0, as asserted above
         elif op == "v_lshrrev_b64":
             self.put(ops[0], self.get(ops[2]) >> self.get(ops[1]))
         elif op == "v_lshl_add_u64":

@@ -208,6 +208,20 @@ def normalise_store():
 
 
 M0_SAVE = "s19"  # m0 is reserved to the compiler: saved here (declared clobbered) and restored
+CARRY_PAIRS = ("vcc", "s[16:17]")  # the mads' (never read) carry-outs, alternated
+
+
+def rotate_carries(lines, pairs=CARRY_PAIRS):
+    """Alternate the carry-out destination of successive v_mad_u64_u32 over `pairs`: mads that all
+    write vcc chain through it (write-after-write) and a wave issues one every ~8.8 clocks, two pairs
+    in turn ~5.8 (tools/microbench/gen_oprate.py).  Every mad stays 8 bytes (the computed jumps)."""
+    out, i = [], 0
+    for ln in lines:
+        if ln.startswith("v_mad_u64_u32") and ", vcc," in ln:
+            ln = ln.replace(", vcc,", f", {pairs[i % len(pairs)]},", 1)
+            i += 1
+        out.append(ln)
+    return out
 
 
 def product(sq):
@@ -224,7 +238,7 @@ def product(sq):
     body += ["s_add_u32 s34, s34, 1", f"s_cmp_lg_u32 s34, {L}", "s_cbranch_scc1 1b"]
     body += normalise_store()
     body += [f"s_mov_b32 m0, {M0_SAVE}", "s_nop 1"]  # m0 read right after the asm: wait state
-    return body
+    return rotate_carries(body)
 
 
 # ------------------------------------------------------------------------------------------
@@ -385,7 +399,7 @@ def square_tri():
                      st(base + k, lo(k))]
         body.append(st(base + NW, carry_lo))
     body += ["s_waitcnt lgkmcnt(0)", f"s_mov_b32 m0, {M0_SAVE}", "s_nop 1"]
-    return body
+    return rotate_carries(body)
 
 
 def sq_mads():
@@ -396,7 +410,7 @@ def sq_mads():
 
 def clobbers():
     regs = [f'"v{i}"' for i in range(236)]
-    regs += [f'"s{i}"' for i in list(range(19, 32)) + [34, 35] + list(range(36, 100))]
+    regs += [f'"s{i}"' for i in [16, 17] + list(range(19, 32)) + [34, 35] + list(range(36, 100))]
     out = [", ".join(regs[i:i + 16]) for i in range(0, len(regs), 16)]
     return " \\\n  ".join(x + "," for x in out[:-1]) + " \\\n  " + out[-1]
 

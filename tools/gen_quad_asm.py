@@ -417,7 +417,24 @@ def pair(g, sq, first_x, second_x):
     return body
 
 
-def product(sq, g=QUAD):
+CARRY_PAIRS = ("vcc", "s[20:21]")  # the mads' (never read) carry-outs, alternated: see rotate_carries
+
+
+def rotate_carries(lines, pairs=CARRY_PAIRS):
+    """Alternate the carry-out destination of successive v_mad_u64_u32 over `pairs`.  Every mad
+    writing vcc chains a wave's mads through one SGPR pair (write-after-write): a wave then issues
+    one every ~8.8 clocks; two pairs in turn cut that to ~5.8 (tools/microbench/gen_oprate.py) and a
+    triple-engine square by 15 % at two waves per SIMD (tools/microbench/tri_variants.py)."""
+    out, i = [], 0
+    for ln in lines:
+        if ln.startswith("v_mad_u64_u32") and ", vcc," in ln:
+            ln = ln.replace(", vcc,", f", {pairs[i % len(pairs)]},", 1)
+            i += 1
+        out.append(ln)
+    return out
+
+
+def product(sq, g=QUAD, carries=CARRY_PAIRS):
     e = Emitter()
     XA, XB = g.XA, g.XB
     e.extend([f"s_mov_b32 {M0_SAVE}, m0"] + load_consts())
@@ -443,7 +460,7 @@ def product(sq, g=QUAD):
              ["s_add_u32 s34, s34, 2", f"s_cmp_lg_u32 s34, {L}", "s_cbranch_scc1 2b"])
     e.extend(normalise_store(g))
     e.extend([f"s_mov_b32 m0, {M0_SAVE}", "s_nop 1"])
-    return e.out
+    return rotate_carries(e.out, carries)
 
 
 def row_mads(sq, g=QUAD):
@@ -456,7 +473,7 @@ def product_mads(sq, g=QUAD):
 
 def clobbers(g):
     regs = [f'"v{i}"' for i in range(g.NREG)]
-    regs += [f'"s{i}"' for i in [19, 34, 35, 36] + list(range(KBASE, KBASE + L))]
+    regs += [f'"s{i}"' for i in [19, 20, 21, 34, 35, 36] + list(range(KBASE, KBASE + L))]
     out = [", ".join(regs[i:i + 16]) for i in range(0, len(regs), 16)]
     return " \\\n  ".join(x + "," for x in out[:-1]) + " \\\n  " + out[-1]
 
