@@ -435,6 +435,8 @@ def rotate_carries(lines, pairs=CARRY_PAIRS):
 
 
 def product(sq, g=QUAD, carries=CARRY_PAIRS):
+    if sq and CYC_SQUARE:
+        return square_cyc(g, carries)
     e = Emitter()
     XA, XB = g.XA, g.XB
     e.extend([f"s_mov_b32 {M0_SAVE}, m0"] + load_consts())
@@ -463,16 +465,241 @@ def product(sq, g=QUAD, carries=CARRY_PAIRS):
     return rotate_carries(e.out, carries)
 
 
+# ------------------------------------------------------------------------------------------
+# The square as a cyclic-band triangular product (round 3).  x0^2 needs each cross product
+# x_a x_b (a < b) once, doubled, and each diagonal x_a^2 once.  Row i's t part multiplies x_i by
+# the lane's b-limbs j = M l + r; whether a product is needed depends only on
+# rho = (j - i) mod M = (r - i) mod M -- the same in every lane of the group, so one instruction
+# stream serves all lanes: rho in 1..ceil(M/2)-1 with 2 x_i (the pair's mirror, rho' = M - rho,
+# is skipped in row j), rho = 0 and rho = M/2 with x_i undoubled (their pairs come up in both
+# rows: twice, undoubled; rho = 0 within a row's own column is the diagonal, once).  7 of 12 t
+# products per lane and row in the triple, 5 of 9 in the quad (49 -> 44 / 37 -> 33 multiplies).
+# Which registers a row multiplies changes with i mod M, so the 36 rows are unrolled; the window
+# shift is static register renaming over M + 1 pairs per digit part (slot r of row i in pair
+# (i + r) mod (M + 1)), every product accumulating in place; the received top slot arrives in RT /
+# RS (hi 0) and is taken in by the top slot's first product of the next row (as addend).  The
+# K'_i are read from s(64 + i) directly (no m0).  Same residues as the looped square.
+# ------------------------------------------------------------------------------------------
+CYC_SQUARE = True
+
+
+class CycPlan:
+    """Register plan of square_cyc for geometry g (pairs named by their low VGPR)."""
+
+    def __init__(self, g):
+        M = g.M
+        self.W = W = M + 1
+        v = 0
+        self.PT = [v + 2 * k for k in range(W)]
+        v += 2 * W
+        self.RT = v
+        v += 2
+        self.PS = [v + 2 * k for k in range(W)]
+        v += 2 * W
+        self.RS = v
+        v += 2
+        self.B0 = [v + r for r in range(M)]
+        v += M
+        self.B1 = [v + r for r in range(M)]
+        v += M
+        self.X = (v, v + 1)  # x0 of even / odd rows
+        self.XD = v + 2      # 2 x0 of the current row
+        v += 3
+        for nm in ("Q", "Q2", "CQ", "MASKV", "QB", "Q2B", "T3", "T4", "TMP", "TMP2"):
+            setattr(self, nm, v)
+            v += 1
+        v += v % 2  # 64-bit pairs start on an even VGPR
+        self.CY, self.CS = v, v + 2
+        v += 4
+        self.NREG = v
+
+
+def _pr(lo):
+    return f"v[{lo}:{lo + 1}]"
+
+
+def cyc_active(g, i):
+    """[(r, doubled)] of row i's t products (see above)."""
+    M = g.M
+    out = []
+    for r in range(M):
+        rho = (r - i) % M
+        if rho == 0 or (M % 2 == 0 and rho == M // 2):
+            out.append((r, False))
+        elif 1 <= rho <= (M - 1) // 2:
+            out.append((r, True))
+    return out
+
+
+def cyc_row(g, P, i):
+    M, W = g.M, P.W
+    first, last = i == 0, i == L - 1
+    xs, xn = P.X[i % 2], P.X[(i + 1) % 2]
+    st = lambda r: P.PT[(i + r) % W]  # noqa: E731
+    ss = lambda r: P.PS[(i + r) % W]  # noqa: E731
+    touched = {"t": set(), "s": set()}
+
+    def addend(part, r):
+        reg = st(r) if part == "t" else ss(r)
+        if r in touched[part]:
+            return _pr(reg)
+        touched[part].add(r)
+        if first:
+            return "0"
+        if r == M - 1:
+            return _pr(P.RT if part == "t" else P.RS)
+        return _pr(reg)
+
+    out = [] if last else [f"ds_read_b32 v{xn}, %[ac] offset:{(i + 1) * g.ROWB}"]
+    acts = cyc_active(g, i)
+    tm = {r: f"v_mad_u64_u32 {_pr(st(r))}, vcc, v{P.XD if dbl else xs}, v{P.B0[r]}, {addend('t', r)}"
+          for r, dbl in acts}
+    sm = [f"v_mad_u64_u32 {_pr(ss(r))}, vcc, v{xs}, v{P.B1[r]}, {addend('s', r)}" for r in range(M)]
+    # pass 1: slot 0's t and s products first, the rest interleaved; the quotient chain threaded in
+    head = ([tm[0]] if 0 in tm else []) + [sm[0]]
+    t_rest = [tm[r] for r, _ in acts if r != 0]
+    s_rest = sm[1:]
+    rest = []
+    for k in range(max(len(t_rest), len(s_rest))):
+        if k < len(t_rest):
+            rest.append(t_rest[k])
+        if k < len(s_rest):
+            rest.append(s_rest[k])
+    K = f"s{KBASE + i}"
+    if g.G == 4:
+        chain = [f"v_mul_lo_u32 v{P.Q}, v{st(0)}, %[np]",
+                 f"v_and_b32_dpp v{P.Q}, v{P.Q}, v{P.MASKV} {dpp((0, 0, 0, 0))}",
+                 f"v_sub_u32 v{P.CQ}, {K}, v{P.Q}",
+                 f"v_mad_u64_u32 {_pr(ss(0))}, vcc, v{P.CQ}, %[e0], {_pr(ss(0))}",
+                 f"v_mul_lo_u32 v{P.Q2}, v{ss(0)}, %[np]",
+                 f"v_and_b32_dpp v{P.Q2}, v{P.Q2}, v{P.MASKV} {dpp((0, 0, 0, 0))}"]
+        gaps = [1 if 0 in tm else 0, 2, 2, 2, 3, 2]
+        qb, q2b = P.Q, P.Q2
+    else:
+        chain = [f"v_mul_lo_u32 v{P.Q}, v{st(0)}, %[np]",
+                 f"v_and_b32 v{P.Q}, {MASK}, v{P.Q}",
+                 f"ds_bpermute_b32 v{P.QB}, %[bp], v{P.Q}",
+                 f"v_sub_u32 v{P.CQ}, {K}, v{P.Q}",
+                 f"v_mad_u64_u32 {_pr(ss(0))}, vcc, v{P.CQ}, %[e0], {_pr(ss(0))}",
+                 f"v_mul_lo_u32 v{P.Q2}, v{ss(0)}, %[np]",
+                 f"v_and_b32 v{P.Q2}, {MASK}, v{P.Q2}",
+                 f"ds_bpermute_b32 v{P.Q2B}, %[bp], v{P.Q2}"]
+        gaps = [1 if 0 in tm else 0, 2, 0, 2, 2, 3, 2, 0]
+        qb, q2b = P.QB, P.Q2B
+    p1 = list(head)
+    ri = 0
+    for k, ins in enumerate(chain):
+        take = gaps[k]
+        p1 += rest[ri:ri + take]
+        ri += take
+        p1.append(ins)
+    p1 += rest[ri:]
+    if g.G == 3:
+        p1.append("s_waitcnt lgkmcnt(1)")  # the row prefetch and QB (Q2B may still be in flight)
+    # pass 2: q N into the t window
+    p2 = [f"v_mad_u64_u32 {_pr(st(r))}, vcc, v{qb}, {N(r)}, {addend('t', r)}" for r in range(M)]
+    # pass 3: q' N into the s window, both retires threaded in:
+    #   T = lo + c 2^29 -> lo (masked) to the lane below's top slot (RT / RS), c into slot 1
+    sq3 = [f"v_mad_u64_u32 {_pr(ss(r))}, vcc, v{q2b}, {N(r)}, {addend('s', r)}" for r in range(M)]
+    ret_t = [g.down("v_and_b32_dpp", f"v{P.RT}", f"v{st(0)}", f", v{P.MASKV}"),
+             f"v_lshrrev_b64 {_pr(st(0))}, {LB}, {_pr(st(0))}",
+             f"v_lshl_add_u64 {_pr(st(1))}, {_pr(st(0))}, 0, {_pr(st(1))}"]
+    ret_s = [g.down("v_and_b32_dpp", f"v{P.RS}", f"v{ss(0)}", f", v{P.MASKV}"),
+             f"v_lshrrev_b64 {_pr(ss(0))}, {LB}, {_pr(ss(0))}",
+             f"v_lshl_add_u64 {_pr(ss(1))}, {_pr(ss(0))}, 0, {_pr(ss(1))}"]
+    p3 = ["s_waitcnt lgkmcnt(0)"]
+    if not last:  # the next row's doubled operand (its x0 has arrived with the wait above)
+        p3.append(f"v_lshlrev_b32 v{P.XD}, 1, v{xn}")
+    p3 += [sq3[0], ret_t[0], sq3[1], ret_t[1], sq3[2], ret_t[2], sq3[3], ret_s[0], sq3[4], ret_s[1], sq3[5],
+           ret_s[2]] + sq3[6:]
+    return out + p1 + p2 + p3
+
+
+def cyc_mid_reduce(g, P, i):
+    """mid_reduce with the window of row i (slots 0..M-2 in their pairs, the top slot in RT / RS)."""
+    M, W = g.M, P.W
+    chains = []
+    for pt, rr, t in ((P.PT, P.RT, P.T3), (P.PS, P.RS, P.T4)):
+        acc = lambda k, pt=pt: pt[(i + k) % W]  # noqa: E731
+        ch = []
+        for k in range(M - 2):
+            ch += [f"v_mad_u64_u32 {_pr(acc(k + 1))}, vcc, v{acc(k) + 1}, 8, {_pr(acc(k + 1))}", f"v_mov_b32 v{acc(k) + 1}, 0"]
+        ch += [f"v_mad_u64_u32 {_pr(rr)}, vcc, v{acc(M - 2) + 1}, 8, {_pr(rr)}", f"v_mov_b32 v{acc(M - 2) + 1}, 0",
+               g.up(f"v{t}", f"v{rr + 1}"),
+               f"v_mov_b32 v{rr + 1}, 0",
+               f"v_mad_u64_u32 {_pr(acc(0))}, vcc, v{t}, 8, {_pr(acc(0))}"]
+        chains.append(ch)
+    out = []
+    for a, b in zip(*chains):
+        out += [a, b]
+    return out
+
+
+def cyc_normalise_store(g, P):
+    """normalise_store with the window after row 35 (slots 0..M-2 in their pairs, the top in RT / RS)."""
+    M, W = g.M, P.W
+    i = L
+    chains = []
+    for pt, rr, breg, cy, t1, t2 in ((P.PT, P.RT, P.B0, P.CY, P.TMP, P.TMP2), (P.PS, P.RS, P.B1, P.CS, P.T3, P.T4)):
+        acc = lambda k, pt=pt: pt[(i + k) % W]  # noqa: E731
+        ch = [f"v_and_b32 v{breg[0]}, {MASK}, v{acc(0)}", f"v_lshrrev_b64 {_pr(cy)}, {LB}, {_pr(acc(0))}"]
+        for r in range(1, M - 1):
+            ch += [f"v_lshl_add_u64 {_pr(acc(r))}, {_pr(cy)}, 0, {_pr(acc(r))}",
+                   f"v_and_b32 v{breg[r]}, {MASK}, v{acc(r)}",
+                   f"v_lshrrev_b64 {_pr(cy)}, {LB}, {_pr(acc(r))}"]
+        ch += [f"v_lshl_add_u64 {_pr(rr)}, {_pr(cy)}, 0, {_pr(rr)}",
+               f"v_and_b32 v{breg[M - 1]}, {MASK}, v{rr}",
+               f"v_lshrrev_b64 {_pr(cy)}, {LB}, {_pr(rr)}",
+               g.up(f"v{t1}", f"v{cy}"),
+               g.up(f"v{t2}", f"v{cy + 1}"),
+               f"v_add_co_u32 v{t1}, vcc, v{t1}, v{breg[0]}|v_addc_co_u32 v{t2}, vcc, 0, v{t2}, vcc",
+               f"v_and_b32 v{breg[0]}, {MASK}, v{t1}",
+               f"v_alignbit_b32 v{t1}, v{t2}, v{t1}, {LB}",
+               f"v_add_u32 v{breg[1]}, v{breg[1]}, v{t1}"]
+        chains.append(ch)
+    out = []
+    for k in range(max(len(c) for c in chains)):
+        for ch in chains:
+            if k < len(ch):
+                out += ch[k].split("|")
+    for d, breg in ((0, P.B0), (1, P.B1)):
+        out += [f"ds_write_b32 %[al], v{breg[r]} offset:{(d * g.D1 + r) * g.ROWB}" for r in range(M)]
+    out.append("s_waitcnt lgkmcnt(0)")
+    return out
+
+
+def square_cyc(g, carries=CARRY_PAIRS):
+    P = CycPlan(g)
+    M = g.M
+    e = Emitter()
+    e.extend(load_consts())
+    for r in range(M):
+        e.emit(f"ds_read_b32 v{P.B0[r]}, %[al] offset:{r * g.ROWB}")
+        e.emit(f"ds_read_b32 v{P.B1[r]}, %[al] offset:{(g.D1 + r) * g.ROWB}")
+    e.extend([f"v_mov_b32 v{P.RT + 1}, 0", f"v_mov_b32 v{P.RS + 1}, 0", f"v_mov_b32 v{P.MASKV}, {MASK}",
+              f"ds_read_b32 v{P.X[0]}, %[ac]", "s_waitcnt lgkmcnt(0)"])
+    e.extend([f"v_lshlrev_b32 v{P.B1[r]}, 1, v{P.B1[r]}" for r in range(M)])  # the s part is x0 * (2 x1)
+    e.emit(f"v_lshlrev_b32 v{P.XD}, 1, v{P.X[0]}")
+    for i in range(L):
+        e.extend(cyc_row(g, P, i))
+        if i == MID - 1:
+            e.extend(cyc_mid_reduce(g, P, i + 1))
+    e.extend(cyc_normalise_store(g, P))
+    return rotate_carries(e.out, carries)
+
+
 def row_mads(sq, g=QUAD):
     return sum(1 for ln in row(g, False, sq, "s35", g.XA, g.XB, g.ROWB) if ln.startswith("v_mad_u64_u32"))
 
 
 def product_mads(sq, g=QUAD):
+    if sq and CYC_SQUARE:  # unrolled: the static count is the executed count
+        return sum(1 for ln in square_cyc(g) if ln.startswith("v_mad_u64_u32"))
     return L * row_mads(sq, g) + sum(1 for ln in mid_reduce(g) if ln.startswith("v_mad_u64_u32"))
 
 
 def clobbers(g):
-    regs = [f'"v{i}"' for i in range(g.NREG)]
+    regs = [f'"v{i}"' for i in range(max(g.NREG, CycPlan(g).NREG))]
     regs += [f'"s{i}"' for i in [19, 20, 21, 34, 35, 36] + list(range(KBASE, KBASE + L))]
     out = [", ".join(regs[i:i + 16]) for i in range(0, len(regs), 16)]
     return " \\\n  ".join(x + "," for x in out[:-1]) + " \\\n  " + out[-1]
@@ -499,8 +726,8 @@ def header(g, pfx, PFX, name):
 // ciphertext, lane l owns limbs {M} l .. {M} l + {M - 1} of both 36-limb digits, radix 2^29,
 // R = 2^1044; {dpp_word}): the LDS column a <- a * b * R^-1 (mod N^2), digits lazily < 2N.
 // See tools/gen_quad_asm.py for the layout, the cross-lane steps and the bounds.
-// {len(mm)} instructions (general, B from global), {len(sq)} (square); per lane and row
-// {row_mads(False, g)} / {row_mads(True, g)} v_mad_u64_u32 -> {product_mads(False, g)} / {product_mads(True, g)} per product.
+// {len(mm)} instructions (general, B from global; a runtime row loop), {len(sq)} (square{", unrolled cyclic-band triangular" if CYC_SQUARE else ""});
+// per lane {product_mads(False, g)} / {product_mads(True, g)} v_mad_u64_u32 per product ({row_mads(False, g)} per general row).
 #pragma once
 #include <stdint.h>
 
@@ -557,8 +784,8 @@ def main():
         out = os.path.join(ROOT, "fedbiomed_amd", "csrc", fn)
         with open(out, "w") as f:
             f.write(hdr)
-        print(f"wrote {out}: general {len(mm)} / square {len(sq)} instructions; mads/row {row_mads(False, g)} / "
-              f"{row_mads(True, g)}; {g.NREG} VGPRs")
+        print(f"wrote {out}: general {len(mm)} / square {len(sq)} instructions; mads/product {product_mads(False, g)} / "
+              f"{product_mads(True, g)}; {max(g.NREG, CycPlan(g).NREG)} VGPRs")
 
 
 if __name__ == "__main__":
