@@ -1520,13 +1520,13 @@ int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32
 // modelled time.  A group engine's launch time is set by its busiest SIMD: with w waves' worth
 // of work on it (w = workgroups per CU, each workgroup's 4 waves on the CU's 4 SIMDs; beyond
 // FBM_GROUP_WAVES resident workgroups the persistent ones loop) it takes about A + B w -- A the
-// part of a lone wave's time another wave cannot fill, B a wave's issue time.  Measured on
-// MI355X (tools/exp_probe.py, 2040-bit exponent, profiles/r2_engine_sweep.jsonl): triple
-// 26.3 / 37.0 / 48.3 / 58.7 ms at w = 2 / 3 / 4 / 5 (A = 4.5, B = 10.8), quad 29.5 / 37.3 / 51.9 /
-// 60.3 at w = 3 / 4 / 6 / 7 (A = 4, B = 8.1).  The one-lane engine: 33.6 ms up to one wave per SIMD,
-// 57 ms for a launch of one round of two, 50 ms per round of longer launches.  (A build with 4
-// resident group waves per SIMD, -DFBM_GROUP_WAVES=4, measured no faster at w = 4: the issue is
-// already saturated at 3.)
+// part of a lone wave's time another wave cannot fill, B a wave's issue time.  Refit on MI355X
+// after round 3's cyclic-band square and carry rotation (tools/exp_probe.py, 2043-bit exponent,
+// profiles/r3_engine_sweep_cyc.jsonl): triple 13.4 / 23.7 / 33.7 / 44.9 / 54.7 ms at w = 1 … 5
+// (A = 3.2, B = 10.3), quad 9.9 / 17.8 / 26.1 / 33.7 / 48.3 at w = 1 / 2 / 3 / 4 / 6 (A = 2.5,
+// B = 7.8).  The one-lane engine: 31.7 ms up to one wave per SIMD, 56 ms for a launch of one round
+// of two, 50 ms per round of longer launches.  (A build with 4 resident group waves per SIMD,
+// -DFBM_GROUP_WAVES=4, measured no faster at w = 4: the issue is already saturated at 3.)
 static std::atomic<int> g_engine{-1};
 
 int jl_engine_policy() {
@@ -1560,13 +1560,13 @@ static double engine_model_ms(int engine, uint64_t n_ct) {
   const uint64_t ncu = (uint64_t)device_num_cu();
   if (engine == FBM_ENGINE_SINGLE) {
     const uint64_t lanes = ncu * 2 * FBM_BLOCK;
-    if (n_ct <= lanes / 2) return 33.6;
-    if (n_ct <= lanes) return 57.0;
+    if (n_ct <= lanes / 2) return 31.7;
+    if (n_ct <= lanes) return 56.0;
     return 50.0 * (double)((n_ct + lanes - 1) / lanes) - (n_ct % lanes && n_ct % lanes <= lanes / 2 ? 16.4 : 0.0);
   }
   const uint64_t wgs = (n_ct + group_ct_per_wg(engine) - 1) / group_ct_per_wg(engine);
   const uint64_t w = (wgs + ncu - 1) / ncu;
-  const double A = engine == FBM_ENGINE_TRIPLE ? 4.5 : 4.0, B = engine == FBM_ENGINE_TRIPLE ? 10.8 : 8.1;
+  const double A = engine == FBM_ENGINE_TRIPLE ? 3.2 : 2.5, B = engine == FBM_ENGINE_TRIPLE ? 10.3 : 7.8;
   return A + B * (double)w;
 }
 

@@ -31,8 +31,10 @@ def test_engine_policy_host():
         assert lib.fbm_jl_engine_for(41_667) == 3  # a config-4 stripe: 2 triple waves per SIMD, 3 quad
         assert lib.fbm_jl_engine_for(30_000) == 4 and lib.fbm_jl_engine_for(200_000) == 1
         # past the group engines' residency (persistent workgroups loop): a config-4 N = 4 stripe's
-        # 83 334 ciphertexts take the triple (48 ms measured against the one-lane engine's 57)
-        assert lib.fbm_jl_engine_for(83_334) == 3 and lib.fbm_jl_engine_for(100_000) == 1
+        # 83 334 ciphertexts take the triple (44 ms measured against the one-lane engine's 56), and so
+        # do 100 000 (five triple waves per SIMD, 54.7 ms at 107 520); 120 000 go to the one-lane engine
+        assert lib.fbm_jl_engine_for(83_334) == 3 and lib.fbm_jl_engine_for(100_000) == 3
+        assert lib.fbm_jl_engine_for(120_000) == 1
     finally:
         lib.fbm_jl_set_engine(prev)
     import importlib.util
