@@ -250,3 +250,24 @@ def _lds_waits_ok(prog, g):
 def test_lds_results_waited_for(geo):
     for prog in PROGS[geo]:
         assert _lds_waits_ok(prog, GEOS[geo])
+
+
+@pytest.mark.parametrize("geo", ["quad", "triple"])
+def test_cyclic_band_square_covers_each_product_once(geo):
+    """The cyclic-band triangular square (gen_quad_asm.cyc_active): over the 36 rows and the G lanes,
+    x_a * x_b (a < b) is added with total weight 2 and x_a^2 with weight 1 -- each pair once doubled or
+    twice undoubled -- and the rows' instruction streams are the same in every lane (activity depends
+    on (r - i) mod M only)."""
+    g = GEOS[geo]
+    weight = {}
+    for i in range(L):
+        for r, dbl in Q.cyc_active(g, i):
+            for lane in range(g.G):
+                j = g.M * lane + r
+                key = (min(i, j), max(i, j))
+                weight[key] = weight.get(key, 0) + (2 if dbl else 1)
+    for a in range(L):
+        for b in range(a, L):
+            assert weight.get((a, b), 0) == (1 if a == b else 2), (a, b, weight.get((a, b)))
+    per_row = [len(Q.cyc_active(g, i)) for i in range(L)]
+    assert per_row == [g.M // 2 + 1] * L  # 7 of 12 (triple), 5 of 9 (quad)
