@@ -224,43 +224,6 @@ static void big_divmod(const Big& a, const Big& m, Big& q, Big& r) {
   }
 }
 
-// Constants of the N-adic engine (tools/gen_nadic_asm.py): R = 2^(37*28) = 2^1036.
-static void build_nadic(const Big& N, const Big& M, const MontCtxN& mn, NadicCtx& na) {
-  memset(&na, 0, sizeof(na));
-  const int L = FBM_NLN;
-  // K = (1 - R) mod N, K'_i = (2^28 - 1) + K_i
-  Big Rm = big_pow2_mod(L * FBM_LB, N);  // R mod N  (N odd >= 3 -> Rm != 0)
-  Big K(N.size() + 1, 0u);
-  K[0] = 1u;
-  if (big_cmp(Rm, K) > 0) {  // K = N + 1 - Rm
-    Big t(N.begin(), N.end());
-    t.push_back(0u);
-    uint64_t c = 1;
-    for (size_t k = 0; k < t.size(); ++k) {
-      c += t[k];
-      t[k] = (uint32_t)c;
-      c >>= 32;
-    }
-    big_sub_inplace(t, Rm);
-    K = t;
-  } else {  // Rm == 1 -> K = 0
-    K.assign(1, 0u);
-  }
-  uint32_t k28[FBM_NLN];
-  to28_host(K, k28, L);
-  for (int j = 0; j < 10; ++j) na.nk[j] = mn.M[j];
-  for (int j = 10; j < L; ++j) na.nk[16 + j - 10] = mn.M[j];
-  for (int j = 0; j < L; ++j) na.nk[43 + j] = FBM_LMASK + k28[j];
-  // R^2, R^3 mod N^2 = u0 + u1 N
-  for (int e = 2; e <= 3; ++e) {
-    const Big u = big_pow2_mod(e * L * FBM_LB, M);
-    Big q, r;
-    big_divmod(u, N, q, r);
-    uint32_t* dst = e == 2 ? na.r2na : na.r3na;
-    to28_host(r, dst, L);
-    to28_host(q, dst + L, L);
-  }
-}
 
 // Constants of the quad engine (tools/gen_quad_asm.py): 29-bit limbs, R = 2^(36*29) = 2^1044.
 static void build_quad(const Big& N, const Big& M, QuadCtx& qa) {
@@ -298,6 +261,17 @@ static void build_quad(const Big& N, const Big& M, QuadCtx& qa) {
   uint32_t inv = N[0];  // Newton: N^-1 mod 2^32
   for (int i = 0; i < 5; ++i) inv *= 2u - N[0] * inv;
   qa.np = (0u - inv) & ((1u << LB) - 1u);
+}
+
+// Constants of the one-lane N-adic engine (tools/gen_nadic_asm.py): the group engines' 29-bit
+// N and K'_i (the same R = 2^1044) in the layout of its scalar loads, and N's 28-bit limbs
+// for the final step shared by all N-adic engines (na_final_digits).
+static void build_nadic(const MontCtxN& mn, const QuadCtx& qa, NadicCtx& na) {
+  static_assert(FBM_NA_LIMBS == FBM_QA_L && FBM_NA_LIMB_BITS == FBM_QA_LB, "one R for all N-adic engines");
+  memset(&na, 0, sizeof(na));
+  for (int j = 0; j < FBM_NLN; ++j) na.nk[j < 10 ? j : 6 + j] = mn.M[j];
+  for (int j = 0; j < FBM_QA_L; ++j) na.nk29[j < 10 ? j : 6 + j] = qa.n[j];
+  for (int j = 0; j < FBM_QA_L; ++j) na.nk29[42 + j] = qa.kp[j];
 }
 
 // SHA-256 midstate over the 14 leading all-zero blocks of t.to_bytes(1024,'big') (FDH.H)
@@ -461,8 +435,8 @@ static int build_jl_params_uncached(const uint32_t* biprime, int es, int cr, con
   while (M.size() > 64) M.pop_back();
   build_mont<FBM_NL>(M, jp.mc);
   build_mont<FBM_NLN>(N, jp.mn);
-  build_nadic(N, M, jp.mn, jp.na);
   build_quad(N, M, jp.qa);
+  build_nadic(jp.mn, jp.qa, jp.na);
   for (int i = 0; i < 32; ++i) jp.N32[i] = biprime[i];
   {  // N^-1 mod 2^1024 by Newton: y <- y (2 - N y); y = N is correct to 3 bits for odd N
     uint32_t y[32], t[32];
@@ -1504,10 +1478,10 @@ int fbm_test_nadic_consts(const uint32_t* n32, uint32_t* nk, uint32_t* r2na, uin
   const uint32_t tau1[16] = {1u};
   int rc = build_jl_params(n32, 34, 30, tau1, 0, jp);
   if (rc) return rc;
-  memcpy(nk, jp.na.nk, sizeof(jp.na.nk));
-  memcpy(r2na, jp.na.r2na, sizeof(jp.na.r2na));
-  memcpy(r3na, jp.na.r3na, sizeof(jp.na.r3na));
-  *np = jp.mn.mp;
+  memcpy(nk, jp.na.nk29, sizeof(jp.na.nk29));
+  memcpy(r2na, jp.qa.r2, sizeof(jp.qa.r2));
+  memcpy(r3na, jp.qa.r3, sizeof(jp.qa.r3));
+  *np = jp.qa.np;
   return FBM_OK;
 }
 

@@ -72,15 +72,16 @@ int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t 
 #define FBM_CST_R2 128
 #define FBM_CST_ONE 256
 #define FBM_CST_RK (256 + FBM_NL * 256)
-// N-adic exponentiation engine (fbm_nadic_asm.hpp): its 80-word constants block (N limbs
-// and K'_i, the layout the assembly's scalar loads expect) and R^2 mod N^2 as two N-adic
-// digits (74 limbs, the uniform A operand that brings h into Montgomery form)
+// N's 28-bit limbs at words 0..9, 16..42 (the final step of every N-adic engine,
+// na_final_digits), then the one-lane engine's (fbm_nadic_asm.hpp) 80-word constants block:
+// N's 29-bit limbs and K'_i in the layout the assembly's scalar loads expect
 #define FBM_CST_NK (FBM_CST_RK + 128)
-#define FBM_CST_R2NA (FBM_CST_NK + 128)
-#define FBM_CST_R3NA (FBM_CST_R2NA + 128)  // R^3 mod N^2 (digits): the high part of a wide h
-// lane-group engines (fbm_quad_asm.hpp / fbm_tri_asm.hpp, 29-bit limbs, R = 2^1044): K'_i
-// (36 words), N's limbs (limb k at word k), R^2 and R^3 mod N^2 as digit pairs (72 limbs each)
-#define FBM_CST_QK (FBM_CST_R3NA + 128)
+#define FBM_CST_NA29 (FBM_CST_NK + 128)
+// lane-group engines (fbm_quad_asm.hpp / fbm_tri_asm.hpp) and the one-lane engine, all 29-bit
+// limbs with R = 2^1044: K'_i (36 words), N's limbs (limb k at word k), R^2 and R^3 mod N^2 as
+// digit pairs (72 limbs each; the uniform A operand that brings h, or a wide h's high part,
+// into Montgomery form)
+#define FBM_CST_QK (FBM_CST_NA29 + 128)
 #define FBM_CST_QNP (FBM_CST_QK + 64)
 #define FBM_CST_QR2 (FBM_CST_QNP + 64)
 #define FBM_CST_QR3 (FBM_CST_QR2 + 128)
@@ -98,14 +99,13 @@ struct JlSched {
   uint16_t op[FBM_MAX_OPS];
 };
 
-// N-adic constants (tools/gen_nadic_asm.py): words 0..9 = N_0..N_9, 16..42 = N_10..N_36,
-// 43..79 = K'_i = (2^28 - 1) + K_i with K = (1 - 2^1036) mod N; r2na / r3na = the digits
-// of R^2 = 2^2072 / R^3 = 2^3108 mod N^2 (u mod N, u div N), 37 limbs each.
+// N-adic constants.  nk: N's 28-bit limbs, words 0..9 = N_0..N_9, 16..42 = N_10..N_36 (the
+// shared final step).  nk29 (tools/gen_nadic_asm.py, 29-bit limbs, R = 2^1044): words
+// 0..9 = N_0..N_9, 16..41 = N_10..N_35, 42..77 = K'_i = (2^29 - 1) + K_i with K = (1 - R) mod N.
+// R^2 / R^3 mod N^2 as 29-bit digit pairs: QuadCtx::r2 / r3 (the same R).
 struct NadicCtx {
   uint32_t nk[80];
-  uint32_t r2na[FBM_NL];
-  uint32_t r3na[FBM_NL];
-  uint32_t pad[4];
+  uint32_t nk29[80];
 };
 
 // lane-group engine constants (tools/gen_quad_asm.py): 29-bit limbs, R = 2^1044

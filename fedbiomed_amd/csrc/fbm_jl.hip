@@ -518,13 +518,48 @@ __device__ __forceinline__ void na_final_digits(uint32_t (&t)[FBM_NLN], uint32_t
   from28<FBM_NL, 64>(v28, w);
 }
 
-__device__ __forceinline__ void na_final(const uint32_t* lds, const uint32_t* NK, uint32_t (&w)[64], int nadic_out) {
-  uint32_t t[FBM_NLN], sd[FBM_NLN];
+#define FBM_QMASK ((1u << FBM_QA_LB) - 1u)  // the 29-bit engines' limb mask
+
+// radix changes between the shared final step's 28-bit limbs and the engines' 29-bit limbs
+// (both normalised: every limb below its radix)
+__device__ __forceinline__ void relimb_29_28(const uint32_t (&x)[FBM_QA_L], uint32_t (&o)[FBM_NLN]) {
 #pragma unroll
-  for (int k = 0; k < FBM_NLN; ++k) {
-    t[k] = lds[k * FBM_BLOCK];
-    sd[k] = lds[(FBM_NLN + k) * FBM_BLOCK];
+  for (int j = 0; j < FBM_NLN; ++j) {
+    const int bit = j * FBM_LB, k = bit / FBM_QA_LB, off = bit % FBM_QA_LB;
+    const uint64_t v = ((uint64_t)(k + 1 < FBM_QA_L ? x[k + 1] : 0u) << FBM_QA_LB) | (k < FBM_QA_L ? x[k] : 0u);
+    o[j] = (uint32_t)(v >> off) & FBM_LMASK;
   }
+}
+__device__ __forceinline__ void relimb_28_29(const uint32_t* x, uint32_t* o) {  // FBM_NLN -> FBM_QA_L limbs
+#pragma unroll
+  for (int k = 0; k < FBM_QA_L; ++k) {
+    const int bit = k * FBM_QA_LB, j = bit / FBM_LB, off = bit % FBM_LB;
+    const uint64_t v = ((uint64_t)(j + 1 < FBM_NLN ? x[j + 1] : 0u) << FBM_LB) | (j < FBM_NLN ? x[j] : 0u);
+    o[k] = (uint32_t)(v >> off) & FBM_QMASK;
+  }
+}
+
+// a 64-word (2048-bit) row -> its 72 29-bit limbs (h_lo, h_hi): h = h_lo + h_hi 2^1044
+__device__ __forceinline__ void to29_row64(const uint32_t (&w)[64], uint32_t (&o)[2 * FBM_QA_L]) {
+#pragma unroll
+  for (int k = 0; k < 2 * FBM_QA_L; ++k) {
+    const int bit = k * FBM_QA_LB, wi = bit >> 5, sh = bit & 31;
+    const uint64_t v = ((uint64_t)(wi + 1 < 64 ? w[wi + 1] : 0u) << 32) | (wi < 64 ? w[wi] : 0u);
+    o[k] = (uint32_t)(v >> sh) & FBM_QMASK;
+  }
+}
+
+// the one-lane engine's result (normalised 29-bit digits in the lane's LDS column) -> na_final_digits
+__device__ __forceinline__ void na_final(const uint32_t* lds, const uint32_t* NK, uint32_t (&w)[64], int nadic_out) {
+  uint32_t t29[FBM_QA_L], s29[FBM_QA_L];
+#pragma unroll
+  for (int k = 0; k < FBM_QA_L; ++k) {
+    t29[k] = lds[k * FBM_BLOCK];
+    s29[k] = lds[(FBM_QA_L + k) * FBM_BLOCK];
+  }
+  uint32_t t[FBM_NLN], sd[FBM_NLN];
+  relimb_29_28(t29, t);
+  relimb_29_28(s29, sd);
   na_final_digits(t, sd, NK, w, nadic_out);
 }
 
@@ -532,7 +567,7 @@ __device__ __forceinline__ void na_final(const uint32_t* lds, const uint32_t* NK
 // mode 1 (DEC): out[ct] = H[ct]^key mod N^2 (plain)                (for the inverse)
 // | FBM_EXP_OUT_NADIC: out rows hold the result's digits (v mod N, v div N) (jl_lift_kernel)
 // N-adic engine (fbm_nadic_asm.hpp): a residue is the digit pair (x0, x1), X = x0 + x1 N,
-// 74 limbs = 2 x 37 in the same blocked columns.  Sliding window (width FBM_WIN,
+// 72 limbs = 2 x 36 of 29 bits in the same blocked columns (entries keep the 74-row stride).  Sliding window (width FBM_WIN,
 // FBM_TABLE odd powers) over the device copy of the host-built schedule.  Per-lane table:
 // FBM_TENTRIES blocked columns (the last = h / h^2 scratch).
 //   a = R^2 (uniform, N-adic digits), b = (h, 0)  -> h*R              -> table[0]
@@ -540,7 +575,7 @@ __device__ __forceinline__ void na_final(const uint32_t* lds, const uint32_t* NK
 //   a = h^(2t-1)*R, b = table[16]                  -> h^(2t+1)*R       -> table[t], t = 1..15
 //   a = table[first], then per op: nsq squarings, one product with table[idx]
 //   a = acc,  b = nude = (1, pt) | 1 = (1, 0)      -> c | h^key (digits) -> t + s N -> out
-// h < 2^1036 (one FDH digest: always, for a 1024-bit N) IS the digit pair (h, 0); a wider h
+// h < R = 2^1044 (one FDH digest: always, for a 1024-bit N) IS the digit pair (h, 0); a wider h
 // (FDH retries, small moduli) enters as h_lo R + h_hi R^2 (one more product, that wave only).
 // Lanes past n_ct (last chunk) redo the last ciphertext and store nothing.
 //
@@ -580,7 +615,9 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
   const int tid = threadIdx.x;
   uint32_t* lds = lds_a + tid;
   const uint32_t aoff = lds_addr(lds);
-  const uint32_t* NK = cst + FBM_CST_NK;
+  const uint32_t* NK = cst + FBM_CST_NA29;
+  constexpr int NA = FBM_NA_LIMBS;
+  static_assert(NA == FBM_QA_L && FBM_NA_LIMB_BITS == FBM_QA_LB && 2 * NA <= FBM_NL, "one-lane engine limbs");
   // byte offset of this lane's table entry 0 (entries FBM_NL*256 words apart)
   const uint32_t tb0 = (uint32_t)(((uint64_t)blockIdx.x * FBM_TENTRIES * FBM_NL * FBM_BLOCK + tid) * 4);
   const uint32_t tstride = FBM_NL * FBM_BLOCK * 4;
@@ -610,7 +647,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
     const bool valid = ct_raw < n_ct;
     const uint64_t ct = valid ? ct_raw : n_ct - 1;
     bool wide = false;
-    {  // h -> 28-bit limbs -> scratch entry 16
+    {  // h -> 29-bit limbs -> scratch entry 16
       uint32_t h[64];
       if (SEG(key_is_zero, key_is_zero_a)) {
 #pragma unroll
@@ -618,49 +655,49 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
       } else {
         load_row64(SEG(H, H_a) + ct * 64, h);
       }
-      uint32_t h28[FBM_NL];
-      {  // h = h_lo + h_hi R (R = 2^1036): the 74-limb decomposition is (h_lo, h_hi)
-        to28<64, FBM_NL>(h, h28);
+      uint32_t h29[2 * NA];
+      {  // h = h_lo + h_hi R: the 72-limb decomposition is (h_lo, h_hi)
+        to29_row64(h, h29);
         uint32_t hi = 0;
 #pragma unroll
-        for (int k = FBM_NLN; k < FBM_NL; ++k) hi |= h28[k];
+        for (int k = NA; k < 2 * NA; ++k) hi |= h29[k];
         wide = hi != 0u;
         if (wide) {  // FDH retries (small moduli only): h_hi R^2 = (h_hi, 0) * R^3 R^-1 -> entry 1
 #pragma unroll
-          for (int k = 0; k < FBM_NLN; ++k) {
-            h28[k] = h28[FBM_NLN + k];
-            h28[FBM_NLN + k] = 0u;
+          for (int k = 0; k < NA; ++k) {
+            h29[k] = h29[NA + k];
+            h29[NA + k] = 0u;
           }
         }
       }
-      col_store(table + (tb0 + FBM_TSCRATCH * tstride) / 4, h28);
+      col_store(table + (tb0 + FBM_TSCRATCH * tstride) / 4, h29);
     }
     if (__any(wide)) {  // wave-uniform: lanes with a narrow h multiply 0 and add nothing
-      lds_store_uniform<FBM_NL>(lds, FBM_BLOCK, cst + FBM_CST_R3NA);
+      lds_store_uniform<2 * NA>(lds, FBM_BLOCK, cst + FBM_CST_QR3);
       fbm_na_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, NK, np);  // h_hi*R^2 (wide lanes)
       lds_to_glb(lds, table + (tb0 + tstride) / 4);
       uint32_t h[64];
       load_row64(SEG(H, H_a) + ct * 64, h);
-      uint32_t h28[FBM_NL];
-      to28<64, FBM_NL>(h, h28);
+      uint32_t h29[2 * NA];
+      to29_row64(h, h29);
 #pragma unroll
-      for (int k = FBM_NLN; k < FBM_NL; ++k) h28[k] = 0u;  // (h_lo, 0)
-      col_store(table + (tb0 + FBM_TSCRATCH * tstride) / 4, h28);
+      for (int k = NA; k < 2 * NA; ++k) h29[k] = 0u;  // (h_lo, 0)
+      col_store(table + (tb0 + FBM_TSCRATCH * tstride) / 4, h29);
     }
-    lds_store_uniform<FBM_NL>(lds, FBM_BLOCK, cst + FBM_CST_R2NA);
+    lds_store_uniform<2 * NA>(lds, FBM_BLOCK, cst + FBM_CST_QR2);
     fbm_na_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, NK, np);  // h*R (narrow) | h_lo*R (wide)
     if (__any(wide)) {  // h R = h_lo R + h_hi R^2: digit-wise sum (< 6N + 2, fine as an operand)
-      uint32_t a[FBM_NL], b[FBM_NL];
+      uint32_t a[2 * NA], b[2 * NA];
       lds_load_col(lds, FBM_BLOCK, a);
       col_load(table + (tb0 + tstride) / 4, b);
 #pragma unroll
       for (int d = 0; d < 2; ++d) {
         uint32_t c = 0;
 #pragma unroll
-        for (int k = 0; k < FBM_NLN; ++k) {
-          const uint32_t v = a[d * FBM_NLN + k] + (wide ? b[d * FBM_NLN + k] : 0u) + c;
-          a[d * FBM_NLN + k] = v & FBM_LMASK;
-          c = v >> FBM_LB;
+        for (int k = 0; k < NA; ++k) {
+          const uint32_t v = a[d * NA + k] + (wide ? b[d * NA + k] : 0u) + c;
+          a[d * NA + k] = k + 1 < NA ? v & FBM_QMASK : v;  // the top limb keeps the digit's excess
+          c = v >> FBM_QA_LB;
         }
       }
       lds_store_col(lds, FBM_BLOCK, a);
@@ -688,12 +725,19 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
       }
     }
     const int mode = SEG(mode, mode_a);
-    if ((mode & FBM_EXP_DEC) == 0)
-      fbm_na_mm_glb(aoff, SEG(nude, nude_a), (uint32_t)((((ct >> 8) * (FBM_NL * 256)) + (ct & 255)) * 4), NK, np);
-    else
+    if ((mode & FBM_EXP_DEC) == 0) {  // nude = (1, pt): 28-bit blocked column -> 29-bit limbs -> scratch
+      const uint32_t* nb = SEG(nude, nude_a) + (ct >> 8) * (FBM_NL * 256) + (ct & 255);
+      uint32_t a28[FBM_NL], b29[2 * NA];
+      col_load(nb, a28);
+      relimb_28_29(a28, b29);
+      relimb_28_29(a28 + FBM_NLN, b29 + NA);
+      col_store(table + (tb0 + FBM_TSCRATCH * tstride) / 4, b29);
+      fbm_na_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, NK, np);
+    } else {
       fbm_na_mm_glb(aoff, cst + FBM_CST_ONE, 0u, NK, np);
+    }
     uint32_t w[64];
-    na_final(lds, NK, w, mode & FBM_EXP_OUT_NADIC);
+    na_final(lds, cst + FBM_CST_NK, w, mode & FBM_EXP_OUT_NADIC);
     if (valid) store_row64(SEG(out, out_a) + ct * 64, w);
 #undef SEG
   }
@@ -718,7 +762,6 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
 #ifndef FBM_GROUP_WAVES  // resident group-engine waves per SIMD (= workgroups per CU): the VGPR budget
 #define FBM_GROUP_WAVES 3
 #endif
-#define FBM_QMASK ((1u << FBM_QA_LB) - 1u)
 
 // limb k (lb bits at bit lb k) of a little-endian number of `nw` words in global memory
 __device__ __forceinline__ uint32_t glb_limb(const uint32_t* p, int nw, int k, int lb) {
@@ -1491,8 +1534,7 @@ __global__ void jl_setup_kernel(JlSched sc, MontCtx mc, MontCtxN mn, NadicCtx na
     cst[FBM_CST_M + t] = t < FBM_NL ? mc.M[t] : 0u;
     cst[FBM_CST_R2 + t] = t < FBM_NL ? mc.R2[t] : 0u;
     cst[FBM_CST_NK + t] = t < 80 ? na.nk[t] : 0u;
-    cst[FBM_CST_R2NA + t] = t < FBM_NL ? na.r2na[t] : 0u;
-    cst[FBM_CST_R3NA + t] = t < FBM_NL ? na.r3na[t] : 0u;
+    cst[FBM_CST_NA29 + t] = t < 80 ? na.nk29[t] : 0u;
   }
   if (t < 64) {  // group engines: K'_i and N's 29-bit limbs
     cst[FBM_CST_QK + t] = t < FBM_QA_L ? qa.kp[t] : 0u;
@@ -1644,7 +1686,7 @@ static int jl_batch_record(const uint32_t* H, uint64_t n_ct, const JlParams& jp,
   if (bt.nseg == 0) {
     g_batch.cst = cst;
     memcpy(g_batch.n32, jp.N32, sizeof(g_batch.n32));
-    g_batch.np = jp.mn.mp;
+    g_batch.np = jp.qa.np;
   } else if (memcmp(g_batch.n32, jp.N32, sizeof(g_batch.n32)) != 0) {
     set_error("every call of a JL exponentiation batch must use the same biprime");
     return FBM_E_ARG;
@@ -1693,7 +1735,7 @@ int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const Jl
   // probe knob (tools/mixed_probe.py): extra dynamic LDS per workgroup, e.g. enough to hold the
   // one-lane engine to one workgroup per CU
   static const unsigned lds_pad = getenv("FBM_EXP_LDS_PAD") ? (unsigned)atoi(getenv("FBM_EXP_LDS_PAD")) : 0u;
-  hipLaunchKernelGGL(jl_exp_kernel<false>, dim3((unsigned)g), dim3(FBM_BLOCK), lds_pad, s, H, n_ct, (uint32_t*)cst, jp.mn.mp,
+  hipLaunchKernelGGL(jl_exp_kernel<false>, dim3((unsigned)g), dim3(FBM_BLOCK), lds_pad, s, H, n_ct, (uint32_t*)cst, jp.qa.np,
                      ops, sc.n_ops, sc.first, mode, jp.key_is_zero, nude, table, out, (const JlExpSeg*)nullptr, 0, 0u,
                      (uint32_t*)nullptr);
   return check_launch("jl_exp_kernel");

@@ -322,8 +322,8 @@ int fbm_test_gen_exp(const uint32_t* h, const uint32_t* pt, int negative, const 
 int fbm_test_gen_combine(const uint32_t* cts, int n_parties, const uint32_t* factor, const uint32_t* biprime,
                          int mode, uint32_t* out, uint32_t* err);
 /* host test hook (no GPU): the N-adic engine's per-modulus constants as the library builds
- * them -- nk: 80 words (N limbs, K'_i), r2na / r3na: 74 limbs (digits of R^2 / R^3 mod N^2,
- * R = 2^1036), np = -N^-1 mod 2^28. */
+ * them -- nk: 80 words (29-bit N limbs, K'_i), r2na / r3na: 72 limbs (29-bit digits of R^2 /
+ * R^3 mod N^2, R = 2^1044), np = -N^-1 mod 2^29. */
 int fbm_test_nadic_consts(const uint32_t* n32, uint32_t* nk, uint32_t* r2na, uint32_t* r3na, uint32_t* np);
 
 /* ---- instrumentation -------------------------------------------------------------------

@@ -3,12 +3,12 @@
 modulo N^2 in N-adic form (the Joye-Libert exponentiation engine).
 
 Why N-adic: the JL modulus is N^2 with N known (1024-bit biprime).  A residue X mod N^2 is
-carried as two 37-limb digits (x0, x1), X = x0 + x1 N (mod N^2), and since N^2 = 0 the
+carried as two 36-limb digits (x0, x1), X = x0 + x1 N (mod N^2), and since N^2 = 0 the
 product needs no x1*y1 term:
 
     X Y = x0 y0 + N (x0 y1 + x1 y0)                      (mod N^2)
 
-With R = 2^1036 (37 limbs of 28 bits) and one Montgomery reduction modulo N of x0 y0,
+With R = 2^1044 (36 limbs of 29 bits) and one Montgomery reduction modulo N of x0 y0,
 x0 y0 + m N = t R  (m = the reduction's quotient digits), we get N R^-1 = N (R^-1 mod N)
 (mod N^2) and therefore
 
@@ -18,49 +18,54 @@ i.e. the Montgomery product modulo N^2 is two interleaved Montgomery products mo
 that share their row loop: the t part reduces x0*y0 and hands its quotient digit q_i of
 row i straight to the s part, which adds (K'_i - q_i) in that row's retiring column.
 -m is taken as (R - 1 - m) + K with K = (1 - R) mod N, so every column stays non-negative:
-K'_i = (2^28 - 1) + K_i (host constants).  Per product 37 rows x (37 + 37 + 74 + 37)
-= 6 845 v_mad_u64_u32 (square: x0*x0 and x0*(2 x1): 5 476) against 10 952 / 8 288 for
-the 74-limb Montgomery product modulo N^2 (fbm_mont_asm.hpp) -- the same arithmetic
-result class at 0.63x / 0.66x of the multiplies.
+K'_i = (2^29 - 1) + K_i (host constants, the group engines' K' too).  Per product 36 rows x
+(36 + 36 + 72 + 36 + 1) + 68 (the mid-product reduction) = 6 584 v_mad_u64_u32 (square,
+triangular: 4 658) -- 4 % fewer than with 37 limbs of 28 bits (rounds 1-3: 6 882 / 4 847).
 
-Bounds (N < 2^1024, R = 2^1036 >= 2^12 N): digits < 2N in -> digits < 2N out
-(t < N + 4N^2/R, s < N + 1 + (8N^2 + N)/R).  A digit up to R - 1 in one operand (the
-hash h < 2^1036 entering as (h, 0), the plaintext digit of N*pt + 1 = (1, pt)) gives
-digits < 3N + 1, which the next product brings back below 2N.  Columns: at most
-111 products < 2^56 plus carries: < 2^63.
+Bounds (N < 2^1024, R = 2^1044 >= 2^20 N): digits < 2N in -> digits < 2N out.  A digit up to
+R - 1 in one operand (the hash h < 2^1044 entering as (h, 0), the plaintext digit of
+N*pt + 1 = (1, pt)) gives digits < 3N + 1, which the next product brings back below 2N.
+Columns: a row adds at most 2^59 (a doubled cross product, or x0 y1 + x1 y0) + 2^58 (q N) to a
+slot, so 36 rows could pass 2^64; after row 17 every slot but the youngest hands its high dword
+to the slot above (x 8 = 2^32 / 2^29) and keeps the low one -- each column then gathers at most
+19 rows' products from below 2^36: 19 * 1.5 * 2^59 + 2^58 + 2^36 < 2^64 (the simulator asserts
+it on every multiply).
 
 Register plan (per lane, wave64):
-  v[2k:2k+1]      k=0..35  t-window accumulators At_k (64-bit)
-  v[72+2k:73+2k]  k=0..35  s-window accumulators As_k
-  v144..v180      B digit 0 limbs b0_j   (square: x0)
-  v181..v217      B digit 1 limbs b1_j   (square: 2 x1, 29-bit limbs)
-  v218, v219      x0_i, x1_i of the current row;  v220, v221 the next row's (prefetch)
-  v[222:223]      Tt = retiring column of the t part;  v[224:225] Ts (s part)
-  v226 q, v227 q', v228 np = -N^-1 mod 2^28, v229 LDS address of x0_i, v230 scratch,
-  v231 K'_i - q
-  s20..s29, s36..s62   N_0..N_9, N_10..N_36 (uniform, loaded once per product)
-  s63..s99             K'_0..K'_36 (row i reads K'_i by s_movrels with m0 = i)
+  v[2k:2k+1]      k=0..34  t-window accumulators At_k (64-bit)
+  v[70+2k:71+2k]  k=0..34  s-window accumulators As_k
+  v140..v175      B digit 0 limbs b0_j
+  v176..v211      B digit 1 limbs b1_j
+  v212, v213      x0_i, x1_i of the current row;  v214, v215 the next row's (prefetch)
+  v[216:217]      Tt = retiring column of the t part;  v[218:219] Ts (s part)
+  v220 q, v221 q', v222 np = -N^-1 mod 2^29, v223 LDS address of x0_i, v224 scratch,
+  v225 K'_i - q
+  s20..s29, s36..s61   N_0..N_9, N_10..N_35 (uniform, loaded once per product)
+  s62..s97             K'_0..K'_35 (row i reads K'_i by s_movrels with m0 = i)
   s34 row counter, s35 K'_i;  vcc: unused carry-out of v_mad_u64_u32;  scc clobbered;
   m0 (reserved to the compiler) saved in s19 on entry and restored on exit.
 
-Operands: A is the lane's LDS column (limb k of the 74 at byte a_off + k*1024: rows 0..36
-digit 0, rows 37..73 digit 1; 75 rows allocated, the last row's prefetch reads row 74)
-and receives the result; B comes from global memory (uniform base + per-lane byte offset,
-limb stride 1024 B: the workgroup-blocked layout of tables and residue columns) or, for
-the square, from the A column itself.  The constants block (80 words, see
-NadicCtx in fbm_internal.hpp) holds N_0..N_9 at words 0..9 and
-N_10..N_36, K'_0..K'_36 at words 16..79.
+Operands: A is the lane's LDS column (limb k of the 72 at byte a_off + k*1024: rows 0..35
+digit 0, rows 36..71 digit 1; the last row's prefetch reads row 72) and receives the result;
+B comes from global memory (uniform base + per-lane byte offset, limb stride 1024 B: the
+workgroup-blocked layout of tables and residue columns) or, for the square, from the A
+column itself.  The constants block (80 words, FBM_CST_NA29 in fbm_internal.hpp) holds
+N_0..N_9 at words 0..9, N_10..N_35 at words 16..41 and K'_0..K'_35 at words 42..77.
 
 Usage:  python tools/gen_nadic_asm.py   (rewrites the header; the build does not run this)
 """
 
 import os
 
-L = 37
+LB = 29     # bits per limb
+L = 36      # limbs per digit (R = 2^(LB L) = 2^1044)
 NW = L - 1  # window accumulators per part
+MID = 18    # rows before the mid-product reduction
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "fedbiomed_amd", "csrc", "fbm_nadic_asm.hpp")
-MASK = "0xfffffff"
+MASK = hex((1 << LB) - 1)
+AS0 = 2 * NW            # s window of the general product
+B00, B10 = 2 * AS0, 2 * AS0 + L
 
 
 def At(k):
@@ -71,31 +76,41 @@ def AtLo(k):
     return f"v{2 * k}"
 
 
+def AtHi(k):
+    return f"v{2 * k + 1}"
+
+
 def As(k):
-    return f"v[{72 + 2 * k}:{73 + 2 * k}]"
+    return f"v[{AS0 + 2 * k}:{AS0 + 2 * k + 1}]"
 
 
 def AsLo(k):
-    return f"v{72 + 2 * k}"
+    return f"v{AS0 + 2 * k}"
+
+
+def AsHi(k):
+    return f"v{AS0 + 2 * k + 1}"
 
 
 def B0(j):
-    return f"v{144 + j}"
+    return f"v{B00 + j}"
 
 
 def B1(j):
-    return f"v{181 + j}"
+    return f"v{B10 + j}"
 
 
 def Ns(j):
     return f"s{20 + j}" if j < 10 else f"s{36 + j - 10}"
 
 
-KBASE = "s63"
-X0, X1, X0N, X1N = "v218", "v219", "v220", "v221"
-TT, TTLO, TS, TSLO = "v[222:223]", "v222", "v[224:225]", "v224"
-Q, Q2, NPV, AADR, TMP, CQ = "v226", "v227", "v228", "v229", "v230", "v231"
-ROW1 = 37 * 1024  # byte offset of digit 1 in the LDS column
+KBASE = f"s{36 + L - 10}"  # K'_0 right after N_35
+_X = B10 + L
+X0, X1, X0N, X1N = f"v{_X}", f"v{_X + 1}", f"v{_X + 2}", f"v{_X + 3}"
+TT, TTLO, TS, TSLO = f"v[{_X + 4}:{_X + 5}]", f"v{_X + 4}", f"v[{_X + 6}:{_X + 7}]", f"v{_X + 6}"
+Q, Q2, NPV, AADR, TMP, CQ = (f"v{_X + 8 + i}" for i in range(6))
+MM_NREG = _X + 14
+ROW1 = L * 1024  # byte offset of digit 1 in the LDS column
 
 
 def load_consts():
@@ -151,7 +166,7 @@ def row(first, sq):
         if j == 6:
             out.append(f"v_and_b32 {Q}, {MASK}, {Q}")
         if j == 8:
-            out.append(f"v_sub_u32 {CQ}, {kreg}, {Q}")  # K'_i - q_i  (>= 0: K'_i >= 2^28 - 1)
+            out.append(f"v_sub_u32 {CQ}, {kreg}, {Q}")  # K'_i - q_i  (>= 0: K'_i >= 2^29 - 1)
     out.append(f"v_mad_u64_u32 {TT}, vcc, {Q}, {Ns(0)}, {TT}")
     for j in range(1, L):
         out.append(f"v_mad_u64_u32 {At(j - 1)}, vcc, {Q}, {Ns(j)}, {At(j - 1)}")
@@ -179,11 +194,32 @@ def row(first, sq):
     for j in range(1, L):
         out.append(f"v_mad_u64_u32 {As(j - 1)}, vcc, {Q2}, {Ns(j)}, {As(j - 1)}")
     # ---- retire column i of both parts ----
-    out += [f"v_lshrrev_b64 {TT}, 28, {TT}", f"v_lshl_add_u64 {At(0)}, {TT}, 0, {At(0)}",
-            f"v_lshrrev_b64 {TS}, 28, {TS}", f"v_lshl_add_u64 {As(0)}, {TS}, 0, {As(0)}",
+    out += [f"v_lshrrev_b64 {TT}, {LB}, {TT}", f"v_lshl_add_u64 {At(0)}, {TT}, 0, {At(0)}",
+            f"v_lshrrev_b64 {TS}, {LB}, {TS}", f"v_lshl_add_u64 {As(0)}, {TS}, 0, {As(0)}",
             f"v_add_u32 {AADR}, 0x400, {AADR}", "s_waitcnt lgkmcnt(0)", f"v_mov_b32 {X0}, {X0N}"]
     if not sq:
         out.append(f"v_mov_b32 {X1}, {X1N}")
+    return out
+
+
+def mid_reduce(pairs):
+    """After row MID - 1: every slot (pair lo register) but the youngest keeps its low dword and
+    hands the high one to the slot above (x 8 = 2^32 / 2^29).  `pairs`: per part, the window's
+    slot pair low registers from the oldest column to the youngest."""
+    chains = []
+    for regs in pairs:
+        ch = []
+        for k in range(len(regs) - 1):
+            lo, nxt = regs[k], regs[k + 1]
+            hi = f"v{int(lo[1:]) + 1}"
+            ch += [f"v_mad_u64_u32 v[{nxt[1:]}:{int(nxt[1:]) + 1}], vcc, {hi}, 8, v[{nxt[1:]}:{int(nxt[1:]) + 1}]",
+                   f"v_mov_b32 {hi}, 0"]
+        chains.append(ch)
+    out = []
+    for k in range(max(len(c) for c in chains)):
+        for ch in chains:
+            if k < len(ch):
+                out.append(ch[k])
     return out
 
 
@@ -196,10 +232,10 @@ def normalise_store():
         return f"ds_write_b32 {TMP}, {reg} offset:{(k - 64) * 1024}"
 
     for acc, lo, carry, carry_lo, base in ((At, AtLo, TT, TTLO, 0), (As, AsLo, TS, TSLO, L)):
-        out += [f"v_lshrrev_b64 {carry}, 28, {acc(0)}", f"v_and_b32 {lo(0)}, {MASK}, {lo(0)}", st(base, lo(0))]
+        out += [f"v_lshrrev_b64 {carry}, {LB}, {acc(0)}", f"v_and_b32 {lo(0)}, {MASK}, {lo(0)}", st(base, lo(0))]
         for k in range(1, NW):
             out += [f"v_lshl_add_u64 {acc(k)}, {carry}, 0, {acc(k)}",
-                    f"v_lshrrev_b64 {carry}, 28, {acc(k)}",
+                    f"v_lshrrev_b64 {carry}, {LB}, {acc(k)}",
                     f"v_and_b32 {lo(k)}, {MASK}, {lo(k)}",
                     st(base + k, lo(k))]
         out.append(st(base + NW, carry_lo))
@@ -235,6 +271,8 @@ def product(sq):
     # s_movrels after an SALU write of m0 needs a wait state (the hazard is not checked in asm)
     body += ["s_mov_b32 s34, 1", "1:", "s_mov_b32 m0, s34", "s_nop 1", f"s_movrels_b32 s35, {KBASE}"]
     body += row(False, sq)
+    body += [f"s_cmp_lg_u32 s34, {MID - 1}", "s_cbranch_scc1 2f"]
+    body += mid_reduce([[AtLo(k) for k in range(NW)], [AsLo(k) for k in range(NW)]]) + ["2:"]
     body += ["s_add_u32 s34, s34, 1", f"s_cmp_lg_u32 s34, {L}", "s_cbranch_scc1 1b"]
     body += normalise_store()
     body += [f"s_mov_b32 m0, {M0_SAVE}", "s_nop 1"]  # m0 read right after the asm: wait state
@@ -247,19 +285,25 @@ def product(sq):
 # 2 x0_i x0_k for k > i -- a contiguous suffix of the row's t multiply sequence, entered by
 # a computed jump (s_setpc_b64; every entry is one 8-byte v_mad_u64_u32) -- and, for even i,
 # the diagonal x0_{i/2}^2 of column i (read from the LDS column along a running address:
-# rows are unrolled in odd/even pairs so the parity is static).  Diagonals of columns 38..72
+# rows are unrolled in odd/even pairs so the parity is static).  Diagonals of columns 36..70
 # are added after the loop from the B registers.  The t products are added in place
-# (At_k, k = window position) and the q*N pass shifts the window, so the t window has 37
-# pairs (At_36 is written, not accumulated, by each row's last cross product).  Column i is
+# (At_k, k = window position) and the q*N pass shifts the window, so the t window has 36
+# pairs (At_35 is written, not accumulated, by each row's last cross product).  Column i is
 # complete when its quotient is taken: cross products of column i come from rows < i, the
 # diagonal from row i itself.  The s part runs full rows of (2 x0_i) * x1 (the doubled row
-# operand serves both parts).  Column bounds: t 18 doubled products < 2^57 + 1 diagonal +
-# 37 q*N < 2^56; s 37 doubled products + 37 q'*N: < 2^63.
-# Register plan: At_k v[2k:2k+1] (k=0..36), As_k v[74+2k:75+2k] (k=0..35), b0 = x0
-# v146..v182, b1 = x1 v183..v219, x0_0 v220, next x0 v221, 2 x0_i v222, Tt v[224:225],
-# Ts v[226:227], q v228, q' v229, np v230, LDS address v231, scratch v232, K'_i - q v233,
-# diagonal limb v234, its LDS address v235;  s[30:31] jump target, s34 row, s35 K'_i / offset.
+# operand serves both parts).  Column bounds as the general product's (the mid-product
+# reduction after row 17, inside the row-pair loop).
+# Register plan: At_k v[2k:2k+1] (k=0..35), As_k v[72+2k:73+2k] (k=0..34), b0 = x0
+# v142..v177, b1 = x1 v178..v213, x0_0 v214, next x0 v215, 2 x0_i v216, Tt v[218:219],
+# Ts v[220:221], q v222, q' v223, np v224, LDS address v225, scratch v226, K'_i - q v227,
+# diagonal limb v228, its LDS address v229;  s[30:31] jump target, s34 row, s35 K'_i / offset.
 # ------------------------------------------------------------------------------------------
+SAS0 = 2 * L                  # s window of the square
+SB00 = SAS0 + 2 * NW
+SB10 = SB00 + L
+_SX = SB10 + L
+
+
 def SAt(k):
     return f"v[{2 * k}:{2 * k + 1}]"
 
@@ -269,29 +313,31 @@ def SAtLo(k):
 
 
 def SAs(k):
-    return f"v[{74 + 2 * k}:{75 + 2 * k}]"
+    return f"v[{SAS0 + 2 * k}:{SAS0 + 2 * k + 1}]"
 
 
 def SAsLo(k):
-    return f"v{74 + 2 * k}"
+    return f"v{SAS0 + 2 * k}"
 
 
 def SB0(j):
-    return f"v{146 + j}"
+    return f"v{SB00 + j}"
 
 
 def SB1(j):
-    return f"v{183 + j}"
+    return f"v{SB10 + j}"
 
 
-SX0, SX0N, SX0D = "v220", "v221", "v222"
-STT, STTLO, STS, STSLO = "v[224:225]", "v224", "v[226:227]", "v226"
-SQ, SQ2, SNPV, SAADR, STMP, SCQ, SDI, SDADDR = "v228", "v229", "v230", "v231", "v232", "v233", "v234", "v235"
+SX0, SX0N, SX0D = f"v{_SX}", f"v{_SX + 1}", f"v{_SX + 2}"
+_ST = _SX + 3 + (_SX + 3) % 2  # 64-bit pairs start on an even VGPR
+STT, STTLO, STS, STSLO = f"v[{_ST}:{_ST + 1}]", f"v{_ST}", f"v[{_ST + 2}:{_ST + 3}]", f"v{_ST + 2}"
+SQ, SQ2, SNPV, SAADR, STMP, SCQ, SDI, SDADDR = (f"v{_ST + 4 + i}" for i in range(8))
+SQ_NREG = _ST + 12
 
 
 def sq_tri(tag, first=False):
-    """Doubled cross products 2 x0_i x0_k, k = 1..36 (entered at k = i + 1 by the jump;
-    whole, with addend 0, for row 0).  k = 36 writes: the shift consumed the old top."""
+    """Doubled cross products 2 x0_i x0_k, k = 1..L-1 (entered at k = i + 1 by the jump;
+    whole, with addend 0, for row 0).  k = L-1 writes: the shift consumed the old top."""
     out = [f"v_mad_u64_u32 {SAt(k)}, vcc, {SX0D}, {SB0(k)}, {'0' if first else SAt(k)}" for k in range(1, L - 1)]
     out.append(f"v_mad_u64_u32 {SAt(L - 1)}, vcc, {SX0D}, {SB0(L - 1)}, 0")
     return out
@@ -310,10 +356,10 @@ def sq_jump(tag, offset_expr):
 
 
 def sq_row(kind, kreg="s35"):
-    """kind: 'first' (row 0), 'odd', 'even' (loop rows), 'r35' (odd, only k = 36 crosses),
-    'last' (row 36, even, no crosses).  On entry X0 = x0_i; s35 = K'_i (kreg)."""
+    """kind: 'first' (row 0), 'odd', 'even' (loop rows), 'last' (row L - 1 = 35: odd, no cross
+    products).  On entry X0 = x0_i; s35 = K'_i (kreg)."""
     first = kind == "first"
-    even = kind in ("first", "even", "last")
+    even = kind in ("first", "even")
     out = [f"ds_read_b32 {SX0N}, {SAADR} offset:1024"]
     if even:  # diagonal x0_{i/2}^2 of column i (DI holds it), then prefetch the next even row's
         out.append(f"v_mad_u64_u32 {SAt(0)}, vcc, {SDI}, {SDI}, {'0' if first else SAt(0)}")
@@ -341,8 +387,6 @@ def sq_row(kind, kreg="s35"):
         out += sq_jump("o", ["s_lshl_b32 s35, s34, 3"]) + sq_tri("o")
     elif kind == "even":
         out += sq_jump("e", ["s_add_u32 s35, s34, 1", "s_lshl_b32 s35, s35, 3"]) + sq_tri("e")
-    elif kind == "r35":
-        out.append(f"v_mad_u64_u32 {SAt(L - 1)}, vcc, {SX0D}, {SB0(L - 1)}, 0")
     # ---- t: q * N (shifting the window);  s: q' * N ----
     top = "0" if kind == "last" else SAt(L - 1)
     out.append(f"v_mad_u64_u32 {STT}, vcc, {SQ}, {Ns(0)}, {SAt(0)}")
@@ -351,8 +395,8 @@ def sq_row(kind, kreg="s35"):
     out.append(f"v_mad_u64_u32 {STS}, vcc, {SQ2}, {Ns(0)}, {STS}")
     for j in range(1, L):
         out.append(f"v_mad_u64_u32 {SAs(j - 1)}, vcc, {SQ2}, {Ns(j)}, {SAs(j - 1)}")
-    out += [f"v_lshrrev_b64 {STT}, 28, {STT}", f"v_lshl_add_u64 {SAt(0)}, {STT}, 0, {SAt(0)}",
-            f"v_lshrrev_b64 {STS}, 28, {STS}", f"v_lshl_add_u64 {SAs(0)}, {STS}, 0, {SAs(0)}",
+    out += [f"v_lshrrev_b64 {STT}, {LB}, {STT}", f"v_lshl_add_u64 {SAt(0)}, {STT}, 0, {SAt(0)}",
+            f"v_lshrrev_b64 {STS}, {LB}, {STS}", f"v_lshl_add_u64 {SAs(0)}, {STS}, 0, {SAs(0)}",
             f"v_add_u32 {SAADR}, 0x400, {SAADR}", "s_waitcnt lgkmcnt(0)", f"v_lshlrev_b32 {SX0D}, 1, {SX0N}"]
     return out
 
@@ -374,15 +418,19 @@ def square_tri():
     body += [f"v_mov_b32 {SNPV}, %[np]", f"v_mov_b32 {SAADR}, %[a]", f"ds_read_b32 {SX0}, %[a]",
              f"ds_read_b32 {SDI}, %[a]", f"v_mov_b32 {SDADDR}, %[a]", "s_waitcnt lgkmcnt(0)",
              f"v_lshlrev_b32 {SX0D}, 1, {SX0}"]
+    assert L % 2 == 0 and (MID - 1) % 2 == 1  # rows 1 .. L-2 in (odd, even) pairs, row L-1 peeled
     body += sq_row("first", kreg=KBASE)
     body += ["s_mov_b32 s34, 1", "1:"]
     body += krow(["s_mov_b32 m0, s34"]) + sq_row("odd")
+    # after row MID - 1 (odd): the mid-product reduction (the t window's top pair is dead here --
+    # the next row's last cross product writes it -- and the s window's youngest is kept)
+    body += [f"s_cmp_lg_u32 s34, {MID - 1}", "s_cbranch_scc1 2f"]
+    body += mid_reduce([[SAtLo(k) for k in range(L - 1)], [SAsLo(k) for k in range(NW)]]) + ["2:"]
     body += krow(["s_add_u32 m0, s34, 1"]) + sq_row("even")
-    body += ["s_add_u32 s34, s34, 2", f"s_cmp_lg_u32 s34, {L - 2}", "s_cbranch_scc1 1b"]
-    body += krow(["s_mov_b32 m0, 35"]) + sq_row("r35")
-    body += krow(["s_mov_b32 m0, 36"]) + sq_row("last")
-    # diagonals of columns 38..72: column 2h sits at window position 2h - 37
-    body += [f"v_mad_u64_u32 {SAt(2 * h - L)}, vcc, {SB0(h)}, {SB0(h)}, {SAt(2 * h - L)}" for h in range(19, L)]
+    body += ["s_add_u32 s34, s34, 2", f"s_cmp_lg_u32 s34, {L - 1}", "s_cbranch_scc1 1b"]
+    body += krow([f"s_mov_b32 m0, {L - 1}"]) + sq_row("last")
+    # diagonals of columns L .. 2L-2 (h >= L/2): column 2h sits at window position 2h - L
+    body += [f"v_mad_u64_u32 {SAt(2 * h - L)}, vcc, {SB0(h)}, {SB0(h)}, {SAt(2 * h - L)}" for h in range(L // 2, L)]
     body.append(f"v_add_u32 {STMP}, 0x10000, %[a]")
 
     def st(k, reg):
@@ -391,10 +439,10 @@ def square_tri():
         return f"ds_write_b32 {STMP}, {reg} offset:{(k - 64) * 1024}"
 
     for acc, lo, carry, carry_lo, base in ((SAt, SAtLo, STT, STTLO, 0), (SAs, SAsLo, STS, STSLO, L)):
-        body += [f"v_lshrrev_b64 {carry}, 28, {acc(0)}", f"v_and_b32 {lo(0)}, {MASK}, {lo(0)}", st(base, lo(0))]
+        body += [f"v_lshrrev_b64 {carry}, {LB}, {acc(0)}", f"v_and_b32 {lo(0)}, {MASK}, {lo(0)}", st(base, lo(0))]
         for k in range(1, NW):
             body += [f"v_lshl_add_u64 {acc(k)}, {carry}, 0, {acc(k)}",
-                     f"v_lshrrev_b64 {carry}, 28, {acc(k)}",
+                     f"v_lshrrev_b64 {carry}, {LB}, {acc(k)}",
                      f"v_and_b32 {lo(k)}, {MASK}, {lo(k)}",
                      st(base + k, lo(k))]
         body.append(st(base + NW, carry_lo))
@@ -403,13 +451,18 @@ def square_tri():
 
 
 def sq_mads():
-    """v_mad_u64_u32 per square (triangular t part)."""
+    """v_mad_u64_u32 per square: triangular t part (cross products + diagonals), the s part's
+    (2 x0) x1 and K' - q, the two q N passes, the mid-product reduction."""
     cross = L * (L - 1) // 2
-    return cross + L + L * L + (L * L + L + L * L)
+    return cross + L + L * L + (L * L + L + L * L) + (L - 2) + (NW - 1)
+
+
+def mm_mads():
+    return L * (5 * L + 1) + 2 * (NW - 1)
 
 
 def clobbers():
-    regs = [f'"v{i}"' for i in range(236)]
+    regs = [f'"v{i}"' for i in range(max(MM_NREG, SQ_NREG))]
     regs += [f'"s{i}"' for i in [16, 17] + list(range(19, 32)) + [34, 35] + list(range(36, 100))]
     out = [", ".join(regs[i:i + 16]) for i in range(0, len(regs), 16)]
     return " \\\n  ".join(x + "," for x in out[:-1]) + " \\\n  " + out[-1]
@@ -428,23 +481,25 @@ def main():
     mm_row, sq_body = row(False, False), sq_row("odd")
     hdr = f"""// GENERATED by tools/gen_nadic_asm.py -- do not edit by hand.
 //
-// gfx950 assembly Montgomery product modulo N^2 in N-adic form: a residue is two 37-limb
-// digits (x0, x1), X = x0 + x1 N (mod N^2), radix 2^28, R = 2^1036.
-//   a (per-lane LDS column, 74 limbs) <- a * b * R^-1 (mod N^2), digits lazily < 2N.
+// gfx950 assembly Montgomery product modulo N^2 in N-adic form: a residue is two {L}-limb
+// digits (x0, x1), X = x0 + x1 N (mod N^2), radix 2^{LB}, R = 2^{LB * L}.
+//   a (per-lane LDS column, {2 * L} limbs) <- a * b * R^-1 (mod N^2), digits lazily < 2N.
 // See tools/gen_nadic_asm.py for the arithmetic, the bounds and the register plan.
 // {len(mm)} instructions (general, B from global), {len(sq)} (square, triangular x0^2); row
-// bodies {len(mm_row)} / <= {len(sq_body)} instructions; {L * count_mads(mm_row)} / {sq_mads()} v_mad_u64_u32 per product.
+// bodies {len(mm_row)} / <= {len(sq_body)} instructions; {mm_mads()} / {sq_mads()} v_mad_u64_u32 per product.
 #pragma once
 #include <stdint.h>
 
-#define FBM_NA_MADS_MUL {L * count_mads(mm_row)}
+#define FBM_NA_LIMB_BITS {LB}
+#define FBM_NA_LIMBS {L}
+#define FBM_NA_MADS_MUL {mm_mads()}
 #define FBM_NA_MADS_SQR {sq_mads()}
 
 #define FBM_NA_CLOBBERS \\
   {clobbers()}
 
 // B operand from global memory: limb k at bb + b_off + k*1024 (bytes; bb uniform).
-// NK: the 80-word constants block (N limbs, K'_i); np = -N^-1 mod 2^28.
+// NK: the 80-word constants block (N limbs, K'_i); np = -N^-1 mod 2^{LB}.
 __device__ __forceinline__ void fbm_na_mm_glb(uint32_t a_off, const uint32_t* bb, uint32_t b_off,
                                               const uint32_t* NK, uint32_t np) {{
   asm volatile(
@@ -465,7 +520,7 @@ __device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK
 }}
 #else
 // A/B variant (-DFBM_NA_PLAIN_SQUARE): the general product with B = A from LDS -- no computed
-// jumps, {L * count_mads(row(False, True))} multiplies instead of {sq_mads()}.
+// jumps, {L * count_mads(row(False, True)) + 2 * (NW - 1)} multiplies instead of {sq_mads()}.
 __device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK, uint32_t np) {{
   asm volatile(
 {c_string(product(True))}
@@ -478,7 +533,7 @@ __device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK
     with open(OUT, "w") as f:
         f.write(hdr)
     print(f"wrote {OUT}: general {len(mm)} / square {len(sq)} instructions; "
-          f"mads/product {L * count_mads(mm_row)} / {sq_mads()}")
+          f"mads/product {mm_mads()} / {sq_mads()}")
 
 
 if __name__ == "__main__":
