@@ -565,6 +565,7 @@ static void jl_rk_for(const uint32_t* n32, int n_parties, JlRk& r) {
 // Left-to-right sliding window (width FBM_WIN) over |key|, odd-power table.
 static int build_schedule(const uint32_t* key, JlSched& sc, int& is_zero) {
   memset(&sc, 0, sizeof(sc));
+  sc.sbits = -1;  // (build_short)
   Big K(key, key + 64);
   const int nb = big_bits(K);
   is_zero = nb == 0;
@@ -609,6 +610,169 @@ static int build_schedule(const uint32_t* key, JlSched& sc, int& is_zero) {
     pending_sq -= nsq;
   }
   return FBM_OK;
+}
+
+// ---- the short path's constants (JlShort, fbm_internal.hpp) ------------------------------
+// 2^E mod m for an odd m of at most 2048 bits and any E: left-to-right, Montgomery squarings
+// (64-bit limbs) and modular doublings -- ~2 050 products for the ~2 050-bit E of a 2 040-bit key
+static Big pow2_mod_big(const Big& E, Big m) {
+  big_trim(m);
+  const int n = (int)((m.size() + 1) / 2);
+  uint64_t M[32] = {0};
+  for (size_t i = 0; i < m.size(); ++i) M[i / 2] |= (uint64_t)m[i] << (32 * (i & 1));
+  uint64_t inv = M[0];  // Newton: M^-1 mod 2^64
+  for (int i = 0; i < 6; ++i) inv *= 2u - M[0] * inv;
+  const uint64_t mi = 0u - inv;
+  auto ge_sub = [&](uint64_t* a, uint64_t top) {  // a <- a - M if (top:a) >= M
+    bool ge = top != 0;
+    if (!ge) {
+      ge = true;
+      for (int k = n - 1; k >= 0; --k)
+        if (a[k] != M[k]) {
+          ge = a[k] > M[k];
+          break;
+        }
+    }
+    if (!ge) return;
+    unsigned __int128 br = 0;
+    for (int k = 0; k < n; ++k) {
+      const unsigned __int128 d = (unsigned __int128)a[k] - M[k] - br;
+      a[k] = (uint64_t)d;
+      br = (d >> 64) & 1u;
+    }
+  };
+  auto mul = [&](const uint64_t* a, const uint64_t* b, uint64_t* r) {  // a b 2^-64n mod M (CIOS)
+    uint64_t t[34] = {0};
+    for (int i = 0; i < n; ++i) {
+      unsigned __int128 c = 0;
+      for (int j = 0; j < n; ++j) {
+        c += (unsigned __int128)a[j] * b[i] + t[j];
+        t[j] = (uint64_t)c;
+        c >>= 64;
+      }
+      c += t[n];
+      t[n] = (uint64_t)c;
+      t[n + 1] = (uint64_t)(c >> 64);
+      const uint64_t q = t[0] * mi;
+      c = ((unsigned __int128)q * M[0] + t[0]) >> 64;
+      for (int j = 1; j < n; ++j) {
+        c += (unsigned __int128)q * M[j] + t[j];
+        t[j - 1] = (uint64_t)c;
+        c >>= 64;
+      }
+      c += t[n];
+      t[n - 1] = (uint64_t)c;
+      t[n] = t[n + 1] + (uint64_t)(c >> 64);
+    }
+    ge_sub(t, t[n]);
+    for (int k = 0; k < n; ++k) r[k] = t[k];
+  };
+  auto dbl = [&](uint64_t* a) {
+    uint64_t c = 0;
+    for (int k = 0; k < n; ++k) {
+      const uint64_t nc = a[k] >> 63;
+      a[k] = (a[k] << 1) | c;
+      c = nc;
+    }
+    ge_sub(a, c);
+  };
+  uint64_t x[32] = {0};
+  x[0] = 1;
+  for (int i = 0; i < 64 * n; ++i) dbl(x);  // 1 in Montgomery form
+  for (int b = big_bits(E) - 1; b >= 0; --b) {
+    mul(x, x, x);
+    if ((E[b >> 5] >> (b & 31)) & 1u) dbl(x);
+  }
+  uint64_t one[32] = {0};
+  one[0] = 1;
+  mul(x, one, x);
+  Big r(2 * (size_t)n, 0u);
+  for (int k = 0; k < n; ++k) {
+    r[2 * k] = (uint32_t)x[k];
+    r[2 * k + 1] = (uint32_t)(x[k] >> 32);
+  }
+  return r;
+}
+
+struct JlShortCacheEntry {
+  uint32_t n32[32];
+  uint32_t key[64];
+  uint32_t corr[72];
+};
+static std::vector<JlShortCacheEntry> g_short_cache;  // guarded by g_jp_mu, at most 32
+
+// The short path (jl_exp_kernel): possible for N > 2^262 (D = N - 2^261 > the product's quotient
+// m < 2^261); used with a nonzero key.  Returns whether N qualifies (then sh.d is valid and the
+// constants block gets it); sets sc.sbits and sh.kw / sh.corr when the key does too.
+static bool build_short(const uint32_t* biprime, const uint32_t* key, int is_zero, JlSched& sc, JlShort& sh) {
+  memset(&sh, 0, sizeof(sh));
+  sc.sbits = -1;
+  Big N(biprime, biprime + 32);
+  big_trim(N);
+  const int KSB = FBM_QA_LB * FBM_NA_SHORT_LIMBS;  // 261
+  if (big_bits(N) < KSB + 2 || !(N[0] & 1u)) return false;
+  {  // D = N - 2^261
+    Big D(N.begin(), N.end());
+    Big p(KSB / 32 + 1, 0u);
+    p[KSB / 32] = 1u << (KSB % 32);
+    big_sub_inplace(D, p);
+    to_limbs_host(D, sh.d, FBM_QA_L, FBM_QA_LB);
+  }
+  if (is_zero) return true;
+  Big K(key, key + 64);
+  const int nb = big_bits(K);
+  for (int i = 0; i < 64; ++i) sh.kw[i] = key[i];
+  sc.sbits = nb - 1;
+  {
+    std::lock_guard<std::mutex> lk(g_jp_mu);
+    for (const JlShortCacheEntry& e : g_short_cache)
+      if (memcmp(e.n32, biprime, sizeof(e.n32)) == 0 && memcmp(e.key, key, sizeof(e.key)) == 0) {
+        memcpy(sh.corr, e.corr, sizeof(sh.corr));
+        return true;
+      }
+  }
+  // E = L (2^s + 1) + 261 (|key| - 2^s), L = 1044, s = nb - 1: the chain leaves h^|key| 2^-(E - 2L)
+  const int s = nb - 1;
+  Big v(K.begin(), K.end());
+  v[s >> 5] &= ~(1u << (s & 31));
+  Big E(66, 0u);
+  uint64_t c = 0;
+  for (int i = 0; i < 64; ++i) {  // 261 v
+    c += (uint64_t)v[i] * (uint64_t)KSB;
+    E[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  E[64] = (uint32_t)c;
+  auto add_at = [&](uint64_t val, int bit) {  // E += val << bit
+    const int w = bit >> 5, sh2 = bit & 31;
+    unsigned __int128 add = (unsigned __int128)val << sh2;
+    uint64_t cy = 0;
+    for (int i = w; i < (int)E.size(); ++i) {
+      const uint64_t t = (uint64_t)E[i] + (uint64_t)(uint32_t)add + cy;
+      E[i] = (uint32_t)t;
+      cy = t >> 32;
+      add >>= 32;
+      if (!add && !cy) break;
+    }
+  };
+  const int Lb = FBM_QA_L * FBM_QA_LB;  // 1044
+  add_at((uint64_t)Lb, s);
+  add_at((uint64_t)Lb, 0);
+  Big M = big_mul(N, N);
+  big_trim(M);
+  const Big C = pow2_mod_big(E, M);
+  Big q, r;
+  big_divmod(C, N, q, r);
+  to_limbs_host(r, sh.corr, FBM_QA_L, FBM_QA_LB);
+  to_limbs_host(q, sh.corr + FBM_QA_L, FBM_QA_L, FBM_QA_LB);
+  JlShortCacheEntry e;
+  memcpy(e.n32, biprime, sizeof(e.n32));
+  memcpy(e.key, key, sizeof(e.key));
+  memcpy(e.corr, sh.corr, sizeof(e.corr));
+  std::lock_guard<std::mutex> lk(g_jp_mu);
+  if (g_short_cache.size() >= 32) g_short_cache.erase(g_short_cache.begin());
+  g_short_cache.push_back(e);
+  return true;
 }
 
 static uint64_t table_slots_for(uint64_t n_ct) {
@@ -683,7 +847,9 @@ extern "C" {
 int fbm_abi_version(void) { return FBM_ABI_VERSION; }
 
 int fbm_jl_window(void) { return FBM_WIN; }
-int fbm_jl_mads(int square) { return square ? FBM_NA_MADS_SQR : FBM_NA_MADS_MUL; }
+int fbm_jl_mads(int square) {  // 0: general product, 1: square, 2: short-base product
+  return square == 2 ? FBM_NA_MADS_SHORT : square ? FBM_NA_MADS_SQR : FBM_NA_MADS_MUL;
+}
 int fbm_jl_quad_mads(int square) { return 4 * (square ? FBM_QA_MADS_SQR : FBM_QA_MADS_MUL); }
 int fbm_jl_triple_mads(int square) { return 3 * (square ? FBM_TA_MADS_SQR : FBM_TA_MADS_MUL); }
 
@@ -838,7 +1004,7 @@ int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t tot
 uint64_t fbm_jl_encrypt_workspace(uint64_t n_ct) {
   const uint64_t slots = table_slots_for(n_ct);
   (void)slots;
-  return align256(FBM_MAX_OPS * 4) + align256(FBM_CST_WORDS * 4) + align256(n_ct * 32 * 4) +
+  return align256(FBM_OPS_WORDS * 4) + align256(FBM_CST_WORDS * 4) + align256(n_ct * 32 * 4) +
          align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4) + 2 * align256(n_ct * 64 * 4) + align256(n_ct * 32 * 4) +
          align256(jl_table_bytes(n_ct));
 }
@@ -846,7 +1012,7 @@ uint64_t fbm_jl_encrypt_workspace(uint64_t n_ct) {
 uint64_t fbm_jl_aggregate_workspace(uint64_t n_ct) {
   const uint64_t slots = table_slots_for(n_ct);
   (void)slots;
-  return align256(FBM_MAX_OPS * 4) + align256(FBM_CST_WORDS * 4) + align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4) +
+  return align256(FBM_OPS_WORDS * 4) + align256(FBM_CST_WORDS * 4) + align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4) +
          3 * align256(n_ct * 64 * 4) + align256(n_ct * 32 * 4) + align256(jl_table_bytes(n_ct));
 }
 
@@ -907,8 +1073,8 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
     if ((rc = build_gen_ctx(biprime, key, key_negative, g)) || (rc = fdh_params_for_biprime(biprime, tau, ct_offset, fp)))
       return rc;
     uint8_t* ws = (uint8_t*)workspace;  // the encrypt workspace's cst | pt | (nude) | H
-    uint32_t* cst = (uint32_t*)(ws + align256(FBM_MAX_OPS * 4));
-    uint32_t* pt = (uint32_t*)(ws + align256(FBM_MAX_OPS * 4) + align256(FBM_CST_WORDS * 4));
+    uint32_t* cst = (uint32_t*)(ws + align256(FBM_OPS_WORDS * 4));
+    uint32_t* pt = (uint32_t*)(ws + align256(FBM_OPS_WORDS * 4) + align256(FBM_CST_WORDS * 4));
     uint32_t* H = (uint32_t*)((uint8_t*)pt + align256(n_ct * 32 * 4) + align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4));
     const uint32_t* ptp = x_dtype == FBM_PT ? (const uint32_t*)x : pt;
     if (phase & 1) {
@@ -931,10 +1097,12 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
     return rc;
   }
   jp.key_is_zero = is_zero;
+  JlShort sh;
+  const bool shq = build_short(biprime, key, is_zero, sc, sh);
   const uint64_t slots = table_slots_for(n_ct);
   uint8_t* ws = (uint8_t*)workspace;
   uint32_t* ops = (uint32_t*)ws;
-  uint64_t off = align256(FBM_MAX_OPS * 4);
+  uint64_t off = align256(FBM_OPS_WORDS * 4);
   uint32_t* cst = (uint32_t*)(ws + off);
   off += align256(FBM_CST_WORDS * 4);
   uint32_t* pt = (uint32_t*)(ws + off);
@@ -950,7 +1118,8 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
   uint32_t* Y = (uint32_t*)(ws + off);
   const bool inverse = key_negative && !is_zero;
   if (phase & 1) {
-    if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s); }))) return rc;
+    if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s, shq ? &sh : nullptr); })))
+      return rc;
     if (x_dtype != FBM_PT &&
         (rc = timed("jl_pack", s, [&] { return launch_jl_pack(x, x_dtype, n, qp, weight, es, cr, n_ct, pt, stats, s); })))
       return rc;
@@ -1013,7 +1182,7 @@ static JlAggWs agg_ws(void* workspace, uint64_t n_ct) {
   w.slots = table_slots_for(n_ct);
   uint64_t off = 0;
   w.ops = (uint32_t*)ws;
-  off += align256(FBM_MAX_OPS * 4);
+  off += align256(FBM_OPS_WORDS * 4);
   w.cst = (uint32_t*)(ws + off);
   off += align256(FBM_CST_WORDS * 4);
   w.X = (uint32_t*)(ws + off);
@@ -1058,10 +1227,13 @@ static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t
     return rc;
   }
   jp.key_is_zero = is_zero;
+  JlShort sh;
+  const bool shq = build_short(biprime, key, is_zero, sc, sh);
   const bool inv = key_negative && !is_zero;
   uint32_t* E = inv ? w.E : factor;
   if (phase & 1) {
-    if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, w.ops, w.cst, s); }))) return rc;
+    if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, w.ops, w.cst, s, shq ? &sh : nullptr); })))
+      return rc;
     if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, w.H, stats, s); }))) return rc;
   }
   if (phase & 2) {
@@ -1346,7 +1518,7 @@ int fbm_jl_powmod(const uint32_t* h, const uint32_t* pt, uint64_t n_ct, const ui
   }
   uint8_t* ws = (uint8_t*)workspace;  // fbm_jl_encrypt_workspace: ops | cst | pt | nude | H | table | H^-1 | y
   uint32_t* ops = (uint32_t*)ws;
-  uint64_t off = align256(FBM_MAX_OPS * 4);
+  uint64_t off = align256(FBM_OPS_WORDS * 4);
   uint32_t* cst = (uint32_t*)(ws + off);
   off += align256(FBM_CST_WORDS * 4) + align256(n_ct * 32 * 4);
   uint32_t* nude = (uint32_t*)(ws + off);
@@ -1370,8 +1542,11 @@ int fbm_jl_powmod(const uint32_t* h, const uint32_t* pt, uint64_t n_ct, const ui
     return rc;
   }
   jp.key_is_zero = is_zero;
+  JlShort sh;
+  const bool shq = build_short(biprime, key, is_zero, sc, sh);
   const uint64_t slots = table_slots_for(n_ct);
-  if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s); }))) return rc;
+  if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s, shq ? &sh : nullptr); })))
+    return rc;
   const int mode = pt ? 0 : FBM_EXP_DEC;
   if (pt && (rc = timed("jl_nude", s, [&] { return launch_jl_nude(pt, n_ct, jp, 0, nude, s); }))) return rc;
   if (key_negative && !is_zero) {  // powmod with a negative exponent: (h^|key|)^-1, then * nude

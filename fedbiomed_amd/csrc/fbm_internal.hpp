@@ -63,6 +63,11 @@ int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t 
 #define FBM_MAX_OPS 512
 #define FBM_TENTRIES (FBM_TABLE + 1)    // + one scratch column (h, then h^2)
 #define FBM_TSCRATCH FBM_TABLE
+// the per-call ops buffer: the sliding-window ops, then the short path's exponent words (|key|,
+// 64 words) and its correction constant C (N-adic digits, 72 29-bit limbs; JlSched::corr)
+#define FBM_OPS_KW FBM_MAX_OPS
+#define FBM_OPS_CORR (FBM_MAX_OPS + 64)
+#define FBM_OPS_WORDS (FBM_MAX_OPS + 64 + 128)
 
 // per-call device constants (words): M, R^2 (74 limbs, padded to 128), the broadcast
 // column 1 (limb k at word k*256) and R^(P+1) mod M (the aggregate's uniform first operand,
@@ -89,14 +94,28 @@ int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t 
 // jl_lift, read through device memory (a laundered pointer into the by-value JlParams
 // kernel argument would make the compiler copy all 3.3 KB of it to scratch per lane)
 #define FBM_CST_MN (FBM_CST_QR3 + 128)
-#define FBM_CST_WORDS (FBM_CST_MN + 128)
+// the short-base product's pairs (D_j, 0), D = N - 2^(29 * 9) (72 words; JlShort::d)
+#define FBM_CST_QD (FBM_CST_MN + 128)
+#define FBM_CST_WORDS (FBM_CST_QD + 128)
 
 // sliding-window schedule, passed by value (kernarg segment -> scalar loads).
 // op k (u16): (squarings before the multiply) << FBM_OP_SHIFT | (table index + 1, 0 = none)
+// sbits: the SHORT path (below) takes bit length of |key| - 1 squarings; -1 = no short path.
 struct JlSched {
   int n_ops;
   int first;       // table index of the leading window
   uint16_t op[FBM_MAX_OPS];
+  int sbits;
+};
+// The SHORT path (one FDH digest h < 2^261, N > 2^262): left-to-right binary over |key| with the
+// short-base product (fbm_na_ms_glb) -- kw = |key|'s words, corr = C = 2^(1044 (2^sbits + 1) +
+// 261 (|key| - 2^sbits)) mod N^2 as N-adic digits (the constant whose product turns the chain's
+// h^|key| 2^-f into h^|key| R), d = N - 2^261 (the short product's s-window start).  Written by
+// jl_short_setup_kernel into the ops buffer (kw, corr) and the constants block (d).
+struct JlShort {
+  uint32_t kw[64];
+  uint32_t corr[72];
+  uint32_t d[36];
 };
 
 // N-adic constants.  nk: N's 28-bit limbs, words 0..9 = N_0..N_9, 16..42 = N_10..N_36 (the
@@ -145,7 +164,8 @@ int launch_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, uint64_t* 
 int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, int negative, uint32_t* nude,
                    hipStream_t s);
 int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s);
-int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32_t* cst, hipStream_t s);
+int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32_t* cst, hipStream_t s,
+                    const JlShort* sh = nullptr);
 // one exponentiation launch over several calls' ciphertexts (jl_exp_kernel<true> segments)
 #define FBM_EXP_MAXSEG 24
 struct JlExpSeg {
@@ -156,6 +176,7 @@ struct JlExpSeg {
   uint64_t n_ct;
   uint32_t chunk0;  // first chunk of this segment in the launch's chunk sequence
   int n_ops, first, mode, key_is_zero;
+  int sbits;        // JlSched::sbits (the short path's exponent bits - 1, or -1)
 };
 struct JlExpBatch {
   int nseg;

@@ -605,7 +605,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
                                                              uint32_t* __restrict__ cst, uint32_t np,
                                                              const uint32_t* __restrict__ ops_a, int n_ops_a,
                                                              int first_a, int mode_a, int key_is_zero_a,
-                                                             const uint32_t* __restrict__ nude_a,
+                                                             int sbits_a, const uint32_t* __restrict__ nude_a,
                                                              uint32_t* __restrict__ table,
                                                              uint32_t* __restrict__ out_a,
                                                              const JlExpSeg* __restrict__ segs, int nseg,
@@ -616,6 +616,10 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
   uint32_t* lds = lds_a + tid;
   const uint32_t aoff = lds_addr(lds);
   const uint32_t* NK = cst + FBM_CST_NA29;
+  // the short-base product's pairs (D_j, 0) in LDS row FBM_NL (no product touches it; the
+  // chunk loop's first barrier orders the writes before any read)
+  const uint32_t doff = lds_addr(lds_a + FBM_NL * FBM_BLOCK);
+  if (tid < 72) lds_a[FBM_NL * FBM_BLOCK + tid] = launder_s(cst)[FBM_CST_QD + tid];
   constexpr int NA = FBM_NA_LIMBS;
   static_assert(NA == FBM_QA_L && FBM_NA_LIMB_BITS == FBM_QA_LB && 2 * NA <= FBM_NL, "one-lane engine limbs");
   // byte offset of this lane's table entry 0 (entries FBM_NL*256 words apart)
@@ -646,7 +650,8 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
     const uint64_t ct_raw = (uint64_t)(chunk - (BATCH ? uniform_val(segs[si].chunk0) : 0u)) * FBM_BLOCK + tid;
     const bool valid = ct_raw < n_ct;
     const uint64_t ct = valid ? ct_raw : n_ct - 1;
-    bool wide = false;
+    bool wide = false, shortp = false;
+    const int sbits = SEG(sbits, sbits_a);
     {  // h -> 29-bit limbs -> scratch entry 16
       uint32_t h[64];
       if (SEG(key_is_zero, key_is_zero_a)) {
@@ -658,10 +663,16 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
       uint32_t h29[2 * NA];
       {  // h = h_lo + h_hi R: the 72-limb decomposition is (h_lo, h_hi)
         to29_row64(h, h29);
-        uint32_t hi = 0;
+        uint32_t hi = 0, mid = 0;
 #pragma unroll
         for (int k = NA; k < 2 * NA; ++k) hi |= h29[k];
+#pragma unroll
+        for (int k = FBM_NA_SHORT_LIMBS; k < NA; ++k) mid |= h29[k];
         wide = hi != 0u;
+        // the short path (binary chain, short-base products): every lane's h below 2^261 -- one
+        // FDH digest, always for a 1024-bit N -- and a schedule for it (sbits >= 0: N > 2^262, key != 0)
+        shortp = sbits >= 0 && !SEG(key_is_zero, key_is_zero_a) && !__any(wide || mid != 0u);
+        if (shortp) lds_store_col(lds, FBM_BLOCK, h29);  // A = (h, 0), raw (no Montgomery form)
         if (wide) {  // FDH retries (small moduli only): h_hi R^2 = (h_hi, 0) * R^3 R^-1 -> entry 1
 #pragma unroll
           for (int k = 0; k < NA; ++k) {
@@ -672,6 +683,24 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
       }
       col_store(table + (tb0 + FBM_TSCRATCH * tstride) / 4, h29);
     }
+    if (shortp) {
+      // left-to-right binary over |key| below its top bit: a squaring per bit, a short-base
+      // product (x h 2^-261) per 1 bit, then C = 2^f R^2 (host-built, ops buffer) turns the
+      // chain's h^|key| 2^-f into h^|key| R -- 1 305 multiplies per 1 bit instead of a window
+      // table's 31 + ~293 general products of 6 584 and its per-lane table traffic
+      const uint32_t* kw = SEG(ops, ops_a) + FBM_OPS_KW;
+      uint32_t w = 0;
+#pragma unroll 1
+      for (int j = sbits - 1; j >= 0; --j) {
+        if (j == sbits - 1 || (j & 31) == 31)  // one exponent word per 32 bits, loaded ahead of the squaring
+          w = __builtin_amdgcn_readfirstlane(launder_s(kw)[j >> 5]);
+        fbm_na_sq_lds(aoff, NK, np);
+        if ((w >> (j & 31)) & 1u) fbm_na_ms_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, doff, NK, np);
+      }
+      lds_to_glb(lds, table + tb0 / 4);  // the chain -> entry 0; A <- C (uniform)
+      lds_store_uniform<2 * NA>(lds, FBM_BLOCK, SEG(ops, ops_a) + FBM_OPS_CORR);
+      fbm_na_mm_glb(aoff, table, tb0, NK, np);
+    } else {
     if (__any(wide)) {  // wave-uniform: lanes with a narrow h multiply 0 and add nothing
       lds_store_uniform<2 * NA>(lds, FBM_BLOCK, cst + FBM_CST_QR3);
       fbm_na_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, NK, np);  // h_hi*R^2 (wide lanes)
@@ -724,6 +753,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
         if (idx >= 0) fbm_na_mm_glb(aoff, table, tb0 + (uint32_t)idx * tstride, NK, np);
       }
     }
+    }  // (table path)
     const int mode = SEG(mode, mode_a);
     if ((mode & FBM_EXP_DEC) == 0) {  // nude = (1, pt): 28-bit blocked column -> 29-bit limbs -> scratch
       const uint32_t* nb = SEG(nude, nude_a) + (ct >> 8) * (FBM_NL * 256) + (ct & 255);
@@ -1550,9 +1580,22 @@ __global__ void jl_setup_kernel(JlSched sc, MontCtx mc, MontCtxN mn, NadicCtx na
   }
 }
 
-int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32_t* cst, hipStream_t s) {
+// the short path's per-call words: |key| and C into the ops buffer, the pairs (D_j, 0) into the
+// constants block
+__global__ void jl_short_setup_kernel(JlShort sh, uint32_t* __restrict__ ops, uint32_t* __restrict__ cst) {
+  const int t = threadIdx.x;
+  if (t < 64) ops[FBM_OPS_KW + t] = sh.kw[t];
+  if (t < 72) ops[FBM_OPS_CORR + t] = sh.corr[t];
+  if (t < 72) cst[FBM_CST_QD + t] = (t & 1) ? 0u : sh.d[t >> 1];
+}
+
+int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32_t* cst, hipStream_t s,
+                    const JlShort* sh) {
   hipLaunchKernelGGL(jl_setup_kernel, dim3(1), dim3(256), 0, s, sc, jp.mc, jp.mn, jp.na, jp.qa, ops, cst);
-  return check_launch("jl_setup_kernel");
+  int rc = check_launch("jl_setup_kernel");
+  if (rc || !sh) return rc;
+  hipLaunchKernelGGL(jl_short_setup_kernel, dim3(1), dim3(128), 0, s, *sh, ops, cst);
+  return check_launch("jl_short_setup_kernel");
 }
 
 // ---- exponentiation engine choice ------------------------------------------------------
@@ -1696,7 +1739,8 @@ static int jl_batch_record(const uint32_t* H, uint64_t n_ct, const JlParams& jp,
     set_error("JL exponentiation batch too large");
     return FBM_E_UNSUPPORTED;
   }
-  bt.seg[bt.nseg++] = JlExpSeg{H, nude, out, ops, n_ct, bt.total_chunks, sc.n_ops, sc.first, mode, jp.key_is_zero};
+  bt.seg[bt.nseg++] =
+      JlExpSeg{H, nude, out, ops, n_ct, bt.total_chunks, sc.n_ops, sc.first, mode, jp.key_is_zero, sc.sbits};
   bt.total_chunks += (uint32_t)chunks;
   return FBM_OK;
 }
@@ -1736,8 +1780,8 @@ int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const Jl
   // one-lane engine to one workgroup per CU
   static const unsigned lds_pad = getenv("FBM_EXP_LDS_PAD") ? (unsigned)atoi(getenv("FBM_EXP_LDS_PAD")) : 0u;
   hipLaunchKernelGGL(jl_exp_kernel<false>, dim3((unsigned)g), dim3(FBM_BLOCK), lds_pad, s, H, n_ct, (uint32_t*)cst, jp.qa.np,
-                     ops, sc.n_ops, sc.first, mode, jp.key_is_zero, nude, table, out, (const JlExpSeg*)nullptr, 0, 0u,
-                     (uint32_t*)nullptr);
+                     ops, sc.n_ops, sc.first, mode, jp.key_is_zero, sc.sbits, nude, table, out, (const JlExpSeg*)nullptr,
+                     0, 0u, (uint32_t*)nullptr);
   return check_launch("jl_exp_kernel");
 }
 
@@ -1764,7 +1808,7 @@ int jl_batch_flush(void* workspace, uint64_t ws_bytes, hipStream_t s) {
   const uint64_t gmax = jl_table_slots() / FBM_BLOCK;
   if (g > gmax) g = gmax;
   hipLaunchKernelGGL(jl_exp_kernel<true>, dim3((unsigned)g), dim3(FBM_BLOCK), 0, s, (const uint32_t*)nullptr, (uint64_t)0,
-                     (uint32_t*)g_batch.cst, g_batch.np, (const uint32_t*)nullptr, 0, 0, 0, 0, (const uint32_t*)nullptr,
+                     (uint32_t*)g_batch.cst, g_batch.np, (const uint32_t*)nullptr, 0, 0, 0, 0, -1, (const uint32_t*)nullptr,
                      table, (uint32_t*)nullptr, (const JlExpSeg*)segs, bt.nseg, bt.total_chunks, ctr);
   return check_launch("jl_exp_kernel (batch)");
 }

@@ -141,6 +141,10 @@ class Lane:
         elif op == "ds_read_b32":
             addr = self.get(ops[1]) + off
             self.put(ops[0], self.lds.get(addr, 0))
+        elif op == "ds_read_b64":
+            addr = self.get(ops[1]) + off
+            assert addr % 8 == 0, f"ds_read_b64 address {addr}"
+            self.put(ops[0], self.lds.get(addr, 0) | (self.lds.get(addr + 4, 0) << 32))
         elif op == "ds_write_b32":
             addr = self.get(ops[0]) + off
             self.lds[addr] = self.get(ops[1])

@@ -72,6 +72,81 @@ def _rand_n(rng, bits):
     return rng.getrandbits(bits) | (1 << (bits - 1)) | 1
 
 
+MS = GEN.mul_short()
+KS = GEN.KS
+
+
+def run_short(N, a, h):
+    """The short-base product a * h * 2^-(29 KS) (mod N^2): a = (digit0, digit1) in the LDS column,
+    h < 2^(29 KS) in a global blocked column, the pairs (D_j, 0), D = N - 2^(29 KS), in LDS."""
+    words, np_ = consts(N)
+    NK, HB, DADDR = 0x4000, 0x100000, 74 * 1024
+    smem = {NK + 4 * i: w for i, w in enumerate(words)}
+    lds = {}
+    for k, v in enumerate(limbs(a[0]) + limbs(a[1])):
+        lds[k * 1024] = v
+    for j, v in enumerate(limbs(N - (1 << (LB * KS)))):
+        lds[DADDR + 8 * j] = v
+        lds[DADDR + 8 * j + 4] = 0
+    glb = {HB + k * 1024: v for k, v in enumerate(limbs(h, KS))}
+    lane = Lane({"a": 0, "h": 0, "hb": HB, "d": DADDR, "NK": NK, "np": np_}, lds=lds, glb=glb, smem=smem)
+    counts = lane.run(MS)
+    out = [lds[k * 1024] for k in range(2 * L)]
+    assert all(v <= MASK for v in out)
+    d0 = sum(v << (LB * k) for k, v in enumerate(out[:L]))
+    d1 = sum(v << (LB * k) for k, v in enumerate(out[L:]))
+    return d0, d1, counts
+
+
+@pytest.mark.parametrize("bits", [263, 700, 1024])
+def test_nadic_asm_short_product(bits):
+    """X h 2^-261 (mod N^2) for h < 2^261 (one FDH digest) and digits < 2N (a square's output,
+    the worst case included): digits < 3N + 2, 1 305 multiplies, every column below 2^64."""
+    rng = random.Random(bits)
+    N = _rand_n(rng, bits)
+    M = N * N
+    f = pow(2, -LB * KS, M)
+    for trial in range(4):
+        a = (rng.randrange(2 * N), rng.randrange(2 * N))
+        h = rng.getrandbits(LB * KS)
+        if trial == 0:
+            a, h = (2 * N - 1, 2 * N - 1), (1 << (LB * KS)) - 1
+        if trial == 1:
+            h = rng.getrandbits(256)
+        A = (a[0] + a[1] * N) % M
+        t, s, counts = run_short(N, a, h)
+        assert (t + s * N) % M == A * h * f % M
+        assert t < 3 * N and s < 3 * N + 2
+        assert counts["v_mad_u64_u32"] == GEN.ms_mads() == 1305
+        # the next squaring brings the digits back below 2N
+        t2, s2, _ = run(N, (t, s))
+        assert (t2 + s2 * N) % M == A * A * h * h * f * f * pow(R, -1, M) % M
+        assert t2 < 2 * N and s2 < 2 * N
+
+
+def test_nadic_asm_binary_chain_with_short_products():
+    """h^e mod N^2 the way jl_exp_kernel's short path sequences it: (h, 0) raw, then per exponent
+    bit below the top a squaring and, on a 1, a short product; one general product with the
+    host-built constant C = 2^(1044 (2^s + 1) + 261 (e - 2^s)) mod N^2 (s = bit length of e - 1)
+    brings the chain to h^e R, the Montgomery form the epilogue expects."""
+    from fedbiomed_amd import workload as W
+
+    N = W.BIPRIME0
+    M = N * N
+    rng = random.Random(11)
+    h, e = rng.getrandbits(256), rng.getrandbits(24) | (1 << 23)
+    s = e.bit_length() - 1
+    x = (h, 0)
+    for bit in bin(e)[3:]:
+        x = run(N, x)[:2]
+        if bit == "1":
+            x = run_short(N, x, h)[:2]
+    E = LB * L * ((1 << s) + 1) + LB * KS * (e - (1 << s))
+    C = pow(2, E, M)
+    y = run(N, (C % N, C // N), x)[:2]
+    assert (y[0] + y[1] * N) % M == pow(h, e, M) * R % M
+
+
 @pytest.mark.parametrize("bits", [2, 24, 1024])
 def test_nadic_asm_product_and_square(bits):
     rng = random.Random(bits)

@@ -450,6 +450,94 @@ def square_tri():
     return rotate_carries(body)
 
 
+# ------------------------------------------------------------------------------------------
+# Product by the SHORT base h < 2^(29 KS) (one FDH digest: 256 bits, KS = 9 limbs) -- the
+# multiply of the binary exponentiation (jl_exp_kernel's short path).  The multiplier rows are
+# h's KS limbs (digit 1 = 0), B = the running value X from the lane's own LDS column, and the
+# Montgomery reduction takes KS quotient digits only:
+#     X h 2^-(29 KS)  (mod N^2)  =  t + N s,
+#     t = (x0 h + m N) / 2^(29 KS)                        (m = sum q_i 2^(29 i), i < KS)
+#     s = (x1 h + (2^(29 KS) - m) + D + m' N) / 2^(29 KS),   D = N - 2^(29 KS)
+# -- 2^(29 KS) - m is the rows' retiring-column adds (2^29 - 1 - q_i, + 1 in row 0), D enters as
+# the s window's initial value (row 0's addends: pairs (D_j, 0) read from LDS), so the s
+# numerator is x1 h - m + N (= x1 h - m mod N, and >= 0: m < 2^(29 KS) < N).  KS (36 + 36 +
+# 36 + 36 + 1) = 1 305 multiplies against 6 584 for a general product, and no table.  Bounds
+# (N > 2^(29 KS)): digits < 2N in -> t < 3N, s < 3N + 2 (the next squaring brings them back
+# below 2N); a column gathers at most KS rows of 2 products < 2^58: < 2^62.2, no mid-product
+# reduction.  The factor 2^-(29 KS) per multiply (and R^-1 per squaring) is a constant of the
+# exponent, cancelled by one product with a host-built constant after the chain.
+# Register plan: the general product's, with h's limbs in v226..v234 and (D_35, 0) in v[214:215]
+# (the row-operand prefetch registers, unused here); the multiplier needs no LDS rows.
+# ------------------------------------------------------------------------------------------
+KS = 9
+HS = [f"v{MM_NREG + i}" for i in range(KS)]
+D35 = f"v[{_X + 2}:{_X + 3}]"
+MS_NREG = MM_NREG + KS
+
+
+def short_row(i):
+    """Row i of the short product: multiplier limb h_i (HS[i]), t then s part, both retires."""
+    x, first = HS[i], i == 0
+    out = [f"v_mad_u64_u32 {TT}, vcc, {x}, {B0(0)}, {'0' if first else At(0)}"]
+    for j in range(1, L):
+        addend = "0" if (first or j == NW) else At(j)
+        out.append(f"v_mad_u64_u32 {At(j - 1)}, vcc, {x}, {B0(j)}, {addend}")
+        if j == 3:
+            out.append(f"v_mul_lo_u32 {Q}, {TTLO}, {NPV}")
+        if j == 6:
+            out.append(f"v_and_b32 {Q}, {MASK}, {Q}")
+        if j == 8:  # 2^29 - 1 - q_i (+ 1 in row 0: the sum over the rows is 2^(29 KS) - m)
+            out.append(f"v_sub_u32 {CQ}, {hex(1 << LB) if first else MASK}, {Q}")
+    out.append(f"v_mad_u64_u32 {TT}, vcc, {Q}, {Ns(0)}, {TT}")
+    for j in range(1, L):
+        out.append(f"v_mad_u64_u32 {At(j - 1)}, vcc, {Q}, {Ns(j)}, {At(j - 1)}")
+    # s part: the window's addends (row 0: D, loaded into it; the top slot's D_35 from D35)
+    out.append(f"v_mad_u64_u32 {TS}, vcc, {x}, {B1(0)}, {As(0)}")
+    for j in range(1, L):
+        addend = (D35 if first else "0") if j == NW else As(j)
+        out.append(f"v_mad_u64_u32 {As(j - 1)}, vcc, {x}, {B1(j)}, {addend}")
+        if j == 12:
+            out.append(f"v_mad_u64_u32 {TS}, vcc, {CQ}, 1, {TS}")
+        if j == 20:
+            out.append(f"v_mul_lo_u32 {Q2}, {TSLO}, {NPV}")
+        if j == 26:
+            out.append(f"v_and_b32 {Q2}, {MASK}, {Q2}")
+    out.append(f"v_mad_u64_u32 {TS}, vcc, {Q2}, {Ns(0)}, {TS}")
+    for j in range(1, L):
+        out.append(f"v_mad_u64_u32 {As(j - 1)}, vcc, {Q2}, {Ns(j)}, {As(j - 1)}")
+    out += [f"v_lshrrev_b64 {TT}, {LB}, {TT}", f"v_lshl_add_u64 {At(0)}, {TT}, 0, {At(0)}",
+            f"v_lshrrev_b64 {TS}, {LB}, {TS}", f"v_lshl_add_u64 {As(0)}, {TS}, 0, {As(0)}"]
+    return out
+
+
+def mul_short():
+    body = list(load_consts())
+    # h's KS limbs: global, workgroup-blocked (limb k at hb + h_off + k * 1024)
+    body += ["s_waitcnt vmcnt(0)", f"v_mov_b32 {TMP}, %[h]"]
+    for k in range(KS):
+        if k and k % 4 == 0:
+            body.append(f"v_add_u32 {TMP}, 0x1000, {TMP}")
+        body.append(f"global_load_dword {HS[k]}, {TMP}, %[hb] offset:{(k % 4) * 1024}")
+    # B = X from the lane's column (undoubled); the s window <- (D_j, 0), D35 <- (D_35, 0)
+    body.append(f"v_add_u32 {AADR}, 0x10000, %[a]")
+    for j in range(2 * L):
+        if j < 64:
+            body.append(f"ds_read_b32 {breg(j)}, %[a] offset:{j * 1024}")
+        else:
+            body.append(f"ds_read_b32 {breg(j)}, {AADR} offset:{(j - 64) * 1024}")
+    body += [f"ds_read_b64 {As(j)}, %[d] offset:{8 * j}" for j in range(NW)]
+    body += [f"ds_read_b64 {D35}, %[d] offset:{8 * NW}", f"v_mov_b32 {NPV}, %[np]",
+             "s_waitcnt vmcnt(0) lgkmcnt(0)"]
+    for i in range(KS):
+        body += short_row(i)
+    body += normalise_store()
+    return rotate_carries(body)
+
+
+def ms_mads():
+    return KS * (4 * L + 1)
+
+
 def sq_mads():
     """v_mad_u64_u32 per square: triangular t part (cross products + diagonals), the s part's
     (2 x0) x1 and K' - q, the two q N passes, the mid-product reduction."""
@@ -462,7 +550,7 @@ def mm_mads():
 
 
 def clobbers():
-    regs = [f'"v{i}"' for i in range(max(MM_NREG, SQ_NREG))]
+    regs = [f'"v{i}"' for i in range(max(MM_NREG, SQ_NREG, MS_NREG))]
     regs += [f'"s{i}"' for i in [16, 17] + list(range(19, 32)) + [34, 35] + list(range(36, 100))]
     out = [", ".join(regs[i:i + 16]) for i in range(0, len(regs), 16)]
     return " \\\n  ".join(x + "," for x in out[:-1]) + " \\\n  " + out[-1]
@@ -477,7 +565,7 @@ def count_mads(lines):
 
 
 def main():
-    mm, sq = product(False), square_tri()
+    mm, sq, ms = product(False), square_tri(), mul_short()
     mm_row, sq_body = row(False, False), sq_row("odd")
     hdr = f"""// GENERATED by tools/gen_nadic_asm.py -- do not edit by hand.
 //
@@ -486,7 +574,8 @@ def main():
 //   a (per-lane LDS column, {2 * L} limbs) <- a * b * R^-1 (mod N^2), digits lazily < 2N.
 // See tools/gen_nadic_asm.py for the arithmetic, the bounds and the register plan.
 // {len(mm)} instructions (general, B from global), {len(sq)} (square, triangular x0^2); row
-// bodies {len(mm_row)} / <= {len(sq_body)} instructions; {mm_mads()} / {sq_mads()} v_mad_u64_u32 per product.
+// bodies {len(mm_row)} / <= {len(sq_body)} instructions; {mm_mads()} / {sq_mads()} v_mad_u64_u32 per product;
+// the short-base product (h < 2^{LB * KS}, {KS} rows): {len(ms)} instructions, {ms_mads()} v_mad_u64_u32.
 #pragma once
 #include <stdint.h>
 
@@ -494,6 +583,8 @@ def main():
 #define FBM_NA_LIMBS {L}
 #define FBM_NA_MADS_MUL {mm_mads()}
 #define FBM_NA_MADS_SQR {sq_mads()}
+#define FBM_NA_MADS_SHORT {ms_mads()}
+#define FBM_NA_SHORT_LIMBS {KS}
 
 #define FBM_NA_CLOBBERS \\
   {clobbers()}
@@ -506,6 +597,17 @@ __device__ __forceinline__ void fbm_na_mm_glb(uint32_t a_off, const uint32_t* bb
 {c_string(mm)}
       :
       : [a] "v"(a_off), [b] "v"(b_off), [bb] "s"(bb), [NK] "s"(NK), [np] "s"(np)
+      : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
+}}
+
+// a <- a * h * 2^-{LB * KS} (mod N^2) for a short h = (h, 0), h < 2^{LB * KS}: h's limbs at hb + h_off + k*1024
+// (bytes; global, blocked), d: LDS byte address of the pairs (D_j, 0), D = N - 2^{LB * KS} (36 x 8 bytes).
+__device__ __forceinline__ void fbm_na_ms_glb(uint32_t a_off, const uint32_t* hb, uint32_t h_off, uint32_t d_off,
+                                              const uint32_t* NK, uint32_t np) {{
+  asm volatile(
+{c_string(ms)}
+      :
+      : [a] "v"(a_off), [h] "v"(h_off), [hb] "s"(hb), [d] "v"(d_off), [NK] "s"(NK), [np] "s"(np)
       : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
 }}
 
