@@ -820,6 +820,10 @@ struct GroupEng<4> {
                             uint32_t e0, uint32_t) {
     fbm_qa_sq_lds(ac, al, QK, np, n, e0);
   }
+  __device__ static void ms(uint32_t ac, uint32_t al, uint32_t dl, uint32_t np, const uint32_t (&n)[M], uint32_t e0,
+                            uint32_t) {
+    fbm_qa_ms_lds(ac, al, dl, np, n, e0);
+  }
 };
 template <>
 struct GroupEng<3> {
@@ -841,6 +845,10 @@ struct GroupEng<3> {
   __device__ static void sq(uint32_t ac, uint32_t al, const uint32_t* QK, uint32_t np, const uint32_t (&n)[M],
                             uint32_t e0, uint32_t bp) {
     fbm_ta_sq_lds(ac, al, QK, np, n, e0, bp);
+  }
+  __device__ static void ms(uint32_t ac, uint32_t al, uint32_t dl, uint32_t np, const uint32_t (&n)[M], uint32_t e0,
+                            uint32_t bp) {
+    fbm_ta_ms_lds(ac, al, dl, np, n, e0, bp);
   }
 };
 
@@ -895,14 +903,19 @@ template <int G>
 __global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(const uint32_t* __restrict__ H, uint64_t n_ct,
                                                                uint32_t* __restrict__ cst, uint32_t np29,
                                                                const uint32_t* __restrict__ ops, int n_ops,
-                                                               int first, int mode, int key_is_zero,
+                                                               int first, int mode, int key_is_zero, int sbits,
                                                                const uint32_t* __restrict__ nude,
                                                                uint32_t* __restrict__ table,
                                                                uint32_t* __restrict__ out) {
   using E = GroupEng<G>;
   constexpr int M = E::M, ROWW = E::ROWW;
   constexpr uint32_t ENTRY = 2 * M * 256;  // words of one table entry
-  __shared__ uint32_t lds_q[(2 * FBM_QA_D1 + 2) * ROWW];
+  // column rows: the two digits, two spare rows, the short path's h limbs (FBM_QA_HROW ..) and their
+  // prefetch row; the pairs (D_j, 0) of the short product, then 12 zero pairs (the dummy lane's)
+  constexpr int ROWS = FBM_QA_HROW + FBM_NA_SHORT_LIMBS + 1;
+  static_assert(FBM_QA_HROW == FBM_TA_HROW && FBM_QA_HROW == 2 * FBM_QA_D1 + 2, "column rows");
+  __shared__ uint32_t lds_q[ROWS * ROWW];
+  __shared__ uint32_t lds_d[96];
   __shared__ uint32_t chunk_s;
   const int tid = threadIdx.x;
   int c, l;
@@ -920,8 +933,10 @@ __global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(co
   const uint32_t bp = (uint32_t)(4 * (dummy ? (tid & 63) : (tid & 63) - l));
   if (dummy) {  // the dummy column stays all-zero: its lanes multiply nothing but zeros
 #pragma unroll 1
-    for (int k = 0; k < 2 * FBM_QA_D1 + 2; ++k) col[k * ROWW] = 0u;
+    for (int k = 0; k < ROWS; ++k) col[k * ROWW] = 0u;
   }
+  if (tid < 96) lds_d[tid] = tid < 72 ? launder_s(cst)[FBM_CST_QD + tid] : 0u;  // (ordered by the loop's barrier)
+  const uint32_t dl = lds_addr(lds_d) + 8u * (uint32_t)(dummy ? FBM_QA_L : M * l);
   // byte offset of this lane's word in table entry 0 of this workgroup's slot
   const uint32_t tb0 = (uint32_t)(((uint64_t)blockIdx.x * FBM_TENTRIES * ENTRY + tid) * 4);
   const uint32_t tstride = ENTRY * 4;
@@ -937,7 +952,7 @@ __global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(co
     const bool valid = !dummy && ct_raw < n_ct;
     const uint64_t ct = ct_raw < n_ct ? ct_raw : n_ct - 1;
     uint32_t* scratch = table + (tb0 + FBM_TSCRATCH * tstride) / 4;
-    bool wide = false;
+    bool wide = false, shortp = false;
     {  // h -> the lane's 29-bit limbs of (h mod R, h div R) -> scratch
       uint32_t h18[2 * M];
       const uint32_t* hr = H + ct * 64;
@@ -956,12 +971,26 @@ __global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(co
         h18[M + r] = hi;
       }
       {
-        uint32_t any = 0;
+        uint32_t any = 0, mid = 0;
 #pragma unroll
-        for (int r = 0; r < M; ++r) any |= h18[M + r];
+        for (int r = 0; r < M; ++r) {
+          any |= h18[M + r];
+          if (M * l + r >= FBM_NA_SHORT_LIMBS) mid |= h18[r];
+        }
+        // the short path (as jl_exp_kernel's): every h of the wave below 2^261 and a schedule for it
+        shortp = sbits >= 0 && !key_is_zero && !__any(any != 0u || mid != 0u);
+        if (shortp) {  // A = (h, 0) raw; h's limbs 0 .. KS (the last: 0, the prefetch row) -> rows HROW ..
+#pragma unroll
+          for (int r = 0; r < M; ++r) {
+            const int k = M * l + r;
+            col[k * ROWW] = h18[r];
+            col[(FBM_QA_D1 + k) * ROWW] = 0u;
+            if (k <= FBM_NA_SHORT_LIMBS) col[(FBM_QA_HROW + k) * ROWW] = h18[r];
+          }
+        }
         // wide is a property of the ciphertext, not of the lane's slice: OR over the group
         wide = E::group_mask(__ballot(any != 0u), tid) != 0u;
-        if (__any(wide)) {  // FDH retries (small moduli): h_hi R^2 = (h_hi, 0) * R^3 R^-1 -> entry 1
+        if (!shortp && __any(wide)) {  // FDH retries (small moduli): h_hi R^2 = (h_hi, 0) * R^3 R^-1 -> entry 1
           uint32_t w18[2 * M];
 #pragma unroll
           for (int r = 0; r < M; ++r) {
@@ -975,8 +1004,21 @@ __global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(co
           qa_lds_to_tbl<M, ROWW>(col, l, table + (tb0 + tstride) / 4);
         }
       }
-      col_store<2 * M>(scratch, h18);
+      if (!shortp) col_store<2 * M>(scratch, h18);
     }
+    if (shortp) {  // binary chain with short-base products, then C (jl_exp_kernel's short path)
+      const uint32_t* kw = ops + FBM_OPS_KW;
+      uint32_t w = 0;
+#pragma unroll 1
+      for (int j = sbits - 1; j >= 0; --j) {
+        if (j == sbits - 1 || (j & 31) == 31) w = __builtin_amdgcn_readfirstlane(launder_s(kw)[j >> 5]);
+        E::sq(ac, al, QK, np29, n, e0, bp);
+        if ((w >> (j & 31)) & 1u) E::ms(ac, al, dl, np29, n, e0, bp);
+      }
+      qa_lds_to_tbl<M, ROWW>(col, l, table + tb0 / 4);
+      if (!dummy) qa_lds_store_uniform<M, ROWW>(col, l, ops + FBM_OPS_CORR);
+      E::mm(ac, al, table, tb0, QK, np29, n, e0, bp);
+    } else {
     if (!dummy) qa_lds_store_uniform<M, ROWW>(col, l, cst + FBM_CST_QR2);
     E::mm(ac, al, table, tb0 + FBM_TSCRATCH * tstride, QK, np29, n, e0, bp);  // h R | h_lo R
     if (__any(wide)) {  // h R = h_lo R + h_hi R^2 (digit-wise, then carries)
@@ -1011,6 +1053,7 @@ __global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(co
         if (idx >= 0) E::mm(ac, al, table, tb0 + (uint32_t)idx * tstride, QK, np29, n, e0, bp);
       }
     }
+    }  // (table path)
     {  // last operand: nude = (1, pt) (encrypt; 28-bit blocked column -> 29-bit slice) or 1
       uint32_t b18[2 * M];
       const uint32_t* nb = nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255);
@@ -1766,11 +1809,11 @@ int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const Jl
     if (g > group_wgs_max()) g = group_wgs_max();
     if (eng == FBM_ENGINE_QUAD) {
       hipLaunchKernelGGL(jl_expg_kernel<4>, dim3((unsigned)g), dim3(FBM_QBLOCK), 0, s, H, n_ct, (uint32_t*)cst,
-                         jp.qa.np, ops, sc.n_ops, sc.first, mode, jp.key_is_zero, nude, table, out);
+                         jp.qa.np, ops, sc.n_ops, sc.first, mode, jp.key_is_zero, sc.sbits, nude, table, out);
       return check_launch("jl_expq_kernel");
     }
     hipLaunchKernelGGL(jl_expg_kernel<3>, dim3((unsigned)g), dim3(FBM_QBLOCK), 0, s, H, n_ct, (uint32_t*)cst,
-                       jp.qa.np, ops, sc.n_ops, sc.first, mode, jp.key_is_zero, nude, table, out);
+                       jp.qa.np, ops, sc.n_ops, sc.first, mode, jp.key_is_zero, sc.sbits, nude, table, out);
     return check_launch("jl_expt_kernel");
   }
   uint64_t g = (n_ct + FBM_BLOCK - 1) / FBM_BLOCK;

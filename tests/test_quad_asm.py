@@ -235,9 +235,14 @@ def _lds_waits_ok(prog, g):
         else:
             r = reads(ln)
             for d in pending:
-                assert d not in r, f"read of {d} before its LDS op retired: {i}: {ln}"
-            if op in ("ds_read_b32", "ds_bpermute_b32"):
-                pending.append(ln.split(" ")[1].rstrip(","))
+                assert not (d & r if isinstance(d, frozenset) else d in r), \
+                    f"read of {d} before its LDS op retired: {i}: {ln}"
+            if op in ("ds_read_b32", "ds_read_b64", "ds_bpermute_b32"):
+                d = ln.split(" ")[1].rstrip(",")
+                if d.startswith("v["):  # a pair: both registers pending (one LDS op)
+                    lo, hi = (int(x) for x in d[2:-1].split(":"))
+                    d = frozenset(f"v{k}" for k in range(lo, hi + 1))
+                pending.append(d)
         if op == "s_cbranch_scc1" and i not in seen_back:
             seen_back.add(i)
             i = lab[ln.split(" ")[1].rstrip("bf")]
@@ -271,3 +276,111 @@ def test_cyclic_band_square_covers_each_product_once(geo):
             assert weight.get((a, b), 0) == (1 if a == b else 2), (a, b, weight.get((a, b)))
     per_row = [len(Q.cyc_active(g, i)) for i in range(L)]
     assert per_row == [g.M // 2 + 1] * L  # 7 of 12 (triple), 5 of 9 (quad)
+
+
+SHORT = {k: Q.mul_short(g) for k, g in GEOS.items()}
+
+
+def run_short_group(N, As, hs, geo):
+    """The group engines' short-base product A h 2^-261 (mod N^2) for whole groups: h's 9 limbs in
+    LDS rows HROW.. of each ciphertext's column, the pairs (D_j, 0) (D = N - 2^261, then 12 zero
+    pairs for the triple's dummy lane) in LDS.  Returns per ciphertext (t, s), the max limb, counts."""
+    g = GEOS[geo]
+    G, ML, ROWB = g.G, g.M, g.ROWB
+    _, np_ = qconsts(N)
+    DADDR = 0x40000
+    lds = {}
+    for j, v in enumerate(limbs(N - (1 << (LB * Q.KS))) + [0] * 12):
+        lds[DADDR + 8 * j] = v
+        lds[DADDR + 8 * j + 4] = 0
+    nl = limbs(N)
+    lanes = []
+    for c in range(len(As)):
+        ac = 4 * c
+        for k, v in enumerate(limbs(As[c][0]) + limbs(As[c][1])):
+            lds[ac + k * ROWB] = v
+        for k, v in enumerate(limbs(hs[c], Q.KS + 1)):  # + the prefetch row (0)
+            lds[ac + (Q.HROW + k) * ROWB] = v
+        for l in range(G):
+            args = {"ac": ac, "al": ac + ML * l * ROWB, "dl": DADDR + 8 * ML * l, "np": np_,
+                    "e0": 1 if l == 0 else 0, "bp": 4 * G * c}
+            args.update({f"n{r}": nl[ML * l + r] for r in range(ML)})
+            lanes.append(Lane(args, lds=lds))
+    if G == 3:
+        tid, ac = G * len(As), 4 * len(As)
+        args = {"ac": ac, "al": ac, "dl": DADDR + 8 * L, "np": np_, "e0": 0, "bp": 4 * tid}
+        args.update({f"n{r}": 0 for r in range(ML)})
+        lanes.append(Lane(args, lds=lds))
+    counts = Wave(lanes).run(SHORT[geo])
+    if G == 3:
+        assert all(lds.get(4 * len(As) + k * ROWB, 0) == 0 for k in range(2 * L)), "dummy column disturbed"
+    out, top = [], 0
+    for c in range(len(As)):
+        col = [lds[4 * c + k * ROWB] for k in range(2 * L)]
+        top = max(top, max(col))
+        out.append((sum(v << (LB * k) for k, v in enumerate(col[:L])), sum(v << (LB * k) for k, v in enumerate(col[L:]))))
+    return out, top, counts
+
+
+@pytest.mark.parametrize("geo", ["quad", "triple"])
+@pytest.mark.parametrize("bits", [263, 1024])
+def test_group_short_product(bits, geo):
+    """x h 2^-261 (mod N^2) for h < 2^261 and digits < 2N (the worst case included) over whole
+    groups: digits < 3N + 2, lazy limbs in bound, 9 rows of 4 M + 1 multiplies per lane."""
+    rng = random.Random(300 + bits)
+    N = _rand_n(rng, bits)
+    M = N * N
+    f = pow(2, -LB * Q.KS, M)
+    As = [(2 * N - 1, 2 * N - 1)] + [(rng.randrange(2 * N), rng.randrange(2 * N)) for _ in range(2)]
+    hs = [(1 << (LB * Q.KS)) - 1, rng.getrandbits(256), rng.getrandbits(LB * Q.KS)]
+    got, top, counts = run_short_group(N, As, hs, geo)
+    assert top < (1 << LB) + (1 << 11)
+    assert counts["v_mad_u64_u32"] == Q.ms_mads(GEOS[geo]) == Q.KS * (4 * GEOS[geo].M + 1)
+    for a, h, (t, s) in zip(As, hs, got):
+        A = (a[0] + a[1] * N) % M
+        assert (t + s * N) % M == A * h * f % M
+        assert t < 3 * N and s < 3 * N + 2
+
+
+@pytest.mark.parametrize("geo", ["quad", "triple"])
+def test_group_short_chain_power(geo):
+    """The short path's chain through the simulated group engine: (h, 0) raw, a squaring per
+    exponent bit and a short product per 1 bit, then the host constant C (one general product):
+    h^e R, and * 1 -> h^e."""
+    from fedbiomed_amd import workload as W
+
+    N = W.BIPRIME0
+    M = N * N
+    rng = random.Random(13)
+    h, e = rng.getrandbits(256), rng.getrandbits(10) | (1 << 9)
+    s = e.bit_length() - 1
+    x = (h, 0)
+    for bit in bin(e)[3:]:
+        (x,), _, _ = run_quad(N, [x], geo=geo)
+        if bit == "1":
+            (x,), _, _ = run_short_group(N, [x], [h], geo)
+    C = pow(2, LB * L * ((1 << s) + 1) + LB * Q.KS * (e - (1 << s)), M)
+    (x,), _, _ = run_quad(N, [(C % N, C // N)], [x], geo=geo)
+    (t, s_), = run_quad(N, [x], [(1, 0)], geo=geo)[0]
+    assert (t + s_ * N) % M == pow(h, e, M)
+
+
+@pytest.mark.parametrize("geo", ["quad", "triple"])
+def test_group_short_product_waits(geo):
+    """DPP wait states and LDS results waited for in the short product too."""
+    prog = SHORT[geo]
+    assert _lds_waits_ok(prog, GEOS[geo])
+    for i, ln in enumerate(prog):
+        if Q.is_dpp(ln):
+            src = ln.split(",")[1].split()[0]
+            dist = 0
+            for prev in reversed(prog[:i]):
+                if prev.startswith("s_nop"):
+                    dist += int(prev.split()[1]) + 1
+                    continue
+                if prev.startswith("v_") and src in Q.Emitter.dests(prev):
+                    break
+                dist += 1
+                if dist >= 2:
+                    break
+            assert dist >= 2, (i, ln)

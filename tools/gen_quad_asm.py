@@ -251,18 +251,20 @@ def load_b_lds(g, double_b1):
     return out
 
 
-def row(g, first, sq, kreg, xs, xn, pre_off):
+def row(g, first, sq, kreg, xs, xn, pre_off, first_s=None):
     """One row with an explicit schedule (every dependent instruction 3+ instructions after
     its producer).  xs = this row's (x0, x1); xn = where the prefetch of the next row's
-    operands goes, read at byte offset pre_off from AADR; kreg = K'_i."""
+    operands goes, read at byte offset pre_off from AADR; kreg = K'_i.  first_s (default: first):
+    whether the s window starts from 0 (False: from its registers -- the short product's D)."""
     M = g.M
     x0, x1 = xs
+    first_s = first if first_s is None else first_s
     out = [f"ds_read_b32 {xn[0]}, {g.AADR} offset:{pre_off}"]
     if not sq:
         out.append(f"ds_read_b32 {xn[1]}, {g.AADR} offset:{pre_off + g.D1 * g.ROWB}")
 
     def addend(acc, r):
-        if first:
+        if first if acc == g.At else first_s:
             return "0"
         if r == M - 1:
             return g.RT if acc == g.At else g.RS
@@ -688,6 +690,42 @@ def square_cyc(g, carries=CARRY_PAIRS):
     return rotate_carries(e.out, carries)
 
 
+# ------------------------------------------------------------------------------------------
+# The short-base product x h 2^-261 (tools/gen_nadic_asm.py's mul_short: rows = h's KS limbs,
+# digit 1 of the multiplier 0, KS quotient digits) over a lane group: the multiplier rows are
+# LDS rows HROW .. HROW + KS - 1 of the ciphertext's column (every lane of the group reads the
+# same word: a broadcast, one row ahead, as the general product's rows), B = the lane's slice of
+# X (its own column, undoubled), the t window from 0, the s window from the pairs (D_j, 0) of
+# the lane's columns (D = N - 2^261; the triple's dummy lane reads zeros: its column stays 0),
+# the retiring-column adds 2^29 - 1 - q_i (+ 1 in row 0) as literals.  KS rows of 4 M + 1
+# multiplies per lane (triple: 49, quad: 37), no mid-product reduction (a column gathers at
+# most KS rows of two products < 2^58).
+# ------------------------------------------------------------------------------------------
+KS = 9
+HROW = 2 * L + 2   # LDS row of h's limb 0 (after the two digits and the two spare rows)
+
+
+def mul_short(g, carries=CARRY_PAIRS):
+    e = Emitter()
+    XA, XB = g.XA, g.XB
+    e.extend(load_b_lds(g, False))
+    e.extend([f"ds_read_b64 {g.As(r)}, %[dl] offset:{8 * r}" for r in range(g.M - 1)] +
+             [f"ds_read_b64 {g.RS}, %[dl] offset:{8 * (g.M - 1)}"])
+    e.extend([f"v_mov_b32 {g.RTHI}, 0", f"v_mov_b32 {g.MASKV}, {MASK}",
+              f"v_add_u32 {g.AADR}, {HROW * g.ROWB}, %[ac]", f"ds_read_b32 {XA[0]}, {g.AADR}",
+              "s_waitcnt lgkmcnt(0)"])
+    for i in range(KS):
+        xs, xn = (XA, XB) if i % 2 == 0 else (XB, XA)
+        e.extend(row(g, i == 0, True, hex(1 << LB) if i == 0 else MASK, xs, xn, g.ROWB, first_s=False))
+        e.extend([f"v_add_u32 {g.AADR}, {g.ROWB}, {g.AADR}", "s_waitcnt lgkmcnt(0)"])
+    e.extend(normalise_store(g))
+    return rotate_carries(e.out, carries)
+
+
+def ms_mads(g):
+    return sum(1 for ln in mul_short(g) if ln.startswith("v_mad_u64_u32"))
+
+
 def row_mads(sq, g=QUAD):
     return sum(1 for ln in row(g, False, sq, "s35", g.XA, g.XB, g.ROWB) if ln.startswith("v_mad_u64_u32"))
 
@@ -711,7 +749,7 @@ def c_string(lines):
 
 def header(g, pfx, PFX, name):
     M = g.M
-    mm, sq = product(False, g), product(True, g)
+    mm, sq, ms = product(False, g), product(True, g), mul_short(g)
     operands = ", ".join([f'[n{r}] "v"(n[{r}])' for r in range(M)])
     bp_doc, bp_arg, bp_op = "", "", ""
     if g.G == 3:
@@ -739,6 +777,8 @@ def header(g, pfx, PFX, name):
 #define FBM_{PFX}_D1 {g.D1}
 #define FBM_{PFX}_MADS_MUL {product_mads(False, g)}
 #define FBM_{PFX}_MADS_SQR {product_mads(True, g)}
+#define FBM_{PFX}_MADS_SHORT {ms_mads(g)}
+#define FBM_{PFX}_HROW {HROW}
 
 #define FBM_{PFX}_CLOBBERS \\
   {clobbers(g)}
@@ -756,6 +796,19 @@ __device__ __forceinline__ void fbm_{pfx}_mm_glb(uint32_t ac, uint32_t al, const
 {c_string(mm)}
       :
       : [ac] "v"(ac), [al] "v"(al), [b] "v"(b_off), [bb] "s"(bb), [QK] "s"(QK), [np] "s"(np), [e0] "v"(e0){bp_op},
+        {operands}
+      : "memory", "vcc", "scc", FBM_{PFX}_CLOBBERS);
+}}
+
+// a <- a h 2^-{LB * KS} (mod N^2), h < 2^{LB * KS} in LDS rows {HROW} .. {HROW + KS - 1} of the column (row {HROW + KS}:
+// the last row's prefetch); dl: LDS byte address of the pairs (D_j, 0) of the lane's columns
+// (D = N - 2^{LB * KS}; zeros for a dummy lane).  {len(ms)} instructions, {ms_mads(g)} v_mad_u64_u32 per lane.
+__device__ __forceinline__ void fbm_{pfx}_ms_lds(uint32_t ac, uint32_t al, uint32_t dl, uint32_t np,
+                                              const uint32_t (&n)[{M}], uint32_t e0{bp_arg}) {{
+  asm volatile(
+{c_string(ms)}
+      :
+      : [ac] "v"(ac), [al] "v"(al), [dl] "v"(dl), [np] "s"(np), [e0] "v"(e0){bp_op},
         {operands}
       : "memory", "vcc", "scc", FBM_{PFX}_CLOBBERS);
 }}
