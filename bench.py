@@ -43,45 +43,24 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 ISA_MAD_TOPS_2400 = 256 * 4 * 16 * 2.4e9 / 1e12  # 39.3 T: quarter-rate v_mad_u64_u32 at 2.4 GHz
 MAD_PEAK_TOPS = 36.48        # measured v_mad_u64_u32 peak, whole chip, best occupancy (tools/microbench/madpeak.hip,
                              # profiles/r1_madpeak.txt: 35.3 T at 2 waves/SIMD, 36.5 T at 4)
-# v_mad_u64_u32 per lane of one N-adic product modulo N^2 (tools/gen_nadic_asm.py: 37 rows x
-# (37 x0*b0 + 37 q*N + 37 x0*b1 + 37 x1*b0 + 37 q'*N), the square without x1*b0) are read
-# from the library (fbm_jl_mads), so the count always matches the engine that ran.
+# v_mad_u64_u32 per lane of one N-adic product modulo N^2 -- the square, the general product and
+# the short-base product (tools/gen_nadic_asm.py) -- are read from the library (fbm_jl_mads), so the
+# count always matches the engine that ran.
 
 
-def products_per_exp(key: int, win: int = 5):
-    """(squarings, general products) of one jl_exp_kernel ciphertext: to-Montgomery, h^2,
-    2^(win-1)-1 odd powers, the sliding-window schedule (mirror of build_schedule in fbm_capi.hip),
-    final product with nude / 1."""
+def products_per_exp(key: int):
+    """(squarings, general products, short-base products) of one jl_exp_kernel ciphertext on the
+    short path (every bench ciphertext: one FDH digest, a 1024-bit N -- fbm_jl.hip): left-to-right
+    binary over |key| below its top bit, a short-base product per 1 bit, then the host constant C and
+    the final product with nude / 1 (two general products)."""
     k = abs(key)
-    if k == 0:
-        return 0, 2
-    bits = bin(k)[2:]
-    nb = len(bits)
-    i, sq, mul, first = nb - 1, 0, 0, True
-    bit = lambda j: (k >> j) & 1  # noqa: E731
-    pending = 0
-    while i >= 0:
-        if not bit(i):
-            pending += 1
-            i -= 1
-            continue
-        lo = max(i - win + 1, 0)
-        while not bit(lo):
-            lo += 1
-        if first:
-            first = False
-        else:
-            sq += pending + (i - lo + 1)
-            mul += 1
-        pending = 0
-        i = lo - 1
-    sq += pending
-    return 1 + sq, 1 + (2 ** (win - 1) - 1) + mul + 1
+    if k == 0:  # h = 1: to-Montgomery and the final product
+        return 0, 2, 0
+    return k.bit_length() - 1, 2, bin(k).count("1") - 1
 
 
-def mads_per_exp(key: int, win: int, mads_mul: int, mads_sq: int) -> int:
-    sq, gen = products_per_exp(key, win)
-    return sq * mads_sq + gen * mads_mul
+def mads_per_exp(key: int, mads: tuple) -> int:
+    return sum(c * m for c, m in zip(products_per_exp(key), mads))
 
 
 def committed_traffic(kernel: str, scheme: str, elements: int, n_ct=None):
@@ -455,11 +434,10 @@ def main():
         # carries every party's and the factor's ciphertexts; the aggregate's own bytes belong to
         # the combine kernel, not to this launch
         alg_bytes = prof_steps * (P * (4 * n + 256 * n_ct) + 256 * n_ct)
-        win = _native.load().fbm_jl_window()
-        mm = sum(sum(products_per_exp(k, win)) for k in keys) + sum(products_per_exp(sk0, win))
-        mads_mul, mads_sq = _native.load().fbm_jl_mads(0), _native.load().fbm_jl_mads(1)
-        mads_step = n_ct * (sum(mads_per_exp(k, win, mads_mul, mads_sq) for k in keys)
-                            + mads_per_exp(sk0, win, mads_mul, mads_sq))
+        mm = sum(sum(products_per_exp(k)) for k in keys) + sum(products_per_exp(sk0))
+        lib = _native.load()
+        mads_mul, mads_sq, mads_short = lib.fbm_jl_mads(0), lib.fbm_jl_mads(1), lib.fbm_jl_mads(2)
+        mads_step = n_ct * sum(mads_per_exp(k, (mads_sq, mads_mul, mads_short)) for k in keys + [sk0])
         mads = prof_steps * mads_step
         # the step's exponentiation kernel: one batched launch over every party and the factor
         # (jl_exp_kernel<true>), or one launch each (<false>, --no-batch-exp)
@@ -481,9 +459,8 @@ def main():
             "avg_launch_ms": (ms / cnt) if cnt else None, "launches": cnt}
     if args.scheme == "jl":
         roof["note"] = ("jl_exp_kernel moves ~1e-4 of the HBM roofline's bytes by construction: it is bound by "
-                        "integer multiply issue (v_mad_u64_u32), reported in roofline_valu; traffic = the "
-                        "sliding-window table reads (DESIGN.md section 4); one launch = every party's and "
-                        "the decryption factor's exponentiations (batched)")
+                        "integer multiply issue (v_mad_u64_u32), reported in roofline_valu; one launch = every "
+                        "party's and the decryption factor's exponentiations (batched)")
     line = {
         "metric": "params/s secagg encrypt+aggregate (device-resident), 10M-elem vector @1/8 GPU",
         "value": value, "unit": "params/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -512,12 +489,14 @@ def main():
                                      "gfx_clock_during_launch": clk,
                                      "isa_T_at_observed_clock": (ISA_MAD_TOPS_2400 * clk["median_mhz"] / 2400.0
                                                                  if clk.get("median_mhz") else None)},
-                                 "products_per_ct_step": mm, "window": win,
+                                 "products_per_ct_step": mm,
                                  "step_achieved": mads_step / (ms_per_step / 1000) / 1e12,
                                  "step_frac": mads_step / (ms_per_step / 1000) / 1e12 / MAD_PEAK_TOPS,
                                  "mads_per_square": mads_sq, "mads_per_product": mads_mul,
-                                 "note": "executed v_mad_u64_u32 of the N-adic engine (per square / product "
-                                         "above); "
+                                 "mads_per_short_product": mads_short,
+                                 "note": "executed v_mad_u64_u32 of the N-adic engine (per square / product / "
+                                         "short-base product above; the short path: a squaring per key bit, a "
+                                         "short product per 1 bit, two general products); "
                                          "achieved/frac: the step's jl_exp launch(es) in a serialised step (HIP "
                                          "events on the launch stream); step_*: the timed step (all kernels)"}
 

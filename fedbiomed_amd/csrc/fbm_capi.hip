@@ -850,8 +850,12 @@ int fbm_jl_window(void) { return FBM_WIN; }
 int fbm_jl_mads(int square) {  // 0: general product, 1: square, 2: short-base product
   return square == 2 ? FBM_NA_MADS_SHORT : square ? FBM_NA_MADS_SQR : FBM_NA_MADS_MUL;
 }
-int fbm_jl_quad_mads(int square) { return 4 * (square ? FBM_QA_MADS_SQR : FBM_QA_MADS_MUL); }
-int fbm_jl_triple_mads(int square) { return 3 * (square ? FBM_TA_MADS_SQR : FBM_TA_MADS_MUL); }
+int fbm_jl_quad_mads(int square) {
+  return 4 * (square == 2 ? FBM_QA_MADS_SHORT : square ? FBM_QA_MADS_SQR : FBM_QA_MADS_MUL);
+}
+int fbm_jl_triple_mads(int square) {
+  return 3 * (square == 2 ? FBM_TA_MADS_SHORT : square ? FBM_TA_MADS_SQR : FBM_TA_MADS_MUL);
+}
 
 int fbm_jl_set_engine(int mode) {
   if (mode != FBM_ENGINE_AUTO && mode != FBM_ENGINE_SINGLE && mode != FBM_ENGINE_GENERIC && mode != FBM_ENGINE_QUAD &&

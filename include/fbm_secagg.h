@@ -257,14 +257,17 @@ int fbm_ass_split_wide(const uint32_t* secret, uint64_t n, int l_in, int n_share
                        void* stream);
 int fbm_ass_reconstruct_wide(const uint32_t* shares, int n_shares, int l, uint64_t n, uint32_t* out, void* stream);
 
-/* Sliding-window width of the JL exponentiation (odd-power table of 2^(w-1) entries); lets the
- * bench count the products one ciphertext costs (its VALU roofline). */
+/* Sliding-window width of the JL exponentiation's table path (odd-power table of 2^(w-1) entries;
+ * the short path -- one FDH digest, N > 2^262: every 1024-bit biprime -- needs no table). */
 int fbm_jl_window(void);
 /* v_mad_u64_u32 per lane of one product of the JL exponentiation engine (N-adic Montgomery
- * product modulo N^2, fedbiomed_amd/csrc/fbm_nadic_asm.hpp): square != 0 -> a squaring. */
+ * product modulo N^2, fedbiomed_amd/csrc/fbm_nadic_asm.hpp): square = 0 a general product, 1 a
+ * squaring, 2 the short path's short-base product (x h 2^-261); lets the bench count the
+ * multiplies one ciphertext costs (its VALU roofline). */
 int fbm_jl_mads(int square);
 /* The same count for the quad / triple engines (4 / 3 lanes per ciphertext): v_mad_u64_u32
- * lane-ops per product summed over the lanes (fedbiomed_amd/csrc/fbm_quad_asm.hpp, fbm_tri_asm.hpp). */
+ * lane-ops per product summed over the lanes (fedbiomed_amd/csrc/fbm_quad_asm.hpp, fbm_tri_asm.hpp);
+ * square = 2: the short-base product. */
 int fbm_jl_quad_mads(int square);
 int fbm_jl_triple_mads(int square);
 
