@@ -526,6 +526,24 @@ class jl_engine:
         return False
 
 
+class jl_short:
+    """The exponentiation's short path (binary chain with the 9-row short-base product, taken for a
+    one-digest FDH h and N > 2^262) on or off for the JL calls issued inside
+    (process-wide, fbm_jl_set_short): off, every wave runs the sliding-window table path.  Results are
+    bit-identical either way -- an A/B and test switch."""
+
+    def __init__(self, on: bool):
+        self._on, self._prev = 1 if on else 0, None
+
+    def __enter__(self):
+        self._prev = N.load().fbm_jl_set_short(self._on)
+        return self
+
+    def __exit__(self, *exc):
+        N.load().fbm_jl_set_short(self._prev)
+        return False
+
+
 def jl_engine_for(n_ct: int) -> str:
     """The engine a launch of n_ct ciphertexts takes under the current policy."""
     return {1: "single", 2: "generic", 3: "triple", 4: "quad"}[N.load().fbm_jl_engine_for(int(n_ct))]

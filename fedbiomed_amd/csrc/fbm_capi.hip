@@ -6,6 +6,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <string>
@@ -704,9 +705,12 @@ static std::vector<JlShortCacheEntry> g_short_cache;  // guarded by g_jp_mu, at 
 // The short path (jl_exp_kernel): possible for N > 2^262 (D = N - 2^261 > the product's quotient
 // m < 2^261); used with a nonzero key.  Returns whether N qualifies (then sh.d is valid and the
 // constants block gets it); sets sc.sbits and sh.kw / sh.corr when the key does too.
+static std::atomic<int> g_short_on{1};  // fbm_jl_set_short: 0 forces the window-table path (A/B, tests)
+
 static bool build_short(const uint32_t* biprime, const uint32_t* key, int is_zero, JlSched& sc, JlShort& sh) {
   memset(&sh, 0, sizeof(sh));
   sc.sbits = -1;
+  if (!g_short_on.load(std::memory_order_relaxed)) return false;
   Big N(biprime, biprime + 32);
   big_trim(N);
   const int KSB = FBM_QA_LB * FBM_NA_SHORT_LIMBS;  // 261
@@ -868,6 +872,8 @@ int fbm_jl_set_engine(int mode) {
 }
 
 int fbm_jl_engine_for(uint64_t n_ct) { return jl_engine_for(n_ct); }
+
+int fbm_jl_set_short(int on) { return g_short_on.exchange(on ? 1 : 0); }
 
 const char* fbm_last_error(void) { return g_err; }
 
@@ -1662,6 +1668,25 @@ int fbm_test_nadic_consts(const uint32_t* n32, uint32_t* nk, uint32_t* r2na, uin
   memcpy(r3na, jp.qa.r3, sizeof(jp.qa.r3));
   *np = jp.qa.np;
   return FBM_OK;
+}
+
+int fbm_test_short_consts(const uint32_t* n32, const uint32_t* key, uint32_t* kw, uint32_t* corr, uint32_t* d) {
+  if (!n32 || !key || !kw || !corr || !d) {
+    set_error("fbm_test_short_consts: null pointer");
+    return FBM_E_ARG;
+  }
+  JlSched sc;
+  int is_zero = 0;
+  int rc = build_schedule(key, sc, is_zero);
+  if (rc) return rc;
+  JlShort sh;
+  const int on = g_short_on.exchange(1);
+  const bool q = build_short(n32, key, is_zero, sc, sh);
+  g_short_on.store(on);
+  memcpy(kw, sh.kw, sizeof(sh.kw));
+  memcpy(corr, sh.corr, sizeof(sh.corr));
+  memcpy(d, sh.d, sizeof(sh.d));
+  return q ? sc.sbits : -2;
 }
 
 int fbm_test_modinv(const uint32_t* x, const uint32_t* n, uint32_t* out, int* batches) {

@@ -283,6 +283,11 @@ int fbm_jl_triple_mads(int square);
  * fbm_jl_engine_for: the engine a launch of n_ct ciphertexts takes under the policy (1-4). */
 int fbm_jl_set_engine(int mode);
 int fbm_jl_engine_for(uint64_t n_ct);
+/* The exponentiation's short path (a binary chain with the 9-row short-base product, taken for a
+ * one-digest FDH h and N > 2^262: DESIGN.md 5.3) on (1, the default) or off (0: every wave runs the
+ * sliding-window table path -- an A/B and test switch; results are bit-identical).  Returns the
+ * previous setting. */
+int fbm_jl_set_short(int on);
 
 /* Batched exponentiation (one-lane engine), for callers that run several parties' encrypts and
  * the decryption factor on one device (simulation, the benchmark): between fbm_jl_batch_begin
@@ -328,6 +333,11 @@ int fbm_test_gen_combine(const uint32_t* cts, int n_parties, const uint32_t* fac
  * them -- nk: 80 words (29-bit N limbs, K'_i), r2na / r3na: 72 limbs (29-bit digits of R^2 /
  * R^3 mod N^2, R = 2^1044), np = -N^-1 mod 2^29. */
 int fbm_test_nadic_consts(const uint32_t* n32, uint32_t* nk, uint32_t* r2na, uint32_t* r3na, uint32_t* np);
+/* host test hook (no GPU): the short path's per-call words as the library builds them -- kw: |key|'s
+ * 64 words, corr: 72 29-bit limbs (the N-adic digits of C = 2^(1044 (2^s + 1) + 261 (|key| - 2^s))
+ * mod N^2), d: 36 limbs of N - 2^261.  Returns s = bit length of |key| - 1 (-1 for a zero key), or
+ * -2 when N is outside the path's domain (N <= 2^262 or even). */
+int fbm_test_short_consts(const uint32_t* n32, const uint32_t* key, uint32_t* kw, uint32_t* corr, uint32_t* d);
 
 /* ---- instrumentation -------------------------------------------------------------------
  * fbm_prof_enable(1) makes every entry point record a HIP event pair around each kernel

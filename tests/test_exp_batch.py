@@ -178,3 +178,29 @@ def test_batch_abort_invalidates_recorded_calls():
     torch.cuda.synchronize()
     assert torch.equal(pend[1].finish(), ref[1]) and torch.equal(out[1], ref[1])  # negative key: ran inline
     assert torch.equal(pe.finish(), ref_even) and torch.equal(out_even, ref_even)  # generic engine: ran inline
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("engine", ["single", "triple", "quad"])
+def test_short_path_equals_table_path(engine):
+    """The short path (binary chain, short-base products, the key's constant C: DESIGN.md 5.3) and the
+    window-table path give the same ciphertexts and decryption factors bit for bit, under every engine:
+    positive and negative keys, a key of one bit, the default biprime."""
+    import torch
+
+    from fedbiomed_amd import _device as D, workload as W
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    dev = D.device()
+    n, P = 3000, 3
+    xs = torch.from_numpy(W.party_params(7, n)).to(dev)
+    jc = SecaggCrypter()
+    out = {}
+    for short in (True, False):
+        with D.jl_short(short), D.jl_engine(engine):
+            cts = [jc.encrypt_tensor(P, 5, xs, k, W.BIPRIME0, weight=3) for k in (W.jl_user_key(1), 1, 1 << 2039)]
+            fac = [D.jl_decrypt_factor(700, W.BIPRIME0, k, 5, dev=dev) for k in (W.jl_server_key(P), -1, 2)]
+            torch.cuda.synchronize()
+            out[short] = [c.cpu() for c in cts] + [f.cpu() for f in fac]
+    for a, b in zip(out[True], out[False]):
+        assert torch.equal(a, b)

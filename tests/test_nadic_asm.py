@@ -246,3 +246,37 @@ def test_library_constants_match_and_drive_the_asm():
     t, s, _ = run(N, x, (1, pt))                       # * (N pt + 1), drops R
     assert (t + s * N) % M == (1 + N * pt) * pow(h, e, M) % M
     assert t <= N and s < 2 * N
+
+
+def test_library_short_path_constants():
+    """The short path's per-call words as the library builds them (fbm_test_short_consts): |key|'s
+    words, the digits of C = 2^(1044 (2^s + 1) + 261 (|key| - 2^s)) mod N^2, D = N - 2^261 -- against
+    Python integers, for the default biprime and random odd moduli, 2 040-bit and short keys; moduli
+    at or below 2^262 (and even ones) are outside the path (-2), a zero key has no chain (-1)."""
+    import numpy as np
+
+    from fedbiomed_amd import _build, _native, workload as W
+
+    _build.build()
+    lib = _native.load()
+    rng = random.Random(21)
+    cases = [(W.BIPRIME0, W.jl_user_key(0)), (W.BIPRIME0, 1), (W.BIPRIME0, 3), (_rand_n(rng, 1024), rng.getrandbits(2040)),
+             (_rand_n(rng, 600), rng.getrandbits(900) | 1), ((1 << 262) + 1, 12345), (W.BIPRIME0, 0),
+             ((1 << 262) - 1, 7), (W.BIPRIME0 + 1, 7)]
+    for N, key in cases:
+        n32 = np.frombuffer(N.to_bytes(128, "little"), dtype=np.uint32).copy()
+        k64 = np.frombuffer(abs(key).to_bytes(256, "little"), dtype=np.uint32).copy()
+        kw, corr, d = np.zeros(64, np.uint32), np.zeros(72, np.uint32), np.zeros(36, np.uint32)
+        r = lib.fbm_test_short_consts(n32.ctypes.data, k64.ctypes.data, kw.ctypes.data, corr.ctypes.data, d.ctypes.data)
+        if N <= (1 << 262) or N % 2 == 0:
+            assert r == -2
+            continue
+        assert [int(v) for v in d] == limbs(N - (1 << (LB * KS)))
+        e = abs(key)
+        if e == 0:
+            assert r == -1
+            continue
+        s = e.bit_length() - 1
+        assert r == s and [int(v) for v in kw] == list(k64)
+        C = pow(2, LB * L * ((1 << s) + 1) + LB * KS * (e - (1 << s)), N * N)
+        assert [int(v) for v in corr] == limbs(C % N) + limbs(C // N)
