@@ -1685,16 +1685,17 @@ static int group_ct_per_wg(int engine) { return engine == FBM_ENGINE_TRIPLE ? 84
 
 // modelled launch time (ms) of n_ct ciphertexts on one engine (relative ranking only); refit on the
 // short path (profiles/r3_engine_sweep_short.jsonl): triple 12.3 / 23.1 / 33.0 / 42.9 / 52.7 ms at
-// w = 1 … 5, quad 9.4 / 17.1 / 24.8 / 32.5 / 46.6 at w = 1 / 2 / 3 / 4 / 6, one lane 31.3 (lone waves),
-// 53 (one round of two), then ~50 per round (a tail of at most half a round: ~25)
+// w = 1 … 5, quad 9.4 / 17.1 / 24.8 / 32.5 / 46.6 at w = 1 / 2 / 3 / 4 / 6; the one-lane engine with its
+// unrolled square (profiles/r3_unroll_ab.jsonl) 27.2 (lone waves), 49 (one round of two), then ~45.5 per
+// round (a tail of at most half a round: ~23)
 static double engine_model_ms(int engine, uint64_t n_ct) {
   const uint64_t ncu = (uint64_t)device_num_cu();
   if (engine == FBM_ENGINE_SINGLE) {
     const uint64_t lanes = ncu * 2 * FBM_BLOCK;
-    if (n_ct <= lanes / 2) return 31.3;
-    if (n_ct <= lanes) return 53.0;
+    if (n_ct <= lanes / 2) return 27.2;
+    if (n_ct <= lanes) return 49.0;
     const uint64_t part = n_ct % lanes;
-    return 50.0 * (double)(n_ct / lanes) + (part == 0 ? 0.0 : part <= lanes / 2 ? 25.0 : 50.0);
+    return 45.5 * (double)(n_ct / lanes) + (part == 0 ? 0.0 : part <= lanes / 2 ? 23.0 : 45.5);
   }
   const uint64_t wgs = (n_ct + group_ct_per_wg(engine) - 1) / group_ct_per_wg(engine);
   const uint64_t w = (wgs + ncu - 1) / ncu;

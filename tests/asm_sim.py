@@ -203,6 +203,9 @@ class Lane:
         elif op == "s_movrels_b32":
             m = _ONE.match(ops[1])
             self.put(ops[0], self.r[f"s{int(m.group(2)) + self.r['m0']}"])
+        elif op == "v_movrels_b32":
+            m = _ONE.match(ops[1])
+            self.put(ops[0], self.r[f"v{int(m.group(2)) + self.r['m0']}"])
         elif op == "s_cmp_lg_u32":
             self.scc = int(self.get(ops[0]) != self.get(ops[1]))
         elif op == "s_cbranch_scc1":

@@ -26,6 +26,7 @@ def _gen():
 
 GEN = _gen()
 MM, SQ, SQ_PLAIN = GEN.product(False), GEN.square_tri(), GEN.product(True)
+SQ_UNROLLED = GEN.square_unrolled()
 
 
 def limbs(x, n=L):
@@ -88,7 +89,7 @@ def run_short(N, a, h):
     for j, v in enumerate(limbs(N - (1 << (LB * KS)))):
         lds[DADDR + 8 * j] = v
         lds[DADDR + 8 * j + 4] = 0
-    glb = {HB + k * 1024: v for k, v in enumerate(limbs(h, KS))}
+    glb = {HB + k * 1024: v for k, v in enumerate(limbs(h, KS + 1))}  # (+ limb KS = 0: the last row's prefetch)
     lane = Lane({"a": 0, "h": 0, "hb": HB, "d": DADDR, "NK": NK, "np": np_}, lds=lds, glb=glb, smem=smem)
     counts = lane.run(MS)
     out = [lds[k * 1024] for k in range(2 * L)]
@@ -172,6 +173,10 @@ def test_nadic_asm_product_and_square(bits):
         # one before its quotient -- so the same quotients and the same result)
         t2, s2, c2 = run(N, a, square=SQ_PLAIN)
         assert (t2, s2) == (t, s) and c2["v_mad_u64_u32"] == 36 * 145 + 68
+        # the unrolled square (the shipped one) is the looped one bit for bit, with no jumps or m0
+        t3, s3, c3 = run(N, a, square=SQ_UNROLLED)
+        assert (t3, s3) == (t, s) and c3["v_mad_u64_u32"] == 4658
+        assert "s_setpc_b64" not in c3 and "s_movrels_b32" not in c3
 
 
 def test_nadic_asm_wide_operands():

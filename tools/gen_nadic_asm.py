@@ -470,14 +470,17 @@ def square_tri():
 # (the row-operand prefetch registers, unused here); the multiplier needs no LDS rows.
 # ------------------------------------------------------------------------------------------
 KS = 9
+SHORT_LOOPED = True   # rows 1..8 as a loop (3 KB of code instead of 14 KB: the unrolled square is 43 KB)
 HS = [f"v{MM_NREG + i}" for i in range(KS)]
 D35 = f"v[{_X + 2}:{_X + 3}]"
-MS_NREG = MM_NREG + KS
+HADDR = X1  # (looped rows) the address of the next row's limb of h
+MS_NREG = MM_NREG if SHORT_LOOPED else MM_NREG + KS
 
 
-def short_row(i):
-    """Row i of the short product: multiplier limb h_i (HS[i]), t then s part, both retires."""
-    x, first = HS[i], i == 0
+def short_row(i, x=None):
+    """Row i of the short product: multiplier limb h_i (HS[i], or the register x), t then s part,
+    both retires (rows >= 1 are the same instruction stream whatever i: the loop body)."""
+    x, first = (x or HS[i]), i == 0
     out = [f"v_mad_u64_u32 {TT}, vcc, {x}, {B0(0)}, {'0' if first else At(0)}"]
     for j in range(1, L):
         addend = "0" if (first or j == NW) else At(j)
@@ -514,10 +517,13 @@ def mul_short():
     body = list(load_consts())
     # h's KS limbs: global, workgroup-blocked (limb k at hb + h_off + k * 1024)
     body += ["s_waitcnt vmcnt(0)", f"v_mov_b32 {TMP}, %[h]"]
-    for k in range(KS):
-        if k and k % 4 == 0:
-            body.append(f"v_add_u32 {TMP}, 0x1000, {TMP}")
-        body.append(f"global_load_dword {HS[k]}, {TMP}, %[hb] offset:{(k % 4) * 1024}")
+    if SHORT_LOOPED:  # limb 0 now, each next one prefetched a row ahead (HADDR = its address)
+        body += [f"global_load_dword {X0}, {TMP}, %[hb]", f"v_add_u32 {HADDR}, 0x400, {TMP}"]
+    else:
+        for k in range(KS):
+            if k and k % 4 == 0:
+                body.append(f"v_add_u32 {TMP}, 0x1000, {TMP}")
+            body.append(f"global_load_dword {HS[k]}, {TMP}, %[hb] offset:{(k % 4) * 1024}")
     # B = X from the lane's column (undoubled); the s window <- (D_j, 0), D35 <- (D_35, 0)
     body.append(f"v_add_u32 {AADR}, 0x10000, %[a]")
     for j in range(2 * L):
@@ -528,14 +534,117 @@ def mul_short():
     body += [f"ds_read_b64 {As(j)}, %[d] offset:{8 * j}" for j in range(NW)]
     body += [f"ds_read_b64 {D35}, %[d] offset:{8 * NW}", f"v_mov_b32 {NPV}, %[np]",
              "s_waitcnt vmcnt(0) lgkmcnt(0)"]
-    for i in range(KS):
-        body += short_row(i)
+    if SHORT_LOOPED:  # row 0 peeled, rows 1 .. KS-1 a runtime loop over row pairs (operands X0N / X0)
+        assert (KS - 1) % 2 == 0
+
+        def pref(dst):  # the next row's limb of h, a row ahead
+            return [f"global_load_dword {dst}, {HADDR}, %[hb]", f"v_add_u32 {HADDR}, 0x400, {HADDR}"]
+
+        xb = AADR  # the second operand register (AADR is free once the prologue's loads are in; X0N
+        #            holds D_35 until row 0's last s product)
+        body += pref(xb) + short_row(0, X0) + ["s_waitcnt vmcnt(0)"]
+        body += ["s_mov_b32 s34, 0", "3:"]
+        body += pref(X0) + short_row(1, xb) + ["s_waitcnt vmcnt(0)"]
+        body += pref(xb) + short_row(1, X0) + ["s_waitcnt vmcnt(0)"]
+        body += ["s_add_u32 s34, s34, 1", f"s_cmp_lg_u32 s34, {(KS - 1) // 2}", "s_cbranch_scc1 3b"]
+    else:
+        for i in range(KS):
+            body += short_row(i)
     body += normalise_store()
     return rotate_carries(body)
 
 
 def ms_mads():
     return KS * (4 * L + 1)
+
+
+# ------------------------------------------------------------------------------------------
+# The triangular square with every row unrolled (round 3): the same arithmetic, registers and
+# instruction order per row as square_tri, but with the row index static -- the cross products
+# k = i + 1 .. 35 emitted directly (no computed jump, s_setpc's instruction-buffer refetch), K'_i
+# read from s(62 + i) (no m0 / s_movrels), the diagonal x_(i/2)^2 of an even row from the B
+# register that holds x_(i/2) (no LDS read, no address add), the row operands read at static
+# offsets from the column base (no address add).  4 273 instructions (~35 KB) instead of a loop;
+# bit-identical results (tests/test_nadic_asm.py runs both).
+# ------------------------------------------------------------------------------------------
+UNROLLED_SQUARE = True
+
+
+def sq_row_static(i):
+    first, last, even = i == 0, i == L - 1, i % 2 == 0
+    kreg = f"s{62 + i}"  # K'_i (KBASE + i)
+    out = [] if last else [f"ds_read_b32 {SX0N}, %[a] offset:{(i + 1) * 1024}"]
+    if even:  # the diagonal x0_(i/2)^2 of column i completes it
+        out.append(f"v_mad_u64_u32 {SAt(0)}, vcc, {SB0(i // 2)}, {SB0(i // 2)}, {'0' if first else SAt(0)}")
+    out.append(f"v_mul_lo_u32 {SQ}, {SAtLo(0)}, {SNPV}")
+    # ---- s part: (2 x0_i) * x1, + (K'_i - q), q' ----
+    out.append(f"v_mad_u64_u32 {STS}, vcc, {SX0D}, {SB1(0)}, {'0' if first else SAs(0)}")
+    for j in range(1, L):
+        addend = "0" if (first or j == NW) else SAs(j)
+        out.append(f"v_mad_u64_u32 {SAs(j - 1)}, vcc, {SX0D}, {SB1(j)}, {addend}")
+        if j == 2:
+            out.append(f"v_and_b32 {SQ}, {MASK}, {SQ}")
+        if j == 4:
+            out.append(f"v_sub_u32 {SCQ}, {kreg}, {SQ}")
+        if j == 12:
+            out.append(f"v_mad_u64_u32 {STS}, vcc, {SCQ}, 1, {STS}")
+        if j == 20:
+            out.append(f"v_mul_lo_u32 {SQ2}, {STSLO}, {SNPV}")
+        if j == 26:
+            out.append(f"v_and_b32 {SQ2}, {MASK}, {SQ2}")
+    # ---- t part: doubled cross products 2 x0_i x0_k, k > i (the top position written fresh) ----
+    for k in range(i + 1, L):
+        addend = "0" if (first or k == L - 1) else SAt(k)
+        out.append(f"v_mad_u64_u32 {SAt(k)}, vcc, {SX0D}, {SB0(k)}, {addend}")
+    # ---- t: q * N (shifting the window);  s: q' * N ----
+    top = "0" if last else SAt(L - 1)
+    out.append(f"v_mad_u64_u32 {STT}, vcc, {SQ}, {Ns(0)}, {SAt(0)}")
+    for k in range(1, L):
+        out.append(f"v_mad_u64_u32 {SAt(k - 1)}, vcc, {SQ}, {Ns(k)}, {SAt(k) if k < L - 1 else top}")
+    out.append(f"v_mad_u64_u32 {STS}, vcc, {SQ2}, {Ns(0)}, {STS}")
+    for j in range(1, L):
+        out.append(f"v_mad_u64_u32 {SAs(j - 1)}, vcc, {SQ2}, {Ns(j)}, {SAs(j - 1)}")
+    out += [f"v_lshrrev_b64 {STT}, {LB}, {STT}", f"v_lshl_add_u64 {SAt(0)}, {STT}, 0, {SAt(0)}",
+            f"v_lshrrev_b64 {STS}, {LB}, {STS}", f"v_lshl_add_u64 {SAs(0)}, {STS}, 0, {SAs(0)}"]
+    if not last:
+        out += ["s_waitcnt lgkmcnt(0)", f"v_lshlrev_b32 {SX0D}, 1, {SX0N}"]
+    return out
+
+
+def square_unrolled():
+    body = list(load_consts())
+    body.append(f"v_add_u32 {STMP}, 0x10000, %[a]")
+    for j in range(2 * L):
+        reg = SB0(j) if j < L else SB1(j - L)
+        if j < 64:
+            body.append(f"ds_read_b32 {reg}, %[a] offset:{j * 1024}")
+        else:
+            body.append(f"ds_read_b32 {reg}, {STMP} offset:{(j - 64) * 1024}")
+    body += [f"v_mov_b32 {SNPV}, %[np]", f"ds_read_b32 {SX0}, %[a]", "s_waitcnt lgkmcnt(0)",
+             f"v_lshlrev_b32 {SX0D}, 1, {SX0}"]
+    for i in range(L):
+        body += sq_row_static(i)
+        if i == MID - 1:
+            body += mid_reduce([[SAtLo(k) for k in range(L - 1)], [SAsLo(k) for k in range(NW)]])
+    # diagonals of columns L .. 2L-2 (h >= L/2): column 2h sits at window position 2h - L
+    body += [f"v_mad_u64_u32 {SAt(2 * h - L)}, vcc, {SB0(h)}, {SB0(h)}, {SAt(2 * h - L)}" for h in range(L // 2, L)]
+    body.append(f"v_add_u32 {STMP}, 0x10000, %[a]")
+
+    def st(k, reg):
+        if k < 64:
+            return f"ds_write_b32 %[a], {reg} offset:{k * 1024}"
+        return f"ds_write_b32 {STMP}, {reg} offset:{(k - 64) * 1024}"
+
+    for acc, lo, carry, carry_lo, base in ((SAt, SAtLo, STT, STTLO, 0), (SAs, SAsLo, STS, STSLO, L)):
+        body += [f"v_lshrrev_b64 {carry}, {LB}, {acc(0)}", f"v_and_b32 {lo(0)}, {MASK}, {lo(0)}", st(base, lo(0))]
+        for k in range(1, NW):
+            body += [f"v_lshl_add_u64 {acc(k)}, {carry}, 0, {acc(k)}",
+                     f"v_lshrrev_b64 {carry}, {LB}, {acc(k)}",
+                     f"v_and_b32 {lo(k)}, {MASK}, {lo(k)}",
+                     st(base + k, lo(k))]
+        body.append(st(base + NW, carry_lo))
+    body.append("s_waitcnt lgkmcnt(0)")
+    return rotate_carries(body)
 
 
 def sq_mads():
@@ -565,7 +674,8 @@ def count_mads(lines):
 
 
 def main():
-    mm, sq, ms = product(False), square_tri(), mul_short()
+    mm, sq, ms = product(False), (square_unrolled() if UNROLLED_SQUARE else square_tri()), mul_short()
+    sq_looped = square_tri()
     mm_row, sq_body = row(False, False), sq_row("odd")
     hdr = f"""// GENERATED by tools/gen_nadic_asm.py -- do not edit by hand.
 //
@@ -611,11 +721,20 @@ __device__ __forceinline__ void fbm_na_ms_glb(uint32_t a_off, const uint32_t* hb
       : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
 }}
 
-#ifndef FBM_NA_PLAIN_SQUARE
-// a <- a^2 R^-1 (mod N^2): triangular x0^2 (computed-jump row suffixes), full x0 * 2 x1.
+#if !defined(FBM_NA_PLAIN_SQUARE) && !defined(FBM_NA_LOOPED_SQUARE)
+// a <- a^2 R^-1 (mod N^2): triangular x0^2, full x0 * 2 x1, every row unrolled ({len(sq)} instructions).
 __device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK, uint32_t np) {{
   asm volatile(
 {c_string(sq)}
+      :
+      : [a] "v"(a_off), [NK] "s"(NK), [np] "s"(np)
+      : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
+}}
+#elif defined(FBM_NA_LOOPED_SQUARE)
+// A/B variant (-DFBM_NA_LOOPED_SQUARE): the row loop with computed-jump row suffixes ({len(sq_looped)} instructions).
+__device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK, uint32_t np) {{
+  asm volatile(
+{c_string(sq_looped)}
       :
       : [a] "v"(a_off), [NK] "s"(NK), [np] "s"(np)
       : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
