@@ -701,6 +701,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
       lds_store_uniform<2 * NA>(lds, FBM_BLOCK, SEG(ops, ops_a) + FBM_OPS_CORR);
       fbm_na_mm_glb(aoff, table, tb0, NK, np);
     } else {
+#ifndef FBM_EXP_SHORT_ONLY  // (a measurement variant: the launch's code without the table path)
     if (__any(wide)) {  // wave-uniform: lanes with a narrow h multiply 0 and add nothing
       lds_store_uniform<2 * NA>(lds, FBM_BLOCK, cst + FBM_CST_QR3);
       fbm_na_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, NK, np);  // h_hi*R^2 (wide lanes)
@@ -733,7 +734,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
     }
     if (!SEG(key_is_zero, key_is_zero_a)) {
       lds_to_glb(lds, table + tb0 / 4);
-      fbm_na_sq_lds(aoff, NK, np);  // h^2*R
+      fbm_na_sq_lds_looped(aoff, NK, np);  // h^2*R
       lds_to_glb(lds, table + (tb0 + FBM_TSCRATCH * tstride) / 4);
       glb_to_lds(table + tb0 / 4, lds);
 #pragma unroll 1
@@ -749,10 +750,11 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
         const int nsq = (int)(op >> FBM_OP_SHIFT);
         const int idx = (int)(op & ((1u << FBM_OP_SHIFT) - 1u)) - 1;
 #pragma unroll 1
-        for (int q = 0; q < nsq; ++q) fbm_na_sq_lds(aoff, NK, np);
+        for (int q = 0; q < nsq; ++q) fbm_na_sq_lds_looped(aoff, NK, np);
         if (idx >= 0) fbm_na_mm_glb(aoff, table, tb0 + (uint32_t)idx * tstride, NK, np);
       }
     }
+#endif
     }  // (table path)
     const int mode = SEG(mode, mode_a);
     if ((mode & FBM_EXP_DEC) == 0) {  // nude = (1, pt): 28-bit blocked column -> 29-bit limbs -> scratch
@@ -820,6 +822,10 @@ struct GroupEng<4> {
                             uint32_t e0, uint32_t) {
     fbm_qa_sq_lds(ac, al, QK, np, n, e0);
   }
+  __device__ static void sq_looped(uint32_t ac, uint32_t al, const uint32_t* QK, uint32_t np, const uint32_t (&n)[M],
+                                   uint32_t e0, uint32_t) {
+    fbm_qa_sq_lds_looped(ac, al, QK, np, n, e0);
+  }
   __device__ static void ms(uint32_t ac, uint32_t al, uint32_t dl, uint32_t np, const uint32_t (&n)[M], uint32_t e0,
                             uint32_t) {
     fbm_qa_ms_lds(ac, al, dl, np, n, e0);
@@ -845,6 +851,10 @@ struct GroupEng<3> {
   __device__ static void sq(uint32_t ac, uint32_t al, const uint32_t* QK, uint32_t np, const uint32_t (&n)[M],
                             uint32_t e0, uint32_t bp) {
     fbm_ta_sq_lds(ac, al, QK, np, n, e0, bp);
+  }
+  __device__ static void sq_looped(uint32_t ac, uint32_t al, const uint32_t* QK, uint32_t np, const uint32_t (&n)[M],
+                                   uint32_t e0, uint32_t bp) {
+    fbm_ta_sq_lds_looped(ac, al, QK, np, n, e0, bp);
   }
   __device__ static void ms(uint32_t ac, uint32_t al, uint32_t dl, uint32_t np, const uint32_t (&n)[M], uint32_t e0,
                             uint32_t bp) {
@@ -1034,7 +1044,7 @@ __global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(co
     }
     if (!key_is_zero) {
       qa_lds_to_tbl<M, ROWW>(col, l, table + tb0 / 4);
-      E::sq(ac, al, QK, np29, n, e0, bp);  // h^2 R
+      E::sq_looped(ac, al, QK, np29, n, e0, bp);  // h^2 R (table path: the looped square, cold code)
       qa_lds_to_tbl<M, ROWW>(col, l, scratch);
       qa_tbl_to_lds<M, ROWW>(table + tb0 / 4, col, l);
 #pragma unroll 1
@@ -1049,7 +1059,7 @@ __global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(co
         const int nsq = (int)(op >> FBM_OP_SHIFT);
         const int idx = (int)(op & ((1u << FBM_OP_SHIFT) - 1u)) - 1;
 #pragma unroll 1
-        for (int q = 0; q < nsq; ++q) E::sq(ac, al, QK, np29, n, e0, bp);
+        for (int q = 0; q < nsq; ++q) E::sq_looped(ac, al, QK, np29, n, e0, bp);
         if (idx >= 0) E::mm(ac, al, table, tb0 + (uint32_t)idx * tstride, QK, np29, n, e0, bp);
       }
     }

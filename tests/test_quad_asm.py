@@ -31,6 +31,7 @@ MASK = (1 << LB) - 1
 R = 1 << (LB * L)
 GEOS = {"quad": Q.QUAD, "triple": Q.TRI}
 PROGS = {k: (Q.product(False, g), Q.product(True, g)) for k, g in GEOS.items()}
+LOOPED_SQ = {k: Q.product(True, g, cyc=False) for k, g in GEOS.items()}  # the table path's square
 
 
 def limbs(x, n=L):
@@ -44,7 +45,7 @@ def qconsts(N):
     return [MASK + v for v in limbs(K)], (-pow(N, -1, 1 << LB)) % (1 << LB)
 
 
-def run_quad(N, As, Bs=None, lazy_in=False, geo="quad", in_bounds=True):
+def run_quad(N, As, Bs=None, lazy_in=False, geo="quad", in_bounds=True, looped=False):
     """As / Bs: lists (one per ciphertext = lane group) of digit pairs; Bs None = square.
     Returns per ciphertext the result digit integers (t, s), the max limb and the counts.
     geo "triple": groups of 3 lanes and a trailing dummy lane (zero column, e0 = 0, N = 0,
@@ -90,6 +91,8 @@ def run_quad(N, As, Bs=None, lazy_in=False, geo="quad", in_bounds=True):
         args.update({f"n{r}": 0 for r in range(ML)})
         lanes.append(Lane(args, lds=lds, glb=glb, smem=smem))
     mm, sq = PROGS[geo]
+    if looped:
+        sq = LOOPED_SQ[geo]
     counts = Wave(lanes).run(mm if Bs is not None else sq)
     if G == 3 and in_bounds:
         assert all(lds.get(4 * len(As) + k * ROWB, 0) == 0 for k in range(2 * L)), "dummy column disturbed"
@@ -384,3 +387,17 @@ def test_group_short_product_waits(geo):
                 if dist >= 2:
                     break
             assert dist >= 2, (i, ln)
+
+
+@pytest.mark.parametrize("geo", ["quad", "triple"])
+def test_looped_square_equals_cyclic_band_square(geo):
+    """The table path's looped square (the rows as a runtime loop, no triangular skip) gives the
+    cyclic-band square's residues bit for bit (same column totals at every quotient)."""
+    rng = random.Random(77)
+    from fedbiomed_amd import workload as W
+
+    N = W.BIPRIME0
+    As = [(2 * N - 1, 2 * N - 1)] + [(rng.randrange(2 * N), rng.randrange(2 * N)) for _ in range(2)]
+    got, _, _ = run_quad(N, As, geo=geo)
+    got2, _, _ = run_quad(N, As, geo=geo, looped=True)
+    assert got == got2

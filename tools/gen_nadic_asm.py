@@ -750,6 +750,16 @@ __device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK
       : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
 }}
 #endif
+
+// The looped triangular square (computed-jump row suffixes, {len(sq_looped)} instructions): the table path's squares
+// (small moduli, FDH retries -- cold), so the launch's hot code keeps one copy of the unrolled square.
+__device__ __forceinline__ void fbm_na_sq_lds_looped(uint32_t a_off, const uint32_t* NK, uint32_t np) {{
+  asm volatile(
+{c_string(sq_looped)}
+      :
+      : [a] "v"(a_off), [NK] "s"(NK), [np] "s"(np)
+      : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
+}}
 """
     with open(OUT, "w") as f:
         f.write(hdr)

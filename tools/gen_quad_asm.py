@@ -436,8 +436,8 @@ def rotate_carries(lines, pairs=CARRY_PAIRS):
     return out
 
 
-def product(sq, g=QUAD, carries=CARRY_PAIRS):
-    if sq and CYC_SQUARE:
+def product(sq, g=QUAD, carries=CARRY_PAIRS, cyc=None):
+    if sq and (CYC_SQUARE if cyc is None else cyc):
         return square_cyc(g, carries)
     e = Emitter()
     XA, XB = g.XA, g.XB
@@ -750,6 +750,7 @@ def c_string(lines):
 def header(g, pfx, PFX, name):
     M = g.M
     mm, sq, ms = product(False, g), product(True, g), mul_short(g)
+    sql = product(True, g, cyc=False)
     operands = ", ".join([f'[n{r}] "v"(n[{r}])' for r in range(M)])
     bp_doc, bp_arg, bp_op = "", "", ""
     if g.G == 3:
@@ -809,6 +810,18 @@ __device__ __forceinline__ void fbm_{pfx}_ms_lds(uint32_t ac, uint32_t al, uint3
 {c_string(ms)}
       :
       : [ac] "v"(ac), [al] "v"(al), [dl] "v"(dl), [np] "s"(np), [e0] "v"(e0){bp_op},
+        {operands}
+      : "memory", "vcc", "scc", FBM_{PFX}_CLOBBERS);
+}}
+
+// The looped square ({len(sql)} instructions): the table path's squares (small moduli, FDH retries -- cold), so
+// the launch's hot code keeps one copy of the unrolled cyclic-band square.
+__device__ __forceinline__ void fbm_{pfx}_sq_lds_looped(uint32_t ac, uint32_t al, const uint32_t* QK, uint32_t np,
+                                                     const uint32_t (&n)[{M}], uint32_t e0{bp_arg}) {{
+  asm volatile(
+{c_string(sql)}
+      :
+      : [ac] "v"(ac), [al] "v"(al), [QK] "s"(QK), [np] "s"(np), [e0] "v"(e0){bp_op},
         {operands}
       : "memory", "vcc", "scc", FBM_{PFX}_CLOBBERS);
 }}
