@@ -247,7 +247,8 @@ def main():
             sk.bind(("127.0.0.1", 0))
             port = sk.getsockname()[1]
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        torch.distributed.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                             timeout=distributed.pg_timeout())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     P, tau = args.parties, 1
@@ -936,4 +937,9 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        from fedbiomed_amd import distributed as _dist_guard
+
+        _dist_guard.run_rank(main)  # a rank that raises ends its process non-zero at once
+    else:
+        main()

@@ -544,6 +544,15 @@ class jl_short:
         return False
 
 
+def jl_clear_caches() -> None:
+    """Drops the library's host-side caches (fbm_jl_clear_caches): the short path's constant C per
+    (N, |key|) -- held under a SHA-256 digest of (N, |key|), never the key, and zeroed -- and the
+    per-biprime public parameters.  The reference keeps nothing between calls (a fresh
+    SecaggCrypter per call, fedbiomed/node/secagg/_secagg_round.py:142); call this after a round to
+    do the same (the next call rebuilds C: a few ms of host arithmetic)."""
+    N.load().fbm_jl_clear_caches()
+
+
 def jl_engine_for(n_ct: int) -> str:
     """The engine a launch of n_ct ciphertexts takes under the current policy."""
     return {1: "single", 2: "generic", 3: "triple", 4: "quad"}[N.load().fbm_jl_engine_for(int(n_ct))]

@@ -56,6 +56,7 @@ SIGNATURES = {
     "fbm_jl_triple_mads": (c_int, [c_int]),
     "fbm_jl_set_engine": (c_int, [c_int]),
     "fbm_jl_set_short": (c_int, [c_int]),
+    "fbm_jl_clear_caches": (None, []),
     "fbm_jl_engine_for": (c_int, [c_u64]),
     "fbm_jl_batch_begin": (c_int, []),
     "fbm_jl_batch_abort": (None, []),
@@ -97,6 +98,7 @@ SIGNATURES = {
     "fbm_test_modinv": (c_int, [c_vp, c_vp, c_vp, c_vp]),
     "fbm_test_nadic_consts": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fbm_test_short_consts": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "fbm_test_short_cache": (c_int, [c_vp, c_int]),
     "fbm_test_fdh_gcd": (c_int, [c_vp, c_vp, c_vp]),
     "fbm_test_gen_exp": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp]),
     "fbm_test_gen_combine": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp]),

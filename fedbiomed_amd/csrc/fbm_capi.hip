@@ -354,6 +354,44 @@ static bool jl_generic(const uint32_t* biprime) {
   return (biprime[0] & 1u) == 0u || jl_engine_policy() == FBM_ENGINE_GENERIC;
 }
 
+static std::atomic<int> g_short_on{1};  // fbm_jl_set_short: 0 forces the window-table path (A/B, tests)
+
+// The path a split call (fbm_jl_encrypt_phase / fbm_jl_decrypt_factor_phase) took at its phase 1
+// -- generic or Montgomery engine, short path or not -- keyed by its workspace: the later phases
+// read the constants phase 1 wrote, so they follow phase 1's choice even if the process-wide
+// switches (fbm_jl_set_engine, fbm_jl_set_short) changed in between.  A later phase with no record
+// (the caller never ran phase 1 on this workspace) takes the current switches.
+struct JlPathRec {
+  const void* ws;
+  bool generic, short_on;
+};
+static std::mutex g_path_mu;
+static std::vector<JlPathRec> g_path_recs;  // most recent last, at most 256
+
+static void jl_path_for(const void* ws, int phase, int full, const uint32_t* biprime, bool& generic, bool& short_on) {
+  if (!(phase & 1)) {
+    std::lock_guard<std::mutex> lk(g_path_mu);
+    for (size_t i = g_path_recs.size(); i-- > 0;)
+      if (g_path_recs[i].ws == ws) {
+        generic = g_path_recs[i].generic || (biprime[0] & 1u) == 0u;
+        short_on = g_path_recs[i].short_on;
+        return;
+      }
+  }
+  generic = jl_generic(biprime);
+  short_on = g_short_on.load(std::memory_order_relaxed) != 0;
+  if ((phase & 1) && phase != full) {
+    std::lock_guard<std::mutex> lk(g_path_mu);
+    for (size_t i = 0; i < g_path_recs.size(); ++i)
+      if (g_path_recs[i].ws == ws) {
+        g_path_recs.erase(g_path_recs.begin() + i);
+        break;
+      }
+    if (g_path_recs.size() >= 256) g_path_recs.erase(g_path_recs.begin());
+    g_path_recs.push_back(JlPathRec{ws, generic, short_on});
+  }
+}
+
 // GenCtx of (N, key): M = N^2, Barrett constants of M and N, M = 2^e m2 with m2 odd, m2^-1 mod 2^e
 static int build_gen_ctx(const uint32_t* biprime, const uint32_t* key, int key_negative, GenCtx& g) {
   memset(&g, 0, sizeof(g));
@@ -695,22 +733,60 @@ static Big pow2_mod_big(const Big& E, Big m) {
   return r;
 }
 
+// The short path's constant C per (N, |key|), cached so a round's repeated calls skip the ~2 050
+// host squarings.  An entry holds no key material: it is found by a SHA-256 digest of (N, |key|)
+// and holds only C (a public function of the key, like the ciphertexts it is used for); entries
+// are zeroed when evicted or cleared (fbm_jl_clear_caches).  The reference keeps nothing between
+// calls (a fresh SecaggCrypter per call: fedbiomed/node/secagg/_secagg_round.py:142).
 struct JlShortCacheEntry {
-  uint32_t n32[32];
-  uint32_t key[64];
+  uint32_t digest[8];  // SHA-256(N's 32 words || |key|'s 64 words, little-endian bytes)
   uint32_t corr[72];
 };
 static std::vector<JlShortCacheEntry> g_short_cache;  // guarded by g_jp_mu, at most 32
 
+static void wipe(void* p, size_t n) {  // a zeroing the optimiser keeps
+  volatile uint8_t* v = (volatile uint8_t*)p;
+  while (n--) *v++ = 0;
+}
+
+// SHA-256 of a little-endian word message (host; the FDH kernel's compression function)
+static void sha256_words(const uint32_t* w, int nw, uint32_t out[8]) {
+  uint32_t st[8], W[16];
+  fbm_sha256_init(st);
+  const uint64_t nbytes = (uint64_t)nw * 4;
+  const int nblocks = (int)((nbytes + 9 + 63) / 64);
+  auto byte_at = [&](uint64_t i) -> uint32_t {
+    if (i < nbytes) return (w[i / 4] >> (8 * (i % 4))) & 0xffu;  // little-endian words
+    if (i == nbytes) return 0x80u;
+    const uint64_t tail = (uint64_t)nblocks * 64 - i;  // the 8-byte big-endian bit length
+    if (tail <= 8) return (uint32_t)(((nbytes * 8) >> (8 * (tail - 1))) & 0xffu);
+    return 0u;
+  };
+  for (int b = 0; b < nblocks; ++b) {
+    for (int j = 0; j < 16; ++j) {
+      const uint64_t i = (uint64_t)b * 64 + 4 * j;
+      W[j] = (byte_at(i) << 24) | (byte_at(i + 1) << 16) | (byte_at(i + 2) << 8) | byte_at(i + 3);
+    }
+    fbm_sha256_compress(st, W);
+  }
+  memcpy(out, st, sizeof(st));
+  wipe(W, sizeof(W));
+}
+
+static void short_cache_clear() {
+  std::lock_guard<std::mutex> lk(g_jp_mu);
+  for (JlShortCacheEntry& e : g_short_cache) wipe(&e, sizeof(e));
+  g_short_cache.clear();
+}
+
 // The short path (jl_exp_kernel): possible for N > 2^262 (D = N - 2^261 > the product's quotient
 // m < 2^261); used with a nonzero key.  Returns whether N qualifies (then sh.d is valid and the
 // constants block gets it); sets sc.sbits and sh.kw / sh.corr when the key does too.
-static std::atomic<int> g_short_on{1};  // fbm_jl_set_short: 0 forces the window-table path (A/B, tests)
-
-static bool build_short(const uint32_t* biprime, const uint32_t* key, int is_zero, JlSched& sc, JlShort& sh) {
+static bool build_short(const uint32_t* biprime, const uint32_t* key, int is_zero, JlSched& sc, JlShort& sh,
+                        bool short_on) {
   memset(&sh, 0, sizeof(sh));
   sc.sbits = -1;
-  if (!g_short_on.load(std::memory_order_relaxed)) return false;
+  if (!short_on) return false;
   Big N(biprime, biprime + 32);
   big_trim(N);
   const int KSB = FBM_QA_LB * FBM_NA_SHORT_LIMBS;  // 261
@@ -727,10 +803,16 @@ static bool build_short(const uint32_t* biprime, const uint32_t* key, int is_zer
   const int nb = big_bits(K);
   for (int i = 0; i < 64; ++i) sh.kw[i] = key[i];
   sc.sbits = nb - 1;
+  uint32_t dg[8];
   {
+    uint32_t msg[96];
+    memcpy(msg, biprime, 32 * 4);
+    memcpy(msg + 32, key, 64 * 4);
+    sha256_words(msg, 96, dg);
+    wipe(msg, sizeof(msg));
     std::lock_guard<std::mutex> lk(g_jp_mu);
     for (const JlShortCacheEntry& e : g_short_cache)
-      if (memcmp(e.n32, biprime, sizeof(e.n32)) == 0 && memcmp(e.key, key, sizeof(e.key)) == 0) {
+      if (memcmp(e.digest, dg, sizeof(dg)) == 0) {
         memcpy(sh.corr, e.corr, sizeof(sh.corr));
         return true;
       }
@@ -769,13 +851,19 @@ static bool build_short(const uint32_t* biprime, const uint32_t* key, int is_zer
   big_divmod(C, N, q, r);
   to_limbs_host(r, sh.corr, FBM_QA_L, FBM_QA_LB);
   to_limbs_host(q, sh.corr + FBM_QA_L, FBM_QA_L, FBM_QA_LB);
+  wipe(v.data(), v.size() * 4);  // (K, v, E: the key and its exponent -- not kept)
+  wipe(K.data(), K.size() * 4);
+  wipe(E.data(), E.size() * 4);
   JlShortCacheEntry e;
-  memcpy(e.n32, biprime, sizeof(e.n32));
-  memcpy(e.key, key, sizeof(e.key));
+  memcpy(e.digest, dg, sizeof(dg));
   memcpy(e.corr, sh.corr, sizeof(e.corr));
   std::lock_guard<std::mutex> lk(g_jp_mu);
-  if (g_short_cache.size() >= 32) g_short_cache.erase(g_short_cache.begin());
+  if (g_short_cache.size() >= 32) {
+    wipe(&g_short_cache.front(), sizeof(JlShortCacheEntry));
+    g_short_cache.erase(g_short_cache.begin());
+  }
   g_short_cache.push_back(e);
+  wipe(&e, sizeof(e));
   return true;
 }
 
@@ -874,6 +962,31 @@ int fbm_jl_set_engine(int mode) {
 int fbm_jl_engine_for(uint64_t n_ct) { return jl_engine_for(n_ct); }
 
 int fbm_jl_set_short(int on) { return g_short_on.exchange(on ? 1 : 0); }
+
+void fbm_jl_clear_caches(void) {
+  short_cache_clear();  // the only one derived from a key (zeroed)
+  {
+    std::lock_guard<std::mutex> lk(g_jp_mu);
+    g_jp_cache.clear();  // per-N public parameters
+    g_rk_cache.clear();
+  }
+  std::lock_guard<std::mutex> lk(g_path_mu);
+  g_path_recs.clear();
+}
+
+int fbm_test_short_cache(uint32_t* out, int cap_words) {
+  std::lock_guard<std::mutex> lk(g_jp_mu);
+  const int per = (int)(sizeof(JlShortCacheEntry) / 4);
+  const int n = (int)g_short_cache.size();
+  if (out) {
+    if (cap_words < n * per) {
+      set_error("fbm_test_short_cache: %d words needed", n * per);
+      return FBM_E_ARG;
+    }
+    for (int i = 0; i < n; ++i) memcpy(out + i * per, &g_short_cache[i], sizeof(JlShortCacheEntry));
+  }
+  return n * per;
+}
 
 const char* fbm_last_error(void) { return g_err; }
 
@@ -1054,6 +1167,10 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
     set_error("null biprime/key");
     return FBM_E_ARG;
   }
+  if (!tau) {  // the round is FDH's input: never defaulted (a NULL would silently mean round 0)
+    set_error("null tau (the round's 16 limbs)");
+    return FBM_E_ARG;
+  }
   if (n == 0) return FBM_OK;
   if (cr < 1) {
     set_error("invalid cr=%d", cr);
@@ -1073,7 +1190,9 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
     set_error("negative weight %lld outside (-2^17, 0)", (long long)(int64_t)weight);
     return FBM_E_ARG;
   }
-  if (jl_generic(biprime)) {  // any N (fbm_gen.hip): pack -> FDH -> H^key (N pt + 1) mod N^2
+  bool generic, short_on;
+  jl_path_for(workspace, phase, 3, biprime, generic, short_on);
+  if (generic) {  // any N (fbm_gen.hip): pack -> FDH -> H^key (N pt + 1) mod N^2
     if (es < 1 || es > 100 || (int64_t)es * cr > 1024) {
       set_error("invalid VES parameters es=%d cr=%d", es, cr);
       return FBM_E_ARG;
@@ -1108,7 +1227,7 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
   }
   jp.key_is_zero = is_zero;
   JlShort sh;
-  const bool shq = build_short(biprime, key, is_zero, sc, sh);
+  const bool shq = build_short(biprime, key, is_zero, sc, sh, short_on);
   const uint64_t slots = table_slots_for(n_ct);
   uint8_t* ws = (uint8_t*)workspace;
   uint32_t* ops = (uint32_t*)ws;
@@ -1217,7 +1336,13 @@ static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t
                           int phase = 7) {
   JlParams jp;
   int rc;
-  if (jl_generic(biprime)) {  // any N: FDH, then H^key mod N^2 with the inverse in the same kernel
+  if (!tau) {
+    set_error("null tau (the round's 16 limbs)");
+    return FBM_E_ARG;
+  }
+  bool generic, short_on;
+  jl_path_for(w.ops, phase, 7, biprime, generic, short_on);
+  if (generic) {  // any N: FDH, then H^key mod N^2 with the inverse in the same kernel
     GenCtx g;
     if ((rc = build_gen_ctx(biprime, key, key_negative, g)) || (rc = fdh_params_for_biprime(biprime, tau, ct_offset, jp)))
       return rc;
@@ -1238,7 +1363,7 @@ static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t
   }
   jp.key_is_zero = is_zero;
   JlShort sh;
-  const bool shq = build_short(biprime, key, is_zero, sc, sh);
+  const bool shq = build_short(biprime, key, is_zero, sc, sh, short_on);
   const bool inv = key_negative && !is_zero;
   uint32_t* E = inv ? w.E : factor;
   if (phase & 1) {
@@ -1442,8 +1567,8 @@ int fbm_jl_fdh(uint64_t n_ct, const uint32_t* modulus_odd, int modulus_even, con
   hipStream_t s = (hipStream_t)stream;
   int rc = zero_stats(stats, s);
   if (rc) return rc;
-  if (!modulus_odd) {
-    set_error("null modulus");
+  if (!modulus_odd || !tau) {
+    set_error("null modulus or tau");
     return FBM_E_ARG;
   }
   JlParams jp;
@@ -1553,7 +1678,7 @@ int fbm_jl_powmod(const uint32_t* h, const uint32_t* pt, uint64_t n_ct, const ui
   }
   jp.key_is_zero = is_zero;
   JlShort sh;
-  const bool shq = build_short(biprime, key, is_zero, sc, sh);
+  const bool shq = build_short(biprime, key, is_zero, sc, sh, g_short_on.load(std::memory_order_relaxed) != 0);
   const uint64_t slots = table_slots_for(n_ct);
   if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s, shq ? &sh : nullptr); })))
     return rc;
@@ -1680,9 +1805,7 @@ int fbm_test_short_consts(const uint32_t* n32, const uint32_t* key, uint32_t* kw
   int rc = build_schedule(key, sc, is_zero);
   if (rc) return rc;
   JlShort sh;
-  const int on = g_short_on.exchange(1);
-  const bool q = build_short(n32, key, is_zero, sc, sh);
-  g_short_on.store(on);
+  const bool q = build_short(n32, key, is_zero, sc, sh, true);
   memcpy(kw, sh.kw, sizeof(sh.kw));
   memcpy(corr, sh.corr, sizeof(sh.corr));
   memcpy(d, sh.d, sizeof(sh.d));

@@ -1747,7 +1747,9 @@ struct JlBatchState {
   bool active = false;
   bool accept = false;  // set by the phase-2 entry points only (jl_batch_accept): other calls launch
   JlExpBatch bt;
-  const uint32_t* cst = nullptr;  // the first segment's constants block (all segments: same N)
+  const uint32_t* cst = nullptr;  // the first segment's constants block (all segments: same N), or
+                                  // the first short-path segment's (short_cst)
+  bool short_cst = false;
   uint32_t n32[32];
   uint32_t np = 0;
 };
@@ -1762,6 +1764,7 @@ int jl_batch_begin() {
   }
   memset(&g_batch.bt, 0, sizeof(g_batch.bt));
   g_batch.cst = nullptr;
+  g_batch.short_cst = false;
   g_batch.active = true;
   return FBM_OK;
 }
@@ -1791,6 +1794,13 @@ static int jl_batch_record(const uint32_t* H, uint64_t n_ct, const JlParams& jp,
   } else if (memcmp(g_batch.n32, jp.N32, sizeof(g_batch.n32)) != 0) {
     set_error("every call of a JL exponentiation batch must use the same biprime");
     return FBM_E_ARG;
+  }
+  // the launch reads the short product's pairs (D_j, 0) -- a function of N alone -- from one
+  // constants block: the first segment's whose setup wrote them (a short-path schedule), not
+  // merely the first segment's (that call may have run with the short path off)
+  if (sc.sbits >= 0 && !g_batch.short_cst) {
+    g_batch.short_cst = true;
+    g_batch.cst = cst;
   }
   const uint64_t chunks = (n_ct + FBM_BLOCK - 1) / FBM_BLOCK;
   if ((uint64_t)bt.total_chunks + chunks > 0xFFFFFFFFull) {

@@ -40,9 +40,23 @@ def env_rank() -> Tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+DEFAULT_TIMEOUT_S = 120.0
+
+
+def pg_timeout():
+    """The process group's collective timeout: FBM_DIST_TIMEOUT_S seconds (default 120).  torch's
+    default for NCCL is 10 min -- as long as the driver's whole bench limit, so a collective stuck in
+    an 8-GPU run would be killed at that limit with no line written.  Bounded, a stuck collective
+    raises (gloo) or is aborted by the NCCL watchdog, and the rank exits non-zero well inside it."""
+    from datetime import timedelta
+
+    return timedelta(seconds=float(os.environ.get("FBM_DIST_TIMEOUT_S", DEFAULT_TIMEOUT_S)))
+
+
 def init(backend: str = "nccl", device: Optional[int] = None):
     """One process per GPU; backend "nccl" is RCCL on ROCm (gloo for CPU tests).
-    `device` overrides LOCAL_RANK as the rank's GPU (rehearsals with shared devices)."""
+    `device` overrides LOCAL_RANK as the rank's GPU (rehearsals with shared devices).
+    Collectives time out after pg_timeout()."""
     import torch
     import torch.distributed as dist
 
@@ -52,8 +66,30 @@ def init(backend: str = "nccl", device: Optional[int] = None):
     if world > 1 and not dist.is_initialized():
         if backend == "nccl":
             torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+            # a timed-out RCCL collective tears the process down instead of hanging in it
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=pg_timeout())
     return rank, world, local
+
+
+def run_rank(fn, *args, **kw):
+    """Runs one rank's body; if it raises, prints the traceback and ends the PROCESS at once with
+    status 1 (os._exit: no interpreter shutdown, which could wait on a collective or the process
+    group's teardown).  Its peers then fail their next collective within pg_timeout() and exit
+    non-zero too; under torch.distributed.run the elastic agent stops them as soon as this rank
+    exits, under bench.py's own spawn_ranks the parent does."""
+    import sys
+    import traceback
+
+    try:
+        return fn(*args, **kw)
+    except SystemExit:  # a deliberate exit keeps its status
+        raise
+    except BaseException:  # noqa: BLE001 -- any failure of a rank ends the run
+        traceback.print_exc()
+        sys.stderr.flush()
+        sys.stdout.flush()
+        os._exit(1)
 
 
 # ------------------------------------------------------------------------------------------

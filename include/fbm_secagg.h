@@ -288,6 +288,12 @@ int fbm_jl_engine_for(uint64_t n_ct);
  * sliding-window table path -- an A/B and test switch; results are bit-identical).  Returns the
  * previous setting. */
 int fbm_jl_set_short(int on);
+/* Drops the library's host-side caches: the short path's constant C per (N, |key|) -- kept under a
+ * SHA-256 digest of (N, |key|), never the key itself, and zeroed here and on eviction -- and the
+ * per-biprime public parameters.  The reference keeps nothing between calls (a fresh
+ * SecaggCrypter per call, fedbiomed/node/secagg/_secagg_round.py:142); a caller that wants the
+ * same can call this after each round.  Thread-safe; in-flight calls are unaffected. */
+void fbm_jl_clear_caches(void);
 
 /* Batched exponentiation (one-lane engine), for callers that run several parties' encrypts and
  * the decryption factor on one device (simulation, the benchmark): between fbm_jl_batch_begin
@@ -338,6 +344,10 @@ int fbm_test_nadic_consts(const uint32_t* n32, uint32_t* nk, uint32_t* r2na, uin
  * mod N^2), d: 36 limbs of N - 2^261.  Returns s = bit length of |key| - 1 (-1 for a zero key), or
  * -2 when N is outside the path's domain (N <= 2^262 or even). */
 int fbm_test_short_consts(const uint32_t* n32, const uint32_t* key, uint32_t* kw, uint32_t* corr, uint32_t* d);
+/* host test hook (no GPU): the raw words of the short path's cache entries (each: an 8-word digest
+ * and 72 limbs of C); returns the word count (out == NULL: a size query), FBM_E_ARG if cap_words is
+ * too small. */
+int fbm_test_short_cache(uint32_t* out, int cap_words);
 
 /* ---- instrumentation -------------------------------------------------------------------
  * fbm_prof_enable(1) makes every entry point record a HIP event pair around each kernel

@@ -204,3 +204,51 @@ def test_short_path_equals_table_path(engine):
             out[short] = [c.cpu() for c in cts] + [f.cpu() for f in fac]
     for a, b in zip(out[True], out[False]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_split_calls_follow_their_phase1_path():
+    """a split call (encrypt with defer_exp, a phased factor) takes the path its
+    phase 1 set up -- generic or Montgomery engine, short path or table path -- even when the
+    process-wide switches change before its later phases; and a batch whose first segment ran with the
+    short path off still gives the short-path segments their D pairs.  Every result equals the
+    unsplit call."""
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    dev = D.device()
+    P, tau, n = 3, 2, 1_500
+    keys = [W.jl_user_key(p) for p in range(P)]
+    ws = [W.party_weight(p) for p in range(P)]
+    xs = [torch.from_numpy(W.party_params(p, n)).to(dev) for p in range(P)]
+    jc = SecaggCrypter()
+    sk0 = -sum(keys)
+    ref = [jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=ws[p]) for p in range(P)]
+    n_ct = ref[0].shape[0]
+    fref = jc.decrypt_factor_tensor(tau, n_ct, sk0, W.BIPRIME0)
+    switches = [lambda: D.jl_engine("generic"), lambda: D.jl_short(False)]
+    for sw in switches:
+        # the switch around phase 1 only
+        with sw():
+            pe = jc.encrypt_tensor(P, tau, xs[0], keys[0], W.BIPRIME0, weight=ws[0], defer_exp=True)
+            pf = jc.decrypt_factor_tensor(tau, n_ct, sk0, W.BIPRIME0, phased=True)
+        assert torch.equal(pe.finish(), ref[0])
+        assert torch.equal(pf.exponentiate().finish(), fref)
+        # the switch around the later phases only
+        pe = jc.encrypt_tensor(P, tau, xs[1], keys[1], W.BIPRIME0, weight=ws[1], defer_exp=True)
+        pf = jc.decrypt_factor_tensor(tau, n_ct, sk0, W.BIPRIME0, phased=True)
+        with sw():
+            c1 = pe.finish()
+            pf.exponentiate()
+            f = pf.finish()
+        assert torch.equal(c1, ref[1]) and torch.equal(f, fref)
+    # a batch: party 0's phase 1 with the short path off, the others' with it on
+    with D.deferred_checks():
+        with D.jl_short(False):
+            pend = [jc.encrypt_tensor(P, tau, xs[0], keys[0], W.BIPRIME0, weight=ws[0], defer_exp=True)]
+        pend += [jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=ws[p], defer_exp=True)
+                 for p in range(1, P)]
+        with D.jl_exp_batch(dev):
+            cts = [q.finish() for q in pend]
+    for p in range(P):
+        assert torch.equal(cts[p], ref[p]), p
+    torch.cuda.synchronize()
