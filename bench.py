@@ -157,6 +157,9 @@ def quiet_clipping_warnings():
     logging.getLogger("fedbiomed_amd").addFilter(Once())
 
 
+XGMI_LINK_BPS = 153e9  # one xGMI link, one direction (7 per MI355X): the all-gather model of the scaling probe
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -584,11 +587,25 @@ def main():
                 hig = distributed.shard_range(n, g, 0, cr)[1]
                 kg = (hig + cr - 1) // cr
                 tg = t_stage(lambda kg=kg, hig=hig: agg_alone(kg, hig))
+                # the split's final all-gather of the float64 output (8 bytes per element): each rank
+                # receives the other (g - 1) stripes -- modelled, not measured (one GPU here), at the xGMI
+                # link rate: over one link at a time (a single-channel ring, the conservative bound) and
+                # over the g - 1 direct links in parallel (a fully connected 8-GPU node)
+                gb = (g - 1) / g * 8 * n
+                t_ring, t_direct = gb / XGMI_LINK_BPS, gb / ((g - 1) * XGMI_LINK_BPS)
                 probe[f"n{g}"] = {"stripe_elements": hig, "stripe_ciphertexts": kg, "T_agg_stripe_ms": 1000 * tg,
-                                  "engine": D.jl_engine_for(kg), "ratio_whole_over_stripe": t_agg / tg}
+                                  "engine": D.jl_engine_for(kg), "ratio_whole_over_stripe": t_agg / tg,
+                                  "gather_bytes_per_rank": gb,
+                                  "T_gather_model_ms": {"ring_one_link": 1000 * t_ring,
+                                                        "direct_all_links": 1000 * t_direct},
+                                  "ratio_with_gather": t_agg / (tg + t_ring),
+                                  "ratio_with_gather_direct": t_agg / (tg + t_direct)}
             line["stages"]["agg_scaling_probe"] = dict(probe["n8"], curve=probe, note=(
                 "T_agg(whole vector) / T_agg(rank 0's stripe of an N-GPU split) on one GPU, N = 2 / 4 / 8: the "
-                "aggregate step's strong-scaling bound (north star: >= 6x at N = 8); top-level fields = N = 8"))
+                "aggregate step's strong-scaling bound (north star: >= 6x at N = 8); top-level fields = N = 8. "
+                "ratio_with_gather adds the split's all-gather of the float64 output to the stripe's time: "
+                "gather_bytes_per_rank / the xGMI link rate (%.0f GB/s per link, 7 links per MI355X; one link at a "
+                "time = the conservative bound; _direct: the g - 1 links in parallel)" % (XGMI_LINK_BPS / 1e9)))
         if args.scheme == "jl":
             del cts_all
 
@@ -913,10 +930,20 @@ def main():
                   for p, u in enumerate(ids)]
             O.lom_crypter_aggregate(ys, total_w)
         tc = time.perf_counter() - t0
+        try:
+            avail = len(os.sched_getaffinity(0))  # the cores this process may run on (the box's CPU share)
+        except (AttributeError, OSError):
+            avail = os.cpu_count() or 1
         line["cpu_baseline"] = {"value": ns / tc, "unit": "params/s", "cores": 1, "kind": "port",
                                 "sample": f"{ns:,} elements x {P} parties, encrypt all + aggregate, "
                                           f"{tc:.1f} s on 1 host core (oracle/secagg_oracle.py; GMP mpz_powm "
-                                          f"via ctypes as gmpy2 does)"}
+                                          f"via ctypes as gmpy2 does)",
+                                "host_cores": {"available": avail, "machine": os.cpu_count()},
+                                "ideal_all_cores": {
+                                    "value": ns / tc * avail, "unit": "params/s", "cores": avail,
+                                    "note": "the 1-core rate x the cores available to this process (SURVEY 8(d)): "
+                                            "the reference is single-threaded; every ciphertext is independent, so "
+                                            "this is the ceiling of a perfectly parallel CPU port, not a measurement"}}
         cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")  # tools/calibrate_cpu.py
         if os.path.exists(cal):
             with open(cal) as fh:

@@ -29,6 +29,7 @@ from .exceptions import FedbiomedSecaggCrypterError, FedbiomedSecaggError
 
 U64_MAX = 2**64 - 1
 FBM_WARN_CLIPPED = 16  # stats flag: some |x| > clipping range (a warning, not an error)
+FBM_STAT_MAXBITS, FBM_STAT_ERRFLAGS = 0, 1  # status words (csrc/fbm_internal.hpp)
 
 logger = logging.getLogger("fedbiomed_amd")
 
@@ -93,6 +94,12 @@ class deferred_checks:
 
     _tls = threading.local()  # per thread: another thread's calls keep their own checks
 
+    def __init__(self, merge: bool = False):
+        """merge: the calls inside are stripes of ONE logical call (the list API's overlapped encrypt):
+        their status words are combined -- error flags OR-ed, the max bit length maxed -- and checked
+        once, so a clipping warning is logged once per call, as the reference logs it."""
+        self._merge = merge
+
     @staticmethod
     def _stack() -> List[list]:
         st = getattr(deferred_checks._tls, "stack", None)
@@ -113,6 +120,12 @@ class deferred_checks:
         for _, _, ev in pending:
             ev.synchronize()
         host = torch.stack([st for st, _, _ in pending]).cpu().numpy()  # one copy for all of them
+        if self._merge:
+            assert len({nodes for _, (nodes, _), _ in pending}) == 1 and all(p is None for _, (_, p), _ in pending)
+            row = host[:1].copy()
+            row[0, FBM_STAT_MAXBITS] = host[:, FBM_STAT_MAXBITS].astype(np.uint32).max()
+            row[0, FBM_STAT_ERRFLAGS] = np.bitwise_or.reduce(host[:, FBM_STAT_ERRFLAGS].astype(np.uint32))
+            pending, host = pending[:1], row
         try:
             for (_, (nodes, post), _), row in zip(pending, host):
                 _check_stats_host(row, nodes)
@@ -551,6 +564,39 @@ def jl_clear_caches() -> None:
     SecaggCrypter per call, fedbiomed/node/secagg/_secagg_round.py:142); call this after a round to
     do the same (the next call rebuilds C: a few ms of host arithmetic)."""
     N.load().fbm_jl_clear_caches()
+
+
+def one_lane_round(dev=None) -> int:
+    """Ciphertexts the one-lane engine holds resident at once: 64 lanes x 2 waves per SIMD x 4 SIMDs
+    per CU x the device's CUs (131 072 on MI355X)."""
+    if os.environ.get("FBM_ONE_LANE_ROUND"):  # (tests: stripes of the list API's overlapped encrypt)
+        return max(1, int(os.environ["FBM_ONE_LANE_ROUND"]))
+    dev = dev or device()
+    return 512 * torch.cuda.get_device_properties(dev).multi_processor_count
+
+
+def list_encrypt_stripes(n_ct: int, dev=None) -> List[Tuple[int, int]]:
+    """Ciphertext stripes [c0, c1) of the list API's overlapped encrypt: one per full one-lane round,
+    the partial round last (a single stripe below two rounds' worth: nothing to overlap there)."""
+    r = one_lane_round(dev)
+    if n_ct < 2 * r:
+        return [(0, n_ct)]
+    cuts = list(range(0, n_ct, r)) + [n_ct]
+    if n_ct - cuts[-2] < r // 8:  # a sliver of a tail rides with the last full round
+        cuts.pop(-2)
+    return list(zip(cuts[:-1], cuts[1:]))
+
+
+_SIDE = {}
+
+
+def side_stream(dev=None) -> torch.cuda.Stream:
+    """A per-device side stream (the list API's device-to-host copies beside the next stripe's compute)."""
+    dev = dev or device()
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=dev)
+    return _SIDE[key]
 
 
 def jl_engine_for(n_ct: int) -> str:

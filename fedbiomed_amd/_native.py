@@ -124,8 +124,14 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             lib = ctypes.CDLL(path)
         except OSError as e:  # pragma: no cover - depends on the box
             raise NativeUnavailable(f"cannot load {path}: {e}") from e
+        variant = "FBM_LIB_PATH" in os.environ  # an A/B build (tools/ab.sh) may predate newer symbols
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
+            try:
+                fn = getattr(lib, name)
+            except AttributeError:
+                if variant:
+                    continue
+                raise
             fn.restype = res
             fn.argtypes = args
         if lib.fbm_abi_version() != ABI_VERSION:

@@ -250,6 +250,30 @@ static void build_quad(const Big& N, const Big& M, QuadCtx& qa) {
   uint32_t k29[FBM_QA_L];
   to_limbs_host(K, k29, L, LB);
   for (int j = 0; j < L; ++j) qa.kp[j] = ((1u << LB) - 1u) + k29[j];
+  {  // the one-lane square's initial s window: 2^29 - 1 + P'_j, P' = (K - E) mod N (fbm_nadic_asm.hpp)
+    Big E(40, 0u);
+    for (int c = 0; c < 64; ++c)
+      if ((FBM_NA_SQ_ONE_MASK >> c) & 1ull) {
+        const int bit = 32 + LB * c;
+        E[bit >> 5] |= 1u << (bit & 31);
+      }
+    Big q, r;
+    big_divmod(E, N, q, r);  // E mod N
+    Big P(K.begin(), K.end());
+    P.resize(N.size() + 1, 0u);
+    if (big_cmp(P, r) < 0) {  // P' = K - r (+ N)
+      uint64_t c = 0;
+      for (size_t k = 0; k < P.size(); ++k) {
+        c += (uint64_t)P[k] + (k < N.size() ? N[k] : 0u);
+        P[k] = (uint32_t)c;
+        c >>= 32;
+      }
+    }
+    big_sub_inplace(P, r);
+    uint32_t p29[FBM_QA_L];
+    to_limbs_host(P, p29, L, LB);
+    for (int j = 0; j < L; ++j) qa.sqp[j] = ((1u << LB) - 1u) + p29[j];
+  }
   to_limbs_host(N, qa.n, L, LB);
   for (int e = 2; e <= 3; ++e) {
     const Big u = big_pow2_mod(e * L * LB, M);

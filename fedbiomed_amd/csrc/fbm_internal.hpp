@@ -67,7 +67,10 @@ int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t 
 // 64 words) and its correction constant C (N-adic digits, 72 29-bit limbs; JlSched::corr)
 #define FBM_OPS_KW FBM_MAX_OPS
 #define FBM_OPS_CORR (FBM_MAX_OPS + 64)
-#define FBM_OPS_WORDS (FBM_MAX_OPS + 64 + 128)
+// C's broadcast column: limb k at word FBM_OPS_CBC + 256 k (the one-lane engine reads it as a B operand
+// with a zero lane offset: every lane the same address)
+#define FBM_OPS_CBC (((FBM_MAX_OPS + 64 + 128) + 255) / 256 * 256)
+#define FBM_OPS_WORDS (FBM_OPS_CBC + 72 * 256)
 
 // per-call device constants (words): M, R^2 (74 limbs, padded to 128), the broadcast
 // column 1 (limb k at word k*256) and R^(P+1) mod M (the aggregate's uniform first operand,
@@ -96,7 +99,10 @@ int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t 
 #define FBM_CST_MN (FBM_CST_QR3 + 128)
 // the short-base product's pairs (D_j, 0), D = N - 2^(29 * 9) (72 words; JlShort::d)
 #define FBM_CST_QD (FBM_CST_MN + 128)
-#define FBM_CST_WORDS (FBM_CST_QD + 128)
+// the one-lane square's initial s window (round 4, K' folded): pairs (2^29 - 1 + P'_j, 0),
+// P' = (K - E) mod N (QuadCtx::sqp; FBM_NA_SQ_ONE_MASK in fbm_nadic_asm.hpp)
+#define FBM_CST_QP (FBM_CST_QD + 128)
+#define FBM_CST_WORDS (FBM_CST_QP + 128)
 
 // sliding-window schedule, passed by value (kernarg segment -> scalar loads).
 // op k (u16): (squarings before the multiply) << FBM_OP_SHIFT | (table index + 1, 0 = none)
@@ -135,6 +141,7 @@ struct QuadCtx {
   uint32_t r3[72];   // R^3 mod N^2 likewise
   uint32_t np;       // -N^-1 mod 2^29
   uint32_t pad[3];
+  uint32_t sqp[36];  // 2^29 - 1 + P'_j: the one-lane square's initial s window (FBM_CST_QP)
 };
 
 struct JlParams {

@@ -139,9 +139,32 @@ __global__ void __launch_bounds__(256) jl_pack_wide_kernel(const uint64_t* __res
   }
 }
 
+#define FBM_QMASK ((1u << FBM_QA_LB) - 1u)  // the 29-bit engines' limb mask
+
+// radix changes between the shared final step's 28-bit limbs and the engines' 29-bit limbs
+// (both normalised: every limb below its radix)
+__device__ __forceinline__ void relimb_29_28(const uint32_t (&x)[FBM_QA_L], uint32_t (&o)[FBM_NLN]) {
+#pragma unroll
+  for (int j = 0; j < FBM_NLN; ++j) {
+    const int bit = j * FBM_LB, k = bit / FBM_QA_LB, off = bit % FBM_QA_LB;
+    const uint64_t v = ((uint64_t)(k + 1 < FBM_QA_L ? x[k + 1] : 0u) << FBM_QA_LB) | (k < FBM_QA_L ? x[k] : 0u);
+    o[j] = (uint32_t)(v >> off) & FBM_LMASK;
+  }
+}
+__device__ __forceinline__ void relimb_28_29(const uint32_t* x, uint32_t* o) {  // FBM_NLN -> FBM_QA_L limbs
+#pragma unroll
+  for (int k = 0; k < FBM_QA_L; ++k) {
+    const int bit = k * FBM_QA_LB, j = bit / FBM_LB, off = bit % FBM_LB;
+    const uint64_t v = ((uint64_t)(j + 1 < FBM_NLN ? x[j + 1] : 0u) << FBM_LB) | (j < FBM_NLN ? x[j] : 0u);
+    o[k] = (uint32_t)(v >> off) & FBM_QMASK;
+  }
+}
+
 // ------------------------------------------------------------------------------------
-// nude = N*pt + 1 as the N-adic digit pair (1, pt)  ->  [limb][ct] 28-bit limbs (the last
-// operand of jl_exp_kernel's encrypt; pt < 2^1024 < R is a valid one-off digit)
+// nude = N*pt + 1 as the N-adic digit pair (1, pt)  ->  [limb][ct] 29-bit limbs in the engines' B
+// layout: rows 0..35 digit 0 (= 1), rows 36..71 digit 1, 256-ciphertext blocks FBM_NL rows apart
+// (the last operand of the exponentiation's encrypt, read in place by jl_exp_kernel; pt < 2^1036
+// < R is a valid one-off digit)
 // ------------------------------------------------------------------------------------
 // negative != 0 (a negative weight, see jl_pack_kernel): pt holds |pt| and N*pt + 1 is
 // (1, M - |pt|) with M = N * 2^(1036 - bits(N)) = 0 (mod N): 2^1035 <= M < R, so the digit is
@@ -169,12 +192,14 @@ __global__ void __launch_bounds__(256) jl_nude_kernel(const uint32_t* __restrict
     }
   }
   // N*pt + 1 in N-adic digits is (1, pt): no arithmetic, only the layout of the
-  // exponentiation's B operand (blocked column, digit 0 in limbs 0..36, digit 1 in 37..73)
+  // exponentiation's B operand (blocked column, 29-bit limbs: digit 0 in rows 0..35, digit 1 in 36..71)
+  uint32_t p29[FBM_QA_L];
+  relimb_28_29(p28, p29);
   uint32_t* dst = launder_v(nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255));
 #pragma unroll
-  for (int k = 0; k < FBM_NLN; ++k) dst[k * 256] = k == 0 ? 1u : 0u;
+  for (int k = 0; k < FBM_QA_L; ++k) dst[k * 256] = k == 0 ? 1u : 0u;
 #pragma unroll
-  for (int k = 0; k < FBM_NLN; ++k) dst[(FBM_NLN + k) * 256] = p28[k];
+  for (int k = 0; k < FBM_QA_L; ++k) dst[(FBM_QA_L + k) * 256] = p29[k];
 }
 
 // ------------------------------------------------------------------------------------
@@ -518,26 +543,6 @@ __device__ __forceinline__ void na_final_digits(uint32_t (&t)[FBM_NLN], uint32_t
   from28<FBM_NL, 64>(v28, w);
 }
 
-#define FBM_QMASK ((1u << FBM_QA_LB) - 1u)  // the 29-bit engines' limb mask
-
-// radix changes between the shared final step's 28-bit limbs and the engines' 29-bit limbs
-// (both normalised: every limb below its radix)
-__device__ __forceinline__ void relimb_29_28(const uint32_t (&x)[FBM_QA_L], uint32_t (&o)[FBM_NLN]) {
-#pragma unroll
-  for (int j = 0; j < FBM_NLN; ++j) {
-    const int bit = j * FBM_LB, k = bit / FBM_QA_LB, off = bit % FBM_QA_LB;
-    const uint64_t v = ((uint64_t)(k + 1 < FBM_QA_L ? x[k + 1] : 0u) << FBM_QA_LB) | (k < FBM_QA_L ? x[k] : 0u);
-    o[j] = (uint32_t)(v >> off) & FBM_LMASK;
-  }
-}
-__device__ __forceinline__ void relimb_28_29(const uint32_t* x, uint32_t* o) {  // FBM_NLN -> FBM_QA_L limbs
-#pragma unroll
-  for (int k = 0; k < FBM_QA_L; ++k) {
-    const int bit = k * FBM_QA_LB, j = bit / FBM_LB, off = bit % FBM_LB;
-    const uint64_t v = ((uint64_t)(j + 1 < FBM_NLN ? x[j + 1] : 0u) << FBM_LB) | (j < FBM_NLN ? x[j] : 0u);
-    o[k] = (uint32_t)(v >> off) & FBM_QMASK;
-  }
-}
 
 // a 64-word (2048-bit) row -> its 72 29-bit limbs (h_lo, h_hi): h = h_lo + h_hi 2^1044
 __device__ __forceinline__ void to29_row64(const uint32_t (&w)[64], uint32_t (&o)[2 * FBM_QA_L]) {
@@ -616,10 +621,19 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
   uint32_t* lds = lds_a + tid;
   const uint32_t aoff = lds_addr(lds);
   const uint32_t* NK = cst + FBM_CST_NA29;
-  // the short-base product's pairs (D_j, 0) in LDS row FBM_NL (no product touches it; the
-  // chunk loop's first barrier orders the writes before any read)
+  // LDS row FBM_NL (no product touches it; the chunk loop's first barrier orders the writes before
+  // any read): words 0..71 the short-base product's initial s pairs (D'_j, 0), D'_j = D_j + (2^29 - 1)
+  // [j < 9] + [j == 0] (fbm_na_ms_reg: the rows' 2^29 - 1 - q_i folded in); words 72..143 the square's
+  // (2^29 - 1 + P'_j, 0) (fbm_na_sq_lds)
   const uint32_t doff = lds_addr(lds_a + FBM_NL * FBM_BLOCK);
-  if (tid < 72) lds_a[FBM_NL * FBM_BLOCK + tid] = launder_s(cst)[FBM_CST_QD + tid];
+  const uint32_t koff = doff + 72u * 4u;
+  if (tid < 72) {
+    uint32_t v = launder_s(cst)[FBM_CST_QD + tid];
+    if (!(tid & 1)) v += ((tid >> 1) < FBM_NA_SHORT_LIMBS ? FBM_QMASK : 0u) + (tid == 0 ? 1u : 0u);
+    lds_a[FBM_NL * FBM_BLOCK + tid] = v;
+  } else if (tid < 144) {
+    lds_a[FBM_NL * FBM_BLOCK + tid] = launder_s(cst)[FBM_CST_QP + tid - 72];
+  }
   constexpr int NA = FBM_NA_LIMBS;
   static_assert(NA == FBM_QA_L && FBM_NA_LIMB_BITS == FBM_QA_LB && 2 * NA <= FBM_NL, "one-lane engine limbs");
   // byte offset of this lane's table entry 0 (entries FBM_NL*256 words apart)
@@ -652,7 +666,8 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
     const uint64_t ct = valid ? ct_raw : n_ct - 1;
     bool wide = false, shortp = false;
     const int sbits = SEG(sbits, sbits_a);
-    {  // h -> 29-bit limbs -> scratch entry 16
+    uint32_t hs[FBM_NA_SHORT_LIMBS];  // the short path's h: its 9 limbs, in registers for the whole chain
+    {  // h -> 29-bit limbs -> (table path) scratch entry 16
       uint32_t h[64];
       if (SEG(key_is_zero, key_is_zero_a)) {
 #pragma unroll
@@ -672,6 +687,8 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
         // the short path (binary chain, short-base products): every lane's h below 2^261 -- one
         // FDH digest, always for a 1024-bit N -- and a schedule for it (sbits >= 0: N > 2^262, key != 0)
         shortp = sbits >= 0 && !SEG(key_is_zero, key_is_zero_a) && !__any(wide || mid != 0u);
+#pragma unroll
+        for (int k = 0; k < FBM_NA_SHORT_LIMBS; ++k) hs[k] = h29[k];
         if (shortp) lds_store_col(lds, FBM_BLOCK, h29);  // A = (h, 0), raw (no Montgomery form)
         if (wide) {  // FDH retries (small moduli only): h_hi R^2 = (h_hi, 0) * R^3 R^-1 -> entry 1
 #pragma unroll
@@ -681,7 +698,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
           }
         }
       }
-      col_store(table + (tb0 + FBM_TSCRATCH * tstride) / 4, h29);
+      if (!shortp) col_store(table + (tb0 + FBM_TSCRATCH * tstride) / 4, h29);
     }
     if (shortp) {
       // left-to-right binary over |key| below its top bit: a squaring per bit, a short-base
@@ -694,12 +711,12 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
       for (int j = sbits - 1; j >= 0; --j) {
         if (j == sbits - 1 || (j & 31) == 31)  // one exponent word per 32 bits, loaded ahead of the squaring
           w = __builtin_amdgcn_readfirstlane(launder_s(kw)[j >> 5]);
-        fbm_na_sq_lds(aoff, NK, np);
-        if ((w >> (j & 31)) & 1u) fbm_na_ms_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, doff, NK, np);
+        fbm_na_sq_lds(aoff, koff, NK, np);
+        if ((w >> (j & 31)) & 1u) fbm_na_ms_reg(aoff, hs, doff, NK, np);
       }
-      lds_to_glb(lds, table + tb0 / 4);  // the chain -> entry 0; A <- C (uniform)
-      lds_store_uniform<2 * NA>(lds, FBM_BLOCK, SEG(ops, ops_a) + FBM_OPS_CORR);
-      fbm_na_mm_glb(aoff, table, tb0, NK, np);
+      // x C: the chain stays the LDS operand, C (uniform) is the B operand read from its broadcast
+      // column in the ops buffer (limb k at word k * 256, every lane the same address)
+      fbm_na_mm_glb(aoff, SEG(ops, ops_a) + FBM_OPS_CBC, 0u, NK, np);
     } else {
 #ifndef FBM_EXP_SHORT_ONLY  // (a measurement variant: the launch's code without the table path)
     if (__any(wide)) {  // wave-uniform: lanes with a narrow h multiply 0 and add nothing
@@ -757,14 +774,10 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
 #endif
     }  // (table path)
     const int mode = SEG(mode, mode_a);
-    if ((mode & FBM_EXP_DEC) == 0) {  // nude = (1, pt): 28-bit blocked column -> 29-bit limbs -> scratch
-      const uint32_t* nb = SEG(nude, nude_a) + (ct >> 8) * (FBM_NL * 256) + (ct & 255);
-      uint32_t a28[FBM_NL], b29[2 * NA];
-      col_load(nb, a28);
-      relimb_28_29(a28, b29);
-      relimb_28_29(a28 + FBM_NLN, b29 + NA);
-      col_store(table + (tb0 + FBM_TSCRATCH * tstride) / 4, b29);
-      fbm_na_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, NK, np);
+    if ((mode & FBM_EXP_DEC) == 0) {  // x nude = (1, pt): jl_nude_kernel's 29-bit blocked column, read in place
+      // (a chunk is one 256-ciphertext block: its base is uniform, the lane's offset is tid)
+      const uint32_t* nb = SEG(nude, nude_a) + uniform_val((uint64_t)(ct >> 8)) * (FBM_NL * 256);
+      fbm_na_mm_glb(aoff, nb, (uint32_t)(ct & 255) * 4u, NK, np);
     } else {
       fbm_na_mm_glb(aoff, cst + FBM_CST_ONE, 0u, NK, np);
     }
@@ -1064,7 +1077,7 @@ __global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(co
       }
     }
     }  // (table path)
-    {  // last operand: nude = (1, pt) (encrypt; 28-bit blocked column -> 29-bit slice) or 1
+    {  // last operand: nude = (1, pt) (encrypt; jl_nude_kernel's 29-bit rows, the lane's slice) or 1
       uint32_t b18[2 * M];
       const uint32_t* nb = nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255);
 #pragma unroll
@@ -1075,10 +1088,7 @@ __global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(co
           uint32_t v = 0;
           if (dummy) {
           } else if ((mode & FBM_EXP_DEC) == 0) {
-            const int bit = k * FBM_QA_LB, j = bit / FBM_LB, off = bit % FBM_LB;
-            const uint32_t a0 = j < FBM_NLN ? nb[(d * FBM_NLN + j) * 256] : 0u;
-            const uint32_t a1 = j + 1 < FBM_NLN ? nb[(d * FBM_NLN + j + 1) * 256] : 0u;
-            v = (uint32_t)((((uint64_t)a1 << FBM_LB) | a0) >> off) & FBM_QMASK;
+            v = nb[(d * FBM_QA_L + k) * 256];  // jl_nude_kernel's 29-bit rows
           } else {
             v = (d == 0 && k == 0) ? 1u : 0u;
           }
@@ -1444,10 +1454,11 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_lift_kernel(uint64_t n_ct, Jl
     mont_csub(acc, mn.M);
   }
   if (nude) {  // v <- (v + p y) mod N; p < 2^1036 = R_N, Y' < 2N: p Y' R_N^-1 < 3N
-    uint32_t p28[FBM_NLN];
+    uint32_t p28[FBM_NLN], p29[FBM_QA_L];
     const uint32_t* nb = nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255);
 #pragma unroll
-    for (int k = 0; k < FBM_NLN; ++k) p28[k] = nb[(FBM_NLN + k) * 256];
+    for (int k = 0; k < FBM_QA_L; ++k) p29[k] = nb[(FBM_QA_L + k) * 256];  // jl_nude_kernel's 29-bit digit 1
+    relimb_29_28(p29, p28);
     mont_mul(p28, lds, ls, mn);  // p y
     uint32_t c = 0;
 #pragma unroll
@@ -1626,6 +1637,7 @@ __global__ void jl_setup_kernel(JlSched sc, MontCtx mc, MontCtxN mn, NadicCtx na
   if (t < 128) {
     cst[FBM_CST_QR2 + t] = t < 2 * FBM_QA_L ? qa.r2[t] : 0u;
     cst[FBM_CST_QR3 + t] = t < 2 * FBM_QA_L ? qa.r3[t] : 0u;
+    cst[FBM_CST_QP + t] = t < 2 * FBM_QA_L && !(t & 1) ? qa.sqp[t >> 1] : 0u;
   }
   for (int i = t; i < FBM_NL * 256; i += blockDim.x) {
     const int k = i >> 8, l = i & 255;
@@ -1639,6 +1651,7 @@ __global__ void jl_short_setup_kernel(JlShort sh, uint32_t* __restrict__ ops, ui
   const int t = threadIdx.x;
   if (t < 64) ops[FBM_OPS_KW + t] = sh.kw[t];
   if (t < 72) ops[FBM_OPS_CORR + t] = sh.corr[t];
+  if (t < 72) ops[FBM_OPS_CBC + t * 256] = sh.corr[t];  // C's broadcast column (the one-lane engine's B)
   if (t < 72) cst[FBM_CST_QD + t] = (t & 1) ? 0u : sh.d[t >> 1];
 }
 

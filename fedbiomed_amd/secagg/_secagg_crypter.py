@@ -159,14 +159,51 @@ class SecaggCrypter:
         _check_weight(weight, jl=True)  # after quantize, before the (empty) protect: the reference's order
         if not params:
             return []
-        x = host.to(D.device())
-        ct = self.encrypt_tensor(num_nodes, current_round, x, key, biprime, clipping_range, weight, target_range)
-        packed = D.to_host(ct).numpy().view(np.uint32)
-        out = D.limbs_to_ints(packed)
+        dev = D.device()
+        x = host.to(dev)
+        _, cr = D.jl_slot(target_range, num_nodes)
+        stripes = D.list_encrypt_stripes((x.numel() + cr - 1) // cr, dev)
+        if len(stripes) == 1:
+            ct = self.encrypt_tensor(num_nodes, current_round, x, key, biprime, clipping_range, weight, target_range)
+            packed = D.to_host(ct).numpy().view(np.uint32)
+            out = D.limbs_to_ints(packed)
+        else:
+            packed, out = self._encrypt_overlapped(num_nodes, current_round, x, key, biprime, clipping_range, weight,
+                                                   target_range, stripes, cr)
         if wire.enabled():
             out = wire.EncryptedParams(out, "jl", packed)
         logger.debug(f"Encryption of the parameters took {time.process_time() - start} seconds.")
         return out
+
+    def _encrypt_overlapped(self, num_nodes, current_round, x, key, biprime, clipping_range, weight, target_range,
+                            stripes, cr):
+        """The list API's encrypt as ct_offset stripes (one per full one-lane round, the partial round
+        last), issued back to back on the current stream; each stripe's ciphertexts go to a pinned host
+        buffer on a side stream, and the host builds the Python ints of stripe k while the GPU
+        exponentiates stripe k + 1 (the ciphertext of index k depends only on k: the stripes
+        concatenate bit for bit to the unsplit call's).  One status check for the whole call (its
+        clipping warning once)."""
+        dev, n = x.device, x.numel()
+        host = D.host_empty((stripes[-1][1], 64), torch.int32)
+        packed = host.numpy().view(np.uint32)
+        side, main = D.side_stream(dev), torch.cuda.current_stream(dev)
+        done = []
+        with D.deferred_checks(merge=True):
+            for c0, c1 in stripes:
+                ct = self.encrypt_tensor(num_nodes, current_round, x[c0 * cr:min(n, c1 * cr)], key, biprime,
+                                         clipping_range, weight, target_range, ct_offset=c0)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    host[c0:c1].copy_(ct, non_blocking=True)
+                    ct.record_stream(side)
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                done.append(ev)
+            out = []
+            for (c0, c1), ev in zip(stripes, done):
+                ev.synchronize()
+                out += D.limbs_to_ints(packed[c0:c1])
+        return packed, out
 
     def aggregate(self, current_round: int, num_nodes: int, params: List[List[int]], key: int, biprime: int,
                   total_sample_size: int, clipping_range: Union[int, None] = None, num_expected_params: int = 1,

@@ -181,6 +181,14 @@ class Lane:
             assert v <= M64, f"v_mad_u64_u32 overflow: {ops}"
             self.put(ops[0], v)
             self.put(ops[1], 0)  # the carry-out (vcc or a rotated SGPR pair): 0, as asserted above
+        elif op == "v_mad_i64_i32":  # signed: the engines use it as  column - q  (q * -1 + column)
+            def s32(x):
+                return x - (1 << 32) if x >> 31 else x
+            a, b = s32(self.get(ops[2]) & M32), s32(self.get(ops[3]) & M32)
+            v = a * b + self.get(ops[4])
+            assert 0 <= v <= M64, f"v_mad_i64_i32 out of [0, 2^64): {ops}"
+            self.put(ops[0], v)
+            self.put(ops[1], 0)
         elif op == "v_lshrrev_b64":
             self.put(ops[0], self.get(ops[2]) >> self.get(ops[1]))
         elif op == "v_lshl_add_u64":

@@ -135,3 +135,34 @@ def test_crypter_fa_wide_range_round_trip():
     out = sc.aggregate(current_round=1, num_nodes=2, params=enc, key=-20, biprime=BIPRIME, total_sample_size=2,
                        clipping_range=C, num_expected_params=2, target_range=T)
     assert [v * 2 for v in out] == pytest.approx([28632.0, 57749421.0], abs=1.0)
+
+
+@pytest.mark.gpu
+def test_list_encrypt_overlapped_stripes_equal_unsplit(monkeypatch, caplog):
+    """the list API's encrypt runs as ct_offset stripes (full one-lane rounds, the
+    partial round last) with each stripe's Python ints built while the next stripe exponentiates.
+    The returned list is bit-identical to the unsplit call's, errors and the clipping warning (once)
+    are as before.  FBM_ONE_LANE_ROUND shrinks the round so small vectors split."""
+    import logging
+
+    from fedbiomed_amd import _device as D, workload as W
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    P, tau, n = 4, 3, 40_003
+    xs = [float(v) for v in W.party_params(2, n)]
+    key = W.jl_user_key(2)
+    jc = SecaggCrypter()
+    ref = jc.encrypt(P, tau, xs, key, W.BIPRIME0, weight=7)
+    for rnd in ("300", "431", "1290"):
+        monkeypatch.setenv("FBM_ONE_LANE_ROUND", rnd)
+        _, cr = D.jl_slot(None, P)
+        stripes = D.list_encrypt_stripes((n + cr - 1) // cr)
+        assert len(stripes) > 1 and stripes[0] == (0, int(rnd)) and stripes[-1][1] == (n + cr - 1) // cr
+        caplog.clear()
+        with caplog.at_level(logging.WARNING, logger="fedbiomed_amd"):
+            got = jc.encrypt(P, tau, xs, key, W.BIPRIME0, weight=7)
+        assert got == ref
+        assert sum("exceeds clipping range" in r.getMessage() for r in caplog.records) == 1
+    monkeypatch.setenv("FBM_ONE_LANE_ROUND", "300")
+    with pytest.raises(Exception):
+        jc.encrypt(P, tau, xs[:-1] + [1], key, W.BIPRIME0)  # a non-float: FB624 before any device work

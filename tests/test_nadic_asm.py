@@ -47,6 +47,16 @@ def consts(N):
     return words, np_
 
 
+def sq_pairs(N):
+    """The unrolled square's initial s window (round 4, K' folded): 2^29 - 1 + P'_j, P' = (K - E) mod N
+    (the library's QuadCtx::sqp, written to the constants block and copied to LDS by the kernel)."""
+    K = (1 - R) % N
+    return [MASK + v for v in limbs((K - GEN.sq_kfold_extra()) % N)]
+
+
+KADDR = 76 * 1024  # the pairs' LDS address in these runs (outside the column's 72 + 1 rows)
+
+
 def run(N, a, b=None, square=None):
     """a, b: (digit0, digit1) pairs; b None = square (`square`: which square body).
     Returns the result digits and the executed-instruction counts."""
@@ -56,11 +66,14 @@ def run(N, a, b=None, square=None):
     lds = {}
     for k, v in enumerate(limbs(a[0]) + limbs(a[1])):
         lds[k * 1024] = v
+    for j, v in enumerate(sq_pairs(N)):
+        lds[KADDR + 8 * j] = v
+        lds[KADDR + 8 * j + 4] = 0
     glb = {}
     if b is not None:
         for k, v in enumerate(limbs(b[0]) + limbs(b[1])):
             glb[BB + k * 1024] = v
-    lane = Lane({"a": 0, "b": 0, "bb": BB, "NK": NK, "np": np_}, lds=lds, glb=glb, smem=smem)
+    lane = Lane({"a": 0, "b": 0, "bb": BB, "k": KADDR, "NK": NK, "np": np_}, lds=lds, glb=glb, smem=smem)
     counts = lane.run(MM if b is not None else (square or SQ))
     out = [lds[k * 1024] for k in range(2 * L)]
     assert all(v <= MASK for v in out)
@@ -73,24 +86,26 @@ def _rand_n(rng, bits):
     return rng.getrandbits(bits) | (1 << (bits - 1)) | 1
 
 
-MS = GEN.mul_short()
+MS = GEN.mul_short_reg()
 KS = GEN.KS
 
 
 def run_short(N, a, h):
     """The short-base product a * h * 2^-(29 KS) (mod N^2): a = (digit0, digit1) in the LDS column,
-    h < 2^(29 KS) in a global blocked column, the pairs (D_j, 0), D = N - 2^(29 KS), in LDS."""
+    h < 2^(29 KS) in registers (%[h0] .. %[h8]), the pairs (D'_j, 0) in LDS, D'_j = D_j + (2^29 - 1)
+    [j < KS] + [j == 0], D = N - 2^(29 KS) (the kernel builds them from the constants block)."""
     words, np_ = consts(N)
-    NK, HB, DADDR = 0x4000, 0x100000, 74 * 1024
+    NK, DADDR = 0x4000, 74 * 1024
     smem = {NK + 4 * i: w for i, w in enumerate(words)}
     lds = {}
     for k, v in enumerate(limbs(a[0]) + limbs(a[1])):
         lds[k * 1024] = v
     for j, v in enumerate(limbs(N - (1 << (LB * KS)))):
-        lds[DADDR + 8 * j] = v
+        lds[DADDR + 8 * j] = v + (MASK if j < KS else 0) + (1 if j == 0 else 0)
         lds[DADDR + 8 * j + 4] = 0
-    glb = {HB + k * 1024: v for k, v in enumerate(limbs(h, KS + 1))}  # (+ limb KS = 0: the last row's prefetch)
-    lane = Lane({"a": 0, "h": 0, "hb": HB, "d": DADDR, "NK": NK, "np": np_}, lds=lds, glb=glb, smem=smem)
+    args = {"a": 0, "d": DADDR, "NK": NK, "np": np_}
+    args.update({f"h{i}": v for i, v in enumerate(limbs(h, KS))})
+    lane = Lane(args, lds=lds, smem=smem)
     counts = lane.run(MS)
     out = [lds[k * 1024] for k in range(2 * L)]
     assert all(v <= MASK for v in out)
@@ -118,7 +133,7 @@ def test_nadic_asm_short_product(bits):
         t, s, counts = run_short(N, a, h)
         assert (t + s * N) % M == A * h * f % M
         assert t < 3 * N and s < 3 * N + 2
-        assert counts["v_mad_u64_u32"] == GEN.ms_mads() == 1305
+        assert counts["v_mad_u64_u32"] + counts.get("v_mad_i64_i32", 0) == GEN.ms_mads() == 1305
         # the next squaring brings the digits back below 2N
         t2, s2, _ = run(N, (t, s))
         assert (t2 + s2 * N) % M == A * A * h * h * f * f * pow(R, -1, M) % M
@@ -139,7 +154,7 @@ def test_nadic_asm_binary_chain_with_short_products():
     s = e.bit_length() - 1
     x = (h, 0)
     for bit in bin(e)[3:]:
-        x = run(N, x)[:2]
+        x = run(N, x, square=SQ_UNROLLED)[:2]  # the shipped square
         if bit == "1":
             x = run_short(N, x, h)[:2]
     E = LB * L * ((1 << s) + 1) + LB * KS * (e - (1 << s))
@@ -167,16 +182,21 @@ def test_nadic_asm_product_and_square(bits):
         t, s, counts = run(N, a)
         assert (t + s * N) % M == A * A * rinv % M
         assert t < 2 * N and s < 2 * N
-        assert counts["v_mad_u64_u32"] == GEN.sq_mads() == 4658
+        assert counts["v_mad_u64_u32"] == 4658
         # the triangular square is the plain square bit for bit (same column totals at
         # every quotient -- the mid-product reduction moves value up a column, never out of
         # one before its quotient -- so the same quotients and the same result)
         t2, s2, c2 = run(N, a, square=SQ_PLAIN)
         assert (t2, s2) == (t, s) and c2["v_mad_u64_u32"] == 36 * 145 + 68
-        # the unrolled square (the shipped one) is the looped one bit for bit, with no jumps or m0
+        # the unrolled square (the shipped one: K' folded, the mid-product reduction on 34 slots):
+        # the same t digit (the same quotients), an s digit equal mod N (its constant is P' + E, not
+        # K), no jumps or m0
         t3, s3, c3 = run(N, a, square=SQ_UNROLLED)
-        assert (t3, s3) == (t, s) and c3["v_mad_u64_u32"] == 4658
-        assert "s_setpc_b64" not in c3 and "s_movrels_b32" not in c3
+        # (its constant adds up to (R + E) / R < 10 to s: below 2N needs N > 2^262 -- the short path's
+        # domain, the only one that runs this square; smaller N take the looped square)
+        assert t3 == t and (s3 - s) % N == 0 and (s3 < 2 * N or N < (1 << 262))
+        assert c3["v_mad_u64_u32"] + c3["v_mad_i64_i32"] == GEN.sq_mads() == 4624
+        assert "s_setpc_b64" not in c3 and "s_movrels_b32" not in c3 and "v_sub_u32" not in c3
 
 
 def test_nadic_asm_wide_operands():
@@ -285,3 +305,54 @@ def test_library_short_path_constants():
         assert r == s and [int(v) for v in kw] == list(k64)
         C = pow(2, LB * L * ((1 << s) + 1) + LB * KS * (e - (1 << s)), N * N)
         assert [int(v) for v in corr] == limbs(C % N) + limbs(C // N)
+
+
+def _bound_lane(top, pairs_at=None, pair_iv=None):
+    """A lane of interval values: the LDS column's limbs 0..34 of each digit in [0, 2^29), limb 35 in
+    [0, top]; N's 29-bit limbs in [0, 2^29) (N_35 < 2^9: N < 2^1024), K'_j = 2^29 - 1 + K_j likewise;
+    np any 29-bit value; optional (lo, 0) pairs at `pairs_at` (%[k] / %[d]) with lo in pair_iv(j)."""
+    from tests.asm_bounds import BoundLane
+
+    NK = 0x4000
+    smem = {NK + 4 * w: (0, 0) for w in range(80)}
+    for j in range(L):
+        w = j if j < 10 else 6 + j
+        nmax = MASK if j < L - 1 else (1 << 9) - 1
+        smem[NK + 4 * w] = (0, nmax)
+        smem[NK + 4 * (42 + j)] = (MASK, MASK + nmax)
+    lds = {k * 1024: (0, MASK if k % L < L - 1 else top) for k in range(2 * L)}
+    lds[2 * L * 1024] = (0, MASK)
+    args = {"a": 0, "NK": NK, "np": (0, MASK)}
+    if pairs_at is not None:
+        args["k"] = args["d"] = (pairs_at, pairs_at)
+        for j in range(L):
+            lds[pairs_at + 8 * j] = pair_iv(j)
+            lds[pairs_at + 8 * j + 4] = (0, 0)
+    return BoundLane(args, lds=lds, smem=smem)
+
+
+def test_column_bounds_proved_for_every_operand():
+    """tests/asm_bounds.py runs the shipped square and short product on intervals: for EVERY input
+    within the products' bounds (digits < 2^1026: limb 35 < 2^11; any N < 2^1024; any np; h < 2^261)
+    no 64-bit multiply-add overflows and no quotient subtraction goes negative -- the proof behind
+    the mid-product reduction's 34 kept slots (of 68) and the folded K' / D' constants -- and a
+    reduction dropped from any one kept slot breaks it (the set is minimal)."""
+    from tests.asm_bounds import Overflow
+
+    top = (1 << 11) - 1
+    nmax = lambda j: MASK if j < L - 1 else (1 << 9) - 1  # noqa: E731
+    kp = lambda j: (MASK, MASK + nmax(j))  # noqa: E731  (2^29 - 1 + a limb of a number < N)
+    dp = lambda j: (MASK + (j == 0), 2 * MASK + 1) if j < KS else (0, nmax(j))  # noqa: E731  (D'_j)
+    _bound_lane(top, KADDR, kp).run(SQ_UNROLLED)
+    lane = _bound_lane(top, KADDR, dp)
+    lane.args.update({f"h{i}": (0, MASK) for i in range(KS)})
+    lane.run(MS)
+    keep = GEN.SQ_MID_KEEP
+    try:
+        for part in (0, 1):
+            for k in sorted(keep[part]):
+                GEN.SQ_MID_KEEP = (keep[0] - {k}, keep[1]) if part == 0 else (keep[0], keep[1] - {k})
+                with pytest.raises(Overflow):
+                    _bound_lane(top, KADDR, kp).run(GEN.square_unrolled())
+    finally:
+        GEN.SQ_MID_KEEP = keep

@@ -202,18 +202,26 @@ def row(first, sq):
     return out
 
 
-def mid_reduce(pairs):
+def mid_reduce(pairs, keep=None, one=None):
     """After row MID - 1: every slot (pair lo register) but the youngest keeps its low dword and
     hands the high one to the slot above (x 8 = 2^32 / 2^29).  `pairs`: per part, the window's
-    slot pair low registers from the oldest column to the youngest."""
+    slot pair low registers from the oldest column to the youngest.  `keep`: per part, the slot
+    indices that need the reduction (None: all) -- the others' columns provably stay below 2^64
+    without it (tests/asm_bounds.py).  `one`: per part, slots whose high dword is set to 1 instead
+    of 0 (the column keeps 2^32 + its low dword: it stays >= 2^32 > any quotient digit a later row
+    subtracts from it; the 2^32 so added per such column is a constant the host cancels in the
+    s window's initial pairs -- sq_kfold_extra)."""
     chains = []
-    for regs in pairs:
+    for part, regs in enumerate(pairs):
         ch = []
         for k in range(len(regs) - 1):
+            if keep is not None and k not in keep[part]:
+                continue
             lo, nxt = regs[k], regs[k + 1]
             hi = f"v{int(lo[1:]) + 1}"
+            hv = 1 if one is not None and k in one[part] else 0
             ch += [f"v_mad_u64_u32 v[{nxt[1:]}:{int(nxt[1:]) + 1}], vcc, {hi}, 8, v[{nxt[1:]}:{int(nxt[1:]) + 1}]",
-                   f"v_mov_b32 {hi}, 0"]
+                   f"v_mov_b32 {hi}, {hv}"]
         chains.append(ch)
     out = []
     for k in range(max(len(c) for c in chains)):
@@ -253,7 +261,7 @@ def rotate_carries(lines, pairs=CARRY_PAIRS):
     in turn ~5.8 (tools/microbench/gen_oprate.py).  Every mad stays 8 bytes (the computed jumps)."""
     out, i = [], 0
     for ln in lines:
-        if ln.startswith("v_mad_u64_u32") and ", vcc," in ln:
+        if ln.startswith(("v_mad_u64_u32", "v_mad_i64_i32")) and ", vcc," in ln:
             ln = ln.replace(", vcc,", f", {pairs[i % len(pairs)]},", 1)
             i += 1
         out.append(ln)
@@ -489,7 +497,7 @@ def short_row(i, x=None):
             out.append(f"v_mul_lo_u32 {Q}, {TTLO}, {NPV}")
         if j == 6:
             out.append(f"v_and_b32 {Q}, {MASK}, {Q}")
-        if j == 8:  # 2^29 - 1 - q_i (+ 1 in row 0: the sum over the rows is 2^(29 KS) - m)
+        if j == 8 and not SHORT_KFOLD:  # 2^29 - 1 - q_i (+ 1 in row 0: the sum over the rows is 2^(29 KS) - m)
             out.append(f"v_sub_u32 {CQ}, {hex(1 << LB) if first else MASK}, {Q}")
     out.append(f"v_mad_u64_u32 {TT}, vcc, {Q}, {Ns(0)}, {TT}")
     for j in range(1, L):
@@ -500,7 +508,8 @@ def short_row(i, x=None):
         addend = (D35 if first else "0") if j == NW else As(j)
         out.append(f"v_mad_u64_u32 {As(j - 1)}, vcc, {x}, {B1(j)}, {addend}")
         if j == 12:
-            out.append(f"v_mad_u64_u32 {TS}, vcc, {CQ}, 1, {TS}")
+            out.append(f"v_mad_i64_i32 {TS}, vcc, {Q}, -1, {TS}" if SHORT_KFOLD else
+                       f"v_mad_u64_u32 {TS}, vcc, {CQ}, 1, {TS}")
         if j == 20:
             out.append(f"v_mul_lo_u32 {Q2}, {TSLO}, {NPV}")
         if j == 26:
@@ -511,6 +520,30 @@ def short_row(i, x=None):
     out += [f"v_lshrrev_b64 {TT}, {LB}, {TT}", f"v_lshl_add_u64 {At(0)}, {TT}, 0, {At(0)}",
             f"v_lshrrev_b64 {TS}, {LB}, {TS}", f"v_lshl_add_u64 {As(0)}, {TS}, 0, {As(0)}"]
     return out
+
+
+# Round 4: the short product with h's KS limbs in registers (asm inputs %[h0] .. %[h8], held by the
+# kernel for the whole chain: no global reads of h per product) and its rows unrolled; the rows'
+# 2^29 - 1 - q_i folded like the square's K': the s window starts at the pairs (D'_j, 0),
+# D'_j = D_j + (2^29 - 1) [j < KS] + [j == 0] -- a non-normalised N (D + 2^261) -- and each row
+# subtracts q_i with one v_mad_i64_i32 (column i >= 2^29 - 1 >= q_i).
+SHORT_KFOLD = True
+
+
+def mul_short_reg():
+    body = list(load_consts())
+    body.append(f"v_add_u32 {AADR}, 0x10000, %[a]")
+    for j in range(2 * L):
+        if j < 64:
+            body.append(f"ds_read_b32 {breg(j)}, %[a] offset:{j * 1024}")
+        else:
+            body.append(f"ds_read_b32 {breg(j)}, {AADR} offset:{(j - 64) * 1024}")
+    body += [f"ds_read_b64 {As(j)}, %[d] offset:{8 * j}" for j in range(NW)]
+    body += [f"ds_read_b64 {D35}, %[d] offset:{8 * NW}", f"v_mov_b32 {NPV}, %[np]", "s_waitcnt lgkmcnt(0)"]
+    for i in range(KS):
+        body += short_row(i, f"%[h{i}]")
+    body += normalise_store()
+    return rotate_carries(body)
 
 
 def mul_short():
@@ -568,6 +601,29 @@ def ms_mads():
 # bit-identical results (tests/test_nadic_asm.py runs both).
 # ------------------------------------------------------------------------------------------
 UNROLLED_SQUARE = True
+# Round 4: (1) K' folded -- the s window starts at the pairs (K'_j, 0) (LDS, %[k]) and each row
+# subtracts its quotient digit with one v_mad_i64_i32 (q * -1 + column; the column holds K'_i >= 2^29 - 1
+# >= q, so it stays non-negative) instead of v_sub (K'_i - q) + v_mad_u64_u32 (+ 1 x (K'_i - q)): one VALU
+# instruction less per row; (2) the mid-product reduction only on the slots whose columns could
+# otherwise pass 2^64 (tests/asm_bounds.py proves the rest stay below it for every operand within the
+# product's input bounds: 6 t slots and 28 s slots of 34 + 34).
+SQ_KFOLD = True
+SQ_MID_KEEP = (set(range(14, 20)), set(range(3, 31)))  # (t slots, s slots); None: every slot
+SQ_MID_T = SQ_MID_S = MID  # the reduction follows row SQ_MID_{T,S} - 1 (t part, s part)
+
+
+def sq_one_slots():
+    """The s slots the mid-product reduction leaves at 2^32 + low dword (mid_reduce's `one`): those
+    reduced whose column (SQ_MID_S + slot) still has a quotient digit to lose (column <= L - 1)."""
+    keep = range(NW - 1) if SQ_MID_KEEP is None else SQ_MID_KEEP[1]
+    return {k for k in keep if SQ_MID_S + k <= L - 1}
+
+
+def sq_kfold_extra():
+    """E: what the reduction's high dwords of 1 add to the square's s numerator, sum over those slots
+    of 2^(32 + 29 column).  The host's initial pairs are (2^29 - 1 + P'_j, 0) with P' = (K - E) mod N, so
+    that the constant added in all is R - 1 + P' + E == 0 (mod N) (K = (1 - R) mod N)."""
+    return sum(1 << (32 + LB * (SQ_MID_S + k)) for k in sq_one_slots()) if SQ_KFOLD else 0
 
 
 def sq_row_static(i):
@@ -577,17 +633,22 @@ def sq_row_static(i):
     if even:  # the diagonal x0_(i/2)^2 of column i completes it
         out.append(f"v_mad_u64_u32 {SAt(0)}, vcc, {SB0(i // 2)}, {SB0(i // 2)}, {'0' if first else SAt(0)}")
     out.append(f"v_mul_lo_u32 {SQ}, {SAtLo(0)}, {SNPV}")
-    # ---- s part: (2 x0_i) * x1, + (K'_i - q), q' ----
-    out.append(f"v_mad_u64_u32 {STS}, vcc, {SX0D}, {SB1(0)}, {'0' if first else SAs(0)}")
+    # ---- s part: (2 x0_i) * x1, - q (K'_i pre-added to column i: SQ_KFOLD) or + (K'_i - q), q' ----
+    s0 = (STS if SQ_KFOLD else "0") if first else SAs(0)
+    out.append(f"v_mad_u64_u32 {STS}, vcc, {SX0D}, {SB1(0)}, {s0}")
     for j in range(1, L):
-        addend = "0" if (first or j == NW) else SAs(j)
+        if first:
+            addend = SAs(j - 1) if SQ_KFOLD else "0"
+        else:
+            addend = "0" if j == NW else SAs(j)
         out.append(f"v_mad_u64_u32 {SAs(j - 1)}, vcc, {SX0D}, {SB1(j)}, {addend}")
         if j == 2:
             out.append(f"v_and_b32 {SQ}, {MASK}, {SQ}")
-        if j == 4:
+        if j == 4 and not SQ_KFOLD:
             out.append(f"v_sub_u32 {SCQ}, {kreg}, {SQ}")
         if j == 12:
-            out.append(f"v_mad_u64_u32 {STS}, vcc, {SCQ}, 1, {STS}")
+            out.append(f"v_mad_i64_i32 {STS}, vcc, {SQ}, -1, {STS}" if SQ_KFOLD else
+                       f"v_mad_u64_u32 {STS}, vcc, {SCQ}, 1, {STS}")
         if j == 20:
             out.append(f"v_mul_lo_u32 {SQ2}, {STSLO}, {SNPV}")
         if j == 26:
@@ -620,12 +681,22 @@ def square_unrolled():
             body.append(f"ds_read_b32 {reg}, %[a] offset:{j * 1024}")
         else:
             body.append(f"ds_read_b32 {reg}, {STMP} offset:{(j - 64) * 1024}")
+    if SQ_KFOLD:  # the s window starts at the pairs (K'_j, 0): column j's K'_j, added once
+        body += [f"ds_read_b64 {STS}, %[k]"] + [f"ds_read_b64 {SAs(j - 1)}, %[k] offset:{8 * j}" for j in range(1, L)]
     body += [f"v_mov_b32 {SNPV}, %[np]", f"ds_read_b32 {SX0}, %[a]", "s_waitcnt lgkmcnt(0)",
              f"v_lshlrev_b32 {SX0D}, 1, {SX0}"]
     for i in range(L):
         body += sq_row_static(i)
-        if i == MID - 1:
-            body += mid_reduce([[SAtLo(k) for k in range(L - 1)], [SAsLo(k) for k in range(NW)]])
+        # the mid-product reduction: the t part after row SQ_MID_T - 1, the s part after row SQ_MID_S - 1
+        # (interleaved when both fall after the same row), each on its SQ_MID_KEEP slots
+        t_regs, s_regs = [SAtLo(k) for k in range(L - 1)], [SAsLo(k) for k in range(NW)]
+        keep = SQ_MID_KEEP or (None, None)
+        parts = ([t_regs], [keep[0]]) if i == SQ_MID_T - 1 else ([], [])
+        if i == SQ_MID_S - 1:
+            parts = (parts[0] + [s_regs], parts[1] + [keep[1]])
+        if parts[0]:
+            one = [set() if r is t_regs else sq_one_slots() for r in parts[0]] if SQ_KFOLD else None
+            body += mid_reduce(parts[0], keep=None if SQ_MID_KEEP is None else parts[1], one=one)
     # diagonals of columns L .. 2L-2 (h >= L/2): column 2h sits at window position 2h - L
     body += [f"v_mad_u64_u32 {SAt(2 * h - L)}, vcc, {SB0(h)}, {SB0(h)}, {SAt(2 * h - L)}" for h in range(L // 2, L)]
     body.append(f"v_add_u32 {STMP}, 0x10000, %[a]")
@@ -648,8 +719,10 @@ def square_unrolled():
 
 
 def sq_mads():
-    """v_mad_u64_u32 per square: triangular t part (cross products + diagonals), the s part's
-    (2 x0) x1 and K' - q, the two q N passes, the mid-product reduction."""
+    """64-bit multiply-adds per square: triangular t part (cross products + diagonals), the s part's
+    (2 x0) x1 and - q (K' - q), the two q N passes, the mid-product reduction (its kept slots)."""
+    if UNROLLED_SQUARE:
+        return count_mads(square_unrolled())
     cross = L * (L - 1) // 2
     return cross + L + L * L + (L * L + L + L * L) + (L - 2) + (NW - 1)
 
@@ -670,11 +743,11 @@ def c_string(lines):
 
 
 def count_mads(lines):
-    return sum(1 for ln in lines if ln.startswith("v_mad_u64_u32"))
+    return sum(1 for ln in lines if ln.startswith(("v_mad_u64_u32", "v_mad_i64_i32")))
 
 
 def main():
-    mm, sq, ms = product(False), (square_unrolled() if UNROLLED_SQUARE else square_tri()), mul_short()
+    mm, sq, ms = product(False), (square_unrolled() if UNROLLED_SQUARE else square_tri()), mul_short_reg()
     sq_looped = square_tri()
     mm_row, sq_body = row(False, False), sq_row("odd")
     hdr = f"""// GENERATED by tools/gen_nadic_asm.py -- do not edit by hand.
@@ -695,6 +768,10 @@ def main():
 #define FBM_NA_MADS_SQR {sq_mads()}
 #define FBM_NA_MADS_SHORT {ms_mads()}
 #define FBM_NA_SHORT_LIMBS {KS}
+// the square's s window starts at the pairs (2^29 - 1 + P'_j, 0), P' = (K - E) mod N, K = (1 - R) mod N,
+// E = sum of 2^(32 + 29 c) over the columns c set in this mask (the mid-product reduction leaves them at
+// 2^32 + low dword: sq_kfold_extra in the generator).  The short product's: (D'_j, 0) (mul_short_reg).
+#define FBM_NA_SQ_ONE_MASK {hex(sum(1 << (SQ_MID_S + k) for k in sq_one_slots()) if SQ_KFOLD else 0)}ull
 
 #define FBM_NA_CLOBBERS \\
   {clobbers()}
@@ -710,29 +787,32 @@ __device__ __forceinline__ void fbm_na_mm_glb(uint32_t a_off, const uint32_t* bb
       : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
 }}
 
-// a <- a * h * 2^-{LB * KS} (mod N^2) for a short h = (h, 0), h < 2^{LB * KS}: h's limbs at hb + h_off + k*1024
-// (bytes; global, blocked), d: LDS byte address of the pairs (D_j, 0), D = N - 2^{LB * KS} (36 x 8 bytes).
-__device__ __forceinline__ void fbm_na_ms_glb(uint32_t a_off, const uint32_t* hb, uint32_t h_off, uint32_t d_off,
+// a <- a * h * 2^-{LB * KS} (mod N^2) for a short h = (h, 0), h < 2^{LB * KS}: h's {KS} limbs in registers,
+// d: LDS byte address of the pairs (D'_j, 0), D'_j = D_j + (2^29 - 1) [j < {KS}] + [j == 0], D = N - 2^{LB * KS}
+// (36 x 8 bytes).
+__device__ __forceinline__ void fbm_na_ms_reg(uint32_t a_off, const uint32_t (&h)[{KS}], uint32_t d_off,
                                               const uint32_t* NK, uint32_t np) {{
   asm volatile(
 {c_string(ms)}
       :
-      : [a] "v"(a_off), [h] "v"(h_off), [hb] "s"(hb), [d] "v"(d_off), [NK] "s"(NK), [np] "s"(np)
+      : [a] "v"(a_off), {", ".join(f'[h{i}] "v"(h[{i}])' for i in range(KS))}, [d] "v"(d_off), [NK] "s"(NK),
+        [np] "s"(np)
       : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
 }}
 
 #if !defined(FBM_NA_PLAIN_SQUARE) && !defined(FBM_NA_LOOPED_SQUARE)
-// a <- a^2 R^-1 (mod N^2): triangular x0^2, full x0 * 2 x1, every row unrolled ({len(sq)} instructions).
-__device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK, uint32_t np) {{
+// a <- a^2 R^-1 (mod N^2): triangular x0^2, full x0 * 2 x1, every row unrolled ({len(sq)} instructions);
+// k: LDS byte address of the s window's initial pairs (2^29 - 1 + P'_j, 0) (FBM_NA_SQ_ONE_MASK).
+__device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, uint32_t k_off, const uint32_t* NK, uint32_t np) {{
   asm volatile(
 {c_string(sq)}
       :
-      : [a] "v"(a_off), [NK] "s"(NK), [np] "s"(np)
+      : [a] "v"(a_off), [k] "v"(k_off), [NK] "s"(NK), [np] "s"(np)
       : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
 }}
 #elif defined(FBM_NA_LOOPED_SQUARE)
 // A/B variant (-DFBM_NA_LOOPED_SQUARE): the row loop with computed-jump row suffixes ({len(sq_looped)} instructions).
-__device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK, uint32_t np) {{
+__device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, uint32_t, const uint32_t* NK, uint32_t np) {{
   asm volatile(
 {c_string(sq_looped)}
       :
@@ -742,7 +822,7 @@ __device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK
 #else
 // A/B variant (-DFBM_NA_PLAIN_SQUARE): the general product with B = A from LDS -- no computed
 // jumps, {L * count_mads(row(False, True)) + 2 * (NW - 1)} multiplies instead of {sq_mads()}.
-__device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, const uint32_t* NK, uint32_t np) {{
+__device__ __forceinline__ void fbm_na_sq_lds(uint32_t a_off, uint32_t, const uint32_t* NK, uint32_t np) {{
   asm volatile(
 {c_string(product(True))}
       :
