@@ -709,6 +709,75 @@ def gen_custom_hash(R):
     dump("custom_hash.json", {"cases": cases})
 
 
+# The reference's caller-level flows (their tests need declearn / tinydb / ..., absent here),
+# restated with their crypter-level inputs and run through the reference crypter itself:
+#  * LomSecureAggregation.aggregate with create_protected_vector's vectors
+#    (tests/test_secure_aggregation.py:383-426, 487-519, 520-558): quantize -> multiply(weight 5) ->
+#    LOM(nonce).protect per node (secrets b"\x02" * 32) -> SecaggLomCrypter.aggregate(total 5, clip);
+#    the reference draws the nonce with token_bytes(16): fixed nonces here;
+#  * the JL aux-var flow of tests/test_optimizer_secagg.py:513-631: SecaggCrypter().encrypt of a
+#    Linear(4, 2) model's 10 weights and of its 10 Scaffold corrections (clip 3, weight 5 or None),
+#    the same ciphertexts from num_nodes in (2, 3, 5, 8, 10) nodes, rounds 1..4, aggregate with key
+#    -(skey num_nodes), total 5 num_nodes or num_nodes, num_expected_params 10, that test's biprime.
+#    The test trains a randomly initialised model with a random 2 040-bit key (torch's default
+#    init, secrets.randbits): seeded vectors of the same shape and scale and a seeded key here.
+OPTIM_SECAGG_BIPRIME = int.from_bytes(
+    b"\xe2+!\x9a\xdc\xc3.\xcaY\x1b\xd6\xfdH\xfc1\xaeG6\xc0O\xa5\x9a"
+    b"\x8bi)i \xac=\x88\xb5\xfdo\xac\xadS\x80\xb3xL\xa6\xc7\xca]\x17"
+    b'\xb1\x16\rB\x8f"\xb1*\x12.J`\xc8AW\x92\xd0\t\x14*fwx"o\xff\xca'
+    b"\xec\x8e\x86G\x7f\x9c\xdf?\x00}&\xa8b\xcd\n!\xa9\x1f\xc0\x99{"
+    b'\x91h"\xe6,j\x87\xf6\xa6\xee0\xc5_\xdbi\x93\xea\x80qJ\x12\xbc'
+    b"\xd7,AE\xb5\xdc\xf1\xf5\x962\xcdms",
+    byteorder="big")
+
+
+def gen_caller_flows(R):
+    LOM = R.lom.LOM
+    q, mul = R.utils.quantize, R.utils.multiply
+    out = {"lom": [], "jl_auxvar": []}
+    parties = ["node-1", "node-2", "node-3"]
+    secrets_ = {u: {v: b"\x02" * 32 for v in parties if v != u} for u in parties}
+    rng = random.Random(4242)
+    lom_cases = [([[1, 2, 3, 4, 5]] * 3, 1000, 5, 1, bytes(range(16))),           # test_lom_secagg_03
+                 ([[1, 2, 3, 4, 5]] * 3, 2000, 5, 1, b"\x5a" * 16),               # 03b: an explicit clip
+                 ([[1, 2, 3, 4, 5], [10, 20, 30, 40, 50], [-7, 0, 7, 700, 999]], 1000, 5, 3, b"\xf0\xff\xff\xff" + bytes(12)),
+                 ([[rng.uniform(-900, 900) for _ in range(64)] for _ in range(3)], 1000, 5, 2, bytes(range(100, 116)))]
+    for params, clip, weight, rnd, nonce in lom_cases:
+        qs = [mul(q(p, clip), weight) for p in params]
+        pv = [LOM(nonce=nonce).protect(u, secrets_[u], rnd, x, parties) for u, x in zip(parties, qs)]
+        agg = R.crypter.SecaggLomCrypter().aggregate(params=pv, total_sample_size=5, clipping_range=clip,
+                                                    target_range=None)
+        out["lom"].append({"params": [[(fhex(v) if isinstance(v, float) else v) for v in p] for p in params],
+                           "clip": clip, "weight": weight, "round": rnd, "nonce": nonce.hex(), "parties": parties,
+                           "quantized": [[ihex(v) for v in x] for x in qs],
+                           "protected": [[ihex(v) for v in y] for y in pv],
+                           "total_sample_size": 5, "agg": [fhex(v) for v in agg]})
+    Crypter = R.crypter.SecaggCrypter
+    rng = np.random.default_rng(513)
+    kr = random.Random(631)
+    for num_nodes in (2, 3, 5, 8, 10):
+        for rnd in range(1, 5):
+            for weighted in (True, False):
+                skey = kr.getrandbits(2040)
+                flat_w = [float(v) for v in rng.uniform(-0.5, 0.5, 10)]   # nn.Linear(4, 2)'s weights and bias
+                flat_a = [float(v) for v in rng.normal(0, 0.05, 10)]      # its Scaffold correction states
+                w = 5 if weighted else None                              # targets1.shape[0]
+                total = 5 * num_nodes if weighted else num_nodes
+                case = {"num_nodes": num_nodes, "round": rnd, "weight": w, "total_sample_size": total,
+                        "key": ihex(skey), "clip": 3, "num_expected_params": 10}
+                for name, flat in (("aux", flat_a), ("weights", flat_w)):
+                    enc = Crypter().encrypt(params=flat, key=skey, num_nodes=num_nodes, current_round=rnd,
+                                            biprime=OPTIM_SECAGG_BIPRIME, clipping_range=3, weight=w)
+                    dec = Crypter().aggregate(params=[enc] * num_nodes, key=-(skey * num_nodes),
+                                              total_sample_size=total, num_nodes=num_nodes, current_round=rnd,
+                                              biprime=OPTIM_SECAGG_BIPRIME, clipping_range=3, num_expected_params=10)
+                    case[name] = {"x": [fhex(v) for v in flat], "enc": [ihex(v) for v in enc],
+                                  "dec": [fhex(v) for v in dec]}
+                out["jl_auxvar"].append(case)
+    out["jl_auxvar_biprime"] = ihex(OPTIM_SECAGG_BIPRIME)
+    dump("caller_flows.json", out)
+
+
 def I(s):  # noqa: E743 - hex string -> int (the fixtures' encoding)
     return int(s, 16)
 
@@ -730,6 +799,9 @@ def main():
     if sys.argv[1:] == ["custom_hash"]:
         gen_custom_hash(R)
         return
+    if sys.argv[1:] == ["caller_flows"]:
+        gen_caller_flows(R)
+        return
     gen_quantize(R)
     gen_lom(R)
     gen_jl(R)
@@ -741,6 +813,7 @@ def main():
     gen_even(R)
     gen_api_edges(R)
     gen_custom_hash(R)
+    gen_caller_flows(R)
     meta = {"generator": "tools/gen_golden.py", "reference": load_reference.REF,
             "note": "outputs of the reference Fed-BioMed crypter (Python), imported via tools/refshim"}
     dump("meta.json", meta)
