@@ -699,20 +699,19 @@ class PendingEncrypt:
         return self._ct
 
 
-JL_ROUND_BITS = 512  # t_k = (k << 512) | tau: a round below 2^512 keeps to FDH's last message block
+JL_ROUND_BITS = 8192  # FDH.H's int(t).to_bytes(1024, 'big') of t = (k << 512) | tau
 
 
 def _check_round(tau: int) -> np.ndarray:
-    """The JL round's domain -> its 16 limbs for the C-ABI.  FDH.H serialises t = (k << 512) | tau
-    (_jls.py:742-760), so a negative round is the reference's OverflowError; a round of 2^512 or more
-    ORs into k's bits there (valid up to 2^8192) and is outside the device path (FB624, DESIGN.md
-    section 8)."""
+    """The JL round -> its N.TAU_LIMBS limbs for the C-ABI (ABI 3: any round the reference hashes).
+    FDH.H serialises t = (k << 512) | tau with int(t).to_bytes(1024, 'big') (_jls.py:451-467, 744-748):
+    a negative round, or one of 2^8192 or more, is the reference's OverflowError there."""
     tau = operator.index(tau)
     if tau < 0:
         raise OverflowError("can't convert negative int to unsigned")
     if tau >> JL_ROUND_BITS:
-        raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: round must be in [0, 2^512)")
-    return int_limbs(tau, 16)
+        raise OverflowError("int too big to convert")
+    return int_limbs(tau, N.TAU_LIMBS)
 
 
 def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, clip=None, target=None,

@@ -19,7 +19,8 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "lib
 # A/B measurement of kernel variants (tools/ab.sh): load another build of the same library
 LIB_PATH = os.environ.get("FBM_LIB_PATH", LIB_PATH)
 
-ABI_VERSION = 2  # include/fbm_secagg.h FBM_ABI_VERSION
+ABI_VERSION = 3  # include/fbm_secagg.h FBM_ABI_VERSION
+TAU_LIMBS = 256  # FBM_TAU_LIMBS: the JL round's 32-bit words (< 2^8192)
 FBM_OK = 0
 FBM_E_ARG = -1
 FBM_E_HIP = -2
@@ -72,7 +73,7 @@ SIGNATURES = {
     "fbm_lom_aggregate": (c_int, [c_vp, c_int, c_u64, c_u64, c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_encrypt_workspace": (c_u64, [c_u64]),
     "fbm_jl_aggregate_workspace": (c_u64, [c_u64]),
-    # the JL round (tau) is a HOST pointer to 16 limbs (< 2^512, ABI 2)
+    # the JL round (tau) is a HOST pointer to TAU_LIMBS limbs (< 2^8192, ABI 3)
     "fbm_jl_encrypt": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_int, c_int, c_vp, c_vp,
                                c_int, c_vp, c_u64, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_encrypt_phase": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_int, c_int, c_vp,

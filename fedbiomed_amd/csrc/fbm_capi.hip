@@ -299,18 +299,41 @@ static void build_nadic(const MontCtxN& mn, const QuadCtx& qa, NadicCtx& na) {
   for (int j = 0; j < FBM_QA_L; ++j) na.nk29[42 + j] = qa.kp[j];
 }
 
-// SHA-256 midstate over the 14 leading all-zero blocks of t.to_bytes(1024,'big') (FDH.H)
-static void fdh_midstate(uint32_t mid[8]) {
+// SHA-256 midstate over the 14 leading blocks of t.to_bytes(1024,'big') (FDH.H), t = (k << 512) | tau:
+// bytes 0..895 = t's bits 1024..8191 = tau's words 32..255 (k < 2^64 never reaches them).  Block b's
+// SHA word j is t's little-endian word 255 - 16 b - j.  All-zero for a round below 2^1024.
+static void fdh_midstate(uint32_t mid[8], const uint32_t* tau = nullptr) {
+  static uint32_t zero_mid[8];
+  static std::once_flag once;
+  std::call_once(once, [] {
+    uint32_t st[8], W[16];
+    fbm_sha256_init(st);
+    memset(W, 0, sizeof(W));
+    for (int b = 0; b < 14; ++b) fbm_sha256_compress(st, W);
+    memcpy(zero_mid, st, sizeof(st));
+  });
+  bool hi = false;
+  for (int i = 32; tau && i < FBM_TAU_LIMBS; ++i) hi |= tau[i] != 0u;
+  if (!hi) {
+    memcpy(mid, zero_mid, sizeof(zero_mid));
+    return;
+  }
   uint32_t st[8], W[16];
   fbm_sha256_init(st);
-  memset(W, 0, sizeof(W));
-  for (int b = 0; b < 14; ++b) fbm_sha256_compress(st, W);
+  for (int b = 0; b < 14; ++b) {
+    for (int j = 0; j < 16; ++j) W[j] = tau[255 - 16 * b - j];
+    fbm_sha256_compress(st, W);
+  }
   memcpy(mid, st, sizeof(st));
 }
 
-// tau (16 LE words, < 2^512) -> FDH block 15 in SHA-256 word order
+// the round tau (FBM_TAU_LIMBS little-endian words, < 2^8192) -> FDH's message blocks: block 15 = tau's
+// words 0..15, block 14 = words 16..31 (the kernel ORs k into its last two words), blocks 0..13 into the
+// midstate -- t.to_bytes(1024, 'big') of t = (k << 512) | tau (_jls.py:451-467, 744-748) for any round
 static void set_tau(JlParams& jp, const uint32_t* tau) {
   for (int i = 0; i < 16; ++i) jp.tau_w[i] = tau ? tau[15 - i] : 0u;
+  for (int i = 0; i < 16; ++i) jp.tau14_w[i] = tau ? tau[31 - i] : 0u;
+  fdh_midstate(jp.mid, tau);
 }
 
 static void big_trim(Big& a) {
@@ -360,7 +383,6 @@ static int fdh_params(const uint32_t* n_odd, int even, const uint32_t* tau, uint
   jp.fdh_even = even ? 1 : 0;
   set_tau(jp, tau);
   jp.ct_offset = ct_offset;
-  fdh_midstate(jp.mid);
   return FBM_OK;
 }
 
@@ -548,7 +570,6 @@ static int build_jl_params_uncached(const uint32_t* biprime, int es, int cr, con
   jp.cr = cr;
   set_tau(jp, tau);
   jp.ct_offset = ct_offset;
-  fdh_midstate(jp.mid);
   return FBM_OK;
 }
 
@@ -1192,7 +1213,7 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
     return FBM_E_ARG;
   }
   if (!tau) {  // the round is FDH's input: never defaulted (a NULL would silently mean round 0)
-    set_error("null tau (the round's 16 limbs)");
+    set_error("null tau (the round's %d limbs)", FBM_TAU_LIMBS);
     return FBM_E_ARG;
   }
   if (n == 0) return FBM_OK;
@@ -1361,7 +1382,7 @@ static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t
   JlParams jp;
   int rc;
   if (!tau) {
-    set_error("null tau (the round's 16 limbs)");
+    set_error("null tau (the round's %d limbs)", FBM_TAU_LIMBS);
     return FBM_E_ARG;
   }
   bool generic, short_on;
@@ -1809,7 +1830,7 @@ int fbm_test_nadic_consts(const uint32_t* n32, uint32_t* nk, uint32_t* r2na, uin
     return FBM_E_ARG;
   }
   JlParams jp;
-  const uint32_t tau1[16] = {1u};
+  uint32_t tau1[FBM_TAU_LIMBS] = {1u};
   int rc = build_jl_params(n32, 34, 30, tau1, 0, jp);
   if (rc) return rc;
   memcpy(nk, jp.na.nk29, sizeof(jp.na.nk29));

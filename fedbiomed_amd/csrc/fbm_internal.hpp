@@ -152,10 +152,11 @@ struct JlParams {
   uint32_t Ninv32[32];           // N^-1 mod 2^1024 (exact divisions by N: jl_prod, jl_lift, jl_split)
   int n_bits;                    // bit length of N
   int es, cr;                    // VES slot size / slots per ciphertext
-  uint32_t tau_w[16];            // the round tau < 2^512 as FDH's message block 15 (t's low 512 bits,
+  uint32_t tau_w[16];            // the round's bits 0..511 as FDH's message block 15 (t's low 512 bits,
                                  // big-endian words: tau_w[15] = tau mod 2^32)
+  uint32_t tau14_w[16];          // its bits 512..1023: block 14, into which the kernel ORs k (t = (k << 512) | tau)
   uint64_t ct_offset;            // global index of ciphertext 0 (element-range shard)
-  uint32_t mid[8];               // SHA-256 state after the 14 all-zero message blocks
+  uint32_t mid[8];               // SHA-256 state after message blocks 0..13 (the round's bits 1024..8191)
   FbmN30 n30;                    // N in signed-30 limbs + N^-1 mod 2^30 (modular inverse)
   int key_is_zero;
   int fdh_even;                  // FDH.H standalone: the modulus is even (r must be odd as well)

@@ -363,8 +363,9 @@ __host__ __device__ inline bool gcd_is_one_r8(const uint32_t (&r)[8], const uint
   return v[0] == 1u && rest == 0u;
 }
 
-// FDH.H(t_k): message = t.to_bytes(1024,'big') || counter (1 byte).  Blocks 0..13 are
-// all zero for k < 2^64 (midstate from the host), block 14 carries k, block 15 tau (< 2^512),
+// FDH.H(t_k): message = t.to_bytes(1024,'big') || counter (1 byte), t = (k << 512) | tau.  Blocks
+// 0..13 hold the round's bits 1024..8191 (the same for every k < 2^64: a midstate from the host), block
+// 14 its bits 512..1023 OR k, block 15 its bits 0..511,
 // block 16 the counter byte + padding (length 8200 bits).  While gcd(r, N^2) != 1 the
 // counter is bumped and r grows by one digest (r = D1 || D2 || ...).  r is tested with 1..7
 // digests only: once 8 digests (256 bytes = bits_size // 8) are in, the reference's inner
@@ -380,12 +381,12 @@ __global__ void __launch_bounds__(256) jl_fdh_kernel(uint64_t n_ct, JlParams jp,
 #pragma unroll
   for (int i = 0; i < 8; ++i) st[i] = jp.mid[i];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) W[i] = 0u;
-  W[14] = (uint32_t)(k >> 32);
-  W[15] = (uint32_t)k;
+  for (int i = 0; i < 16; ++i) W[i] = jp.tau14_w[i];  // block 14: the round's bits 512..1023, OR k
+  W[14] |= (uint32_t)(k >> 32);
+  W[15] |= (uint32_t)k;
   fbm_sha256_compress(st, W);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) W[i] = jp.tau_w[i];  // block 15: the round (any tau < 2^512)
+  for (int i = 0; i < 16; ++i) W[i] = jp.tau_w[i];  // block 15: the round's bits 0..511
   fbm_sha256_compress(st, W);
   uint32_t r[64];
 #pragma unroll

@@ -23,7 +23,7 @@ modulus) -- and the exponentiations on the device (fbm_jl_powmod / fbm_jl_decryp
 
 Domain of the device path (FB624 outside it): 2 <= N < 2^1024 (an even N
 runs on the generic engine, fedbiomed_amd/csrc/fbm_gen.hip, an odd one on the Montgomery engines);
-FDH of bits_size 2048; tau in [0, 2^512) where FDH hashes it; VES values in [0, 2^128) with
+FDH of bits_size 2048; tau in [0, 2^8192) where FDH hashes it (ABI 3); VES values in [0, 2^128) with
 es <= 100; ServerKey.decrypt with delta^2 = 1 (mod N).  Integers are Python ints (gmpy2 is
 not a dependency): where the reference returns gmpy2.mpz this returns int, and FDH takes an
 int modulus.
@@ -153,13 +153,14 @@ def _bases(key: "BaseKey", tau, len_: int, n: int) -> torch.Tensor:
 
 
 def _check_tau(tau) -> int:
-    """A round the device takes: 0 <= tau < 2^512.  A negative one is the reference's OverflowError
-    (FDH.H's int(t).to_bytes, _jls.py:747); 2^512 and above OR into t's k bits there (FB624 here)."""
+    """A round: any 0 <= tau < 2^8192 (the device hashes t = (k << 512) | tau whole, ABI 3).  A negative
+    one, or one of 2^8192 or more, is the reference's OverflowError (FDH.H's int(t).to_bytes(1024),
+    _jls.py:747)."""
     t = operator.index(tau)
     if t < 0:
         raise OverflowError("can't convert negative int to unsigned")
-    if t >> 512:
-        raise _unsupported(f"round tau={t} (device path: 0 <= tau < 2^512)")
+    if t >> D.JL_ROUND_BITS:
+        raise OverflowError("int too big to convert")
     return t
 
 
@@ -442,11 +443,6 @@ class FDH:
 
     def H(self, t: int) -> int:
         """SHA256(t || 1) || SHA256(t || 2) || ... until gcd(r, n_modulus) == 1, t as 1024
-        big-endian bytes -- fbm_jl_fdh with t = (k << 512) | tau (k < 2^64, tau < 2^512)."""
-        t = operator.index(t)
-        if t < 0:  # int(t).to_bytes(...) (_jls.py:747)
-            raise OverflowError("can't convert negative int to unsigned")
-        k, tau = t >> 512, t & ((1 << 512) - 1)
-        if k >= 2**64:
-            raise _unsupported("FDH input t outside {(k << 512) | tau : k < 2^64, tau < 2^512}")
-        return self._hash_range(tau, 1, k)[0]
+        big-endian bytes -- fbm_jl_fdh with tau = t and k = 0 (any 0 <= t < 2^8192)."""
+        t = _check_tau(t)  # int(t).to_bytes(1024, ...)'s OverflowError outside [0, 2^8192) (_jls.py:747)
+        return self._hash_range(t, 1, 0)[0]

@@ -27,7 +27,12 @@
 extern "C" {
 #endif
 
-#define FBM_ABI_VERSION 2 /* 2: the JL round is a 512-bit value (16 limbs), FBM_ABI 1 took a uint64 */
+#define FBM_ABI_VERSION 3 /* 3: the JL round is an 8192-bit value (FBM_TAU_LIMBS limbs); 2 took 16 limbs, 1 a uint64 */
+/* The JL round `tau` of every JL entry point: a HOST pointer to FBM_TAU_LIMBS little-endian 32-bit
+ * words, any round below 2^8192 -- FDH.H hashes t = (k << 512) | tau as t.to_bytes(1024, 'big')
+ * (fedbiomed/common/secagg/_jls.py:451-467, 744-748), whose OverflowError past 2^8192 the Python layer
+ * raises.  Never NULL (FBM_E_ARG). */
+#define FBM_TAU_LIMBS 256
 
 #define FBM_OK 0
 #define FBM_E_ARG (-1)         /* bad argument (type/shape/range)            -> FB624      */
@@ -107,7 +112,7 @@ int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t tot
  *          even one on the generic engine, fedbiomed_amd/csrc/fbm_gen.hip -- same results)
  * key:     HOST, 64 limbs |sk| (< 2^2048);  key_negative: sign of sk
  * es, cr:  VES slot bits / slots per ciphertext (JoyeLibert vector encoder, _jls.py:104-116)
- * tau:     HOST, 16 limbs: the round, < 2^512 (t_k = (k << 512) | tau, FDH.H's input, _jls.py:451-467);
+ * tau:     HOST, FBM_TAU_LIMBS limbs: the round, < 2^8192 (t_k = (k << 512) | tau, FDH.H's input, _jls.py:451-467);
  *          n_ct = ceil(n / cr)
  * ct_offset: global index of ciphertext 0 (t_k = ((k + ct_offset) << 512) | tau) when the
  *          element range is sharded across devices on ciphertext boundaries; 0 otherwise.   */

@@ -68,15 +68,15 @@ def test_negative_round_object_api(golden):
 
 
 def test_round_domain():
-    """Rounds up to 2^512 - 1 reach the C-ABI (16 limbs); 2^512 and above are FB624 (they OR into
-    the ciphertext index bits of t in the reference); a negative one is the reference's OverflowError."""
+    """ABI 3: every round the reference hashes, 0 <= tau < 2^8192, reaches the C-ABI (256 limbs); 2^8192
+    and above, and a negative round, are the reference's OverflowError (int(t).to_bytes(1024))."""
     from fedbiomed_amd import _device as D
-    from fedbiomed_amd.exceptions import FedbiomedSecaggCrypterError
 
-    assert D._check_round(2**512 - 1).tolist() == [0xFFFFFFFF] * 16
-    assert D._check_round(2**64 + 5).tolist() == [5, 0, 1] + [0] * 13
-    with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
-        D._check_round(2**512)
+    assert D._check_round(2**512 - 1).tolist() == [0xFFFFFFFF] * 16 + [0] * 240
+    assert D._check_round(2**64 + 5).tolist() == [5, 0, 1] + [0] * 253
+    assert D._check_round(2**512).tolist() == [0] * 16 + [1] + [0] * 239
+    with pytest.raises(OverflowError):
+        D._check_round(2**8192)
     with pytest.raises(OverflowError):
         D._check_round(-1)
 

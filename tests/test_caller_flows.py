@@ -112,3 +112,54 @@ def test_drop_in_jl_auxvar_flow():
                                             num_nodes=n, current_round=rnd, biprime=N, clipping_range=3,
                                             num_expected_params=10)
             assert _bits(dec) == _bits([F(v) for v in d["dec"]]), (n, rnd, name)
+
+
+def test_oracle_big_rounds():
+    """Rounds of 2^512 and more (ABI 3): the reference ORs them into t = (k << 512) | tau and hashes t
+    whole; the oracle's FDH / encrypt reproduce its values (they pin the GPU test below)."""
+    from fedbiomed_amd import workload as W
+
+    n2 = W.BIPRIME0 ** 2
+    for c in FIX["big_fdh"]:
+        assert O.fdh(I(c["t"]), n2) == I(c["h"])
+    for r in FIX["big_rounds"][::3]:
+        tau, keys = I(r["tau"]), [I(k) for k in r["keys"]]
+        enc = O.jl_encrypt([F(v) for v in r["x"][0]], tau, keys[0], W.BIPRIME0, 2, weight=3)
+        assert enc == [I(v) for v in r["enc"][0]]
+    assert FIX["round_overflow"] == {"error": "OverflowError", "msg": "int too big to convert"}
+
+
+def test_round_limbs_abi3():
+    from fedbiomed_amd import _device as D, _native
+
+    assert _native.TAU_LIMBS == 256
+    assert D._check_round(2**8192 - 1).tolist() == [0xFFFFFFFF] * 256
+    assert D._check_round(2**512 + 7).tolist() == [7] + [0] * 15 + [1] + [0] * 239
+    with pytest.raises(OverflowError, match="int too big to convert"):
+        D._check_round(2**8192)
+    with pytest.raises(OverflowError):
+        D._check_round(-1)
+
+
+@pytest.mark.gpu
+def test_drop_in_big_rounds():
+    """SecaggCrypter.encrypt / aggregate at rounds 2^512 ... 2^8192 - 1 (k's bits ORed with the round's,
+    the round's bits 1024.. in FDH's leading blocks: a per-call midstate) and FDH.H of any t < 2^8192:
+    the reference's values bit for bit; 2^8192 is its OverflowError."""
+    from fedbiomed_amd import workload as W
+    from fedbiomed_amd.secagg import FDH, SecaggCrypter
+
+    jc = SecaggCrypter()
+    for r in FIX["big_rounds"]:
+        tau, keys = I(r["tau"]), [I(k) for k in r["keys"]]
+        enc = [jc.encrypt(num_nodes=2, current_round=tau, params=[F(v) for v in x], key=k, biprime=W.BIPRIME0,
+                          weight=3) for x, k in zip(r["x"], keys)]
+        assert enc == [[I(v) for v in e] for e in r["enc"]], r["tau"][:12]
+        out = jc.aggregate(current_round=tau, num_nodes=2, params=enc, key=-sum(keys), biprime=W.BIPRIME0,
+                           total_sample_size=6, num_expected_params=70)
+        assert _bits(out) == _bits([F(v) for v in r["agg"]])
+    n2 = W.BIPRIME0 ** 2
+    for c in FIX["big_fdh"]:
+        assert FDH(2048, n2).H(I(c["t"])) == I(c["h"])
+    with pytest.raises(OverflowError, match="int too big to convert"):
+        jc.encrypt(num_nodes=2, current_round=2**8192, params=[0.5], key=5, biprime=W.BIPRIME0)

@@ -126,10 +126,9 @@ def test_domain_restrictions_raise_fb624():
         UserKey(PublicParam(123457, 1024, FDH(1024, 123457 ** 2).H), 3).encrypt([1], 1)
     with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
         UserKey(pp_of(1), 3).encrypt([1], 1)  # N = 1 (every N >= 2 is in the domain, even ones included)
-    with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
-        UserKey(pp, 3).encrypt([1], 2**512)  # tau beyond one FDH message block (the device takes < 2^512)
-    with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
-        FDH(2048, 123457).H(1 << 600)  # t not of the (k << 512) | tau form
+    # (rounds of 2^512 and more, FDH.H of any t < 2^8192: on the device since ABI 3 -- tests/test_caller_flows.py)
+    with pytest.raises(OverflowError):
+        UserKey(pp, 3).encrypt([1], 2**8192)  # int(t).to_bytes(1024) of the reference
     with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
         ServerKey(pp, -20).decrypt([EncryptedNumber(pp, 5)], 1, delta=2)  # delta^2 != 1 (mod N)
     with pytest.raises(ZeroDivisionError):

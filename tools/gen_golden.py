@@ -775,6 +775,29 @@ def gen_caller_flows(R):
                                   "dec": [fhex(v) for v in dec]}
                 out["jl_auxvar"].append(case)
     out["jl_auxvar_biprime"] = ihex(OPTIM_SECAGG_BIPRIME)
+    # rounds of 2^512 and more (the reference ORs them into t = (k << 512) | tau, and hashes t whole with
+    # int(t).to_bytes(1024, 'big'): any round below 2^8192, its OverflowError from 2^8192 on)
+    jls = R.jls
+    from gmpy2 import mpz
+    bp = W.BIPRIME0
+    big = []
+    rr = random.Random(8192)
+    for tau in [2 ** 512, 2 ** 512 + (3 << 576) + 5, (2 ** 1023) + 1, (2 ** 1024) + 99,
+                (2 ** 5000) + (2 ** 700) + 1, rr.getrandbits(8191) | 1, 2 ** 8192 - 1]:
+        keys = [rr.getrandbits(2040), rr.getrandbits(2040)]
+        xs = [[float(v) for v in np.random.default_rng(tau % 1000 + p).uniform(-2, 2, 70)] for p in range(2)]
+        enc = [Crypter().encrypt(num_nodes=2, current_round=tau, params=x, key=k, biprime=bp, weight=3)
+               for x, k in zip(xs, keys)]
+        agg = Crypter().aggregate(current_round=tau, num_nodes=2, params=enc, key=-sum(keys), biprime=bp,
+                                  total_sample_size=6, num_expected_params=70)
+        big.append({"tau": ihex(tau), "keys": [ihex(k) for k in keys], "x": [[fhex(v) for v in x] for x in xs],
+                    "enc": [[ihex(c) for c in e] for e in enc], "agg": [fhex(v) for v in agg]})
+    out["big_rounds"] = big
+    n2 = mpz(bp) * mpz(bp)
+    out["big_fdh"] = [{"t": ihex(t), "h": ihex(int(jls.FDH(2048, n2).H(t)))}
+                      for t in (1 << 600, (1 << 8191) + 12345, (7 << 1024) | 3)]
+    out["round_overflow"] = _outcome(lambda: Crypter().encrypt(num_nodes=2, current_round=2 ** 8192,
+                                                               params=[0.5], key=5, biprime=bp))
     dump("caller_flows.json", out)
 
 
