@@ -135,7 +135,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
                 raise
             fn.restype = res
             fn.argtypes = args
-        if lib.fbm_abi_version() != ABI_VERSION:
+        # (an A/B variant may be one ABI older: ABI 2 reads the first 16 of the round's limbs, the same
+        #  call for every round below 2^512)
+        if lib.fbm_abi_version() != ABI_VERSION and not (variant and lib.fbm_abi_version() == ABI_VERSION - 1):
             raise NativeUnavailable("ABI version mismatch")
         _lib = lib
         return lib

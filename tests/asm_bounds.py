@@ -21,6 +21,9 @@ _ONE = re.compile(r"^([vs])(\d+)$")
 def _parse(ln):
     op, _, rest = ln.partition(" ")
     ops = [t.strip() for t in rest.split(",")] if rest else []
+    if "_dpp" in op:  # DPP controls (quad_perm / wave shifts, masks, bound_ctrl) follow the last operand
+        ops = [t.split()[0] if " " in t and not t.startswith("0x") else t for t in ops]
+        ops = [t for t in ops if not t.startswith(("quad_perm", "row_mask", "bank_mask", "bound_ctrl", "wave_"))]
     off = 0
     if ops and "offset:" in ops[-1]:
         last, _, o = ops[-1].partition("offset:")
@@ -134,6 +137,8 @@ class BoundLane:
             return
         if op in ("v_add_u32", "s_add_u32"):
             a, b = g(ops[1]), g(ops[2])
+            if op == "v_add_u32" and a[1] + b[1] > M32:
+                raise Overflow(f"v_add_u32 may wrap: {ops} {a} {b}")
             self.put(ops[0], (a[0] + b[0], a[1] + b[1]))
             return
         if op == "v_sub_u32":
@@ -191,6 +196,38 @@ class BoundLane:
             if hi > M64:
                 raise Overflow(f"v_lshl_add_u64 may overflow: {ops}")
             self.put(ops[0], (lo, hi))
+            return
+        # ---- the lane-group engines (tools/gen_quad_asm.py), bounded on ONE abstract lane whose
+        # intervals are the hull over the group's lanes: a cross-lane read (DPP, ds_bpermute) reads the
+        # same register's hull; a DPP read past the wave's ends (bound_ctrl) reads 0, inside the hull ----
+        if op in ("v_and_b32_dpp", "v_mov_b32_dpp"):
+            src = g(ops[1])
+            if op == "v_mov_b32_dpp":
+                self.put(ops[0], (0, src[1]))
+            else:
+                mk = g(ops[2])
+                self._conc(mk, "DPP mask")
+                self.put(ops[0], (0, min(src[1], mk[0])))
+            return
+        if op == "ds_bpermute_b32":
+            src = g(ops[2])
+            self.put(ops[0], (0, src[1]))
+            return
+        if op in ("v_add_co_u32", "v_addc_co_u32"):
+            a, b = g(ops[2]), g(ops[3])
+            c = g(ops[4]) if op == "v_addc_co_u32" else (0, 0)
+            lo, hi = a[0] + b[0] + c[0], a[1] + b[1] + c[1]
+            self.put(ops[0], (lo, hi) if hi <= M32 else (0, M32))
+            self.put(ops[1], (lo >> 32, hi >> 32))
+            return
+        if op == "v_alignbit_b32":
+            hi_, lo_, k = g(ops[1]), g(ops[2]), self._conc(g(ops[3]), "shift")
+            a, b = ((hi_[0] << 32) + lo_[0]) >> k, ((hi_[1] << 32) + lo_[1]) >> k
+            self.put(ops[0], (a, b) if b <= M32 else (0, M32))
+            return
+        if op == "s_movrels_b32":
+            m = _ONE.match(ops[1])
+            self.put(ops[0], self.r[f"s{int(m.group(2)) + self._conc(self.r['m0'], 'm0')}"])
             return
         if op == "s_cmp_lg_u32":
             self.scc = int(self._conc(g(ops[0]), "s_cmp") != self._conc(g(ops[1]), "s_cmp"))

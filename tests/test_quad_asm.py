@@ -401,3 +401,27 @@ def test_looped_square_equals_cyclic_band_square(geo):
     got, _, _ = run_quad(N, As, geo=geo)
     got2, _, _ = run_quad(N, As, geo=geo, looped=True)
     assert got == got2
+
+
+def test_group_column_bounds_proved_without_mid_reduce():
+    """Round 4 dropped the group engines' mid-product reduction: a column lives in a lane's window for
+    at most M rows (a retire hands only its low 29 bits to the lane below), so it restarts below
+    2^29 + 2^10 whenever it changes lanes.  tests/asm_bounds.py runs every group program (the cyclic-band
+    square, the looped square, the general product, the short-base product) on intervals -- one abstract
+    lane holding the hull over the group's lanes, every operand limb in [0, 2^29 + 2^10) (the lazy limbs),
+    any N limbs, np, K' -- and no 64-bit multiply-add can overflow."""
+    from tests.asm_bounds import BoundLane
+
+    for g in (Q.QUAD, Q.TRI):
+        for prog in (Q.square_cyc(g), Q.product(False, g), Q.product(True, g, cyc=False), Q.mul_short(g)):
+            assert not any(ln.startswith("v_mad_u64_u32") and ", 8," in ln for ln in prog)  # no mid-reduce left
+            QK, BB, DL = 0x4000, 0x100000, 0x40000
+            lim = (0, MASK + (1 << 10))
+            lds = {k * g.ROWB: lim for k in range(2 * L + 20)}
+            lds.update({DL + 4 * j: ((0, MASK) if j % 2 == 0 else (0, 0)) for j in range(2 * g.M + 2)})
+            args = {"ac": 0, "al": 0, "QK": QK, "np": (0, MASK), "e0": (0, 1), "bp": 0, "b": 0, "bb": BB, "dl": DL}
+            args.update({f"n{r}": (0, MASK) for r in range(g.M)})
+            lane = BoundLane(args, lds=lds, smem={QK + 4 * i: (MASK, 2 * MASK) for i in range(40)},
+                             glb={BB + j * 1024: lim for j in range(2 * g.M)})
+            lane.run(prog)
+            assert lane.max_mad < 0.6 * 2**64

@@ -343,11 +343,22 @@ def row(g, first, sq, kreg, xs, xn, pre_off, first_s=None):
     return out + p1 + p2 + p3
 
 
+# Round 4: no mid-product reduction in the group engines.  A column lives in a lane's window for at
+# most M rows: the row that retires a lane's slot 0 hands only its low 29 bits to the lane below (the
+# carry stays, in slot 1), so every column restarts from < 2^29 whenever it changes lanes -- at most M
+# rows of products (12 in the triple: 12 x 3 x 2^58 < 2^64) -- tests/asm_bounds.py proves every 64-bit
+# multiply-add below 2^64 for every operand within the products' bounds without it (the round-3
+# engines carried the one-lane engine's pass after row 17: ~50 VALU instructions per product).
+GROUP_MID_REDUCE = False
+
+
 def mid_reduce(g):
-    """After row 17: every slot keeps its low dword and hands the high one to the slot above
+    """(Unused unless GROUP_MID_REDUCE.)  After row 17: every slot keeps its low dword and hands the high one to the slot above
     (x 8 = 2^32 / 2^29); the top slot's (R) high dword goes to the lane above's slot 0
     (the top lane's is 0: the window's value is below 2^1026).  Values drop below 2^36."""
     M = g.M
+    if not GROUP_MID_REDUCE:
+        return []
     chains = []
     for acc, hi, rr, rhi, t in ((g.At, g.AtHi, g.RT, g.RTHI, g.T3), (g.As, g.AsHi, g.RS, g.RSHI, g.T4)):
         ch = []
@@ -617,23 +628,39 @@ def cyc_row(g, P, i):
     return out + p1 + p2 + p3
 
 
+CYC_MID_KEEP = {}  # geometry name -> (t slots, s slots) reduced ("R": the top slot's hand-up); absent: all
+
+
 def cyc_mid_reduce(g, P, i):
-    """mid_reduce with the window of row i (slots 0..M-2 in their pairs, the top slot in RT / RS)."""
+    """mid_reduce with the window of row i (slots 0..M-2 in their pairs, the top slot in RT / RS).
+    CYC_MID_KEEP[g]: per part the slots that need it (k: slot k's high dword into slot k + 1; "R": the
+    top slot's into the lane above's slot 0) -- the rest provably stay below 2^64 without
+    (tests/asm_bounds.py)."""
     M, W = g.M, P.W
+    if not GROUP_MID_REDUCE:
+        return []
+    keep = CYC_MID_KEEP.get("triple" if g.G == 3 else "quad")
     chains = []
-    for pt, rr, t in ((P.PT, P.RT, P.T3), (P.PS, P.RS, P.T4)):
+    for part, (pt, rr, t) in enumerate(((P.PT, P.RT, P.T3), (P.PS, P.RS, P.T4))):
         acc = lambda k, pt=pt: pt[(i + k) % W]  # noqa: E731
+        kp = None if keep is None else keep[part]
         ch = []
         for k in range(M - 2):
-            ch += [f"v_mad_u64_u32 {_pr(acc(k + 1))}, vcc, v{acc(k) + 1}, 8, {_pr(acc(k + 1))}", f"v_mov_b32 v{acc(k) + 1}, 0"]
-        ch += [f"v_mad_u64_u32 {_pr(rr)}, vcc, v{acc(M - 2) + 1}, 8, {_pr(rr)}", f"v_mov_b32 v{acc(M - 2) + 1}, 0",
-               g.up(f"v{t}", f"v{rr + 1}"),
-               f"v_mov_b32 v{rr + 1}, 0",
-               f"v_mad_u64_u32 {_pr(acc(0))}, vcc, v{t}, 8, {_pr(acc(0))}"]
+            if kp is None or k in kp:
+                ch += [f"v_mad_u64_u32 {_pr(acc(k + 1))}, vcc, v{acc(k) + 1}, 8, {_pr(acc(k + 1))}",
+                       f"v_mov_b32 v{acc(k) + 1}, 0"]
+        if kp is None or M - 2 in kp:
+            ch += [f"v_mad_u64_u32 {_pr(rr)}, vcc, v{acc(M - 2) + 1}, 8, {_pr(rr)}", f"v_mov_b32 v{acc(M - 2) + 1}, 0"]
+        if kp is None or "R" in kp:
+            ch += [g.up(f"v{t}", f"v{rr + 1}"),
+                   f"v_mov_b32 v{rr + 1}, 0",
+                   f"v_mad_u64_u32 {_pr(acc(0))}, vcc, v{t}, 8, {_pr(acc(0))}"]
         chains.append(ch)
     out = []
-    for a, b in zip(*chains):
-        out += [a, b]
+    for k in range(max(len(c) for c in chains)):
+        for ch in chains:
+            if k < len(ch):
+                out.append(ch[k])
     return out
 
 
