@@ -147,7 +147,8 @@ def test_drop_in_big_rounds():
     the round's bits 1024.. in FDH's leading blocks: a per-call midstate) and FDH.H of any t < 2^8192:
     the reference's values bit for bit; 2^8192 is its OverflowError."""
     from fedbiomed_amd import workload as W
-    from fedbiomed_amd.secagg import FDH, SecaggCrypter
+    from fedbiomed_amd.secagg import SecaggCrypter
+    from fedbiomed_amd.secagg._jls import FDH
 
     jc = SecaggCrypter()
     for r in FIX["big_rounds"]:

@@ -12,7 +12,8 @@ lib() { case $1 in new) echo $GRAFT_REPO_ROOT/fedbiomed_amd/_lib/libfbm_secagg.s
 for rep in 1 2; do
   for v in base new; do
     FBM_LIB_PATH=$(lib $v) timeout -k 10 200 python -u tools/exp_probe.py --ct 65536,131072,262144 --engines single --reps 2 > $O/probe_$v.$rep.jsonl 2>&1 || { echo "PROBE FAILED $v"; tail -3 $O/probe_$v.$rep.jsonl; exit 1; }
-    echo "== $v $rep"; grep ct $O/probe_$v.$rep.jsonl
+    FBM_LIB_PATH=$(lib $v) timeout -k 10 200 python -u tools/exp_probe.py --ct 41667,83334 --engines triple --reps 3 > $O/probe_tri_$v.$rep.jsonl 2>&1 || { echo "PROBE FAILED tri $v"; tail -3 $O/probe_tri_$v.$rep.jsonl; exit 1; }
+    echo "== $v $rep"; grep ct $O/probe_$v.$rep.jsonl $O/probe_tri_$v.$rep.jsonl
   done
 done
 for rep in 1 2; do
