@@ -118,7 +118,14 @@ static void* fconv_range(void* arg) {
     return NULL;
 }
 
-static int conv_threads(Py_ssize_t n);
+static int conv_threads(Py_ssize_t n) {
+    const char* e = getenv("FBM_CONV_THREADS");
+    long t = e ? strtol(e, NULL, 10) : 8;
+    if (t < 1) t = 1;
+    if (t > 64) t = 64;
+    if (t > n / 1024) t = n / 1024 > 0 ? (long)(n / 1024) : 1;
+    return (int)t;
+}
 
 /* Large lists are read by several threads WHILE THIS THREAD HOLDS THE GIL: no Python code runs
  * meanwhile, so the list and its items cannot change or be freed under the readers (they touch
@@ -183,14 +190,6 @@ static void* conv_range(void* arg) {
     return NULL;
 }
 
-static int conv_threads(Py_ssize_t n) {
-    const char* e = getenv("FBM_CONV_THREADS");
-    long t = e ? strtol(e, NULL, 10) : 8;
-    if (t < 1) t = 1;
-    if (t > 64) t = 64;
-    if (t > n / 1024) t = n / 1024 > 0 ? (long)(n / 1024) : 1;
-    return (int)t;
-}
 
 /* -1, or the first bad index over all ranges (each range stops at its own first bad item). */
 static Py_ssize_t ints_to_words_parallel(PyObject* seq, Py_ssize_t n, Py_ssize_t nb, unsigned char* dst,
