@@ -3,7 +3,7 @@
 `--ct` ciphertexts under each engine (rocprofv3 --kernel-trace / --pmc attribute the
 dispatches to jl_exp_kernel / jl_expq_kernel).  Prints per-engine wall times.
 
-    python tools/exp_probe.py [--ct 41667[,16384,...]] [--engines single,quad] [--reps 2]
+    python tools/exp_probe.py [--ct 41667[,16384,...]] [--engines single,quad] [--reps 2] [--even]
 """
 
 import argparse
@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--ct", default="41667", help="comma-separated ciphertext counts")
     ap.add_argument("--engines", default="single,quad")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--even", action="store_true",
+                    help="use the even modulus BIPRIME0 + 1 (same width), which only the generic engine takes")
     args = ap.parse_args()
     import torch
 
@@ -28,16 +30,17 @@ def main():
 
     dev = D.device()
     sk0 = W.jl_server_key(8)
+    n = W.BIPRIME0 + 1 if args.even else W.BIPRIME0
     for ct in [int(c) for c in args.ct.split(",")]:
-        out = {"ct": ct}
+        out = {"ct": ct, "modulus": "even" if args.even else "odd"}
         for eng in args.engines.split(","):
             with D.jl_engine(eng):
-                D.jl_decrypt_factor(ct, W.BIPRIME0, sk0, 1, dev=dev)
+                D.jl_decrypt_factor(ct, n, sk0, 1, dev=dev)
                 torch.cuda.synchronize()
                 ts = []
                 for _ in range(args.reps):
                     t0 = time.perf_counter()
-                    D.jl_decrypt_factor(ct, W.BIPRIME0, sk0, 1, dev=dev)
+                    D.jl_decrypt_factor(ct, n, sk0, 1, dev=dev)
                     torch.cuda.synchronize()
                     ts.append(round(1000 * (time.perf_counter() - t0), 3))
             out[eng + "_ms"] = ts
