@@ -493,11 +493,12 @@ def dequantize(u: torch.Tensor, clip=None, target=None) -> torch.Tensor:
 # Joye-Libert
 # ------------------------------------------------------------------------------------------
 def _biprime_limbs(biprime: int) -> np.ndarray:
-    """N as 32 limbs.  Any 2 <= N < 2^1024: an odd N runs on the Montgomery engines, an even one on
-    the generic engine (csrc/fbm_gen.hip), as the reference computes with any N (_jls.py:37-73)."""
-    if biprime < 2 or biprime.bit_length() > 1024:
+    """N as 32 limbs.  Any 1 <= N < 2^1024: an odd N >= 3 runs on the Montgomery engines, an even one
+    and N = 1 on the generic engine (csrc/fbm_gen.hip), as the reference computes with any N
+    (_jls.py:37-73)."""
+    if biprime < 1 or biprime.bit_length() > 1024:
         raise FedbiomedSecaggCrypterError(
-            f"{ErrorNumbers.FB624.value}: biprime must be an integer in [2, 2^1024) (the device path's domain)")
+            f"{ErrorNumbers.FB624.value}: biprime must be an integer in [1, 2^1024) (the device path's domain)")
     return int_limbs(biprime, 32)
 
 

@@ -395,9 +395,18 @@ static int fdh_params_for_biprime(const uint32_t* biprime, const uint32_t* tau, 
   return fdh_params(m.data(), s > 0, tau, ct_offset, jp);
 }
 
-// the generic engine (fbm_gen.hip) takes every even N, and every N under FBM_ENGINE_GENERIC
+// N = 1: the reference computes everything modulo N^2 = 1 (every ciphertext 0) and its decryption's
+// invert(delta^2, N^2) raises; only the generic engine's Barrett products take a modulus of 1
+static bool jl_is_one(const uint32_t* biprime) {
+  if (biprime[0] != 1u) return false;
+  for (int i = 1; i < 32; ++i)
+    if (biprime[i]) return false;
+  return true;
+}
+
+// the generic engine (fbm_gen.hip) takes every even N and N = 1, and every N under FBM_ENGINE_GENERIC
 static bool jl_generic(const uint32_t* biprime) {
-  return (biprime[0] & 1u) == 0u || jl_engine_policy() == FBM_ENGINE_GENERIC;
+  return (biprime[0] & 1u) == 0u || jl_is_one(biprime) || jl_engine_policy() == FBM_ENGINE_GENERIC;
 }
 
 static std::atomic<int> g_short_on{1};  // fbm_jl_set_short: 0 forces the window-table path (A/B, tests)
@@ -419,7 +428,7 @@ static void jl_path_for(const void* ws, int phase, int full, const uint32_t* bip
     std::lock_guard<std::mutex> lk(g_path_mu);
     for (size_t i = g_path_recs.size(); i-- > 0;)
       if (g_path_recs[i].ws == ws) {
-        generic = g_path_recs[i].generic || (biprime[0] & 1u) == 0u;
+        generic = g_path_recs[i].generic || (biprime[0] & 1u) == 0u || jl_is_one(biprime);
         short_on = g_path_recs[i].short_on;
         return;
       }
@@ -443,8 +452,8 @@ static int build_gen_ctx(const uint32_t* biprime, const uint32_t* key, int key_n
   memset(&g, 0, sizeof(g));
   Big N(biprime, biprime + 32);
   big_trim(N);
-  if (big_bits(N) < 2) {
-    set_error("biprime must be >= 2 (N = 1 is outside the device path's domain)");
+  if (big_bits(N) < 1) {
+    set_error("biprime must be >= 1");
     return FBM_E_UNSUPPORTED;
   }
   Big M = big_mul(N, N);
@@ -1446,6 +1455,10 @@ static int jl_combine_impl(const uint32_t* cts, int n_parties, uint64_t n_ct, in
                            uint32_t* x_raw = nullptr) {
   JlParams jp;
   int rc;
+  if (jl_is_one(biprime)) {  // the reference's invert(delta^2, N^2) has no nonzero result modulo 1
+    set_error("invert() no inverse exists");
+    return FBM_E_INVERSE;
+  }
   if (jl_generic(biprime)) {  // any N: product, factor, ((v - 1) // N) mod N, then the decode
     if (es < 1 || cr < 1 || es > 100 || (int64_t)es * cr > 1024) {
       set_error("invalid VES parameters es=%d cr=%d", es, cr);

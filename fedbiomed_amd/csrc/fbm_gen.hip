@@ -294,9 +294,9 @@ __host__ __device__ uint32_t gen_exp_lane(const uint32_t* Hrow, const uint32_t* 
   const int kM = g->kM, kN = g->kN;
   const Glb M{g->M}, muM{g->muM};
   uint32_t err = g_reduce_row(Hrow, 64, kM, M, muM, T, Q, HB);  // h = H mod M
-  // AC = h^|key| mod M: left-to-right binary (1 for a zero key, gmpy2's powmod(h, 0, M))
+  // AC = h^|key| mod M: left-to-right binary (1 mod M for a zero key, gmpy2's powmod(h, 0, M))
   g_zero(AC, kM + 1);
-  AC[0] = 1u;
+  AC[0] = (kM == 1 && M[0] == 1u) ? 0u : 1u;  // h^0 mod 1 = 0
   for (int b = g->key_bits - 1; b >= 0; --b) {
     err |= g_modmul(AC, AC, kM, M, muM, T, Q);
     if ((g->key[b >> 5] >> (b & 31)) & 1u) err |= g_modmul(AC, HB, kM, M, muM, T, Q);

@@ -21,8 +21,8 @@ SecaggCrypter._setup_public_param builds) has its hashes computed as the referen
 the callable per t on the host (one fbm_jl_fdh launch for an FDH of bits_size 2048 against another
 modulus) -- and the exponentiations on the device (fbm_jl_powmod / fbm_jl_decrypt_with).
 
-Domain of the device path (FB624 outside it): 2 <= N < 2^1024 (an even N
-runs on the generic engine, fedbiomed_amd/csrc/fbm_gen.hip, an odd one on the Montgomery engines);
+Domain of the device path (FB624 outside it): 1 <= N < 2^1024 (an even N and
+N = 1 run on the generic engine, fedbiomed_amd/csrc/fbm_gen.hip, an odd one on the Montgomery engines);
 FDH of bits_size 2048; tau in [0, 2^8192) where FDH hashes it (ABI 3); VES values in [0, 2^128) with
 es <= 100; ServerKey.decrypt with delta^2 = 1 (mod N).  Integers are Python ints (gmpy2 is
 not a dependency): where the reference returns gmpy2.mpz this returns int, and FDH takes an
@@ -252,8 +252,8 @@ def _materialize(nums: List[EncryptedNumber]) -> List[int]:
 
 def _modulus_of(pp: PublicParam) -> int:
     n = int(pp.n_modulus)
-    if n < 2 or n.bit_length() > 1024:
-        raise _unsupported("a modulus N outside [2, 2^1024)")
+    if n < 1 or n.bit_length() > 1024:
+        raise _unsupported("a modulus N outside [1, 2^1024)")
     return n
 
 
@@ -334,8 +334,8 @@ class ServerKey(BaseKey):
             raise TypeError("Cipher text should be list of EncryptedNumbers")
         n = _modulus_of(self._public_param)
         d2 = delta ** 2
-        if math.gcd(d2 % (n * n), n * n) != 1:  # invert(delta^2, N^2) runs even on an empty list
-            raise ZeroDivisionError("invert() no inverse exists")
+        if n == 1 or math.gcd(d2 % (n * n), n * n) != 1:  # invert(delta^2, N^2) runs even on an empty
+            raise ZeroDivisionError("invert() no inverse exists")  # list; modulo 1 its result is 0: raises
         if not cipher:
             return []
         if d2 % n != 1:

@@ -108,8 +108,10 @@ int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t tot
                       double step, double* out, uint64_t* sums, uint32_t* stats, void* stream);
 
 /* ---- Joye-Libert (reference fedbiomed/common/secagg/_jls.py) -------------------------
- * biprime: HOST, 32 limbs (N, 2 <= N < 2^1024; an odd N runs on the Montgomery engines, an
- *          even one on the generic engine, fedbiomed_amd/csrc/fbm_gen.hip -- same results)
+ * biprime: HOST, 32 limbs (N, 1 <= N < 2^1024; an odd N >= 3 runs on the Montgomery engines, an
+ *          even one and N = 1 on the generic engine, fedbiomed_amd/csrc/fbm_gen.hip -- same results;
+ *          at N = 1 every ciphertext is 0 and every decryption is FBM_E_INVERSE, the reference's
+ *          invert(delta^2, N^2) modulo 1)
  * key:     HOST, 64 limbs |sk| (< 2^2048);  key_negative: sign of sk
  * es, cr:  VES slot bits / slots per ciphertext (JoyeLibert vector encoder, _jls.py:104-116)
  * tau:     HOST, FBM_TAU_LIMBS limbs: the round, < 2^8192 (t_k = (k << 512) | tau, FDH.H's input, _jls.py:451-467);
@@ -330,7 +332,7 @@ int fbm_test_modinv(const uint32_t* x, const uint32_t* n, uint32_t* out, int* ba
  * not, a negative FBM_E_* code on bad arguments; *err receives device error flags. */
 int fbm_test_fdh_gcd(const uint32_t* r8, const uint32_t* n32, uint32_t* err);
 /* host test hooks (no GPU): one ciphertext of the generic engine (fedbiomed_amd/csrc/fbm_gen.hip)
- * run on the host, any N (2 <= N < 2^1024).  fbm_test_gen_exp: out (64 words) = h^key mod N^2 (the
+ * run on the host, any N (1 <= N < 2^1024).  fbm_test_gen_exp: out (64 words) = h^key mod N^2 (the
  * inverse of h^|key| for key_negative), times (N pt + 1) mod N^2 when pt (32 words; `negative`:
  * pt holds |pt| of a negative packing) is not NULL; h: 64 words.  fbm_test_gen_combine: v =
  * prod of n_parties 64-word rows (cts, row-major) times factor (64 words, may be NULL) mod N^2;

@@ -174,11 +174,11 @@ def test_even_fixture_oracle(golden):
             assert got == [I(v) for v in enc["ok"]], (c["n"], p)
 
 
-def test_domain_n_below_two_is_fb624():
+def test_domain_n_below_one_is_fb624():
     from fedbiomed_amd import _device as D
     from fedbiomed_amd.exceptions import FedbiomedSecaggCrypterError
 
-    for n in (0, 1, -4):
+    for n in (0, -4):  # N = 1 is in the domain since round 4 (tests/test_n_one.py)
         with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
             D._biprime_limbs(n)
     assert D.fdh_modulus(2**64) == (1, True)  # FDH(2048, 2^64): only odd digests are coprime

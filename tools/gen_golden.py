@@ -801,6 +801,42 @@ def gen_caller_flows(R):
     dump("caller_flows.json", out)
 
 
+def gen_n_one(R):
+    """N = 1 (n_one.json): the reference computes modulo N^2 = 1 -- every ciphertext and every product is
+    0 -- and its decryption's invert(delta^2, N^2) (_jls.py:36-58, 556) raises ZeroDivisionError, empty
+    lists included.  A negative key's powmod inverts modulo 1 first: gmpy2 is absent here, so those
+    cases follow the shim's (Python's) pow(h, -1, 1) = 0 -- parity unpinned for them."""
+    jls = R.jls
+    Crypter = R.crypter.SecaggCrypter
+    mpz = sys.modules["gmpy2"].mpz
+    out = {"crypter": [], "object": {}}
+    rng = np.random.default_rng(11)
+    for key, n, w in ((12345, 3, 3), (2 ** 2040 - 3, 61, None), (0, 7, 1), (-77, 5, 2)):
+        xs = [float(v) for v in rng.uniform(-2, 2, n)]
+        enc = _outcome(lambda xs=xs, key=key, w=w: [ihex(c) for c in Crypter().encrypt(
+            num_nodes=2, current_round=1, params=xs, key=key, biprime=1, weight=w)])
+        case = {"key": ihex(key), "weight": w, "x": [fhex(v) for v in xs], "enc": enc}
+        if "ok" in enc:
+            cts = [int(c, 16) for c in enc["ok"]]
+            case["agg"] = _outcome(lambda cts=cts, n=n: Crypter().aggregate(
+                current_round=1, num_nodes=2, params=[cts, cts], key=-key, biprime=1, total_sample_size=4,
+                num_expected_params=n))
+        out["crypter"].append(case)
+    pp = jls.PublicParam(mpz(1), 1024, jls.FDH(2048, mpz(1)).H)
+    o = out["object"]
+    o["user_encrypt"] = _outcome(lambda: [ihex(int(c)) for c in jls.UserKey(pp, 3).encrypt([mpz(1), mpz(5), mpz(0)], 1)])
+    o["user_encrypt_neg"] = _outcome(lambda: [ihex(int(c)) for c in jls.UserKey(pp, -3).encrypt([mpz(1), mpz(5)], 2)])
+    o["user_encrypt_zero_key"] = _outcome(lambda: [ihex(int(c)) for c in jls.UserKey(pp, 0).encrypt([mpz(4)], 1)])
+    o["sum"] = _outcome(lambda: ihex(int((jls.EncryptedNumber(pp, mpz(0)) + jls.EncryptedNumber(pp, mpz(0))).ciphertext)))
+    o["decrypt"] = _outcome(lambda: jls.ServerKey(pp, -3).decrypt([jls.EncryptedNumber(pp, mpz(0))], 1))
+    o["decrypt_empty"] = _outcome(lambda: jls.ServerKey(pp, -3).decrypt([], 1))
+    o["fdh"] = _outcome(lambda: ihex(int(jls.FDH(2048, mpz(1)).H(5))))
+    jl = jls.JoyeLibert()
+    o["protect"] = _outcome(lambda: [ihex(int(c)) for c in jl.protect(pp, jls.UserKey(pp, 3), 1, [1, 2, 3], 2)])
+    o["aggregate"] = _outcome(lambda: jl.aggregate(jls.ServerKey(pp, -6), 1, [[jls.EncryptedNumber(pp, mpz(0))]] * 2, 3))
+    dump("n_one.json", out)
+
+
 def I(s):  # noqa: E743 - hex string -> int (the fixtures' encoding)
     return int(s, 16)
 
@@ -825,6 +861,9 @@ def main():
     if sys.argv[1:] == ["caller_flows"]:
         gen_caller_flows(R)
         return
+    if sys.argv[1:] == ["n_one"]:
+        gen_n_one(R)
+        return
     gen_quantize(R)
     gen_lom(R)
     gen_jl(R)
@@ -837,6 +876,7 @@ def main():
     gen_api_edges(R)
     gen_custom_hash(R)
     gen_caller_flows(R)
+    gen_n_one(R)
     meta = {"generator": "tools/gen_golden.py", "reference": load_reference.REF,
             "note": "outputs of the reference Fed-BioMed crypter (Python), imported via tools/refshim"}
     dump("meta.json", meta)
