@@ -1177,20 +1177,20 @@ int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t tot
 }
 
 // encrypt workspace: ops | cst | pt [n_ct][32] | nude (blocked) | H [n_ct][64] | table |
-//                    H^-1 [n_ct][64] + y [n_ct][32] (negative keys)
+//                    H^-1 [n_ct][64] + y [n_ct][32] (negative keys) | Hc [n_ct][8] (compact H rows)
 uint64_t fbm_jl_encrypt_workspace(uint64_t n_ct) {
   const uint64_t slots = table_slots_for(n_ct);
   (void)slots;
   return align256(FBM_OPS_WORDS * 4) + align256(FBM_CST_WORDS * 4) + align256(n_ct * 32 * 4) +
          align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4) + 2 * align256(n_ct * 64 * 4) + align256(n_ct * 32 * 4) +
-         align256(jl_table_bytes(n_ct));
+         align256(jl_table_bytes(n_ct)) + align256(n_ct * 8 * 4);
 }
 
 uint64_t fbm_jl_aggregate_workspace(uint64_t n_ct) {
   const uint64_t slots = table_slots_for(n_ct);
   (void)slots;
   return align256(FBM_OPS_WORDS * 4) + align256(FBM_CST_WORDS * 4) + align256(((n_ct + 255) / 256) * 256 * FBM_NL * 4) +
-         3 * align256(n_ct * 64 * 4) + align256(n_ct * 32 * 4) + align256(jl_table_bytes(n_ct));
+         3 * align256(n_ct * 64 * 4) + align256(n_ct * 32 * 4) + align256(jl_table_bytes(n_ct)) + align256(n_ct * 8 * 4);
 }
 
 // phase bit 1: the prologue (status word, constants, pack, nude, FDH, and the inverse of H
@@ -1299,6 +1299,8 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
   uint32_t* Hinv = (uint32_t*)(ws + off);  // negative keys only: H^|key| digits (after the table)
   off += align256(n_ct * 64 * 4);
   uint32_t* Y = (uint32_t*)(ws + off);
+  off += align256(n_ct * 32 * 4);
+  uint32_t* Hc = (uint32_t*)(ws + off);  // compact H rows: 32 B per ciphertext (one FDH digest)
   const bool inverse = key_negative && !is_zero;
   if (phase & 1) {
     if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s, shq ? &sh : nullptr); })))
@@ -1309,7 +1311,7 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
     const uint32_t* ptp = x_dtype == FBM_PT ? (const uint32_t*)x : pt;  // UserKey.encrypt: packed already
     const int negw = (int64_t)weight < 0 ? 1 : 0;
     if ((rc = timed("jl_nude", s, [&] { return launch_jl_nude(ptp, n_ct, jp, negw, nude, s); }))) return rc;
-    if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, H, stats, s); }))) return rc;
+    if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, H, stats, s, Hc); }))) return rc;
   }
   if (!(phase & 2)) return FBM_OK;
   if (inverse) {
@@ -1318,14 +1320,14 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
     // by nude in the same pass
     if ((rc = timed("jl_exp", s, [&] {
            return launch_jl_exp(H, n_ct, jp, sc, FBM_EXP_DEC | FBM_EXP_OUT_NADIC, nullptr, table, slots, ops, cst, Hinv,
-                                s);
+                                s, Hc);
          })))
       return rc;
     return timed("jl_inv", s, [&] { return launch_jl_inv(n_ct, jp, cst, Hinv, Y, nude, ct_out, stats, s); });
   }
   // a phase-2-only call inside an open batch (fbm_jl_batch_begin) is recorded, not launched
   // (and not timed: the batch's one launch is, at the flush)
-  auto go = [&] { return launch_jl_exp(H, n_ct, jp, sc, 0, nude, table, slots, ops, cst, ct_out, s); };
+  auto go = [&] { return launch_jl_exp(H, n_ct, jp, sc, 0, nude, table, slots, ops, cst, ct_out, s, Hc); };
   const bool rec = phase == 2 && jl_batch_active();
   const bool acc = jl_batch_accept(rec);
   rc = rec ? go() : timed("jl_exp", s, go);
@@ -1356,7 +1358,7 @@ int fbm_jl_encrypt_phase(const void* x, int x_dtype, uint64_t n, double clip, do
 // aggregate workspace: ops | cst | X (blocked) | H [n_ct][64] | E [n_ct][64] | F [n_ct][64] |
 //                      xs [n_ct][32] | table    (fbm_jl_aggregate_workspace)
 struct JlAggWs {
-  uint32_t *ops, *cst, *X, *H, *E, *F, *xs, *table;
+  uint32_t *ops, *cst, *X, *H, *E, *F, *xs, *table, *Hc;
   uint64_t slots;
 };
 static JlAggWs agg_ws(void* workspace, uint64_t n_ct) {
@@ -1379,6 +1381,8 @@ static JlAggWs agg_ws(void* workspace, uint64_t n_ct) {
   w.xs = (uint32_t*)(ws + off);
   off += align256(n_ct * 32 * 4);
   w.table = (uint32_t*)(ws + off);
+  off += align256(jl_table_bytes(n_ct));
+  w.Hc = (uint32_t*)(ws + off);
   return w;
 }
 
@@ -1423,13 +1427,14 @@ static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t
   if (phase & 1) {
     if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, w.ops, w.cst, s, shq ? &sh : nullptr); })))
       return rc;
-    if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, w.H, stats, s); }))) return rc;
+    if (!is_zero && (rc = timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, w.H, stats, s, w.Hc); })))
+      return rc;
   }
   if (phase & 2) {
     // the inverse starts from the power's N-adic digits (no division by N needed)
     auto go = [&] {
       return launch_jl_exp(w.H, n_ct, jp, sc, FBM_EXP_DEC | (inv ? FBM_EXP_OUT_NADIC : 0), nullptr, w.table, w.slots,
-                           w.ops, w.cst, E, s);
+                           w.ops, w.cst, E, s, w.Hc);
     };
     const bool rec = phase == 2 && jl_batch_active();  // recorded (not launched, not timed) in an open batch
     const bool acc = jl_batch_accept(rec);

@@ -75,6 +75,8 @@ int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t 
 // per-call device constants (words): M, R^2 (74 limbs, padded to 128), the broadcast
 // column 1 (limb k at word k*256) and R^(P+1) mod M (the aggregate's uniform first operand,
 // written by jl_rk_kernel: P parties + the factor leave the product at the plain value)
+// jl_nude_kernel's rows per 256-ciphertext block: digit 1 of (1, pt) only (fbm_na_mm_nude)
+#define FBM_NUDE_ROWS 36
 #define FBM_CST_M 0
 #define FBM_CST_CTR 120  // exp-kernel chunk counter (in M's padding; zeroed by jl_setup_kernel)
 #define FBM_CST_R2 128
@@ -171,13 +173,17 @@ int launch_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, uint64_t* 
                    hipStream_t s);
 int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, int negative, uint32_t* nude,
                    hipStream_t s);
-int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s);
+// Hc != nullptr: the compact form the Montgomery engines read -- Hc[k] = r's 8 words when r is one digest
+// (any real biprime), else the sentinel FBM_HC_FULL (8 words of ones) and the whole row in H[k]; Hc ==
+// nullptr: every row whole in H (the generic engine, fbm_jl_fdh)
+int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s, uint32_t* Hc = nullptr);
 int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32_t* cst, hipStream_t s,
                     const JlShort* sh = nullptr);
 // one exponentiation launch over several calls' ciphertexts (jl_exp_kernel<true> segments)
 #define FBM_EXP_MAXSEG 24
 struct JlExpSeg {
   const uint32_t* H;
+  const uint32_t* Hc;  // compact H rows (jl_fdh_kernel's 8 words per ciphertext; FBM_HC_FULL: read H), or nullptr
   const uint32_t* nude;
   uint32_t* out;
   const uint32_t* ops;
@@ -200,9 +206,10 @@ bool jl_batch_active();
 int jl_batch_count();  // segments recorded in this thread's open batch (0 when none is open)
 uint64_t jl_batch_workspace();
 int jl_batch_flush(void* workspace, uint64_t ws_bytes, hipStream_t s);
+// Hc: launch_jl_fdh's compact rows of the same ciphertexts (nullptr: H holds every row whole)
 int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const JlSched& sc, int mode,
                   const uint32_t* nude, uint32_t* table, uint64_t table_slots, const uint32_t* ops,
-                  const uint32_t* cst, uint32_t* out, hipStream_t s);
+                  const uint32_t* cst, uint32_t* out, hipStream_t s, const uint32_t* Hc = nullptr);
 struct JlRk {  // R^(P+1) mod N^2, 28-bit limbs (jl_rk_kernel -> cst[FBM_CST_RK])
   uint32_t w[FBM_NL];
   uint32_t pad[2];

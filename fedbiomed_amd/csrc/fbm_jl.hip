@@ -161,14 +161,15 @@ __device__ __forceinline__ void relimb_28_29(const uint32_t* x, uint32_t* o) {  
 }
 
 // ------------------------------------------------------------------------------------
-// nude = N*pt + 1 as the N-adic digit pair (1, pt)  ->  [limb][ct] 29-bit limbs in the engines' B
-// layout: rows 0..35 digit 0 (= 1), rows 36..71 digit 1, 256-ciphertext blocks FBM_NL rows apart
-// (the last operand of the exponentiation's encrypt, read in place by jl_exp_kernel; pt < 2^1036
-// < R is a valid one-off digit)
+// nude = N*pt + 1 as the N-adic digit pair (1, pt)  ->  digit 1 only (digit 0 is the constant 1,
+// which the engines take as immediates: fbm_na_mm_nude), [limb][ct] 29-bit limbs in the engines' B
+// layout: rows 0..35, 256-ciphertext blocks FBM_NUDE_ROWS rows apart (the last operand of the
+// exponentiation's encrypt, read in place by jl_exp_kernel; pt < 2^1036 < R is a valid one-off digit)
 // ------------------------------------------------------------------------------------
 // negative != 0 (a negative weight, see jl_pack_kernel): pt holds |pt| and N*pt + 1 is
 // (1, M - |pt|) with M = N * 2^(1036 - bits(N)) = 0 (mod N): 2^1035 <= M < R, so the digit is
 // non-negative and below R for every |pt| < 2^1024.
+static_assert(FBM_NUDE_ROWS == FBM_QA_L, "jl_nude_kernel stores digit 1's 29-bit limbs");
 __global__ void __launch_bounds__(256) jl_nude_kernel(const uint32_t* __restrict__ pt, uint64_t n_ct, JlParams jp,
                                                       int negative, uint32_t* __restrict__ nude) {
   const uint64_t ct = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -192,14 +193,12 @@ __global__ void __launch_bounds__(256) jl_nude_kernel(const uint32_t* __restrict
     }
   }
   // N*pt + 1 in N-adic digits is (1, pt): no arithmetic, only the layout of the
-  // exponentiation's B operand (blocked column, 29-bit limbs: digit 0 in rows 0..35, digit 1 in 36..71)
+  // exponentiation's B operand (blocked column, 29-bit limbs of digit 1; 144 bytes per ciphertext)
   uint32_t p29[FBM_QA_L];
   relimb_28_29(p28, p29);
-  uint32_t* dst = launder_v(nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255));
+  uint32_t* dst = launder_v(nude + (ct >> 8) * (FBM_NUDE_ROWS * 256) + (ct & 255));
 #pragma unroll
-  for (int k = 0; k < FBM_QA_L; ++k) dst[k * 256] = k == 0 ? 1u : 0u;
-#pragma unroll
-  for (int k = 0; k < FBM_QA_L; ++k) dst[(FBM_QA_L + k) * 256] = p29[k];
+  for (int k = 0; k < FBM_QA_L; ++k) dst[k * 256] = p29[k];
 }
 
 // ------------------------------------------------------------------------------------
@@ -372,7 +371,7 @@ __host__ __device__ inline bool gcd_is_one_r8(const uint32_t (&r)[8], const uint
 // loop (_jls.py:746-755) never breaks again and counter.to_bytes(1) overflows at 256 -- its
 // OverflowError, whatever gcd the 8-digest r would have.
 __global__ void __launch_bounds__(256) jl_fdh_kernel(uint64_t n_ct, JlParams jp, uint32_t* __restrict__ H,
-                                                     uint32_t* __restrict__ stats) {
+                                                     uint32_t* __restrict__ stats, uint32_t* __restrict__ Hc) {
   const uint64_t kl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (kl >= n_ct) return;
   const uint64_t k = kl + jp.ct_offset;  // global ciphertext index in t_k = (k << 512) | tau
@@ -420,10 +419,43 @@ __global__ void __launch_bounds__(256) jl_fdh_kernel(uint64_t n_ct, JlParams jp,
     }
   }
   if (!ok) err |= FBM_ERR_FDH_OVERFLOW;
+  if (err) atomicOr(stats + FBM_STAT_ERRFLAGS, err);
+  if (Hc) {  // compact: 32 bytes per ciphertext (one digest), the whole row only behind the sentinel
+    uint32_t wide = 0, ones = ~0u;
+#pragma unroll
+    for (int i = 8; i < 64; ++i) wide |= r[i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ones &= r[i];
+    const bool full = wide != 0u || ones == ~0u;  // (a one-digest r of all ones takes the sentinel too)
+    uint4* c = reinterpret_cast<uint4*>(Hc + kl * 8);
+    c[0] = full ? make_uint4(~0u, ~0u, ~0u, ~0u) : make_uint4(r[0], r[1], r[2], r[3]);
+    c[1] = full ? make_uint4(~0u, ~0u, ~0u, ~0u) : make_uint4(r[4], r[5], r[6], r[7]);
+    if (!full) return;
+  }
   uint4* o = reinterpret_cast<uint4*>(H + kl * 64);
 #pragma unroll
   for (int i = 0; i < 16; ++i) o[i] = make_uint4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
-  if (err) atomicOr(stats + FBM_STAT_ERRFLAGS, err);
+}
+
+// ciphertext ct's H row (64 words) from the compact rows Hc (launch_jl_fdh) or, behind the sentinel / with
+// no compact rows, from H
+__device__ __forceinline__ void load_h(const uint32_t* H, const uint32_t* Hc, uint64_t ct, uint32_t (&h)[64]) {
+  if (Hc) {
+    const uint4* c = reinterpret_cast<const uint4*>(Hc + ct * 8);
+    const uint4 a = c[0], b = c[1];
+    if ((a.x & a.y & a.z & a.w & b.x & b.y & b.z & b.w) != ~0u) {
+      h[0] = a.x; h[1] = a.y; h[2] = a.z; h[3] = a.w; h[4] = b.x; h[5] = b.y; h[6] = b.z; h[7] = b.w;
+#pragma unroll
+      for (int i = 8; i < 64; ++i) h[i] = 0u;
+      return;
+    }
+  }
+  const uint4* s = reinterpret_cast<const uint4*>(H + ct * 64);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint4 v = s[i];
+    h[4 * i] = v.x; h[4 * i + 1] = v.y; h[4 * i + 2] = v.z; h[4 * i + 3] = v.w;
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -615,7 +647,8 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
                                                              uint32_t* __restrict__ table,
                                                              uint32_t* __restrict__ out_a,
                                                              const JlExpSeg* __restrict__ segs, int nseg,
-                                                             uint32_t total_chunks, uint32_t* __restrict__ ctr) {
+                                                             uint32_t total_chunks, uint32_t* __restrict__ ctr,
+                                                             const uint32_t* __restrict__ Hc_a) {
   __shared__ uint32_t lds_a[(FBM_NL + 1) * FBM_BLOCK];
   __shared__ uint32_t chunk_s;
   const int tid = threadIdx.x;
@@ -674,7 +707,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
 #pragma unroll
         for (int i = 0; i < 64; ++i) h[i] = i == 0 ? 1u : 0u;
       } else {
-        load_row64(SEG(H, H_a) + ct * 64, h);
+        load_h(SEG(H, H_a), SEG(Hc, Hc_a), ct, h);
       }
       uint32_t h29[2 * NA];
       {  // h = h_lo + h_hi R: the 72-limb decomposition is (h_lo, h_hi)
@@ -725,7 +758,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
       fbm_na_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, NK, np);  // h_hi*R^2 (wide lanes)
       lds_to_glb(lds, table + (tb0 + tstride) / 4);
       uint32_t h[64];
-      load_row64(SEG(H, H_a) + ct * 64, h);
+      load_h(SEG(H, H_a), SEG(Hc, Hc_a), ct, h);
       uint32_t h29[2 * NA];
       to29_row64(h, h29);
 #pragma unroll
@@ -777,8 +810,8 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
     const int mode = SEG(mode, mode_a);
     if ((mode & FBM_EXP_DEC) == 0) {  // x nude = (1, pt): jl_nude_kernel's 29-bit blocked column, read in place
       // (a chunk is one 256-ciphertext block: its base is uniform, the lane's offset is tid)
-      const uint32_t* nb = SEG(nude, nude_a) + uniform_val((uint64_t)(ct >> 8)) * (FBM_NL * 256);
-      fbm_na_mm_glb(aoff, nb, (uint32_t)(ct & 255) * 4u, NK, np);
+      const uint32_t* nb = SEG(nude, nude_a) + uniform_val((uint64_t)(ct >> 8)) * (FBM_NUDE_ROWS * 256);
+      fbm_na_mm_nude(aoff, nb, (uint32_t)(ct & 255) * 4u, NK, np);
     } else {
       fbm_na_mm_glb(aoff, cst + FBM_CST_ONE, 0u, NK, np);
     }
@@ -930,7 +963,8 @@ __global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(co
                                                                int first, int mode, int key_is_zero, int sbits,
                                                                const uint32_t* __restrict__ nude,
                                                                uint32_t* __restrict__ table,
-                                                               uint32_t* __restrict__ out) {
+                                                               uint32_t* __restrict__ out,
+                                                               const uint32_t* __restrict__ Hc) {
   using E = GroupEng<G>;
   constexpr int M = E::M, ROWW = E::ROWW;
   constexpr uint32_t ENTRY = 2 * M * 256;  // words of one table entry
@@ -979,7 +1013,17 @@ __global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(co
     bool wide = false, shortp = false;
     {  // h -> the lane's 29-bit limbs of (h mod R, h div R) -> scratch
       uint32_t h18[2 * M];
+      // the compact row (8 words, launch_jl_fdh) unless it holds the sentinel (or there is none): the whole row
       const uint32_t* hr = H + ct * 64;
+      int hw = 64;
+      if (Hc) {
+        const uint4* c = reinterpret_cast<const uint4*>(Hc + ct * 8);
+        const uint4 a = c[0], b = c[1];
+        if ((a.x & a.y & a.z & a.w & b.x & b.y & b.z & b.w) != ~0u) {
+          hr = Hc + ct * 8;
+          hw = 8;
+        }
+      }
 #pragma unroll
       for (int r = 0; r < M; ++r) {
         const int k = M * l + r;
@@ -988,8 +1032,8 @@ __global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(co
         } else if (key_is_zero) {
           lo = k == 0 ? 1u : 0u;
         } else {
-          lo = glb_limb(hr, 64, k, FBM_QA_LB);
-          hi = glb_limb(hr, 64, FBM_QA_L + k, FBM_QA_LB);
+          lo = glb_limb(hr, hw, k, FBM_QA_LB);
+          hi = glb_limb(hr, hw, FBM_QA_L + k, FBM_QA_LB);
         }
         h18[r] = lo;
         h18[M + r] = hi;
@@ -1080,7 +1124,7 @@ __global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(co
     }  // (table path)
     {  // last operand: nude = (1, pt) (encrypt; jl_nude_kernel's 29-bit rows, the lane's slice) or 1
       uint32_t b18[2 * M];
-      const uint32_t* nb = nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255);
+      const uint32_t* nb = nude + (ct >> 8) * (FBM_NUDE_ROWS * 256) + (ct & 255);
 #pragma unroll
       for (int d = 0; d < 2; ++d)
 #pragma unroll
@@ -1089,7 +1133,7 @@ __global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(co
           uint32_t v = 0;
           if (dummy) {
           } else if ((mode & FBM_EXP_DEC) == 0) {
-            v = nb[(d * FBM_QA_L + k) * 256];  // jl_nude_kernel's 29-bit rows
+            v = d == 0 ? (k == 0 ? 1u : 0u) : nb[k * 256];  // (1, pt): jl_nude_kernel's 29-bit rows of pt
           } else {
             v = (d == 0 && k == 0) ? 1u : 0u;
           }
@@ -1456,9 +1500,9 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_lift_kernel(uint64_t n_ct, Jl
   }
   if (nude) {  // v <- (v + p y) mod N; p < 2^1036 = R_N, Y' < 2N: p Y' R_N^-1 < 3N
     uint32_t p28[FBM_NLN], p29[FBM_QA_L];
-    const uint32_t* nb = nude + (ct >> 8) * (FBM_NL * 256) + (ct & 255);
+    const uint32_t* nb = nude + (ct >> 8) * (FBM_NUDE_ROWS * 256) + (ct & 255);
 #pragma unroll
-    for (int k = 0; k < FBM_QA_L; ++k) p29[k] = nb[(FBM_QA_L + k) * 256];  // jl_nude_kernel's 29-bit digit 1
+    for (int k = 0; k < FBM_QA_L; ++k) p29[k] = nb[k * 256];  // jl_nude_kernel's 29-bit digit 1
     relimb_29_28(p29, p28);
     mont_mul(p28, lds, ls, mn);  // p y
     uint32_t c = 0;
@@ -1608,9 +1652,9 @@ int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, int ne
   return check_launch("jl_nude_kernel");
 }
 
-int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s) {
+int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s, uint32_t* Hc) {
   if (n_ct == 0) return FBM_OK;
-  hipLaunchKernelGGL(jl_fdh_kernel, grid1(n_ct, 256), dim3(256), 0, s, n_ct, jp, H, stats);
+  hipLaunchKernelGGL(jl_fdh_kernel, grid1(n_ct, 256), dim3(256), 0, s, n_ct, jp, H, stats, Hc);
   return check_launch("jl_fdh_kernel");
 }
 
@@ -1794,7 +1838,8 @@ bool jl_batch_accept(bool on) {
 }
 
 static int jl_batch_record(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const JlSched& sc, int mode,
-                           const uint32_t* nude, const uint32_t* ops, const uint32_t* cst, uint32_t* out) {
+                           const uint32_t* nude, const uint32_t* ops, const uint32_t* cst, uint32_t* out,
+                           const uint32_t* Hc) {
   JlExpBatch& bt = g_batch.bt;
   if (n_ct == 0) return FBM_OK;
   if (bt.nseg >= FBM_EXP_MAXSEG) {
@@ -1822,7 +1867,7 @@ static int jl_batch_record(const uint32_t* H, uint64_t n_ct, const JlParams& jp,
     return FBM_E_UNSUPPORTED;
   }
   bt.seg[bt.nseg++] =
-      JlExpSeg{H, nude, out, ops, n_ct, bt.total_chunks, sc.n_ops, sc.first, mode, jp.key_is_zero, sc.sbits};
+      JlExpSeg{H, Hc, nude, out, ops, n_ct, bt.total_chunks, sc.n_ops, sc.first, mode, jp.key_is_zero, sc.sbits};
   bt.total_chunks += (uint32_t)chunks;
   return FBM_OK;
 }
@@ -1839,20 +1884,20 @@ __global__ void jl_batch_desc_kernel(JlExpBatch bt, JlExpSeg* __restrict__ segs,
 
 int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const JlSched& sc, int mode,
                   const uint32_t* nude, uint32_t* table, uint64_t table_slots, const uint32_t* ops,
-                  const uint32_t* cst, uint32_t* out, hipStream_t s) {
+                  const uint32_t* cst, uint32_t* out, hipStream_t s, const uint32_t* Hc) {
   if (n_ct == 0) return FBM_OK;
-  if (g_batch.active && g_batch.accept) return jl_batch_record(H, n_ct, jp, sc, mode, nude, ops, cst, out);
+  if (g_batch.active && g_batch.accept) return jl_batch_record(H, n_ct, jp, sc, mode, nude, ops, cst, out, Hc);
   const int eng = jl_engine_for(n_ct);
   if (eng == FBM_ENGINE_QUAD || eng == FBM_ENGINE_TRIPLE) {
     uint64_t g = (n_ct + group_ct_per_wg(eng) - 1) / group_ct_per_wg(eng);
     if (g > group_wgs_max()) g = group_wgs_max();
     if (eng == FBM_ENGINE_QUAD) {
       hipLaunchKernelGGL(jl_expg_kernel<4>, dim3((unsigned)g), dim3(FBM_QBLOCK), 0, s, H, n_ct, (uint32_t*)cst,
-                         jp.qa.np, ops, sc.n_ops, sc.first, mode, jp.key_is_zero, sc.sbits, nude, table, out);
+                         jp.qa.np, ops, sc.n_ops, sc.first, mode, jp.key_is_zero, sc.sbits, nude, table, out, Hc);
       return check_launch("jl_expq_kernel");
     }
     hipLaunchKernelGGL(jl_expg_kernel<3>, dim3((unsigned)g), dim3(FBM_QBLOCK), 0, s, H, n_ct, (uint32_t*)cst,
-                       jp.qa.np, ops, sc.n_ops, sc.first, mode, jp.key_is_zero, sc.sbits, nude, table, out);
+                       jp.qa.np, ops, sc.n_ops, sc.first, mode, jp.key_is_zero, sc.sbits, nude, table, out, Hc);
     return check_launch("jl_expt_kernel");
   }
   uint64_t g = (n_ct + FBM_BLOCK - 1) / FBM_BLOCK;
@@ -1863,7 +1908,7 @@ int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const Jl
   static const unsigned lds_pad = getenv("FBM_EXP_LDS_PAD") ? (unsigned)atoi(getenv("FBM_EXP_LDS_PAD")) : 0u;
   hipLaunchKernelGGL(jl_exp_kernel<false>, dim3((unsigned)g), dim3(FBM_BLOCK), lds_pad, s, H, n_ct, (uint32_t*)cst, jp.qa.np,
                      ops, sc.n_ops, sc.first, mode, jp.key_is_zero, sc.sbits, nude, table, out, (const JlExpSeg*)nullptr,
-                     0, 0u, (uint32_t*)nullptr);
+                     0, 0u, (uint32_t*)nullptr, Hc);
   return check_launch("jl_exp_kernel");
 }
 
@@ -1891,7 +1936,7 @@ int jl_batch_flush(void* workspace, uint64_t ws_bytes, hipStream_t s) {
   if (g > gmax) g = gmax;
   hipLaunchKernelGGL(jl_exp_kernel<true>, dim3((unsigned)g), dim3(FBM_BLOCK), 0, s, (const uint32_t*)nullptr, (uint64_t)0,
                      (uint32_t*)g_batch.cst, g_batch.np, (const uint32_t*)nullptr, 0, 0, 0, 0, -1, (const uint32_t*)nullptr,
-                     table, (uint32_t*)nullptr, (const JlExpSeg*)segs, bt.nseg, bt.total_chunks, ctr);
+                     table, (uint32_t*)nullptr, (const JlExpSeg*)segs, bt.nseg, bt.total_chunks, ctr, (const uint32_t*)nullptr);
   return check_launch("jl_exp_kernel (batch)");
 }
 

@@ -163,6 +163,34 @@ def test_nadic_asm_binary_chain_with_short_products():
     assert (y[0] + y[1] * N) % M == pow(h, e, M) * R % M
 
 
+MM_NUDE = GEN.product(False, nude=True)
+
+
+@pytest.mark.parametrize("bits", [2, 263, 1024])
+def test_nadic_asm_nude_product(bits):
+    """fbm_na_mm_nude (round 4): the encrypt's last product by nude = N pt + 1 = (1, pt) with only pt's 36
+    rows in global memory (digit 0 as immediates) -- the general product's result bit for bit, pt up to
+    the one-off operand bound 2^1036 (a negative packing's M - |pt|) included."""
+    rng = random.Random(900 + bits)
+    N = _rand_n(rng, bits)
+    words, np_ = consts(N)
+    NK, BB = 0x4000, 0x100000
+    for trial in range(3):
+        a = (rng.randrange(2 * N), rng.randrange(2 * N))
+        pt = [rng.getrandbits(1024), (1 << 1036) - 1, 0][trial]
+        t, s, _ = run(N, a, (1, pt))
+        lds = {k * 1024: v for k, v in enumerate(limbs(a[0]) + limbs(a[1]))}
+        glb = {BB + k * 1024: v for k, v in enumerate(limbs(pt))}
+        lane = Lane({"a": 0, "b": 0, "bb": BB, "NK": NK, "np": np_}, lds=lds, glb=glb,
+                    smem={NK + 4 * i: w for i, w in enumerate(words)})
+        lane.run(MM_NUDE)
+        out = [lds[k * 1024] for k in range(2 * L)]
+        d0 = sum(v << (LB * k) for k, v in enumerate(out[:L]))
+        d1 = sum(v << (LB * k) for k, v in enumerate(out[L:]))
+        assert (d0, d1) == (t, s), trial
+    assert sum(1 for ln in MM_NUDE if ln.startswith("global_load_dword")) == L  # digit 1's rows only
+
+
 @pytest.mark.parametrize("bits", [2, 24, 1024])
 def test_nadic_asm_product_and_square(bits):
     rng = random.Random(bits)
@@ -347,6 +375,12 @@ def test_column_bounds_proved_for_every_operand():
     lane = _bound_lane(top, KADDR, dp)
     lane.args.update({f"h{i}": (0, MASK) for i in range(KS)})
     lane.run(MS)
+    # the encrypt's last product by (1, pt), pt < 2^1036 (a negative packing's M - |pt| included)
+    lane = _bound_lane(top)
+    BB = 0x100000
+    lane.args.update({"b": (0, 0), "bb": (BB, BB)})
+    lane.glb.update({BB + k * 1024: (0, MASK if k < L - 1 else (1 << 21) - 1) for k in range(L)})
+    lane.run(MM_NUDE)
     keep = GEN.SQ_MID_KEEP
     try:
         for part in (0, 1):

@@ -138,6 +138,18 @@ def load_b_global():
     return out
 
 
+def load_b_nude():
+    """The encrypt's last operand nude = N pt + 1 = the digit pair (1, pt): digit 0 as immediates, only
+    digit 1's rows from global (jl_nude_kernel stores 36 rows per ciphertext block, not 72)."""
+    out = ["s_waitcnt vmcnt(0)", f"v_mov_b32 {TMP}, %[b]"]
+    for j in range(L):
+        if j and j % 4 == 0:
+            out.append(f"v_add_u32 {TMP}, 0x1000, {TMP}")
+        out.append(f"global_load_dword {breg(L + j)}, {TMP}, %[bb] offset:{(j % 4) * 1024}")
+    out += [f"v_mov_b32 {breg(j)}, {1 if j == 0 else 0}" for j in range(L)]
+    return out
+
+
 def load_b_square():
     out = [f"v_add_u32 {TMP}, 0x10000, %[a]"]
     for j in range(2 * L):
@@ -268,9 +280,9 @@ def rotate_carries(lines, pairs=CARRY_PAIRS):
     return out
 
 
-def product(sq):
+def product(sq, nude=False):
     body = [f"s_mov_b32 {M0_SAVE}, m0"] + load_consts()
-    body += load_b_square() if sq else load_b_global()
+    body += load_b_square() if sq else (load_b_nude() if nude else load_b_global())
     body += [f"v_mov_b32 {NPV}, %[np]", f"v_mov_b32 {AADR}, %[a]", f"ds_read_b32 {X0}, {AADR}"]
     if not sq:
         body.append(f"ds_read_b32 {X1}, {AADR} offset:{ROW1}")
@@ -782,6 +794,17 @@ __device__ __forceinline__ void fbm_na_mm_glb(uint32_t a_off, const uint32_t* bb
                                               const uint32_t* NK, uint32_t np) {{
   asm volatile(
 {c_string(mm)}
+      :
+      : [a] "v"(a_off), [b] "v"(b_off), [bb] "s"(bb), [NK] "s"(NK), [np] "s"(np)
+      : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
+}}
+
+// a <- a * (1, p) R^-1 (mod N^2): the encrypt's nude = N p + 1, digit 1's limb k at bb + b_off + k*1024
+// (digit 0 = 1 as immediates: jl_nude_kernel stores only digit 1)
+__device__ __forceinline__ void fbm_na_mm_nude(uint32_t a_off, const uint32_t* bb, uint32_t b_off,
+                                               const uint32_t* NK, uint32_t np) {{
+  asm volatile(
+{c_string(product(False, nude=True))}
       :
       : [a] "v"(a_off), [b] "v"(b_off), [bb] "s"(bb), [NK] "s"(NK), [np] "s"(np)
       : "memory", "vcc", "scc", FBM_NA_CLOBBERS);
