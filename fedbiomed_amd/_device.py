@@ -1024,6 +1024,32 @@ def jl_fdh(n_ct: int, modulus: int, tau: int, ct_offset: int = 0, dev=None) -> t
     return h
 
 
+def jl_fdh_msg(ts: List[int], bits_size: int, modulus: int, dev=None) -> torch.Tensor:
+    """FDH(bits_size, modulus).H(t) for each t (any bits_size; fbm_jl_fdh_msg) -> int32 [len(ts), 128] limbs.
+    The reference's to_bytes errors are raised here first: t < 0 and t >= 2^(8 (bits_size // 2))."""
+    dev = dev or device()
+    L = bits_size // 2
+    if L < 0:
+        raise ValueError("length argument must be non-negative")
+    for t in ts:
+        if t < 0:
+            raise OverflowError("can't convert negative int to unsigned")
+        if t.bit_length() > 8 * L:
+            raise OverflowError("int too big to convert")
+    tw = max(1, (L + 3) // 4)
+    host = np.zeros((len(ts), tw), dtype=np.uint32)
+    for i, t in enumerate(ts):
+        host[i] = int_limbs(t, tw)
+    odd, even = fdh_modulus(modulus)
+    h = torch.empty((len(ts), 128), dtype=torch.int32, device=dev)
+    st = _stats(dev)
+    t_dev = torch.from_numpy(host.view(np.int32)).to(dev)
+    _call(N.load().fbm_jl_fdh_msg, len(ts), _ptr(t_dev), tw, int(bits_size), _np_ptr(int_limbs(odd, 32)),
+          1 if even else 0, _ptr(h), _ptr(st), _stream())
+    _check_stats(st)
+    return h
+
+
 def jl_product(cts: torch.Tensor, biprime: int) -> torch.Tensor:
     """prod_u cts[u] mod N^2 (EncryptedNumber sums): int32 [P, n_ct, 64] -> [n_ct, 64], canonical."""
     P, n_ct, _ = cts.shape

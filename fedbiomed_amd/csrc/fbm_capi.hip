@@ -1052,6 +1052,11 @@ int fbm_check_stats(const uint32_t* st, int lom_nodes, uint32_t* max_bits_out) {
     set_error("FDH: no r of 1..7 digests with gcd(r, N^2) == 1 (reference: OverflowError)");
     return FBM_E_FDH;
   }
+  if (f & FBM_ERR_FDH_WIDE) {
+    set_error("FDH: no coprime r of 1..15 digests; the reference would try 16 or more (bits_size > 4096): "
+              "outside the device path's domain");
+    return FBM_E_UNSUPPORTED;
+  }
   if (f & FBM_ERR_NOT_INVERTIBLE) {
     set_error("invert() no inverse exists");
     return FBM_E_INVERSE;
@@ -1642,6 +1647,41 @@ int fbm_jl_fdh(uint64_t n_ct, const uint32_t* modulus_odd, int modulus_even, con
     return FBM_E_ARG;
   }
   return timed("jl_fdh", s, [&] { return launch_jl_fdh(n_ct, jp, h, stats, s); });
+}
+
+int fbm_jl_fdh_msg(uint64_t n, const uint32_t* t, int t_words, int bits_size, const uint32_t* modulus_odd,
+                   int modulus_even, uint32_t* h, uint32_t* stats, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc = zero_stats(stats, s);
+  if (rc) return rc;
+  if (!modulus_odd || bits_size < 0 || t_words < 0) {
+    set_error("fbm_jl_fdh_msg: null modulus or negative size");
+    return FBM_E_ARG;
+  }
+  const int msg_bytes = bits_size / 2;  // int(t).to_bytes(bits_size // 2, 'big')
+  if ((int64_t)t_words * 4 < msg_bytes) {
+    set_error("fbm_jl_fdh_msg: %d words hold no %d-byte message", t_words, msg_bytes);
+    return FBM_E_ARG;
+  }
+  if (!(modulus_odd[0] & 1u)) {
+    set_error("fbm_jl_fdh_msg: the modulus's odd part must be odd");
+    return FBM_E_ARG;
+  }
+  // digests r may hold: the reference's inner loop breaks while r is shorter than bits_size // 8 bytes
+  const int bytes = bits_size / 8;
+  const int kmax = bytes >= 1 ? (bytes - 1) / 32 : 0;
+  if (n == 0) return FBM_OK;
+  if (kmax == 0) {  // a single digest is already bits_size // 8 bytes: the counter byte overflows at 256
+    set_error("FDH of bits_size %d: r never shorter than bits_size // 8 bytes (reference: OverflowError)", bits_size);
+    return FBM_E_FDH;
+  }
+  if (!t || !h) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  return timed("jl_fdh", s, [&] {
+    return launch_jl_fdh_msg(n, t, t_words, msg_bytes, kmax, modulus_odd, modulus_even ? 1 : 0, h, stats, s);
+  });
 }
 
 int fbm_jl_product(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* biprime, uint32_t* out,

@@ -18,6 +18,8 @@
 #define FBM_ERR_ITER_CAP 8u        // a bounded data-dependent loop hit its cap
 #define FBM_ERR_ROUND_RANGE 128u   // LOM: some i + tau reaches 2^64 with peers to mask with
 #define FBM_ERR_PT_WIDE 32u        // VES: a packed value spills past the 1024-bit plaintext
+#define FBM_ERR_FDH_WIDE 64u       // FDH of bits_size > 4096: no coprime r of 1..15 digests, and the
+                                   // reference would go on to 16 or more (outside the device path's domain)
 #define FBM_WARN_CLIPPED 16u       // not an error: some |x| > clipping range (the reference's
                                    // _check_clipping_range warning, _secagg_utils.py:189-204)
 
@@ -177,6 +179,13 @@ int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, int ne
 // (any real biprime), else the sentinel FBM_HC_FULL (8 words of ones) and the whole row in H[k]; Hc ==
 // nullptr: every row whole in H (the generic engine, fbm_jl_fdh)
 int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s, uint32_t* Hc = nullptr);
+// FDH.H of any bits_size: one lane per t (tw-word rows), message t.to_bytes(msg_bytes) || counter, r of at
+// most kmax digests (fbm_jl_fdh_msg; r of up to FBM_FDH_MSG_DIGESTS digests, FBM_FDH_MSG_ROW-word rows)
+#define FBM_FDH_MSG_DIGESTS 15
+#define FBM_FDH_MSG_WORDS (8 * FBM_FDH_MSG_DIGESTS)
+#define FBM_FDH_MSG_ROW 128
+int launch_jl_fdh_msg(uint64_t n, const uint32_t* t, int tw, int msg_bytes, int kmax, const uint32_t* n32, int even,
+                      uint32_t* H, uint32_t* stats, hipStream_t s);
 int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32_t* cst, hipStream_t s,
                     const JlShort* sh = nullptr);
 // one exponentiation launch over several calls' ciphertexts (jl_exp_kernel<true> segments)

@@ -204,37 +204,39 @@ __global__ void __launch_bounds__(256) jl_nude_kernel(const uint32_t* __restrict
 // ------------------------------------------------------------------------------------
 // FDH
 // ------------------------------------------------------------------------------------
-// gcd(u, N) == 1 for u < 2^2048 (64 limbs), N odd (<= 1024 bits).  Binary GCD, bounded.
-__device__ bool gcd_is_one(uint32_t (&u)[64], const uint32_t* N32, uint32_t& err) {
-  uint32_t v[64];
+// gcd(u, N) == 1 for u < 2^(32 W) (W limbs: 64 for the crypter's FDH, 120 for FDH objects of up to
+// 4096 bits), N odd (<= 1024 bits).  Binary GCD, bounded.
+template <int W>
+__device__ bool gcd_is_one_w(uint32_t (&u)[W], const uint32_t* N32, uint32_t& err) {
+  uint32_t v[W];
 #pragma unroll
-  for (int i = 0; i < 64; ++i) v[i] = i < 32 ? N32[i] : 0u;
+  for (int i = 0; i < W; ++i) v[i] = i < 32 ? N32[i] : 0u;
   uint32_t any = 0;
 #pragma unroll
-  for (int i = 0; i < 64; ++i) any |= u[i];
+  for (int i = 0; i < W; ++i) any |= u[i];
   if (any) {
     int it = 0;
     for (; it < 20000; ++it) {
       // strip factors of two from u (N is odd, so they never divide the gcd)
       while (u[0] == 0u) {
 #pragma unroll
-        for (int i = 0; i < 63; ++i) u[i] = u[i + 1];
-        u[63] = 0u;
+        for (int i = 0; i < W - 1; ++i) u[i] = u[i + 1];
+        u[W - 1] = 0u;
       }
       const int s = __builtin_ctz(u[0]);
       if (s) {
 #pragma unroll
-        for (int i = 0; i < 63; ++i) u[i] = (u[i] >> s) | (u[i + 1] << (32 - s));
-        u[63] >>= s;
+        for (int i = 0; i < W - 1; ++i) u[i] = (u[i] >> s) | (u[i + 1] << (32 - s));
+        u[W - 1] >>= s;
       }
       int cmp = 0;
 #pragma unroll
-      for (int i = 63; i >= 0; --i)
+      for (int i = W - 1; i >= 0; --i)
         if (cmp == 0) cmp = (u[i] > v[i]) - (u[i] < v[i]);
       if (cmp == 0) break;
       if (cmp < 0) {
 #pragma unroll
-        for (int i = 0; i < 64; ++i) {
+        for (int i = 0; i < W; ++i) {
           const uint32_t t = u[i];
           u[i] = v[i];
           v[i] = t;
@@ -242,7 +244,7 @@ __device__ bool gcd_is_one(uint32_t (&u)[64], const uint32_t* N32, uint32_t& err
       }
       uint32_t br = 0;  // u -= v (u > v, both odd: result even and nonzero)
 #pragma unroll
-      for (int i = 0; i < 64; ++i) {
+      for (int i = 0; i < W; ++i) {
         const uint64_t d = (uint64_t)u[i] - v[i] - br;
         u[i] = (uint32_t)d;
         br = (uint32_t)(d >> 63);
@@ -252,9 +254,11 @@ __device__ bool gcd_is_one(uint32_t (&u)[64], const uint32_t* N32, uint32_t& err
   }
   uint32_t rest = 0;
 #pragma unroll
-  for (int i = 1; i < 64; ++i) rest |= v[i];
+  for (int i = 1; i < W; ++i) rest |= v[i];
   return v[0] == 1u && rest == 0;
 }
+
+__device__ bool gcd_is_one(uint32_t (&u)[64], const uint32_t* N32, uint32_t& err) { return gcd_is_one_w<64>(u, N32, err); }
 
 // gcd(r, N) == 1 for a one-digest r (8 limbs), N odd: the common case, far less work than
 // the 64-limb binary gcd above.  Factors of two of r do not divide N, so they are stripped
@@ -456,6 +460,97 @@ __device__ __forceinline__ void load_h(const uint32_t* H, const uint32_t* Hc, ui
     const uint4 v = s[i];
     h[4 * i] = v.x; h[4 * i + 1] = v.y; h[4 * i + 2] = v.z; h[4 * i + 3] = v.w;
   }
+}
+
+// FDH.H of any bits_size (_jls.py:742-762), for FDH objects other than the crypter's FDH(2048, N^2): the
+// message is t.to_bytes(L, 'big') || counter (L = bits_size // 2 bytes), r the digests so far
+// concatenated (r = D1 || D2 || ...), at most kmax of them -- the reference's inner loop stops breaking
+// once r holds bits_size // 8 bytes and its counter byte then overflows.  One lane per t: the blocks of
+// t bytes alone are hashed once, the one or two tail blocks (t's last bytes, the counter, the padding and
+// the length) per counter.  r is kept to 15 digests (120 words: every r an FDH of up to 4096 bits can
+// take); a bits_size that would let the reference try a 16th reports FBM_ERR_FDH_WIDE instead of guessing.
+struct FdhModArg {
+  uint32_t n32[32];  // the modulus's odd part (of M or of sqrt(M)), 32 limbs
+  int even;          // M even: a coprime r must be odd as well
+};
+__device__ __forceinline__ uint32_t fdh_msg_byte(const uint32_t* t, int L, int i) {  // byte i of t.to_bytes(L)
+  const int j = L - 1 - i;
+  return (t[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+}
+__global__ void __launch_bounds__(64) jl_fdh_msg_kernel(uint64_t n, const uint32_t* __restrict__ t, int tw, int L,
+                                                        int kmax, FdhModArg m, uint32_t* __restrict__ H,
+                                                        uint32_t* __restrict__ stats) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t* tr = t + k * (uint64_t)tw;
+  uint32_t st[8], W[16];
+  fbm_sha256_init(st);
+  const int F = L / 64;  // blocks of t bytes only: the same for every counter
+#pragma unroll 1
+  for (int b = 0; b < F; ++b) {
+#pragma unroll 1
+    for (int j = 0; j < 16; ++j) {
+      uint32_t w = 0;
+      for (int q = 0; q < 4; ++q) w = (w << 8) | fdh_msg_byte(tr, L, 64 * b + 4 * j + q);
+      W[j] = w;
+    }
+    fbm_sha256_compress(st, W);
+  }
+  const int rem = L - 64 * F;                    // t bytes left for the tail
+  const int nb = (rem + 1 + 1 + 8 + 63) / 64;    // + counter, 0x80, 64-bit length: 1 or 2 blocks
+  const uint64_t len_bits = 8ull * (uint64_t)(L + 1);
+  uint32_t r[FBM_FDH_MSG_WORDS];
+#pragma unroll
+  for (int i = 0; i < FBM_FDH_MSG_WORDS; ++i) r[i] = 0u;
+  uint32_t err = 0;
+  bool ok = false;
+  const int kuse = kmax < FBM_FDH_MSG_DIGESTS ? kmax : FBM_FDH_MSG_DIGESTS;
+#pragma unroll 1
+  for (int c = 1; c <= kuse && !ok; ++c) {
+    uint32_t d[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = st[i];
+#pragma unroll 1
+    for (int b = 0; b < nb; ++b) {
+#pragma unroll 1
+      for (int j = 0; j < 16; ++j) {
+        uint32_t w = 0;
+        for (int q = 0; q < 4; ++q) {
+          const int p = 64 * b + 4 * j + q;
+          uint32_t v = 0;
+          if (p < rem) v = fdh_msg_byte(tr, L, 64 * F + p);
+          else if (p == rem) v = (uint32_t)c;
+          else if (p == rem + 1) v = 0x80u;
+          else if (p >= 64 * nb - 8) v = (uint32_t)(len_bits >> (8 * (64 * nb - 1 - p))) & 0xFFu;
+          w = (w << 8) | v;
+        }
+        W[j] = w;
+      }
+      fbm_sha256_compress(d, W);
+    }
+#pragma unroll 1
+    for (int i = FBM_FDH_MSG_WORDS - 1; i >= 8; --i) r[i] = r[i - 8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = d[7 - i];
+    if (m.even && !(r[0] & 1u)) {
+      ok = false;
+    } else if (c == 1) {
+      uint32_t r8[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r8[i] = r[i];
+      ok = gcd_is_one_r8(r8, m.n32, err);
+    } else {
+      uint32_t u[FBM_FDH_MSG_WORDS];
+#pragma unroll 1
+      for (int i = 0; i < FBM_FDH_MSG_WORDS; ++i) u[i] = r[i];
+      ok = gcd_is_one_w<FBM_FDH_MSG_WORDS>(u, m.n32, err);
+    }
+  }
+  if (!ok) err |= kmax > FBM_FDH_MSG_DIGESTS ? FBM_ERR_FDH_WIDE : FBM_ERR_FDH_OVERFLOW;
+  uint32_t* o = H + k * FBM_FDH_MSG_ROW;
+#pragma unroll 1
+  for (int i = 0; i < FBM_FDH_MSG_ROW; ++i) o[i] = i < FBM_FDH_MSG_WORDS ? r[i] : 0u;
+  if (err) atomicOr(stats + FBM_STAT_ERRFLAGS, err);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1650,6 +1745,16 @@ int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, int ne
   if (n_ct == 0) return FBM_OK;
   hipLaunchKernelGGL(jl_nude_kernel, grid1(n_ct, 256), dim3(256), 0, s, pt, n_ct, jp, negative, nude);
   return check_launch("jl_nude_kernel");
+}
+
+int launch_jl_fdh_msg(uint64_t n, const uint32_t* t, int tw, int msg_bytes, int kmax, const uint32_t* n32, int even,
+                      uint32_t* H, uint32_t* stats, hipStream_t s) {
+  if (n == 0) return FBM_OK;
+  FdhModArg m;
+  memcpy(m.n32, n32, sizeof(m.n32));
+  m.even = even;
+  hipLaunchKernelGGL(jl_fdh_msg_kernel, grid1(n, 64), dim3(64), 0, s, n, t, tw, msg_bytes, kmax, m, H, stats);
+  return check_launch("jl_fdh_msg_kernel");
 }
 
 int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s, uint32_t* Hc) {

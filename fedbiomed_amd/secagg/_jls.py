@@ -442,7 +442,11 @@ class FDH:
         return D.limbs_to_ints(D.to_host(h).numpy())
 
     def H(self, t: int) -> int:
-        """SHA256(t || 1) || SHA256(t || 2) || ... until gcd(r, n_modulus) == 1, t as 1024
-        big-endian bytes -- fbm_jl_fdh with tau = t and k = 0 (any 0 <= t < 2^8192)."""
+        """SHA256(t || 1) || SHA256(t || 2) || ... until gcd(r, n_modulus) == 1, t as bits_size // 2
+        big-endian bytes -- fbm_jl_fdh with tau = t and k = 0 at bits_size 2048 (any 0 <= t < 2^8192),
+        fbm_jl_fdh_msg at any other bits_size (round 4)."""
+        if self.bits_size != SAParameters.KEY_SIZE:
+            h = D.jl_fdh_msg([operator.index(t)], self.bits_size, int(self._n_modules))
+            return D.limbs_to_ints(D.to_host(h).numpy())[0]
         t = _check_tau(t)  # int(t).to_bytes(1024, ...)'s OverflowError outside [0, 2^8192) (_jls.py:747)
         return self._hash_range(t, 1, 0)[0]

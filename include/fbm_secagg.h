@@ -203,6 +203,15 @@ int fbm_jl_pack(const void* x, int x_dtype, uint64_t n, int es, int cr, uint32_t
 int fbm_jl_unpack(const uint32_t* pt, uint64_t n_ct, int es, int cr, uint64_t n_out, uint64_t* vals, void* stream);
 int fbm_jl_fdh(uint64_t n_ct, const uint32_t* modulus_odd, int modulus_even, const uint32_t* tau, uint64_t ct_offset,
                uint32_t* h, uint32_t* stats, void* stream);
+/* fbm_jl_fdh_msg: FDH(bits_size, M).H(t) for FDH objects of any bits_size (round 4; reference
+ * _jls.py:742-762 -- the crypter's FDH(2048, N^2) takes fbm_jl_fdh): for each of n values t (device,
+ * t_words little-endian 32-bit words each, t < 2^(8 (bits_size / 2)): the caller checks the
+ * reference's to_bytes range), r = SHA256(t.to_bytes(bits_size / 2) || 1) || SHA256(... || 2) || ...
+ * until gcd(r, M) == 1, at most (bits_size / 8 - 1) / 32 digests (FBM_E_FDH when none qualifies or
+ * bits_size < 264: the reference's counter byte overflows; FBM_E_UNSUPPORTED at fbm_check_stats when
+ * bits_size > 4096 would let it try a 16th).  M as in fbm_jl_fdh.  h: n x 128 limbs (device; r < 2^3840). */
+int fbm_jl_fdh_msg(uint64_t n, const uint32_t* t, int t_words, int bits_size, const uint32_t* modulus_odd,
+                   int modulus_even, uint32_t* h, uint32_t* stats, void* stream);
 int fbm_jl_product(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* biprime, uint32_t* out,
                    void* workspace, void* stream);
 int fbm_jl_decrypt(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* biprime, const uint32_t* key,

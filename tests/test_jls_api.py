@@ -122,8 +122,7 @@ def test_encrypted_number_sums_are_lazy():
 
 def test_domain_restrictions_raise_fb624():
     pp = pp_of(123457)
-    with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):  # FDH hashes on the device at 2048 bits only
-        UserKey(PublicParam(123457, 1024, FDH(1024, 123457 ** 2).H), 3).encrypt([1], 1)
+    # (FDH of any other bits_size: on the device since round 4 -- tests/test_fdh_bits.py)
     with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
         UserKey(pp_of(0), 3).encrypt([1], 1)  # N = 0 (every N >= 1 is in the domain: tests/test_n_one.py)
     # (rounds of 2^512 and more, FDH.H of any t < 2^8192: on the device since ABI 3 -- tests/test_caller_flows.py)

@@ -837,6 +837,36 @@ def gen_n_one(R):
     dump("n_one.json", out)
 
 
+def gen_fdh_bits(R):
+    """FDH(bits_size, M).H for bits_size other than 2048 (fdh_bits.json): the message is
+    int(t).to_bytes(bits_size // 2) || counter, r the concatenation of the digests so far; the inner loop
+    stops breaking once r holds bits_size // 8 bytes, after which counter.to_bytes(1) overflows at 256
+    (_jls.py:742-762) -- so bits_size < 264 always raises, and r has at most ceil(bits_size / 256) - 1
+    digests.  Moduli: a real biprime square, small odd / even / prime-power moduli (retries), 1."""
+    jls = R.jls
+    mpz = sys.modules["gmpy2"].mpz
+    rng = random.Random(2048)
+    out = []
+    mods = [W.BIPRIME0 ** 2, 3 * 5 * 7 * 11 * 13, 2 ** 20, 3 ** 40, 1, 1156 ** 2, 6, 255 * 257]
+    for bits in (8, 256, 263, 264, 512, 520, 1000, 1024, 1536, 2040, 2048, 2056, 3072, 4096):
+        L = bits // 2
+        for m in mods:
+            ts = [0, 1, rng.getrandbits(min(8 * L, 600)), (1 << (8 * L)) - 1 if L else 0, 1 << (8 * L), -1]
+            if bits >= 1024:
+                ts.append((5 << 512) | 77)
+            outs = []
+            for t in ts:
+                outs.append({"t": ihex(t), "h": _outcome(lambda t=t, m=m: ihex(int(jls.FDH(bits, mpz(m)).H(t))))})
+            out.append({"bits": bits, "m": ihex(m), "cases": outs})
+    # the object API with such an FDH as the PublicParam's hashing function (called per t, as the
+    # reference's _populate_tau does): tests/test_jls_api.py's former FB624 case, encrypt + decrypt
+    pp = jls.PublicParam(mpz(123457), 1024, jls.FDH(1024, mpz(123457) * mpz(123457)).H)
+    cts = [int(c) for c in jls.UserKey(pp, 3).encrypt([mpz(1), mpz(5)], 1)]
+    dec = [int(v) for v in jls.ServerKey(pp, -3).decrypt([jls.EncryptedNumber(pp, mpz(c)) for c in cts], 1)]
+    dump("fdh_bits.json", {"fdh": out, "user_encrypt_fdh1024": {"n": 123457, "key": 3, "pt": [1, 5], "tau": 1,
+                                                                "ct": [ihex(c) for c in cts], "dec": dec}})
+
+
 def I(s):  # noqa: E743 - hex string -> int (the fixtures' encoding)
     return int(s, 16)
 
@@ -864,6 +894,9 @@ def main():
     if sys.argv[1:] == ["n_one"]:
         gen_n_one(R)
         return
+    if sys.argv[1:] == ["fdh_bits"]:
+        gen_fdh_bits(R)
+        return
     gen_quantize(R)
     gen_lom(R)
     gen_jl(R)
@@ -877,6 +910,7 @@ def main():
     gen_custom_hash(R)
     gen_caller_flows(R)
     gen_n_one(R)
+    gen_fdh_bits(R)
     meta = {"generator": "tools/gen_golden.py", "reference": load_reference.REF,
             "note": "outputs of the reference Fed-BioMed crypter (Python), imported via tools/refshim"}
     dump("meta.json", meta)
