@@ -942,10 +942,10 @@ def int_multiply(vals: torch.Tensor, k: int) -> List[int]:
 
 
 def int_true_divide(vals: torch.Tensor, k) -> List[float]:
-    """[v / k] (utils.divide, _secagg_utils.py:137-149) on the device for v < 2^128: an integer k
-    (0 < |k| < 2^64) with Python's correctly rounded int/int true division, a real k with Python's
-    int / float (float(v), then the IEEE division); the divisor is never truncated.  k == 0 raises
-    the reference's ZeroDivisionError; an integer |k| >= 2^64 is FB624 (the device path's domain)."""
+    """[v / k] (utils.divide, _secagg_utils.py:137-149) on the device for v < 2^128: an integer k of any
+    size with Python's correctly rounded int/int true division (|k| >= 2^64: fbm_int_true_div_big), a
+    real k with Python's int / float (float(v), then the IEEE division); the divisor is never truncated.
+    k == 0 raises the reference's ZeroDivisionError."""
     import numbers
 
     if isinstance(k, numbers.Integral):
@@ -953,8 +953,11 @@ def int_true_divide(vals: torch.Tensor, k) -> List[float]:
         if k == 0:
             raise ZeroDivisionError("division by zero")
         if abs(k) > U64_MAX:
-            raise FedbiomedSecaggCrypterError(f"{ErrorNumbers.FB624.value}: divisor {k} outside (-2^64, 2^64), "
-                                              "the device path's domain")
+            out = torch.empty(vals.shape[0], dtype=torch.float64, device=vals.device)
+            kw = max(1, (abs(k).bit_length() + 31) // 32)
+            _call(N.load().fbm_int_true_div_big, _ptr(vals.contiguous()), vals.shape[0], _np_ptr(int_limbs(abs(k), kw)),
+                  kw, 1 if k < 0 else 0, _ptr(out), _stream())
+            return to_host(out).numpy().tolist()
         op, karg = (1 if k > 0 else 3), abs(k)
     elif isinstance(k, numbers.Real):
         kd = float(k)

@@ -1835,6 +1835,36 @@ int fbm_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, void* out, ui
   });
 }
 
+int fbm_int_true_div_big(const uint64_t* x, uint64_t n, const uint32_t* k, int k_words, int negative, double* out,
+                         void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!k || k_words < 1) {
+    set_error("fbm_int_true_div_big: null or empty divisor");
+    return FBM_E_ARG;
+  }
+  int nz = 0;
+  for (int i = 0; i < k_words; ++i) nz |= k[i] != 0u;
+  if (!nz) {
+    set_error("division by zero");
+    return FBM_E_ARG;
+  }
+  if (n == 0) return FBM_OK;
+  if (!x || !out) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  return timed("int_ops", s, [&] { return launch_int_true_div_big(x, n, k, k_words, negative ? 1 : 0, out, s); });
+}
+
+int fbm_test_true_div_big(const uint64_t* x, uint64_t n, const uint32_t* k, int k_words, int negative, double* out) {
+  if (!k || k_words < 1 || (n > 0 && (!x || !out))) {
+    set_error("fbm_test_true_div_big: bad arguments");
+    return FBM_E_ARG;
+  }
+  host_true_div_big(x, n, k, k_words, negative, out);
+  return FBM_OK;
+}
+
 int fbm_jl_batch_begin(void) { return jl_batch_begin(); }
 
 void fbm_jl_batch_abort(void) { jl_batch_abort(); }

@@ -171,6 +171,10 @@ struct JlParams {
 
 int launch_jl_pack(const void* x, int x_dtype, uint64_t n, const QuantParams& qp, uint64_t weight, int es, int cr,
                    uint64_t n_ct, uint32_t* pt, uint32_t* stats, hipStream_t s);
+// v / k (Python's int / int true division) for an integer |k| >= 2^64 given as k_words host limbs
+int launch_int_true_div_big(const uint64_t* x, uint64_t n, const uint32_t* k, int k_words, int negative, double* out,
+                            hipStream_t s);
+void host_true_div_big(const uint64_t* x, uint64_t n, const uint32_t* k, int k_words, int negative, double* out);
 int launch_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, uint64_t* prod, double* quot, uint32_t* stats,
                    hipStream_t s);
 int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, int negative, uint32_t* nude,

@@ -2124,6 +2124,121 @@ __global__ void __launch_bounds__(256) int_ops_kernel(const uint64_t* __restrict
   prod[3 * i + 2] = (uint64_t)(ph >> 64) + (uint64_t)(mid >> 64);
 }
 
+// v / k for an integer k >= 2^64 (utils.divide with a wide divisor, _secagg_utils.py:137-149): Python's
+// correctly rounded int / int true division (round half to even, subnormal results rounded once) of
+// v < 2^128.  q = floor(v 2^s / k) with s chosen so q has 55 or 56 bits, by 56 steps of restoring long
+// division on the divisor's limbs (at most 38 words: a divisor of more than 1 204 bits makes every
+// quotient round to 0 -- the host passes zero_all); then round q at the result's ulp.
+struct KBig {
+  uint32_t w[40];  // |k|, little-endian words (bits <= 1204)
+  int words, bits, negative, zero_all;
+};
+// one value (__host__ too: the CPU suite checks it against Python's division through fbm_test_true_div_big)
+__host__ __device__ inline double true_div_big(uint64_t lo, uint64_t hi, const KBig& kb) {
+  const double sign = kb.negative ? -1.0 : 1.0;
+  const int la = hi ? 128 - __builtin_clzll(hi) : (lo ? 64 - __builtin_clzll(lo) : 0);
+  if (la == 0 || kb.zero_all || kb.bits - la >= 1076)  // v / k < 2^-1075: rounds to (signed) zero
+    return sign * 0.0;
+  constexpr int W = 42;  // the divisor (<= 1 204 bits) shifted left by at most 9, plus a spare word
+  uint32_t a[4] = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+  const int s = 55 - (la - kb.bits);  // q = floor(v 2^s / k) in [2^54, 2^56); s >= -9 (v < 2^128 <= k 2^64)
+  // B = k << max(-s, 0); the numerator X = v << max(s, 0), consumed a bit at a time from bit 55 down
+  uint32_t B[W], Y[W];
+  const int bs = s < 0 ? -s : 0, xs = s > 0 ? s : 0;
+  for (int j = 0; j < W; ++j) {
+    const int src = j;  // B[j] = (k << bs) word j
+    const uint32_t cur = src < kb.words ? kb.w[src] : 0u;
+    const uint32_t prev = src - 1 >= 0 && src - 1 < kb.words ? kb.w[src - 1] : 0u;
+    B[j] = bs ? (cur << bs) | (prev >> (32 - bs)) : cur;
+  }
+  // Y = X >> 56 = v << (xs - 56) (or v >> (56 - xs)), word by word
+  for (int j = 0; j < W; ++j) {
+    const int sh = xs - 56;  // bit shift of v into Y
+    uint32_t w = 0;
+    for (int b = 0; b < 32; ++b) {  // bit (32 j + b) of Y = bit (32 j + b - sh) of v
+      const int vb = 32 * j + b - sh;
+      if (vb >= 0 && vb < 128 && ((a[vb >> 5] >> (vb & 31)) & 1u)) w |= 1u << b;
+    }
+    Y[j] = w;
+  }
+  uint64_t q = 0;
+  for (int t = 55; t >= 0; --t) {
+    uint32_t carry = 0;  // Y = 2 Y + bit t of X
+    for (int j = 0; j < W; ++j) {
+      const uint32_t nc = Y[j] >> 31;
+      Y[j] = (Y[j] << 1) | carry;
+      carry = nc;
+    }
+    const int vb = t - xs;
+    if (vb >= 0 && vb < 128 && ((a[vb >> 5] >> (vb & 31)) & 1u)) Y[0] |= 1u;
+    int cmp = 0;
+    for (int j = W - 1; j >= 0 && cmp == 0; --j) cmp = (Y[j] > B[j]) - (Y[j] < B[j]);
+    if (cmp >= 0) {
+      uint32_t br = 0;
+      for (int j = 0; j < W; ++j) {
+        const uint64_t d = (uint64_t)Y[j] - B[j] - br;
+        Y[j] = (uint32_t)d;
+        br = (uint32_t)(d >> 63);
+      }
+      q |= 1ull << t;
+    }
+  }
+  uint32_t rem = 0;
+  for (int j = 0; j < W; ++j) rem |= Y[j];
+  const int lq = 64 - __builtin_clzll(q);
+  const int E = lq - 1 - s;                       // floor(log2(v / k))
+  const int ulp = (E < -1022 ? -1022 : E) - 52;  // the result's ulp: 2^ulp
+  const int drop = ulp + s;                       // low bits of q below the ulp (>= 2)
+  uint64_t m = drop >= 64 ? 0ull : q >> drop;
+  const uint64_t rbit = drop - 1 >= 64 ? 0ull : (q >> (drop - 1)) & 1ull;
+  const bool sticky = rem != 0u || (drop - 1 >= 64 ? q != 0ull : (q & ((1ull << (drop - 1)) - 1ull)) != 0ull);
+  if (rbit && (sticky || (m & 1ull))) ++m;
+#ifdef __HIP_DEVICE_COMPILE__
+  return sign * ldexp((double)m, ulp);
+#else
+  return sign * __builtin_ldexp((double)m, ulp);
+#endif
+}
+
+__global__ void __launch_bounds__(256) int_true_div_big_kernel(const uint64_t* __restrict__ x, uint64_t n, KBig kb,
+                                                               double* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = true_div_big(x[2 * i], x[2 * i + 1], kb);
+}
+
+static KBig kbig_of(const uint32_t* k, int k_words, int negative) {
+  KBig kb;
+  memset(&kb, 0, sizeof(kb));
+  kb.negative = negative;
+  int bits = 0;
+  for (int i = k_words - 1; i >= 0; --i)
+    if (k[i]) {
+      bits = 32 * i + 32 - __builtin_clz(k[i]);
+      break;
+    }
+  if (bits > 40 * 32 - 32) {  // > 1 248 bits: every quotient of a v < 2^128 is below 2^-1120
+    kb.zero_all = 1;
+  } else {
+    kb.words = (bits + 31) / 32;
+    for (int i = 0; i < kb.words; ++i) kb.w[i] = k[i];
+    kb.bits = bits;
+  }
+  return kb;
+}
+
+int launch_int_true_div_big(const uint64_t* x, uint64_t n, const uint32_t* k, int k_words, int negative, double* out,
+                            hipStream_t s) {
+  if (n == 0) return FBM_OK;
+  const KBig kb = kbig_of(k, k_words, negative);
+  hipLaunchKernelGGL(int_true_div_big_kernel, grid1(n, 256), dim3(256), 0, s, x, n, kb, out);
+  return check_launch("int_true_div_big_kernel");
+}
+
+void host_true_div_big(const uint64_t* x, uint64_t n, const uint32_t* k, int k_words, int negative, double* out) {
+  const KBig kb = kbig_of(k, k_words, negative);
+  for (uint64_t i = 0; i < n; ++i) out[i] = true_div_big(x[2 * i], x[2 * i + 1], kb);
+}
+
 int launch_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, uint64_t* prod, double* quot, uint32_t* stats,
                    hipStream_t s) {
   if (n == 0) return FBM_OK;

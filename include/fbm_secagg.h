@@ -242,6 +242,13 @@ int fbm_jl_decrypt_with(const uint32_t* cts, int n_parties, uint64_t n_ct, const
  *         correctly rounded, then the IEEE division);
  *   op 3: v / (-k) (k >= 1): op 1 negated.                                                       */
 int fbm_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, void* out, uint32_t* stats, void* stream);
+/* fbm_int_true_div_big (round 4): out[i] = x[i] / k (Python's int / int true division, correctly rounded,
+ * subnormals included) for a divisor of any size -- |k| given as k_words HOST little-endian words,
+ * negative its sign; x as in fbm_int_ops (device u128 pairs), out device float64. */
+int fbm_int_true_div_big(const uint64_t* x, uint64_t n, const uint32_t* k, int k_words, int negative, double* out,
+                         void* stream);
+/* host test hook (no GPU): fbm_int_true_div_big's per-value arithmetic on host arrays. */
+int fbm_test_true_div_big(const uint64_t* x, uint64_t n, const uint32_t* k, int k_words, int negative, double* out);
 
 /* ---- additive secret sharing of vectors (reference fedbiomed/common/secagg/_additive_ss.py) ----
  * fbm_ass_split replaces AdditiveSecret.split / _shares_int (:40-98) for a list secret:

@@ -93,26 +93,93 @@ def test_oracle_jl_rounds(golden):
                 I(c) for c in e]
 
 
+def test_wide_divisor_true_division_host(golden):
+    """fbm_int_true_div_big's per-value arithmetic (host hook fbm_test_true_div_big) against Python's own
+    int / int -- the operation the reference's divide runs (_secagg_utils.py:137-149) -- for v < 2^128 and
+    divisors of 65 ... 1 300 bits of either sign: round half to even, exact quotients, subnormal and zero
+    results, bit for bit; and the fixture's reference outcomes for its wide divisors."""
+    import ctypes
+    import random
+
+    import numpy as np
+
+    from fedbiomed_amd import _native as N
+
+    lib = N.load()
+    rng = random.Random(65)
+
+    def div(vs, k):
+        x = np.array([[v & (2**64 - 1), v >> 64] for v in vs], dtype=np.uint64)
+        kw = max(1, (abs(k).bit_length() + 31) // 32)
+        kl = np.frombuffer(abs(k).to_bytes(4 * kw, "little"), dtype=np.uint32).copy()
+        out = np.zeros(len(vs), dtype=np.float64)
+        rc = lib.fbm_test_true_div_big(ctypes.c_void_p(x.ctypes.data), len(vs), ctypes.c_void_p(kl.ctypes.data), kw,
+                                       1 if k < 0 else 0, ctypes.c_void_p(out.ctypes.data))
+        assert rc == 0, N.last_error()
+        return out.view(np.uint64).tolist()
+
+    vals = [0, 1, 2**128 - 1, 2**64, 3 << 100] + [rng.getrandbits(rng.randrange(1, 129)) for _ in range(200)]
+    divisors = [2**64, 2**64 + 1, 3**41, 2**100, 2**127 - 1, 2**128 + 1, 10**60, 2**1000, 2**1074 + 12345,
+                2**1100 - 1, 2**1180 + 3, 2**1202, 2**1203, 2**1204 + 1, 2**1300]
+    divisors += [rng.getrandbits(rng.randrange(65, 1250)) | (1 << 64) for _ in range(40)]
+    for k in divisors:
+        vs = vals + [k * m for m in (1, 3, 12345) if (k * m).bit_length() <= 128]
+        vs += [k * m + k // 2 for m in (0, 1, 2, 3) if (k * m + k).bit_length() <= 128]  # halfway and near it
+        for sign in (1, -1):
+            want = np.array([v / (sign * k) for v in vs], dtype=np.float64).view(np.uint64).tolist()
+            assert div(vs, sign * k) == want, (k, sign)
+    g = golden["api_edges"]["apply_average"]
+    vals = [I(v) for v in g["vals"]]
+    wide = [c for c in g["cases"] if isinstance(_k(c["k"]), int) and abs(_k(c["k"])) >= 2**64]
+    assert len(wide) >= 12
+    for c in wide:
+        assert div(vals, _k(c["k"])) == _bits([F(v) for v in c["out"]["ok"]]), c["k"]
+
+
 # ------------------------------------------------------------------ GPU
 @pytest.mark.gpu
 def test_apply_average_edges(golden):
     """_apply_average with int divisors of either sign (incl. -2^63 and 2^64 - 1), float divisors (2.5,
-    -2.5, 7.0, 1e-300, inf), zero (both ZeroDivisionErrors): the reference's floats bit for bit.  An
-    integer divisor of 2^64 or more is outside the device path (FB624)."""
-    from fedbiomed_amd.exceptions import FedbiomedSecaggCrypterError
+    -2.5, 7.0, 1e-300, inf), zero (both ZeroDivisionErrors), and (round 4) integer divisors of 2^64 and
+    more -- 2^64 + 1, 10^40, -3^90, 2^1000 + 1, up to 2^1300, whose quotients run into the subnormal
+    range and to zero: the reference's floats bit for bit."""
     from fedbiomed_amd.secagg import SecaggCrypter
 
     g = golden["api_edges"]["apply_average"]
     vals = [I(v) for v in g["vals"]]
     for c in g["cases"]:
         k = _k(c["k"])
-        if isinstance(k, int) and abs(k) >= 2**64:
-            with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
-                SecaggCrypter._apply_average(vals, k)
-            continue
         got = _expect(c["out"], lambda k=k: SecaggCrypter._apply_average(vals, k))
         if got is not None:
             assert _bits(got) == _bits([F(v) for v in c["out"]["ok"]]), c["k"]
+
+
+@pytest.mark.gpu
+def test_wide_divisor_true_division_vs_python():
+    """fbm_int_true_div_big against Python's own int / int (the operation the reference's divide runs,
+    _secagg_utils.py:137-149) on random v < 2^128 and divisors of 65 ... 1 300 bits of either sign,
+    values near halfway cases and exact quotients included: bit-identical float64 results."""
+    import random
+
+    import numpy as np
+    import torch
+
+    from fedbiomed_amd import _device as D
+
+    rng = random.Random(64)
+    vals = [0, 1, 2**128 - 1, 2**64, 3 << 100] + [rng.getrandbits(rng.randrange(1, 129)) for _ in range(300)]
+    divisors = [2**64, 2**64 + 1, 3**41, 2**100, 2**127 - 1, 2**128 + 1, 10**60, 2**1000, 2**1074 + 12345,
+                2**1100 - 1, 2**1180 + 3, 2**1202, 2**1203, 2**1204 + 1]
+    divisors += [rng.getrandbits(rng.randrange(65, 1250)) | (1 << 64) for _ in range(30)]
+    exact = [(d * rng.getrandbits(30), d) for d in divisors[:6] if (d * 3).bit_length() <= 128]
+    for k in divisors:
+        vs = vals + [v for v, d in exact if d == k] + [k * 5 // 2 if (k * 5).bit_length() <= 128 else 1]
+        t = torch.from_numpy(np.array([[v & (2**64 - 1), v >> 64] for v in vs], dtype=np.uint64).view(np.int64)).to(
+            D.device())
+        for sign in (1, -1):
+            got = D.int_true_divide(t, sign * k)
+            want = [v / (sign * k) for v in vs]
+            assert np.array(got).view(np.uint64).tolist() == np.array(want).view(np.uint64).tolist(), (k, sign)
 
 
 @pytest.mark.gpu

@@ -623,7 +623,9 @@ def gen_api_edges(R):
     del ids5
     avg = []
     vals = [0, 1, 5, 2 ** 53 + 1, 2 ** 64 + 3, 2 ** 127 - 1, 10 ** 30 + 7]
-    for k in [2, 7, 2.5, -3, -2.5, 7.0, 1e-300, float("inf"), 2 ** 64 - 1, -(2 ** 63), 0, 0.0, 3 ** 50]:
+    for k in [2, 7, 2.5, -3, -2.5, 7.0, 1e-300, float("inf"), 2 ** 64 - 1, -(2 ** 63), 0, 0.0, 3 ** 50,
+              2 ** 64, -(2 ** 64), 2 ** 64 + 1, 2 ** 100 + 7, 10 ** 40, 2 ** 127 + 5, -(3 ** 90), 2 ** 1000 + 1,
+              2 ** 1100 + 3, 2 ** 1150, 2 ** 1200 - 1, 2 ** 1300]:
         avg.append({"k": repr(k), "out": _outcome(lambda k=k: [fhex(v) for v in Crypter._apply_average(vals, k)])})
     out["apply_average"] = {"vals": [ihex(v) for v in vals], "cases": avg}
     wts = []
