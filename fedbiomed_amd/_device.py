@@ -983,6 +983,44 @@ def jl_pack(vals: torch.Tensor, es: int, cr: int) -> torch.Tensor:
     return pt
 
 
+def _rows_of(vals: List[int], w: int) -> np.ndarray:
+    out = np.zeros((len(vals), w), dtype=np.uint32)
+    for i, v in enumerate(vals):
+        out[i] = int_limbs(v, w)
+    return out
+
+
+def ves_pack_any(V: List[int], es: int, cr: int, dev=None) -> List[int]:
+    """VES.encode of any shape (fbm_ves_pack): non-negative ints of any width, slots of any es, plaintexts
+    of any width; the reference's OR packing (_jls.py:118-144, 169-176)."""
+    dev = dev or device()
+    if not V:
+        return []
+    wv = max(1, (max(v.bit_length() for v in V) + 31) // 32)
+    pw = (es * (cr - 1) + 32 * wv + 31) // 32
+    n_ct = (len(V) + cr - 1) // cr
+    x = torch.from_numpy(_rows_of(V, wv).view(np.int32)).to(dev)
+    pt = torch.empty((n_ct, pw), dtype=torch.int32, device=dev)
+    _call(N.load().fbm_ves_pack, _ptr(x), len(V), wv, es, cr, pw, _ptr(pt), _stream())
+    return limbs_to_ints_w(pt, pw)
+
+
+def ves_unpack_any(E: List[int], es: int, cr: int, v_expected: int, dev=None) -> List[int]:
+    """VES.decode of any shape (fbm_ves_unpack): slot j of each plaintext, (e >> es j) & (2^es - 1), for
+    min(remaining, cr) slots per plaintext (_jls.py:146-167, 179-192); only the low es cr bits of a plaintext
+    are read -- a negative one's two's complement, as Python's shifts and masks see it."""
+    dev = dev or device()
+    n_out = min(int(v_expected), len(E) * cr)
+    if n_out <= 0:
+        return []
+    pw = (es * cr + 31) // 32
+    ow = (es + 31) // 32
+    pts = torch.from_numpy(_rows_of([int(e) & ((1 << (32 * pw)) - 1) for e in E], pw).view(np.int32)).to(dev)
+    vals = torch.empty((n_out, ow), dtype=torch.int32, device=dev)
+    _call(N.load().fbm_ves_unpack, _ptr(pts), len(E), pw, es, cr, n_out, ow, _ptr(vals), _stream())
+    return limbs_to_ints_w(vals, ow)
+
+
 def jl_unpack(pt: torch.Tensor, es: int, cr: int, n_out: int) -> torch.Tensor:
     """VES.decode on the device: int32 [n_ct, 32] limbs -> int64 [n_out, 2] (lo, hi) slot values."""
     n_ct = pt.shape[0]

@@ -90,6 +90,8 @@ SIGNATURES = {
     "fbm_jl_fdh_msg": (c_int, [c_u64, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp]),
     "fbm_int_true_div_big": (c_int, [c_vp, c_u64, c_vp, c_int, c_int, c_vp, c_vp]),
     "fbm_test_true_div_big": (c_int, [c_vp, c_u64, c_vp, c_int, c_int, c_vp]),
+    "fbm_ves_pack": (c_int, [c_vp, c_u64, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    "fbm_ves_unpack": (c_int, [c_vp, c_u64, c_int, c_int, c_int, c_u64, c_int, c_vp, c_vp]),
     "fbm_jl_product": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_decrypt": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp, c_int, c_vp, c_u64, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_powmod": (c_int, [c_vp, c_vp, c_u64, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),

@@ -1835,6 +1835,32 @@ int fbm_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, void* out, ui
   });
 }
 
+int fbm_ves_pack(const uint32_t* x, uint64_t n, int wv, int es, int cr, int pw, uint32_t* pt, void* stream) {
+  if (wv < 1 || es < 1 || cr < 1 || pw < 1 || (int64_t)es * (cr - 1) + 32ll * wv > 32ll * pw) {
+    set_error("fbm_ves_pack: bad shape (wv=%d es=%d cr=%d pw=%d)", wv, es, cr, pw);
+    return FBM_E_ARG;
+  }
+  if (n > 0 && (!x || !pt)) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  return timed("ves_pack", (hipStream_t)stream, [&] { return launch_ves_pack(x, n, wv, es, cr, pw, pt, (hipStream_t)stream); });
+}
+
+int fbm_ves_unpack(const uint32_t* pt, uint64_t n_ct, int pw, int es, int cr, uint64_t n_out, int ow, uint32_t* vals,
+                   void* stream) {
+  if (pw < 1 || es < 1 || cr < 1 || ow < (es + 31) / 32 || (int64_t)es * cr > 32ll * pw || n_out > n_ct * (uint64_t)cr) {
+    set_error("fbm_ves_unpack: bad shape (pw=%d es=%d cr=%d ow=%d)", pw, es, cr, ow);
+    return FBM_E_ARG;
+  }
+  if (n_out > 0 && (!pt || !vals)) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  return timed("ves_unpack", (hipStream_t)stream,
+               [&] { return launch_ves_unpack(pt, pw, es, cr, n_out, ow, vals, (hipStream_t)stream); });
+}
+
 int fbm_int_true_div_big(const uint64_t* x, uint64_t n, const uint32_t* k, int k_words, int negative, double* out,
                          void* stream) {
   hipStream_t s = (hipStream_t)stream;

@@ -183,6 +183,9 @@ int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, int ne
 // (any real biprime), else the sentinel FBM_HC_FULL (8 words of ones) and the whole row in H[k]; Hc ==
 // nullptr: every row whole in H (the generic engine, fbm_jl_fdh)
 int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s, uint32_t* Hc = nullptr);
+// VES of any shape (fbm_ves_pack / fbm_ves_unpack)
+int launch_ves_pack(const uint32_t* x, uint64_t n, int wv, int es, int cr, int pw, uint32_t* pt, hipStream_t s);
+int launch_ves_unpack(const uint32_t* pt, int pw, int es, int cr, uint64_t n_out, int ow, uint32_t* vals, hipStream_t s);
 // FDH.H of any bits_size: one lane per t (tw-word rows), message t.to_bytes(msg_bytes) || counter, r of at
 // most kmax digests (fbm_jl_fdh_msg; r of up to FBM_FDH_MSG_DIGESTS digests, FBM_FDH_MSG_ROW-word rows)
 #define FBM_FDH_MSG_DIGESTS 15

@@ -139,6 +139,49 @@ __global__ void __launch_bounds__(256) jl_pack_wide_kernel(const uint64_t* __res
   }
 }
 
+// VES objects of any shape (round 4; _jls.py:118-192 for element sizes above 100 bits, plaintexts wider
+// than 1024 bits, values of any width): values as wv-word little-endian rows, plaintexts as pw-word rows.
+// Bits [off, off + 32) of a w-word number (off may be negative: the number shifted up by -off).
+__device__ __forceinline__ uint32_t bits32_at(const uint32_t* v, int w, int off) {
+  if (off < 0) return -off < 32 && w > 0 ? v[0] << (-off) : 0u;
+  const int i = off >> 5, b = off & 31;
+  const uint32_t lo = i < w ? v[i] : 0u;
+  const uint32_t hi = b && i + 1 < w ? v[i + 1] : 0u;
+  return b ? (lo >> b) | (hi << (32 - b)) : lo;
+}
+// encode: one thread per plaintext word; slot j's value ORed in at bit es j, its bits past the slot into
+// the next slots (the reference's a |= v << es j)
+__global__ void __launch_bounds__(256) ves_pack_kernel(const uint32_t* __restrict__ x, uint64_t n, int wv, int es,
+                                                       int cr, int pw, uint64_t n_ct, uint32_t* __restrict__ pt) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t ct = gid / (uint64_t)pw;
+  const int L = (int)(gid % (uint64_t)pw);
+  if (ct >= n_ct) return;
+  const uint64_t first = ct * (uint64_t)cr;
+  const int cnt = (n - first) >= (uint64_t)cr ? cr : (int)(n - first);
+  const int64_t lo_bit = 32ll * L;
+  int64_t j0 = lo_bit - 32ll * wv + 1 > 0 ? (lo_bit - 32ll * wv + 1 + es - 1) / es : 0;
+  int64_t j1 = (lo_bit + 31) / es;
+  if (j1 > cnt - 1) j1 = cnt - 1;
+  uint32_t w = 0;
+  for (int64_t j = j0; j <= j1; ++j) w |= bits32_at(x + (first + j) * (uint64_t)wv, wv, (int)(lo_bit - es * j));
+  pt[ct * (uint64_t)pw + L] = w;
+}
+// decode: one thread per output word; value o = slot o % cr of plaintext o / cr, masked to es bits
+__global__ void __launch_bounds__(256) ves_unpack_kernel(const uint32_t* __restrict__ pt, int pw, int es, int cr,
+                                                         uint64_t n_out, int ow, uint32_t* __restrict__ vals) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t o = gid / (uint64_t)ow;
+  const int w = (int)(gid % (uint64_t)ow);
+  if (o >= n_out) return;
+  const uint64_t ct = o / (uint64_t)cr;
+  const int slot = (int)(o % (uint64_t)cr);
+  uint32_t v = bits32_at(pt + ct * (uint64_t)pw, pw, es * slot + 32 * w);
+  const int left = es - 32 * w;  // bits of the value in this word
+  if (left < 32) v = left <= 0 ? 0u : v & ((1u << left) - 1u);
+  vals[o * (uint64_t)ow + w] = v;
+}
+
 #define FBM_QMASK ((1u << FBM_QA_LB) - 1u)  // the 29-bit engines' limb mask
 
 // radix changes between the shared final step's 28-bit limbs and the engines' 29-bit limbs
@@ -1745,6 +1788,21 @@ int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, int ne
   if (n_ct == 0) return FBM_OK;
   hipLaunchKernelGGL(jl_nude_kernel, grid1(n_ct, 256), dim3(256), 0, s, pt, n_ct, jp, negative, nude);
   return check_launch("jl_nude_kernel");
+}
+
+int launch_ves_pack(const uint32_t* x, uint64_t n, int wv, int es, int cr, int pw, uint32_t* pt, hipStream_t s) {
+  const uint64_t n_ct = (n + (uint64_t)cr - 1) / (uint64_t)cr;
+  if (n_ct == 0) return FBM_OK;
+  hipLaunchKernelGGL(ves_pack_kernel, grid1(n_ct * (uint64_t)pw, 256), dim3(256), 0, s, x, n, wv, es, cr, pw, n_ct, pt);
+  return check_launch("ves_pack_kernel");
+}
+
+int launch_ves_unpack(const uint32_t* pt, int pw, int es, int cr, uint64_t n_out, int ow, uint32_t* vals,
+                      hipStream_t s) {
+  if (n_out == 0) return FBM_OK;
+  hipLaunchKernelGGL(ves_unpack_kernel, grid1(n_out * (uint64_t)ow, 256), dim3(256), 0, s, pt, pw, es, cr, n_out, ow,
+                     vals);
+  return check_launch("ves_unpack_kernel");
 }
 
 int launch_jl_fdh_msg(uint64_t n, const uint32_t* t, int tw, int msg_bytes, int kmax, const uint32_t* n32, int even,

@@ -23,8 +23,8 @@ modulus) -- and the exponentiations on the device (fbm_jl_powmod / fbm_jl_decryp
 
 Domain of the device path (FB624 outside it): 1 <= N < 2^1024 (an even N and
 N = 1 run on the generic engine, fedbiomed_amd/csrc/fbm_gen.hip, an odd one on the Montgomery engines);
-FDH of bits_size 2048; tau in [0, 2^8192) where FDH hashes it (ABI 3); VES values in [0, 2^128) with
-es <= 100; ServerKey.decrypt with delta^2 = 1 (mod N).  Integers are Python ints (gmpy2 is
+FDH of any bits_size (an r of up to 15 digests); tau in [0, 2^8192) where FDH hashes it (ABI 3); VES
+values >= 0 of any width, any slot and plaintext size (round 4); ServerKey.decrypt with delta^2 = 1 (mod N).  Integers are Python ints (gmpy2 is
 not a dependency): where the reference returns gmpy2.mpz this returns int, and FDH takes an
 int modulus.
 """
@@ -67,26 +67,32 @@ class VES:
 
     def _slot(self, add_ops: int) -> Tuple[int, int]:
         es, cr = self._get_elements_size_and_compression_ratio(add_ops)
-        if cr < 1 or es > 100 or es * cr > 1024:
-            raise _unsupported(f"VES slot of {es} bits x {cr} (ptsize {self._ptsize})")
+        if cr < 1:  # the reference then packs every value into one plaintext (its bs never reaches 0)
+            raise _unsupported(f"VES slot of {es} bits in a {self._ptsize}-bit plaintext")
         return es, cr
 
     def encode(self, V: List[int], add_ops: int) -> List[int]:
-        """reference _jls.py:118-144 (OR packing, _batch :169-176) -- fbm_jl_pack."""
+        """reference _jls.py:118-144 (OR packing, _batch :169-176) -- fbm_jl_pack for the crypter's shape
+        (es <= 100, es * cr <= 1024, values < 2^128), fbm_ves_pack for any other (round 4)."""
         es, cr = self._slot(add_ops)
         if not V:
             return []
-        pt = D.jl_pack(D.ints_to_u128(V), es, cr)
-        return D.limbs_to_ints_w(pt, 32)
+        if es <= 100 and es * cr <= 1024 and all(0 <= v < 2**128 for v in V):
+            pt = D.jl_pack(D.ints_to_u128(V), es, cr)
+            return D.limbs_to_ints_w(pt, 32)
+        if any(operator.index(v) < 0 for v in V):
+            raise _unsupported("VES.encode of negative values")
+        return D.ves_pack_any([operator.index(v) for v in V], es, cr)
 
     def decode(self, E: List[int], add_ops: int, v_expected: int) -> List[int]:
         """reference _jls.py:146-167 (_debatch :179-192): slot j = (e >> es*j) & (2^es - 1),
-        min(remaining, comp_ratio) values per plaintext -- fbm_jl_unpack."""
+        min(remaining, comp_ratio) values per plaintext -- fbm_jl_unpack for the crypter's shape,
+        fbm_ves_unpack for any other (round 4)."""
         es, cr = self._slot(add_ops)
-        if es > 128:
-            raise _unsupported(f"VES decode of {es}-bit slots")
         if not E or v_expected <= 0:
             return []
+        if es > 128 or es * cr > 1024:
+            return D.ves_unpack_any([int(e) for e in E], es, cr, v_expected)
         # only the low es*cr <= 1024 bits of a plaintext are read: two's-complement truncation
         pts = D.ints_to_pt([int(e) & ((1 << 1024) - 1) for e in E], 1 << 1024)
         return D.u128_to_ints(D.jl_unpack(pts, es, cr, v_expected))
@@ -379,6 +385,10 @@ class JoyeLibert:
         if not x_u_tau:
             return []
         n = _modulus_of(user_key.public_param)
+        if es > 100 or es * cr > 1024 or not all(0 <= v < 2**128 for v in x_u_tau):
+            # a VES shape outside the fused kernels' (a target range past 2^83, values of 2^128 and more):
+            # the reference's two steps, VES.encode then UserKey.encrypt, each on the device
+            return user_key.encrypt(self._vector_encoder.encode(x_u_tau, n_users), tau)
         if not _fdh_standard(user_key.public_param):  # VES on the device, the caller's hashes, fbm_jl_powmod
             _check_hash_domain(user_key.public_param)
             pt = D.jl_pack(D.ints_to_u128(x_u_tau), es, cr)
@@ -412,8 +422,8 @@ class JoyeLibert:
         else:
             _check_hash_domain(sk_0.public_param)
         es, cr = self._vector_encoder._slot(n_user)
-        if es > 128:
-            raise _unsupported(f"VES decode of {es}-bit slots")
+        if es > 128 or es * cr > 1024:  # the reference's two steps, ServerKey.decrypt then VES.decode
+            return self._vector_encoder.decode(sk_0.decrypt(summed, tau), n_user, num_expected_params)
         rows = _term_rows(summed, n)
         factor = None if standard else D.jl_powmod(_bases(sk_0, tau, len(summed), n), n, sk_0.key)
         _, sums = D.jl_aggregate(rows, n, sk_0.key, tau, num_expected_params, 1, want_out=False, want_sums=True,

@@ -247,6 +247,14 @@ int fbm_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, void* out, ui
  * negative its sign; x as in fbm_int_ops (device u128 pairs), out device float64. */
 int fbm_int_true_div_big(const uint64_t* x, uint64_t n, const uint32_t* k, int k_words, int negative, double* out,
                          void* stream);
+/* VES objects of any shape (round 4; reference _jls.py:118-192): fbm_ves_pack ORs value j of each group
+ * of cr into its plaintext at bit es * j (values: n rows of wv little-endian words, device; bits past the
+ * slot land in the next slots, as the reference's a |= v << es j; pt: ceil(n / cr) rows of pw words with
+ * es (cr - 1) + 32 wv <= 32 pw); fbm_ves_unpack writes value o = bits [es (o % cr), + es) of plaintext
+ * o / cr (pt: n_ct rows of pw words, es cr <= 32 pw) as rows of ow >= ceil(es / 32) words. */
+int fbm_ves_pack(const uint32_t* x, uint64_t n, int wv, int es, int cr, int pw, uint32_t* pt, void* stream);
+int fbm_ves_unpack(const uint32_t* pt, uint64_t n_ct, int pw, int es, int cr, uint64_t n_out, int ow, uint32_t* vals,
+                   void* stream);
 /* host test hook (no GPU): fbm_int_true_div_big's per-value arithmetic on host arrays. */
 int fbm_test_true_div_big(const uint64_t* x, uint64_t n, const uint32_t* k, int k_words, int negative, double* out);
 

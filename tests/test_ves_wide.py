@@ -1,0 +1,72 @@
+"""VES objects of any shape (round 4): element sizes above 100 bits, plaintexts wider than 1024 bits,
+values of 2^128 and more (wider than their slot too), decode of plaintexts of any width.
+
+The reference's VES (`_jls.py:76-192`) packs with a |= v << es j and unpacks with (e >> es j) & mask on
+Python ints of any size.  The crypter's shape (es <= 100, es cr <= 1024, values < 2^128) is packed inside
+the encrypt kernels.  Any other shape runs on `ves_pack_kernel` / `ves_unpack_kernel` (fbm_ves_pack /
+fbm_ves_unpack), one thread per output word.  Fixture: tests/golden/ves_wide.json (tools/gen_golden.py
+gen_ves_wide, the reference's outputs).
+"""
+
+import pytest
+
+from oracle import secagg_oracle as O
+from tests.golden_util import I, load
+
+
+@pytest.fixture(scope="module")
+def vw():
+    return load("ves_wide.json")
+
+
+def test_ves_wide_oracle_vs_fixture(vw):
+    """The oracle's VES restatement (any shape) against the reference's encodings and decodings."""
+    for c in vw:
+        es, cr = c["es"], c["cr"]
+        V, E = [I(v) for v in c["V"]], [I(e) for e in c["E"]]
+        assert O.ves_encode(V, es, cr) == E
+        for d in c["decode"]:
+            src = [I(e) for e in d["E"]] if "E" in d else E
+            assert O.ves_decode(src, es, cr, d["v_expected"]) == [I(v) for v in d["out"]["ok"]]
+
+
+@pytest.mark.gpu
+def test_ves_wide_device_vs_fixture(vw):
+    """VES(ptsize, valuesize).encode / decode on the device for every fixture shape (es 31 ... 1 023 bits,
+    cr 1 ... 60, plaintexts of 300 ... 4 096 bits, values up to 2 es + 7 bits): the reference's ints."""
+    from fedbiomed_amd.secagg._jls import VES
+
+    for c in vw:
+        ves = VES(c["ptsize"], c["valuesize"])
+        V, E = [I(v) for v in c["V"]], [I(e) for e in c["E"]]
+        assert ves.encode(V, c["add_ops"]) == E, (c["ptsize"], c["valuesize"])
+        for d in c["decode"]:
+            src = [I(e) for e in d["E"]] if "E" in d else E
+            assert ves.decode(src, c["add_ops"], d["v_expected"]) == [I(v) for v in d["out"]["ok"]], d["v_expected"]
+
+
+@pytest.mark.gpu
+def test_joye_libert_wide_target_round_trip():
+    """JoyeLibert with a target range past the fused kernels' slot (es > 100 bits): protect, aggregate of
+    three users' vectors and the exact column sums back (the reference's VES.encode -> UserKey.encrypt and
+    ServerKey.decrypt -> VES.decode, each on the device), against the oracle's ciphertexts."""
+    import random
+
+    from fedbiomed_amd import workload as W
+    from fedbiomed_amd.secagg._jls import EncryptedNumber, JoyeLibert, ServerKey, UserKey
+    from tests.test_jls_api import pp_of
+
+    rng = random.Random(77)
+    jl = JoyeLibert(target_range=2**150)
+    es, cr = jl._vector_encoder._get_elements_size_and_compression_ratio(3)
+    assert es > 100
+    n = W.BIPRIME0
+    pp = pp_of(n)
+    keys = [rng.getrandbits(2040) for _ in range(3)]
+    xs = [[rng.getrandbits(150) for _ in range(2 * cr + 1)] for _ in range(3)]
+    cts = [jl.protect(pp, UserKey(pp, k), 5, x, 3) for k, x in zip(keys, xs)]
+    want = [O.jl_user_encrypt(O.ves_encode(x, es, cr), 5, k, n) for k, x in zip(keys, xs)]
+    assert cts == want
+    enc = [[EncryptedNumber(pp, c) for c in row] for row in cts]
+    sums = jl.aggregate(ServerKey(pp, -sum(keys)), 5, enc, len(xs[0]))
+    assert sums == [sum(col) for col in zip(*xs)]

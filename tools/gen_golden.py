@@ -869,6 +869,36 @@ def gen_fdh_bits(R):
                                                                 "ct": [ihex(c) for c in cts], "dec": dec}})
 
 
+def gen_ves_wide(R):
+    """VES objects outside the crypter's shape (ves_wide.json): element sizes above 100 bits, plaintexts
+    wider than 1024 bits (ptsize up to 4096), values of 2^128 and more -- wider than their slot too, whose
+    high bits the reference ORs into the next slots -- and decode of plaintexts of any width (negative
+    ones: Python's shifts and masks act on the two's complement)."""
+    jls = R.jls
+    rng = random.Random(4096)
+    out = []
+    for ptsize, valuesize, add_ops in [(1024, 120, 1), (1024, 300, 0), (2048, 100, 7), (2048, 500, 3), (4096, 1000, 1),
+                                       (4096, 64, 15), (300, 40, 2), (1024, 1023, 0), (3000, 129, 1), (1024, 30, 1)]:
+        ves = jls.VES(ptsize, valuesize)
+        es, cr = ves._get_elements_size_and_compression_ratio(add_ops)
+        for n, wmax in ((1, es), (cr, es), (2 * cr + 1, es), (3 * cr - 1, es + 40), (cr + 2, 2 * es + 7)):
+            V = [rng.getrandbits(rng.randrange(1, wmax + 1)) for _ in range(n)]
+            if n > 1:
+                V[0] = (1 << es) - 1
+                V[-1] = 0
+            E = [int(e) for e in ves.encode(V, add_ops)]
+            cases = []
+            for v_exp in (n, max(0, n - 1), n + 5, 1):
+                cases.append({"v_expected": v_exp, "out": _outcome(lambda v_exp=v_exp: [
+                    ihex(v) for v in ves.decode(E, add_ops, v_exp)])})
+            neg = [-e - 1 for e in E[:2]] + [-(1 << (ptsize + 3)) + 12345]
+            cases.append({"E": [ihex(e) for e in neg], "v_expected": 2 * cr,
+                          "out": _outcome(lambda neg=neg: [ihex(v) for v in ves.decode(neg, add_ops, 2 * cr)])})
+            out.append({"ptsize": ptsize, "valuesize": valuesize, "add_ops": add_ops, "es": es, "cr": cr,
+                        "V": [ihex(v) for v in V], "E": [ihex(e) for e in E], "decode": cases})
+    dump("ves_wide.json", out)
+
+
 def I(s):  # noqa: E743 - hex string -> int (the fixtures' encoding)
     return int(s, 16)
 
@@ -899,6 +929,9 @@ def main():
     if sys.argv[1:] == ["fdh_bits"]:
         gen_fdh_bits(R)
         return
+    if sys.argv[1:] == ["ves_wide"]:
+        gen_ves_wide(R)
+        return
     gen_quantize(R)
     gen_lom(R)
     gen_jl(R)
@@ -913,6 +946,7 @@ def main():
     gen_caller_flows(R)
     gen_n_one(R)
     gen_fdh_bits(R)
+    gen_ves_wide(R)
     meta = {"generator": "tools/gen_golden.py", "reference": load_reference.REF,
             "note": "outputs of the reference Fed-BioMed crypter (Python), imported via tools/refshim"}
     dump("meta.json", meta)
