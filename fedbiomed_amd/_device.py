@@ -1068,7 +1068,6 @@ def jl_fdh(n_ct: int, modulus: int, tau: int, ct_offset: int = 0, dev=None) -> t
 def jl_fdh_msg(ts: List[int], bits_size: int, modulus: int, dev=None) -> torch.Tensor:
     """FDH(bits_size, modulus).H(t) for each t (any bits_size; fbm_jl_fdh_msg) -> int32 [len(ts), 128] limbs.
     The reference's to_bytes errors are raised here first: t < 0 and t >= 2^(8 (bits_size // 2))."""
-    dev = dev or device()
     L = bits_size // 2
     if L < 0:
         raise ValueError("length argument must be non-negative")
@@ -1077,6 +1076,7 @@ def jl_fdh_msg(ts: List[int], bits_size: int, modulus: int, dev=None) -> torch.T
             raise OverflowError("can't convert negative int to unsigned")
         if t.bit_length() > 8 * L:
             raise OverflowError("int too big to convert")
+    dev = dev or device()
     tw = max(1, (L + 3) // 4)
     host = np.zeros((len(ts), tw), dtype=np.uint32)
     for i, t in enumerate(ts):

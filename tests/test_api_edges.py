@@ -171,7 +171,7 @@ def test_wide_divisor_true_division_vs_python():
     divisors = [2**64, 2**64 + 1, 3**41, 2**100, 2**127 - 1, 2**128 + 1, 10**60, 2**1000, 2**1074 + 12345,
                 2**1100 - 1, 2**1180 + 3, 2**1202, 2**1203, 2**1204 + 1]
     divisors += [rng.getrandbits(rng.randrange(65, 1250)) | (1 << 64) for _ in range(30)]
-    exact = [(d * rng.getrandbits(30), d) for d in divisors[:6] if (d * 3).bit_length() <= 128]
+    exact = [(v, d) for v, d in ((d * rng.getrandbits(30), d) for d in divisors[:6]) if v.bit_length() <= 128]
     for k in divisors:
         vs = vals + [v for v, d in exact if d == k] + [k * 5 // 2 if (k * 5).bit_length() <= 128 else 1]
         t = torch.from_numpy(np.array([[v & (2**64 - 1), v >> 64] for v in vs], dtype=np.uint64).view(np.int64)).to(
