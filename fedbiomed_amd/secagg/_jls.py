@@ -77,8 +77,9 @@ class VES:
         es, cr = self._slot(add_ops)
         if not V:
             return []
-        if es <= 100 and es * cr <= 1024 and all(0 <= v < 2**128 for v in V):
-            pt = D.jl_pack(D.ints_to_u128(V), es, cr)
+        wmax = max(operator.index(v).bit_length() for v in V)
+        if es <= 100 and es * cr <= 1024 and wmax <= 128 and es * (cr - 1) + wmax <= 1024 and min(V) >= 0:
+            pt = D.jl_pack(D.ints_to_u128(V), es, cr)  # (no bit of any plaintext past 2^1024)
             return D.limbs_to_ints_w(pt, 32)
         if any(operator.index(v) < 0 for v in V):
             raise _unsupported("VES.encode of negative values")
@@ -385,7 +386,8 @@ class JoyeLibert:
         if not x_u_tau:
             return []
         n = _modulus_of(user_key.public_param)
-        if es > 100 or es * cr > 1024 or not all(0 <= v < 2**128 for v in x_u_tau):
+        wmax = max(operator.index(v).bit_length() for v in x_u_tau)
+        if es > 100 or es * cr > 1024 or wmax > 128 or es * (cr - 1) + wmax > 1024 or min(x_u_tau) < 0:
             # a VES shape outside the fused kernels' (a target range past 2^83, values of 2^128 and more):
             # the reference's two steps, VES.encode then UserKey.encrypt, each on the device
             return user_key.encrypt(self._vector_encoder.encode(x_u_tau, n_users), tau)
@@ -457,6 +459,6 @@ class FDH:
         fbm_jl_fdh_msg at any other bits_size (round 4)."""
         if self.bits_size != SAParameters.KEY_SIZE:
             h = D.jl_fdh_msg([operator.index(t)], self.bits_size, int(self._n_modules))
-            return D.limbs_to_ints(D.to_host(h).numpy())[0]
+            return D.limbs_to_ints_w(h, h.shape[1])[0]  # (128-word rows: r of up to 15 digests)
         t = _check_tau(t)  # int(t).to_bytes(1024, ...)'s OverflowError outside [0, 2^8192) (_jls.py:747)
         return self._hash_range(t, 1, 0)[0]
