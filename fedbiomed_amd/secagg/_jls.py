@@ -143,14 +143,6 @@ def _fdh_standard(pp: PublicParam) -> bool:
             and int(fdh._n_modules) == int(pp.n_modulus) ** 2 and pp.bits == _TAU_SHIFT_BITS)
 
 
-def _check_hash_domain(pp: PublicParam) -> None:
-    """FDH hashes on the device at bits_size 2048 only (FB624 before any device work otherwise)."""
-    fdh = getattr(pp._hashing_function, "__self__", None)
-    if (isinstance(fdh, FDH) and getattr(pp._hashing_function, "__func__", None) is FDH.H
-            and fdh.bits_size != SAParameters.KEY_SIZE):
-        raise _unsupported(f"FDH of bits_size {fdh.bits_size} (device path: {SAParameters.KEY_SIZE})")
-
-
 def _bases(key: "BaseKey", tau, len_: int, n: int) -> torch.Tensor:
     """Any other hashing function: BaseKey._populate_tau's values (the callable per t on the host, as
     the reference calls it, or one fbm_jl_fdh launch for an FDH of another modulus) as device limbs of
@@ -316,7 +308,6 @@ class UserKey(BaseKey):
             return []
         n = _modulus_of(self._public_param)
         if not _fdh_standard(self._public_param):  # the caller's hashing function, then fbm_jl_powmod
-            _check_hash_domain(self._public_param)
             pts = D.ints_to_pt(plaintext, n)
             ct = D.jl_powmod(_bases(self, tau, len(plaintext), n), n, self._key, pts)
             return D.limbs_to_ints(D.to_host(ct).numpy())
@@ -348,7 +339,6 @@ class ServerKey(BaseKey):
         if d2 % n != 1:
             raise _unsupported("ServerKey.decrypt with delta^2 != 1 (mod N)")
         if not _fdh_standard(self._public_param):  # fbm_jl_powmod's factor, then fbm_jl_decrypt_with
-            _check_hash_domain(self._public_param)
             rows = _term_rows(cipher, n)
             factor = D.jl_powmod(_bases(self, tau, len(cipher), n), n, d2 * self._key)
             return D.limbs_to_ints_w(D.jl_decrypt_with(rows, n, factor), 32)
@@ -392,7 +382,6 @@ class JoyeLibert:
             # the reference's two steps, VES.encode then UserKey.encrypt, each on the device
             return user_key.encrypt(self._vector_encoder.encode(x_u_tau, n_users), tau)
         if not _fdh_standard(user_key.public_param):  # VES on the device, the caller's hashes, fbm_jl_powmod
-            _check_hash_domain(user_key.public_param)
             pt = D.jl_pack(D.ints_to_u128(x_u_tau), es, cr)
             ct = D.jl_powmod(_bases(user_key, tau, pt.shape[0], n), n, user_key.key, pt)
             return D.limbs_to_ints(D.to_host(ct).numpy())
@@ -421,8 +410,6 @@ class JoyeLibert:
         standard = _fdh_standard(sk_0.public_param)
         if standard:
             tau = _check_tau(tau)
-        else:
-            _check_hash_domain(sk_0.public_param)
         es, cr = self._vector_encoder._slot(n_user)
         if es > 128 or es * cr > 1024:  # the reference's two steps, ServerKey.decrypt then VES.decode
             return self._vector_encoder.decode(sk_0.decrypt(summed, tau), n_user, num_expected_params)

@@ -9,7 +9,6 @@ t), positive and negative keys (tools/gen_golden.py gen_custom_hash)."""
 
 import pytest
 
-from fedbiomed_amd.exceptions import FedbiomedSecaggCrypterError
 from fedbiomed_amd.secagg._jls import FDH, EncryptedNumber, JoyeLibert, PublicParam, ServerKey, UserKey
 from oracle import secagg_oracle as O
 from tests.golden_util import I, custom_hashes
@@ -47,15 +46,17 @@ def test_oracle_matches_reference_fixture(golden):
             assert got == [(a + b) % n for a, b in zip(pts, pts2)]
 
 
-def test_fdh_of_another_bits_size_is_outside_the_device_path():
-    """An FDH of bits_size other than 2048 hashes on the device only at 2048 bits: FB624, before any
-    device work."""
-    n = 123457
-    pp = PublicParam(n, 1024, FDH(1024, n * n).H)
-    with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
-        UserKey(pp, 3).encrypt([1], 1)
-    with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
-        ServerKey(pp, -3).decrypt([EncryptedNumber(pp, 5)], 1)
+def test_fdh_of_another_bits_size_checks_its_message_on_the_host():
+    """FDH of bits_size other than 2048 runs on the device since round 4 (tests/test_fdh_bits.py); its
+    to_bytes errors come first, on the host, as the reference's int(t).to_bytes(bits_size // 2) raises them
+    (messages pinned in tests/golden/fdh_bits.json)."""
+    f = FDH(1024, 123457 ** 2)
+    with pytest.raises(OverflowError, match="can't convert negative int to unsigned"):
+        f.H(-1)
+    with pytest.raises(OverflowError, match="int too big to convert"):
+        f.H(1 << (8 * 512))
+    with pytest.raises(ValueError, match="length argument must be non-negative"):
+        FDH(-2, 7).H(1)
 
 
 # ------------------------------------------------------------------ GPU: the device path against the reference
