@@ -434,8 +434,10 @@ class FDH:
     def _hash_range(self, tau: int, len_: int, k0: int = 0) -> List[int]:
         if len_ <= 0:
             return []
-        if self.bits_size != SAParameters.KEY_SIZE:
-            raise _unsupported(f"FDH of bits_size {self.bits_size} (device path: {SAParameters.KEY_SIZE})")
+        if self.bits_size != SAParameters.KEY_SIZE:  # every t_k = (k << 512) | tau in one fbm_jl_fdh_msg launch
+            ts = [((k0 + k) << (_TAU_SHIFT_BITS // 2)) | operator.index(tau) for k in range(len_)]
+            h = D.jl_fdh_msg(ts, self.bits_size, int(self._n_modules))
+            return D.limbs_to_ints_w(h, h.shape[1])
         tau = _check_tau(tau)
         h = D.jl_fdh(len_, int(self._n_modules), tau, k0)
         return D.limbs_to_ints(D.to_host(h).numpy())
