@@ -1181,6 +1181,12 @@ int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t tot
   return timed("lom_aggregate", s, [&] { return launch_lom_aggregate(y, n_parties, n, total_weight, neg_clip, step, out, sums, stats, s); });
 }
 
+// FBM_COMPACT_H=0 (A/B runs): whole 256-byte H rows for every engine, as before round 4
+static bool jl_compact_h() {
+  static const bool on = !(getenv("FBM_COMPACT_H") && !strcmp(getenv("FBM_COMPACT_H"), "0"));
+  return on;
+}
+
 // encrypt workspace: ops | cst | pt [n_ct][32] | nude (blocked) | H [n_ct][64] | table |
 //                    H^-1 [n_ct][64] + y [n_ct][32] (negative keys) | Hc [n_ct][8] (compact H rows)
 uint64_t fbm_jl_encrypt_workspace(uint64_t n_ct) {
@@ -1305,7 +1311,7 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
   off += align256(n_ct * 64 * 4);
   uint32_t* Y = (uint32_t*)(ws + off);
   off += align256(n_ct * 32 * 4);
-  uint32_t* Hc = (uint32_t*)(ws + off);  // compact H rows: 32 B per ciphertext (one FDH digest)
+  uint32_t* Hc = jl_compact_h() ? (uint32_t*)(ws + off) : nullptr;  // compact H rows: 32 B per ciphertext
   const bool inverse = key_negative && !is_zero;
   if (phase & 1) {
     if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s, shq ? &sh : nullptr); })))
@@ -1387,7 +1393,7 @@ static JlAggWs agg_ws(void* workspace, uint64_t n_ct) {
   off += align256(n_ct * 32 * 4);
   w.table = (uint32_t*)(ws + off);
   off += align256(jl_table_bytes(n_ct));
-  w.Hc = (uint32_t*)(ws + off);
+  w.Hc = jl_compact_h() ? (uint32_t*)(ws + off) : nullptr;
   return w;
 }
 

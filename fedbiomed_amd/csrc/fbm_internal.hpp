@@ -78,7 +78,13 @@ int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t 
 // column 1 (limb k at word k*256) and R^(P+1) mod M (the aggregate's uniform first operand,
 // written by jl_rk_kernel: P parties + the factor leave the product at the plain value)
 // jl_nude_kernel's rows per 256-ciphertext block: digit 1 of (1, pt) only (fbm_na_mm_nude)
+#ifdef FBM_NUDE_BOTH_DIGITS  // A/B variant: both digits stored (72 rows), as before round 4
+#define FBM_NUDE_ROWS 72
+#define FBM_NUDE_D1 36       // digit 1's first row
+#else
 #define FBM_NUDE_ROWS 36
+#define FBM_NUDE_D1 0
+#endif
 #define FBM_CST_M 0
 #define FBM_CST_CTR 120  // exp-kernel chunk counter (in M's padding; zeroed by jl_setup_kernel)
 #define FBM_CST_R2 128

@@ -212,7 +212,7 @@ __device__ __forceinline__ void relimb_28_29(const uint32_t* x, uint32_t* o) {  
 // negative != 0 (a negative weight, see jl_pack_kernel): pt holds |pt| and N*pt + 1 is
 // (1, M - |pt|) with M = N * 2^(1036 - bits(N)) = 0 (mod N): 2^1035 <= M < R, so the digit is
 // non-negative and below R for every |pt| < 2^1024.
-static_assert(FBM_NUDE_ROWS == FBM_QA_L, "jl_nude_kernel stores digit 1's 29-bit limbs");
+static_assert(FBM_NUDE_ROWS == FBM_NUDE_D1 + FBM_QA_L, "jl_nude_kernel stores digit 1's 29-bit limbs");
 __global__ void __launch_bounds__(256) jl_nude_kernel(const uint32_t* __restrict__ pt, uint64_t n_ct, JlParams jp,
                                                       int negative, uint32_t* __restrict__ nude) {
   const uint64_t ct = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -240,8 +240,12 @@ __global__ void __launch_bounds__(256) jl_nude_kernel(const uint32_t* __restrict
   uint32_t p29[FBM_QA_L];
   relimb_28_29(p28, p29);
   uint32_t* dst = launder_v(nude + (ct >> 8) * (FBM_NUDE_ROWS * 256) + (ct & 255));
+#ifdef FBM_NUDE_BOTH_DIGITS
 #pragma unroll
-  for (int k = 0; k < FBM_QA_L; ++k) dst[k * 256] = p29[k];
+  for (int k = 0; k < FBM_QA_L; ++k) dst[k * 256] = k == 0 ? 1u : 0u;
+#endif
+#pragma unroll
+  for (int k = 0; k < FBM_QA_L; ++k) dst[(FBM_NUDE_D1 + k) * 256] = p29[k];
 }
 
 // ------------------------------------------------------------------------------------
@@ -949,7 +953,11 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
     if ((mode & FBM_EXP_DEC) == 0) {  // x nude = (1, pt): jl_nude_kernel's 29-bit blocked column, read in place
       // (a chunk is one 256-ciphertext block: its base is uniform, the lane's offset is tid)
       const uint32_t* nb = SEG(nude, nude_a) + uniform_val((uint64_t)(ct >> 8)) * (FBM_NUDE_ROWS * 256);
+#ifdef FBM_NUDE_BOTH_DIGITS
+      fbm_na_mm_glb(aoff, nb, (uint32_t)(ct & 255) * 4u, NK, np);
+#else
       fbm_na_mm_nude(aoff, nb, (uint32_t)(ct & 255) * 4u, NK, np);
+#endif
     } else {
       fbm_na_mm_glb(aoff, cst + FBM_CST_ONE, 0u, NK, np);
     }
@@ -1271,7 +1279,7 @@ __global__ void __launch_bounds__(FBM_QBLOCK, FBM_GROUP_WAVES) jl_expg_kernel(co
           uint32_t v = 0;
           if (dummy) {
           } else if ((mode & FBM_EXP_DEC) == 0) {
-            v = d == 0 ? (k == 0 ? 1u : 0u) : nb[k * 256];  // (1, pt): jl_nude_kernel's 29-bit rows of pt
+            v = d == 0 ? (k == 0 ? 1u : 0u) : nb[(FBM_NUDE_D1 + k) * 256];  // (1, pt): jl_nude_kernel's rows of pt
           } else {
             v = (d == 0 && k == 0) ? 1u : 0u;
           }
@@ -1640,7 +1648,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_lift_kernel(uint64_t n_ct, Jl
     uint32_t p28[FBM_NLN], p29[FBM_QA_L];
     const uint32_t* nb = nude + (ct >> 8) * (FBM_NUDE_ROWS * 256) + (ct & 255);
 #pragma unroll
-    for (int k = 0; k < FBM_QA_L; ++k) p29[k] = nb[k * 256];  // jl_nude_kernel's 29-bit digit 1
+    for (int k = 0; k < FBM_QA_L; ++k) p29[k] = nb[(FBM_NUDE_D1 + k) * 256];  // jl_nude_kernel's 29-bit digit 1
     relimb_29_28(p29, p28);
     mont_mul(p28, lds, ls, mn);  // p y
     uint32_t c = 0;
