@@ -491,15 +491,25 @@ __global__ void __launch_bounds__(256) jl_fdh_kernel(uint64_t n_ct, JlParams jp,
 // ciphertext ct's H row (64 words) from the compact rows Hc (launch_jl_fdh) or, behind the sentinel / with
 // no compact rows, from H
 __device__ __forceinline__ void load_h(const uint32_t* H, const uint32_t* Hc, uint64_t ct, uint32_t (&h)[64]) {
-  if (Hc) {
+  if (Hc) {  // (uniform)
     const uint4* c = reinterpret_cast<const uint4*>(Hc + ct * 8);
     const uint4 a = c[0], b = c[1];
-    if ((a.x & a.y & a.z & a.w & b.x & b.y & b.z & b.w) != ~0u) {
-      h[0] = a.x; h[1] = a.y; h[2] = a.z; h[3] = a.w; h[4] = b.x; h[5] = b.y; h[6] = b.z; h[7] = b.w;
+    const bool full = (a.x & a.y & a.z & a.w & b.x & b.y & b.z & b.w) == ~0u;
+    h[0] = a.x; h[1] = a.y; h[2] = a.z; h[3] = a.w; h[4] = b.x; h[5] = b.y; h[6] = b.z; h[7] = b.w;
 #pragma unroll
-      for (int i = 8; i < 64; ++i) h[i] = 0u;
-      return;
+    for (int i = 8; i < 64; ++i) h[i] = 0u;
+    if (__any(full)) {  // wave-uniform (FDH retries: small moduli only): whole rows behind the sentinel
+      const uint4* s = reinterpret_cast<const uint4*>(H + ct * 64);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint4 v = s[i];
+        h[4 * i] = full ? v.x : h[4 * i];
+        h[4 * i + 1] = full ? v.y : h[4 * i + 1];
+        h[4 * i + 2] = full ? v.z : h[4 * i + 2];
+        h[4 * i + 3] = full ? v.w : h[4 * i + 3];
+      }
     }
+    return;
   }
   const uint4* s = reinterpret_cast<const uint4*>(H + ct * 64);
 #pragma unroll
@@ -849,7 +859,11 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
 #pragma unroll
         for (int i = 0; i < 64; ++i) h[i] = i == 0 ? 1u : 0u;
       } else {
+#ifdef FBM_EXP_FULL_H_LOAD  // (A/B variant: the round-3 whole-row load)
+        load_row64(SEG(H, H_a) + ct * 64, h);
+#else
         load_h(SEG(H, H_a), SEG(Hc, Hc_a), ct, h);
+#endif
       }
       uint32_t h29[2 * NA];
       {  // h = h_lo + h_hi R: the 72-limb decomposition is (h_lo, h_hi)
@@ -900,7 +914,11 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_exp_kernel(const uint32_t* __
       fbm_na_mm_glb(aoff, table, tb0 + FBM_TSCRATCH * tstride, NK, np);  // h_hi*R^2 (wide lanes)
       lds_to_glb(lds, table + (tb0 + tstride) / 4);
       uint32_t h[64];
+#ifdef FBM_EXP_FULL_H_LOAD  // (A/B variant: the round-3 whole-row load)
+      load_row64(SEG(H, H_a) + ct * 64, h);
+#else
       load_h(SEG(H, H_a), SEG(Hc, Hc_a), ct, h);
+#endif
       uint32_t h29[2 * NA];
       to29_row64(h, h29);
 #pragma unroll
