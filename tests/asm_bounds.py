@@ -150,6 +150,9 @@ class BoundLane:
             return
         if op == "v_and_b32":
             a, b = g(ops[1]), g(ops[2])
+            if a[0] != a[1] and b[0] != b[1]:  # a lane-dependent mask (%[mq]): below both
+                self.put(ops[0], (0, min(a[1], b[1])))
+                return
             mask, val = (a, b) if a[0] == a[1] and (b[0] != b[1] or a[0] & (a[0] + 1) == 0) else (b, a)
             mk = mask[0]
             assert mask[0] == mask[1]
@@ -208,6 +211,12 @@ class BoundLane:
                 mk = g(ops[2])
                 self._conc(mk, "DPP mask")
                 self.put(ops[0], (0, min(src[1], mk[0])))
+            return
+        if op == "v_add_u32_dpp":  # the triple's DPP broadcast (gen_quad_asm.dpp_bcast): a sum over a group's
+            # lanes of a digit masked with %[mq], nonzero in the group's lane 0 only -- so the sum is one lane's
+            # value and stays inside the larger hull (asm_sim checks the values lane by lane)
+            a, b = g(ops[1]), g(ops[2])
+            self.put(ops[0], (0, max(a[1], b[1])))
             return
         if op == "ds_bpermute_b32":
             src = g(ops[2])

@@ -279,6 +279,8 @@ class Wave:
                     vals = src
                 elif op == "v_and_b32_dpp":
                     vals = [src[i] & lane.get(ops[2]) for i, lane in enumerate(self.lanes)]
+                elif op == "v_add_u32_dpp":
+                    vals = [(src[i] + lane.get(ops[2])) & M32 for i, lane in enumerate(self.lanes)]
                 else:
                     raise NotImplementedError(op)
                 for i, lane in enumerate(self.lanes):

@@ -78,7 +78,8 @@ def run_quad(N, As, Bs=None, lazy_in=False, geo="quad", in_bounds=True, looped=F
                     glb[BB + tid * 4 + r * 1024] = bl[ML * l + r]
                     glb[BB + tid * 4 + (ML + r) * 1024] = bh[ML * l + r]
             args = {"ac": ac, "al": ac + ML * l * ROWB, "b": tid * 4, "bb": BB, "QK": QK, "np": np_,
-                    "e0": 1 if l == 0 else 0, "bp": 4 * G * c}
+                    "e0": 1 if l == 0 else 0, "bp": 4 * G * c,
+                    "mq": MASK if l == 0 else 0}
             for r in range(ML):
                 args[f"n{r}"] = nl[ML * l + r]
             lanes.append(Lane(args, lds=lds, glb=glb, smem=smem))
@@ -87,7 +88,7 @@ def run_quad(N, As, Bs=None, lazy_in=False, geo="quad", in_bounds=True, looped=F
         if Bs is not None:
             for j in range(2 * ML):
                 glb[BB + tid * 4 + j * 1024] = 0
-        args = {"ac": ac, "al": ac, "b": tid * 4, "bb": BB, "QK": QK, "np": np_, "e0": 0, "bp": 4 * tid}
+        args = {"ac": ac, "al": ac, "b": tid * 4, "bb": BB, "QK": QK, "np": np_, "e0": 0, "bp": 4 * tid, "mq": 0}
         args.update({f"n{r}": 0 for r in range(ML)})
         lanes.append(Lane(args, lds=lds, glb=glb, smem=smem))
     mm, sq = PROGS[geo]
@@ -306,12 +307,13 @@ def run_short_group(N, As, hs, geo):
             lds[ac + (Q.HROW + k) * ROWB] = v
         for l in range(G):
             args = {"ac": ac, "al": ac + ML * l * ROWB, "dl": DADDR + 8 * ML * l, "np": np_,
-                    "e0": 1 if l == 0 else 0, "bp": 4 * G * c}
+                    "e0": 1 if l == 0 else 0, "bp": 4 * G * c,
+                    "mq": MASK if l == 0 else 0}
             args.update({f"n{r}": nl[ML * l + r] for r in range(ML)})
             lanes.append(Lane(args, lds=lds))
     if G == 3:
         tid, ac = G * len(As), 4 * len(As)
-        args = {"ac": ac, "al": ac, "dl": DADDR + 8 * L, "np": np_, "e0": 0, "bp": 4 * tid}
+        args = {"ac": ac, "al": ac, "dl": DADDR + 8 * L, "np": np_, "e0": 0, "bp": 4 * tid, "mq": 0}
         args.update({f"n{r}": 0 for r in range(ML)})
         lanes.append(Lane(args, lds=lds))
     counts = Wave(lanes).run(SHORT[geo])
@@ -419,7 +421,8 @@ def test_group_column_bounds_proved_without_mid_reduce():
             lim = (0, MASK + (1 << 10))
             lds = {k * g.ROWB: lim for k in range(2 * L + 20)}
             lds.update({DL + 4 * j: ((0, MASK) if j % 2 == 0 else (0, 0)) for j in range(2 * g.M + 2)})
-            args = {"ac": 0, "al": 0, "QK": QK, "np": (0, MASK), "e0": (0, 1), "bp": 0, "b": 0, "bb": BB, "dl": DL}
+            args = {"ac": 0, "al": 0, "QK": QK, "np": (0, MASK), "e0": (0, 1), "mq": (0, MASK), "bp": 0, "b": 0, "bb": BB,
+                    "dl": DL}
             args.update({f"n{r}": (0, MASK) for r in range(g.M)})
             lane = BoundLane(args, lds=lds, smem={QK + 4 * i: (MASK, 2 * MASK) for i in range(40)},
                              glb={BB + j * 1024: lim for j in range(2 * g.M)})

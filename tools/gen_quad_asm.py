@@ -162,8 +162,40 @@ class Geo:
         return f"v_mov_b32_dpp {dst}, {src} wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
 
 
+# Round 4 experiment: the triple's quotient broadcasts on the VALU instead of the LDS pipe.  The
+# quotient digit is masked with a lane-dependent mask (%[mq] = 2^29 - 1 in a group's lane 0, 0 in the
+# others), so a group holds one nonzero copy, and two DPP adds over wave_shr:1 sum it into every lane
+# of the group: QT = Q(i-1) + Q(i), QB = QT(i-1) + Q(i) = Q(i-2) + Q(i-1) + Q(i) -- the value of the
+# group's lane 0 in lanes 0, 1, 2 (the neighbours' copies are 0; lane 0 of the wave reads 0 past the
+# end).  Two VALU instructions per broadcast in place of one ds_bpermute and its LDS latency.
+TRI_DPP_BCAST = os.environ.get("FBM_GEN_TRI_DPP", "0") == "1"  # (an A/B switch until measured)
+
 QUAD = Geo(4, 72)   # 64 ciphertexts per workgroup + 8 words of padding
 TRI = Geo(3, 89)    # 84 ciphertexts + the dummy column + 4 words of padding
+
+
+def dpp_bcast(dst, tmp, src):
+    """The triple's group broadcast of a lane-masked value (TRI_DPP_BCAST): two DPP adds."""
+    sh = "wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+    return [f"v_add_u32_dpp {tmp}, {src}, {src} {sh}", f"v_add_u32_dpp {dst}, {tmp}, {src} {sh}"]
+
+
+def tri_chain(q, q2, qb, q2b, t3, t4, tlo, slo, spair, cq, kreg):
+    """The triple's quotient chain: q from the t column's low word, the s column's K'_i - q, q' from the
+    s column; the broadcasts by ds_bpermute or two DPP adds (TRI_DPP_BCAST).  Returns the instructions
+    and, for each after the first, the independent multiplies to place before it."""
+    fix, fgap = [f"v_sub_u32 {cq}, {kreg}, {q}", f"v_mad_u64_u32 {spair}, vcc, {cq}, %[e0], {spair}"], [2, 2]
+    if TRI_DPP_BCAST:
+        chain = ([f"v_mul_lo_u32 {q}, {tlo}, %[np]", f"v_and_b32 {q}, %[mq], {q}"] + fix + dpp_bcast(qb, t3, q) +
+                 [f"v_mul_lo_u32 {q2}, {slo}, %[np]", f"v_and_b32 {q2}, %[mq], {q2}"] + dpp_bcast(q2b, t4, q2))
+        gaps = [2] + [1] * len(fix) + [1, 2, 1, 2, 2, 2]
+    else:
+        chain = ([f"v_mul_lo_u32 {q}, {tlo}, %[np]", f"v_and_b32 {q}, {MASK}, {q}",
+                  f"ds_bpermute_b32 {qb}, %[bp], {q}"] + fix +
+                 [f"v_mul_lo_u32 {q2}, {slo}, %[np]", f"v_and_b32 {q2}, {MASK}, {q2}",
+                  f"ds_bpermute_b32 {q2b}, %[bp], {q2}"])
+        gaps = [2, 0] + fgap + [3, 2, 0]
+    return chain, gaps
 
 
 def N(r):
@@ -298,16 +330,8 @@ def row(g, first, sq, kreg, xs, xn, pre_off, first_s=None):
         for r in range(2, M):
             rest += [tm(r), sm(r - 1)]
         rest.append(sm(M - 1))
-        chain = [f"v_mul_lo_u32 {g.Q}, {g.TTLO}, %[np]",
-                 f"v_and_b32 {g.Q}, {MASK}, {g.Q}",
-                 f"ds_bpermute_b32 {g.QB}, %[bp], {g.Q}",
-                 f"v_sub_u32 {g.CQ}, {kreg}, {g.Q}",
-                 f"v_mad_u64_u32 {g.TS}, vcc, {g.CQ}, %[e0], {g.TS}",
-                 f"v_mul_lo_u32 {g.Q2}, {g.TSLO}, %[np]",
-                 f"v_and_b32 {g.Q2}, {MASK}, {g.Q2}",
-                 f"ds_bpermute_b32 {g.Q2B}, %[bp], {g.Q2}"]
-        # chain step k after 3 (the first) / 2 .. 3 independent multiplies
-        gaps = [1, 2, 0, 2, 2, 3, 2, 0]
+        chain, gaps = tri_chain(g.Q, g.Q2, g.QB, g.Q2B, g.T3, g.T4, g.TTLO, g.TSLO, g.TS, g.CQ, kreg)
+        gaps = [1] + gaps
         p1 = list(mads)
         ri = 0
         for k, ins in enumerate(chain):
@@ -316,7 +340,8 @@ def row(g, first, sq, kreg, xs, xn, pre_off, first_s=None):
             ri += take
             p1.append(ins)
         p1 += rest[ri:]
-        p1.append("s_waitcnt lgkmcnt(1)")  # QB (the Q2B permute may still be in flight)
+        if not TRI_DPP_BCAST:
+            p1.append("s_waitcnt lgkmcnt(1)")  # QB (the Q2B permute may still be in flight)
     # ---- pass 2: q * N (t), interleaved with x1_i * b0 (s, general product) ----
     tq = [f"v_mad_u64_u32 {g.TT}, vcc, {g.QB}, {N(0)}, {g.TT}"] + \
         [f"v_mad_u64_u32 {g.At(r - 1)}, vcc, {g.QB}, {N(r)}, {g.At(r - 1)}" for r in range(1, M)]
@@ -337,7 +362,7 @@ def row(g, first, sq, kreg, xs, xn, pre_off, first_s=None):
     ret_s = [g.down("v_and_b32_dpp", g.RSLO, g.TSLO, f", {g.MASKV}"),
              f"v_lshrrev_b64 {g.TS}, {LB}, {g.TS}",
              f"v_lshl_add_u64 {g.As(0)}, {g.TS}, 0, {g.As(0)}"]
-    p3 = [] if g.G == 4 else ["s_waitcnt lgkmcnt(0)"]
+    p3 = [] if (g.G == 4 or TRI_DPP_BCAST) else ["s_waitcnt lgkmcnt(0)"]
     p3 += [sq3[0], ret_t[0], sq3[1], ret_t[1], sq3[2], ret_t[2], sq3[3], ret_s[0], sq3[4], ret_s[1], sq3[5],
            ret_s[2]] + sq3[6:]
     return out + p1 + p2 + p3
@@ -494,6 +519,9 @@ def product(sq, g=QUAD, carries=CARRY_PAIRS, cyc=None):
 # K'_i are read from s(64 + i) directly (no m0).  Same residues as the looped square.
 # ------------------------------------------------------------------------------------------
 CYC_SQUARE = True
+# Round 4 experiment: the cyclic-band square's doubled cross products as x_i * (2 b0[r]) from M doubled
+# limb registers made once per square, in place of 2 x_i made once per row (36 -> M shifts per square).
+CYC_B0D = os.environ.get("FBM_GEN_CYC_B0D", "0") == "1"  # (an A/B switch until measured)
 
 
 class CycPlan:
@@ -515,6 +543,9 @@ class CycPlan:
         v += M
         self.B1 = [v + r for r in range(M)]
         v += M
+        if CYC_B0D:
+            self.B0D = [v + r for r in range(M)]
+            v += M
         self.X = (v, v + 1)  # x0 of even / odd rows
         self.XD = v + 2      # 2 x0 of the current row
         v += 3
@@ -565,8 +596,12 @@ def cyc_row(g, P, i):
 
     out = [] if last else [f"ds_read_b32 v{xn}, %[ac] offset:{(i + 1) * g.ROWB}"]
     acts = cyc_active(g, i)
-    tm = {r: f"v_mad_u64_u32 {_pr(st(r))}, vcc, v{P.XD if dbl else xs}, v{P.B0[r]}, {addend('t', r)}"
-          for r, dbl in acts}
+    if CYC_B0D:
+        tm = {r: f"v_mad_u64_u32 {_pr(st(r))}, vcc, v{xs}, v{P.B0D[r] if dbl else P.B0[r]}, {addend('t', r)}"
+              for r, dbl in acts}
+    else:
+        tm = {r: f"v_mad_u64_u32 {_pr(st(r))}, vcc, v{P.XD if dbl else xs}, v{P.B0[r]}, {addend('t', r)}"
+              for r, dbl in acts}
     sm = [f"v_mad_u64_u32 {_pr(ss(r))}, vcc, v{xs}, v{P.B1[r]}, {addend('s', r)}" for r in range(M)]
     # pass 1: slot 0's t and s products first, the rest interleaved; the quotient chain threaded in
     head = ([tm[0]] if 0 in tm else []) + [sm[0]]
@@ -589,15 +624,9 @@ def cyc_row(g, P, i):
         gaps = [1 if 0 in tm else 0, 2, 2, 2, 3, 2]
         qb, q2b = P.Q, P.Q2
     else:
-        chain = [f"v_mul_lo_u32 v{P.Q}, v{st(0)}, %[np]",
-                 f"v_and_b32 v{P.Q}, {MASK}, v{P.Q}",
-                 f"ds_bpermute_b32 v{P.QB}, %[bp], v{P.Q}",
-                 f"v_sub_u32 v{P.CQ}, {K}, v{P.Q}",
-                 f"v_mad_u64_u32 {_pr(ss(0))}, vcc, v{P.CQ}, %[e0], {_pr(ss(0))}",
-                 f"v_mul_lo_u32 v{P.Q2}, v{ss(0)}, %[np]",
-                 f"v_and_b32 v{P.Q2}, {MASK}, v{P.Q2}",
-                 f"ds_bpermute_b32 v{P.Q2B}, %[bp], v{P.Q2}"]
-        gaps = [1 if 0 in tm else 0, 2, 0, 2, 2, 3, 2, 0]
+        chain, gaps = tri_chain(f"v{P.Q}", f"v{P.Q2}", f"v{P.QB}", f"v{P.Q2B}", f"v{P.T3}", f"v{P.T4}",
+                                f"v{st(0)}", f"v{ss(0)}", _pr(ss(0)), f"v{P.CQ}", K)
+        gaps = [1 if 0 in tm else 0] + gaps
         qb, q2b = P.QB, P.Q2B
     p1 = list(head)
     ri = 0
@@ -607,7 +636,7 @@ def cyc_row(g, P, i):
         ri += take
         p1.append(ins)
     p1 += rest[ri:]
-    if g.G == 3:
+    if g.G == 3 and not TRI_DPP_BCAST:
         p1.append("s_waitcnt lgkmcnt(1)")  # the row prefetch and QB (Q2B may still be in flight)
     # pass 2: q N into the t window
     p2 = [f"v_mad_u64_u32 {_pr(st(r))}, vcc, v{qb}, {N(r)}, {addend('t', r)}" for r in range(M)]
@@ -620,11 +649,14 @@ def cyc_row(g, P, i):
     ret_s = [g.down("v_and_b32_dpp", f"v{P.RS}", f"v{ss(0)}", f", v{P.MASKV}"),
              f"v_lshrrev_b64 {_pr(ss(0))}, {LB}, {_pr(ss(0))}",
              f"v_lshl_add_u64 {_pr(ss(1))}, {_pr(ss(0))}, 0, {_pr(ss(1))}"]
-    p3 = ["s_waitcnt lgkmcnt(0)"]
-    if not last:  # the next row's doubled operand (its x0 has arrived with the wait above)
+    early = (g.G == 3 and not TRI_DPP_BCAST) or not CYC_B0D  # Q2B (bpermute) or the XD shift need xn / q' now
+    p3 = ["s_waitcnt lgkmcnt(0)"] if early else []
+    if not last and not CYC_B0D:  # the next row's doubled operand (its x0 has arrived with the wait above)
         p3.append(f"v_lshlrev_b32 v{P.XD}, 1, v{xn}")
     p3 += [sq3[0], ret_t[0], sq3[1], ret_t[1], sq3[2], ret_t[2], sq3[3], ret_s[0], sq3[4], ret_s[1], sq3[5],
            ret_s[2]] + sq3[6:]
+    if not early:  # the next row's operand, prefetched above
+        p3.append("s_waitcnt lgkmcnt(0)")
     return out + p1 + p2 + p3
 
 
@@ -708,7 +740,10 @@ def square_cyc(g, carries=CARRY_PAIRS):
     e.extend([f"v_mov_b32 v{P.RT + 1}, 0", f"v_mov_b32 v{P.RS + 1}, 0", f"v_mov_b32 v{P.MASKV}, {MASK}",
               f"ds_read_b32 v{P.X[0]}, %[ac]", "s_waitcnt lgkmcnt(0)"])
     e.extend([f"v_lshlrev_b32 v{P.B1[r]}, 1, v{P.B1[r]}" for r in range(M)])  # the s part is x0 * (2 x1)
-    e.emit(f"v_lshlrev_b32 v{P.XD}, 1, v{P.X[0]}")
+    if CYC_B0D:
+        e.extend([f"v_lshlrev_b32 v{P.B0D[r]}, 1, v{P.B0[r]}" for r in range(M)])
+    else:
+        e.emit(f"v_lshlrev_b32 v{P.XD}, 1, v{P.X[0]}")
     for i in range(L):
         e.extend(cyc_row(g, P, i))
         if i == MID - 1:
@@ -780,11 +815,15 @@ def header(g, pfx, PFX, name):
     sql = product(True, g, cyc=False)
     operands = ", ".join([f'[n{r}] "v"(n[{r}])' for r in range(M)])
     bp_doc, bp_arg, bp_op = "", "", ""
+    mq_def = ""
     if g.G == 3:
         bp_doc = ("\n// bp: ds_bpermute byte address of the group's lane 0 (4 * (3 * (lane / 3)), the dummy lane 63\n"
                   "// its own).")
         bp_arg = ", uint32_t bp"
         bp_op = ', [bp] "v"(bp)'
+        if TRI_DPP_BCAST:  # the quotient digits' lane mask (see gen_quad_asm.TRI_DPP_BCAST)
+            bp_op += ', [mq] "v"(mq)'
+            mq_def = "  const uint32_t mq = e0 ? 0x1fffffffu : 0u;\n"
     dpp_word = "DPP quad_perm" if g.G == 4 else "ds_bpermute broadcasts, DPP wave shifts"
     return f"""// GENERATED by tools/gen_quad_asm.py -- do not edit by hand.
 //
@@ -820,7 +859,7 @@ def header(g, pfx, PFX, name):
 __device__ __forceinline__ void fbm_{pfx}_mm_glb(uint32_t ac, uint32_t al, const uint32_t* bb, uint32_t b_off,
                                               const uint32_t* QK, uint32_t np, const uint32_t (&n)[{M}],
                                               uint32_t e0{bp_arg}) {{
-  asm volatile(
+{mq_def}  asm volatile(
 {c_string(mm)}
       :
       : [ac] "v"(ac), [al] "v"(al), [b] "v"(b_off), [bb] "s"(bb), [QK] "s"(QK), [np] "s"(np), [e0] "v"(e0){bp_op},
@@ -833,7 +872,7 @@ __device__ __forceinline__ void fbm_{pfx}_mm_glb(uint32_t ac, uint32_t al, const
 // (D = N - 2^{LB * KS}; zeros for a dummy lane).  {len(ms)} instructions, {ms_mads(g)} v_mad_u64_u32 per lane.
 __device__ __forceinline__ void fbm_{pfx}_ms_lds(uint32_t ac, uint32_t al, uint32_t dl, uint32_t np,
                                               const uint32_t (&n)[{M}], uint32_t e0{bp_arg}) {{
-  asm volatile(
+{mq_def}  asm volatile(
 {c_string(ms)}
       :
       : [ac] "v"(ac), [al] "v"(al), [dl] "v"(dl), [np] "s"(np), [e0] "v"(e0){bp_op},
@@ -845,7 +884,7 @@ __device__ __forceinline__ void fbm_{pfx}_ms_lds(uint32_t ac, uint32_t al, uint3
 // the launch's hot code keeps one copy of the unrolled cyclic-band square.
 __device__ __forceinline__ void fbm_{pfx}_sq_lds_looped(uint32_t ac, uint32_t al, const uint32_t* QK, uint32_t np,
                                                      const uint32_t (&n)[{M}], uint32_t e0{bp_arg}) {{
-  asm volatile(
+{mq_def}  asm volatile(
 {c_string(sql)}
       :
       : [ac] "v"(ac), [al] "v"(al), [QK] "s"(QK), [np] "s"(np), [e0] "v"(e0){bp_op},
@@ -856,7 +895,7 @@ __device__ __forceinline__ void fbm_{pfx}_sq_lds_looped(uint32_t ac, uint32_t al
 // a <- a^2 R^-1 (mod N^2): B = A from the LDS column (the s part as x0 * (2 x1)).
 __device__ __forceinline__ void fbm_{pfx}_sq_lds(uint32_t ac, uint32_t al, const uint32_t* QK, uint32_t np,
                                               const uint32_t (&n)[{M}], uint32_t e0{bp_arg}) {{
-  asm volatile(
+{mq_def}  asm volatile(
 {c_string(sq)}
       :
       : [ac] "v"(ac), [al] "v"(al), [QK] "s"(QK), [np] "s"(np), [e0] "v"(e0){bp_op},
