@@ -168,7 +168,9 @@ class Geo:
 # of the group: QT = Q(i-1) + Q(i), QB = QT(i-1) + Q(i) = Q(i-2) + Q(i-1) + Q(i) -- the value of the
 # group's lane 0 in lanes 0, 1, 2 (the neighbours' copies are 0; lane 0 of the wave reads 0 past the
 # end).  Two VALU instructions per broadcast in place of one ds_bpermute and its LDS latency.
-TRI_DPP_BCAST = os.environ.get("FBM_GEN_TRI_DPP", "0") == "1"  # (an A/B switch until measured)
+# Measured equal to the permutes alone and 1 % slower with CYC_B0D (profiles/r4_tri_dpp_ab.jsonl,
+# r4_tri_b0d_ab.jsonl): the 144 extra VALU instructions per square cost what the permutes' LDS latency did.
+TRI_DPP_BCAST = os.environ.get("FBM_GEN_TRI_DPP", "0") == "1"  # (an A/B switch, off)
 
 QUAD = Geo(4, 72)   # 64 ciphertexts per workgroup + 8 words of padding
 TRI = Geo(3, 89)    # 84 ciphertexts + the dummy column + 4 words of padding
@@ -519,9 +521,11 @@ def product(sq, g=QUAD, carries=CARRY_PAIRS, cyc=None):
 # K'_i are read from s(64 + i) directly (no m0).  Same residues as the looped square.
 # ------------------------------------------------------------------------------------------
 CYC_SQUARE = True
-# Round 4 experiment: the cyclic-band square's doubled cross products as x_i * (2 b0[r]) from M doubled
-# limb registers made once per square, in place of 2 x_i made once per row (36 -> M shifts per square).
-CYC_B0D = os.environ.get("FBM_GEN_CYC_B0D", "0") == "1"  # (an A/B switch until measured)
+# Round 4: the cyclic-band square's doubled cross products as x_i * (2 b0[r]) from M doubled limb
+# registers made once per square, in place of 2 x_i made once per row (36 -> M shifts per square): the
+# triple at one rank's 1/8 / 1/4 stripe -0.7 / -1.2 % (profiles/r4_tri_b0d_ab.jsonl).  FBM_GEN_CYC_B0D=0
+# generates the per-row doubling (the A/B base).
+CYC_B0D = os.environ.get("FBM_GEN_CYC_B0D", "1") == "1"
 
 
 class CycPlan:
