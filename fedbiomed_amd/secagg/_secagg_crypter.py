@@ -175,18 +175,23 @@ class SecaggCrypter:
         logger.debug(f"Encryption of the parameters took {time.process_time() - start} seconds.")
         return out
 
+    # A/B switch (tools/node_encrypt_probe.py): each stripe's device-to-host copy on a side stream instead of
+    # in stream order behind its kernels
+    _copy_on_side_stream = False
+
     def _encrypt_overlapped(self, num_nodes, current_round, x, key, biprime, clipping_range, weight, target_range,
                             stripes, cr):
         """The list API's encrypt as ct_offset stripes (one per full one-lane round, the partial round
         last), issued back to back on the current stream; each stripe's ciphertexts go to a pinned host
-        buffer on a side stream, and the host builds the Python ints of stripe k while the GPU
-        exponentiates stripe k + 1 (the ciphertext of index k depends only on k: the stripes
-        concatenate bit for bit to the unsplit call's).  One status check for the whole call (its
+        buffer in stream order, right behind its kernels, and the host builds the Python ints of stripe k
+        while the GPU exponentiates stripe k + 1 (the ciphertext of index k depends only on k: the
+        stripes concatenate bit for bit to the unsplit call's).  One status check for the whole call (its
         clipping warning once)."""
         dev, n = x.device, x.numel()
         host = D.host_empty((stripes[-1][1], 64), torch.int32)
         packed = host.numpy().view(np.uint32)
-        side, main = D.side_stream(dev), torch.cuda.current_stream(dev)
+        main = torch.cuda.current_stream(dev)
+        side = D.side_stream(dev) if self._copy_on_side_stream else main
         done = []
         with D.deferred_checks(merge=True):
             for c0, c1 in stripes:
