@@ -588,18 +588,6 @@ def list_encrypt_stripes(n_ct: int, dev=None) -> List[Tuple[int, int]]:
     return list(zip(cuts[:-1], cuts[1:]))
 
 
-_SIDE = {}
-
-
-def side_stream(dev=None) -> torch.cuda.Stream:
-    """A per-device side stream (the list API's device-to-host copies beside the next stripe's compute)."""
-    dev = dev or device()
-    key = dev.index if dev.index is not None else torch.cuda.current_device()
-    if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(device=dev)
-    return _SIDE[key]
-
-
 def jl_engine_for(n_ct: int) -> str:
     """The engine a launch of n_ct ciphertexts takes under the current policy."""
     return {1: "single", 2: "generic", 3: "triple", 4: "quad"}[N.load().fbm_jl_engine_for(int(n_ct))]

@@ -175,10 +175,6 @@ class SecaggCrypter:
         logger.debug(f"Encryption of the parameters took {time.process_time() - start} seconds.")
         return out
 
-    # A/B switch (tools/node_encrypt_probe.py): each stripe's device-to-host copy on a side stream instead of
-    # in stream order behind its kernels
-    _copy_on_side_stream = False
-
     def _encrypt_overlapped(self, num_nodes, current_round, x, key, biprime, clipping_range, weight, target_range,
                             stripes, cr):
         """The list API's encrypt as ct_offset stripes (one per full one-lane round, the partial round
@@ -191,18 +187,16 @@ class SecaggCrypter:
         host = D.host_empty((stripes[-1][1], 64), torch.int32)
         packed = host.numpy().view(np.uint32)
         main = torch.cuda.current_stream(dev)
-        side = D.side_stream(dev) if self._copy_on_side_stream else main
         done = []
         with D.deferred_checks(merge=True):
             for c0, c1 in stripes:
                 ct = self.encrypt_tensor(num_nodes, current_round, x[c0 * cr:min(n, c1 * cr)], key, biprime,
                                          clipping_range, weight, target_range, ct_offset=c0)
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    host[c0:c1].copy_(ct, non_blocking=True)
-                    ct.record_stream(side)
-                    ev = torch.cuda.Event()
-                    ev.record(side)
+                # (in stream order: a side stream for the copies measured the same, 152-154 ms at 10M --
+                # profiles/r4_node_encrypt_probe.jsonl)
+                host[c0:c1].copy_(ct, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(main)
                 done.append(ev)
             out = []
             for (c0, c1), ev in zip(stripes, done):

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Where one node's SecaggCrypter.encrypt(List[float]) spends its time at 10M elements (the list API's
 overlapped stripes, _secagg_crypter._encrypt_overlapped): host timestamps of every stripe's issue, of its
-ciphertexts' arrival in the pinned buffer (the side stream's event) and of the end of its int
+ciphertexts' arrival in the pinned buffer (the copy's event) and of the end of its int
 conversion, against the whole call.  One JSON line per call.
 
     python tools/node_encrypt_probe.py [--elements 10000000] [--reps 3]"""
@@ -20,7 +20,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--elements", type=int, default=10_000_000)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--side", action="store_true", help="the stripes' copies on a side stream (the round-4 form before)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -31,7 +30,6 @@ def main():
     rng = np.random.default_rng(5)
     xl = (rng.standard_normal(args.elements) * 0.05).astype(np.float32).astype(np.float64).tolist()
     jc = SC.SecaggCrypter()
-    jc._copy_on_side_stream = args.side
     key, P, tau = W.jl_user_key(1), 8, 3
     jc.encrypt(P, tau, xl[:4096], key, W.BIPRIME0, weight=1)  # warm-up
     marks = []
@@ -59,7 +57,7 @@ def main():
             continue  # (the first full-size call allocates the pinned staging)
         n_ct = len(out)
         stripes = D.list_encrypt_stripes(n_ct)
-        print(json.dumps({"copy": "side" if args.side else "in-order", "elements": args.elements, "ciphertexts": n_ct, "stripes": stripes, "ms": 1000 * (t1 - t0),
+        print(json.dumps({"elements": args.elements, "ciphertexts": n_ct, "stripes": stripes, "ms": 1000 * (t1 - t0),
                           "marks_ms": [(k, round(1000 * (t - t0), 2)) for k, t in marks]}), flush=True)
 
 
