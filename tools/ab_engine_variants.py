@@ -23,7 +23,7 @@ def madsonly(lines, addr_regs):
     def keep(ln):
         if not ln.startswith("v_"):
             return True
-        if ln.startswith("v_mad_u64_u32"):
+        if ln.startswith(("v_mad_u64_u32", "v_mad_i64_i32")):
             return True
         if ln.startswith(("v_add_u32 ", "v_mov_b32 ")):
             return ln.split()[1].rstrip(",") in addr_regs
@@ -40,9 +40,9 @@ def build(engine):
     if engine == "tri":
         orig = G.product
 
-        def product(sq, g=G.QUAD, carries=G.CARRY_PAIRS):
-            lines = orig(sq, g, carries)
-            return madsonly(lines, {G.TRI.AADR}) if (sq and g is G.TRI) else lines
+        def product(sq, g=G.QUAD, carries=G.CARRY_PAIRS, cyc=None):
+            lines = orig(sq, g, carries, cyc)
+            return madsonly(lines, {G.TRI.AADR}) if (sq and g is G.TRI and cyc is not False) else lines
 
         G.product = product
         hdr, _, _ = G.header(G.TRI, "ta", "TA", "TRIPLE")
@@ -50,11 +50,12 @@ def build(engine):
         with open(work + "/x/csrc/fbm_tri_asm.hpp", "w") as f:
             f.write(hdr)
     else:
-        orig, out0 = NA.square_tri, NA.OUT
-        NA.square_tri = lambda: madsonly(orig(), {NA.SAADR, NA.SDADDR, NA.STMP})
+        orig, orig_u, out0 = NA.square_tri, NA.square_unrolled, NA.OUT
+        NA.square_tri = lambda: madsonly(orig(), {NA.SAADR, NA.SDADDR, NA.STMP})  # (the looped square)
+        NA.square_unrolled = lambda: madsonly(orig_u(), {NA.SAADR, NA.SDADDR, NA.STMP})  # the shipped square
         NA.OUT = work + "/x/csrc/fbm_nadic_asm.hpp"
         NA.main()
-        NA.square_tri, NA.OUT = orig, out0
+        NA.square_tri, NA.square_unrolled, NA.OUT = orig, orig_u, out0
     os.makedirs(os.path.join(ROOT, "build", "ab"), exist_ok=True)
     out = os.path.join(ROOT, "build", "ab", f"{engine}_madsonly.so")
     cmd = [B.hipcc(), f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
