@@ -11,7 +11,7 @@ for v in "$@"; do
   echo "$v: $(tail -1 $O/pytest_$v.txt)"
 done
 for rep in 1 2 3; do
-  for v in base4 "$@"; do
+  for v in ${BASE:-base4} "$@"; do
     FBM_LIB_PATH=$(lib $v) timeout -k 10 200 python -u tools/exp_probe.py --ct 41667,83334 --engines triple --reps 3 > $O/probe_tri_$v.$rep.jsonl 2>&1 || { echo "PROBE FAILED tri $v"; tail -3 $O/probe_tri_$v.$rep.jsonl; exit 1; }
     echo "== $v $rep $(grep -h triple_ms $O/probe_tri_$v.$rep.jsonl | tr '\n' ' ')"
   done
