@@ -850,12 +850,38 @@ def main():
             t_wire_ser = time.perf_counter() - t0
         finally:
             wire.enable(False)
+
+        def reassembly(nbytes):  # one message of nbytes in the transport's 4 MB chunks (constants.py:121)
+            cut = 4000000 - 33
+            msg = np.random.default_rng(9).integers(0, 256, nbytes, dtype=np.uint8).tobytes()
+            chunks = [msg[i:i + cut] for i in range(0, nbytes, cut)]
+            k = len(chunks)
+            t0 = time.perf_counter()
+            reply = bytes()
+            for c in chunks:  # the reference's loop (transport/server.py:236-239)
+                reply += c
+            t_ref = time.perf_counter() - t0
+            asm = wire.ChunkAssembler()
+            t0 = time.perf_counter()
+            for it, c in enumerate(chunks, 1):
+                out = asm.add(c, k, it)
+            t_asm = time.perf_counter() - t0
+            assert out == reply
+            return {"bytes": nbytes, "chunks": k, "reference_ms": 1000 * t_ref, "chunk_assembler_ms": 1000 * t_asm}
+
+        per_party = 10_000_000 / nl  # one party's update at the metric's 10M elements
+        chunk_reassembly = {"reference_encoding": reassembly(int(ref_bytes / P * per_party)),
+                            "encrypted_params_blob": reassembly(int(wire_bytes / P * per_party)),
+                            "note": "one party's 10M-element update received in the transport's 4 MB chunks: "
+                                    "reply += chunk (the reference) vs fedbiomed_amd.wire.ChunkAssembler "
+                                    "(SURVEY 8(f)2), host only"}
         line["end_to_end"] = {
             "wire": {"elements": nl, "parties": P,
                      "reference_encoding": {"bytes": ref_bytes, "dumps_loads_ms": 1000 * t_ref_ser,
                                             "list_api_plus_wire_params_per_s": nl / (tl + t_ref_ser)},
                      "encrypted_params_blob": {"bytes": wire_bytes, "dumps_loads_ms": 1000 * t_wire_ser,
                                                "list_api_plus_wire_params_per_s": nl / tw},
+                     "chunk_reassembly": chunk_reassembly,
                      "note": "P updates through msgpack (reference Serializer rules) and back, then aggregate; "
                              "blob = fedbiomed_amd.wire hook (SURVEY 8(f)2)"},
             "pinned_host_tensors": {"value": n / te, "unit": "params/s", "ms_per_step": 1000 * te,

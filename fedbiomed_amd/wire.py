@@ -23,6 +23,12 @@ working.  With it enabled:
 
 `from_wire` materialises the Python ints as well, so every consumer that treats the update as
 ``List[int]`` sees exactly the reference's values.
+
+`ChunkAssembler` is the other half of §8(f)2: the gRPC transport streams a serialized message in
+chunks of `MAX_MESSAGE_BYTES_LENGTH` (4 MB) and the receiver rebuilds it with ``reply += chunk``
+(`fedbiomed/transport/server.py:236-239`, `client.py:599-602` in `_call_researcher`), which copies the growing message at
+every chunk -- quadratic in the chunk count (a 10M-parameter JL update is 17-24 chunks).  The
+assembler keeps the chunks and joins them once.
 """
 
 from __future__ import annotations
@@ -162,3 +168,23 @@ def packed_rows(params, scheme: str, n: Optional[int] = None) -> Optional[np.nda
             return None
         n = len(params[0])
     return np.stack([p.packed[:n] for p in params])
+
+
+class ChunkAssembler:
+    """Rebuilds a message streamed as chunks numbered ``iteration`` = 1 .. ``size`` (the transport's
+    `TaskResult` / `TaskResponse` fields) in linear time.  ``add`` returns the whole message on its last
+    chunk (``iteration == size``, the reference's completion test) and None before; the assembler is
+    then empty for the next message, as the reference's loop is after ``Serializer.loads``."""
+
+    __slots__ = ("_parts",)
+
+    def __init__(self) -> None:
+        self._parts: list = []
+
+    def add(self, chunk: bytes, size: int, iteration: int) -> Optional[bytes]:
+        self._parts.append(chunk)
+        if size != iteration:
+            return None
+        out = b"".join(self._parts)
+        self._parts = []
+        return out

@@ -148,3 +148,31 @@ def test_crypters_through_the_wire():
     a = lc.aggregate(recv_l, sum(ws))
     b = lc.aggregate(plain_l, sum(ws))
     assert np.array_equal(np.asarray(a).view(np.uint64), np.asarray(b).view(np.uint64))
+
+
+def test_chunk_assembler_matches_the_reference_loop():
+    """ChunkAssembler returns the bytes the reference's ``reply += answer.bytes_`` loop builds
+    (transport/server.py:236-239): one message per ``size == iteration`` chunk, several messages on one
+    stream, chunk sizes as the sender cuts them (MAX_MESSAGE_BYTES_LENGTH, the last one short), a
+    one-chunk message and an empty one."""
+    import os as _os
+
+    from fedbiomed_amd.wire import ChunkAssembler
+
+    cut = 4000000 - 33  # the reference's MAX_MESSAGE_BYTES_LENGTH (constants.py:121)
+    msgs = [_os.urandom(3 * cut + 12345), b"x" * 17, b"", _os.urandom(cut)]
+    stream = []
+    for m in msgs:
+        starts = list(range(0, len(m), cut)) or [0]
+        for it, st in enumerate(starts, 1):
+            stream.append((m[st:st + cut], len(starts), it))
+    asm, got, ref, reply = ChunkAssembler(), [], [], bytes()
+    for chunk, size, it in stream:
+        out = asm.add(chunk, size, it)
+        if out is not None:
+            got.append(out)
+        reply += chunk  # the reference's loop
+        if size == it:
+            ref.append(reply)
+            reply = bytes()
+    assert got == ref == msgs
