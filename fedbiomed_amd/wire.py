@@ -27,7 +27,7 @@ working.  With it enabled:
 `ChunkAssembler` is the other half of §8(f)2: the gRPC transport streams a serialized message in
 chunks of `MAX_MESSAGE_BYTES_LENGTH` (4 MB) and the receiver rebuilds it with ``reply += chunk``
 (`fedbiomed/transport/server.py:236-239`, `client.py:599-602` in `_call_researcher`), which copies the growing message at
-every chunk -- quadratic in the chunk count (a 10M-parameter JL update is 17-24 chunks).  The
+every chunk -- quadratic in the chunk count (a 10M-parameter JL update is 22-24 chunks).  The
 assembler keeps the chunks and joins them once.
 """
 
