@@ -421,13 +421,14 @@ __host__ __device__ inline bool gcd_is_one_r8(const uint32_t (&r)[8], const uint
 // digests only: once 8 digests (256 bytes = bits_size // 8) are in, the reference's inner
 // loop (_jls.py:746-755) never breaks again and counter.to_bytes(1) overflows at 256 -- its
 // OverflowError, whatever gcd the 8-digest r would have.
-__global__ void __launch_bounds__(256) jl_fdh_kernel(uint64_t n_ct, JlParams jp, uint32_t* __restrict__ H,
-                                                     uint32_t* __restrict__ stats, uint32_t* __restrict__ Hc) {
-  const uint64_t kl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (kl >= n_ct) return;
-  const uint64_t k = kl + jp.ct_offset;  // global ciphertext index in t_k = (k << 512) | tau
-  uint32_t err = 0;
-  uint32_t st[8], W[16];
+//
+// Two kernels: jl_fdh_kernel takes the first digest, which every ciphertext of a real biprime keeps
+// (its gcd on 8 words, gcd_is_one_r8), in few registers; a ciphertext whose first digest is not coprime
+// (small or even moduli) is marked in word 63 of its H row -- never nonzero in an r of at most 7 digests --
+// and jl_fdh_retry_kernel redoes it with r of up to 7 digests (the 64-word gcd).  One kernel holding both
+// paths took 256 VGPRs and ran one wave per SIMD.
+__device__ __forceinline__ void fdh_state_after_t(const JlParams& jp, uint64_t k, uint32_t (&st)[8]) {
+  uint32_t W[16];
 #pragma unroll
   for (int i = 0; i < 8; ++i) st[i] = jp.mid[i];
 #pragma unroll
@@ -438,19 +439,76 @@ __global__ void __launch_bounds__(256) jl_fdh_kernel(uint64_t n_ct, JlParams jp,
 #pragma unroll
   for (int i = 0; i < 16; ++i) W[i] = jp.tau_w[i];  // block 15: the round's bits 0..511
   fbm_sha256_compress(st, W);
+}
+__device__ __forceinline__ void fdh_digest(const uint32_t (&st)[8], uint32_t c, uint32_t (&d)[8]) {
+  uint32_t W[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) d[i] = st[i];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) W[i] = 0u;
+  W[0] = (c << 24) | (0x80u << 16);
+  W[15] = 8200u;
+  fbm_sha256_compress(d, W);
+}
+constexpr uint32_t FBM_FDH_RETRY = ~0u;  // word 63 of an H row: the first digest was not coprime
+
+__global__ void __launch_bounds__(256) jl_fdh_kernel(uint64_t n_ct, JlParams jp, uint32_t* __restrict__ H,
+                                                     uint32_t* __restrict__ stats, uint32_t* __restrict__ Hc) {
+  const uint64_t kl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (kl >= n_ct) return;
+  uint32_t err = 0, st[8], d[8], r8[8];
+  fdh_state_after_t(jp, kl + jp.ct_offset, st);
+  fdh_digest(st, 1u, d);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r8[i] = d[7 - i];  // r = D1 as 8 little-endian limbs
+  const bool ok = !(jp.fdh_even && !(r8[0] & 1u)) && gcd_is_one_r8(r8, jp.N32, err);  // even 2^s N: r odd too
+  if (err) atomicOr(stats + FBM_STAT_ERRFLAGS, err);
+  uint4* o = reinterpret_cast<uint4*>(H + kl * 64);
+  if (!ok) {  // the retry kernel writes the whole row (and the compact row's sentinel stays)
+    if (Hc) {
+      uint4* c = reinterpret_cast<uint4*>(Hc + kl * 8);
+      c[0] = c[1] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    }
+    o[15] = make_uint4(0u, 0u, 0u, FBM_FDH_RETRY);
+    return;
+  }
+  if (Hc) {  // compact: 32 bytes per ciphertext, the whole row only behind the sentinel
+    uint32_t ones = ~0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ones &= r8[i];
+    const bool full = ones == ~0u;  // (a one-digest r of all ones takes the sentinel)
+    uint4* c = reinterpret_cast<uint4*>(Hc + kl * 8);
+    c[0] = full ? make_uint4(~0u, ~0u, ~0u, ~0u) : make_uint4(r8[0], r8[1], r8[2], r8[3]);
+    c[1] = full ? make_uint4(~0u, ~0u, ~0u, ~0u) : make_uint4(r8[4], r8[5], r8[6], r8[7]);
+    if (!full) return;
+  }
+  o[0] = make_uint4(r8[0], r8[1], r8[2], r8[3]);
+  o[1] = make_uint4(r8[4], r8[5], r8[6], r8[7]);
+#pragma unroll
+  for (int i = 2; i < 16; ++i) o[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// The ciphertexts jl_fdh_kernel marked: r of 2 .. 7 digests (_jls.py:746-762), the whole H row.
+// With compact rows only a sentinel row can be marked (the H rows behind other compact rows are not
+// written by this call: their word 63 is not looked at).
+__global__ void __launch_bounds__(64) jl_fdh_retry_kernel(uint64_t n_ct, JlParams jp, uint32_t* __restrict__ H,
+                                                          uint32_t* __restrict__ stats, const uint32_t* __restrict__ Hc) {
+  const uint64_t kl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (kl >= n_ct) return;
+  if (Hc) {
+    const uint4 a = reinterpret_cast<const uint4*>(Hc + kl * 8)[0];
+    if ((a.x & a.y & a.z & a.w) != ~0u) return;
+  }
+  if (H[kl * 64 + 63] != FBM_FDH_RETRY) return;
+  uint32_t err = 0, st[8];
+  fdh_state_after_t(jp, kl + jp.ct_offset, st);
   uint32_t r[64];
 #pragma unroll
   for (int i = 0; i < 64; ++i) r[i] = 0u;
   bool ok = false;
   for (uint32_t c = 1; c <= 7 && !ok; ++c) {
     uint32_t d[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) d[i] = st[i];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) W[i] = 0u;
-    W[0] = (c << 24) | (0x80u << 16);
-    W[15] = 8200u;
-    fbm_sha256_compress(d, W);
+    fdh_digest(st, c, d);
 #pragma unroll
     for (int i = 63; i >= 8; --i) r[i] = r[i - 8];
 #pragma unroll
@@ -471,18 +529,6 @@ __global__ void __launch_bounds__(256) jl_fdh_kernel(uint64_t n_ct, JlParams jp,
   }
   if (!ok) err |= FBM_ERR_FDH_OVERFLOW;
   if (err) atomicOr(stats + FBM_STAT_ERRFLAGS, err);
-  if (Hc) {  // compact: 32 bytes per ciphertext (one digest), the whole row only behind the sentinel
-    uint32_t wide = 0, ones = ~0u;
-#pragma unroll
-    for (int i = 8; i < 64; ++i) wide |= r[i];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) ones &= r[i];
-    const bool full = wide != 0u || ones == ~0u;  // (a one-digest r of all ones takes the sentinel too)
-    uint4* c = reinterpret_cast<uint4*>(Hc + kl * 8);
-    c[0] = full ? make_uint4(~0u, ~0u, ~0u, ~0u) : make_uint4(r[0], r[1], r[2], r[3]);
-    c[1] = full ? make_uint4(~0u, ~0u, ~0u, ~0u) : make_uint4(r[4], r[5], r[6], r[7]);
-    if (!full) return;
-  }
   uint4* o = reinterpret_cast<uint4*>(H + kl * 64);
 #pragma unroll
   for (int i = 0; i < 16; ++i) o[i] = make_uint4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
@@ -1844,7 +1890,10 @@ int launch_jl_fdh_msg(uint64_t n, const uint32_t* t, int tw, int msg_bytes, int 
 int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s, uint32_t* Hc) {
   if (n_ct == 0) return FBM_OK;
   hipLaunchKernelGGL(jl_fdh_kernel, grid1(n_ct, 256), dim3(256), 0, s, n_ct, jp, H, stats, Hc);
-  return check_launch("jl_fdh_kernel");
+  int rc = check_launch("jl_fdh_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(jl_fdh_retry_kernel, grid1(n_ct, 64), dim3(64), 0, s, n_ct, jp, H, stats, (const uint32_t*)Hc);
+  return check_launch("jl_fdh_retry_kernel");
 }
 
 // Per-call device constants: the schedule travels as a kernel argument (copied by the
