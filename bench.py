@@ -176,6 +176,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-lom-extra", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-to-host (H2D/D2H-inclusive) legs")
+    ap.add_argument("--no-e2e-full-agg", action="store_true",
+                    help="skip the researcher list-API aggregate at the full vector size")
     ap.add_argument("--e2e-list-n", type=int, default=1_000_000, help="elements for the list-API end-to-end leg")
     ap.add_argument("--no-factor-overlap", action="store_true",
                     help="JL: compute the decryption factor inside the aggregate (after the encrypts)")
@@ -301,6 +303,10 @@ def main():
 
         return D.jl_engine(mode) if hasattr(D, "jl_engine") else contextlib.nullcontext()
 
+    # the parties' ciphertexts go straight into their rows of the [P, n_ct, 64] block the aggregate
+    # takes (encrypt_tensor(out=...)): no stacking copy inside the step
+    CT = torch.empty((P, n_ct_step, 64), dtype=torch.int32, device=dev) if args.scheme == "jl" else None
+
     def step_jl(serial=False):
         cts = [None] * P
         factor = None
@@ -316,7 +322,7 @@ def main():
                     s_p.wait_stream(main)
                     with torch.cuda.stream(s_p):
                         cts[p] = jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=weights[p],
-                                                   ct_offset=lo // cr)
+                                                   ct_offset=lo // cr, out=CT[p])
             else:
                 # Kernel order: every prologue (the parties' pack / N*pt+1 / FDH, the factor's FDH),
                 # then every exponentiation, then the factor's inverse.  A running exponentiation
@@ -329,7 +335,7 @@ def main():
                     s_p.wait_stream(main)
                     with torch.cuda.stream(s_p):
                         pend[p] = jc.encrypt_tensor(P, tau, xs[p], keys[p], W.BIPRIME0, weight=weights[p],
-                                                    ct_offset=lo // cr, defer_exp=True)
+                                                    ct_offset=lo // cr, defer_exp=True, out=CT[p])
                 f_s = main if serial else factor_stream
                 if overlap_factor:
                     f_s.wait_stream(main)
@@ -364,11 +370,9 @@ def main():
         if not serial:
             for st in pool + [factor_stream]:
                 main.wait_stream(st)
-            for p in range(P):
-                cts[p].record_stream(main)
             if factor is not None:
                 factor.record_stream(main)
-        out = jc.aggregate_tensor(tau, torch.stack(cts), sk0, W.BIPRIME0, total_w, num_expected_params=n,
+        out = jc.aggregate_tensor(tau, CT, sk0, W.BIPRIME0, total_w, num_expected_params=n,
                                   ct_offset=lo // cr, decrypt_factor=factor)
         if gather:  # the split's final gather: the whole averaged vector on every rank (RCCL all-gather)
             out = distributed.all_gather_shards(out, n_total, cr)
@@ -792,21 +796,43 @@ def main():
 
         node_legs = {str(ne): node_encrypt(ne) for ne in args.node_list_n if ne <= n}
         n2 = W.BIPRIME0 * W.BIPRIME0
-        nct_l = len(cl[0])
-        t0 = time.perf_counter()
-        staged = D.host_empty((P, nct_l, 64), torch.int32)
-        limbs = staged.numpy().view(np.uint32)
-        for u in range(P):
-            D.ints_to_limbs(cl[u], n2, out=limbs[u])
-        cts_l = staged.to(dev)
-        torch.cuda.synchronize()
-        t_conv = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        D.to_host(jc.aggregate_tensor(tau, cts_l, sk0, W.BIPRIME0, total_w, num_expected_params=nl)).numpy().tolist()
-        t_gpu = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        jc.aggregate(tau, P, cl, sk0, W.BIPRIME0, total_w, num_expected_params=nl)
-        t_agg_l = time.perf_counter() - t0
+
+        def researcher_aggregate(cl_u, ne, reps=1):
+            """SecaggCrypter.aggregate(List[List[int]]) of the P parties' lists at ne elements, and the
+            same call's two halves alone: the host conversion (ints -> pinned limbs -> H2D) and the GPU
+            (aggregate_tensor + D2H + float list).  Best of `reps` calls."""
+            nct_u = len(cl_u[0])
+            t0 = time.perf_counter()
+            staged = D.host_empty((P, nct_u, 64), torch.int32)
+            limbs = staged.numpy().view(np.uint32)
+            for u in range(P):
+                D.ints_to_limbs(cl_u[u], n2, out=limbs[u])
+            cts_u = staged.to(dev)
+            torch.cuda.synchronize()
+            t_conv = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            ref_out = D.to_host(jc.aggregate_tensor(tau, cts_u, sk0, W.BIPRIME0, total_w,
+                                                    num_expected_params=ne)).numpy().tolist()
+            t_gpu = time.perf_counter() - t0
+            del cts_u, staged
+            best, res = None, None
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                res = jc.aggregate(tau, P, cl_u, sk0, W.BIPRIME0, total_w, num_expected_params=ne)
+                t = time.perf_counter() - t0
+                best = t if best is None else min(best, t)
+            return {"elements": ne, "parties": P, "ciphertexts_per_party": nct_u, "ms": 1000 * best,
+                    "params_per_s": ne / best, "host_conversion_ms": 1000 * t_conv, "gpu_ms": 1000 * t_gpu,
+                    "equals_tensor_api": res == ref_out}
+
+        agg_l = researcher_aggregate(cl, nl)
+        t_agg_l = agg_l["ms"] / 1000
+        # at the metric's size: the P parties' lists of the step's own 10M-element ciphertexts (CT)
+        agg_full = None
+        if n > nl and not args.no_e2e_full_agg:
+            cl_full = [D.limbs_to_ints(D.to_host(CT[p]).numpy().view(np.uint32)) for p in range(P)]
+            agg_full = researcher_aggregate(cl_full, n, reps=2)
+            del cl_full
         # (c) over the wire: the same updates through a msgpack Serializer configured as the
         #     reference's (strict_types, one {"__type__": "int"} map per big int) vs the
         #     EncryptedParams hook (one bin per update), encrypt -> dumps -> loads -> aggregate
@@ -894,12 +920,12 @@ def main():
             "node_encrypt_list_api": dict(node_legs, note=(
                 "one party's SecaggCrypter.encrypt(List[float]) -> List[int] (the node's call); host_in = list -> "
                 "pinned float64 -> H2D, gpu = the encrypt kernels, host_out = D2H + limbs -> Python ints")),
-            "researcher_aggregate_list_api": {
-                "elements": nl, "parties": P, "ms": 1000 * t_agg_l, "params_per_s": nl / t_agg_l,
-                "host_conversion_ms": 1000 * t_conv, "gpu_ms": 1000 * t_gpu,
-                "note": "SecaggCrypter.aggregate(List[List[int]]) of the P parties' ciphertext lists; host_conversion "
-                        "= ints -> pinned limbs -> H2D alone, gpu = aggregate_tensor + D2H + float list alone; the "
-                        "call itself issues the decryption factor before converting, so ms < the sum"}}
+            "researcher_aggregate_list_api": dict(
+                agg_l, at_metric_size=agg_full,
+                note="SecaggCrypter.aggregate(List[List[int]]) of the P parties' ciphertext lists (at_metric_size: "
+                     "the step's own 10M-element ciphertexts as Python ints, best of 2 calls); host_conversion "
+                     "= ints -> pinned limbs -> H2D alone, gpu = aggregate_tensor + D2H + float list alone; the "
+                     "call itself issues the decryption factor before converting, so ms < the sum")}
 
         # (d) LOM from and to host memory: pinned float32 -> H2D -> protect -> D2H u64 rows (one
         #     stream per party), then H2D of the rows -> aggregate -> D2H float64; and the

@@ -700,13 +700,19 @@ def _check_round(tau: int) -> np.ndarray:
         raise OverflowError("can't convert negative int to unsigned")
     if tau >> JL_ROUND_BITS:
         raise OverflowError("int too big to convert")
+    if tau >> 512 and N.loaded_abi is not None and N.loaded_abi < 3:
+        # an ABI 2 A/B variant (FBM_AB_VARIANT=1) reads 16 of the round's limbs: it would hash tau mod 2^512
+        raise FedbiomedSecaggCrypterError(
+            f"{ErrorNumbers.FB624.value}: the loaded library (ABI {N.loaded_abi}) hashes rounds below 2^512 only")
     return int_limbs(tau, N.TAU_LIMBS)
 
 
 def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, clip=None, target=None,
                weight: int = 1, slot: Optional[Tuple[int, int]] = None, ct_offset: int = 0,
-               defer_exp: bool = False, kind: Optional[str] = None):
+               defer_exp: bool = False, kind: Optional[str] = None, out: Optional[torch.Tensor] = None):
     """One party's JL ciphertexts as an int32 [n_ct, 64] tensor of 32-bit limbs.
+    `out`: a contiguous int32 [n_ct, 64] device tensor to write them into (e.g. this party's row of the
+    [P, n_ct, 64] block the aggregate takes), returned instead of a new one.
     `slot` overrides the (element_size, comp_ratio) packing.  `kind` selects a raw input:
     "u128" = int64 [n, 2] (lo, hi) integers packed into the VES slots (JoyeLibert.protect),
     "pt" = int32 [n, 32] plaintext limbs encrypted as they are (UserKey.encrypt; slot (1, 1)).
@@ -729,7 +735,14 @@ def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, 
     else:
         raise ValueError(f"unknown input kind {kind!r}")
     n_ct = (n + cr - 1) // cr
-    ct = torch.empty((n_ct, 64), dtype=torch.int32, device=dev)
+    if out is None:
+        ct = torch.empty((n_ct, 64), dtype=torch.int32, device=dev)
+    else:
+        if (out.dtype != torch.int32 or tuple(out.shape) != (n_ct, 64) or not out.is_contiguous()
+                or out.device != dev):
+            raise ValueError(f"out must be a contiguous int32 ({n_ct}, 64) tensor on {dev}, got "
+                             f"{out.dtype} {tuple(out.shape)} on {out.device}")
+        ct = out
     if n_ct == 0:
         return ct
     bp = _biprime_limbs(biprime)

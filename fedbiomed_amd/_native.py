@@ -16,8 +16,18 @@ import threading
 import torch  # noqa: F401  (loads the HIP runtime the library must share)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libfbm_secagg.so")
-# A/B measurement of kernel variants (tools/ab.sh): load another build of the same library
-LIB_PATH = os.environ.get("FBM_LIB_PATH", LIB_PATH)
+
+
+def ab_variant() -> bool:
+    """An A/B measurement of a kernel variant (tools/ab.sh) sets FBM_AB_VARIANT=1 next to
+    FBM_LIB_PATH: only then may the library lack newer symbols or be one ABI older."""
+    return os.environ.get("FBM_AB_VARIANT") == "1"
+
+
+def lib_path() -> str:
+    """FBM_LIB_PATH (another build of this library) or the in-tree one."""
+    return os.environ.get("FBM_LIB_PATH") or LIB_PATH
+
 
 ABI_VERSION = 3  # include/fbm_secagg.h FBM_ABI_VERSION
 TAU_LIMBS = 256  # FBM_TAU_LIMBS: the JL round's 32-bit words (< 2^8192)
@@ -42,6 +52,7 @@ STATS_WORDS = 4
 
 _lock = threading.Lock()
 _lib = None
+loaded_abi = None  # fbm_abi_version() of the loaded library (ABI_VERSION, or one less for an A/B variant)
 
 c_u64 = ctypes.c_uint64
 c_dbl = ctypes.c_double
@@ -117,12 +128,14 @@ class NativeUnavailable(RuntimeError):
     """The HIP extension is not built or cannot be loaded."""
 
 
-def load(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Loads (once) and returns the C-ABI library; raises NativeUnavailable."""
-    global _lib
+def load(path: str = None) -> ctypes.CDLL:
+    """Loads (once) and returns the C-ABI library; raises NativeUnavailable.  The library must
+    export every symbol of SIGNATURES and report ABI_VERSION, unless FBM_AB_VARIANT=1."""
+    global _lib, loaded_abi
     with _lock:
         if _lib is not None:
             return _lib
+        path = path or lib_path()
         if not os.path.exists(path):
             raise NativeUnavailable(
                 f"HIP extension not built: {path} is missing (run `python -m fedbiomed_amd._build`)")
@@ -130,20 +143,27 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             lib = ctypes.CDLL(path)
         except OSError as e:  # pragma: no cover - depends on the box
             raise NativeUnavailable(f"cannot load {path}: {e}") from e
-        variant = "FBM_LIB_PATH" in os.environ  # an A/B build (tools/ab.sh) may predate newer symbols
+        variant = ab_variant()  # an A/B build (tools/ab.sh) may predate newer symbols
+        missing = []
         for name, (res, args) in SIGNATURES.items():
             try:
                 fn = getattr(lib, name)
             except AttributeError:
-                if variant:
-                    continue
-                raise
+                missing.append(name)
+                continue
             fn.restype = res
             fn.argtypes = args
-        # (an A/B variant may be one ABI older: ABI 2 reads the first 16 of the round's limbs, the same
-        #  call for every round below 2^512)
-        if lib.fbm_abi_version() != ABI_VERSION and not (variant and lib.fbm_abi_version() == ABI_VERSION - 1):
-            raise NativeUnavailable("ABI version mismatch")
+        if missing and not variant:
+            raise NativeUnavailable(f"{path} lacks {len(missing)} entry point(s) of include/fbm_secagg.h: "
+                                    f"{', '.join(missing[:4])}{' ...' if len(missing) > 4 else ''}")
+        if "fbm_abi_version" in missing:
+            raise NativeUnavailable(f"{path} does not export fbm_abi_version")
+        abi = lib.fbm_abi_version()
+        # (an A/B variant may be one ABI older: ABI 2 reads the first 16 of the round's limbs, so the
+        #  device layer refuses rounds >= 2^512 with it -- _device._check_round)
+        if abi != ABI_VERSION and not (variant and abi == ABI_VERSION - 1):
+            raise NativeUnavailable(f"ABI version mismatch: {path} reports {abi}, this binding needs {ABI_VERSION}")
+        loaded_abi = abi
         _lib = lib
         return lib
 

@@ -414,37 +414,43 @@ static std::atomic<int> g_short_on{1};  // fbm_jl_set_short: 0 forces the window
 // The path a split call (fbm_jl_encrypt_phase / fbm_jl_decrypt_factor_phase) took at its phase 1
 // -- generic or Montgomery engine, short path or not -- keyed by its workspace: the later phases
 // read the constants phase 1 wrote, so they follow phase 1's choice even if the process-wide
-// switches (fbm_jl_set_engine, fbm_jl_set_short) changed in between.  A later phase with no record
-// (the caller never ran phase 1 on this workspace) takes the current switches.
+// switches (fbm_jl_set_engine, fbm_jl_set_short) changed in between.  A later phase whose record is
+// missing (phase 1 never ran on this workspace, or its record was evicted by FBM_PATH_RECS newer
+// split calls) is refused with FBM_E_ARG: it would read constants laid out for a path it cannot know.
+// fbm_jl_clear_caches leaves the records alone (they hold no key material).
 struct JlPathRec {
   const void* ws;
   bool generic, short_on;
 };
+static constexpr size_t FBM_PATH_RECS = 4096;
 static std::mutex g_path_mu;
-static std::vector<JlPathRec> g_path_recs;  // most recent last, at most 256
+static std::vector<JlPathRec> g_path_recs;  // most recent last, at most FBM_PATH_RECS
 
-static void jl_path_for(const void* ws, int phase, int full, const uint32_t* biprime, bool& generic, bool& short_on) {
+static int jl_path_for(const void* ws, int phase, int full, const uint32_t* biprime, bool& generic, bool& short_on) {
   if (!(phase & 1)) {
     std::lock_guard<std::mutex> lk(g_path_mu);
     for (size_t i = g_path_recs.size(); i-- > 0;)
       if (g_path_recs[i].ws == ws) {
         generic = g_path_recs[i].generic || (biprime[0] & 1u) == 0u || jl_is_one(biprime);
         short_on = g_path_recs[i].short_on;
-        return;
+        return FBM_OK;
       }
+    set_error("phase %d of a split call on a workspace with no phase-1 record (run phase 1 on it first)", phase);
+    return FBM_E_ARG;
   }
   generic = jl_generic(biprime);
   short_on = g_short_on.load(std::memory_order_relaxed) != 0;
-  if ((phase & 1) && phase != full) {
+  if (phase != full) {
     std::lock_guard<std::mutex> lk(g_path_mu);
     for (size_t i = 0; i < g_path_recs.size(); ++i)
       if (g_path_recs[i].ws == ws) {
         g_path_recs.erase(g_path_recs.begin() + i);
         break;
       }
-    if (g_path_recs.size() >= 256) g_path_recs.erase(g_path_recs.begin());
+    if (g_path_recs.size() >= FBM_PATH_RECS) g_path_recs.erase(g_path_recs.begin());
     g_path_recs.push_back(JlPathRec{ws, generic, short_on});
   }
+  return FBM_OK;
 }
 
 // GenCtx of (N, key): M = N^2, Barrett constants of M and N, M = 2^e m2 with m2 odd, m2^-1 mod 2^e
@@ -1024,8 +1030,6 @@ void fbm_jl_clear_caches(void) {
     g_jp_cache.clear();  // per-N public parameters
     g_rk_cache.clear();
   }
-  std::lock_guard<std::mutex> lk(g_path_mu);
-  g_path_recs.clear();
 }
 
 int fbm_test_short_cache(uint32_t* out, int cap_words) {
@@ -1256,7 +1260,7 @@ static int jl_encrypt_impl(const void* x, int x_dtype, uint64_t n, double clip, 
     return FBM_E_ARG;
   }
   bool generic, short_on;
-  jl_path_for(workspace, phase, 3, biprime, generic, short_on);
+  if ((rc = jl_path_for(workspace, phase, 3, biprime, generic, short_on))) return rc;
   if (generic) {  // any N (fbm_gen.hip): pack -> FDH -> H^key (N pt + 1) mod N^2
     if (es < 1 || es > 100 || (int64_t)es * cr > 1024) {
       set_error("invalid VES parameters es=%d cr=%d", es, cr);
@@ -1410,7 +1414,7 @@ static int jl_factor_impl(uint64_t n_ct, const uint32_t* biprime, const uint32_t
     return FBM_E_ARG;
   }
   bool generic, short_on;
-  jl_path_for(w.ops, phase, 7, biprime, generic, short_on);
+  if ((rc = jl_path_for(w.ops, phase, 7, biprime, generic, short_on))) return rc;
   if (generic) {  // any N: FDH, then H^key mod N^2 with the inverse in the same kernel
     GenCtx g;
     if ((rc = build_gen_ctx(biprime, key, key_negative, g)) || (rc = fdh_params_for_biprime(biprime, tau, ct_offset, jp)))

@@ -411,7 +411,7 @@ class JoyeLibert:
         if standard:
             tau = _check_tau(tau)
         es, cr = self._vector_encoder._slot(n_user)
-        if es > 128 or es * cr > 1024:  # the reference's two steps, ServerKey.decrypt then VES.decode
+        if es > 100 or es * cr > 1024:  # past the fused kernels' slot (fbm_capi build_jl_params): ServerKey.decrypt, VES.decode
             return self._vector_encoder.decode(sk_0.decrypt(summed, tau), n_user, num_expected_params)
         rows = _term_rows(summed, n)
         factor = None if standard else D.jl_powmod(_bases(sk_0, tau, len(summed), n), n, sk_0.key)

@@ -98,9 +98,12 @@ class SecaggCrypter:
     # ---- device fast path ------------------------------------------------------------------
     def encrypt_tensor(self, num_nodes: int, current_round: int, params: torch.Tensor, key: int, biprime: int,
                        clipping_range: Union[int, None] = None, weight: Optional[int] = None,
-                       target_range: Optional[int] = None, ct_offset: int = 0, defer_exp: bool = False):
+                       target_range: Optional[int] = None, ct_offset: int = 0, defer_exp: bool = False,
+                       out: Optional[torch.Tensor] = None):
         """Device tensor (f32/f64) in HBM -> int32 [n_ct, 64] ciphertext limbs in HBM.
         `ct_offset`: global index of this shard's first ciphertext (element-range sharding).
+        `out`: an int32 [n_ct, 64] destination (e.g. this party's row of the [P, n_ct, 64] block
+        aggregate_tensor takes), as SecaggLomCrypter.encrypt_tensor's.
         `defer_exp`: issue the prologue kernels only and return a PendingEncrypt whose
         finish() issues the exponentiation (several parties on one device: every prologue
         before the first exponentiation occupies the chip)."""
@@ -111,7 +114,7 @@ class SecaggCrypter:
         try:
             return D.jl_encrypt(params, biprime, key, current_round, num_nodes, clip=clipping_range,
                                 target=target_range, weight=1 if weight is None else weight, ct_offset=ct_offset,
-                                defer_exp=defer_exp)
+                                defer_exp=defer_exp, out=out)
         except (TypeError, ValueError) as exp:
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value} Error during parameter encryption. {exp}") from exp
@@ -159,9 +162,13 @@ class SecaggCrypter:
         _check_weight(weight, jl=True)  # after quantize, before the (empty) protect: the reference's order
         if not params:
             return []
+        try:  # the reference derives the slot inside jls.protect, under its try/except (:119-129)
+            _, cr = D.jl_slot(target_range, num_nodes)
+        except (TypeError, ValueError) as exp:
+            raise FedbiomedSecaggCrypterError(
+                f"{ErrorNumbers.FB624.value} Error during parameter encryption. {exp}") from exp
         dev = D.device()
         x = host.to(dev)
-        _, cr = D.jl_slot(target_range, num_nodes)
         stripes = D.list_encrypt_stripes((x.numel() + cr - 1) // cr, dev)
         if len(stripes) == 1:
             ct = self.encrypt_tensor(num_nodes, current_round, x, key, biprime, clipping_range, weight, target_range)

@@ -142,7 +142,9 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
 /* fbm_jl_encrypt in two phases on the same arguments and workspace: phase 1 = the prologue
  * kernels (pack, N*pt+1 digits, FDH, the inverse of H for a negative key), phase 2 = the
  * exponentiation, 3 = both (== fbm_jl_encrypt).  Lets a caller running several parties on one
- * device issue every prologue before the first exponentiation takes the whole chip. */
+ * device issue every prologue before the first exponentiation takes the whole chip.  Phase 2
+ * follows the engine / short-path choice phase 1 made on the same workspace; phase 2 on a
+ * workspace phase 1 never ran on (or one of more than 4 096 newer split calls ago) is FBM_E_ARG. */
 int fbm_jl_encrypt_phase(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
                          uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,
                          const uint32_t* key, int key_negative, const uint32_t* tau, uint64_t ct_offset, uint32_t* ct_out,
@@ -172,7 +174,8 @@ int fbm_jl_aggregate(const uint32_t* cts, int n_parties, uint64_t n_ct, int es, 
 int fbm_jl_decrypt_factor(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative, const uint32_t* tau,
                           uint64_t ct_offset, uint32_t* factor, void* workspace, uint32_t* stats, void* stream);
 /* fbm_jl_decrypt_factor in phases on the same arguments and workspace: bit 1 = constants and
- * FDH, bit 2 = the exponentiation, bit 4 = the inverse (negative key); 7 == fbm_jl_decrypt_factor. */
+ * FDH, bit 2 = the exponentiation, bit 4 = the inverse (negative key); 7 == fbm_jl_decrypt_factor.
+ * Bits 2 and 4 without bit 1 need a phase-1 call on the same workspace first (else FBM_E_ARG). */
 int fbm_jl_decrypt_factor_phase(uint64_t n_ct, const uint32_t* biprime, const uint32_t* key, int key_negative,
                                 const uint32_t* tau, uint64_t ct_offset, uint32_t* factor, void* workspace, uint32_t* stats,
                                 void* stream, int phase);
@@ -323,7 +326,8 @@ int fbm_jl_set_short(int on);
  * SHA-256 digest of (N, |key|), never the key itself, and zeroed here and on eviction -- and the
  * per-biprime public parameters.  The reference keeps nothing between calls (a fresh
  * SecaggCrypter per call, fedbiomed/node/secagg/_secagg_round.py:142); a caller that wants the
- * same can call this after each round.  Thread-safe; in-flight calls are unaffected. */
+ * same can call this after each round.  Thread-safe; in-flight calls are unaffected (a split
+ * call's record of its phase-1 path is kept: it holds no key material). */
 void fbm_jl_clear_caches(void);
 
 /* Batched exponentiation (one-lane engine), for callers that run several parties' encrypts and

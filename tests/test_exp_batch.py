@@ -252,3 +252,45 @@ def test_split_calls_follow_their_phase1_path():
     for p in range(P):
         assert torch.equal(cts[p], ref[p]), p
     torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+def test_split_call_survives_clear_caches_and_refuses_unknown_workspace():
+    """fbm_jl_clear_caches between a split call's phases leaves its phase-1 path
+    record alone (the result equals the unsplit call's even with the switches changed in between),
+    and a later phase on a workspace phase 1 never ran on is FBM_E_ARG, not a guess."""
+    import ctypes
+
+    from fedbiomed_amd import _native
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    dev = D.device()
+    lib = _native.load()
+    P, tau, n = 2, 3, 900
+    key = W.jl_user_key(0)
+    x = torch.from_numpy(W.party_params(0, n)).to(dev)
+    jc = SecaggCrypter()
+    ref = jc.encrypt_tensor(P, tau, x, key, W.BIPRIME0)
+    n_ct = ref.shape[0]
+    sk0 = -key
+    fref = jc.decrypt_factor_tensor(tau, n_ct, sk0, W.BIPRIME0)
+    with D.jl_short(False):
+        pe = jc.encrypt_tensor(P, tau, x, key, W.BIPRIME0, defer_exp=True)
+        pf = jc.decrypt_factor_tensor(tau, n_ct, sk0, W.BIPRIME0, phased=True)
+    lib.fbm_jl_clear_caches()
+    assert torch.equal(pe.finish(), ref)
+    assert torch.equal(pf.exponentiate().finish(), fref)
+    # phase 2 of the factor on a fresh workspace: refused
+    ws = torch.zeros(lib.fbm_jl_aggregate_workspace(n_ct), dtype=torch.uint8, device=dev)
+    st = torch.zeros(_native.STATS_WORDS, dtype=torch.int32, device=dev)
+    out = torch.empty((n_ct, 64), dtype=torch.int32, device=dev)
+    nl = D.int_limbs(W.BIPRIME0, 32)
+    kl = D.int_limbs(abs(sk0), 64)
+    tl = D.int_limbs(tau, _native.TAU_LIMBS)
+    rc = lib.fbm_jl_decrypt_factor_phase(n_ct, nl.ctypes.data, kl.ctypes.data, 1, tl.ctypes.data, 0,
+                                         ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                                         ctypes.c_void_p(st.data_ptr()),
+                                         ctypes.c_void_p(torch.cuda.current_stream().cuda_stream), 2)
+    assert rc == _native.FBM_E_ARG
+    assert "phase-1 record" in _native.last_error()
+    torch.cuda.synchronize()

@@ -212,3 +212,60 @@ def test_fdh_gcd_on_host(lib):
             got = lib.fbm_test_fdh_gcd(r8.ctypes.data, n32.ctypes.data, ctypes.byref(err))
             assert got == int(math.gcd(r, N) == 1), (N, r)
             assert err.value == 0
+
+
+def _stub_lib(tmp_path, abi):
+    """A library with fbm_abi_version() only -- every other entry point missing."""
+    src = tmp_path / "stub.c"
+    src.write_text(f"int fbm_abi_version(void) {{ return {abi}; }}\n")
+    so = tmp_path / f"libstub{abi}.so"
+    import subprocess
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+    return str(so)
+
+
+def _load_in_child(env_extra):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (f"import sys; sys.path.insert(0, {root!r})\n"
+            "from fedbiomed_amd import _native as N\n"
+            "try:\n    N.load(); print('LOADED', N.loaded_abi)\n"
+            "except N.NativeUnavailable as e:\n    print('REFUSED', e)\n")
+    env = dict(os.environ)
+    env.pop("FBM_AB_VARIANT", None)
+    env.update(env_extra)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    return r.stdout.strip()
+
+
+def test_lib_path_override_alone_is_strict(tmp_path):
+    """FBM_LIB_PATH alone: the override is loaded under the shipped checks -- a library missing
+    entry points is NativeUnavailable at load(), not an AttributeError at first use."""
+    out = _load_in_child({"FBM_LIB_PATH": _stub_lib(tmp_path, 3)})
+    assert out.startswith("REFUSED") and "lacks" in out, out
+    out = _load_in_child({"FBM_LIB_PATH": _stub_lib(tmp_path, 2)})
+    assert out.startswith("REFUSED"), out
+
+
+def test_lib_path_override_relaxed_only_for_ab_variants(tmp_path):
+    out = _load_in_child({"FBM_LIB_PATH": _stub_lib(tmp_path, 2), "FBM_AB_VARIANT": "1"})
+    assert out == "LOADED 2", out
+    out = _load_in_child({"FBM_LIB_PATH": _stub_lib(tmp_path, 1), "FBM_AB_VARIANT": "1"})
+    assert out.startswith("REFUSED") and "ABI version mismatch" in out, out
+
+
+def test_abi2_variant_refuses_wide_rounds():
+    from fedbiomed_amd import _device as D, _native as N
+    from fedbiomed_amd.exceptions import FedbiomedSecaggCrypterError
+    saved = N.loaded_abi
+    try:
+        N.loaded_abi = 2
+        assert D._check_round(2 ** 512 - 1)[15] == 0xFFFFFFFF
+        with pytest.raises(FedbiomedSecaggCrypterError):
+            D._check_round(2 ** 512)
+        N.loaded_abi = 3
+        assert D._check_round(2 ** 512)[16] == 1
+    finally:
+        N.loaded_abi = saved

@@ -47,9 +47,20 @@ def test_ves_wide_device_vs_fixture(vw):
 
 @pytest.mark.gpu
 def test_joye_libert_wide_target_round_trip():
-    """JoyeLibert with a target range past the fused kernels' slot (es > 100 bits): protect, aggregate of
+    """JoyeLibert with a target range past the fused kernels' slot (es > 128 bits): protect, aggregate of
     three users' vectors and the exact column sums back (the reference's VES.encode -> UserKey.encrypt and
     ServerKey.decrypt -> VES.decode, each on the device), against the oracle's ciphertexts."""
+    _wide_round_trip(2**150, lambda es: es > 128)
+
+
+@pytest.mark.gpu
+def test_joye_libert_round_trip_slot_between_fused_limits():
+    """100 < es <= 128 (target range 2^90: valuesize 107, es 109): the fused aggregate refuses slots
+    past 100 bits, so aggregate takes the reference's two steps here as protect does."""
+    _wide_round_trip(2**90, lambda es: 100 < es <= 128)
+
+
+def _wide_round_trip(target, es_ok):
     import random
 
     from fedbiomed_amd import workload as W
@@ -57,13 +68,14 @@ def test_joye_libert_wide_target_round_trip():
     from tests.test_jls_api import pp_of
 
     rng = random.Random(77)
-    jl = JoyeLibert(target_range=2**150)
+    vbits = target.bit_length() - 1
+    jl = JoyeLibert(target_range=target)
     es, cr = jl._vector_encoder._get_elements_size_and_compression_ratio(3)
-    assert es > 100
+    assert es_ok(es), es
     n = W.BIPRIME0
     pp = pp_of(n)
     keys = [rng.getrandbits(2040) for _ in range(3)]
-    xs = [[rng.getrandbits(150) for _ in range(2 * cr + 1)] for _ in range(3)]
+    xs = [[rng.getrandbits(vbits) for _ in range(2 * cr + 1)] for _ in range(3)]
     cts = [jl.protect(pp, UserKey(pp, k), 5, x, 3) for k, x in zip(keys, xs)]
     want = [O.jl_user_encrypt(O.ves_encode(x, es, cr), 5, k, n) for k, x in zip(keys, xs)]
     assert cts == want

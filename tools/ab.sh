@@ -10,7 +10,7 @@ mkdir -p $O
 cd $R
 for rep in 1 2; do
   for v in "$@"; do
-    FBM_LIB_PATH=$R/build/ab/$v.so timeout -k 10 300 python bench.py $ARGS > $O/$v.$rep.json 2> $O/$v.$rep.err || { echo "FAIL $v"; tail -5 $O/$v.$rep.err; exit 1; }
+    FBM_AB_VARIANT=1 FBM_LIB_PATH=$R/build/ab/$v.so timeout -k 10 300 python bench.py $ARGS > $O/$v.$rep.json 2> $O/$v.$rep.err || { echo "FAIL $v"; tail -5 $O/$v.$rep.err; exit 1; }
     python - "$O/$v.$rep.json" "$v" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])

@@ -2,7 +2,7 @@
 """LOM aggregate alone (fbm_lom_aggregate) at several (parties, elements) shapes, HIP events on the
 launch stream (the library's own per-kernel events), median of 7: for A/B of library builds (FBM_LIB_PATH).  One JSON line per shape.
 
-    FBM_LIB_PATH=build/ab/x.so python tools/agg_ab.py
+    FBM_AB_VARIANT=1 FBM_LIB_PATH=build/ab/x.so python tools/agg_ab.py
 """
 import json
 import os
