@@ -235,8 +235,47 @@ int launch_ass_split(const uint64_t* secret, uint64_t n, const uint32_t* key, ui
   return check_launch("ass_split_kernel");
 }
 
+// Wave-split reconstruct (round 5) for a compile-time share count S: W waves per workgroup, one tile of 64
+// elements; wave w loads shares w, w + W, ... (16-byte nontemporal loads), the W partial int128 sums meet in
+// LDS and the 64 results leave through the workgroup's first wave.  The lom_aggregate_ws_kernel form
+// (fbm_lom.hip), for config 5's 16-share reconstruct.
+#ifndef FBM_ASS_WS
+#define FBM_ASS_WS 1  // 0: ass_reconstruct_kernel for every share count (A/B base)
+#endif
+template <int W, int S>
+__global__ void __launch_bounds__(64 * W) ass_reconstruct_ws_kernel(const int64_t* __restrict__ shares, uint64_t n,
+                                                                    int64_t* __restrict__ out) {
+  static_assert(S % W == 0, "shares per wave");
+  __shared__ unsigned __int128 part[W][64];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const uint64_t i = (uint64_t)blockIdx.x * 64 + l;
+  typedef long long ll2 __attribute__((ext_vector_type(2)));
+  unsigned __int128 acc = 0;
+  if (i < n) {
+    ll2 v[S / W];
+#pragma unroll
+    for (int k = 0; k < S / W; ++k)
+      v[k] = __builtin_nontemporal_load(reinterpret_cast<const ll2*>(shares + ((uint64_t)(w + W * k) * n + i) * 2));
+#pragma unroll
+    for (int k = 0; k < S / W; ++k) acc += ((unsigned __int128)(uint64_t)v[k].y << 64) | (uint64_t)v[k].x;
+  }
+  part[w][l] = acc;
+  __syncthreads();
+  if (w == 0 && i < n) {
+#pragma unroll
+    for (int q = 1; q < W; ++q) acc += part[q][l];
+    const ll2 r = {(long long)(uint64_t)acc, (long long)(uint64_t)(acc >> 64)};
+    __builtin_nontemporal_store(r, reinterpret_cast<ll2*>(out + i * 2));
+  }
+}
+
 int launch_ass_reconstruct(const int64_t* shares, int n_shares, uint64_t n, int64_t* out, hipStream_t s) {
   if (n == 0) return FBM_OK;
+  if (FBM_ASS_WS && n_shares == 16) {
+    hipLaunchKernelGGL((ass_reconstruct_ws_kernel<8, 16>), dim3((unsigned)((n + 63) / 64)), dim3(512), 0, s, shares, n,
+                       out);
+    return check_launch("ass_reconstruct_ws_kernel");
+  }
   hipLaunchKernelGGL(ass_reconstruct_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, shares, n_shares,
                      n, out);
   return check_launch("ass_reconstruct_kernel");

@@ -275,6 +275,70 @@ __global__ void __launch_bounds__(256) lom_aggregate_kernel(const uint64_t* __re
   if (err && out) atomicOr(stats + FBM_STAT_ERRFLAGS, FBM_ERR_DEQUANT_RANGE);
 }
 
+// Wave-split column sum (round 5) for a compile-time party count PC: a workgroup of W waves owns one
+// tile of 64*EPT elements; wave w loads rows w, w + W, ... (PC / W rows of 16-byte nontemporal loads per
+// lane), the W partial sums meet in LDS, and the epilogue (average, dequantise, nontemporal stores of the
+// float64 output and the u64 sums) is spread over the workgroup's threads.  Against lom_aggregate_kernel
+// (one thread loads all PC rows of its 2 elements) at config 5's 16 x 100M on one box: 6.05 -> 6.68 TB/s
+// (tools/microbench/agg_variants.hip, profiles/r5c_agg_variants.jsonl): fewer rows per lane keep more
+// waves resident with the same bytes in flight, and the epilogue's division no longer serialises wave 0.
+// Needs n % EPT == 0 and 16-byte aligned rows (the launcher checks); the last tile is bounds-checked.
+#ifndef FBM_AGG_WS
+#define FBM_AGG_WS 1  // 0: every party count takes lom_aggregate_kernel (A/B base)
+#endif
+#ifndef FBM_AGG_WS_W8
+#define FBM_AGG_WS_W8 4  // waves per workgroup at 8 parties (two rows per wave)
+#endif
+template <int EPT, int W, int PC>
+__global__ void __launch_bounds__(64 * W) lom_aggregate_ws_kernel(const uint64_t* __restrict__ y, uint64_t n,
+                                                                  uint64_t total_weight, double neg_c, double step,
+                                                                  double* __restrict__ out,
+                                                                  uint64_t* __restrict__ sums,
+                                                                  uint32_t* __restrict__ stats) {
+  static_assert(PC % W == 0, "rows per wave");
+  constexpr int TILE = 64 * EPT, RPW = PC / W;
+  __shared__ uint64_t part[W][TILE];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const uint64_t base = (uint64_t)blockIdx.x * TILE;
+  const uint64_t i = base + (uint64_t)l * EPT;
+  uint64_t sm[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) sm[e] = 0;
+  if (base + TILE <= n) {
+    uint64_t v[RPW][EPT];
+#pragma unroll
+    for (int p = 0; p < RPW; ++p) {
+      const uint64_t* row =
+          static_cast<const uint64_t*>(__builtin_assume_aligned(y + (uint64_t)(w + W * p) * n + i, EPT * 8));
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) v[p][e] = __builtin_nontemporal_load(row + e);
+    }
+#pragma unroll
+    for (int p = 0; p < RPW; ++p)
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) sm[e] += v[p][e];
+  } else {
+#pragma unroll
+    for (int p = 0; p < RPW; ++p)
+#pragma unroll
+      for (int e = 0; e < EPT; ++e)
+        if (i + e < n) sm[e] += __builtin_nontemporal_load(y + (uint64_t)(w + W * p) * n + i + e);
+  }
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) part[w][l * EPT + e] = sm[e];
+  __syncthreads();
+  uint32_t err = 0;
+  for (int e = threadIdx.x; e < TILE; e += 64 * W) {
+    if (base + e >= n) break;
+    uint64_t s = 0;
+#pragma unroll
+    for (int q = 0; q < W; ++q) s += part[q][e];
+    if (out) __builtin_nontemporal_store(lom_avg_dequant(s, total_weight, neg_c, step, err), out + base + e);
+    if (sums) __builtin_nontemporal_store(s, sums + base + e);
+  }
+  if (err && out) atomicOr(stats + FBM_STAT_ERRFLAGS, FBM_ERR_DEQUANT_RANGE);
+}
+
 int launch_lom_protect(const void* x, int x_dtype, uint64_t n, const QuantParams& qp, uint64_t weight,
                        const LomPeers& peers, uint64_t* y, uint32_t* stats, hipStream_t s) {
   if (n == 0) return FBM_OK;
@@ -327,6 +391,17 @@ int launch_prf_key(const LomPeers& peers, uint32_t* seed_out, hipStream_t s) {
 int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t total_weight, double neg_c, double step,
                          double* out, uint64_t* sums, uint32_t* stats, hipStream_t s) {
   if (n == 0) return FBM_OK;
+  const bool aligned = (n % 2) == 0 && (reinterpret_cast<uintptr_t>(y) % 16) == 0;
+  if (FBM_AGG_WS && aligned && (n_parties == 16 || n_parties == 8)) {
+    const dim3 grid((unsigned)((n + 127) / 128));
+    if (n_parties == 16)
+      hipLaunchKernelGGL((lom_aggregate_ws_kernel<2, 8, 16>), grid, dim3(512), 0, s, y, n, total_weight, neg_c, step,
+                         out, sums, stats);
+    else
+      hipLaunchKernelGGL((lom_aggregate_ws_kernel<2, FBM_AGG_WS_W8, 8>), grid, dim3(64 * FBM_AGG_WS_W8), 0, s, y, n,
+                         total_weight, neg_c, step, out, sums, stats);
+    return check_launch("lom_aggregate_ws_kernel");
+  }
   constexpr int EPT = FBM_AGG_EPT;
   const uint64_t ngrp = (n + EPT - 1) / EPT;
   uint64_t g = (ngrp + 255) / 256;
