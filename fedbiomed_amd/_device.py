@@ -992,18 +992,30 @@ def _rows_of(vals: List[int], w: int) -> np.ndarray:
 
 
 def ves_pack_any(V: List[int], es: int, cr: int, dev=None) -> List[int]:
-    """VES.encode of any shape (fbm_ves_pack): non-negative ints of any width, slots of any es, plaintexts
-    of any width; the reference's OR packing (_jls.py:118-144, 169-176)."""
+    """VES.encode of any shape (fbm_ves_pack): ints of any width and sign, slots of any es, plaintexts of
+    any width; the reference's OR packing (_jls.py:118-144, 169-176).  With a negative value the rows go
+    to the device in two's complement (one sign bit above the widest value) and its sign extends to the top
+    of its plaintext, which comes back as Python's negative OR: the pw-word pattern minus 2^(32 pw)."""
     dev = dev or device()
     if not V:
         return []
-    wv = max(1, (max(v.bit_length() for v in V) + 31) // 32)
+    signed = min(V) < 0
+    if signed and (N.loaded_abi or 0) < 4:
+        raise FedbiomedSecaggCrypterError(
+            f"{ErrorNumbers.FB624.value}: VES.encode of negative values needs an ABI 4 library (loaded: "
+            f"ABI {N.loaded_abi})")
+    wv = max(1, (max(v.bit_length() for v in V) + (1 if signed else 0) + 31) // 32)
     pw = (es * (cr - 1) + 32 * wv + 31) // 32
     n_ct = (len(V) + cr - 1) // cr
-    x = torch.from_numpy(_rows_of(V, wv).view(np.int32)).to(dev)
+    rows = [v & ((1 << (32 * wv)) - 1) for v in V] if signed else V  # two's complement rows
+    x = torch.from_numpy(_rows_of(rows, wv).view(np.int32)).to(dev)
     pt = torch.empty((n_ct, pw), dtype=torch.int32, device=dev)
-    _call(N.load().fbm_ves_pack, _ptr(x), len(V), wv, es, cr, pw, _ptr(pt), _stream())
-    return limbs_to_ints_w(pt, pw)
+    _call(N.load().fbm_ves_pack, _ptr(x), len(V), wv, es, cr, pw, 1 if signed else 0, _ptr(pt), _stream())
+    out = limbs_to_ints_w(pt, pw)
+    if signed:
+        top, full = 1 << (32 * pw - 1), 1 << (32 * pw)
+        out = [e - full if e & top else e for e in out]
+    return out
 
 
 def ves_unpack_any(E: List[int], es: int, cr: int, v_expected: int, dev=None) -> List[int]:
@@ -1067,7 +1079,8 @@ def jl_fdh(n_ct: int, modulus: int, tau: int, ct_offset: int = 0, dev=None) -> t
 
 
 def jl_fdh_msg(ts: List[int], bits_size: int, modulus: int, dev=None) -> torch.Tensor:
-    """FDH(bits_size, modulus).H(t) for each t (any bits_size; fbm_jl_fdh_msg) -> int32 [len(ts), 128] limbs.
+    """FDH(bits_size, modulus).H(t) for each t (any bits_size; fbm_jl_fdh_msg) -> int32 [len(ts), hw] limbs
+    (hw = fbm_jl_fdh_msg_row_words(bits_size): 128, or 8 per digest when r may take 16 .. 255 digests).
     The reference's to_bytes errors are raised here first: t < 0 and t >= 2^(8 (bits_size // 2))."""
     L = bits_size // 2
     if L < 0:
@@ -1083,11 +1096,13 @@ def jl_fdh_msg(ts: List[int], bits_size: int, modulus: int, dev=None) -> torch.T
     for i, t in enumerate(ts):
         host[i] = int_limbs(t, tw)
     odd, even = fdh_modulus(modulus)
-    h = torch.empty((len(ts), 128), dtype=torch.int32, device=dev)
+    lib = N.load()
+    hw = int(lib.fbm_jl_fdh_msg_row_words(int(bits_size)))  # 128, or 8 per digest past 15 (ABI 4)
+    h = torch.empty((len(ts), hw), dtype=torch.int32, device=dev)
     st = _stats(dev)
     t_dev = torch.from_numpy(host.view(np.int32)).to(dev)
-    _call(N.load().fbm_jl_fdh_msg, len(ts), _ptr(t_dev), tw, int(bits_size), _np_ptr(int_limbs(odd, 32)),
-          1 if even else 0, _ptr(h), _ptr(st), _stream())
+    _call(lib.fbm_jl_fdh_msg, len(ts), _ptr(t_dev), tw, int(bits_size), _np_ptr(int_limbs(odd, 32)),
+          1 if even else 0, _ptr(h), hw, _ptr(st), _stream())
     _check_stats(st)
     return h
 

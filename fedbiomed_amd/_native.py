@@ -29,7 +29,7 @@ def lib_path() -> str:
     return os.environ.get("FBM_LIB_PATH") or LIB_PATH
 
 
-ABI_VERSION = 3  # include/fbm_secagg.h FBM_ABI_VERSION
+ABI_VERSION = 4  # include/fbm_secagg.h FBM_ABI_VERSION
 TAU_LIMBS = 256  # FBM_TAU_LIMBS: the JL round's 32-bit words (< 2^8192)
 FBM_OK = 0
 FBM_E_ARG = -1
@@ -98,10 +98,11 @@ SIGNATURES = {
     "fbm_jl_pack": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_vp, c_vp, c_vp]),
     "fbm_jl_unpack": (c_int, [c_vp, c_u64, c_int, c_int, c_u64, c_vp, c_vp]),
     "fbm_jl_fdh": (c_int, [c_u64, c_vp, c_int, c_vp, c_u64, c_vp, c_vp, c_vp]),
-    "fbm_jl_fdh_msg": (c_int, [c_u64, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp]),
+    "fbm_jl_fdh_msg": (c_int, [c_u64, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp]),
+    "fbm_jl_fdh_msg_row_words": (c_int, [c_int]),
     "fbm_int_true_div_big": (c_int, [c_vp, c_u64, c_vp, c_int, c_int, c_vp, c_vp]),
     "fbm_test_true_div_big": (c_int, [c_vp, c_u64, c_vp, c_int, c_int, c_vp]),
-    "fbm_ves_pack": (c_int, [c_vp, c_u64, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    "fbm_ves_pack": (c_int, [c_vp, c_u64, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     "fbm_ves_unpack": (c_int, [c_vp, c_u64, c_int, c_int, c_int, c_u64, c_int, c_vp, c_vp]),
     "fbm_jl_product": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_decrypt": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp, c_int, c_vp, c_u64, c_vp, c_vp, c_vp, c_vp]),

@@ -1056,9 +1056,8 @@ int fbm_check_stats(const uint32_t* st, int lom_nodes, uint32_t* max_bits_out) {
     set_error("FDH: no r of 1..7 digests with gcd(r, N^2) == 1 (reference: OverflowError)");
     return FBM_E_FDH;
   }
-  if (f & FBM_ERR_FDH_WIDE) {
-    set_error("FDH: no coprime r of 1..15 digests; the reference would try 16 or more (bits_size > 4096): "
-              "outside the device path's domain");
+  if (f & FBM_ERR_FDH_WIDE) {  // (no kernel reports it since round 5: r of up to 255 digests runs on the device)
+    set_error("FDH: r wider than the device path's rows");
     return FBM_E_UNSUPPORTED;
   }
   if (f & FBM_ERR_NOT_INVERTIBLE) {
@@ -1660,7 +1659,7 @@ int fbm_jl_fdh(uint64_t n_ct, const uint32_t* modulus_odd, int modulus_even, con
 }
 
 int fbm_jl_fdh_msg(uint64_t n, const uint32_t* t, int t_words, int bits_size, const uint32_t* modulus_odd,
-                   int modulus_even, uint32_t* h, uint32_t* stats, void* stream) {
+                   int modulus_even, uint32_t* h, int h_words, uint32_t* stats, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   int rc = zero_stats(stats, s);
   if (rc) return rc;
@@ -1689,9 +1688,38 @@ int fbm_jl_fdh_msg(uint64_t n, const uint32_t* t, int t_words, int bits_size, co
     set_error("null pointer argument");
     return FBM_E_ARG;
   }
+  const int need = fbm_jl_fdh_msg_row_words(bits_size);
+  if (h_words < need) {
+    set_error("fbm_jl_fdh_msg: rows of %d words hold no r of bits_size %d (%d words)", h_words, bits_size, need);
+    return FBM_E_ARG;
+  }
+  if (kmax <= FBM_FDH_MSG_DIGESTS) {
+    if (h_words != FBM_FDH_MSG_ROW) {
+      set_error("fbm_jl_fdh_msg: bits_size %d takes rows of %d words", bits_size, FBM_FDH_MSG_ROW);
+      return FBM_E_ARG;
+    }
+    return timed("jl_fdh", s, [&] {
+      return launch_jl_fdh_msg(n, t, t_words, msg_bytes, kmax, modulus_odd, modulus_even ? 1 : 0, h, stats, s);
+    });
+  }
+  // r of up to 255 digests: the incremental Montgomery residue of the wide kernel (fbm_jl.hip)
+  Big m(modulus_odd, modulus_odd + 32);
+  uint32_t inv = m[0];  // Newton: m^-1 mod 2^32
+  for (int i = 0; i < 5; ++i) inv *= 2u - m[0] * inv;
+  Big k1 = big_pow2_mod(1024 + 256, m), k2 = big_pow2_mod(2048, m);
+  k1.resize(32, 0u);
+  k2.resize(32, 0u);
   return timed("jl_fdh", s, [&] {
-    return launch_jl_fdh_msg(n, t, t_words, msg_bytes, kmax, modulus_odd, modulus_even ? 1 : 0, h, stats, s);
+    return launch_jl_fdh_msg_wide(n, t, t_words, msg_bytes, kmax, m.data(), k1.data(), k2.data(), 0u - inv,
+                                  modulus_even ? 1 : 0, h, h_words, stats, s);
   });
+}
+
+int fbm_jl_fdh_msg_row_words(int bits_size) {
+  const int bytes = bits_size / 8;
+  int kmax = bytes >= 1 ? (bytes - 1) / 32 : 0;
+  if (kmax > 255) kmax = 255;
+  return kmax <= FBM_FDH_MSG_DIGESTS ? FBM_FDH_MSG_ROW : 8 * kmax;
 }
 
 int fbm_jl_product(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* biprime, uint32_t* out,
@@ -1845,7 +1873,8 @@ int fbm_int_ops(const uint64_t* x, uint64_t n, uint64_t k, int op, void* out, ui
   });
 }
 
-int fbm_ves_pack(const uint32_t* x, uint64_t n, int wv, int es, int cr, int pw, uint32_t* pt, void* stream) {
+int fbm_ves_pack(const uint32_t* x, uint64_t n, int wv, int es, int cr, int pw, int is_signed, uint32_t* pt,
+                 void* stream) {
   if (wv < 1 || es < 1 || cr < 1 || pw < 1 || (int64_t)es * (cr - 1) + 32ll * wv > 32ll * pw) {
     set_error("fbm_ves_pack: bad shape (wv=%d es=%d cr=%d pw=%d)", wv, es, cr, pw);
     return FBM_E_ARG;
@@ -1854,7 +1883,8 @@ int fbm_ves_pack(const uint32_t* x, uint64_t n, int wv, int es, int cr, int pw, 
     set_error("null pointer argument");
     return FBM_E_ARG;
   }
-  return timed("ves_pack", (hipStream_t)stream, [&] { return launch_ves_pack(x, n, wv, es, cr, pw, pt, (hipStream_t)stream); });
+  return timed("ves_pack", (hipStream_t)stream,
+               [&] { return launch_ves_pack(x, n, wv, es, cr, pw, is_signed ? 1 : 0, pt, (hipStream_t)stream); });
 }
 
 int fbm_ves_unpack(const uint32_t* pt, uint64_t n_ct, int pw, int es, int cr, uint64_t n_out, int ow, uint32_t* vals,

@@ -190,13 +190,17 @@ int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, int ne
 // nullptr: every row whole in H (the generic engine, fbm_jl_fdh)
 int launch_jl_fdh(uint64_t n_ct, const JlParams& jp, uint32_t* H, uint32_t* stats, hipStream_t s, uint32_t* Hc = nullptr);
 // VES of any shape (fbm_ves_pack / fbm_ves_unpack)
-int launch_ves_pack(const uint32_t* x, uint64_t n, int wv, int es, int cr, int pw, uint32_t* pt, hipStream_t s);
+int launch_ves_pack(const uint32_t* x, uint64_t n, int wv, int es, int cr, int pw, int sgn, uint32_t* pt,
+                    hipStream_t s);
 int launch_ves_unpack(const uint32_t* pt, int pw, int es, int cr, uint64_t n_out, int ow, uint32_t* vals, hipStream_t s);
 // FDH.H of any bits_size: one lane per t (tw-word rows), message t.to_bytes(msg_bytes) || counter, r of at
 // most kmax digests (fbm_jl_fdh_msg; r of up to FBM_FDH_MSG_DIGESTS digests, FBM_FDH_MSG_ROW-word rows)
 #define FBM_FDH_MSG_DIGESTS 15
 #define FBM_FDH_MSG_WORDS (8 * FBM_FDH_MSG_DIGESTS)
 #define FBM_FDH_MSG_ROW 128
+int launch_jl_fdh_msg_wide(uint64_t n, const uint32_t* t, int tw, int msg_bytes, int kmax, const uint32_t* m32,
+                           const uint32_t* k1, const uint32_t* k2, uint32_t mp, int even, uint32_t* H, int hw,
+                           uint32_t* stats, hipStream_t s);
 int launch_jl_fdh_msg(uint64_t n, const uint32_t* t, int tw, int msg_bytes, int kmax, const uint32_t* n32, int even,
                       uint32_t* H, uint32_t* stats, hipStream_t s);
 int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32_t* cst, hipStream_t s,

@@ -149,10 +149,22 @@ __device__ __forceinline__ uint32_t bits32_at(const uint32_t* v, int w, int off)
   const uint32_t hi = b && i + 1 < w ? v[i + 1] : 0u;
   return b ? (lo >> b) | (hi << (32 - b)) : lo;
 }
+// the same for a two's-complement value of w words: past its top word the sign bit repeats (Python's ints)
+__device__ __forceinline__ uint32_t bits32_at_signed(const uint32_t* v, int w, int off) {
+  const uint32_t ext = (v[w - 1] >> 31) ? ~0u : 0u;
+  if (off < 0) return -off < 32 ? v[0] << (-off) : 0u;
+  const int i = off >> 5, b = off & 31;
+  const uint32_t lo = i < w ? v[i] : ext;
+  const uint32_t hi = i + 1 < w ? v[i + 1] : ext;
+  return b ? (lo >> b) | (hi << (32 - b)) : lo;
+}
 // encode: one thread per plaintext word; slot j's value ORed in at bit es j, its bits past the slot into
-// the next slots (the reference's a |= v << es j)
+// the next slots (the reference's a |= v << es j).  sgn: the values are two's complement (ABI 4): a
+// negative one's sign extends to the plaintext's top word, whose top bit then marks the plaintext negative
+// (Python's OR of a negative int), and every lower slot can reach word L.
 __global__ void __launch_bounds__(256) ves_pack_kernel(const uint32_t* __restrict__ x, uint64_t n, int wv, int es,
-                                                       int cr, int pw, uint64_t n_ct, uint32_t* __restrict__ pt) {
+                                                       int cr, int pw, int sgn, uint64_t n_ct,
+                                                       uint32_t* __restrict__ pt) {
   const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t ct = gid / (uint64_t)pw;
   const int L = (int)(gid % (uint64_t)pw);
@@ -160,11 +172,16 @@ __global__ void __launch_bounds__(256) ves_pack_kernel(const uint32_t* __restric
   const uint64_t first = ct * (uint64_t)cr;
   const int cnt = (n - first) >= (uint64_t)cr ? cr : (int)(n - first);
   const int64_t lo_bit = 32ll * L;
-  int64_t j0 = lo_bit - 32ll * wv + 1 > 0 ? (lo_bit - 32ll * wv + 1 + es - 1) / es : 0;
+  int64_t j0 = !sgn && lo_bit - 32ll * wv + 1 > 0 ? (lo_bit - 32ll * wv + 1 + es - 1) / es : 0;
   int64_t j1 = (lo_bit + 31) / es;
   if (j1 > cnt - 1) j1 = cnt - 1;
   uint32_t w = 0;
-  for (int64_t j = j0; j <= j1; ++j) w |= bits32_at(x + (first + j) * (uint64_t)wv, wv, (int)(lo_bit - es * j));
+  if (sgn) {
+    for (int64_t j = j0; j <= j1; ++j)
+      w |= bits32_at_signed(x + (first + j) * (uint64_t)wv, wv, (int)(lo_bit - es * j));
+  } else {
+    for (int64_t j = j0; j <= j1; ++j) w |= bits32_at(x + (first + j) * (uint64_t)wv, wv, (int)(lo_bit - es * j));
+  }
   pt[ct * (uint64_t)pw + L] = w;
 }
 // decode: one thread per output word; value o = slot o % cr of plaintext o / cr, masked to es bits
@@ -580,15 +597,10 @@ __device__ __forceinline__ uint32_t fdh_msg_byte(const uint32_t* t, int L, int i
   const int j = L - 1 - i;
   return (t[j >> 2] >> (8 * (j & 3))) & 0xFFu;
 }
-__global__ void __launch_bounds__(64) jl_fdh_msg_kernel(uint64_t n, const uint32_t* __restrict__ t, int tw, int L,
-                                                        int kmax, FdhModArg m, uint32_t* __restrict__ H,
-                                                        uint32_t* __restrict__ stats) {
-  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  const uint32_t* tr = t + k * (uint64_t)tw;
-  uint32_t st[8], W[16];
+// SHA-256 state after the F blocks made of t's bytes alone (shared by every counter)
+__device__ __noinline__ void fdh_msg_prefix(const uint32_t* tr, int L, int F, uint32_t (&st)[8]) {
+  uint32_t W[16];
   fbm_sha256_init(st);
-  const int F = L / 64;  // blocks of t bytes only: the same for every counter
 #pragma unroll 1
   for (int b = 0; b < F; ++b) {
 #pragma unroll 1
@@ -599,6 +611,41 @@ __global__ void __launch_bounds__(64) jl_fdh_msg_kernel(uint64_t n, const uint32
     }
     fbm_sha256_compress(st, W);
   }
+}
+// digest of counter c: the prefix state, then the tail blocks (t's last bytes, c, 0x80, the 64-bit length)
+__device__ __noinline__ void fdh_msg_digest(const uint32_t (&st)[8], const uint32_t* tr, int L, int F, int rem, int nb,
+                                            uint64_t len_bits, int c, uint32_t (&d)[8]) {
+  uint32_t W[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) d[i] = st[i];
+#pragma unroll 1
+  for (int b = 0; b < nb; ++b) {
+#pragma unroll 1
+    for (int j = 0; j < 16; ++j) {
+      uint32_t w = 0;
+      for (int q = 0; q < 4; ++q) {
+        const int p = 64 * b + 4 * j + q;
+        uint32_t v = 0;
+        if (p < rem) v = fdh_msg_byte(tr, L, 64 * F + p);
+        else if (p == rem) v = (uint32_t)c;
+        else if (p == rem + 1) v = 0x80u;
+        else if (p >= 64 * nb - 8) v = (uint32_t)(len_bits >> (8 * (64 * nb - 1 - p))) & 0xFFu;
+        w = (w << 8) | v;
+      }
+      W[j] = w;
+    }
+    fbm_sha256_compress(d, W);
+  }
+}
+__global__ void __launch_bounds__(64) jl_fdh_msg_kernel(uint64_t n, const uint32_t* __restrict__ t, int tw, int L,
+                                                        int kmax, FdhModArg m, uint32_t* __restrict__ H,
+                                                        uint32_t* __restrict__ stats) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t* tr = t + k * (uint64_t)tw;
+  uint32_t st[8];
+  const int F = L / 64;                          // blocks of t bytes only: the same for every counter
+  fdh_msg_prefix(tr, L, F, st);
   const int rem = L - 64 * F;                    // t bytes left for the tail
   const int nb = (rem + 1 + 1 + 8 + 63) / 64;    // + counter, 0x80, 64-bit length: 1 or 2 blocks
   const uint64_t len_bits = 8ull * (uint64_t)(L + 1);
@@ -611,26 +658,7 @@ __global__ void __launch_bounds__(64) jl_fdh_msg_kernel(uint64_t n, const uint32
 #pragma unroll 1
   for (int c = 1; c <= kuse && !ok; ++c) {
     uint32_t d[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) d[i] = st[i];
-#pragma unroll 1
-    for (int b = 0; b < nb; ++b) {
-#pragma unroll 1
-      for (int j = 0; j < 16; ++j) {
-        uint32_t w = 0;
-        for (int q = 0; q < 4; ++q) {
-          const int p = 64 * b + 4 * j + q;
-          uint32_t v = 0;
-          if (p < rem) v = fdh_msg_byte(tr, L, 64 * F + p);
-          else if (p == rem) v = (uint32_t)c;
-          else if (p == rem + 1) v = 0x80u;
-          else if (p >= 64 * nb - 8) v = (uint32_t)(len_bits >> (8 * (64 * nb - 1 - p))) & 0xFFu;
-          w = (w << 8) | v;
-        }
-        W[j] = w;
-      }
-      fbm_sha256_compress(d, W);
-    }
+    fdh_msg_digest(st, tr, L, F, rem, nb, len_bits, c, d);
 #pragma unroll 1
     for (int i = FBM_FDH_MSG_WORDS - 1; i >= 8; --i) r[i] = r[i - 8];
 #pragma unroll
@@ -649,10 +677,133 @@ __global__ void __launch_bounds__(64) jl_fdh_msg_kernel(uint64_t n, const uint32
       ok = gcd_is_one_w<FBM_FDH_MSG_WORDS>(u, m.n32, err);
     }
   }
-  if (!ok) err |= kmax > FBM_FDH_MSG_DIGESTS ? FBM_ERR_FDH_WIDE : FBM_ERR_FDH_OVERFLOW;
+  if (!ok) err |= FBM_ERR_FDH_OVERFLOW;  // (kmax <= FBM_FDH_MSG_DIGESTS here: wider FDHs take the wide kernel)
   uint32_t* o = H + k * FBM_FDH_MSG_ROW;
 #pragma unroll 1
   for (int i = 0; i < FBM_FDH_MSG_ROW; ++i) o[i] = i < FBM_FDH_MSG_WORDS ? r[i] : 0u;
+  if (err) atomicOr(stats + FBM_STAT_ERRFLAGS, err);
+}
+
+// FDH.H of bits_size > 4096 (round 5): r may need 16 .. 255 digests (the counter byte caps it at 255), too
+// wide for registers.  Each digest goes to the output row as it is made (block c - 1, digest order; the
+// blocks are reversed into r's little-endian word order at the end), and coprimality is decided on
+// y = r R mod m (R = 2^1024, m the modulus's odd part, a unit factor that leaves gcd(r, m) alone), kept as
+// r grows: y <- y 2^256 + D R = mont(y, K1) + mont(D, K2), K1 = 2^256 R, K2 = R^2 (mod m), then a 32-word
+// binary gcd of (y, m).  An even M also needs r odd: the last digest's low bit.
+struct FdhWideArg {
+  uint32_t m[32], k1[32], k2[32];
+  uint32_t mp;  // -m^-1 mod 2^32
+  int even;
+};
+// a b R^-1 mod m, a < R, b < m: CIOS over 32 words, result < m
+__device__ __noinline__ void fdh_mont32(const uint32_t (&a)[32], const uint32_t* b, const FdhWideArg& w,
+                                        uint32_t (&o)[32]) {
+  uint32_t t[34];
+#pragma unroll
+  for (int j = 0; j < 34; ++j) t[j] = 0u;
+#pragma unroll 1
+  for (int i = 0; i < 32; ++i) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const uint64_t v = (uint64_t)a[j] * b[i] + t[j] + c;
+      t[j] = (uint32_t)v;
+      c = v >> 32;
+    }
+    uint64_t v = (uint64_t)t[32] + c;
+    t[32] = (uint32_t)v;
+    t[33] = (uint32_t)(v >> 32);
+    const uint32_t q = t[0] * w.mp;
+    c = ((uint64_t)q * w.m[0] + t[0]) >> 32;
+#pragma unroll
+    for (int j = 1; j < 32; ++j) {
+      const uint64_t x = (uint64_t)q * w.m[j] + t[j] + c;
+      t[j - 1] = (uint32_t)x;
+      c = x >> 32;
+    }
+    v = (uint64_t)t[32] + c;
+    t[31] = (uint32_t)v;
+    t[32] = t[33] + (uint32_t)(v >> 32);
+  }
+  // t < 2m: subtract m once if t >= m
+  uint32_t s[32], br = 0;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const uint64_t d = (uint64_t)t[j] - w.m[j] - br;
+    s[j] = (uint32_t)d;
+    br = (uint32_t)(d >> 63);
+  }
+  const bool ge = t[32] || !br;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) o[j] = ge ? s[j] : t[j];
+}
+
+__global__ void __launch_bounds__(64) jl_fdh_msg_wide_kernel(uint64_t n, const uint32_t* __restrict__ t, int tw, int L,
+                                                             int kmax, FdhWideArg w, uint32_t* __restrict__ H, int hw,
+                                                             uint32_t* __restrict__ stats) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t* tr = t + k * (uint64_t)tw;
+  uint32_t st[8];
+  const int F = L / 64;
+  fdh_msg_prefix(tr, L, F, st);
+  const int rem = L - 64 * F;
+  const int nb = (rem + 1 + 1 + 8 + 63) / 64;
+  const uint64_t len_bits = 8ull * (uint64_t)(L + 1);
+  const int kuse = kmax < 255 ? kmax : 255;  // counter.to_bytes(1) overflows at 256
+  uint32_t* o = H + k * (uint64_t)hw;
+  uint32_t y[32], err = 0;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) y[i] = 0u;
+  bool ok = false;
+  int c = 0;
+#pragma unroll 1
+  while (!ok && c < kuse) {
+    ++c;
+    uint32_t d[8];
+    fdh_msg_digest(st, tr, L, F, rem, nb, len_bits, c, d);
+    uint32_t D[32], a[32], b[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) D[i] = i < 8 ? d[7 - i] : 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[8 * (c - 1) + i] = D[i];
+    fdh_mont32(y, w.k1, w, a);  // y 2^256
+    fdh_mont32(D, w.k2, w, b);  // D R
+    uint32_t s[32], br = 0;
+    uint64_t cy = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const uint64_t v = (uint64_t)a[i] + b[i] + cy;
+      y[i] = (uint32_t)v;
+      cy = v >> 32;
+    }
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const uint64_t v = (uint64_t)y[i] - w.m[i] - br;
+      s[i] = (uint32_t)v;
+      br = (uint32_t)(v >> 63);
+    }
+    const bool ge = cy || !br;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) y[i] = ge ? s[i] : y[i];
+    if (w.even && !(D[0] & 1u)) continue;
+    uint32_t u[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) u[i] = y[i];
+    ok = gcd_is_one_w<32>(u, w.m, err);
+  }
+  if (!ok) err |= FBM_ERR_FDH_OVERFLOW;
+  // r = D_1 || ... || D_c: D_c is the least significant block -- reverse the blocks written in digest order
+#pragma unroll 1
+  for (int j = 0; j < c / 2; ++j)
+#pragma unroll 1
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t x = o[8 * j + i];
+      o[8 * j + i] = o[8 * (c - 1 - j) + i];
+      o[8 * (c - 1 - j) + i] = x;
+    }
+#pragma unroll 1
+  for (int i = 8 * c; i < hw; ++i) o[i] = 0u;
   if (err) atomicOr(stats + FBM_STAT_ERRFLAGS, err);
 }
 
@@ -1862,10 +2013,12 @@ int launch_jl_nude(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, int ne
   return check_launch("jl_nude_kernel");
 }
 
-int launch_ves_pack(const uint32_t* x, uint64_t n, int wv, int es, int cr, int pw, uint32_t* pt, hipStream_t s) {
+int launch_ves_pack(const uint32_t* x, uint64_t n, int wv, int es, int cr, int pw, int sgn, uint32_t* pt,
+                    hipStream_t s) {
   const uint64_t n_ct = (n + (uint64_t)cr - 1) / (uint64_t)cr;
   if (n_ct == 0) return FBM_OK;
-  hipLaunchKernelGGL(ves_pack_kernel, grid1(n_ct * (uint64_t)pw, 256), dim3(256), 0, s, x, n, wv, es, cr, pw, n_ct, pt);
+  hipLaunchKernelGGL(ves_pack_kernel, grid1(n_ct * (uint64_t)pw, 256), dim3(256), 0, s, x, n, wv, es, cr, pw, sgn, n_ct,
+                     pt);
   return check_launch("ves_pack_kernel");
 }
 
@@ -1875,6 +2028,20 @@ int launch_ves_unpack(const uint32_t* pt, int pw, int es, int cr, uint64_t n_out
   hipLaunchKernelGGL(ves_unpack_kernel, grid1(n_out * (uint64_t)ow, 256), dim3(256), 0, s, pt, pw, es, cr, n_out, ow,
                      vals);
   return check_launch("ves_unpack_kernel");
+}
+
+int launch_jl_fdh_msg_wide(uint64_t n, const uint32_t* t, int tw, int msg_bytes, int kmax, const uint32_t* m32,
+                           const uint32_t* k1, const uint32_t* k2, uint32_t mp, int even, uint32_t* H, int hw,
+                           uint32_t* stats, hipStream_t s) {
+  if (n == 0) return FBM_OK;
+  FdhWideArg w;
+  memcpy(w.m, m32, sizeof(w.m));
+  memcpy(w.k1, k1, sizeof(w.k1));
+  memcpy(w.k2, k2, sizeof(w.k2));
+  w.mp = mp;
+  w.even = even;
+  hipLaunchKernelGGL(jl_fdh_msg_wide_kernel, grid1(n, 64), dim3(64), 0, s, n, t, tw, msg_bytes, kmax, w, H, hw, stats);
+  return check_launch("jl_fdh_msg_wide_kernel");
 }
 
 int launch_jl_fdh_msg(uint64_t n, const uint32_t* t, int tw, int msg_bytes, int kmax, const uint32_t* n32, int even,

@@ -23,8 +23,9 @@ modulus) -- and the exponentiations on the device (fbm_jl_powmod / fbm_jl_decryp
 
 Domain of the device path (FB624 outside it): 1 <= N < 2^1024 (an even N and
 N = 1 run on the generic engine, fedbiomed_amd/csrc/fbm_gen.hip, an odd one on the Montgomery engines);
-FDH of any bits_size (an r of up to 15 digests); tau in [0, 2^8192) where FDH hashes it (ABI 3); VES
-values >= 0 of any width, any slot and plaintext size (round 4); ServerKey.decrypt with delta^2 = 1 (mod N).  Integers are Python ints (gmpy2 is
+FDH of any bits_size (an r of up to 255 digests, round 5); tau in [0, 2^8192) where FDH hashes it; VES
+values of any width and sign, any slot and plaintext size (rounds 4-5); ServerKey.decrypt with delta^2 = 1
+(mod N).  Integers are Python ints (gmpy2 is
 not a dependency): where the reference returns gmpy2.mpz this returns int, and FDH takes an
 int modulus.
 """
@@ -66,10 +67,9 @@ class VES:
         return element_size, comp_ratio
 
     def _slot(self, add_ops: int) -> Tuple[int, int]:
-        es, cr = self._get_elements_size_and_compression_ratio(add_ops)
-        if cr < 1:  # the reference then packs every value into one plaintext (its bs never reaches 0)
-            raise _unsupported(f"VES slot of {es} bits in a {self._ptsize}-bit plaintext")
-        return es, cr
+        """(element_size, comp_ratio); comp_ratio 0 when a slot is wider than the plaintext (encode then packs
+        every value into one plaintext -- the reference's bs never reaches 0 -- and decode reads none)."""
+        return self._get_elements_size_and_compression_ratio(add_ops)
 
     def encode(self, V: List[int], add_ops: int) -> List[int]:
         """reference _jls.py:118-144 (OR packing, _batch :169-176) -- fbm_jl_pack for the crypter's shape
@@ -77,20 +77,21 @@ class VES:
         es, cr = self._slot(add_ops)
         if not V:
             return []
-        wmax = max(operator.index(v).bit_length() for v in V)
+        V = [operator.index(v) for v in V]
+        if cr < 1:  # bs = 0 - 1 - 1 ... never reaches 0: one plaintext holds every value (round 5)
+            return D.ves_pack_any(V, es, len(V))
+        wmax = max(v.bit_length() for v in V)
         if es <= 100 and es * cr <= 1024 and wmax <= 128 and es * (cr - 1) + wmax <= 1024 and min(V) >= 0:
             pt = D.jl_pack(D.ints_to_u128(V), es, cr)  # (no bit of any plaintext past 2^1024)
             return D.limbs_to_ints_w(pt, 32)
-        if any(operator.index(v) < 0 for v in V):
-            raise _unsupported("VES.encode of negative values")
-        return D.ves_pack_any([operator.index(v) for v in V], es, cr)
+        return D.ves_pack_any(V, es, cr)  # any width, negative values included (round 5)
 
     def decode(self, E: List[int], add_ops: int, v_expected: int) -> List[int]:
         """reference _jls.py:146-167 (_debatch :179-192): slot j = (e >> es*j) & (2^es - 1),
         min(remaining, comp_ratio) values per plaintext -- fbm_jl_unpack for the crypter's shape,
         fbm_ves_unpack for any other (round 4)."""
         es, cr = self._slot(add_ops)
-        if not E or v_expected <= 0:
+        if not E or v_expected <= 0 or cr < 1:  # comp_ratio 0: min(v_expected, 0) values per plaintext
             return []
         if es > 128 or es * cr > 1024:
             return D.ves_unpack_any([int(e) for e in E], es, cr, v_expected)
@@ -448,6 +449,6 @@ class FDH:
         fbm_jl_fdh_msg at any other bits_size (round 4)."""
         if self.bits_size != SAParameters.KEY_SIZE:
             h = D.jl_fdh_msg([operator.index(t)], self.bits_size, int(self._n_modules))
-            return D.limbs_to_ints_w(h, h.shape[1])[0]  # (128-word rows: r of up to 15 digests)
+            return D.limbs_to_ints_w(h, h.shape[1])[0]  # (rows of r's width: up to 255 digests)
         t = _check_tau(t)  # int(t).to_bytes(1024, ...)'s OverflowError outside [0, 2^8192) (_jls.py:747)
         return self._hash_range(t, 1, 0)[0]

@@ -27,7 +27,8 @@
 extern "C" {
 #endif
 
-#define FBM_ABI_VERSION 3 /* 3: the JL round is an 8192-bit value (FBM_TAU_LIMBS limbs); 2 took 16 limbs, 1 a uint64 */
+#define FBM_ABI_VERSION 4 /* 4: fbm_ves_pack takes is_signed; 3: the JL round is an 8192-bit value (FBM_TAU_LIMBS limbs);
+                             2 took 16 limbs, 1 a uint64 */
 /* The JL round `tau` of every JL entry point: a HOST pointer to FBM_TAU_LIMBS little-endian 32-bit
  * words, any round below 2^8192 -- FDH.H hashes t = (k << 512) | tau as t.to_bytes(1024, 'big')
  * (fedbiomed/common/secagg/_jls.py:451-467, 744-748), whose OverflowError past 2^8192 the Python layer
@@ -210,11 +211,13 @@ int fbm_jl_fdh(uint64_t n_ct, const uint32_t* modulus_odd, int modulus_even, con
  * _jls.py:742-762 -- the crypter's FDH(2048, N^2) takes fbm_jl_fdh): for each of n values t (device,
  * t_words little-endian 32-bit words each, t < 2^(8 (bits_size / 2)): the caller checks the
  * reference's to_bytes range), r = SHA256(t.to_bytes(bits_size / 2) || 1) || SHA256(... || 2) || ...
- * until gcd(r, M) == 1, at most (bits_size / 8 - 1) / 32 digests (FBM_E_FDH when none qualifies or
- * bits_size < 264: the reference's counter byte overflows; FBM_E_UNSUPPORTED at fbm_check_stats when
- * bits_size > 4096 would let it try a 16th).  M as in fbm_jl_fdh.  h: n x 128 limbs (device; r < 2^3840). */
+ * until gcd(r, M) == 1, at most min((bits_size / 8 - 1) / 32, 255) digests (FBM_E_FDH at fbm_check_stats
+ * when none qualifies, or at once when bits_size < 264: the reference's counter byte overflows).  M as in
+ * fbm_jl_fdh.  h: n rows of h_words limbs (device), h_words = fbm_jl_fdh_msg_row_words(bits_size): 128 up to
+ * 15 digests (bits_size <= 4096), 8 per digest above (ABI 4: r of up to 255 digests). */
+int fbm_jl_fdh_msg_row_words(int bits_size);
 int fbm_jl_fdh_msg(uint64_t n, const uint32_t* t, int t_words, int bits_size, const uint32_t* modulus_odd,
-                   int modulus_even, uint32_t* h, uint32_t* stats, void* stream);
+                   int modulus_even, uint32_t* h, int h_words, uint32_t* stats, void* stream);
 int fbm_jl_product(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* biprime, uint32_t* out,
                    void* workspace, void* stream);
 int fbm_jl_decrypt(const uint32_t* cts, int n_parties, uint64_t n_ct, const uint32_t* biprime, const uint32_t* key,
@@ -253,9 +256,13 @@ int fbm_int_true_div_big(const uint64_t* x, uint64_t n, const uint32_t* k, int k
 /* VES objects of any shape (round 4; reference _jls.py:118-192): fbm_ves_pack ORs value j of each group
  * of cr into its plaintext at bit es * j (values: n rows of wv little-endian words, device; bits past the
  * slot land in the next slots, as the reference's a |= v << es j; pt: ceil(n / cr) rows of pw words with
- * es (cr - 1) + 32 wv <= 32 pw); fbm_ves_unpack writes value o = bits [es (o % cr), + es) of plaintext
- * o / cr (pt: n_ct rows of pw words, es cr <= 32 pw) as rows of ow >= ceil(es / 32) words. */
-int fbm_ves_pack(const uint32_t* x, uint64_t n, int wv, int es, int cr, int pw, uint32_t* pt, void* stream);
+ * es (cr - 1) + 32 wv <= 32 pw); is_signed (ABI 4): the rows are two's complement and a negative value's
+ * sign bit repeats up to the plaintext's top word (Python's OR of negative ints: the plaintext is then the
+ * negative number pt - 2^(32 pw), its top bit set; keep 32 wv above every value's bit length for its sign);
+ * fbm_ves_unpack writes value o = bits [es (o % cr), + es) of plaintext o / cr (pt: n_ct rows of pw words,
+ * es cr <= 32 pw) as rows of ow >= ceil(es / 32) words. */
+int fbm_ves_pack(const uint32_t* x, uint64_t n, int wv, int es, int cr, int pw, int is_signed, uint32_t* pt,
+                 void* stream);
 int fbm_ves_unpack(const uint32_t* pt, uint64_t n_ct, int pw, int es, int cr, uint64_t n_out, int ow, uint32_t* vals,
                    void* stream);
 /* host test hook (no GPU): fbm_int_true_div_big's per-value arithmetic on host arrays. */

@@ -49,8 +49,8 @@ def test_fdh_bits_oracle_vs_fixture(fb):
 def test_fdh_bits_device_vs_fixture(fb):
     """FDH(bits_size, M).H on the device (jl_fdh_msg_kernel through the object API) equals the reference
     for every case of the fixture: values, OverflowErrors (message too long, negative t, bits_size < 264,
-    no coprime r), bit for bit -- r of up to 11 digests among them (M = 6 at 3072 bits).  A case the
-    reference would solve with 16 or more digests (bits_size > 4096) would be FB624 here."""
+    no coprime r), bit for bit -- r of up to 11 digests among them (M = 6 at 3072 bits).  r of 16 and more
+    digests (bits_size > 4096): tests/test_fdh_wide.py."""
     from fedbiomed_amd.secagg._jls import FDH
 
     for bits, m, t, h in _cases(fb):

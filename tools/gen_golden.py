@@ -869,6 +869,32 @@ def gen_fdh_bits(R):
                                                                 "ct": [ihex(c) for c in cts], "dec": dec}})
 
 
+def gen_fdh_wide(R):
+    """FDH(bits_size, M).H whose r takes 16 or more digests (fdh_wide.json, round 5): bits_size > 4096 lets
+    the reference's inner loop break while r is shorter than bits_size // 8 bytes, i.e. up to
+    min(ceil(bits_size / 256) - 1, 255) digests, the counter byte's own limit.  Moduli with many small prime
+    factors make most candidates fail the gcd: an even primorial (r must also be odd), an odd one, 2^20 and a
+    real biprime's square; bits_size 4104 (at most 16 digests, then OverflowError) up to 70000 (255)."""
+    jls = R.jls
+    mpz = sys.modules["gmpy2"].mpz
+    rng = random.Random(4104)
+    primes = [p for p in range(3, 72) if all(p % q for q in range(2, p))]
+    odd_prim = 1
+    for p in primes:
+        odd_prim *= p
+    out = []
+    for bits, m, nt in ((4104, 2 * odd_prim, 10), (4104, odd_prim, 8), (5000, 2 * odd_prim, 8), (8192, 2 * odd_prim, 8),
+                        (8192, 2 ** 20, 4), (20000, 2 * odd_prim, 5), (70000, 2 * odd_prim, 3), (4200, W.BIPRIME0 ** 2, 2),
+                        (70000, 1, 1)):
+        L = bits // 2
+        ts = [0] + [rng.getrandbits(min(8 * L, 700)) for _ in range(nt - 1)]
+        cases = []
+        for t in ts:
+            cases.append({"t": ihex(t), "h": _outcome(lambda t=t, m=m: ihex(int(jls.FDH(bits, mpz(m)).H(t))))})
+        out.append({"bits": bits, "m": ihex(m), "cases": cases})
+    dump("fdh_wide.json", out)
+
+
 def gen_ves_wide(R):
     """VES objects outside the crypter's shape (ves_wide.json): element sizes above 100 bits, plaintexts
     wider than 1024 bits (ptsize up to 4096), values of 2^128 and more -- wider than their slot too, whose
@@ -899,6 +925,58 @@ def gen_ves_wide(R):
     dump("ves_wide.json", out)
 
 
+def gen_ves_signed(R):
+    """VES.encode of negative values and of slots wider than the plaintext (ves_signed.json, round 5): the
+    reference ORs each value in at bit es j (_jls.py:169-176), so a negative one makes its plaintext the
+    negative int Python's OR gives; with comp_ratio 0 (ptsize < element_size) its `bs` never reaches 0 and
+    one plaintext holds every value, and decode reads min(v_expected, 0) = 0 values per plaintext.  Plus
+    JoyeLibert.protect / aggregate of negative values and of a 0-comp-ratio target range on a small odd
+    modulus (UserKey.encrypt takes N * pt + 1 mod N^2 of the negative packing)."""
+    jls = R.jls
+    mpz = sys.modules["gmpy2"].mpz
+    rng = random.Random(5150)
+    out = {"ves": [], "protect": []}
+    for ptsize, valuesize, add_ops in [(1024, 30, 1), (1024, 120, 3), (300, 40, 2), (2048, 500, 1), (100, 120, 1),
+                                       (64, 64, 0), (1024, 1100, 3), (7, 3, 0)]:
+        ves = jls.VES(ptsize, valuesize)
+        es, cr = ves._get_elements_size_and_compression_ratio(add_ops)
+        for n, wmax, neg in ((1, es, [0]), (max(cr, 1), es, [0]), (2 * max(cr, 1) + 1, es, [1, -1]),
+                             (3 * max(cr, 1) - 1, es + 9, [0, 2]), (5, 2 * es + 3, [4]), (6, es, [])):
+            V = [rng.getrandbits(rng.randrange(1, wmax + 1)) for _ in range(n)]
+            for i in {i % n for i in neg}:
+                V[i] = -V[i] - 1
+            E = _outcome(lambda V=V: [ihex(int(e)) for e in ves.encode([mpz(v) for v in V], add_ops)])
+            cases = []
+            if "ok" in E:
+                enc = [int(e, 16) for e in E["ok"]]
+                for v_exp in (n, 1, n + 3, 0):
+                    cases.append({"v_expected": v_exp, "out": _outcome(lambda v_exp=v_exp: [
+                        ihex(v) for v in ves.decode(enc, add_ops, v_exp)])})
+            out["ves"].append({"ptsize": ptsize, "valuesize": valuesize, "add_ops": add_ops, "es": es, "cr": cr,
+                               "V": [ihex(v) for v in V], "E": E, "decode": cases})
+    n_mod = 1000003 * 1000033
+    pp = jls.PublicParam(mpz(n_mod), 1024, jls.FDH(2048, mpz(n_mod) * mpz(n_mod)).H)
+    keys = [rng.getrandbits(100) for _ in range(3)]
+    sk0 = -sum(keys)
+    for target, xs_of in [(2 ** 13, lambda k: [rng.randrange(-2 ** 20, 2 ** 20) for _ in range(7)]),
+                          (2 ** 1100, lambda k: [rng.getrandbits(200) for _ in range(3)]),
+                          (2 ** 1100, lambda k: [-rng.getrandbits(50) - 1, rng.getrandbits(60)])]:
+        jl = jls.JoyeLibert(target_range=target)
+        xs = [xs_of(k) for k in keys]
+        cts = [_outcome(lambda k=k, x=x: [ihex(int(c)) for c in jl.protect(pp, jls.UserKey(pp, k), 4,
+                                                                          [mpz(v) for v in x], 3)])
+               for k, x in zip(keys, xs)]
+        agg = None
+        if all("ok" in c for c in cts):
+            enc = [[jls.EncryptedNumber(pp, mpz(int(c, 16))) for c in row["ok"]] for row in cts]
+            agg = _outcome(lambda enc=enc: [ihex(int(v)) for v in jl.aggregate(jls.ServerKey(pp, sk0), 4, enc,
+                                                                                len(xs[0]))])
+        out["protect"].append({"n": ihex(n_mod), "target": ihex(target), "keys": [ihex(k) for k in keys],
+                               "sk0": ihex(sk0), "tau": 4, "xs": [[ihex(v) for v in x] for x in xs], "cts": cts,
+                               "aggregate": agg})
+    dump("ves_signed.json", out)
+
+
 def I(s):  # noqa: E743 - hex string -> int (the fixtures' encoding)
     return int(s, 16)
 
@@ -919,6 +997,12 @@ def main():
         return
     if sys.argv[1:] == ["custom_hash"]:
         gen_custom_hash(R)
+        return
+    if sys.argv[1:] == ["ves_signed"]:
+        gen_ves_signed(R)
+        return
+    if sys.argv[1:] == ["fdh_wide"]:
+        gen_fdh_wide(R)
         return
     if sys.argv[1:] == ["caller_flows"]:
         gen_caller_flows(R)
@@ -947,6 +1031,8 @@ def main():
     gen_n_one(R)
     gen_fdh_bits(R)
     gen_ves_wide(R)
+    gen_ves_signed(R)
+    gen_fdh_wide(R)
     meta = {"generator": "tools/gen_golden.py", "reference": load_reference.REF,
             "note": "outputs of the reference Fed-BioMed crypter (Python), imported via tools/refshim"}
     dump("meta.json", meta)
