@@ -248,6 +248,10 @@ class _PyConvFallback:
     no secagg arithmetic happens here."""
 
     @staticmethod
+    def all_ints(seq: list) -> bool:
+        return all(isinstance(v, int) for v in seq)
+
+    @staticmethod
     def floats_to_f64(seq: list, out: np.ndarray) -> int:
         if out.nbytes != 8 * len(seq):
             raise ValueError(f"output buffer holds {out.nbytes} bytes, {8 * len(seq)} needed")
@@ -313,6 +317,11 @@ def to_host(t: torch.Tensor) -> torch.Tensor:
     host = host_empty(t.shape, t.dtype)
     host.copy_(t)
     return host
+
+
+def all_ints(seq: list) -> bool:
+    """all(isinstance(v, int) for v in seq) of a list, in one C pass (csrc/fbm_pyconv.c)."""
+    return bool(_pyconv().all_ints(seq))
 
 
 def floats_to_host(params: list) -> Optional[torch.Tensor]:
@@ -882,7 +891,7 @@ def jl_aggregate(cts: torch.Tensor, biprime: int, key: int, tau: int, n_expected
         else:
             _call(lib.fbm_jl_aggregate_factor, _ptr(part), P, k1 - k0, es, cr, e1 - e0, _np_ptr(bp),
                   _ptr(factor[k0:k1]), int(total_weight), negc, step, o, sm, _ptr(ws), _ptr(st), _stream())
-        _check_stats(st)
+        _check_stats_or_defer(st)  # (inside deferred_checks: at its exit, e.g. the list aggregate's stripes)
     return out, sums
 
 

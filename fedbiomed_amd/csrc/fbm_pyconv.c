@@ -340,7 +340,20 @@ static PyObject* bytes_to_ints(PyObject* self, PyObject* args) {
     return lst;
 }
 
+/* all(isinstance(v, int) for v in seq) for a list: PyLong_Check per item (int subclasses, bool among
+ * them, count as the reference's isinstance does) -- no per-item hashing, unlike set(map(type, seq)). */
+static PyObject* all_ints(PyObject* self, PyObject* args) {
+    PyObject* seq;
+    if (!PyArg_ParseTuple(args, "O!", &PyList_Type, &seq)) return NULL;
+    const Py_ssize_t n = PyList_GET_SIZE(seq);
+    PyObject** items = ((PyListObject*)seq)->ob_item;
+    for (Py_ssize_t i = 0; i < n; ++i)
+        if (!PyLong_Check(items[i])) Py_RETURN_FALSE;
+    Py_RETURN_TRUE;
+}
+
 static PyMethodDef methods[] = {
+    {"all_ints", all_ints, METH_VARARGS, "list -> all items are ints (isinstance)"},
     {"floats_to_f64", floats_to_f64, METH_VARARGS, "list of floats -> float64 buffer; -1 or first bad index"},
     {"ints_to_bytes", ints_to_bytes, METH_VARARGS, "list of ints -> n-byte LE unsigned; -1 or first bad index"},
     {"bytes_to_ints", bytes_to_ints, METH_VARARGS, "buffer of n-byte LE unsigned values -> list of ints"},

@@ -24,8 +24,8 @@ modulus) -- and the exponentiations on the device (fbm_jl_powmod / fbm_jl_decryp
 Domain of the device path (FB624 outside it): 1 <= N < 2^1024 (an even N and
 N = 1 run on the generic engine, fedbiomed_amd/csrc/fbm_gen.hip, an odd one on the Montgomery engines);
 FDH of any bits_size (an r of up to 255 digests, round 5); tau in [0, 2^8192) where FDH hashes it; VES
-values of any width and sign, any slot and plaintext size (rounds 4-5); ServerKey.decrypt with delta^2 = 1
-(mod N).  Integers are Python ints (gmpy2 is
+values of any width and sign, any slot and plaintext size (rounds 4-5); ServerKey.decrypt with any invertible
+delta (round 5).  Integers are Python ints (gmpy2 is
 not a dependency): where the reference returns gmpy2.mpz this returns int, and FDH takes an
 int modulus.
 """
@@ -337,15 +337,26 @@ class ServerKey(BaseKey):
             raise ZeroDivisionError("invert() no inverse exists")  # list; modulo 1 its result is 0: raises
         if not cipher:
             return []
-        if d2 % n != 1:
-            raise _unsupported("ServerKey.decrypt with delta^2 != 1 (mod N)")
         if not _fdh_standard(self._public_param):  # fbm_jl_powmod's factor, then fbm_jl_decrypt_with
             rows = _term_rows(cipher, n)
             factor = D.jl_powmod(_bases(self, tau, len(cipher), n), n, d2 * self._key)
-            return D.limbs_to_ints_w(D.jl_decrypt_with(rows, n, factor), 32)
-        tau = _check_tau(tau)
-        x = D.jl_decrypt(_term_rows(cipher, n), n, d2 * self._key, tau)
+            x = D.jl_decrypt_with(rows, n, factor)
+        else:
+            tau = _check_tau(tau)
+            x = D.jl_decrypt(_term_rows(cipher, n), n, d2 * self._key, tau)
+        if d2 % n != 1:  # x * invert(delta^2, N^2) mod N (round 5), on the device: see _times_mod_n
+            x = _times_mod_n(x, pow(d2, -1, n * n) % n, n)
         return D.limbs_to_ints_w(x, 32)
+
+
+def _times_mod_n(x: torch.Tensor, c: int, n: int) -> torch.Tensor:
+    """c x mod N for plaintext limbs x (int32 [k, 32], x < N) and a constant c, on the device through the
+    binomial identity (1 + N x)^c = 1 + N (c x mod N) (mod N^2): fbm_jl_powmod builds 1 + N x (base 1, key 1,
+    plaintext x), raises it to c, and fbm_jl_decrypt_with's L(v) = ((v - 1) // N) mod N reads c x mod N back."""
+    ones = torch.zeros((x.shape[0], 64), dtype=torch.int32, device=x.device)
+    ones[:, 0] = 1
+    v = D.jl_powmod(D.jl_powmod(ones, n, 1, x), n, c)
+    return D.jl_decrypt_with(v[None], n, ones)
 
 
 class JoyeLibert:

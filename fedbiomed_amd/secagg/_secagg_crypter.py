@@ -47,13 +47,6 @@ def _check_weight(weight: Optional[int], jl: bool) -> None:
             f"{SAParameters.WEIGHT_RANGE}.")
 
 
-def _all_instances(values, cls) -> bool:
-    """all(isinstance(v, cls) for v in values), by element type: one set of the element
-    types (C speed) and an issubclass check per distinct type -- the same answer for plain
-    classes, 3-4x faster on model-sized lists."""
-    return all(issubclass(t, cls) for t in set(map(type, values)))
-
-
 def _check_float_list(params) -> torch.Tensor:
     """The reference's list/float checks; returns the float64 host copy made in the same pass."""
     if not isinstance(params, list):
@@ -72,7 +65,7 @@ def _check_int_lists(params) -> None:
         raise FedbiomedSecaggCrypterError(
             f"{ErrorNumbers.FB624.value}: The parameters to aggregate should be a "
             f"list containing list of parameters")
-    if not all(_all_instances(p, int) for p in params):
+    if not all(D.all_ints(p) for p in params):
         raise FedbiomedSecaggCrypterError(
             f"{ErrorNumbers.FB624.value}: Invalid parameter type. The parameters "
             f"should be of type of integers.")
@@ -226,15 +219,22 @@ class SecaggCrypter:
             # The decryption factor H(t_k)^key needs no ciphertext: issue it first, so the GPU
             # exponentiates while the host validates and converts the parties' lists.  Only
             # when the arguments are well-formed; any error is raised below, in the order
-            # the reference raises it.
-            factor = None
+            # the reference raises it.  Vectors of two one-lane rounds or more run as ct_offset
+            # stripes (the node encrypt's): stripe k's factor, then its combine and D2H, then
+            # stripe k + 1's factor, so the host builds stripe k's floats while the GPU
+            # exponentiates stripe k + 1 (every element depends on its own ciphertext only: the
+            # stripes' outputs concatenate to the unsplit call's).
+            stripes, factors = None, []
             if params and isinstance(key, int) and isinstance(biprime, int) and all(type(p) is list for p in params):
                 n_ct0 = min(len(p) for p in params)
                 if n_ct0:
+                    stripes = D.list_encrypt_stripes(n_ct0, D.device())
+                    factors = [None] * len(stripes)
                     try:
-                        factor = self.decrypt_factor_tensor(current_round, n_ct0, key, biprime)
+                        c0, c1 = stripes[0]
+                        factors[0] = self.decrypt_factor_tensor(current_round, c1 - c0, key, biprime, ct_offset=c0)
                     except Exception:  # noqa: BLE001 -- re-raised by the regular path below
-                        factor = None
+                        stripes = None
             _check_int_lists(params)
             if not isinstance(key, int):
                 raise TypeError("The key should be type of integer")
@@ -246,19 +246,60 @@ class SecaggCrypter:
             n_ct = min(len(p) for p in params)  # zip(*list_y_u_tau) truncates (_jls.py:691-693)
             if n_ct == 0:
                 return []
-            limbs = wire.packed_rows(params, "jl", n_ct)
-            if limbs is None:
-                staged = D.host_empty((len(params), n_ct, 64), torch.int32)
+            dev = D.device()
+            if stripes is None:
+                stripes, factors = [(0, n_ct)], [None]
+            res = self._aggregate_stripes(current_round, params, key, biprime, total_sample_size, clipping_range,
+                                          num_expected_params, target_range, n2, n_ct, stripes, factors, dev)
+        logger.info(f"Aggregating {len(params)} parameters from {num_nodes} nodes.")
+        logger.debug(f"Aggregation is completed in {round(time.process_time() - start, ndigits=2)} seconds.")
+        return res
+
+    def _aggregate_stripes(self, current_round, params, key, biprime, total_sample_size, clipping_range,
+                           num_expected_params, target_range, n2, n_ct, stripes, factors, dev) -> List[float]:
+        """The list API's aggregate over ct_offset stripes (one when the vector is small): per stripe the
+        parties' ints -> pinned limbs -> H2D on a copy stream, the combine with that stripe's factor, the
+        float64 D2H in stream order, then the next stripe's factor; the floats are built as each stripe's
+        D2H lands.  Stripe outputs: elements [c0 cr, c1 cr) capped by num_expected_params, as the unsplit
+        decode (_jls.py:146-167); a stripe past it still runs its checks (the unsplit call's errors)."""
+        _, cr = D.jl_slot(target_range or SAParameters.TARGET_RANGE, len(params))
+        n_exp = int(num_expected_params)
+        packed = wire.packed_rows(params, "jl", n_ct)
+        main = torch.cuda.current_stream(dev)
+        copy = torch.cuda.Stream(device=dev)
+        keep, pending = [], []
+        for k, (c0, c1) in enumerate(stripes):
+            if packed is not None:
+                limbs = packed[:, c0:c1]
+            else:
+                staged = D.host_empty((len(params), c1 - c0, 64), torch.int32)
                 limbs = staged.numpy().view(np.uint32)
                 for u, p in enumerate(params):
-                    D.ints_to_limbs(p if len(p) == n_ct else p[:n_ct], n2, out=limbs[u])
-            dev = D.device()
-            cts = torch.from_numpy(limbs.view(np.int32)).to(dev)
+                    D.ints_to_limbs(p[c0:c1] if (c0, c1) != (0, len(p)) else p, n2, out=limbs[u])
+            host = torch.from_numpy(np.ascontiguousarray(limbs).view(np.int32))
+            copy.wait_stream(main)
+            with torch.cuda.stream(copy):
+                cts = host.to(dev, non_blocking=True)
+            main.wait_stream(copy)
+            cts.record_stream(main)
+            keep.append(host)
+            if factors[k] is None and len(stripes) > 1:
+                factors[k] = self.decrypt_factor_tensor(current_round, c1 - c0, key, biprime, ct_offset=c0)
+            n_out = max(0, min(n_exp - c0 * cr, (c1 - c0) * cr))
             out = self.aggregate_tensor(current_round, cts, key, biprime, total_sample_size, clipping_range,
-                                        num_expected_params, target_range, decrypt_factor=factor)
-        logger.info(f"Aggregating {len(params)} parameters from {num_nodes} nodes.")
-        res = D.to_host(out).numpy().tolist()
-        logger.debug(f"Aggregation is completed in {round(time.process_time() - start, ndigits=2)} seconds.")
+                                        n_out, target_range, ct_offset=c0, decrypt_factor=factors[k])
+            out_h = D.host_empty(out.shape, torch.float64)
+            out_h.copy_(out, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(main)
+            pending.append((out_h, ev))
+            if k + 1 < len(stripes):  # the next stripe's factor right behind this stripe's combine
+                n0, n1 = stripes[k + 1]
+                factors[k + 1] = self.decrypt_factor_tensor(current_round, n1 - n0, key, biprime, ct_offset=n0)
+        res: List[float] = []
+        for out_h, ev in pending:
+            ev.synchronize()
+            res += out_h.numpy().tolist()
         return res
 
     @staticmethod

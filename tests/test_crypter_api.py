@@ -166,3 +166,45 @@ def test_list_encrypt_overlapped_stripes_equal_unsplit(monkeypatch, caplog):
     monkeypatch.setenv("FBM_ONE_LANE_ROUND", "300")
     with pytest.raises(Exception):
         jc.encrypt(P, tau, xs[:-1] + [1], key, W.BIPRIME0)  # a non-float: FB624 before any device work
+
+
+@pytest.mark.gpu
+def test_list_aggregate_stripes_equal_unsplit(monkeypatch):
+    """Round 5: the researcher's aggregate(List[List[int]]) runs as ct_offset stripes (stripe k's combine and
+    D2H, then stripe k + 1's factor, the floats built as each D2H lands).  Bit-identical to the unsplit call for
+    every stripe plan, with num_expected_params cutting inside a stripe, at a stripe edge, past the end and at
+    0, ragged lists (zip truncation) and the wire blob; errors as before (a zero sample size, a bad item)."""
+    from fedbiomed_amd import _device as D, wire, workload as W
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    P, tau, n = 4, 5, 30_001
+    keys = [W.jl_user_key(p) for p in range(P)]
+    jc = SecaggCrypter()
+    cl = [jc.encrypt(P, tau, [float(v) for v in W.party_params(p, n)], keys[p], W.BIPRIME0, weight=3 + p)
+          for p in range(P)]
+    cl[1] = cl[1] + [12345]  # ragged: zip truncates
+    tw = sum(3 + p for p in range(P))
+    _, cr = D.jl_slot(None, P)
+    monkeypatch.delenv("FBM_ONE_LANE_ROUND", raising=False)
+    cases = [n, 7, 250 * cr, 250 * cr + 1, n + 100, 0]
+    ref = {e: jc.aggregate(tau, P, cl, -sum(keys), W.BIPRIME0, tw, num_expected_params=e) for e in cases}
+    assert len(D.list_encrypt_stripes(len(cl[0]))) == 1
+    for rnd in ("250", "333"):
+        monkeypatch.setenv("FBM_ONE_LANE_ROUND", rnd)
+        assert len(D.list_encrypt_stripes(len(cl[0]))) > 2
+        for e in cases:
+            assert jc.aggregate(tau, P, cl, -sum(keys), W.BIPRIME0, tw, num_expected_params=e) == ref[e], (rnd, e)
+        with pytest.raises(ZeroDivisionError):
+            jc.aggregate(tau, P, cl, -sum(keys), W.BIPRIME0, 0, num_expected_params=n)
+        bad = [list(c) for c in cl]
+        bad[2][5] = 1.5
+        with pytest.raises(Exception, match="FB624"):
+            jc.aggregate(tau, P, bad, -sum(keys), W.BIPRIME0, tw, num_expected_params=n)
+    monkeypatch.setenv("FBM_ONE_LANE_ROUND", "250")
+    wire.enable()
+    try:
+        cw = [jc.encrypt(P, tau, [float(v) for v in W.party_params(p, n)], keys[p], W.BIPRIME0, weight=3 + p)
+              for p in range(P)]
+        assert jc.aggregate(tau, P, cw, -sum(keys), W.BIPRIME0, tw, num_expected_params=n) == ref[n]
+    finally:
+        wire.enable(False)

@@ -1,0 +1,49 @@
+"""ServerKey.decrypt with delta^2 != 1 (mod N) (round 5; the object API's last FB624 refusal of a value the
+reference computes).  The reference raises the factor to delta^2 key and multiplies x = L(v) by
+invert(delta^2, N^2) mod N (`_jls.py:520-562`).  On the device: the factor's exponent is delta^2 key, and
+c x mod N (c = delta^-2 mod N) comes from the binomial identity (1 + N x)^c = 1 + N (c x mod N) (mod N^2) --
+fbm_jl_powmod twice, then fbm_jl_decrypt_with's L (`secagg/_jls.py::_times_mod_n`).  Fixture:
+tests/golden/decrypt_delta.json (tools/gen_golden.py gen_decrypt_delta, the reference's outcomes over the
+benchmark biprime, a small odd and an even modulus, deltas of either sign up to 2^70 + 1, and deltas sharing a
+factor with N: invert's ZeroDivisionError)."""
+
+import pytest
+
+from oracle import secagg_oracle as O
+from tests.golden_util import I, load
+
+
+@pytest.fixture(scope="module")
+def dd():
+    return load("decrypt_delta.json")
+
+
+def test_decrypt_delta_oracle_vs_fixture(dd):
+    for c in dd:
+        n, keys = I(c["n"]), [I(k) for k in c["keys"]]
+        summed = [a * b % (n * n) for a, b in zip(*[[I(v) for v in row] for row in c["cts"]])]
+        if "ok" in c["dec"]:
+            assert O.jl_server_decrypt(summed, c["tau"], -sum(keys), n, delta=c["delta"]) == \
+                [I(v) for v in c["dec"]["ok"]], (c["n"], c["delta"])
+        else:
+            with pytest.raises(ZeroDivisionError):
+                O.jl_server_decrypt(summed, c["tau"], -sum(keys), n, delta=c["delta"])
+
+
+@pytest.mark.gpu
+def test_decrypt_delta_device_vs_fixture(dd):
+    from fedbiomed_amd.secagg._jls import EncryptedNumber, ServerKey
+    from tests.test_jls_api import pp_of
+
+    for c in dd:
+        n, keys = I(c["n"]), [I(k) for k in c["keys"]]
+        pp = pp_of(n)
+        rows = [[EncryptedNumber(pp, I(v)) for v in row] for row in c["cts"]]
+        summed = [a + b for a, b in zip(*rows)]
+        sk = ServerKey(pp, -sum(keys))
+        if "ok" in c["dec"]:
+            assert sk.decrypt(summed, c["tau"], delta=c["delta"]) == [I(v) for v in c["dec"]["ok"]], \
+                (c["n"], c["delta"])
+        else:
+            with pytest.raises(ZeroDivisionError, match=c["dec"]["msg"]):
+                sk.decrypt(summed, c["tau"], delta=c["delta"])

@@ -128,8 +128,7 @@ def test_domain_restrictions_raise_fb624():
     # (rounds of 2^512 and more, FDH.H of any t < 2^8192: on the device since ABI 3 -- tests/test_caller_flows.py)
     with pytest.raises(OverflowError):
         UserKey(pp, 3).encrypt([1], 2**8192)  # int(t).to_bytes(1024) of the reference
-    with pytest.raises(FedbiomedSecaggCrypterError, match="FB624"):
-        ServerKey(pp, -20).decrypt([EncryptedNumber(pp, 5)], 1, delta=2)  # delta^2 != 1 (mod N)
+    # (delta^2 != 1 (mod N): on the device since round 5 -- tests/test_decrypt_delta.py)
     with pytest.raises(ZeroDivisionError):
         ServerKey(pp, -20).decrypt([EncryptedNumber(pp, 5)], 1, delta=0)  # invert(0) as the reference
     # a non-FDH hashing function is the caller's own callable: _populate_tau calls it per t

@@ -895,6 +895,29 @@ def gen_fdh_wide(R):
     dump("fdh_wide.json", out)
 
 
+def gen_decrypt_delta(R):
+    """ServerKey.decrypt with delta^2 != 1 (mod N) (decrypt_delta.json, round 5): the reference raises the
+    factor to delta^2 key and multiplies x by invert(delta^2, N^2) mod N (_jls.py:520-562); sums of two users'
+    encryptions decrypted with delta 2, 3, 7 and a large one, over an odd biprime, a small odd and an even
+    modulus, plus deltas sharing a factor with N (invert's ZeroDivisionError)."""
+    jls = R.jls
+    mpz = sys.modules["gmpy2"].mpz
+    rng = random.Random(1331)
+    out = []
+    for n_mod in (W.BIPRIME0, 1000003 * 1000033, 1156):
+        pp = jls.PublicParam(mpz(n_mod), 1024, jls.FDH(2048, mpz(n_mod) * mpz(n_mod)).H)
+        keys = [rng.getrandbits(200), rng.getrandbits(200)]
+        xs = [[rng.getrandbits(40) for _ in range(5)] for _ in keys]
+        cts = [jls.UserKey(pp, k).encrypt([mpz(v) for v in x], 3) for k, x in zip(keys, xs)]
+        summed = [jls.EncryptedNumber(pp, a) + jls.EncryptedNumber(pp, b) for a, b in zip(*cts)]
+        for delta in (2, 3, 7, 2 ** 70 + 1, 17, -5, 1000003, 34):
+            dec = _outcome(lambda delta=delta: [ihex(int(v)) for v in jls.ServerKey(pp, -sum(keys)).decrypt(
+                summed, 3, delta=delta)])
+            out.append({"n": ihex(n_mod), "keys": [ihex(k) for k in keys], "tau": 3, "delta": delta,
+                        "cts": [[ihex(int(c)) for c in row] for row in cts], "dec": dec})
+    dump("decrypt_delta.json", out)
+
+
 def gen_ves_wide(R):
     """VES objects outside the crypter's shape (ves_wide.json): element sizes above 100 bits, plaintexts
     wider than 1024 bits (ptsize up to 4096), values of 2^128 and more -- wider than their slot too, whose
@@ -1004,6 +1027,9 @@ def main():
     if sys.argv[1:] == ["fdh_wide"]:
         gen_fdh_wide(R)
         return
+    if sys.argv[1:] == ["decrypt_delta"]:
+        gen_decrypt_delta(R)
+        return
     if sys.argv[1:] == ["caller_flows"]:
         gen_caller_flows(R)
         return
@@ -1033,6 +1059,7 @@ def main():
     gen_ves_wide(R)
     gen_ves_signed(R)
     gen_fdh_wide(R)
+    gen_decrypt_delta(R)
     meta = {"generator": "tools/gen_golden.py", "reference": load_reference.REF,
             "note": "outputs of the reference Fed-BioMed crypter (Python), imported via tools/refshim"}
     dump("meta.json", meta)

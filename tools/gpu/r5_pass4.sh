@@ -8,3 +8,5 @@ cd $R
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1 || { echo "PYTEST FAILED"; tail -40 $O/pytest_gpu.txt; exit 1; }
 tail -2 $O/pytest_gpu.txt
 bash tools/gpu/r5_pass3.sh ${1:-r5g}
+cd $R && timeout -k 10 300 python -u tools/list_agg_probe.py --threads 4,8,16 > $O/list_agg_probe.jsonl 2>&1 || { echo "LIST AGG PROBE FAILED"; tail -5 $O/list_agg_probe.jsonl; exit 1; }
+cat $O/list_agg_probe.jsonl
