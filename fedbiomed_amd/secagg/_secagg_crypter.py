@@ -71,6 +71,12 @@ def _check_int_lists(params) -> None:
             f"should be of type of integers.")
 
 
+def _stripe_floats(out_h: torch.Tensor, ev) -> List[float]:
+    """One aggregate stripe's Python floats, once its D2H (recorded as `ev`) has landed."""
+    ev.synchronize()
+    return out_h.numpy().tolist()
+
+
 class SecaggCrypter:
     """Joye-Libert secure aggregation (encrypt on nodes, aggregate on the researcher)."""
 
@@ -259,8 +265,9 @@ class SecaggCrypter:
                            num_expected_params, target_range, n2, n_ct, stripes, factors, dev) -> List[float]:
         """The list API's aggregate over ct_offset stripes (one when the vector is small): per stripe the
         parties' ints -> pinned limbs -> H2D on a copy stream, the combine with that stripe's factor, the
-        float64 D2H in stream order, then the next stripe's factor; the floats are built as each stripe's
-        D2H lands.  Stripe outputs: elements [c0 cr, c1 cr) capped by num_expected_params, as the unsplit
+        float64 D2H in stream order, then the next stripe's factor; stripe k - 1's floats are built
+        while the GPU runs stripe k's combine and stripe k + 1's factor (the 10M-element float list is
+        the largest host cost of the call).  Stripe outputs: elements [c0 cr, c1 cr) capped by num_expected_params, as the unsplit
         decode (_jls.py:146-167); a stripe past it still runs its checks (the unsplit call's errors)."""
         _, cr = D.jl_slot(target_range or SAParameters.TARGET_RANGE, len(params))
         n_exp = int(num_expected_params)
@@ -268,21 +275,22 @@ class SecaggCrypter:
         main = torch.cuda.current_stream(dev)
         copy = torch.cuda.Stream(device=dev)
         keep, pending = [], []
+        res: List[float] = []
         for k, (c0, c1) in enumerate(stripes):
+            # the stripe's limbs in a pinned buffer (its H2D is then truly asynchronous: it runs beside the
+            # factors on `main` and neither the host nor the copy waits for them)
+            staged = D.host_empty((len(params), c1 - c0, 64), torch.int32)
+            limbs = staged.numpy().view(np.uint32)
             if packed is not None:
-                limbs = packed[:, c0:c1]
+                limbs[:] = packed[:, c0:c1]
             else:
-                staged = D.host_empty((len(params), c1 - c0, 64), torch.int32)
-                limbs = staged.numpy().view(np.uint32)
                 for u, p in enumerate(params):
                     D.ints_to_limbs(p[c0:c1] if (c0, c1) != (0, len(p)) else p, n2, out=limbs[u])
-            host = torch.from_numpy(np.ascontiguousarray(limbs).view(np.int32))
-            copy.wait_stream(main)
             with torch.cuda.stream(copy):
-                cts = host.to(dev, non_blocking=True)
+                cts = staged.to(dev, non_blocking=True)
             main.wait_stream(copy)
             cts.record_stream(main)
-            keep.append(host)
+            keep.append(staged)
             if factors[k] is None and len(stripes) > 1:
                 factors[k] = self.decrypt_factor_tensor(current_round, c1 - c0, key, biprime, ct_offset=c0)
             n_out = max(0, min(n_exp - c0 * cr, (c1 - c0) * cr))
@@ -296,10 +304,10 @@ class SecaggCrypter:
             if k + 1 < len(stripes):  # the next stripe's factor right behind this stripe's combine
                 n0, n1 = stripes[k + 1]
                 factors[k + 1] = self.decrypt_factor_tensor(current_round, n1 - n0, key, biprime, ct_offset=n0)
-        res: List[float] = []
+            if len(pending) > 1:  # stripe k - 1's floats while the GPU runs stripe k's combine and k + 1's factor
+                res += _stripe_floats(*pending.pop(0))
         for out_h, ev in pending:
-            ev.synchronize()
-            res += out_h.numpy().tolist()
+            res += _stripe_floats(out_h, ev)
         return res
 
     @staticmethod

@@ -7,6 +7,8 @@ tests/golden/decrypt_delta.json (tools/gen_golden.py gen_decrypt_delta, the refe
 benchmark biprime, a small odd and an even modulus, deltas of either sign up to 2^70 + 1, and deltas sharing a
 factor with N: invert's ZeroDivisionError)."""
 
+import re
+
 import pytest
 
 from oracle import secagg_oracle as O
@@ -45,5 +47,5 @@ def test_decrypt_delta_device_vs_fixture(dd):
             assert sk.decrypt(summed, c["tau"], delta=c["delta"]) == [I(v) for v in c["dec"]["ok"]], \
                 (c["n"], c["delta"])
         else:
-            with pytest.raises(ZeroDivisionError, match=c["dec"]["msg"]):
+            with pytest.raises(ZeroDivisionError, match=re.escape(c["dec"]["msg"])):
                 sk.decrypt(summed, c["tau"], delta=c["delta"])

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The researcher's SecaggCrypter.aggregate(List[List[int]]) at the metric size (10M elements, 8 parties:
 8 x 333 334 ciphertexts as Python ints) under several host-conversion thread counts (FBM_CONV_THREADS, read
-per call by csrc/fbm_pyconv.c), best of 3 calls each, with the conversion alone beside it.  One JSON line
+per call by csrc/fbm_pyconv.c), best of 3 calls each, with the conversion and the output float list alone beside it.  One JSON line
 per thread count.
 
     python tools/list_agg_probe.py [--threads 4,8,16] [--elements 10000000]
@@ -58,8 +58,17 @@ def main():
             out = jc.aggregate(tau, P, lists, sk0, W.BIPRIME0, tw, num_expected_params=n)
             calls.append(time.perf_counter() - t0)
         ref = out if ref is None else ref
+        floats = []
+        res_h = np.asarray(out, dtype=np.float64)
+        for _ in range(3):
+            t0 = time.perf_counter()
+            lst = res_h.tolist()
+            floats.append(time.perf_counter() - t0)
+            del lst
         print(json.dumps({"conv_threads": t, "elements": n, "parties": P, "aggregate_ms": 1000 * min(calls),
+                          "aggregate_ms_all": [1000 * c for c in calls],
                           "params_per_s": n / min(calls), "conversion_alone_ms": 1000 * min(conv),
+                          "float_list_alone_ms": 1000 * min(floats),
                           "equal_across_thread_counts": out == ref}), flush=True)
 
 
