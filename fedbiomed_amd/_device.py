@@ -281,6 +281,42 @@ class _PyConvFallback:
             raise ValueError("buffer is not a whole number of values")
         return [int.from_bytes(b[i:i + nb], "little") for i in range(0, len(b), nb)]
 
+    @staticmethod
+    def ints_to_bytes_start(lists: list, lo: int, hi: int, nb: int, out: np.ndarray):
+        """Converts at once (no background threads here); join() returns the answer."""
+        if nb <= 0 or nb % 4 or lo < 0 or hi < lo:
+            raise ValueError("bad range or width (a positive multiple of 4 bytes)")
+        if not all(isinstance(v, list) and len(v) >= hi for v in lists):
+            raise ValueError("every item must be a list holding the range")
+        m = hi - lo
+        if out.nbytes != len(lists) * m * nb:
+            raise ValueError(f"output buffer holds {out.nbytes} bytes, {len(lists) * m * nb} needed")
+        rows = out.reshape(len(lists), m * nb // out.itemsize) if lists else out
+        for u, v in enumerate(lists):
+            bad = _PyConvFallback.ints_to_bytes(v[lo:hi], nb, rows[u])
+            if bad >= 0:
+                return [u * m + bad]
+        return [-1]
+
+    @staticmethod
+    def ints_to_bytes_join(handle) -> int:
+        if not handle:
+            raise ValueError("conversion already joined")
+        return handle.pop()
+
+    @staticmethod
+    def none_list(n: int) -> list:
+        if n < 0:
+            raise ValueError("negative length")
+        return [None] * n
+
+    @staticmethod
+    def f64_into_list(lst: list, off: int, buf) -> None:
+        a = np.frombuffer(memoryview(buf).cast("B"), dtype=np.float64)
+        if off < 0 or off + len(a) > len(lst):
+            raise ValueError("float64 buffer does not fit the list at that offset")
+        lst[off:off + len(a)] = a.tolist()
+
 
 def _pyconv():
     """The list API's C conversion loops (csrc/fbm_pyconv.c), built in-tree by _build; the
@@ -377,6 +413,35 @@ def ints_to_limbs(cts: Sequence[int], modulus: Optional[int] = None, out: Option
         rest = _pyconv().ints_to_bytes(cts[bad + 1:], 256, out[bad + 1:])
         bad = -1 if rest < 0 else bad + 1 + rest
     return out
+
+
+class ints_to_limbs_async:
+    """Items [c0, c1) of every party's ciphertext list -> `out` [P, c1 - c0, 64] uint32 limbs on
+    background host threads (csrc/fbm_pyconv.c ints_to_bytes_start: no GIL needed, so the caller
+    builds the previous stripe's floats meanwhile); join() waits, then takes ints_to_limbs' slow
+    path (reduction mod N^2 of out-of-range values) for any party row that has one."""
+
+    def __init__(self, lists: List[list], c0: int, c1: int, modulus: Optional[int], out: np.ndarray):
+        self.lists, self.c0, self.c1, self.modulus, self.out = lists, c0, c1, modulus, out
+        self.handle = _pyconv().ints_to_bytes_start(lists, c0, c1, 256, out)
+
+    def join(self) -> np.ndarray:
+        bad = _pyconv().ints_to_bytes_join(self.handle)
+        if bad >= 0:  # rare: values outside [0, 2^2048) from this party row on
+            m = self.c1 - self.c0
+            for u in range(bad // max(m, 1), len(self.lists)):
+                ints_to_limbs(self.lists[u][self.c0:self.c1], self.modulus, out=self.out[u])
+        return self.out
+
+
+def float_list(n: int) -> list:
+    """The aggregate's output list, [None] * n, for f64_into_list to fill stripe by stripe."""
+    return _pyconv().none_list(n)
+
+
+def f64_into_list(lst: list, off: int, values: np.ndarray) -> None:
+    """lst[off:off + len(values)] = the float64 values as Python floats, in one pass."""
+    _pyconv().f64_into_list(lst, off, np.ascontiguousarray(values, dtype=np.float64))
 
 
 def limbs_to_ints(arr: np.ndarray) -> List[int]:

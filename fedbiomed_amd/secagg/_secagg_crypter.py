@@ -71,10 +71,10 @@ def _check_int_lists(params) -> None:
             f"should be of type of integers.")
 
 
-def _stripe_floats(out_h: torch.Tensor, ev) -> List[float]:
-    """One aggregate stripe's Python floats, once its D2H (recorded as `ev`) has landed."""
+def _stripe_floats_into(res: List[float], off: int, out_h: torch.Tensor, ev) -> None:
+    """One aggregate stripe's Python floats into res[off:], once its D2H (recorded as `ev`) has landed."""
     ev.synchronize()
-    return out_h.numpy().tolist()
+    D.f64_into_list(res, off, out_h.numpy())
 
 
 class SecaggCrypter:
@@ -263,29 +263,39 @@ class SecaggCrypter:
 
     def _aggregate_stripes(self, current_round, params, key, biprime, total_sample_size, clipping_range,
                            num_expected_params, target_range, n2, n_ct, stripes, factors, dev) -> List[float]:
-        """The list API's aggregate over ct_offset stripes (one when the vector is small): per stripe the
+        """The list API's aggregate over ct_offset stripes (one when the vector is small).  Per stripe: the
         parties' ints -> pinned limbs -> H2D on a copy stream, the combine with that stripe's factor, the
-        float64 D2H in stream order, then the next stripe's factor; stripe k - 1's floats are built
-        while the GPU runs stripe k's combine and stripe k + 1's factor (the 10M-element float list is
-        the largest host cost of the call).  Stripe outputs: elements [c0 cr, c1 cr) capped by num_expected_params, as the unsplit
-        decode (_jls.py:146-167); a stripe past it still runs its checks (the unsplit call's errors)."""
+        float64 D2H in stream order, then the next stripe's factor.  Three things overlap: the next
+        stripe's ints convert on background threads (D.ints_to_limbs_async, no GIL), this thread writes
+        the stripe's floats into the output list (D.f64_into_list, one pass, no intermediate list: the
+        10M-element float list is the call's largest host cost), and the GPU runs the next stripe's
+        factor.  Stripe outputs: elements [c0 cr, c1 cr) capped by
+        num_expected_params, as the unsplit decode (_jls.py:146-167); a stripe past it still runs its
+        checks (the unsplit call's errors)."""
         _, cr = D.jl_slot(target_range or SAParameters.TARGET_RANGE, len(params))
         n_exp = int(num_expected_params)
+        n_outs = [max(0, min(n_exp - c0 * cr, (c1 - c0) * cr)) for c0, c1 in stripes]
+        offs = [sum(n_outs[:k]) for k in range(len(stripes))]
         packed = wire.packed_rows(params, "jl", n_ct)
-        main = torch.cuda.current_stream(dev)
-        copy = torch.cuda.Stream(device=dev)
-        keep, pending = [], []
-        res: List[float] = []
-        for k, (c0, c1) in enumerate(stripes):
-            # the stripe's limbs in a pinned buffer (its H2D is then truly asynchronous: it runs beside the
-            # factors on `main` and neither the host nor the copy waits for them)
+
+        def stage(k):  # stripe k's limbs in a pinned buffer: its H2D is then truly asynchronous
+            c0, c1 = stripes[k]
             staged = D.host_empty((len(params), c1 - c0, 64), torch.int32)
             limbs = staged.numpy().view(np.uint32)
             if packed is not None:
                 limbs[:] = packed[:, c0:c1]
-            else:
-                for u, p in enumerate(params):
-                    D.ints_to_limbs(p[c0:c1] if (c0, c1) != (0, len(p)) else p, n2, out=limbs[u])
+                return staged, None
+            return staged, D.ints_to_limbs_async(params, c0, c1, n2, limbs)
+
+        keep = []
+        nxt = stage(0)  # stripe 0's ints convert while the output list and the copy stream are made
+        main = torch.cuda.current_stream(dev)
+        copy = torch.cuda.Stream(device=dev)
+        res = D.float_list(sum(n_outs))
+        for k, (c0, c1) in enumerate(stripes):
+            staged, conv = nxt
+            if conv is not None:
+                conv.join()
             with torch.cuda.stream(copy):
                 cts = staged.to(dev, non_blocking=True)
             main.wait_stream(copy)
@@ -293,21 +303,19 @@ class SecaggCrypter:
             keep.append(staged)
             if factors[k] is None and len(stripes) > 1:
                 factors[k] = self.decrypt_factor_tensor(current_round, c1 - c0, key, biprime, ct_offset=c0)
-            n_out = max(0, min(n_exp - c0 * cr, (c1 - c0) * cr))
             out = self.aggregate_tensor(current_round, cts, key, biprime, total_sample_size, clipping_range,
-                                        n_out, target_range, ct_offset=c0, decrypt_factor=factors[k])
+                                        n_outs[k], target_range, ct_offset=c0, decrypt_factor=factors[k])
             out_h = D.host_empty(out.shape, torch.float64)
             out_h.copy_(out, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(main)
-            pending.append((out_h, ev))
             if k + 1 < len(stripes):  # the next stripe's factor right behind this stripe's combine
                 n0, n1 = stripes[k + 1]
                 factors[k + 1] = self.decrypt_factor_tensor(current_round, n1 - n0, key, biprime, ct_offset=n0)
-            if len(pending) > 1:  # stripe k - 1's floats while the GPU runs stripe k's combine and k + 1's factor
-                res += _stripe_floats(*pending.pop(0))
-        for out_h, ev in pending:
-            res += _stripe_floats(out_h, ev)
+                nxt = stage(k + 1)  # its ints convert in the background ...
+            # ... while this thread writes stripe k's floats as soon as its combine lands (the GPU has
+            # stripe k + 1's factor queued behind it: the factors pace the call, not the host)
+            _stripe_floats_into(res, offs[k], out_h, ev)
         return res
 
     @staticmethod
