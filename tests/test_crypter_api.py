@@ -171,9 +171,11 @@ def test_list_encrypt_overlapped_stripes_equal_unsplit(monkeypatch, caplog):
 @pytest.mark.gpu
 def test_list_aggregate_stripes_equal_unsplit(monkeypatch):
     """Round 5: the researcher's aggregate(List[List[int]]) runs as ct_offset stripes (stripe k's combine and
-    D2H, then stripe k + 1's factor, the floats built as each D2H lands).  Bit-identical to the unsplit call for
+    D2H, then stripe k + 1's factor; stripe k + 1's ints converted in the background while stripe k's floats are
+    written in place).  Bit-identical to the unsplit call for
     every stripe plan, with num_expected_params cutting inside a stripe, at a stripe edge, past the end and at
-    0, ragged lists (zip truncation) and the wire blob; errors as before (a zero sample size, a bad item)."""
+    0, ragged lists (zip truncation), out-of-range ciphertexts in any stripe and the wire blob; errors as before
+    (a zero sample size, a bad item)."""
     from fedbiomed_amd import _device as D, wire, workload as W
     from fedbiomed_amd.secagg import SecaggCrypter
 
@@ -200,6 +202,13 @@ def test_list_aggregate_stripes_equal_unsplit(monkeypatch):
         bad[2][5] = 1.5
         with pytest.raises(Exception, match="FB624"):
             jc.aggregate(tau, P, bad, -sum(keys), W.BIPRIME0, tw, num_expected_params=n)
+        # values outside [0, N^2) in a later stripe: the background conversion's slow path reduces them
+        n2 = W.BIPRIME0 ** 2
+        shifted = [list(c) for c in cl]
+        shifted[3][600] += n2
+        shifted[0][700] -= n2
+        shifted[1][2] += 5 * n2  # stripe 0 too
+        assert jc.aggregate(tau, P, shifted, -sum(keys), W.BIPRIME0, tw, num_expected_params=n) == ref[n], rnd
     monkeypatch.setenv("FBM_ONE_LANE_ROUND", "250")
     wire.enable()
     try:
