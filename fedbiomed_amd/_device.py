@@ -315,6 +315,8 @@ class _PyConvFallback:
         a = np.frombuffer(memoryview(buf).cast("B"), dtype=np.float64)
         if off < 0 or off + len(a) > len(lst):
             raise ValueError("float64 buffer does not fit the list at that offset")
+        if any(v is not None for v in lst[off:off + len(a)]):
+            raise ValueError("f64_into_list fills slots that hold None only")
         lst[off:off + len(a)] = a.tolist()
 
 

@@ -553,7 +553,8 @@ static PyObject* none_list(PyObject* self, PyObject* args) {
 }
 
 /* list[offset:offset + k] = the k float64 values of buf, as float objects made in place (one pass:
- * no intermediate list as ndarray.tolist() + extend would build). */
+ * no intermediate list as ndarray.tolist() + extend would build).  The slots must hold None (a
+ * none_list): releasing None runs no destructor, so no Python code can resize the list mid-loop. */
 static PyObject* f64_into_list(PyObject* self, PyObject* args) {
     PyObject* lst;
     Py_ssize_t off;
@@ -567,15 +568,20 @@ static PyObject* f64_into_list(PyObject* self, PyObject* args) {
     }
     const double* src = (const double*)view.buf;
     PyObject** items = ((PyListObject*)lst)->ob_item + off;
+    for (Py_ssize_t i = 0; i < k; ++i)
+        if (items[i] != Py_None) {
+            PyBuffer_Release(&view);
+            PyErr_SetString(PyExc_ValueError, "f64_into_list fills slots that hold None only");
+            return NULL;
+        }
     for (Py_ssize_t i = 0; i < k; ++i) {
         PyObject* v = PyFloat_FromDouble(src[i]);
         if (!v) {
             PyBuffer_Release(&view);
             return NULL;
         }
-        PyObject* old = items[i];
         items[i] = v;
-        Py_XDECREF(old);
+        Py_DECREF(Py_None);
     }
     PyBuffer_Release(&view);
     Py_RETURN_NONE;

@@ -270,5 +270,8 @@ def test_conv_contract_float_list(conv):
     with pytest.raises(ValueError):
         conv.f64_into_list(lst, 4, vals)  # past the end
     with pytest.raises(ValueError):
+        conv.f64_into_list(lst, 1, vals[:2])  # slot 2 already filled
+    assert lst[1] is None
+    with pytest.raises(ValueError):
         conv.none_list(-1)
     assert conv.none_list(0) == []
