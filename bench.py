@@ -708,12 +708,14 @@ def main():
         xs_h = [xs[p].cpu().pin_memory() for p in range(P)]
         ct_h = [torch.empty((n_ct, 64), dtype=torch.int32).pin_memory() for _ in range(P)]
         out_h = torch.empty(n, dtype=torch.float64).pin_memory()
+        cts_in = torch.empty((P, n_ct, 64), dtype=torch.int32, device=dev)  # the researcher's received block
 
         def step_e2e():
             # as the device-resident step: one stream per party (H2D -> prologue), the decryption
             # factor's prologue on its own stream, then the exponentiations (one batched launch),
-            # each party's D2H of its ciphertexts, the factor's inverse; then H2D of the
-            # ciphertexts -> combine -> D2H
+            # each party's D2H of its ciphertexts and, on the same stream once it has landed in host
+            # memory, the researcher's H2D of them into its row of the received block (PCIe is full
+            # duplex: party p's H2D runs beside party p + 1's D2H); then combine -> D2H
             with D.deferred_checks():
                 pend = [None] * P
                 for p in range(P):
@@ -739,19 +741,20 @@ def main():
                         with torch.cuda.stream(streams[p]):
                             ct_h[p].copy_(cts_d[p], non_blocking=True)
                             cts_d[p].record_stream(streams[p])
+                            cts_in[p].copy_(ct_h[p], non_blocking=True)
                 else:
                     with torch.cuda.stream(factor_stream):
                         pf.exponentiate()
                     for p in range(P):
                         with torch.cuda.stream(streams[p]):
                             ct_h[p].copy_(pend[p].finish(), non_blocking=True)
+                            cts_in[p].copy_(ct_h[p], non_blocking=True)
                     with torch.cuda.stream(factor_stream):
                         factor = pf.finish()
             for st in pool + [factor_stream]:
                 main.wait_stream(st)
             factor.record_stream(main)
-            cts_d = torch.stack([c.to(dev, non_blocking=True) for c in ct_h])
-            out_h.copy_(jc.aggregate_tensor(tau, cts_d, sk0, W.BIPRIME0, total_w, num_expected_params=n,
+            out_h.copy_(jc.aggregate_tensor(tau, cts_in, sk0, W.BIPRIME0, total_w, num_expected_params=n,
                                             decrypt_factor=factor), non_blocking=True)
             torch.cuda.synchronize()
 
@@ -759,6 +762,10 @@ def main():
         t0 = time.perf_counter()
         step_e2e()
         te = time.perf_counter() - t0
+        # the round trip through host memory changes nothing: the researcher's block is the device step's
+        # ciphertexts and the floats are the tensor aggregate's, bit for bit
+        e2e_equal = bool(torch.equal(cts_in, CT)) and bool(torch.equal(
+            out_h, D.to_host(jc.aggregate_tensor(tau, CT, sk0, W.BIPRIME0, total_w, num_expected_params=n))))
         # (b) the reference's list API (List[float] in, List[int] out per party; List[List[int]] in,
         #     List[float] out), on a bounded sample: Python int <-> limb conversion dominates
         nl = min(args.e2e_list_n, n)
@@ -912,8 +919,10 @@ def main():
                      "note": "P updates through msgpack (reference Serializer rules) and back, then aggregate; "
                              "blob = fedbiomed_amd.wire hook (SURVEY 8(f)2)"},
             "pinned_host_tensors": {"value": n / te, "unit": "params/s", "ms_per_step": 1000 * te,
-                                    "elements": n, "note": "per party stream H2D + encrypt + D2H, factor "
-                                                           "stream, then H2D + combine + D2H"},
+                                    "elements": n, "equals_device_step": e2e_equal,
+                                    "note": "per party stream H2D + encrypt + D2H, then that "
+                                                           "party's H2D into the researcher's block (beside "
+                                                           "the next party's D2H); factor stream; combine + D2H"},
             "list_api": {"value": nl / tl, "unit": "params/s", "ms_per_step": 1000 * tl, "elements": nl,
                          "note": "SecaggCrypter.encrypt (List[float] -> List[int]) x P + aggregate "
                                  "(List[List[int]] -> List[float]), the P parties issued one after another in "
@@ -934,8 +943,12 @@ def main():
         if Y is not None:
             yh = [torch.empty(n, dtype=torch.int64).pin_memory() for _ in range(P)]
             lout_h = torch.empty(n, dtype=torch.float64).pin_memory()
+            y_in = torch.empty_like(Y)  # the researcher's received block
 
             def step_lom_e2e():
+                # per party stream: H2D -> protect -> D2H of its masked row, then (once it is in host
+                # memory) the researcher's H2D of it into its row of the received block, beside the
+                # next party's D2H; then aggregate -> D2H
                 with D.deferred_checks():
                     for p, u in enumerate(ids):
                         streams[p].wait_stream(main)
@@ -943,10 +956,10 @@ def main():
                             x_d = xs_h[p].to(dev, non_blocking=True)
                             lc.encrypt_tensor(tau, u, x_d, secrets_[p], ids, weight=weights[p], out=Y[p])
                             yh[p].copy_(Y[p], non_blocking=True)
+                            y_in[p].copy_(yh[p], non_blocking=True)
                 for st in pool:
                     main.wait_stream(st)
-                y_d = torch.stack([v.to(dev, non_blocking=True) for v in yh])
-                lout_h.copy_(lc.aggregate_tensor(y_d, total_w), non_blocking=True)
+                lout_h.copy_(lc.aggregate_tensor(y_in, total_w), non_blocking=True)
                 torch.cuda.synchronize()
 
             step_lom_e2e()
@@ -955,14 +968,18 @@ def main():
             for _ in range(k3):
                 step_lom_e2e()
             tle = (time.perf_counter() - t0) / k3
+            lom_e2e_equal = bool(torch.equal(y_in, Y)) and bool(torch.equal(
+                lout_h, D.to_host(lc.aggregate_tensor(Y, total_w))))
             t0 = time.perf_counter()
             yl = [lc.encrypt(tau, u, xl[p], secrets_[p], ids, weight=weights[p]) for p, u in enumerate(ids)]
             lc.aggregate(yl, total_w)
             tll = time.perf_counter() - t0
             line["end_to_end"]["lom"] = {
                 "pinned_host_tensors": {"value": n / tle, "unit": "params/s", "ms_per_step": 1000 * tle,
-                                        "elements": n, "note": "per party stream H2D f32 + protect + D2H u64, "
-                                                               "then H2D of the P rows + aggregate + D2H f64"},
+                                        "elements": n, "equals_device_step": lom_e2e_equal,
+                                        "note": "per party stream H2D f32 + protect + D2H u64 + "
+                                                               "H2D of the row into the researcher's block "
+                                                               "(beside the next party's D2H); aggregate + D2H f64"},
                 "list_api": {"value": nl / tll, "unit": "params/s", "ms_per_step": 1000 * tll, "elements": nl,
                              "note": "SecaggLomCrypter.encrypt (List[float] -> List[int]) x P + aggregate "
                                      "(List[List[int]] -> List[float])"}}

@@ -1,0 +1,8 @@
+# round 5: the default bench line alone
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/${1:-r5p}
+mkdir -p $O
+cd $R
+timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "BENCH FAILED"; tail -20 $O/bench.err; exit 1; }
+cat $O/bench.json
