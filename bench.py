@@ -564,6 +564,12 @@ def main():
                                            ct_offset=lo // cr)
 
             t_enc, t_agg = t_stage(enc_all), t_stage(agg_alone)
+            # the combine alone, its factor issued ahead (decrypt_factor_tensor / prepare_aggregate: the
+            # researcher knows the round, key and size before the nodes reply)
+            fac = jc.decrypt_factor_tensor(tau, n_ct, sk0, W.BIPRIME0, ct_offset=lo // cr)
+            t_comb = t_stage(lambda: jc.aggregate_tensor(tau, cts_all, sk0, W.BIPRIME0, total_w, num_expected_params=n,
+                                                         ct_offset=lo // cr, decrypt_factor=fac))
+            del fac
         else:
             def enc_all():
                 with D.deferred_checks():
@@ -577,6 +583,10 @@ def main():
                           "enc_party_params_per_s": P * n_total / t_enc, "agg_params_per_s": n_total / t_agg,
                           "note": "T_enc: all parties' encrypts (one stream each), T_agg: one aggregate alone "
                                   "(decryption factor + combine); max over ranks; rates over elements_total"}
+        if args.scheme == "jl":
+            line["stages"]["T_combine_factor_ahead_ms"] = 1000 * t_comb
+            line["stages"]["note"] += ("; T_combine_factor_ahead: the aggregate with its decryption factor "
+                                       "computed beforehand (the factor's exponentiations off the critical path)")
         if gather:  # the step's final all-gather of the float64 output stripes, alone
             stripe = torch.zeros(n, dtype=torch.float64, device=dev)
             align = cr if args.scheme == "jl" else 8
@@ -829,9 +839,20 @@ def main():
                 res = jc.aggregate(tau, P, cl_u, sk0, W.BIPRIME0, total_w, num_expected_params=ne)
                 t = time.perf_counter() - t0
                 best = t if best is None else min(best, t)
+            eq = res == ref_out
+            # the same call after prepare_aggregate (the factor issued when the training request goes out,
+            # done by the time the nodes reply: the synchronize stands for their training time)
+            res = None
+            prepared = jc.prepare_aggregate(tau, P, sk0, W.BIPRIME0, ne)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            res = jc.aggregate(tau, P, cl_u, sk0, W.BIPRIME0, total_w, num_expected_params=ne)
+            tp = time.perf_counter() - t0
             return {"elements": ne, "parties": P, "ciphertexts_per_party": nct_u, "ms": 1000 * best,
                     "params_per_s": ne / best, "host_conversion_ms": 1000 * t_conv, "gpu_ms": 1000 * t_gpu,
-                    "equals_tensor_api": res == ref_out}
+                    "equals_tensor_api": eq,
+                    "factor_prepared": {"ms": 1000 * tp, "params_per_s": ne / tp, "prepared": prepared,
+                                        "equals_tensor_api": res == ref_out}}
 
         agg_l = researcher_aggregate(cl, nl)
         t_agg_l = agg_l["ms"] / 1000
@@ -935,7 +956,9 @@ def main():
                 note="SecaggCrypter.aggregate(List[List[int]]) of the P parties' ciphertext lists (at_metric_size: "
                      "the step's own 10M-element ciphertexts as Python ints, best of 2 calls); host_conversion "
                      "= ints -> pinned limbs -> H2D alone, gpu = aggregate_tensor + D2H + float list alone; the "
-                     "call itself issues the decryption factor before converting, so ms < the sum")}
+                     "call itself issues the decryption factor before converting, so ms < the sum; "
+                     "factor_prepared: the call after SecaggCrypter.prepare_aggregate (an extension: the "
+                     "factor issued with the training request, done when the nodes reply)")}
 
         # (d) LOM from and to host memory: pinned float32 -> H2D -> protect -> D2H u64 rows (one
         #     stream per party), then H2D of the rows -> aggregate -> D2H float64; and the

@@ -138,6 +138,31 @@ class deferred_checks:
         return False
 
 
+class capture_checks(deferred_checks):
+    """deferred_checks whose status words are NOT checked at exit but kept in `.pending`, for work
+    issued ahead of the call that uses it (SecaggCrypter.prepare_aggregate): that call hands them to
+    adopt_checks() inside its own deferred_checks, so a device condition of the early work is raised
+    by the call that consumes it, in its place."""
+
+    def __exit__(self, exc_type, exc, tb):
+        self.pending = deferred_checks._stack().pop()
+        return False
+
+
+def adopt_checks(pending: list) -> None:
+    """Status words captured by capture_checks: into the current deferred_checks context, or checked
+    now (waiting for their streams) when there is none."""
+    active = deferred_checks._stack()
+    if active:
+        active[-1].extend(pending)
+        return
+    for st, (nodes, post), ev in pending:
+        ev.synchronize()
+        _check_stats_host(st.cpu().numpy(), nodes)
+        if post is not None:
+            raise post
+
+
 def _check_stats_or_defer(stats: torch.Tensor, lom_nodes: int = 0, post: Optional[Exception] = None) -> None:
     """`post`: a host-known error of the same call, raised after the device conditions (the
     reference's order, e.g. LOM's round-counter overflow after its overflow guard)."""

@@ -71,6 +71,14 @@ def _check_int_lists(params) -> None:
             f"should be of type of integers.")
 
 
+def _prep_tag(current_round, num_nodes, key, biprime, target_range) -> bytes:
+    """What prepare_aggregate's factors belong to, without keeping the key: SHA-256 of the arguments."""
+    import hashlib
+
+    return hashlib.sha256(repr((current_round, num_nodes, key, biprime, target_range or SAParameters.TARGET_RANGE))
+                          .encode()).digest()
+
+
 def _stripe_floats_into(res: List[float], off: int, out_h: torch.Tensor, ev) -> None:
     """One aggregate stripe's Python floats into res[off:], once its D2H (recorded as `ev`) has landed."""
     ev.synchronize()
@@ -210,6 +218,66 @@ class SecaggCrypter:
                 out += D.limbs_to_ints(packed[c0:c1])
         return packed, out
 
+    def prepare_aggregate(self, current_round: int, num_nodes: int, key: int, biprime: int,
+                          num_expected_params: int, target_range: Optional[int] = None) -> bool:
+        """Extension (not in the reference): issue the decryption factor of a coming `aggregate` now.
+        The factor H(t_k)^key of every ciphertext depends only on the round, the server key, the
+        biprime and the vector's size, which the researcher knows when it sends the training request
+        (`researcher/secagg/_secure_aggregation.py`), so its exponentiations -- most of the aggregate's
+        GPU time -- can run on a side stream while the nodes train.  The next `aggregate` of the same
+        round, key, biprime, node count, target range and ciphertext count takes it (once); other calls
+        of that round leave it, a call of another round drops it.  A device condition of the early work
+        is raised by the aggregate that takes it.
+        Best effort: False (nothing prepared) where aggregate would refuse the arguments.  The key
+        itself is not kept, only a SHA-256 tag of it."""
+        self._prepared = None
+        try:
+            if not all(isinstance(v, int) for v in (current_round, num_nodes, key, biprime, num_expected_params)):
+                return False
+            if num_nodes < 1:
+                return False
+            _, cr = D.jl_slot(target_range or SAParameters.TARGET_RANGE, num_nodes)
+            n_ct = -(-num_expected_params // cr)
+            if n_ct <= 0:
+                return False
+            dev = D.device()
+            stripes = D.list_encrypt_stripes(n_ct, dev)
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side), D.capture_checks() as checks:
+                factors = [self.decrypt_factor_tensor(current_round, c1 - c0, key, biprime, ct_offset=c0)
+                           for c0, c1 in stripes]
+            ev = torch.cuda.Event()
+            ev.record(side)
+        except Exception:  # noqa: BLE001 -- aggregate raises whatever it is, in the reference's order
+            return False
+        self._prepared = {"round": current_round, "tag": _prep_tag(current_round, num_nodes, key, biprime, target_range),
+                          "n_ct": n_ct,
+                          "stripes": stripes, "factors": factors, "event": ev, "checks": checks.pending}
+        return True
+
+    def _take_prepared(self, current_round, num_nodes, key, biprime, target_range, n_ct, dev):
+        """The prepared factors when they are this call's (waited for on the current stream, their status
+        words adopted by the call's deferred checks; the preparation is then spent), else None.  A call of
+        the same round that is not the prepared one -- the researcher's insecure-validation aggregate of the
+        encryption factors (num_expected_params = 1, `_secure_aggregation.py:372-375`) comes first -- leaves
+        it in place; a call of another round drops it."""
+        prep = getattr(self, "_prepared", None)
+        if prep is None:
+            return None
+        if prep["round"] != current_round:
+            self._prepared = None
+            return None
+        if prep["n_ct"] != n_ct or prep["tag"] != _prep_tag(current_round, num_nodes, key, biprime, target_range):
+            return None
+        self._prepared = None
+        main = torch.cuda.current_stream(dev)
+        main.wait_event(prep["event"])
+        for f in prep["factors"]:
+            f.record_stream(main)
+        D.adopt_checks(prep["checks"])
+        return prep["stripes"], prep["factors"]
+
     def aggregate(self, current_round: int, num_nodes: int, params: List[List[int]], key: int, biprime: int,
                   total_sample_size: int, clipping_range: Union[int, None] = None, num_expected_params: int = 1,
                   target_range: Optional[int] = None) -> List[float]:
@@ -234,13 +302,20 @@ class SecaggCrypter:
             if params and isinstance(key, int) and isinstance(biprime, int) and all(type(p) is list for p in params):
                 n_ct0 = min(len(p) for p in params)
                 if n_ct0:
-                    stripes = D.list_encrypt_stripes(n_ct0, D.device())
-                    factors = [None] * len(stripes)
-                    try:
-                        c0, c1 = stripes[0]
-                        factors[0] = self.decrypt_factor_tensor(current_round, c1 - c0, key, biprime, ct_offset=c0)
-                    except Exception:  # noqa: BLE001 -- re-raised by the regular path below
-                        stripes = None
+                    prep = self._take_prepared(current_round, num_nodes, key, biprime, target_range, n_ct0,
+                                               D.device())
+                    if prep is not None:  # prepare_aggregate's factors: every stripe's, issued ahead
+                        stripes, factors = prep[0], list(prep[1])
+                    else:
+                        stripes = D.list_encrypt_stripes(n_ct0, D.device())
+                        factors = [None] * len(stripes)
+                        try:
+                            c0, c1 = stripes[0]
+                            factors[0] = self.decrypt_factor_tensor(current_round, c1 - c0, key, biprime,
+                                                                    ct_offset=c0)
+                        except Exception:  # noqa: BLE001 -- re-raised by the regular path below
+                            stripes = None
+
             _check_int_lists(params)
             if not isinstance(key, int):
                 raise TypeError("The key should be type of integer")
@@ -311,7 +386,8 @@ class SecaggCrypter:
             ev.record(main)
             if k + 1 < len(stripes):  # the next stripe's factor right behind this stripe's combine
                 n0, n1 = stripes[k + 1]
-                factors[k + 1] = self.decrypt_factor_tensor(current_round, n1 - n0, key, biprime, ct_offset=n0)
+                if factors[k + 1] is None:
+                    factors[k + 1] = self.decrypt_factor_tensor(current_round, n1 - n0, key, biprime, ct_offset=n0)
                 nxt = stage(k + 1)  # its ints convert in the background ...
             # ... while this thread writes stripe k's floats as soon as its combine lands (the GPU has
             # stripe k + 1's factor queued behind it: the factors pace the call, not the host)
@@ -346,6 +422,10 @@ class SecaggCrypter:
 
 class SecaggLomCrypter(SecaggCrypter):
     """Low-Overhead Masking secure aggregation (reference `_secagg_crypter.py:300-455`)."""
+
+    def prepare_aggregate(self, *args, **kwargs) -> bool:
+        """LOM's aggregate is a sum with no exponentiation: nothing to issue ahead."""
+        return False
 
     def __init__(self, nonce: Optional[str] = None):
         if nonce:

@@ -217,3 +217,55 @@ def test_list_aggregate_stripes_equal_unsplit(monkeypatch):
         assert jc.aggregate(tau, P, cw, -sum(keys), W.BIPRIME0, tw, num_expected_params=n) == ref[n]
     finally:
         wire.enable(False)
+
+
+@pytest.mark.gpu
+def test_prepare_aggregate_factor_ahead(monkeypatch):
+    """prepare_aggregate (an extension): the decryption factor issued before the parties' lists exist.  The
+    next aggregate of the same round / key / biprime / node count / size takes it and is bit-identical to an
+    unprepared call, striped or not; it is used once; another call of the round leaves it (the researcher's
+    validation aggregate comes first), a call of another round drops it; arguments aggregate would refuse
+    prepare nothing."""
+    from fedbiomed_amd import workload as W
+    from fedbiomed_amd.secagg import SecaggCrypter, SecaggLomCrypter
+
+    P, tau, n = 4, 6, 20_011
+    keys = [W.jl_user_key(p) for p in range(P)]
+    sk0 = -sum(keys)
+    jc = SecaggCrypter()
+    cl = [jc.encrypt(P, tau, [float(v) for v in W.party_params(p, n)], keys[p], W.BIPRIME0, weight=2 + p)
+          for p in range(P)]
+    tw = sum(2 + p for p in range(P))
+    for rnd in (None, "200"):
+        if rnd is None:
+            monkeypatch.delenv("FBM_ONE_LANE_ROUND", raising=False)
+        else:
+            monkeypatch.setenv("FBM_ONE_LANE_ROUND", rnd)
+        ref = jc.aggregate(tau, P, cl, sk0, W.BIPRIME0, tw, num_expected_params=n)
+        assert jc.prepare_aggregate(tau, P, sk0, W.BIPRIME0, n) is True
+        assert jc._prepared is not None
+        assert jc.aggregate(tau, P, cl, sk0, W.BIPRIME0, tw, num_expected_params=n) == ref, rnd
+        assert jc._prepared is None  # spent
+        assert jc.aggregate(tau, P, cl, sk0, W.BIPRIME0, tw, num_expected_params=n) == ref
+        # another round's preparation is dropped by this round's call
+        assert jc.prepare_aggregate(tau + 1, P, sk0, W.BIPRIME0, n) is True
+        assert jc.aggregate(tau, P, cl, sk0, W.BIPRIME0, tw, num_expected_params=n) == ref
+        assert jc._prepared is None
+        # same round, another key / size: ignored and kept
+        for other in ((tau, P, sk0 - 1, W.BIPRIME0, n), (tau, P, sk0, W.BIPRIME0, n + 10_000)):
+            assert jc.prepare_aggregate(*other) is True
+            assert jc.aggregate(tau, P, cl, sk0, W.BIPRIME0, tw, num_expected_params=n) == ref, other
+            assert jc._prepared is not None
+        # the researcher's flow (_secure_aggregation.py:354-401): the insecure-validation aggregate of
+        # one-ciphertext encryption factors first, then the model's -- which takes the preparation
+        ef = [jc.encrypt(P, tau, [0.25], keys[p], W.BIPRIME0, weight=2 + p) for p in range(P)]
+        val_ref = jc.aggregate(tau, P, ef, sk0, W.BIPRIME0, tw, num_expected_params=1)
+        assert jc.prepare_aggregate(tau, P, sk0, W.BIPRIME0, n) is True
+        assert jc.aggregate(tau, P, ef, sk0, W.BIPRIME0, tw, num_expected_params=1) == val_ref
+        assert jc._prepared is not None
+        assert jc.aggregate(tau, P, cl, sk0, W.BIPRIME0, tw, num_expected_params=n) == ref
+        assert jc._prepared is None
+    for bad in ((tau, P, 1.5, W.BIPRIME0, n), (tau, P, sk0, W.BIPRIME0, 0), (tau, 0, sk0, W.BIPRIME0, n),
+                (tau, P, sk0, "N", n)):
+        assert jc.prepare_aggregate(*bad) is False
+    assert SecaggLomCrypter().prepare_aggregate(tau, P, sk0, W.BIPRIME0, n) is False

@@ -1,0 +1,26 @@
+"""SecaggCrypter.prepare_aggregate (an extension) without a GPU: nothing is prepared and nothing
+raises -- aggregate itself then raises the no-device error, as it does without a preparation.
+CPU only."""
+import torch
+
+from fedbiomed_amd.secagg import SecaggCrypter, SecaggLomCrypter
+from fedbiomed_amd.secagg._secagg_crypter import _prep_tag
+
+
+def test_prepare_without_device_prepares_nothing():
+    jc = SecaggCrypter()
+    if torch.cuda.is_available():  # (the GPU behaviour is tests/test_crypter_api.py's)
+        return
+    assert jc.prepare_aggregate(3, 2, -5, 2**61 - 1, 100) is False
+    assert getattr(jc, "_prepared", None) is None
+    assert SecaggLomCrypter().prepare_aggregate(3, 2, -5, 2**61 - 1, 100) is False
+
+
+def test_prep_tag_keeps_no_key_and_separates_arguments():
+    a = _prep_tag(3, 4, -123456789, 97, None)
+    assert len(a) == 32 and b"123456789" not in a
+    assert a == _prep_tag(3, 4, -123456789, 97, 2**13)  # None = the default target range
+    others = [_prep_tag(4, 4, -123456789, 97, None), _prep_tag(3, 5, -123456789, 97, None),
+              _prep_tag(3, 4, -123456788, 97, None), _prep_tag(3, 4, -123456789, 101, None),
+              _prep_tag(3, 4, -123456789, 97, 2**55)]
+    assert len({a, *others}) == 6
