@@ -265,6 +265,19 @@ def test_prepare_aggregate_factor_ahead(monkeypatch):
         assert jc._prepared is not None
         assert jc.aggregate(tau, P, cl, sk0, W.BIPRIME0, tw, num_expected_params=n) == ref
         assert jc._prepared is None
+    # the wire blobs' packed rows (no int conversion) take the prepared factor too
+    from fedbiomed_amd import wire
+
+    monkeypatch.setenv("FBM_ONE_LANE_ROUND", "200")
+    wire.enable()
+    try:
+        cw = [jc.encrypt(P, tau, [float(v) for v in W.party_params(p, n)], keys[p], W.BIPRIME0, weight=2 + p)
+              for p in range(P)]
+        assert jc.prepare_aggregate(tau, P, sk0, W.BIPRIME0, n) is True
+        assert jc.aggregate(tau, P, cw, sk0, W.BIPRIME0, tw, num_expected_params=n) == ref
+        assert jc._prepared is None
+    finally:
+        wire.enable(False)
     for bad in ((tau, P, 1.5, W.BIPRIME0, n), (tau, P, sk0, W.BIPRIME0, 0), (tau, 0, sk0, W.BIPRIME0, n),
                 (tau, P, sk0, "N", n)):
         assert jc.prepare_aggregate(*bad) is False
