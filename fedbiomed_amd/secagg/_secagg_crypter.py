@@ -299,7 +299,7 @@ class SecaggCrypter:
             # exponentiates stripe k + 1 (every element depends on its own ciphertext only: the
             # stripes' outputs concatenate to the unsplit call's).
             stripes, factors = None, []
-            if params and isinstance(key, int) and isinstance(biprime, int) and all(type(p) is list for p in params):
+            if params and isinstance(key, int) and isinstance(biprime, int) and all(isinstance(p, list) for p in params):
                 n_ct0 = min(len(p) for p in params)
                 if n_ct0:
                     prep = self._take_prepared(current_round, num_nodes, key, biprime, target_range, n_ct0,
