@@ -71,12 +71,19 @@ def _check_int_lists(params) -> None:
             f"should be of type of integers.")
 
 
-def _prep_tag(current_round, num_nodes, key, biprime, target_range) -> bytes:
-    """What prepare_aggregate's factors belong to, without keeping the key: SHA-256 of the arguments."""
+def _prep_tag(current_round, num_nodes, key, biprime, target_range) -> Optional[bytes]:
+    """What prepare_aggregate's factors belong to, without keeping the key: SHA-256 over the arguments'
+    length-prefixed two's-complement bytes (None when one is not an int: nothing matches it)."""
     import hashlib
 
-    return hashlib.sha256(repr((current_round, num_nodes, key, biprime, target_range or SAParameters.TARGET_RANGE))
-                          .encode()).digest()
+    vals = (current_round, num_nodes, key, biprime, target_range or SAParameters.TARGET_RANGE)
+    if not all(isinstance(v, int) for v in vals):
+        return None
+    h = hashlib.sha256()
+    for v in vals:
+        b = v.to_bytes(v.bit_length() // 8 + 1, "little", signed=True)
+        h.update(len(b).to_bytes(8, "little") + b)
+    return h.digest()
 
 
 def _stripe_floats_into(res: List[float], off: int, out_h: torch.Tensor, ev) -> None:
@@ -268,7 +275,8 @@ class SecaggCrypter:
         if prep["round"] != current_round:
             self._prepared = None
             return None
-        if prep["n_ct"] != n_ct or prep["tag"] != _prep_tag(current_round, num_nodes, key, biprime, target_range):
+        tag = _prep_tag(current_round, num_nodes, key, biprime, target_range)
+        if prep["n_ct"] != n_ct or tag is None or prep["tag"] != tag:
             return None
         self._prepared = None
         main = torch.cuda.current_stream(dev)

@@ -24,3 +24,5 @@ def test_prep_tag_keeps_no_key_and_separates_arguments():
               _prep_tag(3, 4, -123456788, 97, None), _prep_tag(3, 4, -123456789, 101, None),
               _prep_tag(3, 4, -123456789, 97, 2**55)]
     assert len({a, *others}) == 6
+    assert _prep_tag(3, 4, 2**100000, 97, None) is not None  # no decimal conversion of a huge key
+    assert _prep_tag(3.0, 4, 5, 97, None) is None and _prep_tag(3, 4, 5, "97", None) is None
