@@ -63,6 +63,25 @@ def mads_per_exp(key: int, mads: tuple) -> int:
     return sum(c * m for c, m in zip(products_per_exp(key), mads))
 
 
+def cgroup_cpu_quota():
+    """CPUs' worth of CPU time the process's cgroup allows (cgroup v2 cpu.max, v1 cfs quota / period),
+    or None when unlimited or unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+            q = int(fh.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+            per = int(fh.read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
 def committed_traffic(kernel: str, scheme: str, elements: int, n_ct=None):
     """(HBM bytes per launch of `kernel`, the profile file) from the committed rocprofv3 PMC summary
     of this workload -- same scheme and elements per GPU (JL: same ciphertexts per party) --
@@ -1024,19 +1043,23 @@ def main():
             O.lom_crypter_aggregate(ys, total_w)
         tc = time.perf_counter() - t0
         try:
-            avail = len(os.sched_getaffinity(0))  # the cores this process may run on (the box's CPU share)
+            avail = len(os.sched_getaffinity(0))  # the cores this process may run on
         except (AttributeError, OSError):
             avail = os.cpu_count() or 1
+        quota = cgroup_cpu_quota()  # the CPU time it may use (a cgroup limit: the box's CPU share)
+        share = max(1, min(avail, int(quota))) if quota else avail
         line["cpu_baseline"] = {"value": ns / tc, "unit": "params/s", "cores": 1, "kind": "port",
                                 "sample": f"{ns:,} elements x {P} parties, encrypt all + aggregate, "
                                           f"{tc:.1f} s on 1 host core (oracle/secagg_oracle.py; GMP mpz_powm "
                                           f"via ctypes as gmpy2 does)",
-                                "host_cores": {"available": avail, "machine": os.cpu_count()},
+                                "host_cores": {"available": avail, "machine": os.cpu_count(),
+                                               "cgroup_cpu_quota": quota, "share": share},
                                 "ideal_all_cores": {
-                                    "value": ns / tc * avail, "unit": "params/s", "cores": avail,
-                                    "note": "the 1-core rate x the cores available to this process (SURVEY 8(d)): "
-                                            "the reference is single-threaded; every ciphertext is independent, so "
-                                            "this is the ceiling of a perfectly parallel CPU port, not a measurement"}}
+                                    "value": ns / tc * share, "unit": "params/s", "cores": share,
+                                    "note": "the 1-core rate x the CPUs this process may use -- its affinity, capped by "
+                                            "its cgroup CPU quota (SURVEY 8(d)): the reference is single-threaded; "
+                                            "every ciphertext is independent, so this is the ceiling of a perfectly "
+                                            "parallel CPU port on this box's share, not a measurement"}}
         cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")  # tools/calibrate_cpu.py
         if os.path.exists(cal):
             with open(cal) as fh:

@@ -1,0 +1,11 @@
+# round 5, pass 11: the N > 1 bench path rehearsed on one GPU at this round's code (gloo, 2 and 4 ranks),
+# and the per-kernel breakdown of the aggregate on rank 0's stripe of a 1/2/4/8-GPU split
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/${1:-r5s}
+mkdir -p $O
+cd $R
+python -c "import os, bench; print(\"cgroup quota\", bench.cgroup_cpu_quota(), \"affinity\", len(os.sched_getaffinity(0)))"
+bash tools/rehearse_dist.sh ${1:-r5s} || exit 1
+timeout -k 10 300 python -u tools/agg_breakdown.py > $O/agg_breakdown.jsonl 2> $O/agg_breakdown.err || { echo "AGG BREAKDOWN FAILED"; tail -20 $O/agg_breakdown.err; exit 1; }
+tail -3 $O/agg_breakdown.jsonl
