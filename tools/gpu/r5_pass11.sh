@@ -9,3 +9,7 @@ python -c "import os, bench; print(\"cgroup quota\", bench.cgroup_cpu_quota(), \
 bash tools/rehearse_dist.sh ${1:-r5s} || exit 1
 timeout -k 10 300 python -u tools/agg_breakdown.py > $O/agg_breakdown.jsonl 2> $O/agg_breakdown.err || { echo "AGG BREAKDOWN FAILED"; tail -20 $O/agg_breakdown.err; exit 1; }
 tail -3 $O/agg_breakdown.jsonl
+timeout -k 10 300 python -u tools/list_agg_probe.py --first-call plain > $O/first_call_plain.jsonl 2>&1 || { echo "FIRST CALL PLAIN FAILED"; tail -5 $O/first_call_plain.jsonl; exit 1; }
+tail -1 $O/first_call_plain.jsonl
+timeout -k 10 300 python -u tools/list_agg_probe.py --first-call prepared > $O/first_call_prepared.jsonl 2>&1 || { echo "FIRST CALL PREPARED FAILED"; tail -5 $O/first_call_prepared.jsonl; exit 1; }
+tail -1 $O/first_call_prepared.jsonl

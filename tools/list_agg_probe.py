@@ -4,7 +4,7 @@
 per call by csrc/fbm_pyconv.c), best of 3 calls each, with the conversion and the output float list alone beside it.  One JSON line
 per thread count.
 
-    python tools/list_agg_probe.py [--threads 4,8,16] [--elements 10000000]
+    python tools/list_agg_probe.py [--threads 4,8,16] [--elements 10000000] [--first-call plain|prepared]
 """
 import argparse
 import json
@@ -20,6 +20,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", default="4,8,16")
     ap.add_argument("--elements", type=int, default=10_000_000)
+    ap.add_argument("--first-call", choices=("plain", "prepared"), default=None,
+                    help="time only the process's first aggregate, with or without prepare_aggregate before it")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -40,6 +42,15 @@ def main():
         del ct, x
     tw = sum(W.party_weight(p) for p in range(P))
     n2 = W.BIPRIME0 * W.BIPRIME0
+    if args.first_call:  # the first aggregate of a fresh crypter process (a researcher's first round)
+        prepared = jc.prepare_aggregate(tau, P, sk0, W.BIPRIME0, n) if args.first_call == "prepared" else False
+        torch.cuda.synchronize()  # (the nodes' training time)
+        t0 = time.perf_counter()
+        jc.aggregate(tau, P, lists, sk0, W.BIPRIME0, tw, num_expected_params=n)
+        t = time.perf_counter() - t0
+        print(json.dumps({"first_call": args.first_call, "prepared": prepared, "elements": n, "parties": P,
+                          "aggregate_ms": 1000 * t}), flush=True)
+        return
     ref = None
     for t in [int(v) for v in args.threads.split(",")]:
         os.environ["FBM_CONV_THREADS"] = str(t)
