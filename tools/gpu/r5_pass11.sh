@@ -6,6 +6,8 @@ O=$R/gpurun_out/${1:-r5s}
 mkdir -p $O
 cd $R
 python -c "import os, bench; print(\"cgroup quota\", bench.cgroup_cpu_quota(), \"affinity\", len(os.sched_getaffinity(0)))"
+timeout -k 10 300 python -u -m pytest tests/test_crypter_api.py -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest_crypter.txt 2>&1 || { echo "PYTEST FAILED"; tail -40 $O/pytest_crypter.txt; exit 1; }
+tail -2 $O/pytest_crypter.txt
 bash tools/rehearse_dist.sh ${1:-r5s} || exit 1
 timeout -k 10 300 python -u tools/agg_breakdown.py > $O/agg_breakdown.jsonl 2> $O/agg_breakdown.err || { echo "AGG BREAKDOWN FAILED"; tail -20 $O/agg_breakdown.err; exit 1; }
 tail -3 $O/agg_breakdown.jsonl
@@ -13,3 +15,5 @@ timeout -k 10 300 python -u tools/list_agg_probe.py --first-call plain > $O/firs
 tail -1 $O/first_call_plain.jsonl
 timeout -k 10 300 python -u tools/list_agg_probe.py --first-call prepared > $O/first_call_prepared.jsonl 2>&1 || { echo "FIRST CALL PREPARED FAILED"; tail -5 $O/first_call_prepared.jsonl; exit 1; }
 tail -1 $O/first_call_prepared.jsonl
+timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "BENCH FAILED"; tail -20 $O/bench.err; exit 1; }
+tail -c 400 $O/bench.json
