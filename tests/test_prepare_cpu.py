@@ -41,3 +41,38 @@ def test_fine_stripes_tile_and_slice():
         owner = max(k for k, (s0, _) in enumerate(st) if s0 <= c0)
         assert t.shape[0] == c1 - c0 and int(t[0, 0]) == c0 - st[owner][0] and t.is_contiguous()
     assert _fine_stripes([(0, 5)], [None]) == ([(0, 5)], [None])
+
+
+class _Ev:
+    def __init__(self):
+        self.waited = False
+
+    def synchronize(self):
+        self.waited = True
+
+
+def test_capture_and_adopt_checks():
+    """Status words of work issued ahead (capture_checks) are checked by the call that adopts them: inside
+    its deferred_checks (at that context's exit) or at once without one -- a device error flag raises
+    there, not in the early call."""
+    import numpy as np
+    import pytest
+
+    from fedbiomed_amd import _device as D
+
+    err = 2  # FBM_ERR_FDH_OVERFLOW (csrc/fbm_internal.hpp): the reference's OverflowError
+    ok, bad = torch.zeros(4, dtype=torch.int32), torch.zeros(4, dtype=torch.int32)
+    bad[D.FBM_STAT_ERRFLAGS] = err
+    with D.capture_checks() as cap:
+        D.deferred_checks._stack()[-1].append((ok, (0, None), _Ev()))
+        D.deferred_checks._stack()[-1].append((bad, (0, None), _Ev()))
+    assert len(cap.pending) == 2 and D.deferred_checks._stack() == []  # nothing checked, nothing raised
+    D.adopt_checks(cap.pending[:1])  # no context: checked at once, waiting for its event
+    assert cap.pending[0][2].waited
+    with pytest.raises(OverflowError):
+        D.adopt_checks(cap.pending[1:])
+    with D.deferred_checks() as outer:  # inside a context: appended, raised at its exit only
+        D.adopt_checks([(ok, (0, None), _Ev())])
+        assert len(D.deferred_checks._stack()[-1]) == 1
+        D.deferred_checks._stack()[-1].clear()  # (no device here to stack the words on)
+    assert outer is not None and np.asarray(bad)[D.FBM_STAT_ERRFLAGS] == err
