@@ -15,5 +15,9 @@ timeout -k 10 300 python -u tools/list_agg_probe.py --first-call plain > $O/firs
 tail -1 $O/first_call_plain.jsonl
 timeout -k 10 300 python -u tools/list_agg_probe.py --first-call prepared > $O/first_call_prepared.jsonl 2>&1 || { echo "FIRST CALL PREPARED FAILED"; tail -5 $O/first_call_prepared.jsonl; exit 1; }
 tail -1 $O/first_call_prepared.jsonl
+FBM_AGG_TAIL_SPLIT=0 timeout -k 10 300 python -u tools/list_agg_probe.py --threads 8 > $O/list_agg_probe_nosplit.jsonl 2>&1 || { echo "PROBE NOSPLIT FAILED"; exit 1; }
+tail -1 $O/list_agg_probe_nosplit.jsonl
+timeout -k 10 300 python -u tools/list_agg_probe.py --threads 8 > $O/list_agg_probe.jsonl 2>&1 || { echo "PROBE FAILED"; exit 1; }
+tail -1 $O/list_agg_probe.jsonl
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "BENCH FAILED"; tail -20 $O/bench.err; exit 1; }
 tail -c 400 $O/bench.json

@@ -88,7 +88,7 @@ def main():
     del out
     (SC._stripe_floats_into, A.__init__, A.join, jc.decrypt_factor_tensor, jc.aggregate_tensor,
      SC._check_int_lists) = orig
-    print(json.dumps({"elements": n, "parties": P, "stripes": D.list_encrypt_stripes(len(lists[0]), dev),
+    print(json.dumps({"elements": n, "parties": P, "stripes": D.list_aggregate_stripes(len(lists[0]), dev),
                       "warm_ms": warm, "profiled_ms": prof_ms, "marked_ms": total,
                       "marks_name_start_ms_dur_ms": marks}), flush=True)
 
