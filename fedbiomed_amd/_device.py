@@ -689,23 +689,6 @@ def list_encrypt_stripes(n_ct: int, dev=None) -> List[Tuple[int, int]]:
     return list(zip(cuts[:-1], cuts[1:]))
 
 
-def list_aggregate_stripes(n_ct: int, dev=None) -> List[Tuple[int, int]]:
-    """The list aggregate's stripes: the encrypt's (full one-lane rounds, the partial round last), with a
-    partial round of a quarter round or more (32 768 ciphertexts on MI355X) cut in two halves.  The aggregate's last stripe is
-    its tail -- its floats are built after the GPU's last factor -- and a half-size partial round costs
-    the group engines about half the time (a 1/8 stripe's 41 667 ciphertexts: 21 ms, 71 190: 38 ms), so
-    the cut trades ~4 ms of GPU for half the tail's float list (~13 ms at 10M x 8).
-    FBM_AGG_TAIL_SPLIT=0 keeps the encrypt's plan (an A/B switch)."""
-    stripes = list_encrypt_stripes(n_ct, dev)
-    if len(stripes) < 2 or os.environ.get("FBM_AGG_TAIL_SPLIT", "1") == "0":
-        return stripes
-    c0, c1 = stripes[-1]
-    if c1 - c0 < max(2, one_lane_round(dev) // 4):
-        return stripes
-    mid = (c0 + c1 + 1) // 2
-    return stripes[:-1] + [(c0, mid), (mid, c1)]
-
-
 def jl_engine_for(n_ct: int) -> str:
     """The engine a launch of n_ct ciphertexts takes under the current policy."""
     return {1: "single", 2: "generic", 3: "triple", 4: "quad"}[N.load().fbm_jl_engine_for(int(n_ct))]

@@ -269,7 +269,7 @@ class SecaggCrypter:
             if n_ct <= 0:
                 return False
             dev = D.device()
-            stripes = D.list_aggregate_stripes(n_ct, dev)
+            stripes = D.list_encrypt_stripes(n_ct, dev)
             side = torch.cuda.Stream(device=dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side), D.capture_checks() as checks:
@@ -343,7 +343,7 @@ class SecaggCrypter:
                     if prep is not None:  # prepare_aggregate's factors: every stripe's, issued ahead
                         stripes, factors = _fine_stripes(*prep)
                     else:
-                        stripes = D.list_aggregate_stripes(n_ct0, D.device())
+                        stripes = D.list_encrypt_stripes(n_ct0, D.device())
                         factors = [None] * len(stripes)
                         try:
                             c0, c1 = stripes[0]

@@ -76,14 +76,3 @@ def test_capture_and_adopt_checks():
         assert len(D.deferred_checks._stack()[-1]) == 1
         D.deferred_checks._stack()[-1].clear()  # (no device here to stack the words on)
     assert outer is not None and np.asarray(bad)[D.FBM_STAT_ERRFLAGS] == err
-
-
-def test_list_aggregate_stripes_split_the_partial_round(monkeypatch):
-    from fedbiomed_amd import _device as D
-
-    monkeypatch.setenv("FBM_ONE_LANE_ROUND", "131072")
-    assert D.list_aggregate_stripes(333334) == [(0, 131072), (131072, 262144), (262144, 297739), (297739, 333334)]
-    assert D.list_aggregate_stripes(100000) == [(0, 100000)]  # one stripe: nothing to overlap
-    assert D.list_aggregate_stripes(262144 + 20000) == D.list_encrypt_stripes(262144 + 20000)  # a short tail rides
-    monkeypatch.setenv("FBM_AGG_TAIL_SPLIT", "0")
-    assert D.list_aggregate_stripes(333334) == D.list_encrypt_stripes(333334)

@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--elements", type=int, default=10_000_000)
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--prepared", action="store_true", help="prepare_aggregate before every call (synchronised)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -45,6 +46,8 @@ def main():
     tw = sum(W.party_weight(p) for p in range(P))
 
     def call():  # the previous result is freed before the clock starts (10M floats: ~50 ms to free)
+        if args.prepared:
+            assert jc.prepare_aggregate(tau, P, sk0, W.BIPRIME0, n)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         out = jc.aggregate(tau, P, lists, sk0, W.BIPRIME0, tw, num_expected_params=n)
@@ -81,6 +84,8 @@ def main():
     jc.decrypt_factor_tensor = mark("factor_issue", jc.decrypt_factor_tensor)
     jc.aggregate_tensor = mark("combine_issue", jc.aggregate_tensor)
     SC._check_int_lists = mark("check_int_lists", SC._check_int_lists)
+    if args.prepared:
+        assert jc.prepare_aggregate(tau, P, sk0, W.BIPRIME0, n)
     torch.cuda.synchronize()
     t_start[0] = time.perf_counter()
     out = jc.aggregate(tau, P, lists, sk0, W.BIPRIME0, tw, num_expected_params=n)
@@ -88,7 +93,9 @@ def main():
     del out
     (SC._stripe_floats_into, A.__init__, A.join, jc.decrypt_factor_tensor, jc.aggregate_tensor,
      SC._check_int_lists) = orig
-    print(json.dumps({"elements": n, "parties": P, "stripes": D.list_aggregate_stripes(len(lists[0]), dev),
+    print(json.dumps({"elements": n, "parties": P, "prepared": args.prepared,
+                      "fine_stripe_ct": os.environ.get("FBM_FINE_STRIPE_CT"),
+                      "stripes": D.list_encrypt_stripes(len(lists[0]), dev),
                       "warm_ms": warm, "profiled_ms": prof_ms, "marked_ms": total,
                       "marks_name_start_ms_dur_ms": marks}), flush=True)
 
