@@ -17,6 +17,9 @@
  *                                      into out [len(lists), hi - lo, n] on background threads that
  *                                      need no GIL, so the caller's thread runs Python meanwhile
  *   ints_to_bytes_join(handle)      -> -1, or the first bad flat index (list u, item i: u (hi-lo) + i)
+ *   convert_and_fill(lists, lo, hi, n, out[, list, offset, buf])
+ *                                   -> ints_to_bytes_start + join and f64_into_list in one call that
+ *                                      holds the GIL: the readers need no pins (see there)
  *   none_list(n)                    -> [None] * n (the output list that f64_into_list fills)
  *   f64_into_list(list, offset, buf) -> list[offset:offset + len(buf)] = floats of the float64 buffer
  *
@@ -534,6 +537,130 @@ static PyObject* ints_to_bytes_join(PyObject* self, PyObject* args) {
     return PyLong_FromSsize_t(bad);
 }
 
+/* The researcher aggregate's host step, one call per stripe, with the GIL held throughout: worker threads
+ * convert items [lo, hi) of every party's ciphertext list into `out` [P, hi - lo, nb] while this thread
+ * writes the previous stripe's float64 values into the output list (or, with no floats, waits).  As the
+ * GIL is never released, no Python code runs until the call returns: no list can change and no int be
+ * freed under the readers, so nothing is pinned (the pinning background conversion pays a reference per
+ * item, taken and dropped on this thread: ~10 ns each, a third of the conversion's own cost).  The
+ * readers touch only the ints' digits and `out`; this thread alone allocates.  Returns -1 or the first
+ * bad flat index (u (hi - lo) + i) of the conversion, as ints_to_bytes_join. */
+typedef struct {
+    PyObject*** rows; /* each party's ob_item + lo */
+    Py_ssize_t m, lo, hi, nb, bad;
+    unsigned char* dst;
+} heldconv_job;
+
+#if FBM_DIGITS_FAST
+static void* heldconv_range(void* arg) {
+    heldconv_job* j = (heldconv_job*)arg;
+    j->bad = -1;
+    for (Py_ssize_t f = j->lo; f < j->hi; ++f) {
+        PyObject* v = j->rows[f / j->m][f % j->m];
+        if (!PyLong_Check(v) || long_to_words((PyLongObject*)v, j->dst + f * j->nb, j->nb) < 0) {
+            j->bad = f;
+            break;
+        }
+    }
+    return NULL;
+}
+#endif
+
+static PyObject* convert_and_fill(PyObject* self, PyObject* args) {
+    PyObject *lists, *out, *lst = Py_None;
+    Py_ssize_t lo, hi, nb, off = 0;
+    Py_buffer fview = {0};
+    int have_floats = 0;
+    if (!PyArg_ParseTuple(args, "O!nnnO|Onz*", &PyList_Type, &lists, &lo, &hi, &nb, &out, &lst, &off, &fview))
+        return NULL;
+    have_floats = lst != Py_None && fview.buf != NULL;
+    const Py_ssize_t P = PyList_GET_SIZE(lists), m = hi - lo;
+    Py_ssize_t k = 0;
+    PyObject** fitems = NULL;
+    const double* fsrc = NULL;
+    Py_buffer oview;
+#define CAF_FAIL(exc, msg)                       \
+    do {                                         \
+        if (fview.buf) PyBuffer_Release(&fview); \
+        PyErr_SetString(exc, msg);               \
+        return NULL;                             \
+    } while (0)
+    if (nb <= 0 || nb % 4 || lo < 0 || m < 0) CAF_FAIL(PyExc_ValueError, "bad range or width (a positive multiple of 4 bytes)");
+    for (Py_ssize_t u = 0; u < P; ++u) {
+        PyObject* l = PyList_GET_ITEM(lists, u);
+        if (!PyList_Check(l) || PyList_GET_SIZE(l) < hi) CAF_FAIL(PyExc_ValueError, "every item must be a list holding the range");
+    }
+    if (have_floats) {
+        if (!PyList_Check(lst)) CAF_FAIL(PyExc_TypeError, "the float list must be a list");
+        k = fview.len / (Py_ssize_t)sizeof(double);
+        if (fview.len % (Py_ssize_t)sizeof(double) || off < 0 || off + k > PyList_GET_SIZE(lst))
+            CAF_FAIL(PyExc_ValueError, "float64 buffer does not fit the list at that offset");
+        fitems = ((PyListObject*)lst)->ob_item + off;
+        for (Py_ssize_t i = 0; i < k; ++i)
+            if (fitems[i] != Py_None) CAF_FAIL(PyExc_ValueError, "f64_into_list fills slots that hold None only");
+        fsrc = (const double*)fview.buf;
+    }
+#undef CAF_FAIL
+    if (get_out(out, &oview, P * m * nb) < 0) {
+        if (fview.buf) PyBuffer_Release(&fview);
+        return NULL;
+    }
+    if (((uintptr_t)oview.buf & 3) != 0) {
+        PyBuffer_Release(&oview);
+        if (fview.buf) PyBuffer_Release(&fview);
+        PyErr_SetString(PyExc_ValueError, "output buffer must be 4-byte aligned");
+        return NULL;
+    }
+    PyObject*** rows = (PyObject***)PyMem_Malloc((size_t)(P > 0 ? P : 1) * sizeof(PyObject**));
+    if (!rows) {
+        PyBuffer_Release(&oview);
+        if (fview.buf) PyBuffer_Release(&fview);
+        return PyErr_NoMemory();
+    }
+    for (Py_ssize_t u = 0; u < P; ++u) rows[u] = ((PyListObject*)PyList_GET_ITEM(lists, u))->ob_item + lo;
+    const Py_ssize_t n = P * m;
+    Py_ssize_t bad = -1;
+#if FBM_DIGITS_FAST
+    int nt = n >= 1024 ? conv_threads(n) : 1;
+    heldconv_job jobs[64];
+    pthread_t tid[64];
+    int started[64] = {0};
+    for (int t = 0; t < nt; ++t) {
+        jobs[t] = (heldconv_job){rows, m > 0 ? m : 1, n * t / nt, n * (t + 1) / nt, nb, -1, (unsigned char*)oview.buf};
+        started[t] = pthread_create(&tid[t], NULL, heldconv_range, &jobs[t]) == 0;
+    }
+    for (Py_ssize_t i = 0; i < k; ++i) { /* the previous stripe's floats, beside the readers */
+        PyObject* v = PyFloat_FromDouble(fsrc[i]);
+        if (!v) break; /* the exception is set: finish the readers first */
+        fitems[i] = v;
+        Py_DECREF(Py_None);
+    }
+    for (int t = 0; t < nt; ++t) {
+        if (started[t])
+            pthread_join(tid[t], NULL);
+        else
+            heldconv_range(&jobs[t]); /* thread creation failed: its range here */
+    }
+    for (int t = 0; t < nt && bad < 0; ++t) bad = jobs[t].bad;
+#else /* the byte API: on this thread, floats first */
+    for (Py_ssize_t i = 0; i < k; ++i) {
+        PyObject* v = PyFloat_FromDouble(fsrc[i]);
+        if (!v) break;
+        fitems[i] = v;
+        Py_DECREF(Py_None);
+    }
+    for (Py_ssize_t f = 0; f < n && bad < 0 && !PyErr_Occurred(); ++f) {
+        PyObject* v = rows[f / m][f % m];
+        if (!PyLong_Check(v) || long_to_bytes_api(v, (unsigned char*)oview.buf + f * nb, nb) < 0) bad = f;
+    }
+#endif
+    PyMem_Free(rows);
+    PyBuffer_Release(&oview);
+    if (fview.buf) PyBuffer_Release(&fview);
+    if (PyErr_Occurred()) return NULL;
+    return PyLong_FromSsize_t(bad);
+}
+
 /* [None] * n, for f64_into_list to fill. */
 static PyObject* none_list(PyObject* self, PyObject* args) {
     Py_ssize_t n;
@@ -595,6 +722,8 @@ static PyMethodDef methods[] = {
     {"ints_to_bytes_start", ints_to_bytes_start, METH_VARARGS, "lists, lo, hi, n, out -> background conversion handle"},
     {"ints_to_bytes_join", ints_to_bytes_join, METH_VARARGS, "handle -> -1 or first bad flat index"},
     {"none_list", none_list, METH_VARARGS, "n -> [None] * n"},
+    {"convert_and_fill", convert_and_fill, METH_VARARGS,
+     "lists, lo, hi, n, out[, float list, offset, float64 buffer] -> -1 or first bad flat index (GIL held)"},
     {"f64_into_list", f64_into_list, METH_VARARGS, "list, offset, float64 buffer -> None (fills the list)"},
     {NULL, NULL, 0, NULL},
 };

@@ -107,12 +107,6 @@ def _fine_stripes(stripes, factors):
     return out_s, out_f
 
 
-def _stripe_floats_into(res: List[float], off: int, out_h: torch.Tensor, ev) -> None:
-    """One aggregate stripe's Python floats into res[off:], once its D2H (recorded as `ev`) has landed."""
-    ev.synchronize()
-    D.f64_into_list(res, off, out_h.numpy())
-
-
 class SecaggCrypter:
     """Joye-Libert secure aggregation (encrypt on nodes, aggregate on the researcher)."""
 
@@ -377,10 +371,10 @@ class SecaggCrypter:
         """The list API's aggregate over ct_offset stripes (one when the vector is small).  Per stripe: the
         parties' ints -> pinned limbs -> H2D on a copy stream, the combine with that stripe's factor, the
         float64 D2H in stream order, then the next stripe's factor.  Three things overlap: the next
-        stripe's ints convert on background threads (D.ints_to_limbs_async, no GIL), this thread writes
-        the stripe's floats into the output list (D.f64_into_list, one pass, no intermediate list: the
-        10M-element float list is the call's largest host cost), and the GPU runs the next stripe's
-        factor.  Stripe outputs: elements [c0 cr, c1 cr) capped by
+        stripe's ints convert on host threads while this thread writes the stripe's floats into the
+        output list (one C call holding the GIL, D.convert_stripe: one pass, no intermediate list, no
+        pins -- the 10M-element float list is the call's largest host cost), and the GPU runs the next
+        stripe's factor.  Stripe outputs: elements [c0 cr, c1 cr) capped by
         num_expected_params, as the unsplit decode (_jls.py:146-167); a stripe past it still runs its
         checks (the unsplit call's errors)."""
         _, cr = D.jl_slot(target_range or SAParameters.TARGET_RANGE, len(params))
@@ -395,18 +389,17 @@ class SecaggCrypter:
             limbs = staged.numpy().view(np.uint32)
             if packed is not None:
                 limbs[:] = packed[:, c0:c1]
-                return staged, None
-            return staged, D.ints_to_limbs_async(params, c0, c1, n2, limbs)
+            return staged, limbs
 
         keep = []
-        nxt = stage(0)  # stripe 0's ints convert while the output list and the copy stream are made
         main = torch.cuda.current_stream(dev)
         copy = torch.cuda.Stream(device=dev)
         res = D.float_list(sum(n_outs))
+        nxt = stage(0)
+        if packed is None:  # stripe 0's ints (on host threads; nothing to overlap them with yet)
+            D.convert_stripe(params, *stripes[0], n2, nxt[1])
         for k, (c0, c1) in enumerate(stripes):
-            staged, conv = nxt
-            if conv is not None:
-                conv.join()
+            staged, _ = nxt
             with torch.cuda.stream(copy):
                 cts = staged.to(dev, non_blocking=True)
             main.wait_stream(copy)
@@ -424,10 +417,14 @@ class SecaggCrypter:
                 n0, n1 = stripes[k + 1]
                 if factors[k + 1] is None:
                     factors[k + 1] = self.decrypt_factor_tensor(current_round, n1 - n0, key, biprime, ct_offset=n0)
-                nxt = stage(k + 1)  # its ints convert in the background ...
-            # ... while this thread writes stripe k's floats as soon as its combine lands (the GPU has
-            # stripe k + 1's factor queued behind it: the factors pace the call, not the host)
-            _stripe_floats_into(res, offs[k], out_h, ev)
+                nxt = stage(k + 1)
+            # this stripe's floats as soon as its combine lands (the GPU has stripe k + 1's factor queued
+            # behind it), and -- in the same C call, on host threads -- stripe k + 1's ints
+            ev.synchronize()
+            if k + 1 < len(stripes) and packed is None:
+                D.convert_stripe(params, *stripes[k + 1], n2, nxt[1], res, offs[k], out_h.numpy())
+            else:
+                D.f64_into_list(res, offs[k], out_h.numpy())
         return res
 
     @staticmethod

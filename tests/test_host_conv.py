@@ -275,3 +275,46 @@ def test_conv_contract_float_list(conv):
     with pytest.raises(ValueError):
         conv.none_list(-1)
     assert conv.none_list(0) == []
+
+
+def test_conv_contract_convert_and_fill(conv):
+    """The aggregate's per-stripe host call: items [lo, hi) of every party's list -> out [P, hi - lo, n] (host
+    threads, GIL held) while the previous stripe's floats fill the output list; -1 or the first bad flat index."""
+    rng = random.Random(26)
+    lists = [[rng.getrandbits(2048) for _ in range(3000)] for _ in range(3)]
+    lo, hi = 300, 2700
+    out = np.empty((3, hi - lo, 64), np.uint32)
+    ref = np.empty_like(out)
+    for u in range(3):
+        assert conv.ints_to_bytes(lists[u][lo:hi], 256, ref[u]) == -1
+    assert conv.convert_and_fill(lists, lo, hi, 256, out) == -1
+    assert out.tobytes() == ref.tobytes()
+    res = conv.none_list(10)
+    vals = np.array([1.5, -2.0, float("inf")], np.float64)
+    out[:] = 0
+    assert conv.convert_and_fill(lists, lo, hi, 256, out, res, 4, vals) == -1
+    assert out.tobytes() == ref.tobytes() and res[4:7] == [1.5, -2.0, float("inf")] and res[7] is None
+    bad = [list(v) for v in lists]
+    bad[2][lo + 9] = -1
+    bad[1][lo + 3] = "x"
+    assert conv.convert_and_fill(bad, lo, hi, 256, out) == (hi - lo) + 3
+    with pytest.raises(ValueError):
+        conv.convert_and_fill(lists, lo, hi, 256, out, res, 4, vals)  # those slots are filled already
+    for args in ((lists, 0, 3001, 256, np.empty((3, 3001, 64), np.uint32)),
+                 (lists, 0, 10, 256, np.empty((3, 11, 64), np.uint32)),
+                 (lists, 0, 10, 256, np.empty((3, 10, 64), np.uint32), res, 9, vals)):  # floats past the end
+        with pytest.raises(ValueError):
+            conv.convert_and_fill(*args)
+
+
+def test_convert_stripe_reduces_out_of_range_and_fills():
+    n2 = (2**1023 + 1155) ** 2
+    rng = random.Random(27)
+    lists = [[rng.getrandbits(2040) for _ in range(50)] for _ in range(3)]
+    lists[1][12] = -7
+    lists[2][30] = 2**2050 + 3
+    out = np.empty((3, 30, 64), np.uint32)
+    res = D.float_list(5)
+    D.convert_stripe(lists, 5, 35, n2, out, res, 1, np.array([0.25, 0.5]))
+    assert [D.limbs_to_ints(out[u]) for u in range(3)] == [[v % n2 for v in lst[5:35]] for lst in lists]
+    assert res == [None, 0.25, 0.5, None, None]

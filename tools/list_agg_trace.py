@@ -75,12 +75,9 @@ def main():
             return r
         return wrapped
 
-    A = D.ints_to_limbs_async
-    orig = (SC._stripe_floats_into, A.__init__, A.join, jc.decrypt_factor_tensor, jc.aggregate_tensor,
-            SC._check_int_lists)
-    SC._stripe_floats_into = mark("floats", SC._stripe_floats_into)
-    A.__init__ = mark("conv_start", A.__init__)
-    A.join = mark("conv_join", A.join)
+    orig = (D.f64_into_list, D.convert_stripe, jc.decrypt_factor_tensor, jc.aggregate_tensor, SC._check_int_lists)
+    D.f64_into_list = mark("floats", D.f64_into_list)
+    D.convert_stripe = mark("convert(+floats)", D.convert_stripe)
     jc.decrypt_factor_tensor = mark("factor_issue", jc.decrypt_factor_tensor)
     jc.aggregate_tensor = mark("combine_issue", jc.aggregate_tensor)
     SC._check_int_lists = mark("check_int_lists", SC._check_int_lists)
@@ -91,8 +88,7 @@ def main():
     out = jc.aggregate(tau, P, lists, sk0, W.BIPRIME0, tw, num_expected_params=n)
     total = 1000 * (time.perf_counter() - t_start[0])
     del out
-    (SC._stripe_floats_into, A.__init__, A.join, jc.decrypt_factor_tensor, jc.aggregate_tensor,
-     SC._check_int_lists) = orig
+    D.f64_into_list, D.convert_stripe, jc.decrypt_factor_tensor, jc.aggregate_tensor, SC._check_int_lists = orig
     print(json.dumps({"elements": n, "parties": P, "prepared": args.prepared,
                       "fine_stripe_ct": os.environ.get("FBM_FINE_STRIPE_CT"),
                       "stripes": D.list_encrypt_stripes(len(lists[0]), dev),
