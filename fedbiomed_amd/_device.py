@@ -331,10 +331,12 @@ class _PyConvFallback:
 
     @staticmethod
     def convert_and_fill(lists: list, lo: int, hi: int, nb: int, out: np.ndarray, lst=None, off: int = 0,
-                         buf=None) -> int:
-        if buf is not None and lst is not None:
+                         buf=None):
+        made = _PyConvFallback.none_list(lst) if isinstance(lst, int) else None  # (ValueError when negative)
+        if buf is not None and isinstance(lst, list):
             _PyConvFallback.f64_into_list(lst, off, buf)
-        return _PyConvFallback.ints_to_bytes_join(_PyConvFallback.ints_to_bytes_start(lists, lo, hi, nb, out))
+        bad = _PyConvFallback.ints_to_bytes_join(_PyConvFallback.ints_to_bytes_start(lists, lo, hi, nb, out))
+        return (bad, made) if made is not None else bad
 
     @staticmethod
     def none_list(n: int) -> list:
@@ -469,18 +471,20 @@ class ints_to_limbs_async:
 
 
 def convert_stripe(lists: List[list], c0: int, c1: int, modulus: Optional[int], out: np.ndarray,
-                   res: Optional[list] = None, off: int = 0, values: Optional[np.ndarray] = None) -> np.ndarray:
+                   res=None, off: int = 0, values: Optional[np.ndarray] = None):
     """Items [c0, c1) of every party's ciphertext list -> `out` [P, c1 - c0, 64] uint32 limbs on host threads
     while this thread writes `values` (the previous stripe's floats) into res[off:] -- one C call that holds
     the GIL, so the readers need no pins (csrc/fbm_pyconv.c convert_and_fill); then ints_to_limbs' slow path
-    (reduction mod N^2 of out-of-range values) for any party row that has one."""
+    (reduction mod N^2 of out-of-range values) for any party row that has one.  `res` an int: no floats --
+    this thread makes the [None] * res output list meanwhile, and the call returns it (else None)."""
     vals = None if values is None else np.ascontiguousarray(values, dtype=np.float64)
-    bad = _pyconv().convert_and_fill(lists, c0, c1, 256, out, res, off, vals)
+    r = _pyconv().convert_and_fill(lists, c0, c1, 256, out, res, off, vals)
+    bad, made = r if isinstance(r, tuple) else (r, None)
     if bad >= 0:  # rare: values outside [0, 2^2048) from this party row on
         m = c1 - c0
         for u in range(bad // max(m, 1), len(lists)):
             ints_to_limbs(lists[u][c0:c1], modulus, out=out[u])
-    return out
+    return made
 
 
 def float_list(n: int) -> list:

@@ -537,6 +537,17 @@ static PyObject* ints_to_bytes_join(PyObject* self, PyObject* args) {
     return PyLong_FromSsize_t(bad);
 }
 
+static PyObject* make_none_list(Py_ssize_t n) {
+    PyObject* lst = PyList_New(n);
+    if (!lst) return NULL;
+    PyObject** items = ((PyListObject*)lst)->ob_item;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        Py_INCREF(Py_None);
+        items[i] = Py_None;
+    }
+    return lst;
+}
+
 /* The researcher aggregate's host step, one call per stripe, with the GIL held throughout: worker threads
  * convert items [lo, hi) of every party's ciphertext list into `out` [P, hi - lo, nb] while this thread
  * writes the previous stripe's float64 values into the output list (or, with no floats, waits).  As the
@@ -573,7 +584,18 @@ static PyObject* convert_and_fill(PyObject* self, PyObject* args) {
     int have_floats = 0;
     if (!PyArg_ParseTuple(args, "O!nnnO|Onz*", &PyList_Type, &lists, &lo, &hi, &nb, &out, &lst, &off, &fview))
         return NULL;
-    have_floats = lst != Py_None && fview.buf != NULL;
+    /* `lst` an int: no floats yet -- this thread makes the [None] * lst output list beside the readers
+     * instead, and the call returns (bad, list) */
+    Py_ssize_t new_len = -1;
+    if (PyLong_Check(lst)) {
+        new_len = PyLong_AsSsize_t(lst);
+        if (new_len < 0) {
+            if (fview.buf) PyBuffer_Release(&fview);
+            if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "negative length");
+            return NULL;
+        }
+    }
+    have_floats = new_len < 0 && lst != Py_None && fview.buf != NULL;
     const Py_ssize_t P = PyList_GET_SIZE(lists), m = hi - lo;
     Py_ssize_t k = 0;
     PyObject** fitems = NULL;
@@ -620,6 +642,7 @@ static PyObject* convert_and_fill(PyObject* self, PyObject* args) {
     for (Py_ssize_t u = 0; u < P; ++u) rows[u] = ((PyListObject*)PyList_GET_ITEM(lists, u))->ob_item + lo;
     const Py_ssize_t n = P * m;
     Py_ssize_t bad = -1;
+    PyObject* made = NULL;
 #if FBM_DIGITS_FAST
     int nt = n >= 1024 ? conv_threads(n) : 1;
     heldconv_job jobs[64];
@@ -635,6 +658,7 @@ static PyObject* convert_and_fill(PyObject* self, PyObject* args) {
         fitems[i] = v;
         Py_DECREF(Py_None);
     }
+    if (new_len >= 0) made = make_none_list(new_len); /* (or the output list, beside them) */
     for (int t = 0; t < nt; ++t) {
         if (started[t])
             pthread_join(tid[t], NULL);
@@ -653,11 +677,19 @@ static PyObject* convert_and_fill(PyObject* self, PyObject* args) {
         PyObject* v = rows[f / m][f % m];
         if (!PyLong_Check(v) || long_to_bytes_api(v, (unsigned char*)oview.buf + f * nb, nb) < 0) bad = f;
     }
+    if (new_len >= 0 && !PyErr_Occurred()) made = make_none_list(new_len);
 #endif
     PyMem_Free(rows);
     PyBuffer_Release(&oview);
     if (fview.buf) PyBuffer_Release(&fview);
-    if (PyErr_Occurred()) return NULL;
+    if (PyErr_Occurred()) {
+        Py_XDECREF(made);
+        return NULL;
+    }
+    if (new_len >= 0) {
+        PyObject* r = Py_BuildValue("(nN)", bad, made);
+        return r;
+    }
     return PyLong_FromSsize_t(bad);
 }
 
@@ -669,14 +701,7 @@ static PyObject* none_list(PyObject* self, PyObject* args) {
         PyErr_SetString(PyExc_ValueError, "negative length");
         return NULL;
     }
-    PyObject* lst = PyList_New(n);
-    if (!lst) return NULL;
-    PyObject** items = ((PyListObject*)lst)->ob_item;
-    for (Py_ssize_t i = 0; i < n; ++i) {
-        Py_INCREF(Py_None);
-        items[i] = Py_None;
-    }
-    return lst;
+    return make_none_list(n);
 }
 
 /* list[offset:offset + k] = the k float64 values of buf, as float objects made in place (one pass:
@@ -723,7 +748,8 @@ static PyMethodDef methods[] = {
     {"ints_to_bytes_join", ints_to_bytes_join, METH_VARARGS, "handle -> -1 or first bad flat index"},
     {"none_list", none_list, METH_VARARGS, "n -> [None] * n"},
     {"convert_and_fill", convert_and_fill, METH_VARARGS,
-     "lists, lo, hi, n, out[, float list, offset, float64 buffer] -> -1 or first bad flat index (GIL held)"},
+     "lists, lo, hi, n, out[, float list, offset, float64 buffer] -> -1 or first bad flat index (GIL held); "
+     "with an int for the list: (bad, [None] * that int)"},
     {"f64_into_list", f64_into_list, METH_VARARGS, "list, offset, float64 buffer -> None (fills the list)"},
     {NULL, NULL, 0, NULL},
 };

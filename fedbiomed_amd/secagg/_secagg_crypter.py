@@ -370,11 +370,11 @@ class SecaggCrypter:
                            num_expected_params, target_range, n2, n_ct, stripes, factors, dev) -> List[float]:
         """The list API's aggregate over ct_offset stripes (one when the vector is small).  Per stripe: the
         parties' ints -> pinned limbs -> H2D on a copy stream, the combine with that stripe's factor, the
-        float64 D2H in stream order, then the next stripe's factor.  Three things overlap: the next
-        stripe's ints convert on host threads while this thread writes the stripe's floats into the
-        output list (one C call holding the GIL, D.convert_stripe: one pass, no intermediate list, no
-        pins -- the 10M-element float list is the call's largest host cost), and the GPU runs the next
-        stripe's factor.  Stripe outputs: elements [c0 cr, c1 cr) capped by
+        float64 D2H in stream order, then the next stripe's factor.  Three things overlap: a later
+        stripe's ints convert on host threads while this thread writes a stripe's floats into the output
+        list (one C call holding the GIL, D.convert_stripe: one pass, no intermediate list, no pins --
+        the 10M-element float list is the call's largest host cost), and the GPU runs the stripe between
+        them and the next factor.  Stripe outputs: elements [c0 cr, c1 cr) capped by
         num_expected_params, as the unsplit decode (_jls.py:146-167); a stripe past it still runs its
         checks (the unsplit call's errors)."""
         _, cr = D.jl_slot(target_range or SAParameters.TARGET_RANGE, len(params))
@@ -394,18 +394,17 @@ class SecaggCrypter:
         keep = []
         main = torch.cuda.current_stream(dev)
         copy = torch.cuda.Stream(device=dev)
-        res = D.float_list(sum(n_outs))
-        nxt = stage(0)
-        if packed is None:  # stripe 0's ints (on host threads; nothing to overlap them with yet)
-            D.convert_stripe(params, *stripes[0], n2, nxt[1])
-        for k, (c0, c1) in enumerate(stripes):
-            staged, _ = nxt
+        S = len(stripes)
+
+        def issue(k):  # stripe k's H2D -> combine -> D2H, then stripe k + 1's factor behind the combine
+            c0, c1 = stripes[k]
+            staged = bufs[k][0]
             with torch.cuda.stream(copy):
                 cts = staged.to(dev, non_blocking=True)
             main.wait_stream(copy)
             cts.record_stream(main)
             keep.append(staged)
-            if factors[k] is None and len(stripes) > 1:
+            if factors[k] is None and S > 1:
                 factors[k] = self.decrypt_factor_tensor(current_round, c1 - c0, key, biprime, ct_offset=c0)
             out = self.aggregate_tensor(current_round, cts, key, biprime, total_sample_size, clipping_range,
                                         n_outs[k], target_range, ct_offset=c0, decrypt_factor=factors[k])
@@ -413,16 +412,35 @@ class SecaggCrypter:
             out_h.copy_(out, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(main)
-            if k + 1 < len(stripes):  # the next stripe's factor right behind this stripe's combine
+            if k + 1 < S and factors[k + 1] is None:
                 n0, n1 = stripes[k + 1]
-                if factors[k + 1] is None:
-                    factors[k + 1] = self.decrypt_factor_tensor(current_round, n1 - n0, key, biprime, ct_offset=n0)
-                nxt = stage(k + 1)
-            # this stripe's floats as soon as its combine lands (the GPU has stripe k + 1's factor queued
-            # behind it), and -- in the same C call, on host threads -- stripe k + 1's ints
+                factors[k + 1] = self.decrypt_factor_tensor(current_round, n1 - n0, key, biprime, ct_offset=n0)
+            return out_h, ev
+
+        # Two stripes converted ahead: stripe k's floats are written (this thread) while stripe k + 2's ints
+        # convert (host threads), in one GIL-held C call, and stripe k + 1 is on the GPU meanwhile (its H2D,
+        # combine and D2H then never wait for the host).  Stripe 0's conversion makes the output list beside
+        # it; stripe 1's runs while stripe 0 crosses PCIe.
+        bufs = [None] * S
+        bufs[0] = stage(0)
+        res = (D.convert_stripe(params, *stripes[0], n2, bufs[0][1], sum(n_outs)) if packed is None
+               else D.float_list(sum(n_outs)))
+        pend = {0: issue(0)}
+        if S > 1:
+            bufs[1] = stage(1)
+            if packed is None:
+                D.convert_stripe(params, *stripes[1], n2, bufs[1][1])
+            pend[1] = issue(1)
+        for k in range(S):
+            out_h, ev = pend.pop(k)
             ev.synchronize()
-            if k + 1 < len(stripes) and packed is None:
-                D.convert_stripe(params, *stripes[k + 1], n2, nxt[1], res, offs[k], out_h.numpy())
+            if k + 2 < S:
+                bufs[k + 2] = stage(k + 2)
+                if packed is None:
+                    D.convert_stripe(params, *stripes[k + 2], n2, bufs[k + 2][1], res, offs[k], out_h.numpy())
+                else:
+                    D.f64_into_list(res, offs[k], out_h.numpy())
+                pend[k + 2] = issue(k + 2)
             else:
                 D.f64_into_list(res, offs[k], out_h.numpy())
         return res

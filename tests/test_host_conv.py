@@ -294,10 +294,15 @@ def test_conv_contract_convert_and_fill(conv):
     out[:] = 0
     assert conv.convert_and_fill(lists, lo, hi, 256, out, res, 4, vals) == -1
     assert out.tobytes() == ref.tobytes() and res[4:7] == [1.5, -2.0, float("inf")] and res[7] is None
+    out[:] = 0
+    b, made = conv.convert_and_fill(lists, lo, hi, 256, out, 7)  # an int: the output list made beside
+    assert b == -1 and made == [None] * 7 and out.tobytes() == ref.tobytes()
     bad = [list(v) for v in lists]
     bad[2][lo + 9] = -1
     bad[1][lo + 3] = "x"
     assert conv.convert_and_fill(bad, lo, hi, 256, out) == (hi - lo) + 3
+    with pytest.raises(ValueError):
+        conv.convert_and_fill(lists, lo, hi, 256, out, -1)
     with pytest.raises(ValueError):
         conv.convert_and_fill(lists, lo, hi, 256, out, res, 4, vals)  # those slots are filled already
     for args in ((lists, 0, 3001, 256, np.empty((3, 3001, 64), np.uint32)),
