@@ -86,27 +86,6 @@ def _prep_tag(current_round, num_nodes, key, biprime, target_range) -> Optional[
     return h.digest()
 
 
-# With its factors prepared, the list aggregate no longer waits on the GPU: the host work (ints in,
-# 10M floats out) sets its time, and finer stripes start the float list sooner.  Ciphertexts per fine
-# stripe (a prepared stripe's factor rows are sliced, contiguous).
-FINE_STRIPE_CT = 32768
-
-
-def _fine_stripes(stripes, factors):
-    """prepare_aggregate's stripes (one-lane rounds: the factors' efficient launches) cut into stripes of
-    at most FINE_STRIPE_CT ciphertexts, with their factor rows (None stays None)."""
-    import os
-
-    step = max(1, int(os.environ.get("FBM_FINE_STRIPE_CT", FINE_STRIPE_CT)))  # (tests shrink it)
-    out_s, out_f = [], []
-    for (c0, c1), f in zip(stripes, factors):
-        for a in range(c0, c1, step):
-            b = min(c1, a + step)
-            out_s.append((a, b))
-            out_f.append(None if f is None else f[a - c0:b - c0])
-    return out_s, out_f
-
-
 class SecaggCrypter:
     """Joye-Libert secure aggregation (encrypt on nodes, aggregate on the researcher)."""
 
@@ -274,9 +253,8 @@ class SecaggCrypter:
             # the aggregate's pinned staging buffers, allocated now and handed back to torch's caching host
             # allocator, which gives them to the aggregate: page-locking ~1 GB is the first call's largest
             # extra cost (315-322 ms against 172 ms warm at 10M x 8)
-            fine, _ = _fine_stripes(stripes, [None] * len(stripes))
-            warm = [D.host_empty((num_nodes, c1 - c0, 64), torch.int32) for c0, c1 in fine]
-            warm += [D.host_empty(((c1 - c0) * cr,), torch.float64) for c0, c1 in fine]
+            warm = [D.host_empty((num_nodes, c1 - c0, 64), torch.int32) for c0, c1 in stripes]
+            warm += [D.host_empty(((c1 - c0) * cr,), torch.float64) for c0, c1 in stripes]
             del warm
         except Exception:  # noqa: BLE001 -- aggregate raises whatever it is, in the reference's order
             return False
@@ -335,7 +313,7 @@ class SecaggCrypter:
                     prep = self._take_prepared(current_round, num_nodes, key, biprime, target_range, n_ct0,
                                                D.device())
                     if prep is not None:  # prepare_aggregate's factors: every stripe's, issued ahead
-                        stripes, factors = _fine_stripes(*prep)
+                        stripes, factors = prep[0], list(prep[1])
                     else:
                         stripes = D.list_encrypt_stripes(n_ct0, D.device())
                         factors = [None] * len(stripes)

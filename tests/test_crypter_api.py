@@ -246,10 +246,6 @@ def test_prepare_aggregate_factor_ahead(monkeypatch):
         assert jc._prepared is not None
         assert jc.aggregate(tau, P, cl, sk0, W.BIPRIME0, tw, num_expected_params=n) == ref, rnd
         assert jc._prepared is None  # spent
-        monkeypatch.setenv("FBM_FINE_STRIPE_CT", "77")  # the prepared stripes cut finer, factor rows sliced
-        assert jc.prepare_aggregate(tau, P, sk0, W.BIPRIME0, n) is True
-        assert jc.aggregate(tau, P, cl, sk0, W.BIPRIME0, tw, num_expected_params=n) == ref, rnd
-        monkeypatch.delenv("FBM_FINE_STRIPE_CT")
         assert jc.aggregate(tau, P, cl, sk0, W.BIPRIME0, tw, num_expected_params=n) == ref
         # another round's preparation is dropped by this round's call
         assert jc.prepare_aggregate(tau + 1, P, sk0, W.BIPRIME0, n) is True

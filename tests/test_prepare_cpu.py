@@ -28,21 +28,6 @@ def test_prep_tag_keeps_no_key_and_separates_arguments():
     assert _prep_tag(3.0, 4, 5, 97, None) is None and _prep_tag(3, 4, 5, "97", None) is None
 
 
-def test_fine_stripes_tile_and_slice():
-    from fedbiomed_amd.secagg._secagg_crypter import FINE_STRIPE_CT, _fine_stripes
-
-    st = [(0, 131072), (131072, 262144), (262144, 333334)]
-    f = [torch.arange(c1 - c0).view(-1, 1) for c0, c1 in st]
-    fs, ff = _fine_stripes(st, f)
-    assert fs[0] == (0, FINE_STRIPE_CT) and fs[-1][1] == 333334
-    assert all(a1 == b0 for (_, a1), (b0, _) in zip(fs, fs[1:]))  # contiguous tiling
-    assert all(0 < c1 - c0 <= FINE_STRIPE_CT for c0, c1 in fs)
-    for (c0, c1), t in zip(fs, ff):  # each slice is its stripe's rows of the owning factor
-        owner = max(k for k, (s0, _) in enumerate(st) if s0 <= c0)
-        assert t.shape[0] == c1 - c0 and int(t[0, 0]) == c0 - st[owner][0] and t.is_contiguous()
-    assert _fine_stripes([(0, 5)], [None]) == ([(0, 5)], [None])
-
-
 class _Ev:
     def __init__(self):
         self.waited = False

@@ -90,7 +90,6 @@ def main():
     del out
     D.f64_into_list, D.convert_stripe, jc.decrypt_factor_tensor, jc.aggregate_tensor, SC._check_int_lists = orig
     print(json.dumps({"elements": n, "parties": P, "prepared": args.prepared,
-                      "fine_stripe_ct": os.environ.get("FBM_FINE_STRIPE_CT"),
                       "stripes": D.list_encrypt_stripes(len(lists[0]), dev),
                       "warm_ms": warm, "profiled_ms": prof_ms, "marked_ms": total,
                       "marks_name_start_ms_dur_ms": marks}), flush=True)
