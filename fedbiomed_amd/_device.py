@@ -307,8 +307,9 @@ class _PyConvFallback:
         return [int.from_bytes(b[i:i + nb], "little") for i in range(0, len(b), nb)]
 
     @staticmethod
-    def ints_to_bytes_start(lists: list, lo: int, hi: int, nb: int, out: np.ndarray):
-        """Converts at once (no background threads here); join() returns the answer."""
+    def convert_and_fill(lists: list, lo: int, hi: int, nb: int, out: np.ndarray, lst=None, off: int = 0,
+                         buf=None):
+        made = _PyConvFallback.none_list(lst) if isinstance(lst, int) else None  # (ValueError when negative)
         if nb <= 0 or nb % 4 or lo < 0 or hi < lo:
             raise ValueError("bad range or width (a positive multiple of 4 bytes)")
         if not all(isinstance(v, list) and len(v) >= hi for v in lists):
@@ -316,26 +317,15 @@ class _PyConvFallback:
         m = hi - lo
         if out.nbytes != len(lists) * m * nb:
             raise ValueError(f"output buffer holds {out.nbytes} bytes, {len(lists) * m * nb} needed")
-        rows = out.reshape(len(lists), m * nb // out.itemsize) if lists else out
-        for u, v in enumerate(lists):
-            bad = _PyConvFallback.ints_to_bytes(v[lo:hi], nb, rows[u])
-            if bad >= 0:
-                return [u * m + bad]
-        return [-1]
-
-    @staticmethod
-    def ints_to_bytes_join(handle) -> int:
-        if not handle:
-            raise ValueError("conversion already joined")
-        return handle.pop()
-
-    @staticmethod
-    def convert_and_fill(lists: list, lo: int, hi: int, nb: int, out: np.ndarray, lst=None, off: int = 0,
-                         buf=None):
-        made = _PyConvFallback.none_list(lst) if isinstance(lst, int) else None  # (ValueError when negative)
         if buf is not None and isinstance(lst, list):
             _PyConvFallback.f64_into_list(lst, off, buf)
-        bad = _PyConvFallback.ints_to_bytes_join(_PyConvFallback.ints_to_bytes_start(lists, lo, hi, nb, out))
+        rows = out.reshape(len(lists), m * nb // out.itemsize) if lists else out
+        bad = -1
+        for u, v in enumerate(lists):
+            b = _PyConvFallback.ints_to_bytes(v[lo:hi], nb, rows[u])
+            if b >= 0:
+                bad = u * m + b
+                break
         return (bad, made) if made is not None else bad
 
     @staticmethod
@@ -449,25 +439,6 @@ def ints_to_limbs(cts: Sequence[int], modulus: Optional[int] = None, out: Option
         rest = _pyconv().ints_to_bytes(cts[bad + 1:], 256, out[bad + 1:])
         bad = -1 if rest < 0 else bad + 1 + rest
     return out
-
-
-class ints_to_limbs_async:
-    """Items [c0, c1) of every party's ciphertext list -> `out` [P, c1 - c0, 64] uint32 limbs on
-    background host threads (csrc/fbm_pyconv.c ints_to_bytes_start: no GIL needed, so the caller
-    builds the previous stripe's floats meanwhile); join() waits, then takes ints_to_limbs' slow
-    path (reduction mod N^2 of out-of-range values) for any party row that has one."""
-
-    def __init__(self, lists: List[list], c0: int, c1: int, modulus: Optional[int], out: np.ndarray):
-        self.lists, self.c0, self.c1, self.modulus, self.out = lists, c0, c1, modulus, out
-        self.handle = _pyconv().ints_to_bytes_start(lists, c0, c1, 256, out)
-
-    def join(self) -> np.ndarray:
-        bad = _pyconv().ints_to_bytes_join(self.handle)
-        if bad >= 0:  # rare: values outside [0, 2^2048) from this party row on
-            m = self.c1 - self.c0
-            for u in range(bad // max(m, 1), len(self.lists)):
-                ints_to_limbs(self.lists[u][self.c0:self.c1], self.modulus, out=self.out[u])
-        return self.out
 
 
 def convert_stripe(lists: List[list], c0: int, c1: int, modulus: Optional[int], out: np.ndarray,

@@ -13,13 +13,11 @@
  *                                      int in [0, 2^(8n)) (the caller then takes its slow
  *                                      path: type error or reduction mod N^2)
  *   bytes_to_ints(buf, n)           -> list of the unsigned little-endian n-byte integers
- *   ints_to_bytes_start(lists, lo, hi, n, out) -> a handle: items [lo, hi) of every list converted
- *                                      into out [len(lists), hi - lo, n] on background threads that
- *                                      need no GIL, so the caller's thread runs Python meanwhile
- *   ints_to_bytes_join(handle)      -> -1, or the first bad flat index (list u, item i: u (hi-lo) + i)
  *   convert_and_fill(lists, lo, hi, n, out[, list, offset, buf])
- *                                   -> ints_to_bytes_start + join and f64_into_list in one call that
- *                                      holds the GIL: the readers need no pins (see there)
+ *                                   -> items [lo, hi) of every list into out [len(lists), hi - lo, n]
+ *                                      on host threads while this one fills the float list, in one call
+ *                                      that holds the GIL: the readers need no pins (see there); -1 or
+ *                                      the first bad flat index (list u, item i: u (hi - lo) + i)
  *   none_list(n)                    -> [None] * n (the output list that f64_into_list fills)
  *   f64_into_list(list, offset, buf) -> list[offset:offset + len(buf)] = floats of the float64 buffer
  *
@@ -397,146 +395,6 @@ static PyObject* all_ints(PyObject* self, PyObject* args) {
     return PyBool_FromLong(ok);
 }
 
-/* The background conversion of the researcher's aggregate: the items of every list's range are
- * pinned (a reference each, under the GIL) into one flat array whose order is out's row order, the
- * output buffer is held (a Py_buffer keeps its exporter alive), and the threads start; the call
- * returns at once.  The threads read only the pinned ints' digits and write only `out`, so Python
- * code (the previous stripe's float list) runs beside them.  join() waits with the GIL released;
- * a handle dropped unjoined joins in its destructor before anything is released. */
-typedef struct {
-    PyObject** items;
-    Py_ssize_t n, nb;
-    Py_buffer view;
-    int nt, joined;
-    pthread_t tid[64];
-    int started[64];
-    conv_job jobs[64];
-} conv_async;
-
-#define CONV_ASYNC_NAME "fbm_pyconv.conv_async"
-
-static void conv_async_wait(conv_async* h) {
-    if (h->joined) return;
-    for (int t = 0; t < h->nt; ++t) {
-        if (h->started[t])
-            pthread_join(h->tid[t], NULL);
-#if FBM_DIGITS_FAST
-        else
-            conv_range(&h->jobs[t]); /* thread creation failed: its range here */
-#endif
-    }
-    h->joined = 1;
-}
-
-static void conv_async_release(conv_async* h) {
-    for (Py_ssize_t i = 0; i < h->n; ++i) Py_DECREF(h->items[i]);
-    PyMem_Free(h->items);
-    h->items = NULL;
-    PyBuffer_Release(&h->view);
-}
-
-static void conv_async_destroy(PyObject* cap) {
-    conv_async* h = (conv_async*)PyCapsule_GetPointer(cap, CONV_ASYNC_NAME);
-    if (!h) return;
-    if (h->items) {
-        Py_BEGIN_ALLOW_THREADS
-        conv_async_wait(h);
-        Py_END_ALLOW_THREADS
-        conv_async_release(h);
-    }
-    PyMem_Free(h);
-}
-
-static PyObject* ints_to_bytes_start(PyObject* self, PyObject* args) {
-    PyObject *lists, *out;
-    Py_ssize_t lo, hi, nb;
-    if (!PyArg_ParseTuple(args, "O!nnnO", &PyList_Type, &lists, &lo, &hi, &nb, &out)) return NULL;
-    const Py_ssize_t P = PyList_GET_SIZE(lists), m = hi - lo;
-    if (nb <= 0 || nb % 4 || lo < 0 || m < 0) {
-        PyErr_SetString(PyExc_ValueError, "bad range or width (a positive multiple of 4 bytes)");
-        return NULL;
-    }
-    for (Py_ssize_t u = 0; u < P; ++u) {
-        PyObject* l = PyList_GET_ITEM(lists, u);
-        if (!PyList_Check(l) || PyList_GET_SIZE(l) < hi) {
-            PyErr_SetString(PyExc_ValueError, "every item must be a list holding the range");
-            return NULL;
-        }
-    }
-    conv_async* h = (conv_async*)PyMem_Calloc(1, sizeof(conv_async));
-    if (!h) return PyErr_NoMemory();
-    h->nb = nb;
-    if (get_out(out, &h->view, P * m * nb) < 0) {
-        PyMem_Free(h);
-        return NULL;
-    }
-    if (((uintptr_t)h->view.buf & 3) != 0) {
-        PyBuffer_Release(&h->view);
-        PyMem_Free(h);
-        PyErr_SetString(PyExc_ValueError, "output buffer must be 4-byte aligned");
-        return NULL;
-    }
-    h->n = P * m;
-    h->items = (PyObject**)PyMem_Malloc((size_t)(h->n > 0 ? h->n : 1) * sizeof(PyObject*));
-    if (!h->items) {
-        PyBuffer_Release(&h->view);
-        PyMem_Free(h);
-        return PyErr_NoMemory();
-    }
-    for (Py_ssize_t u = 0; u < P; ++u) {
-        PyObject** src = ((PyListObject*)PyList_GET_ITEM(lists, u))->ob_item + lo;
-        for (Py_ssize_t i = 0; i < m; ++i) {
-            h->items[u * m + i] = src[i];
-            Py_INCREF(src[i]);
-        }
-    }
-#if FBM_DIGITS_FAST
-    h->nt = h->n >= 1024 ? conv_threads(h->n) : 1;
-    for (int t = 0; t < h->nt; ++t) {
-        h->jobs[t] = (conv_job){h->items, (unsigned char*)h->view.buf, h->n * t / h->nt, h->n * (t + 1) / h->nt, nb, -1};
-        h->started[t] = pthread_create(&h->tid[t], NULL, conv_range, &h->jobs[t]) == 0;
-    }
-#else /* the byte API needs the GIL: convert here, the handle already joined */
-    h->nt = 1;
-    h->jobs[0] = (conv_job){h->items, (unsigned char*)h->view.buf, 0, h->n, nb, -1};
-    for (Py_ssize_t i = 0; i < h->n; ++i) {
-        PyObject* v = h->items[i];
-        if (!PyLong_Check(v) || long_to_bytes_api(v, (unsigned char*)h->view.buf + i * nb, nb) < 0) {
-            h->jobs[0].bad = i;
-            break;
-        }
-    }
-    h->joined = 1;
-#endif
-    PyObject* cap = PyCapsule_New(h, CONV_ASYNC_NAME, conv_async_destroy);
-    if (!cap) { /* the threads run on pinned items: wait for them before giving anything back */
-        Py_BEGIN_ALLOW_THREADS
-        conv_async_wait(h);
-        Py_END_ALLOW_THREADS
-        conv_async_release(h);
-        PyMem_Free(h);
-    }
-    return cap;
-}
-
-static PyObject* ints_to_bytes_join(PyObject* self, PyObject* args) {
-    PyObject* cap;
-    if (!PyArg_ParseTuple(args, "O", &cap)) return NULL;
-    conv_async* h = (conv_async*)PyCapsule_GetPointer(cap, CONV_ASYNC_NAME);
-    if (!h) return NULL;
-    if (!h->items) {
-        PyErr_SetString(PyExc_ValueError, "conversion already joined");
-        return NULL;
-    }
-    Py_BEGIN_ALLOW_THREADS
-    conv_async_wait(h);
-    Py_END_ALLOW_THREADS
-    Py_ssize_t bad = -1;
-    for (int t = 0; t < h->nt && bad < 0; ++t) bad = h->jobs[t].bad;
-    conv_async_release(h);
-    return PyLong_FromSsize_t(bad);
-}
-
 static PyObject* make_none_list(Py_ssize_t n) {
     PyObject* lst = PyList_New(n);
     if (!lst) return NULL;
@@ -552,10 +410,10 @@ static PyObject* make_none_list(Py_ssize_t n) {
  * convert items [lo, hi) of every party's ciphertext list into `out` [P, hi - lo, nb] while this thread
  * writes the previous stripe's float64 values into the output list (or, with no floats, waits).  As the
  * GIL is never released, no Python code runs until the call returns: no list can change and no int be
- * freed under the readers, so nothing is pinned (the pinning background conversion pays a reference per
- * item, taken and dropped on this thread: ~10 ns each, a third of the conversion's own cost).  The
+ * freed under the readers, so nothing is pinned (ints_to_bytes, which releases the GIL, pays a reference
+ * per item, taken and dropped on this thread: ~10 ns each, a third of the conversion's own cost).  The
  * readers touch only the ints' digits and `out`; this thread alone allocates.  Returns -1 or the first
- * bad flat index (u (hi - lo) + i) of the conversion, as ints_to_bytes_join. */
+ * bad flat index (u (hi - lo) + i) of the conversion. */
 typedef struct {
     PyObject*** rows; /* each party's ob_item + lo */
     Py_ssize_t m, lo, hi, nb, bad;
@@ -744,8 +602,6 @@ static PyMethodDef methods[] = {
     {"floats_to_f64", floats_to_f64, METH_VARARGS, "list of floats -> float64 buffer; -1 or first bad index"},
     {"ints_to_bytes", ints_to_bytes, METH_VARARGS, "list of ints -> n-byte LE unsigned; -1 or first bad index"},
     {"bytes_to_ints", bytes_to_ints, METH_VARARGS, "buffer of n-byte LE unsigned values -> list of ints"},
-    {"ints_to_bytes_start", ints_to_bytes_start, METH_VARARGS, "lists, lo, hi, n, out -> background conversion handle"},
-    {"ints_to_bytes_join", ints_to_bytes_join, METH_VARARGS, "handle -> -1 or first bad flat index"},
     {"none_list", none_list, METH_VARARGS, "n -> [None] * n"},
     {"convert_and_fill", convert_and_fill, METH_VARARGS,
      "lists, lo, hi, n, out[, float list, offset, float64 buffer] -> -1 or first bad flat index (GIL held); "

@@ -199,65 +199,6 @@ def test_conv_contract_floats(conv):
         conv.floats_to_f64([1.0], np.empty(2, np.float64))
 
 
-def test_conv_contract_async_ranges(conv):
-    """The researcher aggregate's background conversion: items [lo, hi) of every party's list into
-    out [P, hi - lo, n], the first bad flat index u (hi - lo) + i on join, as per-row ints_to_bytes."""
-    rng = random.Random(23)
-    lists = [[rng.getrandbits(2048) for _ in range(3000)] for _ in range(3)]
-    lo, hi = 700, 2900
-    out = np.empty((3, hi - lo, 64), np.uint32)
-    h = conv.ints_to_bytes_start(lists, lo, hi, 256, out)
-    assert conv.ints_to_bytes_join(h) == -1
-    ref = np.empty_like(out)
-    for u in range(3):
-        assert conv.ints_to_bytes(lists[u][lo:hi], 256, ref[u]) == -1
-    assert out.tobytes() == ref.tobytes()
-    with pytest.raises(ValueError):
-        conv.ints_to_bytes_join(h)  # joined once
-    bad = [list(v) for v in lists]
-    bad[1][lo + 5] = -1
-    bad[2][lo + 1] = 2**2048
-    assert conv.ints_to_bytes_join(conv.ints_to_bytes_start(bad, lo, hi, 256, out)) == (hi - lo) + 5
-    bad[1][lo + 5] = 3
-    bad[0][hi] = "outside the range"  # not converted, not reported
-    assert conv.ints_to_bytes_join(conv.ints_to_bytes_start(bad, lo, hi, 256, out)) == 2 * (hi - lo) + 1
-    empty = np.empty((3, 0, 64), np.uint32)
-    assert conv.ints_to_bytes_join(conv.ints_to_bytes_start(lists, 5, 5, 256, empty)) == -1
-    for args in ((lists, 0, 3001, 256, np.empty((3, 3001, 64), np.uint32)),  # past a list's end
-                 (lists, 0, 10, 256, np.empty((3, 11, 64), np.uint32)),  # buffer size
-                 (lists, 0, 10, 6, np.empty((3, 10, 6), np.uint8)),  # width not a word multiple
-                 ([lists[0], (1, 2)], 0, 1, 256, np.empty((2, 1, 64), np.uint32))):
-        with pytest.raises(ValueError):
-            conv.ints_to_bytes_start(*args)
-
-
-def test_async_handle_dropped_unjoined():
-    """A handle released without join() (an exception between start and join) waits for its
-    threads before it lets go of the items and the buffer."""
-    m = D._pyconv()
-    rng = random.Random(24)
-    lists = [[rng.getrandbits(2048) for _ in range(20000)] for _ in range(2)]
-    for _ in range(5):
-        out = np.empty((2, 20000, 64), np.uint32)
-        h = m.ints_to_bytes_start(lists, 0, 20000, 256, out)
-        del h, out
-    lists2 = [[rng.getrandbits(2048) for _ in range(20000)]]
-    out = np.empty((1, 20000, 64), np.uint32)
-    assert m.ints_to_bytes_join(m.ints_to_bytes_start(lists2, 0, 20000, 256, out)) == -1
-    assert D.limbs_to_ints(out[0]) == lists2[0]
-
-
-def test_ints_to_limbs_async_reduces_out_of_range():
-    n2 = (2**1023 + 1155) ** 2
-    rng = random.Random(25)
-    lists = [[rng.getrandbits(2040) for _ in range(40)] for _ in range(3)]
-    lists[1][12] = -7
-    lists[2][30] = 2**2050 + 3
-    out = np.empty((3, 30, 64), np.uint32)
-    D.ints_to_limbs_async(lists, 5, 35, n2, out).join()
-    assert [D.limbs_to_ints(out[u]) for u in range(3)] == [[v % n2 for v in lst[5:35]] for lst in lists]
-
-
 def test_conv_contract_float_list(conv):
     vals = np.array([0.5, -0.0, float("nan"), float("inf"), 1e-310, -3.75], dtype=np.float64)
     lst = conv.none_list(9)
