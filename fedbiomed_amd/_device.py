@@ -329,6 +329,12 @@ class _PyConvFallback:
         return (bad, made) if made is not None else bad
 
     @staticmethod
+    def float_pool(n: int) -> list:
+        if n < 0:
+            raise ValueError("negative length")
+        return [float(0) for _ in range(n)]
+
+    @staticmethod
     def none_list(n: int) -> list:
         if n < 0:
             raise ValueError("negative length")
@@ -339,8 +345,8 @@ class _PyConvFallback:
         a = np.frombuffer(memoryview(buf).cast("B"), dtype=np.float64)
         if off < 0 or off + len(a) > len(lst):
             raise ValueError("float64 buffer does not fit the list at that offset")
-        if any(v is not None for v in lst[off:off + len(a)]):
-            raise ValueError("f64_into_list fills slots that hold None only")
+        if any(v is not None and type(v) is not float for v in lst[off:off + len(a)]):
+            raise ValueError("f64_into_list fills slots that hold None or floats only")
         lst[off:off + len(a)] = a.tolist()
 
 
@@ -461,6 +467,12 @@ def convert_stripe(lists: List[list], c0: int, c1: int, modulus: Optional[int], 
 def float_list(n: int) -> list:
     """The aggregate's output list, [None] * n, for f64_into_list to fill stripe by stripe."""
     return _pyconv().none_list(n)
+
+
+def float_pool(n: int) -> list:
+    """n fresh 0.0 floats held by the returned list only: an aggregate's output list made ahead
+    (prepare_aggregate); f64_into_list / convert_stripe then write its values in place, no allocation."""
+    return _pyconv().float_pool(n)
 
 
 def f64_into_list(lst: list, off: int, values: np.ndarray) -> None:

@@ -19,6 +19,7 @@
  *                                      that holds the GIL: the readers need no pins (see there); -1 or
  *                                      the first bad flat index (list u, item i: u (hi - lo) + i)
  *   none_list(n)                    -> [None] * n (the output list that f64_into_list fills)
+ *   float_pool(n)                   -> n fresh 0.0 floats: an output list made ahead, filled in place
  *   f64_into_list(list, offset, buf) -> list[offset:offset + len(buf)] = floats of the float64 buffer
  *
  * `out` is any writable C-contiguous buffer (a numpy array) of the exact size.  Host code,
@@ -395,6 +396,35 @@ static PyObject* all_ints(PyObject* self, PyObject* args) {
     return PyBool_FromLong(ok);
 }
 
+/* The output list's slots: None (a none_list) or exact floats (a float_pool).  Writing value d into a
+ * slot: None -> a new float; a float only this list holds (reference count 1, made by float_pool and
+ * never handed out) -> its value overwritten in place, no allocation (the object is not yet visible to
+ * any Python code: the list is returned only once filled); a float someone else also holds -> replaced
+ * by a new one (its release cannot free it, so no destructor runs mid-loop).  Anything else refused. */
+static int check_slots(PyObject* const* items, Py_ssize_t k) {
+    for (Py_ssize_t i = 0; i < k; ++i)
+        if (items[i] != Py_None && !PyFloat_CheckExact(items[i])) {
+            PyErr_SetString(PyExc_ValueError, "f64_into_list fills slots that hold None or floats only");
+            return -1;
+        }
+    return 0;
+}
+
+static int fill_slots(PyObject** items, const double* src, Py_ssize_t k) {
+    for (Py_ssize_t i = 0; i < k; ++i) {
+        PyObject* o = items[i];
+        if (o != Py_None && Py_REFCNT(o) == 1) {
+            ((PyFloatObject*)o)->ob_fval = src[i];
+            continue;
+        }
+        PyObject* v = PyFloat_FromDouble(src[i]);
+        if (!v) return -1;
+        items[i] = v;
+        Py_DECREF(o); /* None, or a float with another holder: never freed here */
+    }
+    return 0;
+}
+
 static PyObject* make_none_list(Py_ssize_t n) {
     PyObject* lst = PyList_New(n);
     if (!lst) return NULL;
@@ -476,8 +506,10 @@ static PyObject* convert_and_fill(PyObject* self, PyObject* args) {
         if (fview.len % (Py_ssize_t)sizeof(double) || off < 0 || off + k > PyList_GET_SIZE(lst))
             CAF_FAIL(PyExc_ValueError, "float64 buffer does not fit the list at that offset");
         fitems = ((PyListObject*)lst)->ob_item + off;
-        for (Py_ssize_t i = 0; i < k; ++i)
-            if (fitems[i] != Py_None) CAF_FAIL(PyExc_ValueError, "f64_into_list fills slots that hold None only");
+        if (check_slots(fitems, k) < 0) {
+            PyBuffer_Release(&fview);
+            return NULL;
+        }
         fsrc = (const double*)fview.buf;
     }
 #undef CAF_FAIL
@@ -510,12 +542,8 @@ static PyObject* convert_and_fill(PyObject* self, PyObject* args) {
         jobs[t] = (heldconv_job){rows, m > 0 ? m : 1, n * t / nt, n * (t + 1) / nt, nb, -1, (unsigned char*)oview.buf};
         started[t] = pthread_create(&tid[t], NULL, heldconv_range, &jobs[t]) == 0;
     }
-    for (Py_ssize_t i = 0; i < k; ++i) { /* the previous stripe's floats, beside the readers */
-        PyObject* v = PyFloat_FromDouble(fsrc[i]);
-        if (!v) break; /* the exception is set: finish the readers first */
-        fitems[i] = v;
-        Py_DECREF(Py_None);
-    }
+    if (k) fill_slots(fitems, fsrc, k); /* the previous stripe's floats, beside the readers (on failure
+                                             the exception is set: finish the readers first) */
     if (new_len >= 0) made = make_none_list(new_len); /* (or the output list, beside them) */
     for (int t = 0; t < nt; ++t) {
         if (started[t])
@@ -525,12 +553,7 @@ static PyObject* convert_and_fill(PyObject* self, PyObject* args) {
     }
     for (int t = 0; t < nt && bad < 0; ++t) bad = jobs[t].bad;
 #else /* the byte API: on this thread, floats first */
-    for (Py_ssize_t i = 0; i < k; ++i) {
-        PyObject* v = PyFloat_FromDouble(fsrc[i]);
-        if (!v) break;
-        fitems[i] = v;
-        Py_DECREF(Py_None);
-    }
+    if (k) fill_slots(fitems, fsrc, k);
     for (Py_ssize_t f = 0; f < n && bad < 0 && !PyErr_Occurred(); ++f) {
         PyObject* v = rows[f / m][f % m];
         if (!PyLong_Check(v) || long_to_bytes_api(v, (unsigned char*)oview.buf + f * nb, nb) < 0) bad = f;
@@ -562,9 +585,34 @@ static PyObject* none_list(PyObject* self, PyObject* args) {
     return make_none_list(n);
 }
 
-/* list[offset:offset + k] = the k float64 values of buf, as float objects made in place (one pass:
- * no intermediate list as ndarray.tolist() + extend would build).  The slots must hold None (a
- * none_list): releasing None runs no destructor, so no Python code can resize the list mid-loop. */
+/* n distinct float objects (0.0), each held by the returned list only: the aggregate's output made
+ * ahead (SecaggCrypter.prepare_aggregate), whose values fill_slots then writes in place. */
+static PyObject* float_pool(PyObject* self, PyObject* args) {
+    Py_ssize_t n;
+    if (!PyArg_ParseTuple(args, "n", &n)) return NULL;
+    if (n < 0) {
+        PyErr_SetString(PyExc_ValueError, "negative length");
+        return NULL;
+    }
+    PyObject* lst = PyList_New(n);
+    if (!lst) return NULL;
+    PyObject** items = ((PyListObject*)lst)->ob_item;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        items[i] = PyFloat_FromDouble(0.0);
+        if (!items[i]) {
+            for (Py_ssize_t j = i; j < n; ++j) { /* the rest None: the list stays well-formed */
+                Py_INCREF(Py_None);
+                items[j] = Py_None;
+            }
+            Py_DECREF(lst);
+            return NULL;
+        }
+    }
+    return lst;
+}
+
+/* list[offset:offset + k] = the k float64 values of buf (one pass: no intermediate list as
+ * ndarray.tolist() + extend would build), slot by slot as fill_slots says. */
 static PyObject* f64_into_list(PyObject* self, PyObject* args) {
     PyObject* lst;
     Py_ssize_t off;
@@ -578,22 +626,9 @@ static PyObject* f64_into_list(PyObject* self, PyObject* args) {
     }
     const double* src = (const double*)view.buf;
     PyObject** items = ((PyListObject*)lst)->ob_item + off;
-    for (Py_ssize_t i = 0; i < k; ++i)
-        if (items[i] != Py_None) {
-            PyBuffer_Release(&view);
-            PyErr_SetString(PyExc_ValueError, "f64_into_list fills slots that hold None only");
-            return NULL;
-        }
-    for (Py_ssize_t i = 0; i < k; ++i) {
-        PyObject* v = PyFloat_FromDouble(src[i]);
-        if (!v) {
-            PyBuffer_Release(&view);
-            return NULL;
-        }
-        items[i] = v;
-        Py_DECREF(Py_None);
-    }
+    const int rc = check_slots(items, k) < 0 ? -1 : fill_slots(items, src, k);
     PyBuffer_Release(&view);
+    if (rc < 0) return NULL;
     Py_RETURN_NONE;
 }
 
@@ -603,6 +638,7 @@ static PyMethodDef methods[] = {
     {"ints_to_bytes", ints_to_bytes, METH_VARARGS, "list of ints -> n-byte LE unsigned; -1 or first bad index"},
     {"bytes_to_ints", bytes_to_ints, METH_VARARGS, "buffer of n-byte LE unsigned values -> list of ints"},
     {"none_list", none_list, METH_VARARGS, "n -> [None] * n"},
+    {"float_pool", float_pool, METH_VARARGS, "n -> n distinct 0.0 floats held by the list only"},
     {"convert_and_fill", convert_and_fill, METH_VARARGS,
      "lists, lo, hi, n, out[, float list, offset, float64 buffer] -> -1 or first bad flat index (GIL held); "
      "with an int for the list: (bad, [None] * that int)"},

@@ -256,10 +256,13 @@ class SecaggCrypter:
             warm = [D.host_empty((num_nodes, c1 - c0, 64), torch.int32) for c0, c1 in stripes]
             warm += [D.host_empty(((c1 - c0) * cr,), torch.float64) for c0, c1 in stripes]
             del warm
+            # and its output list: the float objects made now, their values written in place by the
+            # aggregate (making 10M Python floats is most of its host time, ~100 ms)
+            pool = D.float_pool(max(0, min(num_expected_params, n_ct * cr)))
         except Exception:  # noqa: BLE001 -- aggregate raises whatever it is, in the reference's order
             return False
         self._prepared = {"round": current_round, "tag": _prep_tag(current_round, num_nodes, key, biprime, target_range),
-                          "n_ct": n_ct,
+                          "n_ct": n_ct, "pool": pool,
                           "stripes": stripes, "factors": factors, "event": ev, "checks": checks.pending}
         return True
 
@@ -284,7 +287,7 @@ class SecaggCrypter:
         for f in prep["factors"]:
             f.record_stream(main)
         D.adopt_checks(prep["checks"])
-        return prep["stripes"], prep["factors"]
+        return prep["stripes"], prep["factors"], prep["pool"]
 
     def aggregate(self, current_round: int, num_nodes: int, params: List[List[int]], key: int, biprime: int,
                   total_sample_size: int, clipping_range: Union[int, None] = None, num_expected_params: int = 1,
@@ -306,14 +309,14 @@ class SecaggCrypter:
             # stripe k + 1's factor, so the host builds stripe k's floats while the GPU
             # exponentiates stripe k + 1 (every element depends on its own ciphertext only: the
             # stripes' outputs concatenate to the unsplit call's).
-            stripes, factors = None, []
+            stripes, factors, pool = None, [], None
             if params and isinstance(key, int) and isinstance(biprime, int) and all(isinstance(p, list) for p in params):
                 n_ct0 = min(len(p) for p in params)
                 if n_ct0:
                     prep = self._take_prepared(current_round, num_nodes, key, biprime, target_range, n_ct0,
                                                D.device())
-                    if prep is not None:  # prepare_aggregate's factors: every stripe's, issued ahead
-                        stripes, factors = prep[0], list(prep[1])
+                    if prep is not None:  # prepare_aggregate's factors (every stripe's) and output list
+                        stripes, factors, pool = prep[0], list(prep[1]), prep[2]
                     else:
                         stripes = D.list_encrypt_stripes(n_ct0, D.device())
                         factors = [None] * len(stripes)
@@ -339,13 +342,14 @@ class SecaggCrypter:
             if stripes is None:
                 stripes, factors = [(0, n_ct)], [None]
             res = self._aggregate_stripes(current_round, params, key, biprime, total_sample_size, clipping_range,
-                                          num_expected_params, target_range, n2, n_ct, stripes, factors, dev)
+                                          num_expected_params, target_range, n2, n_ct, stripes, factors, dev, pool)
         logger.info(f"Aggregating {len(params)} parameters from {num_nodes} nodes.")
         logger.debug(f"Aggregation is completed in {round(time.process_time() - start, ndigits=2)} seconds.")
         return res
 
     def _aggregate_stripes(self, current_round, params, key, biprime, total_sample_size, clipping_range,
-                           num_expected_params, target_range, n2, n_ct, stripes, factors, dev) -> List[float]:
+                           num_expected_params, target_range, n2, n_ct, stripes, factors, dev,
+                           pool=None) -> List[float]:
         """The list API's aggregate over ct_offset stripes (one when the vector is small).  Per stripe: the
         parties' ints -> pinned limbs -> H2D on a copy stream, the combine with that stripe's factor, the
         float64 D2H in stream order, then the next stripe's factor.  Three things overlap: a later
@@ -354,7 +358,8 @@ class SecaggCrypter:
         the 10M-element float list is the call's largest host cost), and the GPU runs the stripe between
         them and the next factor.  Stripe outputs: elements [c0 cr, c1 cr) capped by
         num_expected_params, as the unsplit decode (_jls.py:146-167); a stripe past it still runs its
-        checks (the unsplit call's errors)."""
+        checks (the unsplit call's errors).  `pool`: prepare_aggregate's output list (its floats made
+        ahead, written in place here) when it has this call's length."""
         _, cr = D.jl_slot(target_range or SAParameters.TARGET_RANGE, len(params))
         n_exp = int(num_expected_params)
         n_outs = [max(0, min(n_exp - c0 * cr, (c1 - c0) * cr)) for c0, c1 in stripes]
@@ -401,8 +406,13 @@ class SecaggCrypter:
         # it; stripe 1's runs while stripe 0 crosses PCIe.
         bufs = [None] * S
         bufs[0] = stage(0)
-        res = (D.convert_stripe(params, *stripes[0], n2, bufs[0][1], sum(n_outs)) if packed is None
-               else D.float_list(sum(n_outs)))
+        if pool is not None and len(pool) == sum(n_outs):  # prepare_aggregate's floats, filled in place
+            res = pool
+            if packed is None:
+                D.convert_stripe(params, *stripes[0], n2, bufs[0][1])
+        else:
+            res = (D.convert_stripe(params, *stripes[0], n2, bufs[0][1], sum(n_outs)) if packed is None
+                   else D.float_list(sum(n_outs)))
         pend = {0: issue(0)}
         if S > 1:
             bufs[1] = stage(1)

@@ -210,9 +210,11 @@ def test_conv_contract_float_list(conv):
     conv.f64_into_list(lst, 0, vals[:0])
     with pytest.raises(ValueError):
         conv.f64_into_list(lst, 4, vals)  # past the end
+    conv.f64_into_list(lst, 1, vals[4:6])  # a filled slot is written again
+    assert lst[1] == 1e-310 and lst[2] == -3.75
+    lst[3] = "x"
     with pytest.raises(ValueError):
-        conv.f64_into_list(lst, 1, vals[:2])  # slot 2 already filled
-    assert lst[1] is None
+        conv.f64_into_list(lst, 3, vals[:1])  # neither None nor a float
     with pytest.raises(ValueError):
         conv.none_list(-1)
     assert conv.none_list(0) == []
@@ -244,8 +246,9 @@ def test_conv_contract_convert_and_fill(conv):
     assert conv.convert_and_fill(bad, lo, hi, 256, out) == (hi - lo) + 3
     with pytest.raises(ValueError):
         conv.convert_and_fill(lists, lo, hi, 256, out, -1)
+    res[5] = "x"
     with pytest.raises(ValueError):
-        conv.convert_and_fill(lists, lo, hi, 256, out, res, 4, vals)  # those slots are filled already
+        conv.convert_and_fill(lists, lo, hi, 256, out, res, 4, vals)  # a slot neither None nor a float
     for args in ((lists, 0, 3001, 256, np.empty((3, 3001, 64), np.uint32)),
                  (lists, 0, 10, 256, np.empty((3, 11, 64), np.uint32)),
                  (lists, 0, 10, 256, np.empty((3, 10, 64), np.uint32), res, 9, vals)):  # floats past the end
@@ -264,3 +267,24 @@ def test_convert_stripe_reduces_out_of_range_and_fills():
     D.convert_stripe(lists, 5, 35, n2, out, res, 1, np.array([0.25, 0.5]))
     assert [D.limbs_to_ints(out[u]) for u in range(3)] == [[v % n2 for v in lst[5:35]] for lst in lists]
     assert res == [None, 0.25, 0.5, None, None]
+
+
+def test_float_pool_filled_in_place():
+    """prepare_aggregate's output list made ahead: its floats' values are written in place (the same objects)
+    while only the list holds them; a float something else also holds is replaced, never changed."""
+    m = D._pyconv()
+    pool = m.float_pool(6)
+    assert pool == [0.0] * 6 and len({id(v) for v in pool}) == 6
+    ids = [id(v) for v in pool]
+    held = pool[3]  # a second holder
+    m.f64_into_list(pool, 1, np.array([1.5, -2.25, 3.0, float("nan")]))
+    assert pool[1:3] == [1.5, -2.25] and [id(v) for v in pool[1:3]] == ids[1:3]  # in place
+    assert held == 0.0 and pool[3] == 3.0 and id(pool[3]) != ids[3]  # replaced, the held one unchanged
+    assert pool[4] != pool[4] and pool[0] == 0.0 and pool[5] == 0.0
+    b = m.convert_and_fill([[1, 2], [3, 4]], 0, 2, 256, np.empty((2, 2, 64), np.uint32), pool, 0,
+                           np.array([7.0, 8.0]))
+    assert b == -1 and pool[:2] == [7.0, 8.0] and id(pool[0]) == ids[0]
+    with pytest.raises(ValueError):
+        m.f64_into_list(["x", 1.0], 0, np.array([1.0]))  # neither None nor a float
+    with pytest.raises(ValueError):
+        m.float_pool(-1)
