@@ -307,9 +307,7 @@ class _PyConvFallback:
         return [int.from_bytes(b[i:i + nb], "little") for i in range(0, len(b), nb)]
 
     @staticmethod
-    def convert_and_fill(lists: list, lo: int, hi: int, nb: int, out: np.ndarray, lst=None, off: int = 0,
-                         buf=None):
-        made = _PyConvFallback.none_list(lst) if isinstance(lst, int) else None  # (ValueError when negative)
+    def ints_to_bytes_held(lists: list, lo: int, hi: int, nb: int, out: np.ndarray) -> int:
         if nb <= 0 or nb % 4 or lo < 0 or hi < lo:
             raise ValueError("bad range or width (a positive multiple of 4 bytes)")
         if not all(isinstance(v, list) and len(v) >= hi for v in lists):
@@ -317,16 +315,12 @@ class _PyConvFallback:
         m = hi - lo
         if out.nbytes != len(lists) * m * nb:
             raise ValueError(f"output buffer holds {out.nbytes} bytes, {len(lists) * m * nb} needed")
-        if buf is not None and isinstance(lst, list):
-            _PyConvFallback.f64_into_list(lst, off, buf)
         rows = out.reshape(len(lists), m * nb // out.itemsize) if lists else out
-        bad = -1
         for u, v in enumerate(lists):
             b = _PyConvFallback.ints_to_bytes(v[lo:hi], nb, rows[u])
             if b >= 0:
-                bad = u * m + b
-                break
-        return (bad, made) if made is not None else bad
+                return u * m + b
+        return -1
 
     @staticmethod
     def float_pool(n: int) -> list:
@@ -447,31 +441,22 @@ def ints_to_limbs(cts: Sequence[int], modulus: Optional[int] = None, out: Option
     return out
 
 
-def convert_stripe(lists: List[list], c0: int, c1: int, modulus: Optional[int], out: np.ndarray,
-                   res=None, off: int = 0, values: Optional[np.ndarray] = None):
+def convert_stripe(lists: List[list], c0: int, c1: int, modulus: Optional[int], out: np.ndarray) -> np.ndarray:
     """Items [c0, c1) of every party's ciphertext list -> `out` [P, c1 - c0, 64] uint32 limbs on host threads
-    while this thread writes `values` (the previous stripe's floats) into res[off:] -- one C call that holds
-    the GIL, so the readers need no pins (csrc/fbm_pyconv.c convert_and_fill); then ints_to_limbs' slow path
-    (reduction mod N^2 of out-of-range values) for any party row that has one.  `res` an int: no floats --
-    this thread makes the [None] * res output list meanwhile, and the call returns it (else None)."""
-    vals = None if values is None else np.ascontiguousarray(values, dtype=np.float64)
-    r = _pyconv().convert_and_fill(lists, c0, c1, 256, out, res, off, vals)
-    bad, made = r if isinstance(r, tuple) else (r, None)
+    in one C call that holds the GIL, so the readers need no pins (csrc/fbm_pyconv.c ints_to_bytes_held);
+    then ints_to_limbs' slow path (reduction mod N^2 of out-of-range values) for any party row that has one."""
+    bad = _pyconv().ints_to_bytes_held(lists, c0, c1, 256, out)
     if bad >= 0:  # rare: values outside [0, 2^2048) from this party row on
         m = c1 - c0
         for u in range(bad // max(m, 1), len(lists)):
             ints_to_limbs(lists[u][c0:c1], modulus, out=out[u])
-    return made
-
-
-def float_list(n: int) -> list:
-    """The aggregate's output list, [None] * n, for f64_into_list to fill stripe by stripe."""
-    return _pyconv().none_list(n)
+    return out
 
 
 def float_pool(n: int) -> list:
     """n fresh 0.0 floats held by the returned list only: an aggregate's output list made ahead
-    (prepare_aggregate); f64_into_list / convert_stripe then write its values in place, no allocation."""
+    (prepare_aggregate, or made while the GPU exponentiates); f64_into_list then writes its values in
+    place, no allocation."""
     return _pyconv().float_pool(n)
 
 

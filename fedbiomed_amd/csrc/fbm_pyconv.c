@@ -13,11 +13,11 @@
  *                                      int in [0, 2^(8n)) (the caller then takes its slow
  *                                      path: type error or reduction mod N^2)
  *   bytes_to_ints(buf, n)           -> list of the unsigned little-endian n-byte integers
- *   convert_and_fill(lists, lo, hi, n, out[, list, offset, buf])
+ *   ints_to_bytes_held(lists, lo, hi, n, out)
  *                                   -> items [lo, hi) of every list into out [len(lists), hi - lo, n]
- *                                      on host threads while this one fills the float list, in one call
- *                                      that holds the GIL: the readers need no pins (see there); -1 or
- *                                      the first bad flat index (list u, item i: u (hi - lo) + i)
+ *                                      on host threads in one call that holds the GIL: the readers need
+ *                                      no pins (see there); -1 or the first bad flat index (list u,
+ *                                      item i: u (hi - lo) + i)
  *   none_list(n)                    -> [None] * n (the output list that f64_into_list fills)
  *   float_pool(n)                   -> n fresh 0.0 floats: an output list made ahead, filled in place
  *   f64_into_list(list, offset, buf) -> list[offset:offset + len(buf)] = floats of the float64 buffer
@@ -436,14 +436,13 @@ static PyObject* make_none_list(Py_ssize_t n) {
     return lst;
 }
 
-/* The researcher aggregate's host step, one call per stripe, with the GIL held throughout: worker threads
- * convert items [lo, hi) of every party's ciphertext list into `out` [P, hi - lo, nb] while this thread
- * writes the previous stripe's float64 values into the output list (or, with no floats, waits).  As the
- * GIL is never released, no Python code runs until the call returns: no list can change and no int be
- * freed under the readers, so nothing is pinned (ints_to_bytes, which releases the GIL, pays a reference
- * per item, taken and dropped on this thread: ~10 ns each, a third of the conversion's own cost).  The
- * readers touch only the ints' digits and `out`; this thread alone allocates.  Returns -1 or the first
- * bad flat index (u (hi - lo) + i) of the conversion. */
+/* The researcher aggregate's ciphertext conversion, one call per stripe: worker threads convert items
+ * [lo, hi) of every party's list into `out` [P, hi - lo, nb] while this thread waits, the GIL held
+ * throughout.  As the GIL is never released, no Python code runs until the call returns: no list can
+ * change and no int be freed under the readers, so nothing is pinned (ints_to_bytes, which releases the
+ * GIL, pays a reference per item, taken and dropped on this thread: ~10 ns each, a third of the
+ * conversion's own cost).  The readers touch only the ints' digits and `out`.  Returns -1 or the first
+ * bad flat index (u (hi - lo) + i). */
 typedef struct {
     PyObject*** rows; /* each party's ob_item + lo */
     Py_ssize_t m, lo, hi, nb, bad;
@@ -465,74 +464,37 @@ static void* heldconv_range(void* arg) {
 }
 #endif
 
-static PyObject* convert_and_fill(PyObject* self, PyObject* args) {
-    PyObject *lists, *out, *lst = Py_None;
-    Py_ssize_t lo, hi, nb, off = 0;
-    Py_buffer fview = {0};
-    int have_floats = 0;
-    if (!PyArg_ParseTuple(args, "O!nnnO|Onz*", &PyList_Type, &lists, &lo, &hi, &nb, &out, &lst, &off, &fview))
-        return NULL;
-    /* `lst` an int: no floats yet -- this thread makes the [None] * lst output list beside the readers
-     * instead, and the call returns (bad, list) */
-    Py_ssize_t new_len = -1;
-    if (PyLong_Check(lst)) {
-        new_len = PyLong_AsSsize_t(lst);
-        if (new_len < 0) {
-            if (fview.buf) PyBuffer_Release(&fview);
-            if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "negative length");
-            return NULL;
-        }
-    }
-    have_floats = new_len < 0 && lst != Py_None && fview.buf != NULL;
+static PyObject* ints_to_bytes_held(PyObject* self, PyObject* args) {
+    PyObject *lists, *out;
+    Py_ssize_t lo, hi, nb;
+    if (!PyArg_ParseTuple(args, "O!nnnO", &PyList_Type, &lists, &lo, &hi, &nb, &out)) return NULL;
     const Py_ssize_t P = PyList_GET_SIZE(lists), m = hi - lo;
-    Py_ssize_t k = 0;
-    PyObject** fitems = NULL;
-    const double* fsrc = NULL;
-    Py_buffer oview;
-#define CAF_FAIL(exc, msg)                       \
-    do {                                         \
-        if (fview.buf) PyBuffer_Release(&fview); \
-        PyErr_SetString(exc, msg);               \
-        return NULL;                             \
-    } while (0)
-    if (nb <= 0 || nb % 4 || lo < 0 || m < 0) CAF_FAIL(PyExc_ValueError, "bad range or width (a positive multiple of 4 bytes)");
+    if (nb <= 0 || nb % 4 || lo < 0 || m < 0) {
+        PyErr_SetString(PyExc_ValueError, "bad range or width (a positive multiple of 4 bytes)");
+        return NULL;
+    }
     for (Py_ssize_t u = 0; u < P; ++u) {
         PyObject* l = PyList_GET_ITEM(lists, u);
-        if (!PyList_Check(l) || PyList_GET_SIZE(l) < hi) CAF_FAIL(PyExc_ValueError, "every item must be a list holding the range");
-    }
-    if (have_floats) {
-        if (!PyList_Check(lst)) CAF_FAIL(PyExc_TypeError, "the float list must be a list");
-        k = fview.len / (Py_ssize_t)sizeof(double);
-        if (fview.len % (Py_ssize_t)sizeof(double) || off < 0 || off + k > PyList_GET_SIZE(lst))
-            CAF_FAIL(PyExc_ValueError, "float64 buffer does not fit the list at that offset");
-        fitems = ((PyListObject*)lst)->ob_item + off;
-        if (check_slots(fitems, k) < 0) {
-            PyBuffer_Release(&fview);
+        if (!PyList_Check(l) || PyList_GET_SIZE(l) < hi) {
+            PyErr_SetString(PyExc_ValueError, "every item must be a list holding the range");
             return NULL;
         }
-        fsrc = (const double*)fview.buf;
     }
-#undef CAF_FAIL
-    if (get_out(out, &oview, P * m * nb) < 0) {
-        if (fview.buf) PyBuffer_Release(&fview);
-        return NULL;
-    }
+    Py_buffer oview;
+    if (get_out(out, &oview, P * m * nb) < 0) return NULL;
     if (((uintptr_t)oview.buf & 3) != 0) {
         PyBuffer_Release(&oview);
-        if (fview.buf) PyBuffer_Release(&fview);
         PyErr_SetString(PyExc_ValueError, "output buffer must be 4-byte aligned");
         return NULL;
     }
     PyObject*** rows = (PyObject***)PyMem_Malloc((size_t)(P > 0 ? P : 1) * sizeof(PyObject**));
     if (!rows) {
         PyBuffer_Release(&oview);
-        if (fview.buf) PyBuffer_Release(&fview);
         return PyErr_NoMemory();
     }
     for (Py_ssize_t u = 0; u < P; ++u) rows[u] = ((PyListObject*)PyList_GET_ITEM(lists, u))->ob_item + lo;
     const Py_ssize_t n = P * m;
     Py_ssize_t bad = -1;
-    PyObject* made = NULL;
 #if FBM_DIGITS_FAST
     int nt = n >= 1024 ? conv_threads(n) : 1;
     heldconv_job jobs[64];
@@ -540,37 +502,24 @@ static PyObject* convert_and_fill(PyObject* self, PyObject* args) {
     int started[64] = {0};
     for (int t = 0; t < nt; ++t) {
         jobs[t] = (heldconv_job){rows, m > 0 ? m : 1, n * t / nt, n * (t + 1) / nt, nb, -1, (unsigned char*)oview.buf};
-        started[t] = pthread_create(&tid[t], NULL, heldconv_range, &jobs[t]) == 0;
+        started[t] = t > 0 && pthread_create(&tid[t], NULL, heldconv_range, &jobs[t]) == 0;
     }
-    if (k) fill_slots(fitems, fsrc, k); /* the previous stripe's floats, beside the readers (on failure
-                                             the exception is set: finish the readers first) */
-    if (new_len >= 0) made = make_none_list(new_len); /* (or the output list, beside them) */
-    for (int t = 0; t < nt; ++t) {
+    heldconv_range(&jobs[0]);
+    for (int t = 1; t < nt; ++t) {
         if (started[t])
             pthread_join(tid[t], NULL);
         else
             heldconv_range(&jobs[t]); /* thread creation failed: its range here */
     }
     for (int t = 0; t < nt && bad < 0; ++t) bad = jobs[t].bad;
-#else /* the byte API: on this thread, floats first */
-    if (k) fill_slots(fitems, fsrc, k);
-    for (Py_ssize_t f = 0; f < n && bad < 0 && !PyErr_Occurred(); ++f) {
+#else /* the byte API: on this thread */
+    for (Py_ssize_t f = 0; f < n && bad < 0; ++f) {
         PyObject* v = rows[f / m][f % m];
         if (!PyLong_Check(v) || long_to_bytes_api(v, (unsigned char*)oview.buf + f * nb, nb) < 0) bad = f;
     }
-    if (new_len >= 0 && !PyErr_Occurred()) made = make_none_list(new_len);
 #endif
     PyMem_Free(rows);
     PyBuffer_Release(&oview);
-    if (fview.buf) PyBuffer_Release(&fview);
-    if (PyErr_Occurred()) {
-        Py_XDECREF(made);
-        return NULL;
-    }
-    if (new_len >= 0) {
-        PyObject* r = Py_BuildValue("(nN)", bad, made);
-        return r;
-    }
     return PyLong_FromSsize_t(bad);
 }
 
@@ -639,9 +588,8 @@ static PyMethodDef methods[] = {
     {"bytes_to_ints", bytes_to_ints, METH_VARARGS, "buffer of n-byte LE unsigned values -> list of ints"},
     {"none_list", none_list, METH_VARARGS, "n -> [None] * n"},
     {"float_pool", float_pool, METH_VARARGS, "n -> n distinct 0.0 floats held by the list only"},
-    {"convert_and_fill", convert_and_fill, METH_VARARGS,
-     "lists, lo, hi, n, out[, float list, offset, float64 buffer] -> -1 or first bad flat index (GIL held); "
-     "with an int for the list: (bad, [None] * that int)"},
+    {"ints_to_bytes_held", ints_to_bytes_held, METH_VARARGS,
+     "lists, lo, hi, n, out -> -1 or first bad flat index (host threads, GIL held, no pins)"},
     {"f64_into_list", f64_into_list, METH_VARARGS, "list, offset, float64 buffer -> None (fills the list)"},
     {NULL, NULL, 0, NULL},
 };

@@ -355,11 +355,10 @@ class SecaggCrypter:
                            pool=None) -> List[float]:
         """The list API's aggregate over ct_offset stripes (one when the vector is small).  Per stripe: the
         parties' ints -> pinned limbs -> H2D on a copy stream, the combine with that stripe's factor, the
-        float64 D2H in stream order, then the next stripe's factor.  Three things overlap: a later
-        stripe's ints convert on host threads while this thread writes a stripe's floats into the output
-        list (one C call holding the GIL, D.convert_stripe: one pass, no intermediate list, no pins --
-        the 10M-element float list is the call's largest host cost), and the GPU runs the stripe between
-        them and the next factor.  Stripe outputs: elements [c0 cr, c1 cr) capped by
+        float64 D2H in stream order, then the next stripe's factor.  The host converts every stripe's ints
+        first (host threads, one GIL-held C call each: no per-item pins) and issues its GPU work, then makes
+        the output's float objects while the GPU runs the factors (the 10M-element float list is the call's
+        largest host cost) and writes each stripe's values into them in place as its D2H lands.  Stripe outputs: elements [c0 cr, c1 cr) capped by
         num_expected_params, as the unsplit decode (_jls.py:146-167); a stripe past it still runs its
         checks (the unsplit call's errors).  `pool`: prepare_aggregate's output list (its floats made
         ahead, written in place here) when it has this call's length."""
@@ -403,37 +402,20 @@ class SecaggCrypter:
                 factors[k + 1] = self.decrypt_factor_tensor(current_round, n1 - n0, key, biprime, ct_offset=n0)
             return out_h, ev
 
-        # Two stripes converted ahead: stripe k's floats are written (this thread) while stripe k + 2's ints
-        # convert (host threads), in one GIL-held C call, and stripe k + 1 is on the GPU meanwhile (its H2D,
-        # combine and D2H then never wait for the host).  Stripe 0's conversion makes the output list beside
-        # it; stripe 1's runs while stripe 0 crosses PCIe.
-        bufs = [None] * S
-        bufs[0] = stage(0)
-        if pool is not None and len(pool) == sum(n_outs):  # prepare_aggregate's floats, filled in place
-            res = pool
-            if packed is None:
-                D.convert_stripe(params, *stripes[0], n2, bufs[0][1])
-        else:
-            res = (D.convert_stripe(params, *stripes[0], n2, bufs[0][1], sum(n_outs)) if packed is None
-                   else D.float_list(sum(n_outs)))
-        pend = {0: issue(0)}
-        if S > 1:
-            bufs[1] = stage(1)
-            if packed is None:
-                D.convert_stripe(params, *stripes[1], n2, bufs[1][1])
-            pend[1] = issue(1)
+        # Every stripe's ints are converted (host threads, one GIL-held C call each) and its H2D -> combine
+        # -> D2H issued first; then the output list's float objects are made while the GPU runs the
+        # factors (or, prepared, were made ahead), and each stripe's values are written into them in place
+        # as its D2H lands -- the host's largest cost, the 10M float objects, off the GPU's critical path.
+        bufs, pend = [None] * S, []
         for k in range(S):
-            out_h, ev = pend.pop(k)
+            bufs[k] = stage(k)
+            if packed is None:
+                D.convert_stripe(params, *stripes[k], n2, bufs[k][1])
+            pend.append(issue(k))
+        res = pool if pool is not None and len(pool) == sum(n_outs) else D.float_pool(sum(n_outs))
+        for k, (out_h, ev) in enumerate(pend):
             ev.synchronize()
-            if k + 2 < S:
-                bufs[k + 2] = stage(k + 2)
-                if packed is None:
-                    D.convert_stripe(params, *stripes[k + 2], n2, bufs[k + 2][1], res, offs[k], out_h.numpy())
-                else:
-                    D.f64_into_list(res, offs[k], out_h.numpy())
-                pend[k + 2] = issue(k + 2)
-            else:
-                D.f64_into_list(res, offs[k], out_h.numpy())
+            D.f64_into_list(res, offs[k], out_h.numpy())
         return res
 
     @staticmethod

@@ -220,9 +220,9 @@ def test_conv_contract_float_list(conv):
     assert conv.none_list(0) == []
 
 
-def test_conv_contract_convert_and_fill(conv):
-    """The aggregate's per-stripe host call: items [lo, hi) of every party's list -> out [P, hi - lo, n] (host
-    threads, GIL held) while the previous stripe's floats fill the output list; -1 or the first bad flat index."""
+def test_conv_contract_ints_to_bytes_held(conv):
+    """The aggregate's per-stripe conversion: items [lo, hi) of every party's list -> out [P, hi - lo, n] on
+    host threads in one GIL-held call (no pins); -1 or the first bad flat index u (hi - lo) + i."""
     rng = random.Random(26)
     lists = [[rng.getrandbits(2048) for _ in range(3000)] for _ in range(3)]
     lo, hi = 300, 2700
@@ -230,43 +230,33 @@ def test_conv_contract_convert_and_fill(conv):
     ref = np.empty_like(out)
     for u in range(3):
         assert conv.ints_to_bytes(lists[u][lo:hi], 256, ref[u]) == -1
-    assert conv.convert_and_fill(lists, lo, hi, 256, out) == -1
+    assert conv.ints_to_bytes_held(lists, lo, hi, 256, out) == -1
     assert out.tobytes() == ref.tobytes()
-    res = conv.none_list(10)
-    vals = np.array([1.5, -2.0, float("inf")], np.float64)
-    out[:] = 0
-    assert conv.convert_and_fill(lists, lo, hi, 256, out, res, 4, vals) == -1
-    assert out.tobytes() == ref.tobytes() and res[4:7] == [1.5, -2.0, float("inf")] and res[7] is None
-    out[:] = 0
-    b, made = conv.convert_and_fill(lists, lo, hi, 256, out, 7)  # an int: the output list made beside
-    assert b == -1 and made == [None] * 7 and out.tobytes() == ref.tobytes()
     bad = [list(v) for v in lists]
     bad[2][lo + 9] = -1
     bad[1][lo + 3] = "x"
-    assert conv.convert_and_fill(bad, lo, hi, 256, out) == (hi - lo) + 3
-    with pytest.raises(ValueError):
-        conv.convert_and_fill(lists, lo, hi, 256, out, -1)
-    res[5] = "x"
-    with pytest.raises(ValueError):
-        conv.convert_and_fill(lists, lo, hi, 256, out, res, 4, vals)  # a slot neither None nor a float
-    for args in ((lists, 0, 3001, 256, np.empty((3, 3001, 64), np.uint32)),
-                 (lists, 0, 10, 256, np.empty((3, 11, 64), np.uint32)),
-                 (lists, 0, 10, 256, np.empty((3, 10, 64), np.uint32), res, 9, vals)):  # floats past the end
+    assert conv.ints_to_bytes_held(bad, lo, hi, 256, out) == (hi - lo) + 3
+    bad[1][lo + 3] = 5
+    bad[0][hi] = "outside the range"  # not converted, not reported
+    assert conv.ints_to_bytes_held(bad, lo, hi, 256, out) == 2 * (hi - lo) + 9
+    assert conv.ints_to_bytes_held(lists, 5, 5, 256, np.empty((3, 0, 64), np.uint32)) == -1
+    for args in ((lists, 0, 3001, 256, np.empty((3, 3001, 64), np.uint32)),  # past a list's end
+                 (lists, 0, 10, 256, np.empty((3, 11, 64), np.uint32)),  # buffer size
+                 (lists, 0, 10, 6, np.empty((3, 10, 6), np.uint8)),  # width not a word multiple
+                 ([lists[0], (1, 2)], 0, 1, 256, np.empty((2, 1, 64), np.uint32))):
         with pytest.raises(ValueError):
-            conv.convert_and_fill(*args)
+            conv.ints_to_bytes_held(*args)
 
 
-def test_convert_stripe_reduces_out_of_range_and_fills():
+def test_convert_stripe_reduces_out_of_range():
     n2 = (2**1023 + 1155) ** 2
     rng = random.Random(27)
     lists = [[rng.getrandbits(2040) for _ in range(50)] for _ in range(3)]
     lists[1][12] = -7
     lists[2][30] = 2**2050 + 3
     out = np.empty((3, 30, 64), np.uint32)
-    res = D.float_list(5)
-    D.convert_stripe(lists, 5, 35, n2, out, res, 1, np.array([0.25, 0.5]))
+    D.convert_stripe(lists, 5, 35, n2, out)
     assert [D.limbs_to_ints(out[u]) for u in range(3)] == [[v % n2 for v in lst[5:35]] for lst in lists]
-    assert res == [None, 0.25, 0.5, None, None]
 
 
 def test_float_pool_filled_in_place():
@@ -281,9 +271,8 @@ def test_float_pool_filled_in_place():
     assert pool[1:3] == [1.5, -2.25] and [id(v) for v in pool[1:3]] == ids[1:3]  # in place
     assert held == 0.0 and pool[3] == 3.0 and id(pool[3]) != ids[3]  # replaced, the held one unchanged
     assert pool[4] != pool[4] and pool[0] == 0.0 and pool[5] == 0.0
-    b = m.convert_and_fill([[1, 2], [3, 4]], 0, 2, 256, np.empty((2, 2, 64), np.uint32), pool, 0,
-                           np.array([7.0, 8.0]))
-    assert b == -1 and pool[:2] == [7.0, 8.0] and id(pool[0]) == ids[0]
+    m.f64_into_list(pool, 0, np.array([7.0, 8.0]))
+    assert pool[:2] == [7.0, 8.0] and id(pool[0]) == ids[0]
     with pytest.raises(ValueError):
         m.f64_into_list(["x", 1.0], 0, np.array([1.0]))  # neither None nor a float
     with pytest.raises(ValueError):
