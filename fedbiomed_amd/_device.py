@@ -323,7 +323,12 @@ class _PyConvFallback:
         return -1
 
     @staticmethod
-    def float_pool(n: int) -> list:
+    def none_list(n: int) -> list:
+    """[None] * n in one C pass: an output list whose float objects f64_into_list makes."""
+    return _pyconv().none_list(n)
+
+
+def float_pool(n: int) -> list:
         if n < 0:
             raise ValueError("negative length")
         return [float(0) for _ in range(n)]
@@ -451,6 +456,11 @@ def convert_stripe(lists: List[list], c0: int, c1: int, modulus: Optional[int], 
         for u in range(bad // max(m, 1), len(lists)):
             ints_to_limbs(lists[u][c0:c1], modulus, out=out[u])
     return out
+
+
+def none_list(n: int) -> list:
+    """[None] * n in one C pass: an output list whose float objects f64_into_list makes."""
+    return _pyconv().none_list(n)
 
 
 def float_pool(n: int) -> list:

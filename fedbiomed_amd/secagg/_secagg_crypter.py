@@ -357,8 +357,8 @@ class SecaggCrypter:
         parties' ints -> pinned limbs -> H2D on a copy stream, the combine with that stripe's factor, the
         float64 D2H in stream order, then the next stripe's factor.  The host converts every stripe's ints
         first (host threads, one GIL-held C call each: no per-item pins) and issues its GPU work, then makes
-        the output's float objects while the GPU runs the factors (the 10M-element float list is the call's
-        largest host cost) and writes each stripe's values into them in place as its D2H lands.  Stripe outputs: elements [c0 cr, c1 cr) capped by
+        the output list and the last stripe's float objects while the GPU runs the factors (the 10M-element
+        float list is the call's largest host cost) and writes each stripe's values as its D2H lands.  Stripe outputs: elements [c0 cr, c1 cr) capped by
         num_expected_params, as the unsplit decode (_jls.py:146-167); a stripe past it still runs its
         checks (the unsplit call's errors).  `pool`: prepare_aggregate's output list (its floats made
         ahead, written in place here) when it has this call's length."""
@@ -403,16 +403,21 @@ class SecaggCrypter:
             return out_h, ev
 
         # Every stripe's ints are converted (host threads, one GIL-held C call each) and its H2D -> combine
-        # -> D2H issued first; then the output list's float objects are made while the GPU runs the
-        # factors (or, prepared, were made ahead), and each stripe's values are written into them in place
-        # as its D2H lands -- the host's largest cost, the 10M float objects, off the GPU's critical path.
+        # -> D2H issued first; then, while the GPU runs the factors, the output list and the last stripe's
+        # float objects are made (prepared: all of them were made ahead); each stripe's floats are made with
+        # their values as its D2H lands, the last stripe's values written in place -- so the host's largest
+        # cost, the 10M float objects, runs beside the factors instead of after the last one.
         bufs, pend = [None] * S, []
         for k in range(S):
             bufs[k] = stage(k)
             if packed is None:
                 D.convert_stripe(params, *stripes[k], n2, bufs[k][1])
             pend.append(issue(k))
-        res = pool if pool is not None and len(pool) == sum(n_outs) else D.float_pool(sum(n_outs))
+        if pool is not None and len(pool) == sum(n_outs):
+            res = pool
+        else:  # the last stripe's float objects made now (its values land last); the others' as they land
+            res = D.none_list(sum(n_outs))
+            D.f64_into_list(res, offs[-1], np.zeros(n_outs[-1]))
         for k, (out_h, ev) in enumerate(pend):
             ev.synchronize()
             D.f64_into_list(res, offs[k], out_h.numpy())
