@@ -323,12 +323,7 @@ class _PyConvFallback:
         return -1
 
     @staticmethod
-    def none_list(n: int) -> list:
-    """[None] * n in one C pass: an output list whose float objects f64_into_list makes."""
-    return _pyconv().none_list(n)
-
-
-def float_pool(n: int) -> list:
+    def float_pool(n: int) -> list:
         if n < 0:
             raise ValueError("negative length")
         return [float(0) for _ in range(n)]
