@@ -171,11 +171,13 @@ static PyObject* floats_to_f64(PyObject* self, PyObject* args) {
     return PyLong_FromSsize_t(bad);
 }
 
-/* Ciphertext-sized conversions run on several host threads with the GIL released: the
- * items are pinned first (a reference each, taken under the GIL), so a list mutated by
- * another Python thread meanwhile cannot free them; PyLong digits are immutable and
- * long_to_words touches no interpreter state.  FBM_CONV_THREADS overrides the thread count
- * (default 8, the GPU box's CPU share is 16). */
+/* Ciphertext-sized conversions run on several host threads WHILE THIS THREAD HOLDS THE GIL (as
+ * floats_to_f64): no Python code runs meanwhile, so the list cannot change and its ints cannot be
+ * freed under the readers, which read only the ints' digits (immutable; long_to_words touches no
+ * interpreter state) -- no reference per item is needed.  (Round 4's form released the GIL and pinned
+ * every item first: a reference taken and dropped on this thread, ~10 ns each, a third of the
+ * conversion's own cost.)  FBM_CONV_THREADS overrides the thread count (default 8, the GPU box's CPU
+ * share is 16). */
 #define PAR_MIN_BYTES (1 << 20)
 
 typedef struct {
@@ -202,16 +204,10 @@ static void* conv_range(void* arg) {
 /* -1, or the first bad index over all ranges (each range stops at its own first bad item). */
 static Py_ssize_t ints_to_words_parallel(PyObject* seq, Py_ssize_t n, Py_ssize_t nb, unsigned char* dst,
                                          int nt) {
-    PyObject** items = (PyObject**)PyMem_Malloc((size_t)n * sizeof(PyObject*));
-    if (!items) return -2;
-    for (Py_ssize_t i = 0; i < n; ++i) {
-        items[i] = PyList_GET_ITEM(seq, i);
-        Py_INCREF(items[i]);
-    }
+    PyObject** items = ((PyListObject*)seq)->ob_item;
     conv_job jobs[64];
     pthread_t tid[64];
     int started[64] = {0};
-    Py_BEGIN_ALLOW_THREADS
     for (int t = 0; t < nt; ++t) {
         jobs[t] = (conv_job){items, dst, n * t / nt, n * (t + 1) / nt, nb, -1};
         if (t > 0) started[t] = pthread_create(&tid[t], NULL, conv_range, &jobs[t]) == 0;
@@ -223,11 +219,8 @@ static Py_ssize_t ints_to_words_parallel(PyObject* seq, Py_ssize_t n, Py_ssize_t
         else
             conv_range(&jobs[t]); /* thread creation failed: do its range here */
     }
-    Py_END_ALLOW_THREADS
     Py_ssize_t bad = -1;
     for (int t = 0; t < nt && bad < 0; ++t) bad = jobs[t].bad;
-    for (Py_ssize_t i = 0; i < n; ++i) Py_DECREF(items[i]);
-    PyMem_Free(items);
     return bad;
 }
 #endif
@@ -255,10 +248,6 @@ static PyObject* ints_to_bytes(PyObject* self, PyObject* args) {
 #if FBM_DIGITS_FAST
         bad = ints_to_words_parallel(seq, n, nb, dst, nt);
 #endif
-        if (bad == -2) {
-            PyBuffer_Release(&view);
-            return PyErr_NoMemory();
-        }
     } else {
         for (Py_ssize_t i = 0; i < n; ++i) {
             PyObject* v = PyList_GET_ITEM(seq, i);
