@@ -13,7 +13,7 @@ import pytest
 
 from fedbiomed_amd import _device as D, workload as W
 
-N_CASES = 20
+N_CASES = 48
 
 
 def _bits(xs):
