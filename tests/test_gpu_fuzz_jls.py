@@ -1,0 +1,87 @@
+"""Seeded random cases of the Joye-Libert object API (fedbiomed_amd.secagg._jls, the reference's _jls.py
+mirrored with every vector operation on the device) against the oracle's restatement
+(oracle/secagg_oracle.py, pinned by tests/golden/jls_api.json, ves_wide.json, ves_signed.json): VES of random
+shapes and values (negative and wider than their slot included) through encode / decode, and
+JoyeLibert.protect -> aggregate round trips at random target ranges (the fused kernels' shape and past it),
+party counts, rounds and keys, with the ciphertexts compared bit for bit."""
+
+import math
+import random
+
+import pytest
+
+from fedbiomed_amd import workload as W
+from fedbiomed_amd.constants import SAParameters
+
+N_CASES = 24
+
+
+def _ves_case(i):
+    rng = random.Random(9500 + i)
+    ptsize = rng.choice([1024, 1024, 300, 2048, 4096])
+    valuesize = rng.choice([13, 30, 47, 64, 100, 130, 257])
+    add_ops = rng.randint(1, 20)
+    es = valuesize + math.ceil(math.log2(add_ops + 1))
+    cr = ptsize // es
+    n = rng.choice([1, 2, max(1, cr - 1), max(1, cr), cr + 1, rng.randint(1, 400)])
+    kind = rng.choice(["fit", "fit", "wide", "signed"])
+    if kind == "fit":
+        V = [rng.getrandbits(valuesize) for _ in range(n)]
+    elif kind == "wide":  # values wider than their slot: their high bits spill into the next slots, as there
+        V = [rng.getrandbits(es + rng.randint(1, 9)) for _ in range(n)]
+    else:
+        V = [rng.getrandbits(valuesize) * rng.choice([1, -1]) for _ in range(n)]
+    v_expected = rng.choice([n, max(0, n - 3), n + 4])
+    return ptsize, valuesize, add_ops, es, cr, V, v_expected
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i", range(N_CASES))
+def test_ves_fuzz_vs_oracle(i):
+    from oracle import secagg_oracle as O
+    from fedbiomed_amd.secagg._jls import VES
+
+    ptsize, valuesize, add_ops, es, cr, V, v_expected = _ves_case(i)
+    ves = VES(ptsize, valuesize)
+    E = ves.encode(V, add_ops)
+    assert E == O.ves_encode(V, es, cr), i
+    assert ves.decode(E, add_ops, v_expected) == (O.ves_decode(E, es, cr, v_expected) if cr >= 1 else []), i
+
+
+def _jl_case(i):
+    rng = random.Random(9700 + i)
+    P = rng.randint(1, 7)
+    target = rng.choice([None, 2**16, 2**40, 2**90, 2**150])
+    n = rng.choice([1, rng.randint(2, 200), rng.randint(2, 200)])
+    tau = rng.choice([0, 5, rng.getrandbits(64), rng.getrandbits(600)])
+    keys = [rng.getrandbits(rng.choice([100, 2040])) for _ in range(P)]
+    tr = target or SAParameters.TARGET_RANGE
+    xs = [[rng.randrange(0, tr * (SAParameters.WEIGHT_RANGE // 2) // max(P, 1)) for _ in range(n)] for _ in range(P)]
+    n_exp = rng.choice([n, max(1, n - 2)])
+    return P, target, n, tau, keys, xs, n_exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i", range(N_CASES))
+def test_joye_libert_fuzz_vs_oracle(i):
+    from oracle import secagg_oracle as O
+    from fedbiomed_amd.secagg._jls import FDH, EncryptedNumber, JoyeLibert, PublicParam, ServerKey, UserKey
+
+    P, target, n, tau, keys, xs, n_exp = _jl_case(i)
+    N = W.BIPRIME0
+    pp = PublicParam(n_modulus=N, bits=SAParameters.KEY_SIZE // 2,
+                     hashing_function=FDH(SAParameters.KEY_SIZE, N * N).H)
+    jl = JoyeLibert(target_range=target)
+    es, cr = jl._vector_encoder._slot(P)
+    cts = []
+    for p in range(P):
+        got = jl.protect(pp, UserKey(pp, keys[p]), tau, xs[p], P)
+        ref = O.jl_user_encrypt(O.ves_encode(xs[p], es, cr), tau, keys[p], N)
+        assert got == ref, (i, p)
+        cts.append([EncryptedNumber(pp, c) for c in got])
+    sk0 = -sum(keys)
+    out = jl.aggregate(ServerKey(pp, sk0), tau, cts, n_exp)
+    summed = [math.prod(int(c.ciphertext) for c in col) % (N * N) for col in zip(*cts)]
+    ref = O.ves_decode(O.jl_server_decrypt(summed, tau, sk0, N), es, cr, n_exp)
+    assert out == ref, i
+    assert out == [sum(col) for col in zip(*xs)][:n_exp]  # and the plain sums, as the scheme promises
