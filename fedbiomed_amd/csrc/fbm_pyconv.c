@@ -280,15 +280,24 @@ static PyObject* long_from_bytes_api(const unsigned char* src, Py_ssize_t nb) {
 
 #if FBM_DIGITS_FAST
 /* nw little-endian 32-bit words -> int, built straight in CPython's 30-bit digits
- * (_PyLong_FromByteArray goes byte by byte). */
-static PyObject* words_to_long(const uint32_t* w, Py_ssize_t nw) {
+ * (_PyLong_FromByteArray goes byte by byte).  Split in two so that a long list is made in two
+ * passes: this thread allocates every object (the allocator is the interpreter's), then host
+ * threads write the digits of the objects nobody else has seen yet (pure arithmetic). */
+static Py_ssize_t words_used(const uint32_t* w, Py_ssize_t nw) {
     while (nw > 0 && w[nw - 1] == 0) --nw;
-    if (nw <= 1) return PyLong_FromUnsignedLong(nw ? w[0] : 0); /* small-int cache for 0..256 */
-    uint32_t top = w[nw - 1];
-    Py_ssize_t nbits = 32 * (nw - 1) + (32 - __builtin_clz(top));
-    Py_ssize_t nd = (nbits + PyLong_SHIFT - 1) / PyLong_SHIFT;
-    PyLongObject* v = _PyLong_New(nd);
-    if (!v) return NULL;
+    return nw;
+}
+
+/* An int of nw significant words: the small ones (nw <= 1, the small-int cache among them) made
+ * whole, the others allocated with their digits left for long_fill. */
+static PyObject* long_alloc(const uint32_t* w, Py_ssize_t nw) {
+    if (nw <= 1) return PyLong_FromUnsignedLong(nw ? w[0] : 0);
+    Py_ssize_t nbits = 32 * (nw - 1) + (32 - __builtin_clz(w[nw - 1]));
+    return (PyObject*)_PyLong_New((nbits + PyLong_SHIFT - 1) / PyLong_SHIFT);
+}
+
+static void long_fill(PyLongObject* v, const uint32_t* w, Py_ssize_t nw) {
+    const Py_ssize_t nd = Py_SIZE(v);
     uint64_t acc = 0;
     int bits = 0;
     Py_ssize_t k = 0, d = 0;
@@ -301,10 +310,54 @@ static PyObject* words_to_long(const uint32_t* w, Py_ssize_t nw) {
         acc >>= PyLong_SHIFT;
         bits -= PyLong_SHIFT;
     }
-    return (PyObject*)v;
+}
+
+typedef struct {
+    PyObject** items;
+    const unsigned char* src;
+    Py_ssize_t lo, hi, nb;
+} fill_job;
+
+static void* fill_range(void* arg) {
+    fill_job* j = (fill_job*)arg;
+    for (Py_ssize_t i = j->lo; i < j->hi; ++i) {
+        const uint32_t* w = (const uint32_t*)(j->src + i * j->nb);
+        Py_ssize_t nw = words_used(w, j->nb / 4);
+        if (nw > 1) long_fill((PyLongObject*)j->items[i], w, nw);
+    }
+    return NULL;
+}
+
+/* n values of nb bytes (nb % 4 == 0, src 4-byte aligned) into the NULL-initialised list: 0, or -1 with
+ * an exception set (the items made so far stay in the list, their digits unread by anyone). */
+static int words_into_list(PyObject* lst, const unsigned char* src, Py_ssize_t n, Py_ssize_t nb) {
+    PyObject** items = ((PyListObject*)lst)->ob_item;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        const uint32_t* w = (const uint32_t*)(src + i * nb);
+        if (!(items[i] = long_alloc(w, words_used(w, nb / 4)))) return -1;
+    }
+    int nt = n * nb >= PAR_MIN_BYTES ? conv_threads(n) : 1;
+    fill_job jobs[64];
+    pthread_t tid[64];
+    int started[64] = {0};
+    for (int t = 0; t < nt; ++t) {
+        jobs[t] = (fill_job){items, src, n * t / nt, n * (t + 1) / nt, nb};
+        if (t > 0) started[t] = pthread_create(&tid[t], NULL, fill_range, &jobs[t]) == 0;
+    }
+    fill_range(&jobs[0]);
+    for (int t = 1; t < nt; ++t) {
+        if (started[t])
+            pthread_join(tid[t], NULL);
+        else
+            fill_range(&jobs[t]);
+    }
+    return 0;
 }
 #endif
 
+/* The list is made by this thread; for the word layout the digits are written by host threads
+ * once every object exists, while this thread holds the GIL and before the list is returned: no
+ * other code can see an object whose digits are still being written. */
 static PyObject* bytes_to_ints(PyObject* self, PyObject* args) {
     Py_buffer view;
     Py_ssize_t nb;
@@ -318,14 +371,15 @@ static PyObject* bytes_to_ints(PyObject* self, PyObject* args) {
     PyObject* lst = PyList_New(n);
     if (lst) {
         const unsigned char* src = (const unsigned char*)view.buf;
-        for (Py_ssize_t i = 0; i < n; ++i) {
 #if FBM_DIGITS_FAST
-            const int words = nb % 4 == 0 && ((uintptr_t)src & 3) == 0;
-            PyObject* v = words ? words_to_long((const uint32_t*)(src + i * nb), nb / 4)
-                                : long_from_bytes_api(src + i * nb, nb);
-#else
-            PyObject* v = long_from_bytes_api(src + i * nb, nb);
+        if (nb % 4 == 0 && ((uintptr_t)src & 3) == 0) {
+            if (words_into_list(lst, src, n, nb) < 0) Py_CLEAR(lst);
+            PyBuffer_Release(&view);
+            return lst;
+        }
 #endif
+        for (Py_ssize_t i = 0; i < n; ++i) {
+            PyObject* v = long_from_bytes_api(src + i * nb, nb);
             if (!v) {
                 Py_CLEAR(lst);
                 break;

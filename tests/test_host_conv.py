@@ -111,6 +111,11 @@ def test_threaded_ints_to_bytes_first_bad_index(monkeypatch, threads):
         v2[bad_at] = bad
         v2[5998] = -1  # a later bad item in another range: the first one is reported
         assert m.ints_to_bytes(v2, 256, out) == min(bad_at, 5998)
+    # and back: 6000 x 256 B is past the threaded size, so the digits are written on host threads
+    assert m.ints_to_bytes(vals, 256, out) == -1
+    back = m.bytes_to_ints(out, 256)
+    assert back == vals and all(type(v) is int for v in back)
+    assert all(v is w for v, w in zip(back[:2], range(2)))  # the small-int cache, never written by the fill
 
 
 def test_bytes_to_ints_word_path_edges():
