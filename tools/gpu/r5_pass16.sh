@@ -1,8 +1,8 @@
-# round 5, pass 16: bytes_to_ints with its digits written on host threads -- the conversion alone
+# round 5, pass 16: bytes_to_ints with its digits written on host threads; results freed outside the clock --
 # (box CPUs), one node's 10M-element list encrypt, and the bench line
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/${1:-r5ag}
+O=$R/gpurun_out/${1:-r5ah}
 mkdir -p $O
 cd $R
 timeout -k 10 120 python -u tools/convbench.py 1 8 16 > $O/convbench.txt 2>&1 || { echo "CONVBENCH FAILED"; tail -20 $O/convbench.txt; exit 1; }
