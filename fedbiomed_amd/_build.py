@@ -22,6 +22,10 @@ SOURCES = ["fbm_lom.hip", "fbm_jl.hip", "fbm_gen.hip", "fbm_ass.hip", "fbm_capi.
 PYCONV_SRC = os.path.join(CSRC, "fbm_pyconv.c")
 PYCONV_OUT = os.path.join(HERE, "_lib", "_fbm_pyconv" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
 ARCH = os.environ.get("FBM_OFFLOAD_ARCH", "gfx950")
+# a plain C99 caller of the C ABI (tests/test_c_client.py): the binding a non-Python host would write
+CCLIENT_SRC = os.path.join(ROOT, "tests", "c_client", "fbm_c_roundtrip.c")
+CCLIENT_OUT = os.path.join(ROOT, "tests", "c_client", "fbm_c_roundtrip")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 
 def hipcc() -> str:
@@ -55,6 +59,26 @@ def build_pyconv(force: bool = False, verbose: bool = False) -> str:
     return PYCONV_OUT
 
 
+def build_c_client(force: bool = False, verbose: bool = False) -> str:
+    """gcc, C99, against include/fbm_secagg.h and the in-tree library (found through an $ORIGIN rpath,
+    so the tree can move, as it does to the GPU box) plus the HIP runtime for its device buffers."""
+    deps = [CCLIENT_SRC, OUT, os.path.join(ROOT, "include", "fbm_secagg.h")]
+    if not force and os.path.exists(CCLIENT_OUT) and all(
+            os.path.getmtime(CCLIENT_OUT) >= os.path.getmtime(d) for d in deps):
+        return CCLIENT_OUT
+    rel = os.path.relpath(os.path.dirname(OUT), os.path.dirname(CCLIENT_OUT))
+    tmp = CCLIENT_OUT + ".tmp"
+    cmd = [os.environ.get("CC", "gcc"), "-std=c99", "-O2", "-Wall", "-Wextra", "-Werror", "-D__HIP_PLATFORM_AMD__",
+           "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROCM, "include"), CCLIENT_SRC,
+           "-L" + os.path.dirname(OUT), "-lfbm_secagg", "-L" + os.path.join(ROCM, "lib"), "-lamdhip64",
+           "-Wl,-rpath,$ORIGIN/" + rel, "-Wl,-rpath," + os.path.join(ROCM, "lib"), "-o", tmp]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, CCLIENT_OUT)
+    return CCLIENT_OUT
+
+
 def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
     """`out` / `defines`: variant builds for A/B measurement (tools/ab.sh); the product is OUT.
     The host conversion module is optional: if it does not build (an interpreter whose headers
@@ -66,6 +90,7 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
         except (subprocess.CalledProcessError, OSError) as e:
             print(f"warning: {PYCONV_SRC} did not build ({e}); the list API falls back to Python conversions")
     if out == OUT and not defines and not force and not needs_build():
+        build_c_client(force, verbose)
         return OUT
     os.makedirs(os.path.dirname(out), exist_ok=True)
     tmp = out + ".tmp"
@@ -76,6 +101,8 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(tmp, out)
+    if out == OUT and not defines:
+        build_c_client(True, verbose)
     return out
 
 
