@@ -63,25 +63,6 @@ def mads_per_exp(key: int, mads: tuple) -> int:
     return sum(c * m for c, m in zip(products_per_exp(key), mads))
 
 
-def cgroup_cpu_quota():
-    """CPUs' worth of CPU time the process's cgroup allows (cgroup v2 cpu.max, v1 cfs quota / period),
-    or None when unlimited or unreadable."""
-    try:
-        with open("/sys/fs/cgroup/cpu.max") as fh:
-            q, per = fh.read().split()[:2]
-        return None if q == "max" else int(q) / int(per)
-    except (OSError, ValueError):
-        pass
-    try:
-        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
-            q = int(fh.read())
-        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
-            per = int(fh.read())
-        return None if q <= 0 else q / per
-    except (OSError, ValueError):
-        return None
-
-
 def committed_traffic(kernel: str, scheme: str, elements: int, n_ct=None):
     """(HBM bytes per launch of `kernel`, the profile file) from the committed rocprofv3 PMC summary
     of this workload -- same scheme and elements per GPU (JL: same ciphertexts per party) --
@@ -1053,8 +1034,8 @@ def main():
             avail = len(os.sched_getaffinity(0))  # the cores this process may run on
         except (AttributeError, OSError):
             avail = os.cpu_count() or 1
-        quota = cgroup_cpu_quota()  # the CPU time it may use (a cgroup limit: the box's CPU share)
-        share = max(1, min(avail, int(quota))) if quota else avail
+        quota = D.cgroup_cpu_quota()  # the CPU time it may use (a cgroup limit: the box's CPU share)
+        share = D.host_cpu_share()
         line["cpu_baseline"] = {"value": ns / tc, "unit": "params/s", "cores": 1, "kind": "port",
                                 "sample": f"{ns:,} elements x {P} parties, encrypt all + aggregate, "
                                           f"{tc:.1f} s on 1 host core (oracle/secagg_oracle.py; GMP mpz_powm "

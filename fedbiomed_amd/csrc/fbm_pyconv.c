@@ -21,6 +21,7 @@
  *   none_list(n)                    -> [None] * n (the output list that f64_into_list fills)
  *   float_pool(n)                   -> n fresh 0.0 floats: an output list made ahead, filled in place
  *   f64_into_list(list, offset, buf) -> list[offset:offset + len(buf)] = floats of the float64 buffer
+ *   set_conv_threads(t)             -> the threaded loops' default host-thread count (returns the old one)
  *
  * `out` is any writable C-contiguous buffer (a numpy array) of the exact size.  Host code,
  * not part of the GPU compute path: the arithmetic stays in the HIP library.
@@ -126,9 +127,22 @@ static void* fconv_range(void* arg) {
     return NULL;
 }
 
+/* Host threads of the threaded loops: FBM_CONV_THREADS when set, else the default the Python side
+ * sets once from the process's CPU share (its affinity, capped by a cgroup quota; at most 16,
+ * fedbiomed_amd/_device.py:host_cpu_share), else 8. */
+static long g_default_threads = 8;
+
+static PyObject* set_conv_threads(PyObject* self, PyObject* args) {
+    long t;
+    if (!PyArg_ParseTuple(args, "l", &t)) return NULL;
+    long old = g_default_threads;
+    g_default_threads = t < 1 ? 1 : t > 64 ? 64 : t;
+    return PyLong_FromLong(old);
+}
+
 static int conv_threads(Py_ssize_t n) {
     const char* e = getenv("FBM_CONV_THREADS");
-    long t = e ? strtol(e, NULL, 10) : 8;
+    long t = e ? strtol(e, NULL, 10) : g_default_threads;
     if (t < 1) t = 1;
     if (t > 64) t = 64;
     if (t > n / 1024) t = n / 1024 > 0 ? (long)(n / 1024) : 1;
@@ -176,8 +190,7 @@ static PyObject* floats_to_f64(PyObject* self, PyObject* args) {
  * freed under the readers, which read only the ints' digits (immutable; long_to_words touches no
  * interpreter state) -- no reference per item is needed.  (Round 4's form released the GIL and pinned
  * every item first: a reference taken and dropped on this thread, ~10 ns each, a third of the
- * conversion's own cost.)  FBM_CONV_THREADS overrides the thread count (default 8, the GPU box's CPU
- * share is 16). */
+ * conversion's own cost.)  Thread count: conv_threads above. */
 #define PAR_MIN_BYTES (1 << 20)
 
 typedef struct {
@@ -630,6 +643,8 @@ static PyMethodDef methods[] = {
     {"ints_to_bytes", ints_to_bytes, METH_VARARGS, "list of ints -> n-byte LE unsigned; -1 or first bad index"},
     {"bytes_to_ints", bytes_to_ints, METH_VARARGS, "buffer of n-byte LE unsigned values -> list of ints"},
     {"none_list", none_list, METH_VARARGS, "n -> [None] * n"},
+    {"set_conv_threads", set_conv_threads, METH_VARARGS,
+     "default host-thread count of the threaded loops (FBM_CONV_THREADS overrides it) -> the previous one"},
     {"float_pool", float_pool, METH_VARARGS, "n -> n distinct 0.0 floats held by the list only"},
     {"ints_to_bytes_held", ints_to_bytes_held, METH_VARARGS,
      "lists, lo, hi, n, out -> -1 or first bad flat index (host threads, GIL held, no pins)"},

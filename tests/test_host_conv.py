@@ -7,6 +7,7 @@ Python path (reduction mod N^2, numpy's errors).  CPU only.
 """
 
 import array
+import os
 import random
 
 import numpy as np
@@ -282,3 +283,22 @@ def test_float_pool_filled_in_place():
         m.f64_into_list(["x", 1.0], 0, np.array([1.0]))  # neither None nor a float
     with pytest.raises(ValueError):
         m.float_pool(-1)
+
+
+def test_default_threads_follow_the_cpu_share(monkeypatch):
+    """The threaded loops default to the process's CPU share (affinity capped by a cgroup quota), at
+    most 16; FBM_CONV_THREADS still overrides it per call."""
+    avail = len(os.sched_getaffinity(0))
+    monkeypatch.setattr(D, "cgroup_cpu_quota", lambda: 2.5)
+    assert D.host_cpu_share() == min(avail, 2)
+    monkeypatch.setattr(D, "cgroup_cpu_quota", lambda: None)
+    assert D.host_cpu_share() == avail
+    m = D._pyconv()
+    if m is D._PyConvFallback:
+        pytest.skip("C conversion module not built")
+    old = m.set_conv_threads(3)
+    try:
+        assert old == min(16, D.host_cpu_share())
+        assert m.set_conv_threads(0) == 3 and m.set_conv_threads(1000) == 1 and m.set_conv_threads(old) == 64
+    finally:
+        m.set_conv_threads(old)

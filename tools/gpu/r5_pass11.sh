@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${1:-r5s}
 mkdir -p $O
 cd $R
-python -c "import os, bench; print(\"cgroup quota\", bench.cgroup_cpu_quota(), \"affinity\", len(os.sched_getaffinity(0)))"
+python -c "import os; from fedbiomed_amd import _device as D; print(\"cgroup quota\", D.cgroup_cpu_quota(), \"affinity\", len(os.sched_getaffinity(0)))"
 timeout -k 10 300 python -u -m pytest tests/test_crypter_api.py -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest_crypter.txt 2>&1 || { echo "PYTEST FAILED"; tail -40 $O/pytest_crypter.txt; exit 1; }
 tail -2 $O/pytest_crypter.txt
 bash tools/rehearse_dist.sh ${1:-r5s} || exit 1

@@ -5,6 +5,7 @@ per call by csrc/fbm_pyconv.c), best of 3 calls each, with the conversion and th
 per thread count.
 
     python tools/list_agg_probe.py [--threads 4,8,16] [--elements 10000000] [--first-call plain|prepared]
+                                   [--prepare-each]
 """
 import argparse
 import json
@@ -22,6 +23,9 @@ def main():
     ap.add_argument("--elements", type=int, default=10_000_000)
     ap.add_argument("--first-call", choices=("plain", "prepared"), default=None,
                     help="time only the process's first aggregate, with or without prepare_aggregate before it")
+    ap.add_argument("--prepare-each", action="store_true",
+                    help="prepare_aggregate before every timed call (outside the clock, then a sync: the nodes' "
+                         "training time)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -65,6 +69,8 @@ def main():
         calls = []
         for _ in range(3):
             out = None  # the previous call's list is freed outside the clock
+            if args.prepare_each:
+                assert jc.prepare_aggregate(tau, P, sk0, W.BIPRIME0, n)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             out = jc.aggregate(tau, P, lists, sk0, W.BIPRIME0, tw, num_expected_params=n)
@@ -77,7 +83,7 @@ def main():
             lst = res_h.tolist()
             floats.append(time.perf_counter() - t0)
             del lst
-        print(json.dumps({"conv_threads": t, "elements": n, "parties": P, "aggregate_ms": 1000 * min(calls),
+        print(json.dumps({"conv_threads": t, "prepared": args.prepare_each, "elements": n, "parties": P, "aggregate_ms": 1000 * min(calls),
                           "aggregate_ms_all": [1000 * c for c in calls],
                           "params_per_s": n / min(calls), "conversion_alone_ms": 1000 * min(conv),
                           "float_list_alone_ms": 1000 * min(floats),
