@@ -798,7 +798,16 @@ def main():
             t0 = time.perf_counter()
             r = jc.encrypt(P, tau, xl0, keys[0], W.BIPRIME0, weight=weights[0])
             t_tot = time.perf_counter() - t0
-            del r
+            # the same call after SecaggCrypter.prepare_encrypt (an extension: H(t_k)^key issued with the
+            # training request, done while the node trains): one product per ciphertext instead of an
+            # exponentiation
+            prepared = jc.prepare_encrypt(tau, P, keys[0], W.BIPRIME0, ne)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r2 = jc.encrypt(P, tau, xl0, keys[0], W.BIPRIME0, weight=weights[0])
+            t_prep = time.perf_counter() - t0
+            same = r2 == r
+            del r, r2
             # the same call in its parts: list -> pinned f64 -> device | encrypt kernels | D2H -> ints
             t0 = time.perf_counter()
             x_d = D.floats_to_host(xl0).to(dev)
@@ -812,7 +821,9 @@ def main():
             del r
             return {"elements": ne, "ciphertexts": (ne + cr - 1) // cr, "ms": 1000 * t_tot, "params_per_s": ne / t_tot,
                     "host_in_ms": 1000 * (t1 - t0), "gpu_ms": 1000 * (t2 - t1), "host_out_ms": 1000 * (t3 - t2),
-                    "engine": D.jl_engine_for((ne + cr - 1) // cr)}
+                    "engine": D.jl_engine_for((ne + cr - 1) // cr),
+                    "factor_prepared": {"ms": 1000 * t_prep, "params_per_s": ne / t_prep, "prepared": prepared,
+                                        "equals_unprepared": same}}
 
         node_legs = {str(ne): node_encrypt(ne) for ne in args.node_list_n if ne <= n}
         n2 = W.BIPRIME0 * W.BIPRIME0
@@ -956,7 +967,9 @@ def main():
                                  "one process (a simulation artefact: each node encrypts on its own GPU)"},
             "node_encrypt_list_api": dict(node_legs, note=(
                 "one party's SecaggCrypter.encrypt(List[float]) -> List[int] (the node's call); host_in = list -> "
-                "pinned float64 -> H2D, gpu = the encrypt kernels, host_out = D2H + limbs -> Python ints")),
+                "pinned float64 -> H2D, gpu = the encrypt kernels, host_out = D2H + limbs -> Python ints; "
+                "factor_prepared: the call after SecaggCrypter.prepare_encrypt (an extension: the node's H(t_k)^key "
+                "issued with the training request, done while it trains)")),
             "researcher_aggregate_list_api": dict(
                 agg_l, at_metric_size=agg_full,
                 note="SecaggCrypter.aggregate(List[List[int]]) of the P parties' ciphertext lists (at_metric_size: "

@@ -841,8 +841,12 @@ def _check_round(tau: int) -> np.ndarray:
 
 def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, clip=None, target=None,
                weight: int = 1, slot: Optional[Tuple[int, int]] = None, ct_offset: int = 0,
-               defer_exp: bool = False, kind: Optional[str] = None, out: Optional[torch.Tensor] = None):
+               defer_exp: bool = False, kind: Optional[str] = None, out: Optional[torch.Tensor] = None,
+               factor: Optional[torch.Tensor] = None):
     """One party's JL ciphertexts as an int32 [n_ct, 64] tensor of 32-bit limbs.
+    `factor`: this party's H(t_k)^key for these ciphertexts computed ahead (jl_decrypt_factor with the
+    party's key, round and ct_offset): the encrypt is then (N pt + 1) F mod N^2 (fbm_jl_encrypt_factor),
+    bit for bit the exponentiation's; odd N >= 3 only.
     `out`: a contiguous int32 [n_ct, 64] device tensor to write them into (e.g. this party's row of the
     [P, n_ct, 64] block the aggregate takes), returned instead of a new one.
     `slot` overrides the (element_size, comp_ratio) packing.  `kind` selects a raw input:
@@ -881,6 +885,22 @@ def jl_encrypt(x: torch.Tensor, biprime: int, key: int, tau: int, n_users: int, 
     kl, kneg = _key_limbs(key)
     chunk = jl_chunk_ct()  # calls above the library's per-call cap run as ct_offset stripes
     ws = torch.empty(int(lib.fbm_jl_encrypt_workspace(min(n_ct, chunk))), dtype=torch.uint8, device=dev)
+    if factor is not None:
+        if defer_exp:
+            raise ValueError("an encrypt with its factor computed ahead has no exponentiation to defer")
+        if (factor.dtype != torch.int32 or tuple(factor.shape) != (n_ct, 64) or not factor.is_contiguous()
+                or factor.device != dev):
+            raise ValueError(f"factor must be the contiguous int32 ({n_ct}, 64) H(t_k)^key of these ciphertexts "
+                             f"on {dev}")
+        for k0 in range(0, n_ct, chunk):
+            k1 = min(n_ct, k0 + chunk)
+            xs = x[k0 * cr:min(n, k1 * cr)]
+            st = _stats(dev)
+            _call(lib.fbm_jl_encrypt_factor, _ptr(xs), xdt, xs.shape[0] if kind else xs.numel(), c, c2, tf, tm1,
+                  int(weight) & U64_MAX, es, cr, _np_ptr(bp), _ptr(factor[k0:k1]), _ptr(ct[k0:k1]), _ptr(ws),
+                  _ptr(st), _stream())
+            _check_stats_or_defer(st)
+        return ct
     if defer_exp:
         if n_ct > chunk:
             raise FedbiomedSecaggCrypterError(

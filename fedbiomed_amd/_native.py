@@ -29,7 +29,7 @@ def lib_path() -> str:
     return os.environ.get("FBM_LIB_PATH") or LIB_PATH
 
 
-ABI_VERSION = 4  # include/fbm_secagg.h FBM_ABI_VERSION
+ABI_VERSION = 5  # include/fbm_secagg.h FBM_ABI_VERSION
 TAU_LIMBS = 256  # FBM_TAU_LIMBS: the JL round's 32-bit words (< 2^8192)
 FBM_OK = 0
 FBM_E_ARG = -1
@@ -89,6 +89,8 @@ SIGNATURES = {
                                c_int, c_vp, c_u64, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_encrypt_phase": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_int, c_int, c_vp,
                                      c_vp, c_int, c_vp, c_u64, c_vp, c_vp, c_vp, c_vp, c_int]),
+    "fbm_jl_encrypt_factor": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_int, c_int, c_vp,
+                                      c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_aggregate": (c_int, [c_vp, c_int, c_u64, c_int, c_int, c_u64, c_vp, c_vp, c_int, c_vp, c_u64, c_u64,
                                  c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_decrypt_factor": (c_int, [c_u64, c_vp, c_vp, c_int, c_vp, c_u64, c_vp, c_vp, c_vp, c_vp]),

@@ -1357,6 +1357,79 @@ int fbm_jl_encrypt(const void* x, int x_dtype, uint64_t n, double clip, double t
                          key_negative, tau, ct_offset, ct_out, workspace, stats, stream, 3);
 }
 
+// The encrypt with its factor computed ahead: c_k = (N pt_k + 1) F_k mod N^2, F_k = H(t_k)^sk the
+// decryption-factor kernels' output for the party's key (fbm_jl_decrypt_factor) -- fbm_jl_encrypt's
+// ciphertexts bit for bit (the exponentiation's only input besides the plaintext is H(t_k)).  Any
+// engine policy; the modulus must be odd and >= 3 (other moduli: fbm_jl_encrypt).
+int fbm_jl_encrypt_factor(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
+                          uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,
+                          const uint32_t* factor, uint32_t* ct_out, void* workspace, uint32_t* stats, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int rc = zero_stats(stats, s);
+  if (rc) return rc;
+  QuantParams qp;
+  if ((rc = quant_params(clip, two_clip, target_f, target_m1, qp))) return rc;
+  if (x_dtype != FBM_F32 && x_dtype != FBM_F64 && x_dtype != FBM_U64 && x_dtype != FBM_U128 && x_dtype != FBM_PT) {
+    set_error("x_dtype must be FBM_F32, FBM_F64, FBM_U64, FBM_U128 or FBM_PT");
+    return FBM_E_ARG;
+  }
+  if ((x_dtype == FBM_U128 || x_dtype == FBM_PT) && weight != 1) {
+    set_error("raw-integer / plaintext inputs take weight 1");
+    return FBM_E_ARG;
+  }
+  if (x_dtype == FBM_PT && cr != 1) {
+    set_error("plaintext input (FBM_PT) takes cr = 1");
+    return FBM_E_ARG;
+  }
+  if (!biprime) {
+    set_error("null biprime");
+    return FBM_E_ARG;
+  }
+  if (n == 0) return FBM_OK;
+  if (cr < 1) {
+    set_error("invalid cr=%d", cr);
+    return FBM_E_ARG;
+  }
+  const uint64_t n_ct = (n + (uint64_t)cr - 1) / (uint64_t)cr;
+  if (n_ct > FBM_JL_MAX_CT) {
+    set_error("%llu ciphertexts exceed FBM_JL_MAX_CT per call; split the range with ct_offset",
+              (unsigned long long)n_ct);
+    return FBM_E_UNSUPPORTED;
+  }
+  if (!x || !factor || !ct_out || !workspace) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  if ((int64_t)weight <= -(int64_t)(1 << 17)) {
+    set_error("negative weight %lld outside (-2^17, 0)", (long long)(int64_t)weight);
+    return FBM_E_ARG;
+  }
+  if ((biprime[0] & 1u) == 0u || jl_is_one(biprime)) {
+    set_error("fbm_jl_encrypt_factor takes an odd N >= 3 (fbm_jl_encrypt takes any N)");
+    return FBM_E_UNSUPPORTED;
+  }
+  JlParams jp;
+  if ((rc = build_jl_params(biprime, es, cr, nullptr, 0, jp))) return rc;
+  JlSched none;
+  memset(&none, 0, sizeof(none));
+  uint8_t* ws = (uint8_t*)workspace;  // the encrypt workspace's ops | cst | pt
+  uint32_t* ops = (uint32_t*)ws;
+  uint32_t* cst = (uint32_t*)(ws + align256(FBM_OPS_WORDS * 4));
+  uint32_t* pt = (uint32_t*)(ws + align256(FBM_OPS_WORDS * 4) + align256(FBM_CST_WORDS * 4));
+  if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, none, ops, cst, s); }))) return rc;
+  {  // R^2 mod N^2: two products, each dropping one R
+    JlRk r;
+    jl_rk_for(jp.N32, 1, r);
+    if ((rc = timed("jl_rk", s, [&] { return launch_jl_rk(r, cst, s); }))) return rc;
+  }
+  if (x_dtype != FBM_PT &&
+      (rc = timed("jl_pack", s, [&] { return launch_jl_pack(x, x_dtype, n, qp, weight, es, cr, n_ct, pt, stats, s); })))
+    return rc;
+  const uint32_t* ptp = x_dtype == FBM_PT ? (const uint32_t*)x : pt;
+  const int negw = (int64_t)weight < 0 ? 1 : 0;
+  return timed("jl_encf", s, [&] { return launch_jl_encf(ptp, n_ct, jp, cst, negw, factor, ct_out, s); });
+}
+
 int fbm_jl_encrypt_phase(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
                          uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,
                          const uint32_t* key, int key_negative, const uint32_t* tau, uint64_t ct_offset, uint32_t* ct_out,

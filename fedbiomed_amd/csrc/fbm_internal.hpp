@@ -242,6 +242,8 @@ struct JlRk {  // R^(P+1) mod N^2, 28-bit limbs (jl_rk_kernel -> cst[FBM_CST_RK]
 };
 int launch_jl_rk(const JlRk& rk, uint32_t* cst, hipStream_t s);
 // x_k = (prod_u c_u * F_k mod N^2 - 1) div N   (cst[FBM_CST_RK] = R^(P+1) mod N^2)
+int launch_jl_encf(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, const uint32_t* cst, int negative,
+                   const uint32_t* factor, uint32_t* out, hipStream_t s);
 int launch_jl_prod(const uint32_t* cts, int n_parties, uint64_t n_ct, const JlParams& jp, const uint32_t* cst,
                    const uint32_t* factor, uint32_t* xout, hipStream_t s);
 #define FBM_EXP_DEC 1        // jl_exp mode bits: plain power (no nude product)

@@ -7,6 +7,8 @@
 //   jl_fdh_kernel    FDH.H(t_k), t_k = (k<<512)|tau       (_jls.py:451-467,727-762)
 //   jl_exp_kernel    H^sk mod N^2 (GMP mpz_powm via gmpy2, _jls.py:60-73,500-501) and
 //                    the final product with nude           (_jls.py:502)
+// Encrypt with its factor computed ahead (fbm_jl_encrypt_factor):  pack -> encf
+//   jl_encf_kernel   (N*pt + 1) * F mod N^2, F = H^sk from the aggregate's factor kernels
 // Aggregate:  fdh -> exp(DEC, digits out) -> inv -> lift -> prod -> decode
 //   jl_exp_kernel    H^|sk0| mod N^2 as N-adic digits     (_jls.py:550-551)
 //   jl_inv_modn_kernel, jl_lift_kernel
@@ -1712,6 +1714,86 @@ __global__ void __launch_bounds__(FBM_BLOCK, 1) jl_prod_kernel(const uint32_t* _
 }
 
 // ------------------------------------------------------------------------------------
+// encrypt with its factor computed ahead (fbm_jl_encrypt_factor, UserKey.encrypt, _jls.py:473-505):
+//   c = (N pt + 1) F mod N^2,  F = H(t_k)^sk mod N^2 (jl_factor: the decryption factor's
+// kernels with the party's key, run before the plaintext exists), the exponentiation's encrypt
+// bit for bit.  Two Montgomery products mod M = N^2 from a = R^2 (jl_rk_kernel), as jl_prod_kernel:
+//   b = N pt + 1 (formed in registers: pt < 2^1024, N < 2^1024, so b < 2^2048 qualifies)  -> R b
+//   b = F                                                                           -> b F mod M
+// A negative weight (pt = |pt|, see jl_pack_kernel) encrypts 1 - N |pt|: b = N |pt| - 1, and
+// the product is negated mod M at the end ((1 - N |pt|) F = -(N |pt| - 1) F); |pt| = 0 is 1.
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(FBM_BLOCK, 1) jl_encf_kernel(const uint32_t* __restrict__ pt, uint64_t n_ct,
+                                                              const uint32_t* __restrict__ cst, JlParams jp,
+                                                              int negative, const uint32_t* __restrict__ factor,
+                                                              uint32_t* __restrict__ out) {
+  __shared__ uint32_t lds_a[(FBM_NL + 1) * FBM_BLOCK];
+  __shared__ uint32_t lds_b[(FBM_NL + 1) * FBM_BLOCK];
+  const int tid = threadIdx.x;
+  uint32_t* lds = lds_a + tid;
+  const uint32_t aoff = lds_addr(lds), boff = lds_addr(lds_b + tid);
+  const uint32_t* M = cst + FBM_CST_M;
+  const uint64_t ct_raw = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
+  const bool valid = ct_raw < n_ct;  // no early return: every lane runs the products
+  const uint64_t ct = valid ? ct_raw : n_ct - 1;
+  lds_store_uniform<FBM_NL>(lds, FBM_BLOCK, cst + FBM_CST_RK);
+  bool neg;
+  {
+    uint32_t p[32], b[64], b28[FBM_NL];
+    load_row32(reinterpret_cast<const uint4*>(pt + ct * 32), p);
+    uint32_t any = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) any |= p[i];
+    neg = negative && any;
+    mul1024(p, jp.N32, b);  // N |pt| <= (2^1024 - 1)^2
+    if (neg) {  // N |pt| - 1: N |pt| >= N >= 3, no borrow out
+      uint32_t br = 1;
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const uint64_t d = (uint64_t)b[i] - br;
+        b[i] = (uint32_t)d;
+        br = (uint32_t)(d >> 63);
+      }
+    } else {  // N pt + 1 < 2^2048: no carry out
+      uint32_t c = 1;
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const uint64_t t = (uint64_t)b[i] + c;
+        b[i] = (uint32_t)t;
+        c = (uint32_t)(t >> 32);
+      }
+    }
+    to28<64, FBM_NL>(b, b28);
+    lds_store_col(lds_b + tid, FBM_BLOCK, b28);
+  }
+  fbm_mm_lds(aoff, boff, M, jp.mc.mp);  // a = R b
+  {
+    uint32_t c32[64], c28[FBM_NL];
+    load_row64(factor + ct * 64, c32);
+    to28<64, FBM_NL>(c32, c28);
+    lds_store_col(lds_b + tid, FBM_BLOCK, c28);
+  }
+  fbm_mm_lds(aoff, boff, M, jp.mc.mp);  // a = b F (lazy)
+  uint32_t v[FBM_NL], D[64];
+  lds_load_col(lds, FBM_BLOCK, v);
+  mont_csub(v, jp.mc.M);
+  uint32_t nz = 0;
+#pragma unroll
+  for (int k = 0; k < FBM_NL; ++k) nz |= v[k];
+  if (neg && nz) {  // M - v, v in (0, M)
+    int32_t br = 0;
+#pragma unroll
+    for (int k = 0; k < FBM_NL; ++k) {
+      const int32_t d = (int32_t)jp.mc.M[k] - (int32_t)v[k] + br;
+      v[k] = (uint32_t)d & FBM_LMASK;
+      br = d >> FBM_LB;
+    }
+  }
+  from28<FBM_NL, 64>(v, D);
+  if (valid) store_row64(out + ct * 64, D);
+}
+
+// ------------------------------------------------------------------------------------
 // inverse mod N^2 from N-adic digits: y = e0^-1 mod N (Bernstein-Yang divsteps), then
 // one N-adic lift step (jl_lift_kernel).  e = H^|sk0| mod N^2 (the factor) or H (a
 // negative-key encrypt).
@@ -2343,6 +2425,14 @@ int jl_batch_flush(void* workspace, uint64_t ws_bytes, hipStream_t s) {
                      (uint32_t*)g_batch.cst, g_batch.np, (const uint32_t*)nullptr, 0, 0, 0, 0, -1, (const uint32_t*)nullptr,
                      table, (uint32_t*)nullptr, (const JlExpSeg*)segs, bt.nseg, bt.total_chunks, ctr, (const uint32_t*)nullptr);
   return check_launch("jl_exp_kernel (batch)");
+}
+
+int launch_jl_encf(const uint32_t* pt, uint64_t n_ct, const JlParams& jp, const uint32_t* cst, int negative,
+                   const uint32_t* factor, uint32_t* out, hipStream_t s) {
+  if (n_ct == 0) return FBM_OK;
+  hipLaunchKernelGGL(jl_encf_kernel, grid1(n_ct, FBM_BLOCK), dim3(FBM_BLOCK), 0, s, pt, n_ct, cst, jp, negative, factor,
+                     out);
+  return check_launch("jl_encf_kernel");
 }
 
 int launch_jl_prod(const uint32_t* cts, int n_parties, uint64_t n_ct, const JlParams& jp, const uint32_t* cst,

@@ -107,8 +107,11 @@ class SecaggCrypter:
     def encrypt_tensor(self, num_nodes: int, current_round: int, params: torch.Tensor, key: int, biprime: int,
                        clipping_range: Union[int, None] = None, weight: Optional[int] = None,
                        target_range: Optional[int] = None, ct_offset: int = 0, defer_exp: bool = False,
-                       out: Optional[torch.Tensor] = None):
+                       out: Optional[torch.Tensor] = None, factor: Optional[torch.Tensor] = None):
         """Device tensor (f32/f64) in HBM -> int32 [n_ct, 64] ciphertext limbs in HBM.
+        `factor`: this party's H(t_k)^key of these ciphertexts computed ahead (`decrypt_factor_tensor` with
+        the party's key, round and ct_offset; `prepare_encrypt` issues it for the list API): the encrypt is
+        then one product per ciphertext instead of an exponentiation, with the same ciphertexts.
         `ct_offset`: global index of this shard's first ciphertext (element-range sharding).
         `out`: an int32 [n_ct, 64] destination (e.g. this party's row of the [P, n_ct, 64] block
         aggregate_tensor takes), as SecaggLomCrypter.encrypt_tensor's.
@@ -122,7 +125,7 @@ class SecaggCrypter:
         try:
             return D.jl_encrypt(params, biprime, key, current_round, num_nodes, clip=clipping_range,
                                 target=target_range, weight=1 if weight is None else weight, ct_offset=ct_offset,
-                                defer_exp=defer_exp, out=out)
+                                defer_exp=defer_exp, out=out, factor=factor)
         except (TypeError, ValueError) as exp:
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value} Error during parameter encryption. {exp}") from exp
@@ -177,8 +180,15 @@ class SecaggCrypter:
                 f"{ErrorNumbers.FB624.value} Error during parameter encryption. {exp}") from exp
         dev = D.device()
         x = host.to(dev)
-        stripes = D.list_encrypt_stripes((x.numel() + cr - 1) // cr, dev)
-        if len(stripes) == 1:
+        n_ct = (x.numel() + cr - 1) // cr
+        factor = self._take_prepared_encrypt(current_round, num_nodes, key, biprime, target_range, n_ct, dev)
+        stripes = D.list_encrypt_stripes(n_ct, dev) if factor is None else [(0, n_ct)]
+        if factor is not None:  # prepare_encrypt's factor: one product per ciphertext, no exponentiation
+            ct = self.encrypt_tensor(num_nodes, current_round, x, key, biprime, clipping_range, weight, target_range,
+                                     factor=factor)
+            packed = D.to_host(ct).numpy().view(np.uint32)
+            out = D.limbs_to_ints(packed)
+        elif len(stripes) == 1:
             ct = self.encrypt_tensor(num_nodes, current_round, x, key, biprime, clipping_range, weight, target_range)
             packed = D.to_host(ct).numpy().view(np.uint32)
             out = D.limbs_to_ints(packed)
@@ -218,6 +228,68 @@ class SecaggCrypter:
                 ev.synchronize()
                 out += D.limbs_to_ints(packed[c0:c1])
         return packed, out
+
+    def prepare_encrypt(self, current_round: int, num_nodes: int, key: int, biprime: int, num_params: int,
+                        target_range: Optional[int] = None) -> bool:
+        """Extension (not in the reference): issue a coming `encrypt`'s exponentiations now.  A node's
+        ciphertext is c_k = (N pt_k + 1) H(t_k)^key mod N^2 (UserKey.encrypt, `_jls.py:473-505`); the
+        factor H(t_k)^key depends only on the round, the node's key, the biprime and the vector's size,
+        all known when the training request arrives (`node/secagg/_secagg_round.py`), so it can run on
+        a side stream while the node trains.  The next `encrypt` of the same round, node count, key,
+        biprime, target range and ciphertext count takes it (once) and only multiplies: the same
+        ciphertexts, bit for bit.  Other calls of that round leave it, a call of another round drops
+        it; a device condition of the early work is raised by the encrypt that takes it.  It also warms
+        the encrypt's pinned staging buffers.  Best effort: False (nothing prepared) where the encrypt
+        would refuse the arguments, for an even N or N = 1, or with a library older than ABI 5.  The
+        key itself is not kept, only a SHA-256 tag of it."""
+        self._prepared_enc = None
+        try:
+            if not all(isinstance(v, int) for v in (current_round, num_nodes, key, biprime, num_params)):
+                return False
+            if num_nodes < 1 or biprime < 3 or biprime % 2 == 0:
+                return False
+            _, cr = D.jl_slot(target_range or SAParameters.TARGET_RANGE, num_nodes)
+            n_ct = -(-num_params // cr)
+            if n_ct <= 0:
+                return False
+            dev = D.device()
+            from .. import _native as N
+
+            if (N.loaded_abi or 0) < 5:
+                return False
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side), D.capture_checks() as checks:
+                factor = self.decrypt_factor_tensor(current_round, n_ct, key, biprime)
+            ev = torch.cuda.Event()
+            ev.record(side)
+            warm = [D.host_empty((num_params,), torch.float64), D.host_empty((n_ct, 64), torch.int32)]
+            del warm
+        except Exception:  # noqa: BLE001 -- encrypt raises whatever it is, in the reference's order
+            return False
+        self._prepared_enc = {"round": current_round,
+                              "tag": _prep_tag(current_round, num_nodes, key, biprime, target_range),
+                              "n_ct": n_ct, "factor": factor, "event": ev, "checks": checks.pending}
+        return True
+
+    def _take_prepared_encrypt(self, current_round, num_nodes, key, biprime, target_range, n_ct, dev):
+        """prepare_encrypt's factor when it is this call's (waited for on the current stream, its status
+        words adopted; the preparation is then spent), else None.  A call of another round drops it."""
+        prep = getattr(self, "_prepared_enc", None)
+        if prep is None:
+            return None
+        if prep["round"] != current_round:
+            self._prepared_enc = None
+            return None
+        tag = _prep_tag(current_round, num_nodes, key, biprime, target_range)
+        if prep["n_ct"] != n_ct or tag is None or prep["tag"] != tag:
+            return None
+        self._prepared_enc = None
+        main = torch.cuda.current_stream(dev)
+        main.wait_event(prep["event"])
+        prep["factor"].record_stream(main)
+        D.adopt_checks(prep["checks"])
+        return prep["factor"]
 
     def prepare_aggregate(self, current_round: int, num_nodes: int, key: int, biprime: int,
                           num_expected_params: int, target_range: Optional[int] = None) -> bool:

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FBM_ABI_VERSION 4 /* 4: fbm_ves_pack takes is_signed; 3: the JL round is an 8192-bit value (FBM_TAU_LIMBS limbs);
+#define FBM_ABI_VERSION 5 /* 5: fbm_jl_encrypt_factor; 4: fbm_ves_pack takes is_signed; 3: the JL round is an 8192-bit value (FBM_TAU_LIMBS limbs);
                              2 took 16 limbs, 1 a uint64 */
 /* The JL round `tau` of every JL entry point: a HOST pointer to FBM_TAU_LIMBS little-endian 32-bit
  * words, any round below 2^8192 -- FDH.H hashes t = (k << 512) | tau as t.to_bytes(1024, 'big')
@@ -150,6 +150,16 @@ int fbm_jl_encrypt_phase(const void* x, int x_dtype, uint64_t n, double clip, do
                          uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,
                          const uint32_t* key, int key_negative, const uint32_t* tau, uint64_t ct_offset, uint32_t* ct_out,
                          void* workspace, uint32_t* stats, void* stream, int phase);
+
+/* fbm_jl_encrypt with its factor computed ahead: c_k = (N pt_k + 1) F_k mod N^2, where F is
+ * fbm_jl_decrypt_factor(n_ct, biprime, key, key_negative, tau, ct_offset, ...) for the PARTY's key --
+ * H(t_k)^sk needs no plaintext, so a node can compute it while it trains.  Equal bit for bit to
+ * fbm_jl_encrypt of the same key, round and ct_offset (UserKey.encrypt, _jls.py:473-505).
+ *   factor: device, n_ct x 64 uint32 limbs;  workspace: fbm_jl_encrypt_workspace(n_ct) bytes.
+ * An even N or N = 1 is FBM_E_UNSUPPORTED (fbm_jl_encrypt takes every N).                    */
+int fbm_jl_encrypt_factor(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
+                          uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,
+                          const uint32_t* factor, uint32_t* ct_out, void* workspace, uint32_t* stats, void* stream);
 
 /* JL aggregate: prod_u c_u * H(t_k)^sk0 mod N^2, x = ((v-1)//N) mod N, VES decode,
  * average, dequantise.  Replaces SecaggCrypter.aggregate (_secagg_crypter.py:139-230) =

@@ -1,0 +1,145 @@
+"""The encrypt with its factor computed ahead (fbm_jl_encrypt_factor, SecaggCrypter.prepare_encrypt -- an
+extension): c_k = (N pt_k + 1) F_k mod N^2 with F = H(t_k)^key from the decryption-factor kernels, against
+the exponentiation's encrypt (fbm_jl_encrypt) bit for bit and against the oracle (oracle/secagg_oracle.py,
+pinned by tests/golden/): both key signs and key 0, negative / zero / large weights, clipping and target
+ranges, ct_offset stripes, the object API's raw-integer and plaintext inputs; then the list API's
+preparation life cycle (taken once, left by another call of its round, dropped by another round, refused
+where it cannot apply).  The CPU part: prepare_encrypt without a device prepares nothing."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from fedbiomed_amd import _device as D, workload as W
+
+
+def test_prepare_encrypt_without_device_prepares_nothing():
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    if torch.cuda.is_available():
+        return
+    jc = SecaggCrypter()
+    assert jc.prepare_encrypt(3, 2, 5, W.BIPRIME0, 100) is False
+    assert getattr(jc, "_prepared_enc", None) is None
+
+
+CASES = [  # (parties, n, key, weight, clip, target, ct_offset)
+    (4, 3001, "user", 1, None, None, 0),
+    (4, 3001, "user", 37, 3, 2**16, 0),
+    (8, 4097, "neg", 2**17 - 1, None, None, 0),
+    (3, 700, "user", -5, None, None, 0),      # a negative weight: (1 - N |pt|) F
+    (3, 700, "neg", -(2**17 - 1), 1, 2**20, 0),
+    (5, 999, "zero", 3, None, None, 0),       # key 0: F = 1
+    (6, 2500, "user", 11, None, None, 1234),  # a stripe of a sharded vector
+    (2, 1, "user", 1, None, None, 0),
+]
+
+
+def _key(kind, rng):
+    return {"user": rng.getrandbits(2040), "neg": -rng.getrandbits(2043), "zero": 0}[kind]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES)
+def test_encrypt_with_factor_equals_exponentiation(case):
+    from oracle import secagg_oracle as O
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    P, n, kind, w, clip, target, k0 = case
+    rng = random.Random(4100 + CASES.index(case))
+    key, tau = _key(kind, rng), rng.getrandbits(64)
+    scale = (clip or 3) * 1.3
+    xs = [rng.uniform(-scale, scale) for _ in range(n)]
+    xs[0] = 0.0  # a zero element (its slot's q is the clipping floor's quantisation)
+    x = torch.tensor(xs, dtype=torch.float64, device=D.device())
+    jc = SecaggCrypter()
+    _, cr = D.jl_slot(target or None, P)
+    n_ct = -(-n // cr)
+    plain = jc.encrypt_tensor(P, tau, x, key, W.BIPRIME0, clip, w, target, ct_offset=k0)
+    F = jc.decrypt_factor_tensor(tau, n_ct, key, W.BIPRIME0, ct_offset=k0)
+    got = jc.encrypt_tensor(P, tau, x, key, W.BIPRIME0, clip, w, target, ct_offset=k0, factor=F)
+    assert torch.equal(got, plain), case
+    if k0 == 0 and n <= 1000:
+        ref = O.jl_encrypt(xs, tau, key, W.BIPRIME0, P, clip=clip, weight=w, target=target)
+        assert D.limbs_to_ints(D.to_host(got).numpy().view(np.uint32)) == ref, case
+
+
+@pytest.mark.gpu
+def test_encrypt_with_factor_raw_inputs():
+    """The object API's inputs: VES-packed raw integers (FBM_U128, JoyeLibert.protect) and ready
+    plaintexts (FBM_PT, UserKey.encrypt)."""
+    rng = random.Random(77)
+    key, tau = rng.getrandbits(2040), 9
+    vals = torch.tensor([[rng.getrandbits(40), 0] for _ in range(300)], dtype=torch.int64, device=D.device())
+    slot = (47, 21)
+    n_ct = -(-300 // 21)
+    F = D.jl_decrypt_factor(n_ct, W.BIPRIME0, key, tau)
+    a = D.jl_encrypt(vals, W.BIPRIME0, key, tau, 3, slot=slot, kind="u128")
+    b = D.jl_encrypt(vals, W.BIPRIME0, key, tau, 3, slot=slot, kind="u128", factor=F)
+    assert torch.equal(a, b)
+    pts = torch.from_numpy(np.stack([D.int_limbs(rng.getrandbits(1023), 32) for _ in range(50)]).view(np.int32))
+    pts = pts.to(D.device())
+    F = D.jl_decrypt_factor(50, W.BIPRIME0, -key, tau)
+    a = D.jl_encrypt(pts, W.BIPRIME0, -key, tau, 3, kind="pt")
+    b = D.jl_encrypt(pts, W.BIPRIME0, -key, tau, 3, kind="pt", factor=F)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_encrypt_with_factor_refuses_what_it_cannot_do():
+    from fedbiomed_amd.exceptions import FedbiomedSecaggCrypterError
+
+    x = torch.zeros(64, dtype=torch.float64, device=D.device())
+    _, cr = D.jl_slot(None, 2)
+    n_ct = -(-64 // cr)
+    F = D.jl_decrypt_factor(n_ct, W.BIPRIME0, 5, 1)
+    with pytest.raises(ValueError):  # a factor of another shape
+        D.jl_encrypt(x, W.BIPRIME0, 5, 1, 2, factor=F[:-1] if n_ct > 1 else F.repeat(2, 1))
+    with pytest.raises(ValueError):  # nothing to defer
+        D.jl_encrypt(x, W.BIPRIME0, 5, 1, 2, factor=F, defer_exp=True)
+    even = W.BIPRIME0 + 1
+    Fe = D.jl_decrypt_factor(n_ct, even, 5, 1)
+    with pytest.raises(FedbiomedSecaggCrypterError):  # FBM_E_UNSUPPORTED: fbm_jl_encrypt takes even moduli
+        D.jl_encrypt(x, even, 5, 1, 2, factor=Fe)
+
+
+@pytest.mark.gpu
+def test_prepare_encrypt_life_cycle(monkeypatch):
+    """prepare_encrypt: the next encrypt of the same round / node count / key / biprime / target range / size
+    takes the factor, once, with the ciphertexts of an unprepared call (striped or not); another call of the
+    round leaves it, a call of another round drops it; what it cannot serve prepares nothing."""
+    from oracle import secagg_oracle as O
+    from fedbiomed_amd.secagg import SecaggCrypter
+
+    P, tau, n = 4, 6, 20_011
+    key = W.jl_user_key(1)
+    xs = [float(v) for v in W.party_params(1, n)]
+    jc = SecaggCrypter()
+    for rnd in (None, "200"):  # one stripe / the list encrypt's ct_offset stripes
+        if rnd is None:
+            monkeypatch.delenv("FBM_ONE_LANE_ROUND", raising=False)
+        else:
+            monkeypatch.setenv("FBM_ONE_LANE_ROUND", rnd)
+        ref = jc.encrypt(P, tau, xs, key, W.BIPRIME0, weight=3)
+        assert jc.prepare_encrypt(tau, P, key, W.BIPRIME0, n) is True
+        assert jc._prepared_enc is not None
+        assert jc.encrypt(P, tau, xs, key, W.BIPRIME0, weight=3) == ref, rnd
+        assert jc._prepared_enc is None  # spent
+        # same round, another key / size / node count: ignored and kept
+        for other in ((tau, P, key + 1, W.BIPRIME0, n), (tau, P, key, W.BIPRIME0, n + 5000),
+                      (tau, P + 1, key, W.BIPRIME0, n)):
+            assert jc.prepare_encrypt(*other) is True
+            assert jc.encrypt(P, tau, xs, key, W.BIPRIME0, weight=3) == ref, other
+            assert jc._prepared_enc is not None
+        assert jc.prepare_encrypt(tau + 1, P, key, W.BIPRIME0, n) is True  # dropped by this round's call
+        assert jc.encrypt(P, tau, xs, key, W.BIPRIME0, weight=3) == ref
+        assert jc._prepared_enc is None
+    small = xs[:500]
+    assert jc.prepare_encrypt(tau, P, key, W.BIPRIME0, len(small), target_range=2**20) is True
+    got = jc.encrypt(P, tau, small, key, W.BIPRIME0, clipping_range=5, weight=2, target_range=2**20)
+    assert jc._prepared_enc is None
+    assert got == O.jl_encrypt(small, tau, key, W.BIPRIME0, P, clip=5, weight=2, target=2**20)
+    for bad in ((tau, P, 1.5, W.BIPRIME0, n), (tau, P, key, W.BIPRIME0, 0), (tau, 0, key, W.BIPRIME0, n),
+                (tau, P, key, "N", n), (tau, P, key, W.BIPRIME0 + 1, n), (tau, P, key, 1, n)):
+        assert jc.prepare_encrypt(*bad) is False, bad

@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol(lib):
     for s in declared_symbols():
         assert hasattr(lib, s), f"missing export {s}"
         assert s in _native.SIGNATURES, f"no ctypes signature for {s}"
-    assert lib.fbm_abi_version() == _native.ABI_VERSION == 4
+    assert lib.fbm_abi_version() == _native.ABI_VERSION == 5
 
 
 def test_check_stats_lom_guard(lib):
@@ -243,16 +243,18 @@ def _load_in_child(env_extra):
 def test_lib_path_override_alone_is_strict(tmp_path):
     """FBM_LIB_PATH alone: the override is loaded under the shipped checks -- a library missing
     entry points is NativeUnavailable at load(), not an AttributeError at first use."""
-    out = _load_in_child({"FBM_LIB_PATH": _stub_lib(tmp_path, 4)})
+    from fedbiomed_amd import _native as N
+    out = _load_in_child({"FBM_LIB_PATH": _stub_lib(tmp_path, N.ABI_VERSION)})
     assert out.startswith("REFUSED") and "lacks" in out, out
-    out = _load_in_child({"FBM_LIB_PATH": _stub_lib(tmp_path, 3)})
+    out = _load_in_child({"FBM_LIB_PATH": _stub_lib(tmp_path, N.ABI_VERSION - 1)})
     assert out.startswith("REFUSED"), out
 
 
 def test_lib_path_override_relaxed_only_for_ab_variants(tmp_path):
-    out = _load_in_child({"FBM_LIB_PATH": _stub_lib(tmp_path, 3), "FBM_AB_VARIANT": "1"})
-    assert out == "LOADED 3", out
-    out = _load_in_child({"FBM_LIB_PATH": _stub_lib(tmp_path, 2), "FBM_AB_VARIANT": "1"})
+    from fedbiomed_amd import _native as N
+    out = _load_in_child({"FBM_LIB_PATH": _stub_lib(tmp_path, N.ABI_VERSION - 1), "FBM_AB_VARIANT": "1"})
+    assert out == f"LOADED {N.ABI_VERSION - 1}", out
+    out = _load_in_child({"FBM_LIB_PATH": _stub_lib(tmp_path, N.ABI_VERSION - 2), "FBM_AB_VARIANT": "1"})
     assert out.startswith("REFUSED") and "ABI version mismatch" in out, out
 
 
