@@ -89,6 +89,10 @@ def _prep_tag(current_round, num_nodes, key, biprime, target_range) -> Optional[
 class SecaggCrypter:
     """Joye-Libert secure aggregation (encrypt on nodes, aggregate on the researcher)."""
 
+    # prepare_encrypt's factor, held by the class: the node makes a SecaggCrypter per encrypt call
+    # (`node/secagg/_secagg_round.py:139-157`), so the call that takes it is another instance's
+    _enc_prep = None
+
     @staticmethod
     def _setup_public_param(biprime: int) -> PublicParam:
         """reference _secagg_crypter.py:28-43: N = biprime, bits 1024, FDH(2048, N^2).H (the
@@ -241,8 +245,9 @@ class SecaggCrypter:
         it; a device condition of the early work is raised by the encrypt that takes it.  It also warms
         the encrypt's pinned staging buffers.  Best effort: False (nothing prepared) where the encrypt
         would refuse the arguments, for an even N or N = 1, or with a library older than ABI 5.  The
-        key itself is not kept, only a SHA-256 tag of it."""
-        self._prepared_enc = None
+        key itself is not kept, only a SHA-256 tag of it.  The preparation is the class's, not this
+        instance's (one at a time): the node's encrypt runs on a fresh SecaggCrypter."""
+        SecaggCrypter._enc_prep = None
         try:
             if not all(isinstance(v, int) for v in (current_round, num_nodes, key, biprime, num_params)):
                 return False
@@ -267,24 +272,24 @@ class SecaggCrypter:
             del warm
         except Exception:  # noqa: BLE001 -- encrypt raises whatever it is, in the reference's order
             return False
-        self._prepared_enc = {"round": current_round,
-                              "tag": _prep_tag(current_round, num_nodes, key, biprime, target_range),
-                              "n_ct": n_ct, "factor": factor, "event": ev, "checks": checks.pending}
+        SecaggCrypter._enc_prep = {"round": current_round,
+                                   "tag": _prep_tag(current_round, num_nodes, key, biprime, target_range),
+                                   "n_ct": n_ct, "factor": factor, "event": ev, "checks": checks.pending}
         return True
 
     def _take_prepared_encrypt(self, current_round, num_nodes, key, biprime, target_range, n_ct, dev):
         """prepare_encrypt's factor when it is this call's (waited for on the current stream, its status
         words adopted; the preparation is then spent), else None.  A call of another round drops it."""
-        prep = getattr(self, "_prepared_enc", None)
+        prep = SecaggCrypter._enc_prep
         if prep is None:
             return None
         if prep["round"] != current_round:
-            self._prepared_enc = None
+            SecaggCrypter._enc_prep = None
             return None
         tag = _prep_tag(current_round, num_nodes, key, biprime, target_range)
         if prep["n_ct"] != n_ct or tag is None or prep["tag"] != tag:
             return None
-        self._prepared_enc = None
+        SecaggCrypter._enc_prep = None
         main = torch.cuda.current_stream(dev)
         main.wait_event(prep["event"])
         prep["factor"].record_stream(main)

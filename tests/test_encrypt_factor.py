@@ -21,7 +21,7 @@ def test_prepare_encrypt_without_device_prepares_nothing():
         return
     jc = SecaggCrypter()
     assert jc.prepare_encrypt(3, 2, 5, W.BIPRIME0, 100) is False
-    assert getattr(jc, "_prepared_enc", None) is None
+    assert SecaggCrypter._enc_prep is None
 
 
 CASES = [  # (parties, n, key, weight, clip, target, ct_offset)
@@ -123,22 +123,26 @@ def test_prepare_encrypt_life_cycle(monkeypatch):
             monkeypatch.setenv("FBM_ONE_LANE_ROUND", rnd)
         ref = jc.encrypt(P, tau, xs, key, W.BIPRIME0, weight=3)
         assert jc.prepare_encrypt(tau, P, key, W.BIPRIME0, n) is True
-        assert jc._prepared_enc is not None
+        assert SecaggCrypter._enc_prep is not None
         assert jc.encrypt(P, tau, xs, key, W.BIPRIME0, weight=3) == ref, rnd
-        assert jc._prepared_enc is None  # spent
+        assert SecaggCrypter._enc_prep is None  # spent
         # same round, another key / size / node count: ignored and kept
         for other in ((tau, P, key + 1, W.BIPRIME0, n), (tau, P, key, W.BIPRIME0, n + 5000),
                       (tau, P + 1, key, W.BIPRIME0, n)):
             assert jc.prepare_encrypt(*other) is True
             assert jc.encrypt(P, tau, xs, key, W.BIPRIME0, weight=3) == ref, other
-            assert jc._prepared_enc is not None
+            assert SecaggCrypter._enc_prep is not None
         assert jc.prepare_encrypt(tau + 1, P, key, W.BIPRIME0, n) is True  # dropped by this round's call
         assert jc.encrypt(P, tau, xs, key, W.BIPRIME0, weight=3) == ref
-        assert jc._prepared_enc is None
+        assert SecaggCrypter._enc_prep is None
+    # the node's flow (node/secagg/_secagg_round.py:139-157): a fresh SecaggCrypter per encrypt call
+    assert SecaggCrypter().prepare_encrypt(tau, P, key, W.BIPRIME0, n) is True
+    assert SecaggCrypter().encrypt(P, tau, xs, key, W.BIPRIME0, weight=3) == ref
+    assert SecaggCrypter._enc_prep is None
     small = xs[:500]
     assert jc.prepare_encrypt(tau, P, key, W.BIPRIME0, len(small), target_range=2**20) is True
     got = jc.encrypt(P, tau, small, key, W.BIPRIME0, clipping_range=5, weight=2, target_range=2**20)
-    assert jc._prepared_enc is None
+    assert SecaggCrypter._enc_prep is None
     assert got == O.jl_encrypt(small, tau, key, W.BIPRIME0, P, clip=5, weight=2, target=2**20)
     for bad in ((tau, P, 1.5, W.BIPRIME0, n), (tau, P, key, W.BIPRIME0, 0), (tau, 0, key, W.BIPRIME0, n),
                 (tau, P, key, "N", n), (tau, P, key, W.BIPRIME0 + 1, n), (tau, P, key, 1, n)):
