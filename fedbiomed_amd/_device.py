@@ -502,6 +502,19 @@ def f64_into_list(lst: list, off: int, values: np.ndarray) -> None:
     _pyconv().f64_into_list(lst, off, np.ascontiguousarray(values, dtype=np.float64))
 
 
+def int_pool(n: int) -> Optional[list]:
+    """n ciphertext-sized ints made ahead (prepare_encrypt's output list; limbs_into_pool writes their
+    values in place), or None where the C module cannot make them (not built, or CPython >= 3.12)."""
+    m = _pyconv()
+    return None if m is _PyConvFallback else m.int_pool(n, 256)
+
+
+def limbs_into_pool(pool: list, arr: np.ndarray) -> list:
+    """int_pool's ints take the [n, 64] uint32 limb rows' values in place (host threads); the pool."""
+    _pyconv().words_into_pool(pool, np.ascontiguousarray(arr, dtype=np.uint32), 256)
+    return pool
+
+
 def limbs_to_ints(arr: np.ndarray) -> List[int]:
     return _pyconv().bytes_to_ints(np.ascontiguousarray(arr, dtype=np.uint32), 256)
 

@@ -22,6 +22,8 @@
  *   float_pool(n)                   -> n fresh 0.0 floats: an output list made ahead, filled in place
  *   f64_into_list(list, offset, buf) -> list[offset:offset + len(buf)] = floats of the float64 buffer
  *   set_conv_threads(t)             -> the threaded loops' default host-thread count (returns the old one)
+ *   int_pool(n, nb)                 -> n fresh ints with room for nb-byte values: an output list made ahead
+ *   words_into_pool(pool, buf, nb)  -> the pool's ints take buf's values in place
  *
  * `out` is any writable C-contiguous buffer (a numpy array) of the exact size.  Host code,
  * not part of the GPU compute path: the arithmetic stays in the HIP library.
@@ -616,6 +618,112 @@ static PyObject* float_pool(PyObject* self, PyObject* args) {
     return lst;
 }
 
+/* An output list of ints made ahead (prepare_encrypt): n ints allocated with room for the digits of an
+ * nb-byte value and holding 0 (ob_size 0: no digit is read).  words_into_pool later writes each one's value
+ * in place -- no allocation on the encrypt's critical path (making 333 334 ciphertext-sized ints is ~17 ms
+ * of page faults and allocator work on one thread).  None where the digit layout is not this build's
+ * (FBM_DIGITS_FAST=0). */
+static PyObject* int_pool(PyObject* self, PyObject* args) {
+    Py_ssize_t n, nb;
+    if (!PyArg_ParseTuple(args, "nn", &n, &nb)) return NULL;
+    if (n < 0 || nb <= 0 || nb % 4) {
+        PyErr_SetString(PyExc_ValueError, "int_pool takes n >= 0 and a positive width in whole 32-bit words");
+        return NULL;
+    }
+#if FBM_DIGITS_FAST
+    const Py_ssize_t nd = (8 * nb + PyLong_SHIFT - 1) / PyLong_SHIFT;
+    PyObject* lst = PyList_New(n);
+    if (!lst) return NULL;
+    PyObject** items = ((PyListObject*)lst)->ob_item;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        PyLongObject* v = _PyLong_New(nd);
+        if (!v) {
+            Py_DECREF(lst); /* the NULL slots after i are skipped by the list's deallocation */
+            return NULL;
+        }
+        Py_SET_SIZE(v, 0);
+        items[i] = (PyObject*)v;
+    }
+    return lst;
+#else
+    Py_RETURN_NONE;
+#endif
+}
+
+#if FBM_DIGITS_FAST
+typedef struct {
+    PyObject** items;
+    const unsigned char* src;
+    Py_ssize_t lo, hi, nb;
+} pool_job;
+
+static void* pool_range(void* arg) {
+    pool_job* j = (pool_job*)arg;
+    for (Py_ssize_t i = j->lo; i < j->hi; ++i) {
+        const uint32_t* w = (const uint32_t*)(j->src + i * j->nb);
+        const Py_ssize_t nw = words_used(w, j->nb / 4);
+        PyLongObject* v = (PyLongObject*)j->items[i];
+        if (nw == 0) {
+            Py_SET_SIZE(v, 0);
+            continue;
+        }
+        const Py_ssize_t nbits = 32 * (nw - 1) + (32 - __builtin_clz(w[nw - 1]));
+        Py_SET_SIZE(v, (nbits + PyLong_SHIFT - 1) / PyLong_SHIFT);
+        long_fill(v, w, nw);
+    }
+    return NULL;
+}
+#endif
+
+/* The values of buf (n x nb bytes, unsigned little-endian, nb the pool's width) into int_pool's ints, in
+ * place, on host threads while this thread holds the GIL.  Every item must be an exact int that only the
+ * list holds (refcount 1): the pool's own, never handed out -- anything else is a ValueError and nothing
+ * is written. */
+static PyObject* words_into_pool(PyObject* self, PyObject* args) {
+    PyObject* lst;
+    Py_buffer view;
+    Py_ssize_t nb;
+    if (!PyArg_ParseTuple(args, "O!y*n", &PyList_Type, &lst, &view, &nb)) return NULL;
+#if FBM_DIGITS_FAST
+    const Py_ssize_t n = PyList_GET_SIZE(lst);
+    if (nb <= 0 || nb % 4 || view.len != n * nb || ((uintptr_t)view.buf & 3)) {
+        PyBuffer_Release(&view);
+        PyErr_SetString(PyExc_ValueError, "buffer does not hold the pool's values as whole 32-bit words");
+        return NULL;
+    }
+    PyObject** items = ((PyListObject*)lst)->ob_item;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        if (!PyLong_CheckExact(items[i]) || Py_REFCNT(items[i]) != 1) {
+            PyBuffer_Release(&view);
+            PyErr_SetString(PyExc_ValueError, "words_into_pool fills the ints of an int_pool that nothing else holds");
+            return NULL;
+        }
+    }
+    const int nt = n * nb >= PAR_MIN_BYTES ? conv_threads(n) : 1;
+    pool_job jobs[64];
+    pthread_t tid[64];
+    int started[64] = {0};
+    for (int t = 0; t < nt; ++t) {
+        jobs[t] = (pool_job){items, (const unsigned char*)view.buf, n * t / nt, n * (t + 1) / nt, nb};
+        if (t > 0) started[t] = pthread_create(&tid[t], NULL, pool_range, &jobs[t]) == 0;
+    }
+    pool_range(&jobs[0]);
+    for (int t = 1; t < nt; ++t) {
+        if (started[t])
+            pthread_join(tid[t], NULL);
+        else
+            pool_range(&jobs[t]);
+    }
+    PyBuffer_Release(&view);
+    Py_RETURN_NONE;
+#else
+    (void)lst, (void)nb;
+    PyBuffer_Release(&view);
+    PyErr_SetString(PyExc_ValueError, "no int pools in this build (FBM_DIGITS_FAST=0)");
+    return NULL;
+#endif
+}
+
 /* list[offset:offset + k] = the k float64 values of buf (one pass: no intermediate list as
  * ndarray.tolist() + extend would build), slot by slot as fill_slots says. */
 static PyObject* f64_into_list(PyObject* self, PyObject* args) {
@@ -646,6 +754,9 @@ static PyMethodDef methods[] = {
     {"set_conv_threads", set_conv_threads, METH_VARARGS,
      "default host-thread count of the threaded loops (FBM_CONV_THREADS overrides it) -> the previous one"},
     {"float_pool", float_pool, METH_VARARGS, "n -> n distinct 0.0 floats held by the list only"},
+    {"int_pool", int_pool, METH_VARARGS, "n, nb -> n fresh ints with room for nb-byte values (None: not this build)"},
+    {"words_into_pool", words_into_pool, METH_VARARGS,
+     "int_pool list, buffer of n nb-byte LE values, nb -> None (each int's value written in place)"},
     {"ints_to_bytes_held", ints_to_bytes_held, METH_VARARGS,
      "lists, lo, hi, n, out -> -1 or first bad flat index (host threads, GIL held, no pins)"},
     {"f64_into_list", f64_into_list, METH_VARARGS, "list, offset, float64 buffer -> None (fills the list)"},

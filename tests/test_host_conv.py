@@ -302,3 +302,54 @@ def test_default_threads_follow_the_cpu_share(monkeypatch):
         assert m.set_conv_threads(0) == 3 and m.set_conv_threads(1000) == 1 and m.set_conv_threads(old) == 64
     finally:
         m.set_conv_threads(old)
+
+
+def test_int_pool_filled_in_place():
+    """prepare_encrypt's output list: ints made ahead (value 0), their values written in place later from
+    limb rows -- the same ints int.from_bytes makes (normalised: comparisons, hashing and arithmetic agree),
+    on host threads past the threaded size; a pool item held elsewhere, a foreign item or a buffer of
+    another size is refused before anything is written."""
+    m = D._pyconv()
+    if m is D._PyConvFallback:
+        pytest.skip("C conversion module not built")
+    rng = random.Random(31)
+    vals = [0, 1, 255, 2**30 - 1, 2**30, 2**32, 2**2047, 2**2048 - 1] + [rng.getrandbits(rng.randint(1, 2048))
+                                                                           for _ in range(6000)]
+    pool = D.int_pool(len(vals))
+    assert len(pool) == len(vals) and all(type(v) is int and v == 0 for v in pool)
+    rows = np.frombuffer(b"".join(v.to_bytes(256, "little") for v in vals), np.uint32).reshape(-1, 64)
+    assert D.limbs_into_pool(pool, rows) is pool
+    assert pool == vals and all(type(v) is int for v in pool)
+    assert [hash(v) for v in pool[:50]] == [hash(v) for v in vals[:50]]
+    assert sum(pool) == sum(vals) and pool[8] + 1 == vals[8] + 1 and str(pool[7]) == str(vals[7])
+    pool2 = D.int_pool(3)
+    held = pool2[1]
+    with pytest.raises(ValueError):  # refcount 2: someone else holds it
+        D.limbs_into_pool(pool2, rows[:3])
+    assert pool2 == [0, 0, 0] and held == 0
+    del held
+    with pytest.raises(ValueError):
+        m.words_into_pool([0, 5, 2**100], rows[:3].tobytes(), 256)  # not a pool
+    with pytest.raises(ValueError):
+        D.limbs_into_pool(D.int_pool(2), rows[:3])  # size
+
+
+def test_int_pool_absent_from_the_portable_build(tmp_path):
+    import importlib.util
+    import shutil
+    import subprocess
+    import sysconfig
+
+    from fedbiomed_amd import _build
+
+    if not shutil.which("gcc"):
+        pytest.skip("no gcc")
+    out = tmp_path / ("_fbm_pyconv" + sysconfig.get_config_var("EXT_SUFFIX"))
+    subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-Wall", "-Werror", "-pthread", "-DFBM_DIGITS_FAST=0",
+                    "-I" + sysconfig.get_paths()["include"], _build.PYCONV_SRC, "-o", str(out)], check=True)
+    spec = importlib.util.spec_from_file_location("_fbm_pyconv", str(out))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.int_pool(4, 256) is None
+    with pytest.raises(ValueError):
+        mod.words_into_pool([0], bytes(256), 256)
