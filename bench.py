@@ -1017,6 +1017,40 @@ def main():
             agg_ll = lc.aggregate(yl, total_w)
             tll = time.perf_counter() - t0
             del agg_ll, yl
+            # the same with the output lists made ahead (SecaggLomCrypter.prepare_encrypt per party before
+            # its encrypt, prepare_aggregate before the aggregate -- extensions, issued outside the clock as
+            # a node does with the training request and the researcher before the replies)
+            tlp = 0.0
+            yl = []
+            for p, u in enumerate(ids):
+                lc.prepare_encrypt(tau, u, nl)
+                t0 = time.perf_counter()
+                yl.append(lc.encrypt(tau, u, xl[p], secrets_[p], ids, weight=weights[p]))
+                tlp += time.perf_counter() - t0
+            lc.prepare_aggregate(nl)
+            t0 = time.perf_counter()
+            agg_lp = lc.aggregate(yl, total_w)
+            tlp += time.perf_counter() - t0
+            del agg_lp, yl
+
+            def lom_node_encrypt(ne):  # one party's encrypt(List[float]) -> List[int], as the JL legs
+                xl0 = xs_h[0][:ne].tolist()
+                lc.encrypt(tau, ids[0], xl0[:4096], secrets_[0], ids, weight=weights[0])  # warm the staging
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                r = lc.encrypt(tau, ids[0], xl0, secrets_[0], ids, weight=weights[0])
+                t_plain = time.perf_counter() - t0
+                prepared = lc.prepare_encrypt(tau, ids[0], ne)
+                t0 = time.perf_counter()
+                r2 = lc.encrypt(tau, ids[0], xl0, secrets_[0], ids, weight=weights[0])
+                t_prep = time.perf_counter() - t0
+                same = r2 == r
+                del r, r2
+                return {"elements": ne, "ms": 1000 * t_plain, "params_per_s": ne / t_plain,
+                        "output_prepared": {"ms": 1000 * t_prep, "params_per_s": ne / t_prep, "prepared": prepared,
+                                            "equals_unprepared": same}}
+
+            lom_node = {str(ne): lom_node_encrypt(ne) for ne in args.node_list_n if ne <= n}
             line["end_to_end"]["lom"] = {
                 "pinned_host_tensors": {"value": n / tle, "unit": "params/s", "ms_per_step": 1000 * tle,
                                         "elements": n, "equals_device_step": lom_e2e_equal,
@@ -1024,8 +1058,14 @@ def main():
                                                                "H2D of the row into the researcher's block "
                                                                "(beside the next party's D2H); aggregate + D2H f64"},
                 "list_api": {"value": nl / tll, "unit": "params/s", "ms_per_step": 1000 * tll, "elements": nl,
+                             "output_prepared": {"value": nl / tlp, "ms_per_step": 1000 * tlp},
                              "note": "SecaggLomCrypter.encrypt (List[float] -> List[int]) x P + aggregate "
-                                     "(List[List[int]] -> List[float])"}}
+                                     "(List[List[int]] -> List[float]); output_prepared: the same with each "
+                                     "output list's objects made ahead (prepare_encrypt / prepare_aggregate, "
+                                     "extensions; outside the clock)"},
+                "node_encrypt_list_api": dict(lom_node, note=(
+                    "one party's SecaggLomCrypter.encrypt(List[float]) -> List[int]; output_prepared: after "
+                    "prepare_encrypt (the output's int objects made ahead, their values written in place)"))}
 
     # ---- CPU baseline: the oracle (CPU restatement of the reference, GMP powm) on a bounded sample ----
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

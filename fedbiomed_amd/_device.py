@@ -502,11 +502,18 @@ def f64_into_list(lst: list, off: int, values: np.ndarray) -> None:
     _pyconv().f64_into_list(lst, off, np.ascontiguousarray(values, dtype=np.float64))
 
 
-def int_pool(n: int) -> Optional[list]:
-    """n ciphertext-sized ints made ahead (prepare_encrypt's output list; limbs_into_pool writes their
-    values in place), or None where the C module cannot make them (not built, or CPython >= 3.12)."""
+def int_pool(n: int, nbytes: int = 256) -> Optional[list]:
+    """n ints with room for nbytes-byte values made ahead (a prepared encrypt's output list: JL
+    ciphertexts, 256 bytes, through limbs_into_pool; LOM's masked values, 8 bytes, through
+    u64_into_pool), or None where the C module cannot make them (not built, or CPython >= 3.12)."""
     m = _pyconv()
-    return None if m is _PyConvFallback else m.int_pool(n, 256)
+    return None if m is _PyConvFallback else m.int_pool(n, nbytes)
+
+
+def u64_into_pool(pool: list, arr: np.ndarray) -> list:
+    """int_pool(n, 8)'s ints take the uint64 values' in place (host threads); the pool."""
+    _pyconv().words_into_pool(pool, np.ascontiguousarray(arr, dtype=np.uint64).view(np.uint32), 8)
+    return pool
 
 
 def limbs_into_pool(pool: list, arr: np.ndarray) -> list:

@@ -535,9 +535,44 @@ class SecaggCrypter:
 class SecaggLomCrypter(SecaggCrypter):
     """Low-Overhead Masking secure aggregation (reference `_secagg_crypter.py:300-455`)."""
 
-    def prepare_aggregate(self, *args, **kwargs) -> bool:
-        """LOM's aggregate is a sum with no exponentiation: nothing to issue ahead."""
-        return False
+    def prepare_aggregate(self, *args, num_params: Optional[int] = None, **kwargs) -> bool:
+        """Extension (not in the reference): `prepare_aggregate(num_params)`.  LOM's aggregate is a sum with
+        no exponentiation, so nothing runs ahead on the device; what is made ahead is the output list's
+        float objects (`float_pool`), whose values the next `aggregate` of `num_params` values writes in
+        place (making 10M Python floats is ~100 ms of the call).  An aggregate of another size -- the
+        researcher's one-value validation aggregate comes first (`_secure_aggregation.py:372-387`) --
+        leaves it.  False (nothing prepared) for anything but one positive int: the Joye-Libert form
+        (round, nodes, key, biprime, size) has no LOM counterpart."""
+        self._lom_agg_pool = None
+        if num_params is None and len(args) == 1:
+            num_params = args[0]
+        elif args:
+            return False
+        if not isinstance(num_params, int) or isinstance(num_params, bool) or num_params <= 0:
+            return False
+        self._lom_agg_pool = D.float_pool(num_params)
+        return True
+
+    def prepare_encrypt(self, current_round: int, node_id: str, num_params: int) -> bool:
+        """Extension (not in the reference): make the next `encrypt`'s output list ahead -- its int objects
+        (`int_pool`), whose values the encrypt of that round, node and size writes in place (making 10M
+        Python ints is most of a 10M-element list encrypt).  Nothing secret is computed or kept.  False
+        (nothing prepared) where the pool cannot be made (CPython >= 3.12 builds) or for bad arguments."""
+        self._lom_enc_prep = None
+        if not isinstance(num_params, int) or isinstance(num_params, bool) or num_params <= 0:
+            return False
+        pool = D.int_pool(num_params, 8)
+        if pool is None:
+            return False
+        self._lom_enc_prep = {"round": current_round, "node_id": node_id, "n": num_params, "pool": pool}
+        return True
+
+    def _take_enc_pool(self, current_round, node_id, n):
+        prep = getattr(self, "_lom_enc_prep", None)
+        if prep is None or prep["round"] != current_round or prep["node_id"] != node_id or prep["n"] != n:
+            return None
+        self._lom_enc_prep = None
+        return prep["pool"]
 
     def __init__(self, nonce: Optional[str] = None):
         if nonce:
@@ -609,7 +644,8 @@ class SecaggLomCrypter(SecaggCrypter):
         y = self.encrypt_tensor(current_round, node_id, x, pairwise_secrets, node_ids, clipping_range, weight,
                                 target_range)
         packed = D.to_host(y).numpy().view(np.uint64)
-        out = packed.tolist()
+        pool = self._take_enc_pool(current_round, node_id, packed.shape[0])
+        out = D.u64_into_pool(pool, packed) if pool is not None else packed.tolist()
         if wire.enabled():
             out = wire.EncryptedParams(out, "lom", packed)
         logger.debug(f"Encryption of the parameters took {time.process_time() - start} seconds.")
@@ -632,6 +668,13 @@ class SecaggLomCrypter(SecaggCrypter):
             return []
         out = self.aggregate_tensor(Y, total_sample_size, clipping_range, target_range)
         logger.info(f"Aggregating {len(params)} parameters from {num_nodes} nodes.")
-        res = D.to_host(out).numpy().tolist()
+        res_h = D.to_host(out).numpy()
+        pool = getattr(self, "_lom_agg_pool", None)
+        if pool is not None and len(pool) == res_h.shape[0]:  # prepare_aggregate's floats, written in place
+            self._lom_agg_pool = None
+            D.f64_into_list(pool, 0, res_h)
+            res = pool
+        else:
+            res = res_h.tolist()
         logger.debug(f"Aggregation is completed in {round(time.process_time() - start, ndigits=2)} seconds.")
         return res

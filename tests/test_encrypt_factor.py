@@ -147,3 +147,40 @@ def test_prepare_encrypt_life_cycle(monkeypatch):
     for bad in ((tau, P, 1.5, W.BIPRIME0, n), (tau, P, key, W.BIPRIME0, 0), (tau, 0, key, W.BIPRIME0, n),
                 (tau, P, key, "N", n), (tau, P, key, W.BIPRIME0 + 1, n), (tau, P, key, 1, n)):
         assert jc.prepare_encrypt(*bad) is False, bad
+
+
+@pytest.mark.gpu
+def test_lom_prepared_output_lists():
+    """SecaggLomCrypter.prepare_encrypt / prepare_aggregate (extensions): the output lists' objects made
+    ahead, their values written in place -- the same lists as unprepared calls; an encrypt of another round,
+    node or size, or an aggregate of another size (the researcher's one-value validation aggregate comes
+    first), leaves the preparation for the call it was made for."""
+    from oracle import secagg_oracle as O
+    from fedbiomed_amd.secagg import SecaggLomCrypter
+
+    P, tau, n = 4, 11, 30_000
+    ids = W.node_ids(P)
+    lc = SecaggLomCrypter("lom_prepared")
+    xs = [[float(v) for v in W.party_params(p, n)] for p in range(P)]
+    ref_y, got_y = [], []
+    for p, u in enumerate(ids):
+        sec = W.pairwise_secrets_for(u, ids)
+        ref_y.append(lc.encrypt(tau, u, xs[p], sec, ids, weight=p + 1))
+        assert lc.prepare_encrypt(tau, u, n) is True
+        assert lc.encrypt(tau + 1, u, xs[p][:10], sec, ids, weight=p + 1) is not None  # another call: left
+        assert lc._lom_enc_prep is not None
+        got_y.append(lc.encrypt(tau, u, xs[p], sec, ids, weight=p + 1))
+        assert lc._lom_enc_prep is None
+        assert got_y[-1] == ref_y[-1] and all(type(v) is int for v in got_y[-1][:100]), p
+    nonce = O.lom_nonce("lom_prepared")
+    assert got_y[0] == [int(v) for v in np.asarray(
+        O.lom_encrypt(np.asarray(xs[0]), tau, ids[0], W.pairwise_secrets_for(ids[0], ids), ids, nonce, weight=1),
+        dtype=np.uint64)]
+    tw = sum(range(1, P + 1))
+    ref = lc.aggregate(ref_y, tw)
+    assert lc.prepare_aggregate(n) is True
+    val = lc.aggregate([y[:1] for y in got_y], tw)  # the validation aggregate: another size, left
+    assert len(val) == 1 and lc._lom_agg_pool is not None
+    out = lc.aggregate(got_y, tw)
+    assert lc._lom_agg_pool is None
+    assert np.asarray(out).view(np.uint64).tolist() == np.asarray(ref).view(np.uint64).tolist()

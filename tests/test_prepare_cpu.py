@@ -61,3 +61,14 @@ def test_capture_and_adopt_checks():
         assert len(D.deferred_checks._stack()[-1]) == 1
         D.deferred_checks._stack()[-1].clear()  # (no device here to stack the words on)
     assert outer is not None and np.asarray(bad)[D.FBM_STAT_ERRFLAGS] == err
+
+
+def test_lom_prepare_aggregate_makes_floats_only():
+    """SecaggLomCrypter.prepare_aggregate(num_params) (an extension): the output's floats, host only;
+    the Joye-Libert form of the call and bad sizes prepare nothing."""
+    lc = SecaggLomCrypter()
+    assert lc.prepare_aggregate(5) is True and lc._lom_agg_pool == [0.0] * 5
+    assert lc.prepare_aggregate(num_params=3) is True and len(lc._lom_agg_pool) == 3
+    for bad in ((0,), (-1,), (2.0,), (True,), (3, 2, -5, 2**61 - 1, 100)):
+        assert lc.prepare_aggregate(*bad) is False and lc._lom_agg_pool is None, bad
+    assert lc.prepare_encrypt(1, "n", 0) is False and lc._lom_enc_prep is None
