@@ -277,6 +277,12 @@ class _PyConvFallback:
         return all(isinstance(v, int) for v in seq)
 
     @staticmethod
+    def all_ints_lists(lists: list) -> int:
+        if not all(isinstance(r, list) for r in lists):
+            raise TypeError("all_ints_lists takes a list of lists")
+        return next((u for u, r in enumerate(lists) if not all(isinstance(v, int) for v in r)), -1)
+
+    @staticmethod
     def floats_to_f64(seq: list, out: np.ndarray) -> int:
         if out.nbytes != 8 * len(seq):
             raise ValueError(f"output buffer holds {out.nbytes} bytes, {8 * len(seq)} needed")
@@ -416,6 +422,11 @@ def to_host(t: torch.Tensor) -> torch.Tensor:
 def all_ints(seq: list) -> bool:
     """all(isinstance(v, int) for v in seq) of a list, in one C pass (csrc/fbm_pyconv.c)."""
     return bool(_pyconv().all_ints(seq))
+
+
+def all_ints_lists(lists: list) -> bool:
+    """Every item of every list (a list of lists) is an int (isinstance), in one C pass over host threads."""
+    return _pyconv().all_ints_lists(lists) < 0
 
 
 def floats_to_host(params: list) -> Optional[torch.Tensor]:

@@ -65,7 +65,7 @@ def _check_int_lists(params) -> None:
         raise FedbiomedSecaggCrypterError(
             f"{ErrorNumbers.FB624.value}: The parameters to aggregate should be a "
             f"list containing list of parameters")
-    if not all(D.all_ints(p) for p in params):
+    if not D.all_ints_lists(params):
         raise FedbiomedSecaggCrypterError(
             f"{ErrorNumbers.FB624.value}: Invalid parameter type. The parameters "
             f"should be of type of integers.")

@@ -353,3 +353,23 @@ def test_int_pool_absent_from_the_portable_build(tmp_path):
     assert mod.int_pool(4, 256) is None
     with pytest.raises(ValueError):
         mod.words_into_pool([0], bytes(256), 256)
+
+
+@pytest.mark.parametrize("threads", ["1", "5"])
+def test_all_ints_lists(conv, monkeypatch, threads):
+    """The researcher's type check of every party's list in one pass: -1, or the first list with a
+    non-int (bool and int subclasses are ints, as isinstance says); empty lists anywhere."""
+    monkeypatch.setenv("FBM_CONV_THREADS", threads)
+    rng = random.Random(41)
+    lists = [[rng.getrandbits(64) for _ in range(30_000)] for _ in range(4)] + [[]] + [[1, True, 2**3000]]
+    assert conv.all_ints_lists(lists) == -1
+    assert conv.all_ints_lists([]) == -1 and conv.all_ints_lists([[], []]) == -1
+    for u, i, bad in ((0, 0, 1.0), (2, 29_999, "x"), (3, 15_000, None), (5, 2, 2.5)):
+        l2 = [list(r) for r in lists]
+        l2[u][i] = bad
+        assert conv.all_ints_lists(l2) == u
+        if u < 5:  # a later bad list never hides an earlier one
+            l2[5][0] = 0.5
+            assert conv.all_ints_lists(l2) == u
+    with pytest.raises(TypeError):
+        conv.all_ints_lists([[1], (2,)])
