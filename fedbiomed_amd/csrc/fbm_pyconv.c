@@ -791,6 +791,69 @@ static PyObject* words_into_pool(PyObject* self, PyObject* args) {
 
 /* list[offset:offset + k] = the k float64 values of buf (one pass: no intermediate list as
  * ndarray.tolist() + extend would build), slot by slot as fill_slots says. */
+/* A long f64_into_list on host threads WHILE THIS THREAD HOLDS THE GIL: a check pass (every slot None or an
+ * exact float: the type pointers only), then the in-place writes of the floats nothing else holds (ob_fval
+ * of objects only the list references -- a prepared pool's 10M floats: ~22 ms on one thread).  The slots
+ * left (None, or a float with another holder: an allocation and a DECREF each) go through fill_slots on
+ * this thread, which skips the floats already written. */
+typedef struct {
+    PyObject** items;
+    const double* src;
+    Py_ssize_t lo, hi, bad, rest;
+} slot_job;
+
+static void* slot_check_range(void* arg) {
+    slot_job* j = (slot_job*)arg;
+    j->bad = -1;
+    for (Py_ssize_t i = j->lo; i < j->hi; ++i)
+        if (j->items[i] != Py_None && !PyFloat_CheckExact(j->items[i])) {
+            j->bad = i;
+            break;
+        }
+    return NULL;
+}
+
+static void* slot_fill_range(void* arg) {
+    slot_job* j = (slot_job*)arg;
+    j->rest = 0;
+    for (Py_ssize_t i = j->lo; i < j->hi; ++i) {
+        PyObject* o = j->items[i];
+        if (o != Py_None && Py_REFCNT(o) == 1)
+            ((PyFloatObject*)o)->ob_fval = j->src[i];
+        else
+            ++j->rest;
+    }
+    return NULL;
+}
+
+static void run_slot_jobs(slot_job* jobs, int nt, void* (*fn)(void*)) {
+    pthread_t tid[64];
+    int started[64] = {0};
+    for (int t = 1; t < nt; ++t) started[t] = pthread_create(&tid[t], NULL, fn, &jobs[t]) == 0;
+    fn(&jobs[0]);
+    for (int t = 1; t < nt; ++t) {
+        if (started[t])
+            pthread_join(tid[t], NULL);
+        else
+            fn(&jobs[t]);
+    }
+}
+
+static int slots_parallel(PyObject** items, const double* src, Py_ssize_t k, int nt) {
+    slot_job jobs[64];
+    for (int t = 0; t < nt; ++t) jobs[t] = (slot_job){items, src, k * t / nt, k * (t + 1) / nt, -1, 0};
+    run_slot_jobs(jobs, nt, slot_check_range);
+    for (int t = 0; t < nt; ++t)
+        if (jobs[t].bad >= 0) {
+            PyErr_SetString(PyExc_ValueError, "f64_into_list fills slots that hold None or floats only");
+            return -1;
+        }
+    run_slot_jobs(jobs, nt, slot_fill_range);
+    Py_ssize_t rest = 0;
+    for (int t = 0; t < nt; ++t) rest += jobs[t].rest;
+    return rest ? fill_slots(items, src, k) : 0;
+}
+
 static PyObject* f64_into_list(PyObject* self, PyObject* args) {
     PyObject* lst;
     Py_ssize_t off;
@@ -804,7 +867,13 @@ static PyObject* f64_into_list(PyObject* self, PyObject* args) {
     }
     const double* src = (const double*)view.buf;
     PyObject** items = ((PyListObject*)lst)->ob_item + off;
-    const int rc = check_slots(items, k) < 0 ? -1 : fill_slots(items, src, k);
+    const int nt = k >= (1 << 16) ? conv_threads(k) : 1;
+    int rc;
+    if (nt == 1) {
+        rc = check_slots(items, k) < 0 ? -1 : fill_slots(items, src, k);
+    } else {
+        rc = slots_parallel(items, src, k, nt);
+    }
     PyBuffer_Release(&view);
     if (rc < 0) return NULL;
     Py_RETURN_NONE;

@@ -285,6 +285,29 @@ def test_float_pool_filled_in_place():
         m.float_pool(-1)
 
 
+@pytest.mark.parametrize("threads", ["1", "7"])
+def test_float_pool_filled_on_threads(monkeypatch, threads):
+    """Past the threaded size (65 536 slots) the in-place writes run on host threads: the pool's own floats
+    written in place, None slots and floats held elsewhere replaced on the calling thread, a bad slot
+    anywhere refused before any write."""
+    monkeypatch.setenv("FBM_CONV_THREADS", threads)
+    m = D._pyconv()
+    n = 200_000
+    vals = np.random.default_rng(3).standard_normal(n)
+    pool = m.float_pool(n)
+    ids = [id(v) for v in pool[:1000]]
+    pool[5] = None
+    held = pool[150_000]
+    m.f64_into_list(pool, 0, vals)
+    assert np.array(pool).tobytes() == vals.tobytes() and all(type(v) is float for v in pool)
+    assert [id(v) for v in pool[:5]] == ids[:5] and held == 0.0 and id(pool[150_000]) != id(held)
+    bad = m.float_pool(n)
+    bad[123_456] = 1
+    with pytest.raises(ValueError):
+        m.f64_into_list(bad, 0, vals)
+    assert bad[0] == 0.0 and bad[199_999] == 0.0  # nothing written
+
+
 def test_default_threads_follow_the_cpu_share(monkeypatch):
     """The threaded loops default to the process's CPU share (affinity capped by a cgroup quota), at
     most 16; FBM_CONV_THREADS still overrides it per call."""
