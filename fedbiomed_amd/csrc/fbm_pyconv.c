@@ -867,7 +867,8 @@ static PyObject* f64_into_list(PyObject* self, PyObject* args) {
     }
     const double* src = (const double*)view.buf;
     PyObject** items = ((PyListObject*)lst)->ob_item + off;
-    const int nt = k >= (1 << 16) ? conv_threads(k) : 1;
+    /* threads for a pool's floats; a list of None (the unprepared aggregate's) allocates every slot here */
+    const int nt = k >= (1 << 16) && items[0] != Py_None ? conv_threads(k) : 1;
     int rc;
     if (nt == 1) {
         rc = check_slots(items, k) < 0 ? -1 : fill_slots(items, src, k);
