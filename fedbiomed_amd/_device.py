@@ -522,14 +522,22 @@ def int_pool(n: int, nbytes: int = 256) -> Optional[list]:
 
 
 def u64_into_pool(pool: list, arr: np.ndarray) -> list:
-    """int_pool(n, 8)'s ints take the uint64 values' in place (host threads); the pool."""
-    _pyconv().words_into_pool(pool, np.ascontiguousarray(arr, dtype=np.uint64).view(np.uint32), 8)
+    """int_pool(n, 8)'s ints take the uint64 values in place (host threads); the pool -- or a fresh list
+    when a pool int is also held elsewhere (it is then never written)."""
+    try:
+        _pyconv().words_into_pool(pool, np.ascontiguousarray(arr, dtype=np.uint64).view(np.uint32), 8)
+    except ValueError:
+        return np.asarray(arr, dtype=np.uint64).tolist()
     return pool
 
 
 def limbs_into_pool(pool: list, arr: np.ndarray) -> list:
-    """int_pool's ints take the [n, 64] uint32 limb rows' values in place (host threads); the pool."""
-    _pyconv().words_into_pool(pool, np.ascontiguousarray(arr, dtype=np.uint32), 256)
+    """int_pool's ints take the [n, 64] uint32 limb rows' values in place (host threads); the pool -- or
+    a fresh list when a pool int is also held elsewhere (it is then never written)."""
+    try:
+        _pyconv().words_into_pool(pool, np.ascontiguousarray(arr, dtype=np.uint32), 256)
+    except ValueError:
+        return limbs_to_ints(arr)
     return pool
 
 

@@ -348,13 +348,17 @@ def test_int_pool_filled_in_place():
     pool2 = D.int_pool(3)
     held = pool2[1]
     with pytest.raises(ValueError):  # refcount 2: someone else holds it
-        D.limbs_into_pool(pool2, rows[:3])
+        m.words_into_pool(pool2, rows[:3].tobytes(), 256)
     assert pool2 == [0, 0, 0] and held == 0
+    got = D.limbs_into_pool(pool2, rows[:3])  # the device layer then makes a fresh list
+    assert got == vals[:3] and got is not pool2 and pool2 == [0, 0, 0] and held == 0
+    u64 = np.array([0, 1, 2**64 - 1], np.uint64)
+    assert D.u64_into_pool(pool2, u64) == [0, 1, 2**64 - 1] and held == 0
     del held
     with pytest.raises(ValueError):
         m.words_into_pool([0, 5, 2**100], rows[:3].tobytes(), 256)  # not a pool
     with pytest.raises(ValueError):
-        D.limbs_into_pool(D.int_pool(2), rows[:3])  # size
+        m.words_into_pool(D.int_pool(2), rows[:3].tobytes(), 256)  # size
 
 
 def test_int_pool_absent_from_the_portable_build(tmp_path):
