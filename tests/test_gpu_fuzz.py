@@ -3,7 +3,8 @@ pinned to the reference's own outcomes by tests/golden/): party counts, vector l
 count and the list aggregate's stripe edges, weights, clipping and target ranges, rounds up to 2^64 - 1,
 keys of many lengths and both signs of the server key, num_expected_params cutting inside the vector.
 Ciphertexts / masked vectors bit for bit, float64 outputs as bit patterns.  Half of the JL cases run the
-list aggregate in ct_offset stripes (FBM_ONE_LANE_ROUND shrunk), and some take a prepared factor."""
+list aggregate in ct_offset stripes (FBM_ONE_LANE_ROUND shrunk), some take a prepared factor, and every third
+party's encrypt takes its factor computed ahead (prepare_encrypt)."""
 
 import logging
 import random
@@ -50,6 +51,8 @@ def test_jl_fuzz_vs_oracle(i, monkeypatch, caplog):
     jc = SecaggCrypter()
     cts = []
     for p in range(c["P"]):
+        if (i + p) % 3 == 0:  # some parties' encrypts with their factor computed ahead (prepare_encrypt)
+            assert jc.prepare_encrypt(c["tau"], c["P"], c["keys"][p], W.BIPRIME0, c["n"], target_range=c["target"])
         got = jc.encrypt(c["P"], c["tau"], c["x"][p], c["keys"][p], W.BIPRIME0, clipping_range=c["clip"],
                          weight=c["weights"][p], target_range=c["target"])
         ref = O.jl_encrypt(c["x"][p], c["tau"], c["keys"][p], W.BIPRIME0, c["P"], clip=c["clip"],
@@ -97,6 +100,8 @@ def test_lom_fuzz_vs_oracle(i, caplog):
     ys = []
     for p, u in enumerate(ids):
         sec = W.pairwise_secrets_for(u, ids)
+        if (i + p) % 2 == 0:  # the output's ints made ahead (prepare_encrypt)
+            lc.prepare_encrypt(c["tau"], u, c["n"])
         got = lc.encrypt(c["tau"], u, c["x"][p], sec, ids, clipping_range=c["clip"], weight=c["weights"][p],
                          target_range=c["target"])
         ref = O.lom_encrypt(np.asarray(c["x"][p], np.float64), c["tau"], u, sec, ids, nonce, clip=c["clip"],
@@ -104,6 +109,8 @@ def test_lom_fuzz_vs_oracle(i, caplog):
         assert got == [int(v) for v in np.asarray(ref, dtype=np.uint64)], (i, p)
         ys.append(got)
     total = sum(w if w is not None else 1 for w in c["weights"])
+    if i % 2:  # the output's floats made ahead (prepare_aggregate)
+        assert lc.prepare_aggregate(c["n"])
     out = lc.aggregate(ys, total, clipping_range=c["clip"], target_range=c["target"])
     ref = O.lom_crypter_aggregate([np.asarray(y, dtype=np.uint64) for y in ys], total, clip=c["clip"],
                                   target=c["target"])
