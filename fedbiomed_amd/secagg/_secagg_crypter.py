@@ -186,20 +186,22 @@ class SecaggCrypter:
         x = host.to(dev)
         n_ct = (x.numel() + cr - 1) // cr
         prep = self._take_prepared_encrypt(current_round, num_nodes, key, biprime, target_range, n_ct, dev)
-        stripes = D.list_encrypt_stripes(n_ct, dev) if prep is None else [(0, n_ct)]
         if prep is not None:  # prepare_encrypt's factor: one product per ciphertext, no exponentiation
             factor, pool = prep
             ct = self.encrypt_tensor(num_nodes, current_round, x, key, biprime, clipping_range, weight, target_range,
                                      factor=factor)
             packed = D.to_host(ct).numpy().view(np.uint32)
             out = D.limbs_into_pool(pool, packed) if pool is not None else D.limbs_to_ints(packed)
-        elif len(stripes) == 1:
-            ct = self.encrypt_tensor(num_nodes, current_round, x, key, biprime, clipping_range, weight, target_range)
-            packed = D.to_host(ct).numpy().view(np.uint32)
-            out = D.limbs_to_ints(packed)
         else:
-            packed, out = self._encrypt_overlapped(num_nodes, current_round, x, key, biprime, clipping_range, weight,
-                                                   target_range, stripes, cr)
+            stripes = D.list_encrypt_stripes(n_ct, dev)
+            if len(stripes) == 1:
+                ct = self.encrypt_tensor(num_nodes, current_round, x, key, biprime, clipping_range, weight,
+                                         target_range)
+                packed = D.to_host(ct).numpy().view(np.uint32)
+                out = D.limbs_to_ints(packed)
+            else:
+                packed, out = self._encrypt_overlapped(num_nodes, current_round, x, key, biprime, clipping_range,
+                                                       weight, target_range, stripes, cr)
         if wire.enabled():
             out = wire.EncryptedParams(out, "jl", packed)
         logger.debug(f"Encryption of the parameters took {time.process_time() - start} seconds.")
