@@ -1466,6 +1466,28 @@ def limbs_tc_to_ints(arr: np.ndarray) -> List[int]:
     return out
 
 
+def reference_share_draws(bls: Sequence[int], draws: int) -> List[List[int]]:
+    """The reference's additive-share draws from the global `random`, exactly (`_additive_ss.py:94-96`):
+    random.randint(0, 2**bl) for every element (outer) and share (inner); rows [draws][n].  The C module
+    runs CPython's MT19937 from random.getstate() and hands the state back with random.setstate(), so the
+    stream continues where the reference's would (bit lengths up to 126; past that, or without the
+    module, the same calls through `random` itself)."""
+    import random
+
+    n = len(bls)
+    m = _pyconv()
+    if draws <= 0 or n == 0:
+        return [[] for _ in range(max(draws, 0))]
+    if m is _PyConvFallback or max(bls) > 126:
+        cols = [[random.randint(0, 2**bl) for _ in range(draws)] for bl in bls]
+        return [[c[j] for c in cols] for j in range(draws)]
+    version, state, gauss = random.getstate()
+    out = np.empty((draws, n, 2), dtype=np.int64)
+    new = m.mt_share_draws(state, np.asarray(bls, dtype=np.uint32).tobytes(), draws, out)
+    random.setstate((version, new, gauss))
+    return [int128_to_ints(out[j]) for j in range(draws)]
+
+
 def ints_to_int128(values: Sequence[int]) -> np.ndarray:
     """Python ints in [-2^127, 2^127) -> int64 [n, 2] (lo, hi) two's complement."""
     out = np.empty((len(values), 2), dtype=np.int64)

@@ -619,6 +619,121 @@ static PyObject* float_pool(PyObject* self, PyObject* args) {
     return lst;
 }
 
+/* ---- the reference's additive-share draws, exactly (AdditiveSecret.split with reference_rng) ----------
+ * The reference draws every share with the global `random` (`_additive_ss.py:96`: random.randint(0, 2**bl)
+ * per element, per share, element-major), i.e. CPython's MT19937 (Matsumoto & Nishimura 1998, the 32-bit
+ * generator with its tempering) behind randint -> randrange -> _randbelow_with_getrandbits(n = 2**bl + 1):
+ * k = n.bit_length() bits per attempt, getrandbits(k) = 32-bit outputs least significant first with the
+ * last one shifted right to its k mod 32 bits, rejected while >= n.  mt_share_draws runs that from the
+ * state `random.getstate()` holds and returns the state `random.setstate()` takes back, so the Python
+ * stream goes on where the reference's would. */
+#define MT_N 624
+#define MT_M 397
+
+static uint32_t mt_next(uint32_t* mt, Py_ssize_t* idx) {
+    if (*idx >= MT_N) {
+        int kk;
+        uint32_t y;
+        for (kk = 0; kk < MT_N - MT_M; ++kk) {
+            y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+            mt[kk] = mt[kk + MT_M] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        for (; kk < MT_N - 1; ++kk) {
+            y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+            mt[kk] = mt[kk + (MT_M - MT_N)] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        y = (mt[MT_N - 1] & 0x80000000u) | (mt[0] & 0x7fffffffu);
+        mt[MT_N - 1] = mt[MT_M - 1] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        *idx = 0;
+    }
+    uint32_t y = mt[(*idx)++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+/* randint(0, 2**bl) for bl <= 126, as (lo, hi) of a non-negative int128 */
+static void mt_randint_pow2(uint32_t* mt, Py_ssize_t* idx, int bl, uint64_t* lo, uint64_t* hi) {
+    const int k = bl == 0 ? 2 : bl + 1; /* (2**bl + 1).bit_length() */
+    for (;;) {
+        uint32_t w[4] = {0, 0, 0, 0};
+        int rem = k;
+        for (int i = 0; rem > 0; ++i, rem -= 32) {
+            uint32_t r = mt_next(mt, idx);
+            if (rem < 32) r >>= 32 - rem;
+            w[i] = r;
+        }
+        const uint64_t l = (uint64_t)w[0] | ((uint64_t)w[1] << 32), h = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+        const int accept = bl < 64 ? h == 0 && l <= (1ull << bl)  /* r <= 2**bl */
+                                   : h < (1ull << (bl - 64)) || (h == (1ull << (bl - 64)) && l == 0);
+        if (accept) {
+            *lo = l;
+            *hi = h;
+            return;
+        }
+    }
+}
+
+static PyObject* mt_share_draws(PyObject* self, PyObject* args) {
+    /* (state: 625-tuple of ints, bls: uint32 buffer [n], draws: int, out: int64 buffer [draws, n, 2])
+     * -> the 625-tuple after the draws */
+    PyObject *state, *out;
+    Py_buffer bv, ov;
+    Py_ssize_t reps;
+    if (!PyArg_ParseTuple(args, "O!y*nO", &PyTuple_Type, &state, &bv, &reps, &out)) return NULL;
+    if (PyTuple_GET_SIZE(state) != MT_N + 1 || bv.len % 4 || reps < 0) {
+        PyBuffer_Release(&bv);
+        PyErr_SetString(PyExc_ValueError, "mt_share_draws takes a 625-entry MT19937 state and uint32 bit lengths");
+        return NULL;
+    }
+    const Py_ssize_t n = bv.len / 4;
+    if (get_out(out, &ov, reps * n * 16) < 0) {
+        PyBuffer_Release(&bv);
+        return NULL;
+    }
+    uint32_t mt[MT_N];
+    for (int i = 0; i < MT_N; ++i) mt[i] = (uint32_t)PyLong_AsUnsignedLongMask(PyTuple_GET_ITEM(state, i));
+    Py_ssize_t idx = PyLong_AsSsize_t(PyTuple_GET_ITEM(state, MT_N));
+    const uint32_t* bls = (const uint32_t*)bv.buf;
+    uint64_t* o = (uint64_t*)ov.buf;
+    int bad = PyErr_Occurred() != NULL || idx < 0 || idx > MT_N;
+    for (Py_ssize_t i = 0; i < n && !bad; ++i) {
+        if (bls[i] > 126) {
+            bad = 1;
+            break;
+        }
+        for (Py_ssize_t j = 0; j < reps; ++j) {
+            uint64_t* d = o + 2 * (j * n + i);
+            mt_randint_pow2(mt, &idx, (int)bls[i], d, d + 1);
+        }
+    }
+    PyBuffer_Release(&bv);
+    PyBuffer_Release(&ov);
+    if (bad) {
+        if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "bit length above 126 or a bad MT19937 index");
+        return NULL;
+    }
+    PyObject* res = PyTuple_New(MT_N + 1);
+    if (!res) return NULL;
+    for (int i = 0; i < MT_N; ++i) {
+        PyObject* v = PyLong_FromUnsignedLong(mt[i]);
+        if (!v) {
+            Py_DECREF(res);
+            return NULL;
+        }
+        PyTuple_SET_ITEM(res, i, v);
+    }
+    PyObject* v = PyLong_FromSsize_t(idx);
+    if (!v) {
+        Py_DECREF(res);
+        return NULL;
+    }
+    PyTuple_SET_ITEM(res, MT_N, v);
+    return res;
+}
+
 /* all_ints over a list of lists in one call: every party's list at once, split evenly over host threads
  * (the researcher's type check of 8 x 333 334 ciphertexts: one thread pool instead of one per list) ->
  * -1, or the index of the first list holding an item that is not an int (isinstance semantics). */
@@ -882,6 +997,9 @@ static PyObject* f64_into_list(PyObject* self, PyObject* args) {
 
 static PyMethodDef methods[] = {
     {"all_ints", all_ints, METH_VARARGS, "list -> all items are ints (isinstance)"},
+    {"mt_share_draws", mt_share_draws, METH_VARARGS,
+     "MT19937 state (625-tuple), uint32 bit lengths [n], draws, int64 out [draws, n, 2] -> the state after: "
+     "random.randint(0, 2**bl) element-major, as the reference's AdditiveSecret.split draws"},
     {"all_ints_lists", all_ints_lists, METH_VARARGS,
      "list of lists -> -1, or the first list holding a non-int (isinstance)"},
     {"floats_to_f64", floats_to_f64, METH_VARARGS, "list of floats -> float64 buffer; -1 or first bad index"},

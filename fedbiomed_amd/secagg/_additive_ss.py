@@ -10,15 +10,20 @@ per-element vector use -- and `fbm_ass_split_wide` / `fbm_ass_reconstruct_wide`
 the key setup splits (`node/secagg/_secagg_setups.py:248-268`) and the server-key shares the
 researcher sums (`researcher/secagg/_secagg_context.py:380-382`).
 
-The reference draws shares from Python's MT19937 (`random.randint`); here they come from a
-counter-based ChaCha20 stream.  What both guarantee -- and what the tests pin -- is the
-contract: the shares sum exactly to the secret, the first n-1 lie in [0, 2**bit_length].
+The reference draws shares from Python's MT19937 (`random.randint`, `_additive_ss.py:96`).  An int
+secret -- the JL key setup's only use (`node/secagg/_secagg_setups.py:248-249`) -- draws its n-1 shares
+from that same stream, call for call, so a seeded run gives the reference's shares and leaves `random` in
+the reference's state; the last share (secret - sum) is computed on the device.  A vector secret's
+shares come from a counter-based ChaCha20 stream on the device (100M x 16 shares in milliseconds; MT19937
+is sequential).  What both guarantee -- and what the tests pin -- is the contract: the shares sum exactly
+to the secret, the first n-1 lie in [0, 2**bit_length].
 
 `split_tensor` / `reconstruct_tensor` are the device fast path (int64 tensors in HBM).
 """
 
 from __future__ import annotations
 
+import random
 from math import log2
 from typing import List, Optional, Union
 
@@ -55,7 +60,12 @@ class AdditiveSecret:
     def secret(self) -> Union[List, int]:
         return self._secret
 
-    def split(self, num_shares: int, bit_length: Optional[int] = None) -> "AdditiveShares":
+    def split(self, num_shares: int, bit_length: Optional[int] = None,
+              reference_rng: bool = False) -> "AdditiveShares":
+        """`reference_rng` (an extension): a vector secret's shares drawn from the reference's own stream
+        (the global `random`'s MT19937, element by element, D.reference_share_draws) instead of the
+        device's ChaCha20 -- seeded, the reference's shares exactly; the last share is still computed on
+        the device.  An int secret always draws from that stream."""
         if num_shares <= 0:
             raise FedbiomedValueError("Number of shares must be greater than 0")
         values = [self._secret] if isinstance(self._secret, int) else list(self._secret)
@@ -65,6 +75,16 @@ class AdditiveSecret:
                     raise FedbiomedValueError("Bit length must be greater or equal than the secret's bit length")
         if not values:
             return AdditiveShares([AdditiveShare([]) for _ in range(num_shares)])
+        if isinstance(self._secret, int):  # the reference's own draws (_additive_ss.py:94-98), then secret - sum
+            bl = self._secret.bit_length() if bit_length is None else bit_length
+            draws = [random.randint(0, 2**bl) for _ in range(num_shares - 1)]
+            last = _reconstruct([[self._secret]] + [[-d] for d in draws])[0]
+            return AdditiveShares([AdditiveShare(d) for d in draws] + [AdditiveShare(last)])
+        if reference_rng:
+            bls = [v.bit_length() if bit_length is None else bit_length for v in values]
+            rows = D.reference_share_draws(bls, num_shares - 1)
+            last = _reconstruct([values] + [[-d for d in r] for r in rows])
+            return AdditiveShares([AdditiveShare(r) for r in rows] + [AdditiveShare(last)])
         if _in_64bit_domain(values) and (bit_length is None or bit_length <= 64):
             unsigned = _device_domain(values)
             host = np.array([v if not unsigned or v < 2**63 else v - 2**64 for v in values], dtype=np.int64)

@@ -1,9 +1,9 @@
 """Additive secret sharing of vectors (reference secagg/_additive_ss.py).
 
-Contract (the reference draws from MT19937, which is not part of it): split shares sum
-exactly to the secret and the first n-1 lie in [0, 2**bit_length] (bit_length = the
-secret's bit length unless given); reconstruct is an exact column sum -- checked against
-the reference's own shares in tests/golden/ass.json.
+Contract: split shares sum exactly to the secret and the first n-1 lie in [0, 2**bit_length]
+(bit_length = the secret's bit length unless given); reconstruct is an exact column sum -- checked
+against the reference's own shares in tests/golden/ass.json.  An int secret's shares are the
+reference's own MT19937 draws (seeded as the fixture was made); a vector's come from ChaCha20.
 """
 
 import numpy as np
@@ -50,6 +50,43 @@ def dev():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return D.device()
+
+
+@pytest.mark.gpu
+def test_int_split_is_the_reference_stream(golden, dev):
+    """An int secret (the key setup's use) draws its shares from Python's MT19937 call for call: seeded as
+    tools/gen_golden.py seeded the reference, the shares are the reference's own (the 64- and 2040-bit
+    cases of tests/golden/ass.json), and `random` is left where the reference leaves it; a vector secret
+    does with reference_rng=True (the fixture's list case)."""
+    import random
+
+    from fedbiomed_amd.secagg import AdditiveSecret
+
+    cases = [c for c in golden["ass"]["cases"] if not isinstance(c["secret"], list)]
+    assert len(cases) == 2
+    for case in cases:
+        secret, n = I(case["secret"]), len(case["shares"])
+        random.seed(99)
+        assert AdditiveSecret(secret).split(n).to_list() == [I(s) for s in case["shares"]]
+        after = random.getstate()
+        random.seed(99)
+        for _ in range(n - 1):
+            random.randint(0, 2**secret.bit_length())
+        assert random.getstate() == after
+    # a vector secret with reference_rng (an extension): the reference's list case, share for share
+    (case,) = [c for c in golden["ass"]["cases"] if isinstance(c["secret"], list)]
+    random.seed(99)
+    got = AdditiveSecret([I(v) for v in case["secret"]]).split(len(case["shares"]), reference_rng=True)
+    assert got.to_list() == [[I(x) for x in s] for s in case["shares"]]
+    random.seed(3)  # and wide, negative and bit_length-given vectors keep the contract
+    vals = [2**200 + 1, -(2**90), 0, 7]
+    sh = AdditiveSecret(vals).split(5, reference_rng=True)
+    assert sh.reconstruct() == vals and all(0 <= v <= 2**abs(x).bit_length() for s in sh.to_list()[:-1]
+                                            for v, x in zip(s, vals))
+    assert AdditiveSecret([5, 6]).split(3, bit_length=70, reference_rng=True).reconstruct() == [5, 6]
+    random.seed(7)
+    assert AdditiveSecret(-12345).split(1).to_list() == [-12345]
+    assert AdditiveSecret(2**70).split(3, bit_length=100).reconstruct() == 2**70
 
 
 @pytest.mark.gpu

@@ -400,3 +400,27 @@ def test_all_ints_lists(conv, monkeypatch, threads):
             assert conv.all_ints_lists(l2) == u
     with pytest.raises(TypeError):
         conv.all_ints_lists([[1], (2,)])
+
+
+def test_reference_share_draws_are_python_random():
+    """AdditiveSecret.split(reference_rng=True)'s draws: CPython's MT19937 run in C from random.getstate() --
+    the same values random.randint(0, 2**bl) gives, element-major (the reference's loop order), for bit
+    lengths around every 32-bit word boundary, and `random` left in the same state; past 126 bits the
+    module hands over to `random` itself."""
+    import random as R
+
+    bls = [0, 1, 2, 5, 31, 32, 33, 63, 64, 65, 95, 96, 97, 126, 13, 13, 13]
+    for seed in (99, 12345):
+        R.seed(seed)
+        ref = [[R.randint(0, 2**bl) for _ in range(4)] for bl in bls]
+        ref_state = R.getstate()
+        R.seed(seed)
+        got = D.reference_share_draws(bls, 4)
+        assert got == [[c[j] for c in ref] for j in range(4)]
+        assert R.getstate() == ref_state
+    R.seed(5)
+    a = D.reference_share_draws([127, 3], 2)  # past 126 bits: through `random`
+    R.seed(5)
+    ref = [[R.randint(0, 2**127) for _ in range(2)], [R.randint(0, 2**3) for _ in range(2)]]
+    assert a == [[ref[0][j], ref[1][j]] for j in range(2)]
+    assert D.reference_share_draws([], 3) == [[], [], []] and D.reference_share_draws([4], 0) == []
