@@ -531,12 +531,15 @@ def u64_into_pool(pool: list, arr: np.ndarray) -> list:
     return pool
 
 
-def limbs_into_pool(pool: list, arr: np.ndarray) -> list:
-    """int_pool's ints take the [n, 64] uint32 limb rows' values in place (host threads); the pool -- or
-    a fresh list when a pool int is also held elsewhere (it is then never written)."""
+def limbs_into_pool(pool: list, arr: np.ndarray, off: int = 0, strict: bool = False) -> list:
+    """int_pool's ints [off, off + n) take the [n, 64] uint32 limb rows' values in place (host threads); the
+    pool.  When a pool int is also held elsewhere nothing is written and, unless `strict` (a caller that
+    fills a private pool by slices: ValueError), a fresh list of the rows' values is returned instead."""
     try:
-        _pyconv().words_into_pool(pool, np.ascontiguousarray(arr, dtype=np.uint32), 256)
+        _pyconv().words_into_pool(pool, np.ascontiguousarray(arr, dtype=np.uint32), 256, off)
     except ValueError:
+        if strict:
+            raise
         return limbs_to_ints(arr)
     return pool
 

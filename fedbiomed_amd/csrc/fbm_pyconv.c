@@ -24,7 +24,7 @@
  *   set_conv_threads(t)             -> the threaded loops' default host-thread count (returns the old one)
  *   all_ints_lists(lists)           -> -1, or the first list holding a non-int (every list in one pass)
  *   int_pool(n, nb)                 -> n fresh ints with room for nb-byte values: an output list made ahead
- *   words_into_pool(pool, buf, nb)  -> the pool's ints take buf's values in place
+ *   words_into_pool(pool, buf, nb[, off]) -> the pool's ints [off, ...) take buf's values in place
  *
  * `out` is any writable C-contiguous buffer (a numpy array) of the exact size.  Host code,
  * not part of the GPU compute path: the arithmetic stays in the HIP library.
@@ -855,23 +855,24 @@ static void* pool_range(void* arg) {
 }
 #endif
 
-/* The values of buf (n x nb bytes, unsigned little-endian, nb the pool's width) into int_pool's ints, in
- * place, on host threads while this thread holds the GIL.  Every item must be an exact int that only the
+/* The values of buf (n x nb bytes, unsigned little-endian, nb the pool's width) into int_pool's ints
+ * [off, off + n), in place, on host threads while this thread holds the GIL.  Every item must be an exact int that only the
  * list holds (refcount 1): the pool's own, never handed out -- anything else is a ValueError and nothing
  * is written. */
 static PyObject* words_into_pool(PyObject* self, PyObject* args) {
     PyObject* lst;
     Py_buffer view;
-    Py_ssize_t nb;
-    if (!PyArg_ParseTuple(args, "O!y*n", &PyList_Type, &lst, &view, &nb)) return NULL;
+    Py_ssize_t nb, off = 0;
+    if (!PyArg_ParseTuple(args, "O!y*n|n", &PyList_Type, &lst, &view, &nb, &off)) return NULL;
 #if FBM_DIGITS_FAST
-    const Py_ssize_t n = PyList_GET_SIZE(lst);
-    if (nb <= 0 || nb % 4 || view.len != n * nb || ((uintptr_t)view.buf & 3)) {
+    const Py_ssize_t n = nb > 0 ? view.len / nb : 0;
+    if (nb <= 0 || nb % 4 || view.len % nb || ((uintptr_t)view.buf & 3) || off < 0 ||
+        off + n > PyList_GET_SIZE(lst)) {
         PyBuffer_Release(&view);
-        PyErr_SetString(PyExc_ValueError, "buffer does not hold the pool's values as whole 32-bit words");
+        PyErr_SetString(PyExc_ValueError, "buffer does not hold whole 32-bit-word values for the pool at that offset");
         return NULL;
     }
-    PyObject** items = ((PyListObject*)lst)->ob_item;
+    PyObject** items = ((PyListObject*)lst)->ob_item + off;
     for (Py_ssize_t i = 0; i < n; ++i) {
         if (!PyLong_CheckExact(items[i]) || Py_REFCNT(items[i]) != 1) {
             PyBuffer_Release(&view);
@@ -897,7 +898,7 @@ static PyObject* words_into_pool(PyObject* self, PyObject* args) {
     PyBuffer_Release(&view);
     Py_RETURN_NONE;
 #else
-    (void)lst, (void)nb;
+    (void)lst, (void)nb, (void)off;
     PyBuffer_Release(&view);
     PyErr_SetString(PyExc_ValueError, "no int pools in this build (FBM_DIGITS_FAST=0)");
     return NULL;
@@ -1011,7 +1012,7 @@ static PyMethodDef methods[] = {
     {"float_pool", float_pool, METH_VARARGS, "n -> n distinct 0.0 floats held by the list only"},
     {"int_pool", int_pool, METH_VARARGS, "n, nb -> n fresh ints with room for nb-byte values (None: not this build)"},
     {"words_into_pool", words_into_pool, METH_VARARGS,
-     "int_pool list, buffer of n nb-byte LE values, nb -> None (each int's value written in place)"},
+     "int_pool list, buffer of n nb-byte LE values, nb[, offset] -> None (each int's value written in place)"},
     {"ints_to_bytes_held", ints_to_bytes_held, METH_VARARGS,
      "lists, lo, hi, n, out -> -1 or first bad flat index (host threads, GIL held, no pins)"},
     {"f64_into_list", f64_into_list, METH_VARARGS, "list, offset, float64 buffer -> None (fills the list)"},

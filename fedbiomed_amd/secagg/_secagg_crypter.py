@@ -195,10 +195,12 @@ class SecaggCrypter:
         else:
             stripes = D.list_encrypt_stripes(n_ct, dev)
             if len(stripes) == 1:
-                ct = self.encrypt_tensor(num_nodes, current_round, x, key, biprime, clipping_range, weight,
-                                         target_range)
-                packed = D.to_host(ct).numpy().view(np.uint32)
-                out = D.limbs_to_ints(packed)
+                with D.deferred_checks():  # (checked at the exit, once the ciphertexts are back)
+                    ct = self.encrypt_tensor(num_nodes, current_round, x, key, biprime, clipping_range, weight,
+                                             target_range)
+                    pool = D.int_pool(n_ct)  # the output's ints, made while the GPU exponentiates
+                    packed = D.to_host(ct).numpy().view(np.uint32)
+                out = D.limbs_into_pool(pool, packed, strict=True) if pool is not None else D.limbs_to_ints(packed)
             else:
                 packed, out = self._encrypt_overlapped(num_nodes, current_round, x, key, biprime, clipping_range,
                                                        weight, target_range, stripes, cr)
@@ -211,10 +213,11 @@ class SecaggCrypter:
                             stripes, cr):
         """The list API's encrypt as ct_offset stripes (one per full one-lane round, the partial round
         last), issued back to back on the current stream; each stripe's ciphertexts go to a pinned host
-        buffer in stream order, right behind its kernels, and the host builds the Python ints of stripe k
-        while the GPU exponentiates stripe k + 1 (the ciphertext of index k depends only on k: the
-        stripes concatenate bit for bit to the unsplit call's).  One status check for the whole call (its
-        clipping warning once)."""
+        buffer in stream order, right behind its kernels.  While the GPU exponentiates stripe 0 the host
+        makes the output's int objects (`int_pool`), then writes stripe k's values into them while the GPU
+        exponentiates stripe k + 1 (the ciphertext of index k depends only on k: the stripes concatenate
+        bit for bit to the unsplit call's).  One status check for the whole call (its clipping warning
+        once)."""
         dev, n = x.device, x.numel()
         host = D.host_empty((stripes[-1][1], 64), torch.int32)
         packed = host.numpy().view(np.uint32)
@@ -230,10 +233,14 @@ class SecaggCrypter:
                 ev = torch.cuda.Event()
                 ev.record(main)
                 done.append(ev)
-            out = []
+            pool = D.int_pool(stripes[-1][1])  # the output's ints, made while the GPU exponentiates stripe 0
+            out = pool if pool is not None else []
             for (c0, c1), ev in zip(stripes, done):
                 ev.synchronize()
-                out += D.limbs_to_ints(packed[c0:c1])
+                if pool is not None:
+                    D.limbs_into_pool(pool, packed[c0:c1], c0, strict=True)
+                else:
+                    out += D.limbs_to_ints(packed[c0:c1])
         return packed, out
 
     def prepare_encrypt(self, current_round: int, num_nodes: int, key: int, biprime: int, num_params: int,

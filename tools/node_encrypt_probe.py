@@ -33,7 +33,7 @@ def main():
     key, P, tau = W.jl_user_key(1), 8, 3
     jc.encrypt(P, tau, xl[:4096], key, W.BIPRIME0, weight=1)  # warm-up
     marks = []
-    orig_ev, orig_conv = torch.cuda.Event.synchronize, D.limbs_to_ints
+    orig_ev, orig_conv, orig_pool = torch.cuda.Event.synchronize, D.limbs_to_ints, D.limbs_into_pool
 
     def ev_sync(self):
         orig_ev(self)
@@ -44,17 +44,22 @@ def main():
         marks.append(("converted", time.perf_counter()))
         return r
 
+    def into_pool(*a, **k):
+        r = orig_pool(*a, **k)
+        marks.append(("converted", time.perf_counter()))
+        return r
+
     out = None
     for rep in range(args.reps + 1):
         out = None  # the previous call's ints freed outside the clock (a node keeps its result)
         marks.clear()
-        torch.cuda.Event.synchronize, D.limbs_to_ints = ev_sync, conv
+        torch.cuda.Event.synchronize, D.limbs_to_ints, D.limbs_into_pool = ev_sync, conv, into_pool
         try:
             t0 = time.perf_counter()
             out = jc.encrypt(P, tau, xl, key, W.BIPRIME0, weight=1)
             t1 = time.perf_counter()
         finally:
-            torch.cuda.Event.synchronize, D.limbs_to_ints = orig_ev, orig_conv
+            torch.cuda.Event.synchronize, D.limbs_to_ints, D.limbs_into_pool = orig_ev, orig_conv, orig_pool
         if rep == 0:
             continue  # (the first full-size call allocates the pinned staging)
         n_ct = len(out)
