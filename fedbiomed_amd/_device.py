@@ -119,7 +119,9 @@ class deferred_checks:
         # each), not the whole device: other threads' work keeps running
         for _, _, ev in pending:
             ev.synchronize()
-        host = torch.stack([st for st, _, _ in pending]).cpu().numpy()  # one copy for all of them
+        # the status words were copied to pinned host memory behind their kernels (_check_stats_or_defer):
+        # no device work and no copy here; a device tensor (adopted from elsewhere) is copied now
+        host = np.stack([(st if st.device.type == "cpu" else st.cpu()).numpy() for st, _, _ in pending])
         if self._merge:
             assert len({nodes for _, (nodes, _), _ in pending}) == 1 and all(p is None for _, (_, p), _ in pending)
             row = host[:1].copy()
@@ -168,8 +170,12 @@ def _check_stats_or_defer(stats: torch.Tensor, lom_nodes: int = 0, post: Optiona
     reference's order, e.g. LOM's round-counter overflow after its overflow guard)."""
     active = deferred_checks._stack()
     if active:
+        if stats.device.type != "cpu":  # to pinned host memory on the current stream, right behind the
+            host = host_empty(stats.shape, stats.dtype)  # kernels that write it: the exit reads it without
+            host.copy_(stats, non_blocking=True)  # a copy of its own (one synchronisation less per call)
+            stats = host
         ev = torch.cuda.Event()
-        ev.record()  # on the current stream, right after the kernels that write `stats`
+        ev.record()  # on the current stream, after the kernels (and the copy)
         active[-1].append((stats, (lom_nodes, post), ev))
     else:
         _check_stats(stats, lom_nodes)
@@ -454,7 +460,7 @@ def u64_to_device(rows, dev=None) -> torch.Tensor:
         host = host_empty((len(rows), len(rows[0])), torch.int64)
         buf = host.numpy()
         if all(_pyconv().ints_to_bytes(r, 8, buf[u]) < 0 for u, r in enumerate(rows)):
-            return host.to(dev)
+            return host.to(dev, non_blocking=True)  # stream-ordered (the pinned block is held until it lands)
     arr = np.array(rows, dtype=np.uint64)  # anything else, with numpy's exact errors
     return torch.from_numpy(arr.view(np.int64)).to(dev)
 
@@ -650,7 +656,7 @@ def lom_aggregate(Y: torch.Tensor, total_weight: int, clip=None, target=None,
     st = _stats(dev)
     _call(lib.fbm_lom_aggregate, _ptr(Y), P, n, int(total_weight), negc, step, _ptr(out), _ptr(sums), _ptr(st),
           _stream())
-    _check_stats(st)
+    _check_stats_or_defer(st)  # (inside deferred_checks: at its exit, e.g. the list aggregate's, after the D2H)
     return out, sums
 
 

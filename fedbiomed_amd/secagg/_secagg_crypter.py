@@ -183,7 +183,7 @@ class SecaggCrypter:
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value} Error during parameter encryption. {exp}") from exp
         dev = D.device()
-        x = host.to(dev)
+        x = host.to(dev, non_blocking=True)  # stream-ordered before the encrypt's kernels
         n_ct = (x.numel() + cr - 1) // cr
         prep = self._take_prepared_encrypt(current_round, num_nodes, key, biprime, target_range, n_ct, dev)
         if prep is not None:  # prepare_encrypt's factor: one product per ciphertext, no exponentiation
@@ -649,10 +649,11 @@ class SecaggLomCrypter(SecaggCrypter):
         if not params:
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value} Error during parameter encryption. max() arg is an empty sequence")
-        x = host.to(D.device())
-        y = self.encrypt_tensor(current_round, node_id, x, pairwise_secrets, node_ids, clipping_range, weight,
-                                target_range)
-        packed = D.to_host(y).numpy().view(np.uint64)
+        with D.deferred_checks():  # the status word checked once the masked vector is back (one sync per call)
+            x = host.to(D.device(), non_blocking=True)
+            y = self.encrypt_tensor(current_round, node_id, x, pairwise_secrets, node_ids, clipping_range, weight,
+                                    target_range)
+            packed = D.to_host(y).numpy().view(np.uint64)
         pool = self._take_enc_pool(current_round, node_id, packed.shape[0])
         out = D.u64_into_pool(pool, packed) if pool is not None else packed.tolist()
         if wire.enabled():
@@ -675,9 +676,10 @@ class SecaggLomCrypter(SecaggCrypter):
                 f"is not successful: {e}") from e
         if Y.dim() != 2 or Y.shape[1] == 0:
             return []
-        out = self.aggregate_tensor(Y, total_sample_size, clipping_range, target_range)
+        with D.deferred_checks():  # the status word checked once the averages are back
+            out = self.aggregate_tensor(Y, total_sample_size, clipping_range, target_range)
+            res_h = D.to_host(out).numpy()
         logger.info(f"Aggregating {len(params)} parameters from {num_nodes} nodes.")
-        res_h = D.to_host(out).numpy()
         pool = getattr(self, "_lom_agg_pool", None)
         if pool is not None and len(pool) == res_h.shape[0]:  # prepare_aggregate's floats, written in place
             self._lom_agg_pool = None
