@@ -15,7 +15,6 @@ Besides the list API, `encrypt_tensor` / `aggregate_tensor` take device tensors 
 from __future__ import annotations
 
 import logging
-import os
 import secrets
 import time
 from typing import Dict, List, Optional, Union
@@ -85,21 +84,6 @@ def _prep_tag(current_round, num_nodes, key, biprime, target_range) -> Optional[
         b = v.to_bytes(v.bit_length() // 8 + 1, "little", signed=True)
         h.update(len(b).to_bytes(8, "little") + b)
     return h.digest()
-
-
-def _pipeline_stripes(stripes, factors):
-    """A prepared aggregate's stripes cut to at most FBM_PREP_STRIPE_CT ciphertexts each (default 32 768), with
-    views of their factors: with every factor computed ahead nothing on the GPU sets the stripe size, and
-    finer stripes overlap more of the ints' conversion with the H2D of the stripe before (PCIe ~57 GB/s)."""
-    step = max(1, int(os.environ.get("FBM_PREP_STRIPE_CT", 1 << 15)))
-    fine, fine_f = [], []
-    for (c0, c1), f in zip(stripes, factors):
-        m = max(1, -(-(c1 - c0) // step))
-        for j in range(m):
-            a, b = c0 + (c1 - c0) * j // m, c0 + (c1 - c0) * (j + 1) // m
-            fine.append((a, b))
-            fine_f.append(None if f is None else f[a - c0:b - c0])
-    return fine, fine_f
 
 
 class SecaggCrypter:
@@ -364,9 +348,8 @@ class SecaggCrypter:
             # the aggregate's pinned staging buffers, allocated now and handed back to torch's caching host
             # allocator, which gives them to the aggregate: page-locking ~1 GB is the first call's largest
             # extra cost (315-322 ms against 172 ms warm at 10M x 8)
-            fine, _ = _pipeline_stripes(stripes, [None] * len(stripes))
-            warm = [D.host_empty((num_nodes, c1 - c0, 64), torch.int32) for c0, c1 in fine]
-            warm += [D.host_empty(((c1 - c0) * cr,), torch.float64) for c0, c1 in fine]
+            warm = [D.host_empty((num_nodes, c1 - c0, 64), torch.int32) for c0, c1 in stripes]
+            warm += [D.host_empty(((c1 - c0) * cr,), torch.float64) for c0, c1 in stripes]
             del warm
             # and its output list: the float objects made now, their values written in place by the
             # aggregate (making 10M Python floats is most of its host time, ~100 ms)
@@ -428,8 +411,7 @@ class SecaggCrypter:
                     prep = self._take_prepared(current_round, num_nodes, key, biprime, target_range, n_ct0,
                                                D.device())
                     if prep is not None:  # prepare_aggregate's factors (every stripe's) and output list
-                        stripes, factors = _pipeline_stripes(prep[0], prep[1])
-                        pool = prep[2]
+                        stripes, factors, pool = prep[0], list(prep[1]), prep[2]
                     else:
                         stripes = D.list_encrypt_stripes(n_ct0, D.device())
                         factors = [None] * len(stripes)
