@@ -3,6 +3,8 @@
  * side in the loop.  It runs both crypters' device round trip -- every party's encrypt, then the
  * aggregate -- on device buffers it allocates itself with the HIP runtime, and writes the ciphertexts,
  * masked vectors and averages for tests/test_c_client.py to compare with the oracle and the Python API.
+ * The Joye-Libert round also runs with every factor computed ahead (fbm_jl_decrypt_factor ->
+ * fbm_jl_encrypt_factor / fbm_jl_aggregate_factor, ABI 5), which must give the same bytes.
  *
  *   fbm_c_roundtrip --abi          prints the ABI version (touches no device)
  *   fbm_c_roundtrip IN OUT         IN: the case (layout below, written by tests/test_c_client.py)
@@ -136,6 +138,52 @@ int main(int argc, char** argv) {
            "fbm_jl_aggregate");
     hip_ok(hipStreamSynchronize(stream), "sync");
     stats_ok(d_stats, 0, "fbm_jl_aggregate status");
+
+    /* the same round with every factor computed ahead (ABI 5): each party's H(t_k)^key by
+     * fbm_jl_decrypt_factor with its own key, then fbm_jl_encrypt_factor; the server's by
+     * fbm_jl_decrypt_factor, then fbm_jl_aggregate_factor -- the same bytes as above, or exit 1 */
+    {
+        uint32_t* d_f = dalloc((size_t)n_ct * 64 * 4);
+        uint32_t* d_cts2 = dalloc((size_t)P * n_ct * 64 * 4);
+        double* d_avg2 = dalloc(n_out * sizeof(double));
+        const size_t ct_bytes = (size_t)P * n_ct * 64 * 4;
+        for (uint32_t p = 0; p < P; ++p) {
+            fbm_ok(fbm_jl_decrypt_factor(n_ct, biprime, keys + (size_t)p * 64, key_negative[p], jl_tau, 0, d_f, d_ws,
+                                         d_stats, stream),
+                   "fbm_jl_decrypt_factor (party key)");
+            hip_ok(hipStreamSynchronize(stream), "sync");
+            stats_ok(d_stats, 0, "fbm_jl_decrypt_factor status");
+            fbm_ok(fbm_jl_encrypt_factor(d_x + (size_t)p * n, FBM_F32, n, clip, two_clip, target_f, target_m1, weight[p],
+                                         (int)es, (int)cr, biprime, d_f, d_cts2 + (size_t)p * n_ct * 64, d_ws, d_stats,
+                                         stream),
+                   "fbm_jl_encrypt_factor");
+            hip_ok(hipStreamSynchronize(stream), "sync");
+            stats_ok(d_stats, 0, "fbm_jl_encrypt_factor status");
+        }
+        fbm_ok(fbm_jl_decrypt_factor(n_ct, biprime, server_key, sk_negative, jl_tau, 0, d_f, d_ws, d_stats, stream),
+               "fbm_jl_decrypt_factor (server key)");
+        hip_ok(hipStreamSynchronize(stream), "sync");
+        stats_ok(d_stats, 0, "fbm_jl_decrypt_factor status");
+        fbm_ok(fbm_jl_aggregate_factor(d_cts2, (int)P, n_ct, (int)es, (int)cr, n_out, biprime, d_f, total_weight,
+                                       neg_clip, step, d_avg2, NULL, d_ws, d_stats, stream),
+               "fbm_jl_aggregate_factor");
+        hip_ok(hipStreamSynchronize(stream), "sync");
+        stats_ok(d_stats, 0, "fbm_jl_aggregate_factor status");
+        unsigned char* a = xmalloc(ct_bytes);
+        unsigned char* b = xmalloc(ct_bytes);
+        hip_ok(hipMemcpy(a, d_cts, ct_bytes, hipMemcpyDeviceToHost), "D2H");
+        hip_ok(hipMemcpy(b, d_cts2, ct_bytes, hipMemcpyDeviceToHost), "D2H");
+        if (memcmp(a, b, ct_bytes) != 0) die("factor ahead", "ciphertexts differ from fbm_jl_encrypt's");
+        free(a), free(b);
+        a = xmalloc(n_out * sizeof(double));
+        b = xmalloc(n_out * sizeof(double));
+        hip_ok(hipMemcpy(a, d_jl_avg, n_out * sizeof(double), hipMemcpyDeviceToHost), "D2H");
+        hip_ok(hipMemcpy(b, d_avg2, n_out * sizeof(double), hipMemcpyDeviceToHost), "D2H");
+        if (n_out && memcmp(a, b, n_out * sizeof(double)) != 0) die("factor ahead", "averages differ from fbm_jl_aggregate's");
+        free(a), free(b);
+        void* bufs[] = {d_f, d_cts2, d_avg2};
+        for (size_t k = 0; k < 3; ++k) hip_ok(hipFree(bufs[k]), "hipFree");
+    }
 
     /* LOM: each party's masked vector, then the column sums' average */
     for (uint32_t p = 0; p < P; ++p) {

@@ -3,7 +3,9 @@ the client links the in-tree library and agrees on the ABI (CPU), and -- on the 
 allocates its own device buffers runs both crypters' round trip (every party's fbm_jl_encrypt /
 fbm_lom_protect, then fbm_jl_aggregate / fbm_lom_aggregate) with results bit-identical to the oracle
 (oracle/secagg_oracle.py, pinned by tests/golden/) and to the Python API on the same inputs.  This is the
-boundary a non-Python host (cgo, JNI, N-API) would bind; INTEGRATION.md shows the ctypes one."""
+boundary a non-Python host (cgo, JNI, N-API) would bind; INTEGRATION.md shows the ctypes one.  The client
+also runs the Joye-Libert round with every factor computed ahead (fbm_jl_decrypt_factor ->
+fbm_jl_encrypt_factor / fbm_jl_aggregate_factor, ABI 5) and exits non-zero unless its bytes are the same."""
 
 import os
 import random
