@@ -17,6 +17,12 @@ T_agg (the aggregate alone: decryption factor + combine), P*N/T_enc and N/T_agg 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scheme jl|lom] [--elements 10000000]
                     [--parties 8] [--weak]
 
+At N = 1 the line also carries `end_to_end` (SURVEY 8(f), rank 0 only, outside the headline's clock): the
+same work from pinned host memory, the reference's list API (one node's encrypt at 1M / 10M, the
+researcher's aggregate at 1M x 8 and at the metric size, JL and LOM list round trips), each also after the
+extensions that issue a call's work ahead (`prepare_encrypt` / `prepare_aggregate`: the factors, the output
+objects), and the msgpack wire legs; and `cpu_baseline` (the oracle on a bounded sample, one host core).
+
 With --gpus N > 1 and no torch.distributed.run environment, bench.py starts the N rank
 processes itself (before anything touches a GPU) and relays rank 0's line.
 """
