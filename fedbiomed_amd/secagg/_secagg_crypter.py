@@ -254,8 +254,9 @@ class SecaggCrypter:
         ciphertexts, bit for bit.  Other calls of that round leave it, a call of another round drops
         it; a device condition of the early work is raised by the encrypt that takes it.  It also warms
         the encrypt's pinned staging buffers and makes its output list's int objects, whose values the
-        encrypt writes in place (making 333 334 ciphertext-sized ints is ~17 ms).  Best effort: False (nothing prepared) where the encrypt
-        would refuse the arguments, for an even N or N = 1, or with a library older than ABI 5.  The
+        encrypt writes in place (making 333 334 ciphertext-sized ints is ~17 ms).  Best effort: False
+        (nothing prepared) where the encrypt would refuse the arguments, for an even N or N = 1, or with a
+        library older than ABI 5.  The
         key itself is not kept, only a SHA-256 tag of it.  The preparation is the class's, not this
         instance's (one at a time): the node's encrypt runs on a fresh SecaggCrypter."""
         SecaggCrypter._enc_prep = None
@@ -294,7 +295,8 @@ class SecaggCrypter:
 
     def _take_prepared_encrypt(self, current_round, num_nodes, key, biprime, target_range, n_ct, dev):
         """(prepare_encrypt's factor, its int pool or None) when they are this call's (the factor waited for
-        on the current stream, its status words adopted; the preparation is then spent), else None.  A call of another round drops it."""
+        on the current stream, its status words adopted; the preparation is then spent), else None.  A call
+        of another round drops it."""
         prep = SecaggCrypter._enc_prep
         if prep is None:
             return None
@@ -450,7 +452,8 @@ class SecaggCrypter:
         float64 D2H in stream order, then the next stripe's factor.  The host converts every stripe's ints
         first (host threads, one GIL-held C call each: no per-item pins) and issues its GPU work, then makes
         the output list and the last stripe's float objects while the GPU runs the factors (the 10M-element
-        float list is the call's largest host cost) and writes each stripe's values as its D2H lands.  Stripe outputs: elements [c0 cr, c1 cr) capped by
+        float list is the call's largest host cost) and writes each stripe's values as its D2H lands.
+        Stripe outputs: elements [c0 cr, c1 cr) capped by
         num_expected_params, as the unsplit decode (_jls.py:146-167); a stripe past it still runs its
         checks (the unsplit call's errors).  `pool`: prepare_aggregate's output list (its floats made
         ahead, written in place here) when it has this call's length."""
