@@ -359,6 +359,14 @@ def test_int_pool_filled_in_place():
         m.words_into_pool([0, 5, 2**100], rows[:3].tobytes(), 256)  # not a pool
     with pytest.raises(ValueError):
         m.words_into_pool(D.int_pool(2), rows[:3].tobytes(), 256)  # size
+    # by slices (the striped encrypt): rows [3, 7) at offset 3, the rest left at 0; past the end refused
+    pool3 = D.int_pool(10)
+    assert D.limbs_into_pool(pool3, rows[8:12], 3, strict=True) is pool3
+    assert pool3 == [0, 0, 0] + vals[8:12] + [0, 0, 0]
+    with pytest.raises(ValueError):
+        D.limbs_into_pool(pool3, rows[:4], 7, strict=True)
+    with pytest.raises(ValueError):
+        m.words_into_pool(pool3, rows[:1].tobytes(), 256, -1)
 
 
 def test_int_pool_absent_from_the_portable_build(tmp_path):
