@@ -31,7 +31,7 @@ def load(name):
 
 def load_all():
     return {k: load(k + ".json") for k in ("quantize", "lom", "jl", "ass", "edge", "dh", "jls_api", "crypter_sweep", "even",
-                                           "api_edges", "custom_hash")}
+                                           "api_edges", "custom_hash", "ass_stream")}
 
 
 def custom_hashes():

@@ -89,6 +89,42 @@ def test_int_split_is_the_reference_stream(golden, dev):
     assert AdditiveSecret(2**70).split(3, bit_length=100).reconstruct() == 2**70
 
 
+def test_reference_stream_draws_match_fixture(golden):
+    """CPU: the draws alone (D.reference_share_draws, the C MT19937 replay) against the reference's own
+    shares from tests/golden/ass_stream.json, seeded as the reference was, and the stream's next 64 bits."""
+    import random
+
+    for case in golden["ass_stream"]["cases"]:
+        secret = case["secret"]
+        if not isinstance(secret, list):
+            continue  # (an int secret's draws are `random.randint` itself)
+        vals = [I(v) for v in secret]
+        bls = [v.bit_length() if case["bit_length"] is None else case["bit_length"] for v in vals]
+        random.seed(case["seed"])
+        rows = D.reference_share_draws(bls, case["n"] - 1)
+        assert rows == [[I(x) for x in s] for s in case["shares"][:-1]], case["seed"]
+        assert random.getrandbits(64) == I(case["next_getrandbits64"]), case["seed"]
+
+
+@pytest.mark.gpu
+def test_split_reference_stream_fixture(golden, dev):
+    """The reference's seeded splits (tests/golden/ass_stream.json: vectors of mixed widths and signs, a given
+    bit_length, an int secret with bit_length 300, a value past 126 bits) share for share, last share
+    included, and `random` left where the reference left it."""
+    import random
+
+    from fedbiomed_amd.secagg import AdditiveSecret
+
+    for case in golden["ass_stream"]["cases"]:
+        secret = case["secret"]
+        secret = [I(v) for v in secret] if isinstance(secret, list) else I(secret)
+        random.seed(case["seed"])
+        sh = AdditiveSecret(secret).split(case["n"], case["bit_length"], reference_rng=True)
+        want = [[I(x) for x in s] if isinstance(s, list) else I(s) for s in case["shares"]]
+        assert sh.to_list() == want, case["seed"]
+        assert random.getrandbits(64) == I(case["next_getrandbits64"]), case["seed"]
+
+
 @pytest.mark.gpu
 def test_reconstruct_reference_shares(golden, dev):
     """Reconstruct the reference's own shares (int and list secrets) bit-exactly."""

@@ -271,6 +271,32 @@ def gen_ass(R):
     dump("ass.json", {"cases": out})
 
 
+def gen_ass_stream(R):
+    """The reference's additive shares drawn from a seeded global `random` (MT19937), with the next
+    getrandbits(64) after each split (the stream's continuation): vectors of many widths and signs,
+    a given bit_length, an int secret, a value past 126 bits."""
+    ass = R.ass
+    rng = random.Random(23)
+    cases = [
+        ([rng.getrandbits(rng.choice([1, 7, 31, 32, 33, 63, 64])) for _ in range(300)], 5, None, 7),
+        ([2 ** 70, 5, 0, -3, -(2 ** 40) - 1], 3, None, 11),
+        ([rng.getrandbits(79) for _ in range(50)], 4, 80, 13),
+        (rng.getrandbits(250), 4, 300, 17),
+        ([2 ** 130 + 5, 9], 3, None, 19),
+    ]
+    out = []
+    for secret, n, bl, seed in cases:
+        random.seed(seed)
+        shares = ass.AdditiveSecret(secret).split(n, bl) if bl is not None else ass.AdditiveSecret(secret).split(n)
+        after = random.getrandbits(64)
+        vals = shares.to_list()
+        out.append({"secret": ihex(secret) if isinstance(secret, int) else [ihex(v) for v in secret], "n": n,
+                    "bit_length": bl, "seed": seed,
+                    "shares": [ihex(v) if isinstance(v, int) else [ihex(x) for x in v] for v in vals],
+                    "next_getrandbits64": ihex(after)})
+    dump("ass_stream.json", {"cases": out})
+
+
 def _outcome(fn):
     """{"ok": value} or {"error": type, "msg": str} of one reference call."""
     try:
@@ -1041,6 +1067,9 @@ def main():
         return
     if sys.argv[1:] == ["ves_wide"]:
         gen_ves_wide(R)
+        return
+    if sys.argv[1:] == ["ass_stream"]:
+        gen_ass_stream(R)
         return
     gen_quantize(R)
     gen_lom(R)
