@@ -82,9 +82,10 @@ class EncryptedParams(list):
     def from_packed(cls, scheme: str, packed: np.ndarray) -> "EncryptedParams":
         packed = np.ascontiguousarray(packed)
         if scheme == "jl":
+            from . import _device as D  # (the C conversion module: the ints' digits written on host threads)
+
             packed = packed.view(np.uint32).reshape(-1, 64)
-            b = packed.tobytes()
-            values = [int.from_bytes(b[256 * i:256 * (i + 1)], "little") for i in range(packed.shape[0])]
+            values = D.limbs_to_ints(packed)
         else:
             packed = packed.view(np.uint64).reshape(-1)
             values = packed.tolist()
