@@ -2377,13 +2377,23 @@ int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const Jl
   const int eng = jl_engine_for(n_ct);
   if (eng == FBM_ENGINE_QUAD || eng == FBM_ENGINE_TRIPLE) {
     uint64_t g = (n_ct + group_ct_per_wg(eng) - 1) / group_ct_per_wg(eng);
-    if (g > group_wgs_max()) g = group_wgs_max();
+    // Workgroups launched per CU (each pulls chunks until none are left).  Up to four chunks per CU, two
+    // resident workgroups finish first: the aggregate's 1/4 stripe (83 334 ciphertexts) 43.0 -> 40.8 ms,
+    // 64 512 ciphertexts 33.7 -> 31.1 (triple) and 32.9 -> 30.6 (quad); past that three (100 000: 51.8
+    // against 60.3) -- profiles/r5bm_group_wgs.jsonl.  FBM_GROUP_WGS = 1..3 overrides (A/B).
+    static const uint64_t wgs_env = getenv("FBM_GROUP_WGS") ? (uint64_t)atoi(getenv("FBM_GROUP_WGS")) : 0u;
+    const uint64_t ncu = (uint64_t)device_num_cu();
+    const uint64_t wgs_cu = wgs_env >= 1 && wgs_env <= FBM_GROUP_WGS_PER_CU ? wgs_env : g <= 4 * ncu ? 2u : 3u;
+    if (g > ncu * wgs_cu) g = ncu * wgs_cu;
+    // probe knob (A/B of workgroup placement): extra dynamic LDS per workgroup, e.g. enough to hold a
+    // group launch to two workgroups per CU
+    static const unsigned glds_pad = getenv("FBM_GROUP_LDS_PAD") ? (unsigned)atoi(getenv("FBM_GROUP_LDS_PAD")) : 0u;
     if (eng == FBM_ENGINE_QUAD) {
-      hipLaunchKernelGGL(jl_expg_kernel<4>, dim3((unsigned)g), dim3(FBM_QBLOCK), 0, s, H, n_ct, (uint32_t*)cst,
+      hipLaunchKernelGGL(jl_expg_kernel<4>, dim3((unsigned)g), dim3(FBM_QBLOCK), glds_pad, s, H, n_ct, (uint32_t*)cst,
                          jp.qa.np, ops, sc.n_ops, sc.first, mode, jp.key_is_zero, sc.sbits, nude, table, out, Hc);
       return check_launch("jl_expq_kernel");
     }
-    hipLaunchKernelGGL(jl_expg_kernel<3>, dim3((unsigned)g), dim3(FBM_QBLOCK), 0, s, H, n_ct, (uint32_t*)cst,
+    hipLaunchKernelGGL(jl_expg_kernel<3>, dim3((unsigned)g), dim3(FBM_QBLOCK), glds_pad, s, H, n_ct, (uint32_t*)cst,
                        jp.qa.np, ops, sc.n_ops, sc.first, mode, jp.key_is_zero, sc.sbits, nude, table, out, Hc);
     return check_launch("jl_expt_kernel");
   }
