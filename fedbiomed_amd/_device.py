@@ -451,18 +451,25 @@ def floats_to_device(params: Sequence[float], dev=None) -> torch.Tensor:
     return host.to(dev)
 
 
-def u64_to_device(rows, dev=None) -> torch.Tensor:
-    """list[int] or list[list[int]] -> int64 tensor holding the uint64 bit patterns.
-    np.array(..., dtype=uint64) raises exactly where the reference's conversion raises."""
-    dev = dev or device()
+def u64_to_host(rows) -> Tuple[torch.Tensor, bool]:
+    """list[int] or list[list[int]] -> host int64 tensor holding the uint64 bit patterns, and whether it
+    is the pinned staging block.  np.array(..., dtype=uint64) raises exactly where the reference's
+    conversion raises."""
     if isinstance(rows, list) and rows and all(isinstance(r, list) for r in rows) and \
             len(set(map(len, rows))) == 1:  # fast path: equal-length rows of in-range ints
         host = host_empty((len(rows), len(rows[0])), torch.int64)
         buf = host.numpy()
         if all(_pyconv().ints_to_bytes(r, 8, buf[u]) < 0 for u, r in enumerate(rows)):
-            return host.to(dev, non_blocking=True)  # stream-ordered (the pinned block is held until it lands)
+            return host, True
     arr = np.array(rows, dtype=np.uint64)  # anything else, with numpy's exact errors
-    return torch.from_numpy(arr.view(np.int64)).to(dev)
+    return torch.from_numpy(arr.view(np.int64)), False
+
+
+def u64_to_device(rows, dev=None) -> torch.Tensor:
+    """u64_to_host's tensor on the device."""
+    dev = dev or device()
+    host, pinned = u64_to_host(rows)
+    return host.to(dev, non_blocking=pinned)  # stream-ordered (the pinned block is held until it lands)
 
 
 def u64_from_device(t: torch.Tensor) -> List[int]:
@@ -621,6 +628,73 @@ def lom_protect(x: torch.Tensor, secrets: Sequence[bytes], signs: Sequence[int],
     else:
         _check_stats_or_defer(st, lom_nodes=n_nodes, post=post)
     return y
+
+
+# Vectors up to this many elements take the one-call host-buffer path of the LOM list API
+# (fbm_lom_protect_host / fbm_lom_aggregate_host): a 1 000-element call is launch-bound.
+LOM_HOST_CALL_MAX = 1 << 16
+
+_host_ws_tls = threading.local()
+
+
+def _host_workspace(nbytes: int, dev) -> torch.Tensor:
+    """This thread's device workspace for the synchronous host-buffer calls (one call at a time per
+    thread; grown, never shrunk)."""
+    ws = getattr(_host_ws_tls, "ws", None)
+    if ws is None or ws.numel() < nbytes or ws.device != dev:
+        ws = _host_ws_tls.ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)
+    return ws
+
+
+def lom_protect_host(x: np.ndarray, secrets: Sequence[bytes], signs: Sequence[int], nonce: bytes, tau: int,
+                     n_nodes: int, clip=None, target=None, weight: int = 1) -> np.ndarray:
+    """lom_protect of a HOST float64 vector into a host uint64 vector, in one synchronous C call
+    (copy in, kernel, copy out); the status words checked before returning, as lom_protect(check_now)."""
+    dev = device()
+    lib = N.load()
+    target = target or SAParameters.TARGET_RANGE
+    c, c2, tf, tm1 = quant_params(clip, target)
+    sec = _secret_block(secrets)
+    sg = np.asarray([1 if s > 0 else -1 for s in signs] or [0], dtype=np.int8)
+    nb = _nonce_block(nonce)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    n = x.shape[0]
+    post = None  # (lom_protect's round-counter domain, in the reference's order)
+    if secrets and n > 0 and not 0 <= tau <= U64_MAX:
+        post = OverflowError("can't convert negative int to unsigned" if tau < 0 else "int too big to convert")
+        tau = 0
+    tau &= U64_MAX
+    blk = host_empty(n + N.STATS_WORDS // 2, torch.int64).numpy()  # pinned: output then status words
+    y, st = blk[:n].view(np.uint64), blk[n:].view(np.uint32)
+    ws = _host_workspace(int(lib.fbm_lom_host_workspace(n, 1)), dev)
+    _call(lib.fbm_lom_protect_host, _np_ptr(x), N.FBM_F64, n, c, c2, tf, tm1, int(weight), _np_ptr(sec),
+          _np_ptr(sg), len(secrets), 0, _np_ptr(nb), int(tau), 0, _np_ptr(y), _np_ptr(st), _ptr(ws), _stream())
+    _check_stats_host(st, n_nodes)
+    if post is not None:
+        raise post
+    return y
+
+
+def lom_aggregate_host(Y: np.ndarray, total_weight: int, clip=None, target=None) -> np.ndarray:
+    """lom_aggregate of a HOST [P, n] uint64 matrix into host float64 averages, in one synchronous C call."""
+    dev = device()
+    lib = N.load()
+    target = target or SAParameters.TARGET_RANGE
+    if total_weight == 0:
+        raise ZeroDivisionError("division by zero")
+    if total_weight < 0 or total_weight > U64_MAX:
+        raise FedbiomedSecaggCrypterError(
+            f"{ErrorNumbers.FB624.value}: total_sample_size must be in [1, 2^64) for the device path")
+    negc, step = dequant_params(clip, target)
+    Y = np.ascontiguousarray(Y)
+    P, n = Y.shape
+    blk = host_empty(n + N.STATS_WORDS // 2, torch.int64).numpy()  # pinned: averages then status words
+    out, st = blk[:n].view(np.float64), blk[n:].view(np.uint32)
+    ws = _host_workspace(int(lib.fbm_lom_host_workspace(n, P)), dev)
+    _call(lib.fbm_lom_aggregate_host, _np_ptr(Y), P, n, int(total_weight), negc, step, _np_ptr(out), _np_ptr(st),
+          _ptr(ws), _stream())
+    _check_stats_host(st)
+    return out
 
 
 def prf_key(secret: bytes, nonce: bytes, tau: int, dev=None) -> bytes:

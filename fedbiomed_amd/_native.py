@@ -29,7 +29,7 @@ def lib_path() -> str:
     return os.environ.get("FBM_LIB_PATH") or LIB_PATH
 
 
-ABI_VERSION = 5  # include/fbm_secagg.h FBM_ABI_VERSION
+ABI_VERSION = 6  # include/fbm_secagg.h FBM_ABI_VERSION
 TAU_LIMBS = 256  # FBM_TAU_LIMBS: the JL round's 32-bit words (< 2^8192)
 FBM_OK = 0
 FBM_E_ARG = -1
@@ -82,6 +82,11 @@ SIGNATURES = {
     "fbm_prf_key": (c_int, [c_vp, c_vp, c_u64, c_vp, c_vp]),
     "fbm_dequantize": (c_int, [c_vp, c_u64, c_dbl, c_dbl, c_vp, c_vp]),
     "fbm_lom_aggregate": (c_int, [c_vp, c_int, c_u64, c_u64, c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp]),
+    # host-buffer LOM calls, synchronous (ABI 6)
+    "fbm_lom_host_workspace": (c_u64, [c_u64, c_int]),
+    "fbm_lom_protect_host": (c_int, [c_vp, c_int, c_u64, c_dbl, c_dbl, c_dbl, c_u64, c_u64, c_vp, c_vp, c_int,
+                                     c_int, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),
+    "fbm_lom_aggregate_host": (c_int, [c_vp, c_int, c_u64, c_u64, c_dbl, c_dbl, c_vp, c_vp, c_vp, c_vp]),
     "fbm_jl_encrypt_workspace": (c_u64, [c_u64]),
     "fbm_jl_aggregate_workspace": (c_u64, [c_u64]),
     # the JL round (tau) is a HOST pointer to TAU_LIMBS limbs (< 2^8192, ABI 3)

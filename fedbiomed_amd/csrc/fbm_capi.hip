@@ -1184,6 +1184,94 @@ int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t tot
   return timed("lom_aggregate", s, [&] { return launch_lom_aggregate(y, n_parties, n, total_weight, neg_clip, step, out, sums, stats, s); });
 }
 
+// ---- host-buffer LOM calls (small vectors): copy in, kernel, copy out, one stream synchronisation ----
+// A 1 000-element list call is launch-bound; these fold its H2D copy, kernel, output and status copies
+// and the wait into one C call (no device tensors made per call on the host side).
+
+static int host_copy(void* dst, const void* src, uint64_t bytes, hipMemcpyKind kind, hipStream_t s, const char* what) {
+  if (!bytes) return FBM_OK;
+  hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, s);
+  if (e != hipSuccess) {
+    set_error("hipMemcpyAsync(%s): %s", what, hipGetErrorString(e));
+    return FBM_E_HIP;
+  }
+  return FBM_OK;
+}
+
+static int host_wait(hipStream_t s) {
+  hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    set_error("hipStreamSynchronize: %s", hipGetErrorString(e));
+    return FBM_E_HIP;
+  }
+  return FBM_OK;
+}
+
+// workspace: input rows | output (n words) immediately followed by the status words, so that a caller
+// whose host output and status words are adjacent too gets both back in one copy
+uint64_t fbm_lom_host_workspace(uint64_t n, int n_parties) {
+  const uint64_t rows = n_parties > 1 ? (uint64_t)n_parties : 1u;
+  return align256(rows * n * 8) + align256(n * 8 + FBM_STATS_WORDS * 4);
+}
+
+static int host_copy_back(void* out_host, const void* out, uint64_t n, uint32_t* stats_host, const uint32_t* st,
+                          hipStream_t s) {
+  if ((uint8_t*)stats_host == (uint8_t*)out_host + n * 8)  // adjacent on the host as on the device: one copy
+    return host_copy(out_host, out, n * 8 + FBM_STATS_WORDS * 4, hipMemcpyDeviceToHost, s, "output+stats");
+  int rc = host_copy(out_host, out, n * 8, hipMemcpyDeviceToHost, s, "output");
+  return rc ? rc : host_copy(stats_host, st, FBM_STATS_WORDS * 4, hipMemcpyDeviceToHost, s, "stats");
+}
+
+int fbm_lom_protect_host(const void* x_host, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
+                         uint64_t target_m1, uint64_t weight, const uint8_t* secrets, const int8_t* signs, int n_peers,
+                         int raw_seeds, const uint8_t* nonce, uint64_t tau, uint64_t elem_offset, uint64_t* y_host,
+                         uint32_t* stats_host, void* workspace, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!workspace || !stats_host || (n > 0 && (!x_host || !y_host))) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  if (x_dtype != FBM_F32 && x_dtype != FBM_F64 && x_dtype != FBM_U64) {
+    set_error("x_dtype must be FBM_F32, FBM_F64 or FBM_U64");
+    return FBM_E_ARG;
+  }
+  uint8_t* w = (uint8_t*)workspace;
+  void* x = w;
+  uint64_t* y = (uint64_t*)(w + align256(n * 8));
+  uint32_t* st = (uint32_t*)(w + align256(n * 8) + n * 8);
+  const uint64_t xb = n * (x_dtype == FBM_F32 ? 4u : 8u);
+  int rc = host_copy(x, x_host, xb, hipMemcpyHostToDevice, s, "x");
+  if (!rc) rc = fbm_lom_protect(x, x_dtype, n, clip, two_clip, target_f, target_m1, weight, secrets, signs, n_peers,
+                                raw_seeds, nonce, tau, elem_offset, y, st, stream);
+  if (!rc) rc = host_copy_back(y_host, y, n, stats_host, st, s);
+  const int wrc = host_wait(s);  // (also after an error: nothing of this call left in flight on the buffers)
+  return rc ? rc : wrc;
+}
+
+int fbm_lom_aggregate_host(const uint64_t* y_host, int n_parties, uint64_t n, uint64_t total_weight, double neg_clip,
+                           double step, double* out_host, uint32_t* stats_host, void* workspace, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!workspace || !stats_host || (n > 0 && (!y_host || !out_host))) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  if (n_parties < 1) {
+    set_error("invalid aggregate arguments (n_parties=%d, total_weight=%llu)", n_parties,
+              (unsigned long long)total_weight);
+    return FBM_E_ARG;
+  }
+  uint8_t* w = (uint8_t*)workspace;
+  const uint64_t yb = (uint64_t)n_parties * n * 8;
+  uint64_t* y = (uint64_t*)w;
+  double* out = (double*)(w + align256(yb));
+  uint32_t* st = (uint32_t*)(w + align256(yb) + n * 8);
+  int rc = host_copy(y, y_host, yb, hipMemcpyHostToDevice, s, "y");
+  if (!rc) rc = fbm_lom_aggregate(y, n_parties, n, total_weight, neg_clip, step, out, nullptr, st, stream);
+  if (!rc) rc = host_copy_back(out_host, out, n, stats_host, st, s);
+  const int wrc = host_wait(s);
+  return rc ? rc : wrc;
+}
+
 // FBM_COMPACT_H=0 (A/B runs): whole 256-byte H rows for every engine, as before round 4
 static bool jl_compact_h() {
   static const bool on = !(getenv("FBM_COMPACT_H") && !strcmp(getenv("FBM_COMPACT_H"), "0"));

@@ -608,12 +608,7 @@ class SecaggLomCrypter(SecaggCrypter):
         if params.numel() == 0:
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value} Error during parameter encryption. max() arg is an empty sequence")
-        peers = [p for p in node_ids if p != node_id]
-        secrets_ = [pairwise_secrets[p] for p in peers]
-        signs = [1 if p < node_id else -1 for p in peers]
-        if len(node_ids) == 0:
-            raise FedbiomedSecaggCrypterError(
-                f"{ErrorNumbers.FB624.value} Error during parameter encryption. math domain error")
+        secrets_, signs = self._peer_masks(node_id, pairwise_secrets, node_ids)
         if weight is None or weight >= 0:
             return D.lom_protect(params, secrets_, signs, self._nonce, current_round, len(node_ids),
                                  clip=clipping_range, target=target_range, weight=1 if weight is None else weight,
@@ -632,6 +627,17 @@ class SecaggLomCrypter(SecaggCrypter):
             qv = int(q[int(nz[0, 0])].item()) & D.U64_MAX
             raise OverflowError(f"Python integer {qv * weight} out of bounds for uint64")
         return y
+
+    @staticmethod
+    def _peer_masks(node_id: str, pairwise_secrets: Dict[str, bytes], node_ids: List[str]):
+        """The peers' pairwise secrets in node order and their mask signs (LOM.protect, _lom.py:151-173)."""
+        peers = [p for p in node_ids if p != node_id]
+        secrets_ = [pairwise_secrets[p] for p in peers]
+        signs = [1 if p < node_id else -1 for p in peers]
+        if len(node_ids) == 0:
+            raise FedbiomedSecaggCrypterError(
+                f"{ErrorNumbers.FB624.value} Error during parameter encryption. math domain error")
+        return secrets_, signs
 
     def aggregate_tensor(self, Y: torch.Tensor, total_sample_size: int, clipping_range: Union[int, None] = None,
                          target_range: Optional[int] = None, want_sums: bool = False):
@@ -652,11 +658,18 @@ class SecaggLomCrypter(SecaggCrypter):
         if not params:
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value} Error during parameter encryption. max() arg is an empty sequence")
-        with D.deferred_checks():  # the status word checked once the masked vector is back (one sync per call)
-            x = host.to(D.device(), non_blocking=True)
-            y = self.encrypt_tensor(current_round, node_id, x, pairwise_secrets, node_ids, clipping_range, weight,
-                                    target_range)
-            packed = D.to_host(y).numpy().view(np.uint64)
+        if len(params) <= D.LOM_HOST_CALL_MAX and (weight is None or weight >= 0):
+            # a small vector: copy in, kernel, copy out and status in one synchronous C call
+            secrets_, signs = self._peer_masks(node_id, pairwise_secrets, node_ids)
+            packed = D.lom_protect_host(host.numpy(), secrets_, signs, self._nonce, current_round, len(node_ids),
+                                        clip=clipping_range, target=target_range,
+                                        weight=1 if weight is None else weight)
+        else:
+            with D.deferred_checks():  # the status word checked once the masked vector is back (one sync per call)
+                x = host.to(D.device(), non_blocking=True)
+                y = self.encrypt_tensor(current_round, node_id, x, pairwise_secrets, node_ids, clipping_range,
+                                        weight, target_range)
+                packed = D.to_host(y).numpy().view(np.uint64)
         pool = self._take_enc_pool(current_round, node_id, packed.shape[0])
         out = D.u64_into_pool(pool, packed) if pool is not None else packed.tolist()
         if wire.enabled():
@@ -670,18 +683,24 @@ class SecaggLomCrypter(SecaggCrypter):
         _check_int_lists(params)
         num_nodes = len(params)
         packed = wire.packed_rows(params, "lom")
+        dev = D.device()
         try:
-            Y = (torch.from_numpy(packed.view(np.int64)).to(D.device()) if packed is not None
-                 else D.u64_to_device(params))
+            Yh, pinned = (torch.from_numpy(packed.view(np.int64)), False) if packed is not None else \
+                D.u64_to_host(params)
         except (ValueError, TypeError) as e:
             raise FedbiomedSecaggCrypterError(
                 f"{ErrorNumbers.FB624.value}: The aggregation of encrypted parameters "
                 f"is not successful: {e}") from e
-        if Y.dim() != 2 or Y.shape[1] == 0:
+        if Yh.dim() != 2 or Yh.shape[1] == 0:
             return []
-        with D.deferred_checks():  # the status word checked once the averages are back
-            out = self.aggregate_tensor(Y, total_sample_size, clipping_range, target_range)
-            res_h = D.to_host(out).numpy()
+        if Yh.shape[1] <= D.LOM_HOST_CALL_MAX:  # a small vector: one synchronous C call, host to host
+            res_h = D.lom_aggregate_host(Yh.numpy().view(np.uint64), total_sample_size, clipping_range,
+                                         target_range or SAParameters.TARGET_RANGE)
+        else:
+            with D.deferred_checks():  # the status word checked once the averages are back
+                out = self.aggregate_tensor(Yh.to(dev, non_blocking=pinned), total_sample_size, clipping_range,
+                                            target_range)
+                res_h = D.to_host(out).numpy()
         logger.info(f"Aggregating {len(params)} parameters from {num_nodes} nodes.")
         pool = getattr(self, "_lom_agg_pool", None)
         if pool is not None and len(pool) == res_h.shape[0]:  # prepare_aggregate's floats, written in place

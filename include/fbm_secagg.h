@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FBM_ABI_VERSION 5 /* 5: fbm_jl_encrypt_factor; 4: fbm_ves_pack takes is_signed; 3: the JL round is an 8192-bit value (FBM_TAU_LIMBS limbs);
+#define FBM_ABI_VERSION 6 /* 6: fbm_lom_*_host; 5: fbm_jl_encrypt_factor; 4: fbm_ves_pack takes is_signed; 3: the JL round is an 8192-bit value (FBM_TAU_LIMBS limbs);
                              2 took 16 limbs, 1 a uint64 */
 /* The JL round `tau` of every JL entry point: a HOST pointer to FBM_TAU_LIMBS little-endian 32-bit
  * words, any round below 2^8192 -- FDH.H hashes t = (k << 512) | tau as t.to_bytes(1024, 'big')
@@ -107,6 +107,22 @@ int fbm_dequantize(const uint64_t* u, uint64_t n, double neg_clip, double step, 
  *   out    device, n float64 (may be NULL); sums device, n uint64 (may be NULL)           */
 int fbm_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t total_weight, double neg_clip,
                       double step, double* out, uint64_t* sums, uint32_t* stats, void* stream);
+
+/* ---- LOM on host buffers (small vectors, e.g. BASELINE config 1's 1 000 elements) ----------------
+ * The same computation as fbm_lom_protect / fbm_lom_aggregate with the operands in HOST memory
+ * (pinned or not): the input copied to the device workspace, the kernel, the output and the status
+ * words copied back, and the stream synchronised -- SYNCHRONOUS, unlike every other entry point: on
+ * FBM_OK the host outputs are written.  Status words as the device calls' (fbm_check_stats on
+ * stats_host).  A list call of 1 000 elements is launch-bound; this is its one-call form.
+ *   workspace  device, fbm_lom_host_workspace(n, 1) bytes (protect) / (n, n_parties) (aggregate);
+ *              one call at a time per workspace                                                    */
+uint64_t fbm_lom_host_workspace(uint64_t n, int n_parties);
+int fbm_lom_protect_host(const void* x_host, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
+                         uint64_t target_m1, uint64_t weight, const uint8_t* secrets, const int8_t* signs, int n_peers,
+                         int raw_seeds, const uint8_t* nonce, uint64_t tau, uint64_t elem_offset, uint64_t* y_host,
+                         uint32_t* stats_host, void* workspace, void* stream);
+int fbm_lom_aggregate_host(const uint64_t* y_host, int n_parties, uint64_t n, uint64_t total_weight, double neg_clip,
+                           double step, double* out_host, uint32_t* stats_host, void* workspace, void* stream);
 
 /* ---- Joye-Libert (reference fedbiomed/common/secagg/_jls.py) -------------------------
  * biprime: HOST, 32 limbs (N, 1 <= N < 2^1024; an odd N >= 3 runs on the Montgomery engines, an

@@ -1,0 +1,116 @@
+"""The LOM list API's one-call form for small vectors (fbm_lom_protect_host / fbm_lom_aggregate_host,
+include/fbm_secagg.h, ABI 6) against its device-tensor form, which the oracle tests pin
+(test_gpu_parity, test_crypter_sweep): `encrypt` and `aggregate` below D.LOM_HOST_CALL_MAX elements take
+the host-buffer call; the same calls with the threshold at 0 take the device path.  Outputs equal, and
+the reference's errors (overflow guard, round counter past 2^64, negative round, bad secrets) raised
+alike, message for message.  SecaggLomCrypter.encrypt / aggregate: reference
+fedbiomed/common/secagg/_secagg_crypter.py:318-455."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import secagg_oracle as O
+from fedbiomed_amd import _device as D, workload as W
+from fedbiomed_amd.secagg import SecaggLomCrypter
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _both(monkeypatch, fn):
+    """fn() through the host-buffer call, then through the device path: (result or exception) pairs."""
+    out = []
+    for limit in (D.LOM_HOST_CALL_MAX, 0):
+        monkeypatch.setattr(D, "LOM_HOST_CALL_MAX", limit)
+        try:
+            out.append(("ok", fn()))
+        except Exception as e:  # noqa: BLE001 -- compared, type and message
+            out.append((type(e).__name__, str(e)))
+    return out
+
+
+@pytest.mark.parametrize("n,P,weight", [(1, 2, None), (7, 3, 5), (1000, 2, 7), (4099, 4, 1),
+                                        (D.LOM_HOST_CALL_MAX, 5, 2**17 - 1)])
+def test_host_call_matches_device_path(monkeypatch, n, P, weight):
+    ids = W.node_ids(P)
+    rng = np.random.default_rng(n + P)
+    xs = [rng.uniform(-4, 4, n).tolist() for _ in range(P)]  # past the clipping range too: clipped alike
+    lc = SecaggLomCrypter("host_call")
+
+    def enc():
+        return [lc.encrypt(3, u, xs[p], W.pairwise_secrets_for(u, ids), ids, clipping_range=3, weight=weight)
+                for p, u in enumerate(ids)]
+
+    (k1, ys), (k2, ys_dev) = _both(monkeypatch, enc)
+    assert k1 == k2 == "ok" and ys == ys_dev
+    tw = P * (1 if weight is None else weight)
+    (k1, a), (k2, a_dev) = _both(monkeypatch, lambda: lc.aggregate(ys, tw, clipping_range=3))
+    assert k1 == k2 == "ok" and a == a_dev and len(a) == n
+
+
+def test_host_call_errors_match(monkeypatch):
+    ids = W.node_ids(2)
+    sec = W.pairwise_secrets_for(ids[0], ids)
+    lc = SecaggLomCrypter("host_err")
+    cases = {
+        # the overflow guard: (T - 1) * 16 needs 64 bits, 63 available for 2 nodes
+        "overflow": lambda: lc.encrypt(1, ids[0], [3.0, 0.5], sec, ids, clipping_range=3, weight=16,
+                                       target_range=2**60),
+        "round_past_2_64": lambda: lc.encrypt(2**64 - 2, ids[0], [0.5] * 16, sec, ids),
+        "negative_round": lambda: lc.encrypt(-1, ids[0], [0.5] * 16, sec, ids),
+        "bad_secret": lambda: lc.encrypt(1, ids[0], [0.5], {ids[1]: b"short"}, ids),
+        "zero_weight_total": lambda: lc.aggregate([[1, 2], [3, 4]], 0),
+    }
+    for name, fn in cases.items():
+        (k1, m1), (k2, m2) = _both(monkeypatch, fn)
+        assert k1 != "ok" and (k1, m1) == (k2, m2), name
+
+
+def test_host_call_clip_warning_and_oracle(caplog):
+    """On the host path: the clipping warning logged once per call, the masked vectors and the averages
+    equal to the oracle's LOM restatement (oracle/secagg_oracle.py lom_encrypt / lom_crypter_aggregate)."""
+    ids = W.node_ids(3)
+    lc = SecaggLomCrypter("host_warn")
+    xs = [[0.25, -5.0, 1.0], [0.5, 0.0, -1.0], [1.5, 2.0, 9.0]]
+    with caplog.at_level("WARNING"):
+        ys = [lc.encrypt(1, u, xs[p], W.pairwise_secrets_for(u, ids), ids, clipping_range=3, weight=2)
+              for p, u in enumerate(ids)]
+    assert sum("exceeds clipping range" in r.getMessage() for r in caplog.records) == 2
+    for p, u in enumerate(ids):
+        ref = O.lom_encrypt(xs[p], 1, u, W.pairwise_secrets_for(u, ids), ids, lc.nonce, clip=3, weight=2)
+        assert ys[p] == [int(v) for v in ref]
+    avg = lc.aggregate(ys, 6, clipping_range=3)
+    assert avg == [float(v) for v in O.lom_crypter_aggregate(ys, 6, clip=3)]
+
+
+def test_host_call_separate_status_buffer():
+    """The C call with the status words NOT adjacent to the output on the host (two copies back) gives the
+    bytes the adjacent layout (one copy, as lom_protect_host lays it out) gives."""
+    import ctypes
+
+    from fedbiomed_amd import _native as N
+    lib = N.load()
+    ids = W.node_ids(3)
+    lc = SecaggLomCrypter("host_sep")
+    sm, sg = lc._peer_masks(ids[1], W.pairwise_secrets_for(ids[1], ids), ids)
+    x = np.random.default_rng(5).uniform(-3, 3, 333)
+    ref = D.lom_protect_host(x, sm, sg, lc.nonce, 4, 3, weight=3)
+    c, c2, tf, tm1 = D.quant_params(None, None)
+    sec = np.frombuffer(b"".join(sm), dtype=np.uint8).copy()
+    sgn = np.asarray(sg, dtype=np.int8)
+    nb = np.frombuffer(lc.nonce, dtype=np.uint8).copy()
+    y = np.full(333, 7, dtype=np.uint64)
+    st = np.full(N.STATS_WORDS, 9, dtype=np.uint32)
+    ws = torch.empty(int(lib.fbm_lom_host_workspace(333, 1)), dtype=torch.uint8, device=D.device())
+    vp = ctypes.c_void_p
+    rc = lib.fbm_lom_protect_host(vp(x.ctypes.data), N.FBM_F64, 333, c, c2, tf, tm1, 3, vp(sec.ctypes.data),
+                                  vp(sgn.ctypes.data), 2, 0, vp(nb.ctypes.data), 4, 0, vp(y.ctypes.data),
+                                  vp(st.ctypes.data), vp(ws.data_ptr()), vp(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0, N.last_error()
+    assert np.array_equal(y, ref)
+    assert lib.fbm_check_stats(vp(st.ctypes.data), 3, None) == 0 and int(st[1]) == 0

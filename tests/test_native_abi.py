@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol(lib):
     for s in declared_symbols():
         assert hasattr(lib, s), f"missing export {s}"
         assert s in _native.SIGNATURES, f"no ctypes signature for {s}"
-    assert lib.fbm_abi_version() == _native.ABI_VERSION == 5
+    assert lib.fbm_abi_version() == _native.ABI_VERSION == 6
 
 
 def test_check_stats_lom_guard(lib):

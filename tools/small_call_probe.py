@@ -33,7 +33,8 @@ def main():
     sec = W.pairwise_secrets_for(ids[0], ids)
     dev = D.device()
     steps = {k: [] for k in ("floats_to_host", "h2d", "protect_and_check", "d2h", "tolist", "encrypt_call",
-                             "aggregate_call")}
+                             "aggregate_call", "protect_host_call", "aggregate_host_call", "peer_masks")}
+    Yh = np.array(ys, dtype=np.uint64)
     ys = [lc.encrypt(1, u, xs[p], W.pairwise_secrets_for(u, ids), ids, weight=7) for p, u in enumerate(ids)]
     for _ in range(args.reps):
         t0 = time.perf_counter()
@@ -51,8 +52,15 @@ def main():
         t6 = time.perf_counter()
         lc.aggregate(ys, 14)
         t7 = time.perf_counter()
+        sm, sg = lc._peer_masks(ids[0], sec, ids)
+        t8 = time.perf_counter()
+        D.lom_protect_host(host.numpy(), sm, sg, lc.nonce, 1, P, weight=7)
+        t9 = time.perf_counter()
+        D.lom_aggregate_host(Yh, 14)
+        t10 = time.perf_counter()
         for k, a, b in (("floats_to_host", t0, t1), ("h2d", t1, t2), ("protect_and_check", t2, t3), ("d2h", t3, t4),
-                        ("tolist", t4, t5), ("encrypt_call", t5, t6), ("aggregate_call", t6, t7)):
+                        ("tolist", t4, t5), ("encrypt_call", t5, t6), ("aggregate_call", t6, t7), ("peer_masks", t7, t8),
+                        ("protect_host_call", t8, t9), ("aggregate_host_call", t9, t10)):
             steps[k].append(1e6 * (b - a))
     torch.cuda.synchronize()
     print(json.dumps({"elements": n, "median_us": {k: round(statistics.median(v), 1) for k, v in steps.items()}}))
