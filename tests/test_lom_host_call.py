@@ -100,7 +100,7 @@ def test_host_call_separate_status_buffer():
     sm, sg = lc._peer_masks(ids[1], W.pairwise_secrets_for(ids[1], ids), ids)
     x = np.random.default_rng(5).uniform(-3, 3, 333)
     ref = D.lom_protect_host(x, sm, sg, lc.nonce, 4, 3, weight=3)
-    c, c2, tf, tm1 = D.quant_params(None, None)
+    c, c2, tf, tm1 = D.quant_params(None, 2**13)
     sec = np.frombuffer(b"".join(sm), dtype=np.uint8).copy()
     sgn = np.asarray(sg, dtype=np.int8)
     nb = np.frombuffer(lc.nonce, dtype=np.uint8).copy()

@@ -34,8 +34,8 @@ def main():
     dev = D.device()
     steps = {k: [] for k in ("floats_to_host", "h2d", "protect_and_check", "d2h", "tolist", "encrypt_call",
                              "aggregate_call", "protect_host_call", "aggregate_host_call", "peer_masks")}
-    Yh = np.array(ys, dtype=np.uint64)
     ys = [lc.encrypt(1, u, xs[p], W.pairwise_secrets_for(u, ids), ids, weight=7) for p, u in enumerate(ids)]
+    Yh = np.array(ys, dtype=np.uint64)
     for _ in range(args.reps):
         t0 = time.perf_counter()
         host = D.floats_to_host(xs[0])
