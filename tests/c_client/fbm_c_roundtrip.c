@@ -4,7 +4,8 @@
  * aggregate -- on device buffers it allocates itself with the HIP runtime, and writes the ciphertexts,
  * masked vectors and averages for tests/test_c_client.py to compare with the oracle and the Python API.
  * The Joye-Libert round also runs with every factor computed ahead (fbm_jl_decrypt_factor ->
- * fbm_jl_encrypt_factor / fbm_jl_aggregate_factor, ABI 5), which must give the same bytes.
+ * fbm_jl_encrypt_factor / fbm_jl_aggregate_factor, ABI 5), and the LOM round again on host buffers
+ * (fbm_lom_protect_host / fbm_lom_aggregate_host, ABI 6); both must give the same bytes.
  *
  *   fbm_c_roundtrip --abi          prints the ABI version (touches no device)
  *   fbm_c_roundtrip IN OUT         IN: the case (layout below, written by tests/test_c_client.py)
@@ -198,6 +199,34 @@ int main(int argc, char** argv) {
            "fbm_lom_aggregate");
     hip_ok(hipStreamSynchronize(stream), "sync");
     stats_ok(d_stats, 0, "fbm_lom_aggregate status");
+
+    /* the same LOM round on host buffers (ABI 6, synchronous): each party's fbm_lom_protect_host from its
+     * host floats, then fbm_lom_aggregate_host of the host rows -- the same bytes as above, or exit 1 */
+    {
+        uint64_t wsb = fbm_lom_host_workspace(n, (int)P);
+        void* d_hws = dalloc(wsb);
+        uint64_t* y = xmalloc((size_t)P * n * 8);
+        double* avg = xmalloc(n * sizeof(double));
+        uint32_t st[FBM_STATS_WORDS];
+        for (uint32_t p = 0; p < P; ++p) {
+            fbm_ok(fbm_lom_protect_host(x + (size_t)p * n, FBM_F32, n, clip, two_clip, target_f, target_m1, weight[p],
+                                        secrets + (size_t)p * n_peers * 32, signs + (size_t)p * n_peers, n_peers, 0,
+                                        nonce, lom_tau, 0, y + (size_t)p * n, st, d_hws, stream),
+                   "fbm_lom_protect_host");
+            fbm_ok(fbm_check_stats(st, (int)P, NULL), "fbm_lom_protect_host status");
+        }
+        fbm_ok(fbm_lom_aggregate_host(y, (int)P, n, total_weight, neg_clip, step, avg, st, d_hws, stream),
+               "fbm_lom_aggregate_host");
+        fbm_ok(fbm_check_stats(st, 0, NULL), "fbm_lom_aggregate_host status");
+        uint64_t* y_dev = xmalloc((size_t)P * n * 8);
+        double* avg_dev = xmalloc(n * sizeof(double));
+        hip_ok(hipMemcpy(y_dev, d_y, (size_t)P * n * 8, hipMemcpyDeviceToHost), "D2H");
+        hip_ok(hipMemcpy(avg_dev, d_lom_avg, n * sizeof(double), hipMemcpyDeviceToHost), "D2H");
+        if (memcmp(y, y_dev, (size_t)P * n * 8) != 0) die("host buffers", "masked vectors differ from fbm_lom_protect's");
+        if (memcmp(avg, avg_dev, n * sizeof(double)) != 0) die("host buffers", "averages differ from fbm_lom_aggregate's");
+        free(y), free(avg), free(y_dev), free(avg_dev);
+        hip_ok(hipFree(d_hws), "hipFree");
+    }
 
     FILE* out = fopen(argv[2], "wb");
     if (!out) die("cannot open", argv[2]);
