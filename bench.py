@@ -72,7 +72,9 @@ def mads_per_exp(key: int, mads: tuple) -> int:
 def committed_traffic(kernel: str, scheme: str, elements: int, n_ct=None):
     """(HBM bytes per launch of `kernel`, the profile file) from the committed rocprofv3 PMC summary
     of this workload -- same scheme and elements per GPU (JL: same ciphertexts per party) --
-    (profiles/*_hbm_traffic.json, written by tools/prof_summary.py), else (None, None).  Not
+    (profiles/*_hbm_traffic.json, written by tools/prof_summary.py), else (None, None).  `kernel` is
+    the launched kernel's exact name with its template arguments (e.g. "lom_aggregate_ws_kernel<2, 4,
+    8>"): a profile of another kernel or of another instantiation never stands in for it.  Not
     measured in the run: a PMC pass needs its own rocprofv3 process."""
     import glob
 
@@ -85,9 +87,9 @@ def committed_traffic(kernel: str, scheme: str, elements: int, n_ct=None):
         cfg = d.get("meta", {}).get("bench_config") or {}
         if (cfg.get("scheme") == scheme and cfg.get("elements_per_gpu") == elements
                 and (scheme != "jl" or cfg.get("ciphertexts_per_party_per_gpu") == n_ct)):
-            for name, k in d.get("kernels", {}).items():  # exact, or template arguments stripped
-                if name == "fbm::" + kernel or ("<" not in kernel and name.split("<")[0] == "fbm::" + kernel):
-                    return k["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+            k = d.get("kernels", {}).get("fbm::" + kernel)  # the exact instantiation only
+            if k is not None:
+                return k["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
     return None, None
 
 
@@ -302,12 +304,14 @@ def main():
     batch_exp = not args.no_batch_exp and not args.no_prologue_first
 
     def engine_ctx(mode):
-        """JL exponentiation engine for the launches issued inside (library policy otherwise):
-        the step's P + 1 concurrent exponentiations fill the chip together, so they take the
-        throughput engine (one lane per ciphertext) even when each alone would be small."""
+        """--no-batch-exp (an A/B form): the step's P + 1 concurrent exponentiation launches fill the
+        chip together, so they take the throughput engine (one lane per ciphertext) even when each
+        alone would be small -- the test build's per-thread switch, so those steps run through it.  The
+        default step needs none: its one batched launch is the one-lane kernel, and it runs the product
+        library throughout."""
         import contextlib
 
-        return D.jl_engine(mode) if hasattr(D, "jl_engine") else contextlib.nullcontext()
+        return D.jl_engine(mode) if not batch_exp else contextlib.nullcontext()
 
     # the parties' ciphertexts go straight into their rows of the [P, n_ct, 64] block the aggregate
     # takes (encrypt_tensor(out=...)): no stacking copy inside the step
@@ -403,29 +407,68 @@ def main():
             out = lc.aggregate_tensor(Y, total_w)
         return distributed.all_gather_shards(out, n_total, 8) if gather else out
 
+    def lom_cold_aggregate(reps=5):
+        """The LOM aggregate with its input evicted from the chip's caches: the protects, then a write of
+        a scratch buffer twice the MALL's 256 MB (MI355X_MICROARCH.md), then the aggregate alone, timed by
+        the test build's HIP events on its stream (median of `reps`).  Inside the step the aggregate reads
+        rows the protects wrote microseconds earlier, up to 256 MB of them from the MALL: that warm figure
+        can exceed what HBM alone streams."""
+        scratch = torch.empty(512 * 2 ** 20 // 8, dtype=torch.int64, device=dev)
+
+        def once():
+            with D.deferred_checks():
+                for p, u in enumerate(ids):
+                    lc.encrypt_tensor(tau, u, xs_l[p], secrets_[p], ids, weight=weights[p], elem_offset=lo_l,
+                                      out=Y[p])
+            scratch.fill_(1)
+            torch.cuda.synchronize()
+            _native.prof_enable(True)
+            lc.aggregate_tensor(Y, total_w)
+            torch.cuda.synchronize()
+            _native.prof_enable(False)
+            return _native.prof_report().get("lom_aggregate", (0, 0.0))
+
+        with _native.test_hooks():
+            once()  # warm-up through the test build
+            runs = [once() for _ in range(reps)]
+        del scratch
+        ms = sorted(t / c for c, t in runs if c)[len(runs) // 2] if all(c for c, _ in runs) else None
+        ab1 = 8 * (P + 1) * (hi_l - lo_l)
+        return {"ms": ms, "hbm_GBps": ab1 / (ms / 1000) / 1e9 if ms else None,
+                "hbm_frac": ab1 / (ms / 1000) / 1e9 / HBM_PEAK_GBS if ms else None, "runs": reps,
+                "kernel": D.lom_aggregate_kernel(P, Y),
+                "note": "median of %d: protects, 512 MB scratch write (2x the MALL), then the aggregate alone "
+                        "(HIP events on its stream); the warm figure is the aggregate inside the step" % reps}
+
     def timed(step, steps, warmup, prof=False):
         """prof=True: serialised launches (one stream) with per-kernel HIP events, so each
-        event pair brackets exactly one kernel's execution (roofline durations)."""
-        for _ in range(warmup):
-            step(serial=prof)
-        if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize()
-        if prof:
-            _native.prof_enable(True)
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            step(serial=prof)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        if prof:
-            _native.prof_enable(False)
-        if world > 1:
-            torch.distributed.barrier()
-        el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-        if world > 1:
-            torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
-        return el.item(), (_native.prof_report() if prof else {})
+        event pair brackets exactly one kernel's execution (roofline durations).  The event timer
+        is the test build's (include/fbm_secagg_test.h): a profiled step runs through it
+        (_native.test_hooks: the same kernel objects, the C ABI compiled with the timer), after one
+        warm-up step of its own there; the timed steps of `value` run the product library."""
+        import contextlib
+
+        with (_native.test_hooks() if prof else contextlib.nullcontext()):
+            for _ in range(warmup + (1 if prof else 0)):
+                step(serial=prof)
+            if world > 1:
+                torch.distributed.barrier()
+            torch.cuda.synchronize()
+            if prof:
+                _native.prof_enable(True)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step(serial=prof)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            if prof:
+                _native.prof_enable(False)
+            if world > 1:
+                torch.distributed.barrier()
+            el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+            if world > 1:
+                torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+            return el.item(), (_native.prof_report() if prof else {})
 
     step = step_jl if args.scheme == "jl" else step_lom
     if args.serial:
@@ -449,7 +492,7 @@ def main():
         # the combine kernel, not to this launch
         alg_bytes = prof_steps * (P * (4 * n + 256 * n_ct) + 256 * n_ct)
         mm = sum(sum(products_per_exp(k)) for k in keys) + sum(products_per_exp(sk0))
-        lib = _native.load()
+        lib = _native.load_test()  # the engine's multiply counts (include/fbm_secagg_test.h)
         mads_mul, mads_sq, mads_short = lib.fbm_jl_mads(0), lib.fbm_jl_mads(1), lib.fbm_jl_mads(2)
         mads_step = n_ct * sum(mads_per_exp(k, (mads_sq, mads_mul, mads_short)) for k in keys + [sk0])
         mads = prof_steps * mads_step
@@ -459,7 +502,7 @@ def main():
     else:
         cnt, ms = kprof.get("lom_aggregate", (0, 0.0))
         alg_bytes = prof_steps * 8 * (P + 1) * n
-        mads, kname = 0, "lom_aggregate_kernel"
+        mads, kname = 0, D.lom_aggregate_kernel(P, Y)  # the instantiation the launch takes
     sec = ms / 1000.0 if ms > 0 else float("nan")
     achieved = alg_bytes / sec / 1e9 if ms > 0 else None
     traffic, traffic_src = committed_traffic(kname, args.scheme, n, n_ct)
@@ -471,6 +514,8 @@ def main():
                                "launch, committed; a PMC pass needs its own profiler process, so it is looked up, "
                                "not measured in this run)") if traffic_src else None,
             "avg_launch_ms": (ms / cnt) if cnt else None, "launches": cnt}
+    if args.scheme == "lom":
+        roof["cold"] = lom_cold_aggregate()
     if args.scheme == "jl":
         roof["note"] = ("jl_exp_kernel moves ~1e-4 of the HBM roofline's bytes by construction: it is bound by "
                         "integer multiply issue (v_mad_u64_u32), reported in roofline_valu; one launch = every "
@@ -636,12 +681,15 @@ def main():
         _, kp2 = timed(step_lom, 1, 0, prof=True)  # one instrumented step: per-kernel durations
         c2, m2 = kp2.get("lom_aggregate", (0, 0.0))
         ab = c2 * 8 * (P + 1) * (hi_l - lo_l)
+        lom_kname = D.lom_aggregate_kernel(P, Y)  # the instantiation the launch takes
         line["lom"] = {"value": n_total * k2 / el2, "unit": "params/s",
                        "ms_per_step": 1000 * el2 / k2,
-                       "aggregate_traffic": committed_traffic("lom_aggregate_kernel", "lom", hi_l - lo_l),
+                       "aggregate_kernel": lom_kname,
+                       "aggregate_traffic": committed_traffic(lom_kname, "lom", hi_l - lo_l),
                        "aggregate_hbm_GBps": ab / (m2 / 1000) / 1e9 if m2 else None,
                        "aggregate_hbm_frac": (ab / (m2 / 1000) / 1e9) / HBM_PEAK_GBS if m2 else None,
                        "kernels_ms": {k: {"launches": c, "total_ms": round(t, 3)} for k, (c, t) in sorted(kp2.items())}}
+        line["lom"]["aggregate_cold"] = lom_cold_aggregate()
 
     # ---- secondary, N > 1: party-per-rank LOM -- the north star's RCCL reduce of the masked sum.
     #      Rank r protects parties r, r + N, ... over the WHOLE vector (the concatenation of every
@@ -693,7 +741,7 @@ def main():
         n_ct_all = (args.n + cr - 1) // cr
 
         def step_pj(serial=False):
-            with D.deferred_checks(), engine_ctx("single"):
+            with D.deferred_checks():  # the whole vector per party: the cost model's one-lane engine
                 cts_mine = torch.stack([jc.encrypt_tensor(P, tau, xs_pj[i], keys[p], W.BIPRIME0, weight=weights[p])
                                         for i, p in enumerate(mine)])
             stripe, k0 = distributed.all_to_all_ciphertexts(cts_mine, ppr)

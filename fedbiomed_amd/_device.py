@@ -768,13 +768,14 @@ _ENGINES = {"auto": 0, "single": 1, "generic": 2, "triple": 3, "quad": 4}
 
 
 class jl_engine:
-    """Exponentiation engine for the JL calls issued inside (process-wide policy,
-    fbm_jl_set_engine): "auto" (the library's choice by launch size), "single" (one lane per
-    ciphertext: several concurrent launches that fill the chip together), "quad" / "triple"
-    (four / three lanes per ciphertext: latency of a launch below the chip's lane count),
-    "generic" (csrc/fbm_gen.hip, Barrett products for any modulus: even biprimes always take it;
-    under this policy odd ones do too -- a cross-check of the Montgomery engines).
-    Results are bit-identical under every engine.
+    """Exponentiation engine for the JL calls this thread issues inside (the test build's per-thread
+    policy, fbm_jl_set_engine in include/fbm_secagg_test.h; the block's calls run through the test
+    build, _native.test_hooks): "auto" (the library's choice by launch size -- the product library's
+    only policy), "single" (one lane per ciphertext: several concurrent launches that fill the chip
+    together), "quad" / "triple" (four / three lanes per ciphertext: latency of a launch below the
+    chip's lane count), "generic" (csrc/fbm_gen.hip, Barrett products for any modulus: even biprimes
+    always take it; under this policy odd ones do too -- a cross-check of the Montgomery engines).
+    Results are bit-identical under every engine; other threads are unaffected.
 
         with D.jl_engine("single"):
             ...  # the parties' concurrent encrypts
@@ -783,33 +784,35 @@ class jl_engine:
     def __init__(self, mode: str):
         if mode not in _ENGINES:
             raise ValueError(f"engine must be one of {sorted(_ENGINES)}")
-        self._mode, self._prev = _ENGINES[mode], None
+        self._mode, self._prev, self._hooks = _ENGINES[mode], None, N.test_hooks()
 
     def __enter__(self):
-        self._prev = N.load().fbm_jl_set_engine(self._mode)
+        self._hooks.__enter__()
+        self._prev = N.load_test().fbm_jl_set_engine(self._mode)
         return self
 
     def __exit__(self, *exc):
-        N.load().fbm_jl_set_engine(self._prev)
-        return False
+        N.load_test().fbm_jl_set_engine(self._prev)
+        return self._hooks.__exit__(*exc)
 
 
 class jl_short:
     """The exponentiation's short path (binary chain with the 9-row short-base product, taken for a
-    one-digest FDH h and N > 2^262) on or off for the JL calls issued inside
-    (process-wide, fbm_jl_set_short): off, every wave runs the sliding-window table path.  Results are
-    bit-identical either way -- an A/B and test switch."""
+    one-digest FDH h and N > 2^262) on or off for the JL calls this thread issues inside
+    (the test build's fbm_jl_set_short; the block's calls run through the test build): off, every wave
+    runs the sliding-window table path.  Results are bit-identical either way -- an A/B and test switch."""
 
     def __init__(self, on: bool):
-        self._on, self._prev = 1 if on else 0, None
+        self._on, self._prev, self._hooks = 1 if on else 0, None, N.test_hooks()
 
     def __enter__(self):
-        self._prev = N.load().fbm_jl_set_short(self._on)
+        self._hooks.__enter__()
+        self._prev = N.load_test().fbm_jl_set_short(self._on)
         return self
 
     def __exit__(self, *exc):
-        N.load().fbm_jl_set_short(self._prev)
-        return False
+        N.load_test().fbm_jl_set_short(self._prev)
+        return self._hooks.__exit__(*exc)
 
 
 def jl_clear_caches() -> None:
@@ -843,8 +846,16 @@ def list_encrypt_stripes(n_ct: int, dev=None) -> List[Tuple[int, int]]:
 
 
 def jl_engine_for(n_ct: int) -> str:
-    """The engine a launch of n_ct ciphertexts takes under the current policy."""
-    return {1: "single", 2: "generic", 3: "triple", 4: "quad"}[N.load().fbm_jl_engine_for(int(n_ct))]
+    """The engine a launch of n_ct ciphertexts takes under this thread's policy (test build)."""
+    return {1: "single", 2: "generic", 3: "triple", 4: "quad"}[N.load_test().fbm_jl_engine_for(int(n_ct))]
+
+
+def lom_aggregate_kernel(n_parties: int, y: torch.Tensor) -> str:
+    """The LOM aggregate kernel a launch over y ([n_parties, n] in HBM) takes, as rocprofv3 names it
+    without the "fbm::" namespace (test build, fbm_test_lom_aggregate_kernel)."""
+    buf = ctypes.create_string_buffer(128)
+    _call(N.load_test().fbm_test_lom_aggregate_kernel, int(n_parties), int(y.shape[-1]), _ptr(y), buf, len(buf))
+    return buf.value.decode()
 
 
 def jl_chunk_ct() -> int:

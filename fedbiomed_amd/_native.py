@@ -4,6 +4,12 @@ The library is built in-tree (`python -m fedbiomed_amd._build` or
 `__graft_entry__.build()`) to `fedbiomed_amd/_lib/libfbm_secagg.so`.  There is NO
 CPU fallback: if the library or a GPU is missing, every compute call raises.
 
+`load()` is the product library.  The test build `libfbm_secagg_test.so` (the same kernels; its
+C ABI adds include/fbm_secagg_test.h: host runs of device routines, the calling thread's engine
+switches, the per-kernel event timer) is `load_test()`; inside `with test_hooks():` the calling
+thread's `load()` returns it too, so a whole computation (the bench's timed-kernel step, a test
+pinned to one engine) runs through one library.  FBM_TEST_HOOKS=1 routes every thread there.
+
 torch is imported first so that the process has exactly one HIP runtime: torch's
 bundled `libamdhip64.so` has the same SONAME (`libamdhip64.so.7`) our library links
 against, so the dynamic loader binds us to the already-loaded copy.
@@ -16,6 +22,7 @@ import threading
 import torch  # noqa: F401  (loads the HIP runtime the library must share)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libfbm_secagg.so")
+TEST_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libfbm_secagg_test.so")
 
 
 def ab_variant() -> bool:
@@ -29,7 +36,13 @@ def lib_path() -> str:
     return os.environ.get("FBM_LIB_PATH") or LIB_PATH
 
 
-ABI_VERSION = 6  # include/fbm_secagg.h FBM_ABI_VERSION
+def test_lib_path() -> str:
+    """FBM_LIB_PATH (an A/B variant: built with the test build's exports, tools/ab.sh) or the in-tree
+    test build."""
+    return os.environ.get("FBM_LIB_PATH") or TEST_LIB_PATH
+
+
+ABI_VERSION = 7  # include/fbm_secagg.h FBM_ABI_VERSION
 TAU_LIMBS = 256  # FBM_TAU_LIMBS: the JL round's 32-bit words (< 2^8192)
 FBM_OK = 0
 FBM_E_ARG = -1
@@ -51,7 +64,8 @@ FBM_PT = 5
 STATS_WORDS = 4
 
 _lock = threading.Lock()
-_lib = None
+_libs = {}  # path -> CDLL
+_tls = threading.local()  # .test: depth of test_hooks() on this thread
 loaded_abi = None  # fbm_abi_version() of the loaded library (ABI_VERSION, or one less for an A/B variant)
 
 c_u64 = ctypes.c_uint64
@@ -62,14 +76,7 @@ c_vp = ctypes.c_void_p
 # name -> (restype, argtypes); must match include/fbm_secagg.h exactly
 SIGNATURES = {
     "fbm_abi_version": (c_int, []),
-    "fbm_jl_window": (c_int, []),
-    "fbm_jl_mads": (c_int, [c_int]),
-    "fbm_jl_quad_mads": (c_int, [c_int]),
-    "fbm_jl_triple_mads": (c_int, [c_int]),
-    "fbm_jl_set_engine": (c_int, [c_int]),
-    "fbm_jl_set_short": (c_int, [c_int]),
     "fbm_jl_clear_caches": (None, []),
-    "fbm_jl_engine_for": (c_int, [c_u64]),
     "fbm_jl_batch_begin": (c_int, []),
     "fbm_jl_batch_abort": (None, []),
     "fbm_jl_batch_count": (c_int, []),
@@ -108,7 +115,6 @@ SIGNATURES = {
     "fbm_jl_fdh_msg": (c_int, [c_u64, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp]),
     "fbm_jl_fdh_msg_row_words": (c_int, [c_int]),
     "fbm_int_true_div_big": (c_int, [c_vp, c_u64, c_vp, c_int, c_int, c_vp, c_vp]),
-    "fbm_test_true_div_big": (c_int, [c_vp, c_u64, c_vp, c_int, c_int, c_vp]),
     "fbm_ves_pack": (c_int, [c_vp, c_u64, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     "fbm_ves_unpack": (c_int, [c_vp, c_u64, c_int, c_int, c_int, c_u64, c_int, c_vp, c_vp]),
     "fbm_jl_product": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp, c_vp, c_vp]),
@@ -120,6 +126,18 @@ SIGNATURES = {
     "fbm_ass_reconstruct": (c_int, [c_vp, c_int, c_u64, c_vp, c_vp]),
     "fbm_ass_split_wide": (c_int, [c_vp, c_u64, c_int, c_int, c_int, c_int, c_vp, c_vp, c_u64, c_vp, c_vp]),
     "fbm_ass_reconstruct_wide": (c_int, [c_vp, c_int, c_int, c_u64, c_vp, c_vp]),
+}
+
+# include/fbm_secagg_test.h: exported by the test build only
+TEST_SIGNATURES = {
+    "fbm_jl_window": (c_int, []),
+    "fbm_jl_mads": (c_int, [c_int]),
+    "fbm_jl_quad_mads": (c_int, [c_int]),
+    "fbm_jl_triple_mads": (c_int, [c_int]),
+    "fbm_jl_set_engine": (c_int, [c_int]),
+    "fbm_jl_set_short": (c_int, [c_int]),
+    "fbm_jl_engine_for": (c_int, [c_u64]),
+    "fbm_test_true_div_big": (c_int, [c_vp, c_u64, c_vp, c_int, c_int, c_vp]),
     "fbm_test_modinv": (c_int, [c_vp, c_vp, c_vp, c_vp]),
     "fbm_test_nadic_consts": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fbm_test_short_consts": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -127,6 +145,7 @@ SIGNATURES = {
     "fbm_test_fdh_gcd": (c_int, [c_vp, c_vp, c_vp]),
     "fbm_test_gen_exp": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp]),
     "fbm_test_gen_combine": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "fbm_test_lom_aggregate_kernel": (c_int, [c_int, c_u64, c_vp, ctypes.c_char_p, c_int]),
     "fbm_prof_enable": (c_int, [c_int]),
     "fbm_prof_report": (c_int, [ctypes.c_char_p, c_int]),
 }
@@ -136,24 +155,24 @@ class NativeUnavailable(RuntimeError):
     """The HIP extension is not built or cannot be loaded."""
 
 
-def load(path: str = None) -> ctypes.CDLL:
-    """Loads (once) and returns the C-ABI library; raises NativeUnavailable.  The library must
-    export every symbol of SIGNATURES and report ABI_VERSION, unless FBM_AB_VARIANT=1."""
-    global _lib, loaded_abi
+def _open(path: str, sigs: dict) -> ctypes.CDLL:
+    """Loads (once per path) a build of the library; it must export every symbol of `sigs` and report
+    ABI_VERSION, unless FBM_AB_VARIANT=1."""
+    global loaded_abi
     with _lock:
-        if _lib is not None:
-            return _lib
-        path = path or lib_path()
+        lib = _libs.get(path)
+        if lib is not None and all(hasattr(lib, n) for n in sigs):
+            return lib
         if not os.path.exists(path):
             raise NativeUnavailable(
                 f"HIP extension not built: {path} is missing (run `python -m fedbiomed_amd._build`)")
         try:
-            lib = ctypes.CDLL(path)
+            lib = _libs.get(path) or ctypes.CDLL(path)
         except OSError as e:  # pragma: no cover - depends on the box
             raise NativeUnavailable(f"cannot load {path}: {e}") from e
         variant = ab_variant()  # an A/B build (tools/ab.sh) may predate newer symbols
         missing = []
-        for name, (res, args) in SIGNATURES.items():
+        for name, (res, args) in sigs.items():
             try:
                 fn = getattr(lib, name)
             except AttributeError:
@@ -162,7 +181,7 @@ def load(path: str = None) -> ctypes.CDLL:
             fn.restype = res
             fn.argtypes = args
         if missing and not variant:
-            raise NativeUnavailable(f"{path} lacks {len(missing)} entry point(s) of include/fbm_secagg.h: "
+            raise NativeUnavailable(f"{path} lacks {len(missing)} entry point(s) of its header(s): "
                                     f"{', '.join(missing[:4])}{' ...' if len(missing) > 4 else ''}")
         if "fbm_abi_version" in missing:
             raise NativeUnavailable(f"{path} does not export fbm_abi_version")
@@ -172,8 +191,41 @@ def load(path: str = None) -> ctypes.CDLL:
         if abi != ABI_VERSION and not (variant and abi == ABI_VERSION - 1):
             raise NativeUnavailable(f"ABI version mismatch: {path} reports {abi}, this binding needs {ABI_VERSION}")
         loaded_abi = abi
-        _lib = lib
+        _libs[path] = lib
         return lib
+
+
+def load(path: str = None) -> ctypes.CDLL:
+    """The product library (include/fbm_secagg.h), loaded once; raises NativeUnavailable.  Inside
+    test_hooks() on this thread, or with FBM_TEST_HOOKS=1, the test build instead (load_test())."""
+    if path is None and (getattr(_tls, "test", 0) or os.environ.get("FBM_TEST_HOOKS") == "1"):
+        return load_test()
+    return _open(path or lib_path(), SIGNATURES)
+
+
+def load_test() -> ctypes.CDLL:
+    """The test build (include/fbm_secagg.h + include/fbm_secagg_test.h): the test suite's host
+    hooks, the calling thread's engine / short-path switches, the per-kernel event timer."""
+    return _open(test_lib_path(), {**SIGNATURES, **TEST_SIGNATURES})
+
+
+class test_hooks:
+    """Routes this thread's load() to the test build for the duration (re-entrant), so every
+    library call of a computation goes through the library whose switches / timer it sets:
+
+        with _native.test_hooks():
+            _native.prof_enable(True)
+            ...
+    """
+
+    def __enter__(self):
+        load_test()
+        _tls.test = getattr(_tls, "test", 0) + 1
+        return self
+
+    def __exit__(self, *exc):
+        _tls.test -= 1
+        return False
 
 
 def last_error() -> str:
@@ -181,12 +233,13 @@ def last_error() -> str:
 
 
 def prof_enable(on: bool) -> None:
-    load().fbm_prof_enable(1 if on else 0)
+    """The test build's per-kernel event timer (calls made through load_test() / test_hooks())."""
+    load_test().fbm_prof_enable(1 if on else 0)
 
 
 def prof_report() -> dict:
-    """{kernel: (launches, total_ms)} of the launches recorded since the last report."""
-    lib = load()
+    """{kernel: (launches, total_ms)} of the test build's launches recorded since the last report."""
+    lib = load_test()
     need = lib.fbm_prof_report(None, 0)  # non-destructive size query
     buf = ctypes.create_string_buffer(need + 4096)
     lib.fbm_prof_report(buf, len(buf))

@@ -17,6 +17,9 @@
 #include "fbm_quad_asm.hpp"
 #include "fbm_tri_asm.hpp"
 #include "fbm_safegcd.hpp"
+#ifdef FBM_TEST_HOOKS
+#include "../../include/fbm_secagg_test.h"
+#endif
 
 namespace fbm {
 
@@ -409,12 +412,14 @@ static bool jl_generic(const uint32_t* biprime) {
   return (biprime[0] & 1u) == 0u || jl_is_one(biprime) || jl_engine_policy() == FBM_ENGINE_GENERIC;
 }
 
-static std::atomic<int> g_short_on{1};  // fbm_jl_set_short: 0 forces the window-table path (A/B, tests)
+// the short path on (1) or off (0: every wave runs the window-table path) for this thread's calls; only the
+// test build's fbm_jl_set_short changes it (include/fbm_secagg_test.h)
+static thread_local int t_short_on = 1;
 
 // The path a split call (fbm_jl_encrypt_phase / fbm_jl_decrypt_factor_phase) took at its phase 1
 // -- generic or Montgomery engine, short path or not -- keyed by its workspace: the later phases
 // read the constants phase 1 wrote, so they follow phase 1's choice even if the process-wide
-// switches (fbm_jl_set_engine, fbm_jl_set_short) changed in between.  A later phase whose record is
+// switches (the test build's fbm_jl_set_engine, fbm_jl_set_short) changed in between.  A later phase whose record is
 // missing (phase 1 never ran on this workspace, or its record was evicted by FBM_PATH_RECS newer
 // split calls) is refused with FBM_E_ARG: it would read constants laid out for a path it cannot know.
 // fbm_jl_clear_caches leaves the records alone (they hold no key material).
@@ -439,7 +444,7 @@ static int jl_path_for(const void* ws, int phase, int full, const uint32_t* bipr
     return FBM_E_ARG;
   }
   generic = jl_generic(biprime);
-  short_on = g_short_on.load(std::memory_order_relaxed) != 0;
+  short_on = t_short_on != 0;
   if (phase != full) {
     std::lock_guard<std::mutex> lk(g_path_mu);
     for (size_t i = 0; i < g_path_recs.size(); ++i)
@@ -936,9 +941,11 @@ static uint64_t table_slots_for(uint64_t n_ct) {
 static uint64_t align256(uint64_t v) { return (v + 255) & ~255ull; }
 
 // ---------------------------------------------------------------------------------------
-// optional per-kernel event timer (fbm_prof_enable / fbm_prof_report): records a HIP event
-// pair on the launch stream around each kernel launch; costs nothing when disabled.
+// optional per-kernel event timer (test build only: fbm_prof_enable / fbm_prof_report,
+// include/fbm_secagg_test.h): records a HIP event pair on the launch stream around each kernel
+// launch; costs nothing when disabled.  The product library launches directly.
 // ---------------------------------------------------------------------------------------
+#ifdef FBM_TEST_HOOKS
 struct ProfRec {
   const char* name;
   hipEvent_t a, b;
@@ -976,6 +983,12 @@ static int timed(const char* name, hipStream_t s, F f) {
   g_prof.push_back(r);
   return rc;
 }
+#else
+template <class F>
+static int timed(const char*, hipStream_t, F f) {
+  return f();
+}
+#endif
 
 static void fill_peers(LomPeers& pe, const uint8_t* nonce, uint64_t tau) {
   memset(&pe, 0, sizeof(pe));
@@ -998,31 +1011,6 @@ extern "C" {
 
 int fbm_abi_version(void) { return FBM_ABI_VERSION; }
 
-int fbm_jl_window(void) { return FBM_WIN; }
-int fbm_jl_mads(int square) {  // 0: general product, 1: square, 2: short-base product
-  return square == 2 ? FBM_NA_MADS_SHORT : square ? FBM_NA_MADS_SQR : FBM_NA_MADS_MUL;
-}
-int fbm_jl_quad_mads(int square) {
-  return 4 * (square == 2 ? FBM_QA_MADS_SHORT : square ? FBM_QA_MADS_SQR : FBM_QA_MADS_MUL);
-}
-int fbm_jl_triple_mads(int square) {
-  return 3 * (square == 2 ? FBM_TA_MADS_SHORT : square ? FBM_TA_MADS_SQR : FBM_TA_MADS_MUL);
-}
-
-int fbm_jl_set_engine(int mode) {
-  if (mode != FBM_ENGINE_AUTO && mode != FBM_ENGINE_SINGLE && mode != FBM_ENGINE_GENERIC && mode != FBM_ENGINE_QUAD &&
-      mode != FBM_ENGINE_TRIPLE) {
-    set_error("fbm_jl_set_engine: mode must be 0 (auto), 1 (one lane per ciphertext), 2 (generic: any modulus), "
-              "3 (three lanes) or 4 (four)");
-    return FBM_E_ARG;
-  }
-  return jl_engine_set(mode);
-}
-
-int fbm_jl_engine_for(uint64_t n_ct) { return jl_engine_for(n_ct); }
-
-int fbm_jl_set_short(int on) { return g_short_on.exchange(on ? 1 : 0); }
-
 void fbm_jl_clear_caches(void) {
   short_cache_clear();  // the only one derived from a key (zeroed)
   {
@@ -1030,20 +1018,6 @@ void fbm_jl_clear_caches(void) {
     g_jp_cache.clear();  // per-N public parameters
     g_rk_cache.clear();
   }
-}
-
-int fbm_test_short_cache(uint32_t* out, int cap_words) {
-  std::lock_guard<std::mutex> lk(g_jp_mu);
-  const int per = (int)(sizeof(JlShortCacheEntry) / 4);
-  const int n = (int)g_short_cache.size();
-  if (out) {
-    if (cap_words < n * per) {
-      set_error("fbm_test_short_cache: %d words needed", n * per);
-      return FBM_E_ARG;
-    }
-    for (int i = 0; i < n; ++i) memcpy(out + i * per, &g_short_cache[i], sizeof(JlShortCacheEntry));
-  }
-  return n * per;
 }
 
 const char* fbm_last_error(void) { return g_err; }
@@ -1272,10 +1246,14 @@ int fbm_lom_aggregate_host(const uint64_t* y_host, int n_parties, uint64_t n, ui
   return rc ? rc : wrc;
 }
 
-// FBM_COMPACT_H=0 (A/B runs): whole 256-byte H rows for every engine, as before round 4
+// FBM_COMPACT_H=0 (A/B builds with -DFBM_AB_KNOBS): whole 256-byte H rows for every engine, as before round 4
 static bool jl_compact_h() {
+#ifdef FBM_AB_KNOBS
   static const bool on = !(getenv("FBM_COMPACT_H") && !strcmp(getenv("FBM_COMPACT_H"), "0"));
   return on;
+#else
+  return true;
+#endif
 }
 
 // encrypt workspace: ops | cst | pt [n_ct][32] | nude (blocked) | H [n_ct][64] | table |
@@ -1980,7 +1958,7 @@ int fbm_jl_powmod(const uint32_t* h, const uint32_t* pt, uint64_t n_ct, const ui
   }
   jp.key_is_zero = is_zero;
   JlShort sh;
-  const bool shq = build_short(biprime, key, is_zero, sc, sh, g_short_on.load(std::memory_order_relaxed) != 0);
+  const bool shq = build_short(biprime, key, is_zero, sc, sh, t_short_on != 0);
   const uint64_t slots = table_slots_for(n_ct);
   if ((rc = timed("jl_setup", s, [&] { return launch_jl_setup(jp, sc, ops, cst, s, shq ? &sh : nullptr); })))
     return rc;
@@ -2083,15 +2061,6 @@ int fbm_int_true_div_big(const uint64_t* x, uint64_t n, const uint32_t* k, int k
   return timed("int_ops", s, [&] { return launch_int_true_div_big(x, n, k, k_words, negative ? 1 : 0, out, s); });
 }
 
-int fbm_test_true_div_big(const uint64_t* x, uint64_t n, const uint32_t* k, int k_words, int negative, double* out) {
-  if (!k || k_words < 1 || (n > 0 && (!x || !out))) {
-    set_error("fbm_test_true_div_big: bad arguments");
-    return FBM_E_ARG;
-  }
-  host_true_div_big(x, n, k, k_words, negative, out);
-  return FBM_OK;
-}
-
 int fbm_jl_batch_begin(void) { return jl_batch_begin(); }
 
 void fbm_jl_batch_abort(void) { jl_batch_abort(); }
@@ -2103,6 +2072,146 @@ uint64_t fbm_jl_batch_workspace(void) { return jl_batch_workspace(); }
 int fbm_jl_batch_flush(void* workspace, uint64_t workspace_bytes, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   return timed("jl_exp", s, [&] { return jl_batch_flush(workspace, workspace_bytes, s); });
+}
+
+int fbm_ass_split(const void* secret, int secret_dtype, uint64_t n, int n_shares, int bit_length,
+                  const uint8_t* seed, const uint8_t* nonce, uint64_t elem_offset, int64_t* shares, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n_shares < 1 || bit_length > 64 || !seed || !nonce || (secret_dtype != FBM_U64 && secret_dtype != FBM_I64)) {
+    set_error("invalid additive-sharing arguments (n_shares >= 1, bit_length <= 64, 64-bit secrets)");
+    return FBM_E_ARG;
+  }
+  if (n == 0) return FBM_OK;
+  if (!secret || !shares) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  uint32_t key[8], nw[2];
+  memcpy(key, seed, 32);
+  memcpy(nw, nonce, 8);
+  return timed("ass_split", s, [&] {
+    return launch_ass_split((const uint64_t*)secret, n, key, nw[0], nw[1], elem_offset, n_shares, bit_length,
+                            secret_dtype == FBM_I64, shares, s);
+  });
+}
+
+int fbm_ass_reconstruct(const int64_t* shares, int n_shares, uint64_t n, int64_t* out, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n_shares < 1) {
+    set_error("n_shares must be >= 1");
+    return FBM_E_ARG;
+  }
+  if (n == 0) return FBM_OK;
+  if (!shares || !out) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  return timed("ass_reconstruct", s, [&] { return launch_ass_reconstruct(shares, n_shares, n, out, s); });
+}
+
+int fbm_ass_split_wide(const uint32_t* secret, uint64_t n, int l_in, int n_shares, int bit_length, int l_out,
+                       const uint8_t* seed, const uint8_t* nonce, uint64_t elem_offset, uint32_t* shares,
+                       void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int bmax = bit_length >= 0 ? bit_length : 32 * l_in;
+  int pbits = 0;
+  while ((1ll << pbits) < (long long)n_shares) ++pbits;
+  if (n_shares < 1 || l_in < 1 || l_in > 4096 || l_out < l_in || !seed || !nonce ||
+      32ll * l_out < (long long)bmax + pbits + 2 || bmax > (1 << 20)) {
+    set_error("invalid wide additive-sharing arguments (n_shares >= 1, 1 <= l_in <= l_out, "
+              "32*l_out >= bits + ceil(log2 n_shares) + 2)");
+    return FBM_E_ARG;
+  }
+  if (n == 0) return FBM_OK;
+  if (!secret || !shares) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  uint32_t key[8], nw[2];
+  memcpy(key, seed, 32);
+  memcpy(nw, nonce, 8);
+  return timed("ass_split_wide", s, [&] {
+    return launch_ass_split_wide(secret, n, l_in, key, nw[0], nw[1], elem_offset, n_shares, bit_length, l_out,
+                                 shares, s);
+  });
+}
+
+int fbm_ass_reconstruct_wide(const uint32_t* shares, int n_shares, int l, uint64_t n, uint32_t* out, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n_shares < 1 || l < 1) {
+    set_error("n_shares and l must be >= 1");
+    return FBM_E_ARG;
+  }
+  if (n == 0) return FBM_OK;
+  if (!shares || !out) {
+    set_error("null pointer argument");
+    return FBM_E_ARG;
+  }
+  return timed("ass_reconstruct_wide", s,
+               [&] { return launch_ass_reconstruct_wide(shares, n_shares, l, n, out, s); });
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------
+// The test build's entry points (include/fbm_secagg_test.h; libfbm_secagg_test.so, compiled with
+// -DFBM_TEST_HOOKS from this same file and linked with the same kernel objects): host runs of device
+// routines, engine / short-path switches of the calling thread, engine and multiply counts, and the
+// per-kernel event timer.  The product library (libfbm_secagg.so) exports none of them.
+// ---------------------------------------------------------------------------------------
+#ifdef FBM_TEST_HOOKS
+extern "C" {
+
+int fbm_jl_window(void) { return FBM_WIN; }
+int fbm_jl_mads(int square) {  // 0: general product, 1: square, 2: short-base product
+  return square == 2 ? FBM_NA_MADS_SHORT : square ? FBM_NA_MADS_SQR : FBM_NA_MADS_MUL;
+}
+int fbm_jl_quad_mads(int square) {
+  return 4 * (square == 2 ? FBM_QA_MADS_SHORT : square ? FBM_QA_MADS_SQR : FBM_QA_MADS_MUL);
+}
+int fbm_jl_triple_mads(int square) {
+  return 3 * (square == 2 ? FBM_TA_MADS_SHORT : square ? FBM_TA_MADS_SQR : FBM_TA_MADS_MUL);
+}
+
+int fbm_jl_set_engine(int mode) {
+  if (mode != FBM_ENGINE_AUTO && mode != FBM_ENGINE_SINGLE && mode != FBM_ENGINE_GENERIC && mode != FBM_ENGINE_QUAD &&
+      mode != FBM_ENGINE_TRIPLE) {
+    set_error("fbm_jl_set_engine: mode must be 0 (auto), 1 (one lane per ciphertext), 2 (generic: any modulus), "
+              "3 (three lanes) or 4 (four)");
+    return FBM_E_ARG;
+  }
+  return jl_engine_set(mode);
+}
+
+int fbm_jl_engine_for(uint64_t n_ct) { return jl_engine_for(n_ct); }
+
+int fbm_jl_set_short(int on) {
+  const int prev = t_short_on;
+  t_short_on = on ? 1 : 0;
+  return prev;
+}
+
+int fbm_test_short_cache(uint32_t* out, int cap_words) {
+  std::lock_guard<std::mutex> lk(g_jp_mu);
+  const int per = (int)(sizeof(JlShortCacheEntry) / 4);
+  const int n = (int)g_short_cache.size();
+  if (out) {
+    if (cap_words < n * per) {
+      set_error("fbm_test_short_cache: %d words needed", n * per);
+      return FBM_E_ARG;
+    }
+    for (int i = 0; i < n; ++i) memcpy(out + i * per, &g_short_cache[i], sizeof(JlShortCacheEntry));
+  }
+  return n * per;
+}
+
+int fbm_test_true_div_big(const uint64_t* x, uint64_t n, const uint32_t* k, int k_words, int negative, double* out) {
+  if (!k || k_words < 1 || (n > 0 && (!x || !out))) {
+    set_error("fbm_test_true_div_big: bad arguments");
+    return FBM_E_ARG;
+  }
+  host_true_div_big(x, n, k, k_words, negative, out);
+  return FBM_OK;
 }
 
 int fbm_test_fdh_gcd(const uint32_t* r8, const uint32_t* n32, uint32_t* err) {
@@ -2198,86 +2307,11 @@ int fbm_test_modinv(const uint32_t* x, const uint32_t* n, uint32_t* out, int* ba
   return FBM_OK;
 }
 
-int fbm_ass_split(const void* secret, int secret_dtype, uint64_t n, int n_shares, int bit_length,
-                  const uint8_t* seed, const uint8_t* nonce, uint64_t elem_offset, int64_t* shares, void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  if (n_shares < 1 || bit_length > 64 || !seed || !nonce || (secret_dtype != FBM_U64 && secret_dtype != FBM_I64)) {
-    set_error("invalid additive-sharing arguments (n_shares >= 1, bit_length <= 64, 64-bit secrets)");
-    return FBM_E_ARG;
-  }
-  if (n == 0) return FBM_OK;
-  if (!secret || !shares) {
-    set_error("null pointer argument");
-    return FBM_E_ARG;
-  }
-  uint32_t key[8], nw[2];
-  memcpy(key, seed, 32);
-  memcpy(nw, nonce, 8);
-  return timed("ass_split", s, [&] {
-    return launch_ass_split((const uint64_t*)secret, n, key, nw[0], nw[1], elem_offset, n_shares, bit_length,
-                            secret_dtype == FBM_I64, shares, s);
-  });
+int fbm_test_lom_aggregate_kernel(int n_parties, uint64_t n, const void* y, char* buf, int len) {
+  const int rc = lom_aggregate_kernel_name(n_parties, n, y, buf, len);
+  if (rc) set_error("fbm_test_lom_aggregate_kernel: bad arguments or buffer too small");
+  return rc;
 }
-
-int fbm_ass_reconstruct(const int64_t* shares, int n_shares, uint64_t n, int64_t* out, void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  if (n_shares < 1) {
-    set_error("n_shares must be >= 1");
-    return FBM_E_ARG;
-  }
-  if (n == 0) return FBM_OK;
-  if (!shares || !out) {
-    set_error("null pointer argument");
-    return FBM_E_ARG;
-  }
-  return timed("ass_reconstruct", s, [&] { return launch_ass_reconstruct(shares, n_shares, n, out, s); });
-}
-
-int fbm_ass_split_wide(const uint32_t* secret, uint64_t n, int l_in, int n_shares, int bit_length, int l_out,
-                       const uint8_t* seed, const uint8_t* nonce, uint64_t elem_offset, uint32_t* shares,
-                       void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  const int bmax = bit_length >= 0 ? bit_length : 32 * l_in;
-  int pbits = 0;
-  while ((1ll << pbits) < (long long)n_shares) ++pbits;
-  if (n_shares < 1 || l_in < 1 || l_in > 4096 || l_out < l_in || !seed || !nonce ||
-      32ll * l_out < (long long)bmax + pbits + 2 || bmax > (1 << 20)) {
-    set_error("invalid wide additive-sharing arguments (n_shares >= 1, 1 <= l_in <= l_out, "
-              "32*l_out >= bits + ceil(log2 n_shares) + 2)");
-    return FBM_E_ARG;
-  }
-  if (n == 0) return FBM_OK;
-  if (!secret || !shares) {
-    set_error("null pointer argument");
-    return FBM_E_ARG;
-  }
-  uint32_t key[8], nw[2];
-  memcpy(key, seed, 32);
-  memcpy(nw, nonce, 8);
-  return timed("ass_split_wide", s, [&] {
-    return launch_ass_split_wide(secret, n, l_in, key, nw[0], nw[1], elem_offset, n_shares, bit_length, l_out,
-                                 shares, s);
-  });
-}
-
-int fbm_ass_reconstruct_wide(const uint32_t* shares, int n_shares, int l, uint64_t n, uint32_t* out, void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  if (n_shares < 1 || l < 1) {
-    set_error("n_shares and l must be >= 1");
-    return FBM_E_ARG;
-  }
-  if (n == 0) return FBM_OK;
-  if (!shares || !out) {
-    set_error("null pointer argument");
-    return FBM_E_ARG;
-  }
-  return timed("ass_reconstruct_wide", s,
-               [&] { return launch_ass_reconstruct_wide(shares, n_shares, l, n, out, s); });
-}
-
-}  // extern "C"
-
-extern "C" {
 
 int fbm_prof_enable(int on) {
   std::lock_guard<std::mutex> g(g_prof_mu);
@@ -2318,3 +2352,4 @@ int fbm_prof_report(char* buf, int len) {
 }
 
 }  // extern "C"
+#endif  // FBM_TEST_HOOKS

@@ -51,6 +51,8 @@ int launch_lom_protect(const void* x, int x_dtype, uint64_t n, const QuantParams
 int launch_lom_mask_accumulate(uint64_t n, const LomPeers& peers, uint64_t* y, hipStream_t s);
 int launch_dequantize(const uint64_t* u, uint64_t n, double neg_c, double step, double* out, hipStream_t s);
 int launch_prf_key(const LomPeers& peers, uint32_t* seed_out, hipStream_t s);
+// the aggregate kernel's name (test build: fbm_test_lom_aggregate_kernel)
+int lom_aggregate_kernel_name(int n_parties, uint64_t n, const void* y, char* buf, int len);
 int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t total_weight, double neg_c,
                          double step, double* out, uint64_t* sums, uint32_t* stats, hipStream_t s);
 

@@ -2210,27 +2210,16 @@ int launch_jl_setup(const JlParams& jp, const JlSched& sc, uint32_t* ops, uint32
 // B = 7.8).  The one-lane engine: 31.7 ms up to one wave per SIMD, 56 ms for a launch of one round
 // of two, 50 ms per round of longer launches.  (A build with 4 resident group waves per SIMD,
 // -DFBM_GROUP_WAVES=4, measured no faster at w = 4: the issue is already saturated at 3.)
-static std::atomic<int> g_engine{-1};
+// The policy is per THREAD (round 6): a caller that picks an engine for its launches (the test build's
+// fbm_jl_set_engine, include/fbm_secagg_test.h) changes nothing for the process's other threads.  The
+// product library never sets it: every launch takes the cost model's engine (FBM_ENGINE_AUTO).
+static thread_local int t_engine = FBM_ENGINE_AUTO;
 
-int jl_engine_policy() {
-  int e = g_engine.load(std::memory_order_relaxed);
-  if (e < 0) {  // first use: FBM_JL_ENGINE=auto|single|quad|triple (A/B runs), default auto
-    const char* v = getenv("FBM_JL_ENGINE");
-    e = FBM_ENGINE_AUTO;
-    if (v && !strcmp(v, "single")) e = FBM_ENGINE_SINGLE;
-    if (v && !strcmp(v, "quad")) e = FBM_ENGINE_QUAD;
-    if (v && !strcmp(v, "triple")) e = FBM_ENGINE_TRIPLE;
-    if (v && !strcmp(v, "generic")) e = FBM_ENGINE_GENERIC;
-    int expect = -1;
-    g_engine.compare_exchange_strong(expect, e);
-    e = g_engine.load(std::memory_order_relaxed);
-  }
-  return e;
-}
+int jl_engine_policy() { return t_engine; }
 
 int jl_engine_set(int mode) {
-  const int prev = jl_engine_policy();
-  g_engine.store(mode, std::memory_order_relaxed);
+  const int prev = t_engine;
+  t_engine = mode;
   return prev;
 }
 
@@ -2381,13 +2370,21 @@ int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const Jl
     // resident workgroups finish first: the aggregate's 1/4 stripe (83 334 ciphertexts) 43.0 -> 40.8 ms,
     // 64 512 ciphertexts 33.7 -> 31.1 (triple) and 32.9 -> 30.6 (quad); past that three (100 000: 51.8
     // against 60.3) -- profiles/r5bm_group_wgs.jsonl.  FBM_GROUP_WGS = 1..3 overrides (A/B).
+#ifdef FBM_AB_KNOBS  // A/B builds only (python -m fedbiomed_amd._build --out ... -DFBM_AB_KNOBS)
     static const uint64_t wgs_env = getenv("FBM_GROUP_WGS") ? (uint64_t)atoi(getenv("FBM_GROUP_WGS")) : 0u;
+#else
+    constexpr uint64_t wgs_env = 0u;
+#endif
     const uint64_t ncu = (uint64_t)device_num_cu();
     const uint64_t wgs_cu = wgs_env >= 1 && wgs_env <= FBM_GROUP_WGS_PER_CU ? wgs_env : g <= 4 * ncu ? 2u : 3u;
     if (g > ncu * wgs_cu) g = ncu * wgs_cu;
     // probe knob (A/B of workgroup placement): extra dynamic LDS per workgroup, e.g. enough to hold a
     // group launch to two workgroups per CU
+#ifdef FBM_AB_KNOBS
     static const unsigned glds_pad = getenv("FBM_GROUP_LDS_PAD") ? (unsigned)atoi(getenv("FBM_GROUP_LDS_PAD")) : 0u;
+#else
+    constexpr unsigned glds_pad = 0u;
+#endif
     if (eng == FBM_ENGINE_QUAD) {
       hipLaunchKernelGGL(jl_expg_kernel<4>, dim3((unsigned)g), dim3(FBM_QBLOCK), glds_pad, s, H, n_ct, (uint32_t*)cst,
                          jp.qa.np, ops, sc.n_ops, sc.first, mode, jp.key_is_zero, sc.sbits, nude, table, out, Hc);
@@ -2402,7 +2399,11 @@ int launch_jl_exp(const uint32_t* H, uint64_t n_ct, const JlParams& jp, const Jl
   if (g > gmax) g = gmax;
   // probe knob (tools/mixed_probe.py): extra dynamic LDS per workgroup, e.g. enough to hold the
   // one-lane engine to one workgroup per CU
+#ifdef FBM_AB_KNOBS
   static const unsigned lds_pad = getenv("FBM_EXP_LDS_PAD") ? (unsigned)atoi(getenv("FBM_EXP_LDS_PAD")) : 0u;
+#else
+  constexpr unsigned lds_pad = 0u;
+#endif
   hipLaunchKernelGGL(jl_exp_kernel<false>, dim3((unsigned)g), dim3(FBM_BLOCK), lds_pad, s, H, n_ct, (uint32_t*)cst, jp.qa.np,
                      ops, sc.n_ops, sc.first, mode, jp.key_is_zero, sc.sbits, nude, table, out, (const JlExpSeg*)nullptr,
                      0, 0u, (uint32_t*)nullptr, Hc);

@@ -10,6 +10,8 @@
 //
 // Layout in HBM: x (f32 or f64, n), y (u64, n) per party; aggregate input is a
 // P x n row-major u64 matrix (party-major) -> out f64 n (+ optional u64 sums).
+#include <cstdio>
+
 #include "fbm_internal.hpp"
 
 namespace fbm {
@@ -388,11 +390,32 @@ int launch_prf_key(const LomPeers& peers, uint32_t* seed_out, hipStream_t s) {
   return check_launch("prf_key_kernel");
 }
 
+// The column-sum kernel a launch of n_parties rows of n elements at y takes: the wave-split form for
+// 8 and 16 parties on 16-byte aligned rows of an even length, the one-thread-per-EPT-elements form
+// otherwise (PC = the compiled party count, 0 = any).  launch_lom_aggregate dispatches on it, and the
+// test build names it (fbm_test_lom_aggregate_kernel): the bench keys its committed HBM-traffic
+// profile on the kernel that ran.
+static bool lom_agg_ws(int n_parties, uint64_t n, const uint64_t* y) {
+  const bool aligned = (n % 2) == 0 && (reinterpret_cast<uintptr_t>(y) % 16) == 0;
+  return FBM_AGG_WS && aligned && (n_parties == 16 || n_parties == 8);
+}
+
+int lom_aggregate_kernel_name(int n_parties, uint64_t n, const void* y, char* buf, int len) {
+  if (n_parties < 1 || !buf || len < 1) return FBM_E_ARG;
+  int w;
+  if (lom_agg_ws(n_parties, n, (const uint64_t*)y))
+    w = snprintf(buf, (size_t)len, "lom_aggregate_ws_kernel<2, %d, %d>", n_parties == 16 ? 8 : FBM_AGG_WS_W8, n_parties);
+  else {
+    const int pc = (n_parties == 2 || n_parties == 3 || n_parties == 4 || n_parties == 8 || n_parties == 16) ? n_parties : 0;
+    w = snprintf(buf, (size_t)len, "lom_aggregate_kernel<%d, %d>", FBM_AGG_EPT, pc);
+  }
+  return w < len ? FBM_OK : FBM_E_ARG;
+}
+
 int launch_lom_aggregate(const uint64_t* y, int n_parties, uint64_t n, uint64_t total_weight, double neg_c, double step,
                          double* out, uint64_t* sums, uint32_t* stats, hipStream_t s) {
   if (n == 0) return FBM_OK;
-  const bool aligned = (n % 2) == 0 && (reinterpret_cast<uintptr_t>(y) % 16) == 0;
-  if (FBM_AGG_WS && aligned && (n_parties == 16 || n_parties == 8)) {
+  if (lom_agg_ws(n_parties, n, y)) {
     const dim3 grid((unsigned)((n + 127) / 128));
     if (n_parties == 16)
       hipLaunchKernelGGL((lom_aggregate_ws_kernel<2, 8, 16>), grid, dim3(512), 0, s, y, n, total_weight, neg_c, step,

@@ -16,6 +16,10 @@
  *  - big integers are little-endian arrays of uint32 limbs (== int.to_bytes(.., 'little')).
  *  - return value: FBM_OK or a negative FBM_E_* code; fbm_last_error() has the message
  *    (thread-local).
+ *  - libfbm_secagg.so exports exactly the functions declared here (a linker version script made
+ *    from this header; tests/test_native_abi.py checks `nm -D`).  The test suite's and the bench's
+ *    hooks -- host runs of device routines, per-thread engine switches, the per-kernel event timer
+ *    -- are declared in fbm_secagg_test.h and exported by libfbm_secagg_test.so only.
  */
 #ifndef FBM_SECAGG_H
 #define FBM_SECAGG_H
@@ -27,7 +31,8 @@
 extern "C" {
 #endif
 
-#define FBM_ABI_VERSION 6 /* 6: fbm_lom_*_host; 5: fbm_jl_encrypt_factor; 4: fbm_ves_pack takes is_signed; 3: the JL round is an 8192-bit value (FBM_TAU_LIMBS limbs);
+#define FBM_ABI_VERSION 7 /* 7: the test, A/B and profiling hooks left this header for fbm_secagg_test.h (exported by
+                             the test build only); 6: fbm_lom_*_host; 5: fbm_jl_encrypt_factor; 4: fbm_ves_pack takes is_signed; 3: the JL round is an 8192-bit value (FBM_TAU_LIMBS limbs);
                              2 took 16 limbs, 1 a uint64 */
 /* The JL round `tau` of every JL entry point: a HOST pointer to FBM_TAU_LIMBS little-endian 32-bit
  * words, any round below 2^8192 -- FDH.H hashes t = (k << 512) | tau as t.to_bytes(1024, 'big')
@@ -291,8 +296,6 @@ int fbm_ves_pack(const uint32_t* x, uint64_t n, int wv, int es, int cr, int pw, 
                  void* stream);
 int fbm_ves_unpack(const uint32_t* pt, uint64_t n_ct, int pw, int es, int cr, uint64_t n_out, int ow, uint32_t* vals,
                    void* stream);
-/* host test hook (no GPU): fbm_int_true_div_big's per-value arithmetic on host arrays. */
-int fbm_test_true_div_big(const uint64_t* x, uint64_t n, const uint32_t* k, int k_words, int negative, double* out);
 
 /* ---- additive secret sharing of vectors (reference fedbiomed/common/secagg/_additive_ss.py) ----
  * fbm_ass_split replaces AdditiveSecret.split / _shares_int (:40-98) for a list secret:
@@ -324,37 +327,6 @@ int fbm_ass_split_wide(const uint32_t* secret, uint64_t n, int l_in, int n_share
                        void* stream);
 int fbm_ass_reconstruct_wide(const uint32_t* shares, int n_shares, int l, uint64_t n, uint32_t* out, void* stream);
 
-/* Sliding-window width of the JL exponentiation's table path (odd-power table of 2^(w-1) entries;
- * the short path -- one FDH digest, N > 2^262: every 1024-bit biprime -- needs no table). */
-int fbm_jl_window(void);
-/* v_mad_u64_u32 per lane of one product of the JL exponentiation engine (N-adic Montgomery
- * product modulo N^2, fedbiomed_amd/csrc/fbm_nadic_asm.hpp): square = 0 a general product, 1 a
- * squaring, 2 the short path's short-base product (x h 2^-261); lets the bench count the
- * multiplies one ciphertext costs (its VALU roofline). */
-int fbm_jl_mads(int square);
-/* The same count for the quad / triple engines (4 / 3 lanes per ciphertext): v_mad_u64_u32
- * lane-ops per product summed over the lanes (fedbiomed_amd/csrc/fbm_quad_asm.hpp, fbm_tri_asm.hpp);
- * square = 2: the short-base product. */
-int fbm_jl_quad_mads(int square);
-int fbm_jl_triple_mads(int square);
-
-/* Exponentiation engine policy of this process for the JL entry points (encrypt, decryption
- * factor, aggregate): 0 = auto (the default: the engine of least modelled launch time for the
- * launch's ciphertext count -- lane groups of 4 or 3 below the chip's one-lane round, one lane
- * otherwise; fedbiomed_amd/csrc/fbm_jl.hip engine_model_ms), 1 = one lane per ciphertext
- * (throughput: several concurrent launches that fill the chip together), 3 / 4 = three / four
- * lanes per ciphertext (latency), 2 = the generic engine for every modulus (fbm_gen.hip: Barrett
- * products, any N; even N always take it -- under this policy odd N do too, a cross-check of the
- * Montgomery engines).  Results are bit-identical either way.  Returns the previous policy (or
- * FBM_E_ARG).  FBM_JL_ENGINE=auto|single|triple|quad|generic sets the initial one.
- * fbm_jl_engine_for: the engine a launch of n_ct ciphertexts takes under the policy (1-4). */
-int fbm_jl_set_engine(int mode);
-int fbm_jl_engine_for(uint64_t n_ct);
-/* The exponentiation's short path (a binary chain with the 9-row short-base product, taken for a
- * one-digest FDH h and N > 2^262: DESIGN.md 5.3) on (1, the default) or off (0: every wave runs the
- * sliding-window table path -- an A/B and test switch; results are bit-identical).  Returns the
- * previous setting. */
-int fbm_jl_set_short(int on);
 /* Drops the library's host-side caches: the short path's constant C per (N, |key|) -- kept under a
  * SHA-256 digest of (N, |key|), never the key itself, and zeroed here and on eviction -- and the
  * per-biprime public parameters.  The reference keeps nothing between calls (a fresh
@@ -383,47 +355,6 @@ void fbm_jl_batch_abort(void);
 int fbm_jl_batch_count(void);
 uint64_t fbm_jl_batch_workspace(void);
 int fbm_jl_batch_flush(void* workspace, uint64_t workspace_bytes, void* stream);
-
-/* ---- host test hook (no GPU): the device modular-inverse routine (Bernstein-Yang divsteps,
- * fedbiomed_amd/csrc/fbm_safegcd.hpp) run on the host, for unit tests.
- * x, n, out: 32 little-endian words (n odd);  batches: number of 30-divstep batches used. */
-int fbm_test_modinv(const uint32_t* x, const uint32_t* n, uint32_t* out, int* batches);
-/* host test hook (no GPU): the FDH's one-digest coprimality test (fbm_jl.hip gcd_is_one_r8) --
- * r8: 8 words (a 256-bit digest), n32: 32 words (odd N).  Returns 1 if gcd(r, N) == 1, 0 if
- * not, a negative FBM_E_* code on bad arguments; *err receives device error flags. */
-int fbm_test_fdh_gcd(const uint32_t* r8, const uint32_t* n32, uint32_t* err);
-/* host test hooks (no GPU): one ciphertext of the generic engine (fedbiomed_amd/csrc/fbm_gen.hip)
- * run on the host, any N (1 <= N < 2^1024).  fbm_test_gen_exp: out (64 words) = h^key mod N^2 (the
- * inverse of h^|key| for key_negative), times (N pt + 1) mod N^2 when pt (32 words; `negative`:
- * pt holds |pt| of a negative packing) is not NULL; h: 64 words.  fbm_test_gen_combine: v =
- * prod of n_parties 64-word rows (cts, row-major) times factor (64 words, may be NULL) mod N^2;
- * mode 0: out = v (64 words), mode 1: out = ((v - 1) // N) mod N (32 words).  *err receives the
- * device error flags. */
-int fbm_test_gen_exp(const uint32_t* h, const uint32_t* pt, int negative, const uint32_t* biprime, const uint32_t* key,
-                     int key_negative, uint32_t* out, uint32_t* err);
-int fbm_test_gen_combine(const uint32_t* cts, int n_parties, const uint32_t* factor, const uint32_t* biprime,
-                         int mode, uint32_t* out, uint32_t* err);
-/* host test hook (no GPU): the N-adic engine's per-modulus constants as the library builds
- * them -- nk: 80 words (29-bit N limbs, K'_i), r2na / r3na: 72 limbs (29-bit digits of R^2 /
- * R^3 mod N^2, R = 2^1044), np = -N^-1 mod 2^29. */
-int fbm_test_nadic_consts(const uint32_t* n32, uint32_t* nk, uint32_t* r2na, uint32_t* r3na, uint32_t* np);
-/* host test hook (no GPU): the short path's per-call words as the library builds them -- kw: |key|'s
- * 64 words, corr: 72 29-bit limbs (the N-adic digits of C = 2^(1044 (2^s + 1) + 261 (|key| - 2^s))
- * mod N^2), d: 36 limbs of N - 2^261.  Returns s = bit length of |key| - 1 (-1 for a zero key), or
- * -2 when N is outside the path's domain (N <= 2^262 or even). */
-int fbm_test_short_consts(const uint32_t* n32, const uint32_t* key, uint32_t* kw, uint32_t* corr, uint32_t* d);
-/* host test hook (no GPU): the raw words of the short path's cache entries (each: an 8-word digest
- * and 72 limbs of C); returns the word count (out == NULL: a size query), FBM_E_ARG if cap_words is
- * too small. */
-int fbm_test_short_cache(uint32_t* out, int cap_words);
-
-/* ---- instrumentation -------------------------------------------------------------------
- * fbm_prof_enable(1) makes every entry point record a HIP event pair around each kernel
- * launch (on the caller's stream); fbm_prof_report() synchronises them and returns the
- * bytes needed for the "kernel count total_ms" lines; when len >= that, it writes them
- * into buf and clears the aggregate (buf == NULL is a non-destructive size query).       */
-int fbm_prof_enable(int on);
-int fbm_prof_report(char* buf, int len);
 
 #ifdef __cplusplus
 }

@@ -105,7 +105,7 @@ def test_wide_divisor_true_division_host(golden):
 
     from fedbiomed_amd import _native as N
 
-    lib = N.load()
+    lib = N.load_test()  # the test build's host hook
     rng = random.Random(65)
 
     def div(vs, k):

@@ -181,10 +181,15 @@ def test_cfg4_jl_10m_8_parties_8_stripes(dev):
                                         ct_offset=k0))
         del cts
     assert torch.equal(torch.cat(outs), out_whole)
-    # sampled ciphertexts (first, last/partial, stripe boundaries, random) vs the oracle
+    # sampled ciphertexts vs the oracle: every stripe's first and last ciphertext (so both sides of
+    # each of the 7 cut points, the vector's first and its last, partial one), and random ones
     rng = np.random.default_rng(4)
-    bounds = [Dd.jl_shard(n, world, r, cr_)[0] // cr_ for r in range(1, world)]
-    ks = sorted({0, n_ct - 1, *bounds, *rng.choice(n_ct, 22, replace=False).tolist()})
+    edges = set()
+    for r in range(world):
+        lo, hi = Dd.jl_shard(n, world, r, cr_)
+        edges |= {lo // cr_, (hi + cr_ - 1) // cr_ - 1}
+    assert len(edges) == 2 * world and {0, n_ct - 1} <= edges
+    ks = sorted(edges | set(rng.choice(n_ct, 22, replace=False).tolist()))
     for p in range(P):
         got = D.limbs_to_ints(whole[p, ks].cpu().numpy())
         for k, g in zip(ks, got):
@@ -201,41 +206,69 @@ def test_cfg4_jl_10m_8_parties_8_stripes(dev):
     assert np.array_equal(out_whole.cpu().numpy()[idx].view(np.uint64), ref.view(np.uint64))
 
 
+def _host_qw_sum(acc: np.ndarray, x: np.ndarray, w: int, threads: int = 8) -> None:
+    """acc += O.quantize(x) * w (mod 2^64), on host threads over chunks (numpy releases the GIL):
+    the oracle's quantise of a 100M-element vector in about a second instead of six."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    step = -(-len(x) // threads)
+
+    def part(a):
+        with np.errstate(over="ignore"):
+            acc[a:a + step] += O.quantize(x[a:a + step]) * np.uint64(w)
+
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(part, range(0, len(x), step)))
+
+
 def test_cfg5_lom_ass_100m_16_parties(dev):
+    """Config 5 on one GPU: 16 parties' LOM protects of a 100M-element vector, the aggregate and
+    the additive sharing of the sum.  Every expected value comes from the CPU oracle: the exact
+    masked sum is sum_p quantize(x_p) * w_p computed on the host (_lom.py:105-175: the masks
+    cancel), and every party's masked vector is checked bit for bit on windows at each cut point
+    of an 8-GPU element-range split (distributed.lom_shard) and at both ends of the vector."""
+    from fedbiomed_amd import distributed as Dd
     from fedbiomed_amd.secagg import AdditiveSecret, AdditiveShares, SecaggLomCrypter
 
-    n, P, tau = 100_000_000, 16, 1
+    n, P, tau, world = 100_000_000, 16, 1, 8
     ids, ws = W.node_ids(P), [W.party_weight(p) for p in range(P)]
     nonce = O.lom_nonce(W.LOM_NONCE)
     cr = SecaggLomCrypter(W.LOM_NONCE)
     gen = torch.Generator(device=dev)
     Y = torch.empty((P, n), dtype=torch.int64, device=dev)
-    qsum = torch.zeros(n, dtype=torch.int64, device=dev)
-    x1 = None
+    want = np.zeros(n, dtype=np.uint64)  # the oracle's sum_p q_p w_p (mod 2^64)
+    cuts = [Dd.lom_shard(n, world, r)[0] for r in range(1, world)]
+    assert all(c % 8 == 0 for c in cuts)
+    m = 512  # a window of m elements on each side of every cut point, and at both ends
+    wins = [(0, m)] + [(c - m, 2 * m) for c in cuts] + [(n - m - 3, m + 3)]
     for p, u in enumerate(ids):
         gen.manual_seed(500 + p)
         x = torch.randn(n, generator=gen, device=dev, dtype=torch.float32) * 0.05
         x[:: 997] = 4.0 * (1 - 2 * (p & 1))  # clipped entries
         Y[p] = cr.encrypt_tensor(tau, u, x, W.pairwise_secrets_for(u, ids), ids, weight=ws[p])
-        qsum += D.lom_protect(x, [], [], b"\0" * 16, 0, 0, weight=ws[p])  # q*w, no masks
-        if p == 5:
-            x1 = x
-    # masks cancel exactly over all 100M elements (u64 wrap == int64 wrap)
+        xh = x.cpu().numpy()
+        _host_qw_sum(want, xh, ws[p])
+        for off, k in wins:
+            ref = _lom_window_oracle(u, ids, tau, _qw(xh[off:off + k], ws[p]), off, nonce)
+            assert np.array_equal(_u64(Y[p, off:off + k]), ref), (p, off)
+        del x, xh
+    # masks cancel exactly over all 100M elements (u64 wrap == int64 wrap), against the host sum
     out, sums = cr.aggregate_tensor(Y, sum(ws), want_sums=True)
-    assert torch.equal(sums, qsum)
-    # party 5 bit-exact on windows at the start, an interior, the end (ChaCha counter-indexed)
-    for off, m in ((0, 4096), (57_345_672, 4096), (n - 1000, 1000)):
-        xw = x1[off:off + m].cpu().numpy()
-        ref = _lom_window_oracle(ids[5], ids, tau, _qw(xw, ws[5]), off, nonce)
-        assert np.array_equal(_u64(Y[5, off:off + m]), ref), off
+    assert np.array_equal(_u64(sums), want)
     idx = np.random.default_rng(5).choice(n, 3000, replace=False)
-    s_np = _u64(sums)[idx]
-    refo = O.reverse_quantize(O.apply_average([int(v) for v in s_np], sum(ws)))
+    idx = np.concatenate([idx, np.asarray([0, n - 1] + cuts + [c - 1 for c in cuts])])
+    refo = O.reverse_quantize(O.apply_average([int(v) for v in want[idx]], sum(ws)))
     assert np.array_equal(out.cpu().numpy()[idx].view(np.uint64), refo.view(np.uint64))
     del Y, out
-    # additive secret sharing of the 100M summed vector into 16 shares, and back (exact)
+    # additive secret sharing of the 100M summed vector into 16 shares, and back: the exact column
+    # sum (_additive_ss.py:252-267) is the oracle's sum again
     shares = AdditiveSecret.split_tensor(sums, P, unsigned=True)
     rec = AdditiveShares.reconstruct_tensor(shares)
-    assert torch.equal(rec[:, 0], sums) and bool((rec[:, 1] == 0).all())
+    assert np.array_equal(_u64(rec[:, 0]), want) and bool((rec[:, 1] == 0).all())
     hi = shares[:-1, :, 1]
     assert bool(((hi == 0) | (hi == 1)).all())  # first P-1 shares in [0, 2^64]
+    # a sampled column of shares summed on the host as Python ints (no modulus, as the reference)
+    cols = shares[:, idx[:64]].cpu().numpy()
+    for j, e in enumerate(idx[:64]):
+        tot = sum(int(cols[q, j, 0]) % 2 ** 64 + (int(cols[q, j, 1]) << 64) for q in range(P))
+        assert tot == int(want[e]), e

@@ -161,6 +161,62 @@ def _gather_shards(rank, world):
     return res
 
 
+N8_U64 = 10_003  # ragged: not a multiple of 8 * 8
+N8_CT = 1_237  # ciphertexts per party, ragged over 8 stripes
+
+
+def _local_u64(rank):
+    """Rank r's local masked sum: deterministic int64 bit patterns spanning the whole u64 range."""
+    rng = np.random.default_rng(800 + rank)
+    return rng.integers(-2**63, 2**63 - 1, N8_U64, dtype=np.int64, endpoint=True)
+
+
+def _local_cts(rank, ppr):
+    """Rank r's parties' ciphertext limbs [ppr, N8_CT, 64] (int32), distinct per (party, ct, limb)."""
+    rng = np.random.default_rng(900 + rank)
+    return rng.integers(-2**31, 2**31 - 1, (ppr, N8_CT, 64), dtype=np.int32, endpoint=True)
+
+
+def _world8_collectives(rank, world):
+    """every collective of distributed.py at the driver's world size -- the LOM
+    reduce-scatter of u64 sums, the stripes' all-gather back, the JL all-to-all of ciphertext stripes
+    (one and two parties per rank) and the element-range split's final gather -- on gloo."""
+    out = {}
+    stripe = Dd.reduce_scatter_u64(torch.from_numpy(_local_u64(rank)), N8_U64)
+    out["rs_stripe"] = stripe.numpy().copy()
+    out["rs_full"] = Dd.all_gather_stripes(stripe, N8_U64, 8).numpy()
+    for ppr in (1, 2):
+        got, k0 = Dd.all_to_all_ciphertexts(torch.from_numpy(_local_cts(rank, ppr)), ppr)
+        out[f"a2a{ppr}"] = (got.numpy(), k0)
+    lo, hi = Dd.shard_range(10_000_000, world, rank, 30)
+    full = torch.arange(lo, hi, dtype=torch.float64) * 0.25
+    g = Dd.all_gather_shards(full, 10_000_000, 30)
+    out["shards_ok"] = bool(torch.equal(g, torch.arange(10_000_000, dtype=torch.float64) * 0.25))
+    return out
+
+
+def test_world8_collectives_equal_single_rank_gloo():
+    """The 8-rank form of every exchange (gloo, 8 processes, 127.0.0.1) equals the single-rank
+    result: the u64 sum mod 2^64 of all ranks' vectors, every party's ciphertexts in rank-major party
+    order for each stripe of stripe_bounds, and the whole output vector on every rank."""
+    world = 8
+    res = _spawn("_world8_collectives", world)
+    with np.errstate(over="ignore"):
+        want = sum(_local_u64(r).view(np.uint64) for r in range(world)).view(np.int64)
+    per, bounds = Dd.stripe_bounds(N8_U64, world, 8)
+    cper, cbounds = Dd.stripe_bounds(N8_CT, world, 1)
+    for r in range(world):
+        lo, hi = bounds[r]
+        assert np.array_equal(res[r]["rs_stripe"], want[lo:hi]), r
+        assert np.array_equal(res[r]["rs_full"], want), r
+        for ppr in (1, 2):
+            allp = np.concatenate([_local_cts(q, ppr) for q in range(world)])  # rank-major parties
+            got, k0 = res[r][f"a2a{ppr}"]
+            c0, c1 = cbounds[r]
+            assert k0 == c0 and np.array_equal(got, allp[:, c0:c1]), (r, ppr)
+        assert res[r]["shards_ok"], r
+
+
 # ---- tests ---------------------------------------------------------------------------------
 @pytest.mark.parametrize("world", [2, 3])
 def test_all_gather_shards_gloo(world):

@@ -45,12 +45,12 @@ def _run(outcome, fn):
 
 
 class _Host:
-    """The generic engine's per-ciphertext work run on the host (include/fbm_secagg.h test hooks)."""
+    """The generic engine's per-ciphertext work run on the host (include/fbm_secagg_test.h hooks)."""
 
     def __init__(self):
         from fedbiomed_amd import _native as N
 
-        self.lib = N.load()
+        self.lib = N.load_test()
         self.N = N
 
     def exp(self, h: int, key: int, n: int, pt=None, negative=False) -> int:

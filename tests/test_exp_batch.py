@@ -206,8 +206,18 @@ def test_short_path_equals_table_path(engine):
         assert torch.equal(a, b)
 
 
+@pytest.fixture
+def test_build():
+    """The whole test through the test build (_native.test_hooks): a split call's phases must run in
+    the library whose switches set its path, and whose records hold it."""
+    from fedbiomed_amd import _native
+
+    with _native.test_hooks():
+        yield _native.load_test()
+
+
 @pytest.mark.gpu
-def test_split_calls_follow_their_phase1_path():
+def test_split_calls_follow_their_phase1_path(test_build):
     """a split call (encrypt with defer_exp, a phased factor) takes the path its
     phase 1 set up -- generic or Montgomery engine, short path or table path -- even when the
     process-wide switches change before its later phases; and a batch whose first segment ran with the
@@ -255,7 +265,7 @@ def test_split_calls_follow_their_phase1_path():
 
 
 @pytest.mark.gpu
-def test_split_call_survives_clear_caches_and_refuses_unknown_workspace():
+def test_split_call_survives_clear_caches_and_refuses_unknown_workspace(test_build):
     """fbm_jl_clear_caches between a split call's phases leaves its phase-1 path
     record alone (the result equals the unsplit call's even with the switches changed in between),
     and a later phase on a workspace phase 1 never ran on is FBM_E_ARG, not a guess."""
@@ -265,7 +275,7 @@ def test_split_call_survives_clear_caches_and_refuses_unknown_workspace():
     from fedbiomed_amd.secagg import SecaggCrypter
 
     dev = D.device()
-    lib = _native.load()
+    lib = test_build
     P, tau, n = 2, 3, 900
     key = W.jl_user_key(0)
     x = torch.from_numpy(W.party_params(0, n)).to(dev)

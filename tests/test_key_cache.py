@@ -17,7 +17,7 @@ ENTRY_WORDS = 8 + 72
 
 def _lib():
     _build.build()
-    return _native.load()
+    return _native.load_test()  # fbm_test_short_* (include/fbm_secagg_test.h)
 
 
 def _consts(lib, N, key):

@@ -256,7 +256,7 @@ def test_library_constants_match_and_drive_the_asm():
     from fedbiomed_amd import _build, _native, workload as W
 
     _build.build()
-    lib = _native.load()
+    lib = _native.load_test()
     for N in (W.BIPRIME0, 0xC9F2B5, (1 << 1023) + 12345677, 3, 5):  # 3, 5 divide R - 1: K = 0
         n32 = np.frombuffer(N.to_bytes(128, "little"), dtype=np.uint32).copy()
         nk = np.zeros(80, np.uint32)
@@ -311,7 +311,7 @@ def test_library_short_path_constants():
     from fedbiomed_amd import _build, _native, workload as W
 
     _build.build()
-    lib = _native.load()
+    lib = _native.load_test()
     rng = random.Random(21)
     cases = [(W.BIPRIME0, W.jl_user_key(0)), (W.BIPRIME0, 1), (W.BIPRIME0, 3), (_rand_n(rng, 1024), rng.getrandbits(2040)),
              (_rand_n(rng, 600), rng.getrandbits(900) | 1), ((1 << 262) + 1, 12345), (W.BIPRIME0, 0),

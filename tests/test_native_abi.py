@@ -1,6 +1,6 @@
-"""CPU-side checks of the drop-in boundary: the C-ABI library builds/loads, exports every
-symbol include/fbm_secagg.h declares, and the host-side parameter logic matches the
-reference's Python formulas.  No GPU compute is called here."""
+"""CPU-side checks of the drop-in boundary: the C-ABI library builds/loads, exports exactly the
+symbols include/fbm_secagg.h declares (the test build: + include/fbm_secagg_test.h), and the
+host-side parameter logic matches the reference's Python formulas.  No GPU compute is called here."""
 
 import ctypes
 import math
@@ -12,11 +12,20 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "fbm_secagg.h")
+TEST_HEADER = os.path.join(ROOT, "include", "fbm_secagg_test.h")
 
 
-def declared_symbols():
-    text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|uint64_t|const char\*)\s+(fbm_\w+)\s*\(", text, re.M)))
+def declared_symbols(header=HEADER):
+    text = open(header).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|uint64_t|const char\*)\s+(fbm_\w+)\s*\(", text, re.M)))
+
+
+def exported(path):
+    """The library's dynamic function exports (nm -D --defined-only, text symbols)."""
+    import subprocess
+
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return sorted({ln.split()[-1] for ln in out.splitlines() if len(ln.split()) == 3 and ln.split()[1] in "TtWi"})
 
 
 @pytest.fixture(scope="module")
@@ -39,7 +48,65 @@ def test_library_exports_every_declared_symbol(lib):
     for s in declared_symbols():
         assert hasattr(lib, s), f"missing export {s}"
         assert s in _native.SIGNATURES, f"no ctypes signature for {s}"
-    assert lib.fbm_abi_version() == _native.ABI_VERSION == 6
+    assert lib.fbm_abi_version() == _native.ABI_VERSION == 7
+    assert set(_native.SIGNATURES) == set(declared_symbols())
+    assert set(_native.TEST_SIGNATURES) == set(declared_symbols(TEST_HEADER))
+
+
+def test_product_library_exports_exactly_its_header(lib):
+    """`nm -D` of the shipped library is the set include/fbm_secagg.h documents -- no
+    test, A/B or profiling hook, no internal C++ symbol; the test build adds exactly
+    include/fbm_secagg_test.h's."""
+    from fedbiomed_amd import _native
+
+    prod, test = exported(_native.LIB_PATH), exported(_native.TEST_LIB_PATH)
+    assert prod == declared_symbols(), set(prod) ^ set(declared_symbols())
+    assert test == sorted(set(declared_symbols()) | set(declared_symbols(TEST_HEADER)))
+    assert not any(n.startswith(("fbm_test_", "fbm_prof_")) for n in prod)
+    assert not {"fbm_jl_set_engine", "fbm_jl_set_short", "fbm_jl_engine_for"} & set(prod)
+    t = _native.load_test()
+    assert t is not lib and t.fbm_abi_version() == lib.fbm_abi_version()
+
+
+def test_test_hooks_route_only_this_thread(lib):
+    """_native.test_hooks() sends the calling thread's load() to the test build and no other thread's."""
+    import threading
+
+    from fedbiomed_amd import _native
+
+    seen = {}
+    with _native.test_hooks():
+        assert _native.load() is _native.load_test()
+        t = threading.Thread(target=lambda: seen.setdefault("other", _native.load()))
+        t.start()
+        t.join()
+    assert seen["other"] is lib and _native.load() is lib
+
+
+def test_engine_policy_is_per_thread():
+    """the test build's engine / short-path switches are the calling thread's (the
+    product library has none); a switch on one thread leaves another thread's policy alone."""
+    import threading
+
+    from fedbiomed_amd import _native
+
+    t = _native.load_test()
+    prev = t.fbm_jl_set_engine(3)
+    try:
+        other = {}
+
+        def probe():
+            other["engine"] = t.fbm_jl_engine_for(10**7)  # auto here: the one-lane engine
+            other["prev_short"] = t.fbm_jl_set_short(0)
+            t.fbm_jl_set_short(other["prev_short"])
+
+        th = threading.Thread(target=probe)
+        th.start()
+        th.join()
+        assert other == {"engine": 1, "prev_short": 1}
+        assert t.fbm_jl_engine_for(10**7) == 3  # this thread's policy stands
+    finally:
+        t.fbm_jl_set_engine(prev)
 
 
 def test_check_stats_lom_guard(lib):
@@ -155,7 +222,7 @@ def test_device_modinv_on_host():
     from fedbiomed_amd import _native as N
     from fedbiomed_amd.workload import BIPRIME0
 
-    lib = N.load()
+    lib = N.load_test()  # fbm_test_modinv (include/fbm_secagg_test.h)
 
     def limbs(v):
         return np.frombuffer(int(v).to_bytes(128, "little"), dtype=np.uint32).copy()
@@ -186,7 +253,7 @@ def test_device_modinv_on_host():
     assert worst <= 99
 
 
-def test_fdh_gcd_on_host(lib):
+def test_fdh_gcd_on_host():
     """The FDH's one-digest coprimality test (Montgomery reduction of N by the odd part of
     the digest, then a binary gcd) against math.gcd, on the host: random digests, digests
     sharing a factor with N, zero, powers of two, and moduli from 3 to 1024 bits."""
@@ -194,6 +261,9 @@ def test_fdh_gcd_on_host(lib):
 
     from fedbiomed_amd import workload as W
 
+    from fedbiomed_amd import _native
+
+    lib = _native.load_test()  # fbm_test_fdh_gcd (include/fbm_secagg_test.h)
     rng = random.Random(11)
     moduli = [W.BIPRIME0, 3, 9, 15, 3 * 5 * 7 * 11 * 13 * 17 * 19 * 23, (1 << 1024) - 1,
               rng.getrandbits(1024) | 1, rng.getrandbits(300) | 1]

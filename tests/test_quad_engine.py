@@ -19,7 +19,7 @@ def test_engine_policy_host():
     from fedbiomed_amd import _build, _native
 
     _build.build()
-    lib = _native.load()
+    lib = _native.load_test()  # the calling thread's engine policy (include/fbm_secagg_test.h)
     prev = lib.fbm_jl_set_engine(1)
     try:
         assert lib.fbm_jl_engine_for(10) == 1
