@@ -10,13 +10,16 @@ per-element vector use -- and `fbm_ass_split_wide` / `fbm_ass_reconstruct_wide`
 the key setup splits (`node/secagg/_secagg_setups.py:248-268`) and the server-key shares the
 researcher sums (`researcher/secagg/_secagg_context.py:380-382`).
 
-The reference draws shares from Python's MT19937 (`random.randint`, `_additive_ss.py:96`).  An int
-secret -- the JL key setup's only use (`node/secagg/_secagg_setups.py:248-249`) -- draws its n-1 shares
-from that same stream, call for call, so a seeded run gives the reference's shares and leaves `random` in
-the reference's state; the last share (secret - sum) is computed on the device.  A vector secret's
-shares come from a counter-based ChaCha20 stream on the device (100M x 16 shares in milliseconds; MT19937
-is sequential).  What both guarantee -- and what the tests pin -- is the contract: the shares sum exactly
-to the secret, the first n-1 lie in [0, 2**bit_length].
+The reference draws shares from Python's MT19937 (`random.randint`, `_additive_ss.py:96`), a predictable
+generator: its output reveals its state.  Here every secret -- an int (the JL key setup's only use,
+`node/secagg/_secagg_setups.py:248-249`: a node's 2040-bit key) or a vector -- draws its shares from a
+counter-based ChaCha20 stream on the device keyed from the OS (`os.urandom`), so a key's shares are not
+predictable PRNG output (100M x 16 shares in milliseconds; MT19937 is sequential).  `reference_rng=True`
+(an extension, for parity runs) draws them from the reference's own stream instead -- the global `random`'s
+MT19937, call for call, so a seeded run gives the reference's shares exactly and leaves `random` in the
+reference's state; the last share (secret - sum) is still computed on the device.  What both guarantee --
+and what the tests pin -- is the contract: the shares sum exactly to the secret, the first n-1 lie in
+[0, 2**bit_length].
 
 `split_tensor` / `reconstruct_tensor` are the device fast path (int64 tensors in HBM).
 """
@@ -62,10 +65,11 @@ class AdditiveSecret:
 
     def split(self, num_shares: int, bit_length: Optional[int] = None,
               reference_rng: bool = False) -> "AdditiveShares":
-        """`reference_rng` (an extension): a vector secret's shares drawn from the reference's own stream
-        (the global `random`'s MT19937, element by element, D.reference_share_draws) instead of the
-        device's ChaCha20 -- seeded, the reference's shares exactly; the last share is still computed on
-        the device.  An int secret always draws from that stream."""
+        """`reference_rng` (an extension, for parity runs): the shares drawn from the reference's own
+        stream (the global `random`'s MT19937: `random.randint` for an int secret, element by element
+        through D.reference_share_draws for a vector) instead of the device's OS-keyed ChaCha20 --
+        seeded, the reference's shares exactly; the last share is still computed on the device.  Off
+        (the default), no share comes from `random`: a node's key shares are not predictable."""
         if num_shares <= 0:
             raise FedbiomedValueError("Number of shares must be greater than 0")
         values = [self._secret] if isinstance(self._secret, int) else list(self._secret)
@@ -75,7 +79,7 @@ class AdditiveSecret:
                     raise FedbiomedValueError("Bit length must be greater or equal than the secret's bit length")
         if not values:
             return AdditiveShares([AdditiveShare([]) for _ in range(num_shares)])
-        if isinstance(self._secret, int):  # the reference's own draws (_additive_ss.py:94-98), then secret - sum
+        if isinstance(self._secret, int) and reference_rng:  # the reference's own draws (:94-98), then secret - sum
             bl = self._secret.bit_length() if bit_length is None else bit_length
             draws = [random.randint(0, 2**bl) for _ in range(num_shares - 1)]
             last = _reconstruct([[self._secret]] + [[-d] for d in draws])[0]

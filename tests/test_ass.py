@@ -54,10 +54,10 @@ def dev():
 
 @pytest.mark.gpu
 def test_int_split_is_the_reference_stream(golden, dev):
-    """An int secret (the key setup's use) draws its shares from Python's MT19937 call for call: seeded as
-    tools/gen_golden.py seeded the reference, the shares are the reference's own (the 64- and 2040-bit
-    cases of tests/golden/ass.json), and `random` is left where the reference leaves it; a vector secret
-    does with reference_rng=True (the fixture's list case)."""
+    """With reference_rng=True an int secret (the key setup's use) draws its shares from Python's MT19937
+    call for call: seeded as tools/gen_golden.py seeded the reference, the shares are the reference's own
+    (the 64- and 2040-bit cases of tests/golden/ass.json), and `random` is left where the reference leaves
+    it; a vector secret does too (the fixture's list case)."""
     import random
 
     from fedbiomed_amd.secagg import AdditiveSecret
@@ -67,7 +67,7 @@ def test_int_split_is_the_reference_stream(golden, dev):
     for case in cases:
         secret, n = I(case["secret"]), len(case["shares"])
         random.seed(99)
-        assert AdditiveSecret(secret).split(n).to_list() == [I(s) for s in case["shares"]]
+        assert AdditiveSecret(secret).split(n, reference_rng=True).to_list() == [I(s) for s in case["shares"]]
         after = random.getstate()
         random.seed(99)
         for _ in range(n - 1):
@@ -85,6 +85,32 @@ def test_int_split_is_the_reference_stream(golden, dev):
                                             for v, x in zip(s, vals))
     assert AdditiveSecret([5, 6]).split(3, bit_length=70, reference_rng=True).reconstruct() == [5, 6]
     random.seed(7)
+    assert AdditiveSecret(-12345).split(1, reference_rng=True).to_list() == [-12345]
+    assert AdditiveSecret(2**70).split(3, bit_length=100, reference_rng=True).reconstruct() == 2**70
+
+
+@pytest.mark.gpu
+def test_int_split_default_is_not_the_mt19937_stream(golden, dev):
+    """by default an int secret -- a node's 2040-bit JL key at setup -- draws its shares
+    from the device's OS-keyed ChaCha20, never from `random`: the global stream is left untouched, two
+    splits of the same secret under the same seed differ, and the contract holds (exact sum, the first
+    n - 1 shares in [0, 2**bit_length])."""
+    import random
+
+    from fedbiomed_amd.secagg import AdditiveSecret
+
+    for case in [c for c in golden["ass"]["cases"] if not isinstance(c["secret"], list)]:
+        secret, n = I(case["secret"]), len(case["shares"])
+        random.seed(99)
+        before = random.getstate()
+        a = AdditiveSecret(secret).split(n).to_list()
+        assert random.getstate() == before  # no draw from the reference's MT19937
+        assert a != [I(s) for s in case["shares"]]
+        random.seed(99)
+        b = AdditiveSecret(secret).split(n).to_list()
+        assert a != b
+        for sh in (a, b):
+            assert sum(sh) == secret and all(0 <= v <= 2**secret.bit_length() for v in sh[:-1])
     assert AdditiveSecret(-12345).split(1).to_list() == [-12345]
     assert AdditiveSecret(2**70).split(3, bit_length=100).reconstruct() == 2**70
 

@@ -240,7 +240,8 @@ def test_cfg5_lom_ass_100m_16_parties(dev):
     cuts = [Dd.lom_shard(n, world, r)[0] for r in range(1, world)]
     assert all(c % 8 == 0 for c in cuts)
     m = 512  # a window of m elements on each side of every cut point, and at both ends
-    wins = [(0, m)] + [(c - m, 2 * m) for c in cuts] + [(n - m - 3, m + 3)]
+    e0 = (n - m - 3) // 8 * 8  # (the window oracle starts on a ChaCha20 block: 8-aligned offsets)
+    wins = [(0, m)] + [(c - m, 2 * m) for c in cuts] + [(e0, n - e0)]
     for p, u in enumerate(ids):
         gen.manual_seed(500 + p)
         x = torch.randn(n, generator=gen, device=dev, dtype=torch.float32) * 0.05
