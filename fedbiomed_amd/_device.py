@@ -17,6 +17,7 @@ import logging
 import math
 import operator
 import os
+import sys
 import threading
 from typing import List, Optional, Sequence, Tuple
 
@@ -526,12 +527,39 @@ def f64_into_list(lst: list, off: int, values: np.ndarray) -> None:
     _pyconv().f64_into_list(lst, off, np.ascontiguousarray(values, dtype=np.float64))
 
 
-def int_pool(n: int, nbytes: int = 256) -> Optional[list]:
+def inplace_allowed(version=None) -> bool:
+    """Writes into output objects made ahead -- an int_pool int's digits, a float_pool float's value,
+    written by csrc/fbm_pyconv.c before the list is handed out -- only on CPython 3.10 / 3.11, the
+    object layouts the module is written and tested against (the C module compiles them out on any
+    other version; this refuses them besides, whatever the build)."""
+    import platform
+
+    v = sys.version_info if version is None else version
+    return tuple(v[:2]) in ((3, 10), (3, 11)) and platform.python_implementation() == "CPython"
+
+
+# The unprepared list calls' in-place writes (the encrypt's int_pool, the aggregate's last-stripe floats
+# made while the GPU exponentiates).  Off: the unprepared calls make every output object with its value;
+# the prepare_* extensions keep theirs (their objects are made outside the call).  DESIGN.md section 7
+# has the measurement behind the default (tools/inplace_probe.py).
+INPLACE_UNPREPARED = False
+
+
+def inplace(prepared: bool) -> bool:
+    """Whether a call may write into output objects made ahead: an interpreter the C module's writes are
+    for, a module built with them, and -- for an unprepared call -- INPLACE_UNPREPARED."""
+    m = _pyconv()
+    if m is _PyConvFallback or not inplace_allowed() or not m.build_flags()[0]:
+        return False
+    return prepared or INPLACE_UNPREPARED
+
+
+def int_pool(n: int, nbytes: int = 256, prepared: bool = True) -> Optional[list]:
     """n ints with room for nbytes-byte values made ahead (a prepared encrypt's output list: JL
     ciphertexts, 256 bytes, through limbs_into_pool; LOM's masked values, 8 bytes, through
-    u64_into_pool), or None where the C module cannot make them (not built, or CPython >= 3.12)."""
-    m = _pyconv()
-    return None if m is _PyConvFallback else m.int_pool(n, nbytes)
+    u64_into_pool), or None where they may not be made (inplace(prepared): the module not built, an
+    interpreter other than CPython 3.10 / 3.11, an unprepared call with INPLACE_UNPREPARED off)."""
+    return _pyconv().int_pool(n, nbytes) if inplace(prepared) else None
 
 
 def u64_into_pool(pool: list, arr: np.ndarray) -> list:
@@ -634,16 +662,35 @@ def lom_protect(x: torch.Tensor, secrets: Sequence[bytes], signs: Sequence[int],
 # (fbm_lom_protect_host / fbm_lom_aggregate_host): a 1 000-element call is launch-bound.
 LOM_HOST_CALL_MAX = 1 << 16
 
-_host_ws_tls = threading.local()
+_host_ws = {}  # thread ident -> that thread's device workspace of the synchronous host-buffer calls
+_host_ws_lock = threading.Lock()
 
 
 def _host_workspace(nbytes: int, dev) -> torch.Tensor:
     """This thread's device workspace for the synchronous host-buffer calls (one call at a time per
-    thread; grown, never shrunk)."""
-    ws = getattr(_host_ws_tls, "ws", None)
-    if ws is None or ws.numel() < nbytes or ws.device != dev:
-        ws = _host_ws_tls.ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)
+    thread; grown, never shrunk).  It holds a call's plaintext parameters and masked vector only until
+    _scrub_host_workspace zeroes it behind the call; release_host_workspaces drops every thread's."""
+    key = threading.get_ident()
+    with _host_ws_lock:
+        ws = _host_ws.get(key)
+        if ws is None or ws.numel() < nbytes or ws.device != dev:
+            ws = _host_ws[key] = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)
     return ws
+
+
+def _scrub_host_workspace(ws: torch.Tensor, nbytes: int) -> None:
+    """Zeroes the bytes a synchronous host-buffer call used (no node's parameters or masked
+    vector left in HBM after its call), queued on the call's stream behind it: the call returns without
+    waiting for it."""
+    ws[:nbytes].zero_()
+
+
+def release_host_workspaces() -> None:
+    """Zeroes and drops every thread's host-call workspace (the clear-caches path)."""
+    with _host_ws_lock:
+        for ws in _host_ws.values():
+            ws.zero_()
+        _host_ws.clear()
 
 
 def lom_protect_host(x: np.ndarray, secrets: Sequence[bytes], signs: Sequence[int], nonce: bytes, tau: int,
@@ -666,9 +713,13 @@ def lom_protect_host(x: np.ndarray, secrets: Sequence[bytes], signs: Sequence[in
     tau &= U64_MAX
     blk = host_empty(n + N.STATS_WORDS // 2, torch.int64).numpy()  # pinned: output then status words
     y, st = blk[:n].view(np.uint64), blk[n:].view(np.uint32)
-    ws = _host_workspace(int(lib.fbm_lom_host_workspace(n, 1)), dev)
-    _call(lib.fbm_lom_protect_host, _np_ptr(x), N.FBM_F64, n, c, c2, tf, tm1, int(weight), _np_ptr(sec),
-          _np_ptr(sg), len(secrets), 0, _np_ptr(nb), int(tau), 0, _np_ptr(y), _np_ptr(st), _ptr(ws), _stream())
+    wsb = int(lib.fbm_lom_host_workspace(n, 1))
+    ws = _host_workspace(wsb, dev)
+    try:
+        _call(lib.fbm_lom_protect_host, _np_ptr(x), N.FBM_F64, n, c, c2, tf, tm1, int(weight), _np_ptr(sec),
+              _np_ptr(sg), len(secrets), 0, _np_ptr(nb), int(tau), 0, _np_ptr(y), _np_ptr(st), _ptr(ws), _stream())
+    finally:
+        _scrub_host_workspace(ws, wsb)
     _check_stats_host(st, n_nodes)
     if post is not None:
         raise post
@@ -690,9 +741,13 @@ def lom_aggregate_host(Y: np.ndarray, total_weight: int, clip=None, target=None)
     P, n = Y.shape
     blk = host_empty(n + N.STATS_WORDS // 2, torch.int64).numpy()  # pinned: averages then status words
     out, st = blk[:n].view(np.float64), blk[n:].view(np.uint32)
-    ws = _host_workspace(int(lib.fbm_lom_host_workspace(n, P)), dev)
-    _call(lib.fbm_lom_aggregate_host, _np_ptr(Y), P, n, int(total_weight), negc, step, _np_ptr(out), _np_ptr(st),
-          _ptr(ws), _stream())
+    wsb = int(lib.fbm_lom_host_workspace(n, P))
+    ws = _host_workspace(wsb, dev)
+    try:
+        _call(lib.fbm_lom_aggregate_host, _np_ptr(Y), P, n, int(total_weight), negc, step, _np_ptr(out),
+              _np_ptr(st), _ptr(ws), _stream())
+    finally:
+        _scrub_host_workspace(ws, wsb)
     _check_stats_host(st)
     return out
 
@@ -815,13 +870,24 @@ class jl_short:
         return self._hooks.__exit__(*exc)
 
 
+_clear_hooks = []  # callables run by jl_clear_caches (SecaggCrypter.drop_prepared registers itself)
+
+
 def jl_clear_caches() -> None:
-    """Drops the library's host-side caches (fbm_jl_clear_caches): the short path's constant C per
-    (N, |key|) -- held under a SHA-256 digest of (N, |key|), never the key, and zeroed -- and the
-    per-biprime public parameters.  The reference keeps nothing between calls (a fresh
-    SecaggCrypter per call, fedbiomed/node/secagg/_secagg_round.py:142); call this after a round to
-    do the same (the next call rebuilds C: a few ms of host arithmetic)."""
+    """Drops what the process keeps between calls: the library's host-side caches
+    (fbm_jl_clear_caches: the short path's constant C per (N, |key|) -- held under a SHA-256 digest
+    of (N, |key|), never the key, and zeroed -- and the per-biprime public parameters), the
+    synchronous host calls' device workspaces (zeroed), and any prepared factor of prepare_encrypt /
+    prepare_aggregate (zeroed: with a node's ciphertext, its H(t_k)^key decrypts that node's update).
+    The reference keeps nothing between calls (a fresh SecaggCrypter per call,
+    fedbiomed/node/secagg/_secagg_round.py:142); call this after a round to do the same (the next call
+    rebuilds C: a few ms of host arithmetic)."""
     N.load().fbm_jl_clear_caches()
+    if N.TEST_LIB_PATH in N._libs:  # the test build keeps its own caches
+        N._libs[N.TEST_LIB_PATH].fbm_jl_clear_caches()
+    release_host_workspaces()
+    for hook in list(_clear_hooks):
+        hook()
 
 
 def one_lane_round(dev=None) -> int:

@@ -40,14 +40,23 @@
 #include <string.h>
 
 /* The digit-level fast paths read CPython's PyLongObject layout (ob_digit, Py_SIZE as the
- * signed digit count), which holds up to 3.11; 3.12 changed it (long_value.ob_digit, lv_tag).
- * From 3.12 on the conversions go through the byte-array API instead, on one thread. */
+ * signed digit count), which is the layout of 3.10 and 3.11 (the versions this module is built and
+ * tested on); 3.12 changed it (long_value.ob_digit, lv_tag).  On any other version the conversions
+ * go through the byte-array API instead, on one thread. */
 #ifndef FBM_DIGITS_FAST /* -DFBM_DIGITS_FAST=0 builds the portable path on any version (tested) */
-#if PY_VERSION_HEX < 0x030C0000
+#if PY_VERSION_HEX >= 0x030A0000 && PY_VERSION_HEX < 0x030C0000
 #define FBM_DIGITS_FAST 1
 #else
 #define FBM_DIGITS_FAST 0
 #endif
+#endif
+
+/* In-place writes into objects the module made and nothing else holds yet -- a float_pool float's
+ * ob_fval, an int_pool int's digits -- only on 3.10 / 3.11 (or -DFBM_INPLACE=0: never, tested).  Off, a
+ * pool float is replaced by a new float (its release frees it before the list is returned) and there
+ * are no int pools: every output object is made with its value. */
+#ifndef FBM_INPLACE
+#define FBM_INPLACE FBM_DIGITS_FAST
 #endif
 
 #if FBM_DIGITS_FAST
@@ -472,14 +481,15 @@ static int check_slots(PyObject* const* items, Py_ssize_t k) {
 static int fill_slots(PyObject** items, const double* src, Py_ssize_t k) {
     for (Py_ssize_t i = 0; i < k; ++i) {
         PyObject* o = items[i];
-        if (o != Py_None && Py_REFCNT(o) == 1) {
+        if (FBM_INPLACE && o != Py_None && Py_REFCNT(o) == 1) {
             ((PyFloatObject*)o)->ob_fval = src[i];
             continue;
         }
         PyObject* v = PyFloat_FromDouble(src[i]);
         if (!v) return -1;
         items[i] = v;
-        Py_DECREF(o); /* None, or a float with another holder: never freed here */
+        Py_DECREF(o); /* None, a float with another holder, or (FBM_INPLACE off) a pool float: a float's
+                         deallocation runs no Python code */
     }
     return 0;
 }
@@ -810,7 +820,7 @@ static PyObject* int_pool(PyObject* self, PyObject* args) {
         PyErr_SetString(PyExc_ValueError, "int_pool takes n >= 0 and a positive width in whole 32-bit words");
         return NULL;
     }
-#if FBM_DIGITS_FAST
+#if FBM_DIGITS_FAST && FBM_INPLACE
     const Py_ssize_t nd = (8 * nb + PyLong_SHIFT - 1) / PyLong_SHIFT;
     PyObject* lst = PyList_New(n);
     if (!lst) return NULL;
@@ -830,7 +840,7 @@ static PyObject* int_pool(PyObject* self, PyObject* args) {
 #endif
 }
 
-#if FBM_DIGITS_FAST
+#if FBM_DIGITS_FAST && FBM_INPLACE
 typedef struct {
     PyObject** items;
     const unsigned char* src;
@@ -864,7 +874,7 @@ static PyObject* words_into_pool(PyObject* self, PyObject* args) {
     Py_buffer view;
     Py_ssize_t nb, off = 0;
     if (!PyArg_ParseTuple(args, "O!y*n|n", &PyList_Type, &lst, &view, &nb, &off)) return NULL;
-#if FBM_DIGITS_FAST
+#if FBM_DIGITS_FAST && FBM_INPLACE
     const Py_ssize_t n = nb > 0 ? view.len / nb : 0;
     if (nb <= 0 || nb % 4 || view.len % nb || ((uintptr_t)view.buf & 3) || off < 0 ||
         off + n > PyList_GET_SIZE(lst)) {
@@ -900,7 +910,7 @@ static PyObject* words_into_pool(PyObject* self, PyObject* args) {
 #else
     (void)lst, (void)nb, (void)off;
     PyBuffer_Release(&view);
-    PyErr_SetString(PyExc_ValueError, "no int pools in this build (FBM_DIGITS_FAST=0)");
+    PyErr_SetString(PyExc_ValueError, "no int pools in this build (CPython other than 3.10 / 3.11, or FBM_INPLACE=0)");
     return NULL;
 #endif
 }
@@ -934,7 +944,7 @@ static void* slot_fill_range(void* arg) {
     j->rest = 0;
     for (Py_ssize_t i = j->lo; i < j->hi; ++i) {
         PyObject* o = j->items[i];
-        if (o != Py_None && Py_REFCNT(o) == 1)
+        if (FBM_INPLACE && o != Py_None && Py_REFCNT(o) == 1)
             ((PyFloatObject*)o)->ob_fval = j->src[i];
         else
             ++j->rest;
@@ -996,7 +1006,15 @@ static PyObject* f64_into_list(PyObject* self, PyObject* args) {
     Py_RETURN_NONE;
 }
 
+/* Whether this build writes into objects it made ahead (FBM_INPLACE) and reads / builds ints digit by digit
+ * (FBM_DIGITS_FAST): (inplace, digits). */
+static PyObject* build_flags(PyObject* self, PyObject* args) {
+    (void)self, (void)args;
+    return Py_BuildValue("(ii)", FBM_INPLACE ? 1 : 0, FBM_DIGITS_FAST ? 1 : 0);
+}
+
 static PyMethodDef methods[] = {
+    {"build_flags", build_flags, METH_NOARGS, "-> (in-place writes into pool objects, digit-level int paths)"},
     {"all_ints", all_ints, METH_VARARGS, "list -> all items are ints (isinstance)"},
     {"mt_share_draws", mt_share_draws, METH_VARARGS,
      "MT19937 state (625-tuple), uint32 bit lengths [n], draws, int64 out [draws, n, 2] -> the state after: "

@@ -86,6 +86,25 @@ def _prep_tag(current_round, num_nodes, key, biprime, target_range) -> Optional[
     return h.digest()
 
 
+def _scrub_prep(prep, keys) -> None:
+    """Zeroes a dropped preparation's factor tensors in HBM, on the current stream once their
+    exponentiations (on the preparation's side stream) are done; the memory then returns to torch's
+    caching allocator only after the zeroing."""
+    if not prep:
+        return
+    ev = prep.get("event")
+    for k in keys:
+        v = prep.get(k)
+        for t in (v if isinstance(v, list) else [v]):
+            if t is None:
+                continue
+            st = torch.cuda.current_stream(t.device)
+            if ev is not None:
+                st.wait_event(ev)
+            t.record_stream(st)
+            t.zero_()
+
+
 class SecaggCrypter:
     """Joye-Libert secure aggregation (encrypt on nodes, aggregate on the researcher)."""
 
@@ -166,7 +185,15 @@ class SecaggCrypter:
     def encrypt(self, num_nodes: int, current_round: int, params: List[float], key: int, biprime: int,
                 clipping_range: Union[int, None] = None, weight: Optional[int] = None,
                 target_range: Optional[int] = None) -> List[int]:
-        """Encrypts model parameters (reference `_secagg_crypter.py:45-137`)."""
+        """Encrypts model parameters (reference `_secagg_crypter.py:45-137`).  If it raises, a
+        prepare_encrypt preparation is dropped (drop_prepared)."""
+        try:
+            return self._encrypt(num_nodes, current_round, params, key, biprime, clipping_range, weight, target_range)
+        except BaseException:
+            SecaggCrypter.drop_prepared()
+            raise
+
+    def _encrypt(self, num_nodes, current_round, params, key, biprime, clipping_range, weight, target_range):
         start = time.process_time()
         host = _check_float_list(params)
         if not isinstance(key, int):
@@ -198,7 +225,7 @@ class SecaggCrypter:
                 with D.deferred_checks():  # (checked at the exit, once the ciphertexts are back)
                     ct = self.encrypt_tensor(num_nodes, current_round, x, key, biprime, clipping_range, weight,
                                              target_range)
-                    pool = D.int_pool(n_ct)  # the output's ints, made while the GPU exponentiates
+                    pool = D.int_pool(n_ct, prepared=False)  # the output's ints, made while the GPU exponentiates
                     packed = D.to_host(ct).numpy().view(np.uint32)
                 out = D.limbs_into_pool(pool, packed, strict=True) if pool is not None else D.limbs_to_ints(packed)
             else:
@@ -233,7 +260,7 @@ class SecaggCrypter:
                 ev = torch.cuda.Event()
                 ev.record(main)
                 done.append(ev)
-            pool = D.int_pool(stripes[-1][1])  # the output's ints, made while the GPU exponentiates stripe 0
+            pool = D.int_pool(stripes[-1][1], prepared=False)  # made while the GPU exponentiates stripe 0
             out = pool if pool is not None else []
             for (c0, c1), ev in zip(stripes, done):
                 ev.synchronize()
@@ -259,7 +286,7 @@ class SecaggCrypter:
         library older than ABI 5.  The
         key itself is not kept, only a SHA-256 tag of it.  The preparation is the class's, not this
         instance's (one at a time): the node's encrypt runs on a fresh SecaggCrypter."""
-        SecaggCrypter._enc_prep = None
+        SecaggCrypter.drop_prepared()
         try:
             if not all(isinstance(v, int) for v in (current_round, num_nodes, key, biprime, num_params)):
                 return False
@@ -293,6 +320,22 @@ class SecaggCrypter:
                                    "checks": checks.pending}
         return True
 
+    @staticmethod
+    def drop_prepared() -> None:
+        """Extension: drops prepare_encrypt's preparation (the class's: the node's H(t_k)^key factor and
+        its int pool), its factor zeroed in HBM first -- with the ciphertext the node sends, that factor
+        decrypts the node's individual update (c / F = 1 + N x).  The encrypt that takes it spends it, a
+        call of another round drops it, an encrypt that raises drops it, and so does
+        _device.jl_clear_caches (the clear-caches path).  A researcher's prepare_aggregate preparation is
+        its instance's (drop it with `crypter.drop_prepared_aggregate()`)."""
+        prep, SecaggCrypter._enc_prep = SecaggCrypter._enc_prep, None
+        _scrub_prep(prep, ("factor",))
+
+    def drop_prepared_aggregate(self) -> None:
+        """Extension: drops this instance's prepare_aggregate preparation, its factors zeroed first."""
+        prep, self._prepared = getattr(self, "_prepared", None), None
+        _scrub_prep(prep, ("factors",))
+
     def _take_prepared_encrypt(self, current_round, num_nodes, key, biprime, target_range, n_ct, dev):
         """(prepare_encrypt's factor, its int pool or None) when they are this call's (the factor waited for
         on the current stream, its status words adopted; the preparation is then spent), else None.  A call
@@ -301,7 +344,7 @@ class SecaggCrypter:
         if prep is None:
             return None
         if prep["round"] != current_round:
-            SecaggCrypter._enc_prep = None
+            SecaggCrypter.drop_prepared()
             return None
         tag = _prep_tag(current_round, num_nodes, key, biprime, target_range)
         if prep["n_ct"] != n_ct or tag is None or prep["tag"] != tag:
@@ -328,7 +371,7 @@ class SecaggCrypter:
         takes 45 ms instead of 158 (`profiles/r5x_bench.json`).
         Best effort: False (nothing prepared) where aggregate would refuse the arguments.  The key
         itself is not kept, only a SHA-256 tag of it."""
-        self._prepared = None
+        self.drop_prepared_aggregate()
         try:
             if not all(isinstance(v, int) for v in (current_round, num_nodes, key, biprime, num_expected_params)):
                 return False
@@ -373,7 +416,7 @@ class SecaggCrypter:
         if prep is None:
             return None
         if prep["round"] != current_round:
-            self._prepared = None
+            self.drop_prepared_aggregate()
             return None
         tag = _prep_tag(current_round, num_nodes, key, biprime, target_range)
         if prep["n_ct"] != n_ct or tag is None or prep["tag"] != tag:
@@ -512,7 +555,8 @@ class SecaggCrypter:
             res = pool
         else:  # the last stripe's float objects made now (its values land last); the others' as they land
             res = D.none_list(sum(n_outs))
-            D.f64_into_list(res, offs[-1], np.zeros(n_outs[-1]))
+            if D.inplace(prepared=False):
+                D.f64_into_list(res, offs[-1], np.zeros(n_outs[-1]))
         for k, (out_h, ev) in enumerate(pend):
             ev.synchronize()
             D.f64_into_list(res, offs[k], out_h.numpy())
@@ -711,3 +755,6 @@ class SecaggLomCrypter(SecaggCrypter):
             res = res_h.tolist()
         logger.debug(f"Aggregation is completed in {round(time.process_time() - start, ndigits=2)} seconds.")
         return res
+
+
+D._clear_hooks.append(SecaggCrypter.drop_prepared)  # _device.jl_clear_caches drops the node's prepared factor

@@ -432,3 +432,58 @@ def test_reference_share_draws_are_python_random():
     ref = [[R.randint(0, 2**127) for _ in range(2)], [R.randint(0, 2**3) for _ in range(2)]]
     assert a == [[ref[0][j], ref[1][j]] for j in range(2)]
     assert D.reference_share_draws([], 3) == [[], [], []] and D.reference_share_draws([4], 0) == []
+
+
+def _build_pyconv(tmp_path, *defines):
+    import importlib.util
+    import shutil
+    import subprocess
+    import sysconfig
+
+    from fedbiomed_amd import _build
+
+    if not shutil.which("gcc"):
+        pytest.skip("no gcc")
+    out = tmp_path / ("_fbm_pyconv" + sysconfig.get_config_var("EXT_SUFFIX"))
+    subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-Wall", "-Werror", "-pthread", *defines,
+                    "-I" + sysconfig.get_paths()["include"], _build.PYCONV_SRC, "-o", str(out)], check=True)
+    spec = importlib.util.spec_from_file_location("_fbm_pyconv", str(out))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_inplace_writes_only_on_cpython_310_311(tmp_path, monkeypatch):
+    """writes into objects made ahead (an int_pool int's digits, a float_pool float's value)
+    happen only on CPython 3.10 / 3.11.  The Python gate refuses every other version whatever the build; a
+    build without them (-DFBM_INPLACE=0, what another interpreter compiles) makes no int pools, and its
+    f64_into_list replaces a pool's floats by new ones instead of writing them; the unprepared list calls
+    take none of it unless INPLACE_UNPREPARED."""
+    import sys as _sys
+
+    assert D.inplace_allowed((3, 10, 12)) and D.inplace_allowed((3, 11, 0))
+    for v in ((3, 9, 18), (3, 12, 0), (3, 13, 1), (4, 0, 0)):
+        assert not D.inplace_allowed(v), v
+    assert D.inplace_allowed() == (_sys.version_info[:2] in ((3, 10), (3, 11)))
+    m = D._pyconv()
+    if m is not D._PyConvFallback:
+        assert tuple(m.build_flags()) == ((1, 1) if D.inplace_allowed() else (0, 0))
+    # an interpreter outside the gate: no pools, whatever the module
+    monkeypatch.setattr(D, "inplace_allowed", lambda version=None: False)
+    assert D.int_pool(4) is None and D.int_pool(4, 8, prepared=True) is None and not D.inplace(True)
+    monkeypatch.undo()
+    assert D.int_pool(4, prepared=False) is None  # unprepared calls: INPLACE_UNPREPARED off (the default)
+    # the build without in-place writes
+    mod = _build_pyconv(tmp_path, "-DFBM_INPLACE=0")
+    assert tuple(mod.build_flags()) == (0, 1 if D.inplace_allowed() else 0)
+    assert mod.int_pool(4, 256) is None
+    with pytest.raises(ValueError):
+        mod.words_into_pool([0], bytes(256), 256)
+    for n in (5, 100_000):  # one thread, and the threaded check / fill passes
+        pool = mod.float_pool(n)
+        ids = [id(v) for v in pool[:5]]
+        keep = pool[3]  # a float held elsewhere too: never written, replaced
+        vals = np.arange(n, dtype=np.float64) * 0.5
+        mod.f64_into_list(pool, 0, vals)
+        assert pool == vals.tolist() and keep == 0.0
+        assert all(id(v) != i for v, i in zip(pool[:5], ids) if v != 0.0)  # new objects, not overwritten

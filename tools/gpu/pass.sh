@@ -14,6 +14,7 @@
 #   dist8      bench.py --gpus 8 through spawn_ranks: 8 gloo ranks sharing this GPU, 2M elements
 #   dist8full  the same at the metric's 10M elements
 #   TEST=path  one test file / node id (e.g. TEST=tests/test_configs.py)
+#   RUN=tools/x.py[,args]  a probe script (args comma-separated)         -> x.jsonl
 # Summaries: python tools/prof_summary.py gpurun_out/TAG/jl profiles/TAG_jl (and .../lom).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -42,6 +43,12 @@ run_step() {
     local t=${s#TEST=}; local f=$O/pytest_$(basename ${t%%::*} .py).txt
     timeout -k 10 900 $PY -m pytest $t -m gpu -x -v --timeout 600 --timeout-method thread > $f 2>&1
     local rc=$?; tail -3 $f; return $rc ;;
+  RUN=*)
+    local spec=${s#RUN=}; local script=${spec%%,*}; local a=""
+    [ "$spec" != "$script" ] && a=$(echo ${spec#*,} | tr ',' ' ')
+    local f=$O/$(basename $script .py).jsonl
+    timeout -k 10 900 $PY $script $a > $f 2> ${f%.jsonl}.err
+    local rc=$?; tail -c 1500 $f; return $rc ;;
   smoke)
     timeout -k 10 300 $PY -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1
     local rc=$?; tail -1 $O/smoke.txt; return $rc ;;
