@@ -12,7 +12,8 @@
 #   jlpmc      its FETCH_SIZE / WRITE_SIZE passes (separate runs)                 -> jl/pmc_*
 #   lompmc     kernel trace + FETCH_SIZE / WRITE_SIZE of the LOM bench (10M x 8)  -> lom/...
 #   dist8      bench.py --gpus 8 through spawn_ranks: 8 gloo ranks sharing this GPU, 2M elements
-#   dist8full  the same at the metric's 10M elements
+#   dist8full  the same at the metric's 10M elements and the driver's --steps 20 --warmup 5 (all 8 ranks'
+#              work on one GPU: an upper bound on the driver's 8-GPU wall time)
 #   TEST=path  one test file / node id (e.g. TEST=tests/test_configs.py)
 #   RUN=tools/x.py[,args]  a probe script (args comma-separated)         -> x.jsonl
 # Summaries: python tools/prof_summary.py gpurun_out/TAG/jl profiles/TAG_jl (and .../lom).
@@ -77,10 +78,10 @@ run_step() {
         python3 $R/bench.py $LOMARGS > /dev/null 2> $O/lom/pmc_write.err)
     local rc=$?; tail -c 800 $O/lom/prof_bench.json; echo; return $rc ;;
   dist8|dist8full)
-    local n=2000000; [ $s = dist8full ] && n=10000000
+    local a="--elements 2000000 --steps 2 --warmup 1"
+    [ $s = dist8full ] && a="--elements 10000000 --steps 20 --warmup 5"
     local t0=$(date +%s)
-    timeout -k 10 900 $PY bench.py --gpus 8 --dist-backend gloo --elements $n --steps 2 --warmup 1 \
-      > $O/$s.json 2> $O/$s.err
+    timeout -k 10 900 $PY bench.py --gpus 8 --dist-backend gloo $a > $O/$s.json 2> $O/$s.err
     local rc=$?
     echo "{\"step\": \"$s\", \"rc\": $rc, \"wall_s\": $(( $(date +%s) - t0 )), \"lines\": $(wc -l < $O/$s.json)}" \
       > $O/$s.meta.json
