@@ -674,7 +674,7 @@ def _host_workspace(nbytes: int, dev) -> torch.Tensor:
     with _host_ws_lock:
         ws = _host_ws.get(key)
         if ws is None or ws.numel() < nbytes or ws.device != dev:
-            ws = _host_ws[key] = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)
+            ws = _host_ws[key] = torch.zeros(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)
     return ws
 
 
