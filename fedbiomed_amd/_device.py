@@ -538,27 +538,29 @@ def inplace_allowed(version=None) -> bool:
     return tuple(v[:2]) in ((3, 10), (3, 11)) and platform.python_implementation() == "CPython"
 
 
-# The unprepared list calls' in-place writes (the encrypt's int_pool, the aggregate's last-stripe floats
-# made while the GPU exponentiates).  Off: the unprepared calls make every output object with its value;
-# the prepare_* extensions keep theirs (their objects are made outside the call).  DESIGN.md section 7
-# has the measurement behind the default (tools/inplace_probe.py).
-INPLACE_UNPREPARED = False
+# The unprepared list calls' in-place writes, per call (kept only where they gain >= 10 %).
+# Measured at 10M on MI355X (tools/inplace_probe.py, profiles/r6b_inplace_probe.jsonl, interleaved medians of
+# 5): the node's JL encrypt 138.4 ms with its int_pool against 143.0 without (3.3 %: off), the researcher's
+# aggregate 140.1 ms with its last stripe's floats made while the GPU exponentiates against 157.9 without
+# (11.3 %: on).  Off, the call makes every output object with its value; the prepare_* extensions keep
+# their pools (their objects are made outside the call).
+INPLACE_UNPREPARED = {"encrypt": False, "aggregate": True}
 
 
-def inplace(prepared: bool) -> bool:
+def inplace(prepared: bool, call: str = "encrypt") -> bool:
     """Whether a call may write into output objects made ahead: an interpreter the C module's writes are
-    for, a module built with them, and -- for an unprepared call -- INPLACE_UNPREPARED."""
+    for, a module built with them, and -- for an unprepared call -- INPLACE_UNPREPARED[call]."""
     m = _pyconv()
     if m is _PyConvFallback or not inplace_allowed() or not m.build_flags()[0]:
         return False
-    return prepared or INPLACE_UNPREPARED
+    return prepared or bool(INPLACE_UNPREPARED.get(call))
 
 
 def int_pool(n: int, nbytes: int = 256, prepared: bool = True) -> Optional[list]:
     """n ints with room for nbytes-byte values made ahead (a prepared encrypt's output list: JL
     ciphertexts, 256 bytes, through limbs_into_pool; LOM's masked values, 8 bytes, through
     u64_into_pool), or None where they may not be made (inplace(prepared): the module not built, an
-    interpreter other than CPython 3.10 / 3.11, an unprepared call with INPLACE_UNPREPARED off)."""
+    interpreter other than CPython 3.10 / 3.11, an unprepared encrypt with INPLACE_UNPREPARED off)."""
     return _pyconv().int_pool(n, nbytes) if inplace(prepared) else None
 
 

@@ -555,7 +555,7 @@ class SecaggCrypter:
             res = pool
         else:  # the last stripe's float objects made now (its values land last); the others' as they land
             res = D.none_list(sum(n_outs))
-            if D.inplace(prepared=False):
+            if D.inplace(prepared=False, call="aggregate"):
                 D.f64_into_list(res, offs[-1], np.zeros(n_outs[-1]))
         for k, (out_h, ev) in enumerate(pend):
             ev.synchronize()

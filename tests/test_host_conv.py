@@ -472,7 +472,8 @@ def test_inplace_writes_only_on_cpython_310_311(tmp_path, monkeypatch):
     monkeypatch.setattr(D, "inplace_allowed", lambda version=None: False)
     assert D.int_pool(4) is None and D.int_pool(4, 8, prepared=True) is None and not D.inplace(True)
     monkeypatch.undo()
-    assert D.int_pool(4, prepared=False) is None  # unprepared calls: INPLACE_UNPREPARED off (the default)
+    assert D.int_pool(4, prepared=False) is None  # the unprepared encrypt: INPLACE_UNPREPARED["encrypt"] off
+    assert D.inplace(False, "aggregate") == D.inplace(True)  # the unprepared aggregate keeps its (11 % gain)
     # the build without in-place writes
     mod = _build_pyconv(tmp_path, "-DFBM_INPLACE=0")
     assert tuple(mod.build_flags()) == (0, 1 if D.inplace_allowed() else 0)

@@ -2,7 +2,7 @@
 """what the unprepared list calls gain from writing into output objects made ahead
 (csrc/fbm_pyconv.c: int_pool + words_into_pool in the JL encrypt, the aggregate's last-stripe floats
 made while the GPU exponentiates and then overwritten).  Times, interleaved, with
-_device.INPLACE_UNPREPARED on and off:
+_device.INPLACE_UNPREPARED[call] on and off:
   * one node's SecaggCrypter.encrypt(List[float]) -> List[int] at --elements (the node's call),
   * the researcher's SecaggCrypter.aggregate(List[List[int]]) of P parties' lists at --elements,
 each the median of --reps calls (the previous result freed outside the clock), outputs compared equal.
@@ -55,12 +55,14 @@ def main():
 
     results, times = {}, {}
     for name, fn in (("node_encrypt", enc), ("researcher_aggregate", agg)):
+        key = "encrypt" if name == "node_encrypt" else "aggregate"
+        saved = dict(D.INPLACE_UNPREPARED)
         for setting in (True, False):
-            D.INPLACE_UNPREPARED = setting
+            D.INPLACE_UNPREPARED[key] = setting
             fn()  # a warm call of this setting
         for rep in range(args.reps):
             for setting in ((True, False) if rep % 2 == 0 else (False, True)):
-                D.INPLACE_UNPREPARED = setting
+                D.INPLACE_UNPREPARED[key] = setting
                 res = None
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
@@ -78,6 +80,7 @@ def main():
                               "median_ms": 1000 * ts[len(ts) // 2], "min_ms": 1000 * ts[0], "max_ms": 1000 * ts[-1],
                               "reps": len(ts), "equal_outputs": same}), flush=True)
         results.clear()
+        D.INPLACE_UNPREPARED.update(saved)
     summ = {}
     for name in ("node_encrypt", "researcher_aggregate"):
         on = sorted(times[(name, True)])[args.reps // 2]
