@@ -43,6 +43,22 @@ def _qw(x: np.ndarray, w: int) -> np.ndarray:
         return O.quantize(x) * np.uint64(w)
 
 
+def _oracle_outputs(want: np.ndarray, total_w: int) -> np.ndarray:
+    """The reference's float64 outputs for every element: reverse_quantize(_apply_average(sums)) of the
+    oracle's exact integer sums.  _apply_average is Python's int / int (correctly rounded); for sums and
+    weights below 2^53 both convert to float64 exactly and IEEE division rounds the same quotient, so numpy
+    gives it for the whole vector -- pinned against the oracle's own apply_average on a sample."""
+    assert int(want.max()) < 2**53 and total_w < 2**53
+    avg = want.astype(np.float64) / float(total_w)
+    idx = np.linspace(0, len(want) - 1, 4096).astype(np.int64)
+    assert avg[idx].tolist() == O.apply_average([int(v) for v in want[idx]], total_w)
+    c = O.CLIPPING_RANGE  # reverse_quantize (_secagg_utils.py:152-187): truncate to u64, then -c + step * u
+    step = (c - (-c)) / (O.TARGET_RANGE - 1)
+    out = float(-c) + step * avg.astype(np.uint64).astype(np.float64)
+    assert out[idx].view(np.uint64).tolist() == O.reverse_quantize(avg[idx].tolist()).view(np.uint64).tolist()
+    return out
+
+
 def _lom_window_oracle(u, ids, tau, qw_window, offset, nonce):
     """LOM.protect (secagg/_lom.py:105-175) restricted to elements [offset, offset+len):
     ChaCha20 blocks from offset/8 on (the keystream is counter-indexed)."""
@@ -201,9 +217,10 @@ def test_cfg4_jl_10m_8_parties_8_stripes(dev):
     for p in range(P):
         want += _qw(xs[p], ws[p])
     assert (sums[:, 1] == 0).all() and np.array_equal(sums[:, 0], want)
-    idx = rng.choice(n, 5000, replace=False)
-    ref = O.reverse_quantize(O.apply_average([int(v) for v in want[idx]], sum(ws)))
-    assert np.array_equal(out_whole.cpu().numpy()[idx].view(np.uint64), ref.view(np.uint64))
+    # every one of the 10M float64 outputs bit for bit against the oracle (so the batched and the 8 stripes'
+    # outputs too: they equal this vector above)
+    ref = _oracle_outputs(want, sum(ws))
+    assert np.array_equal(out_whole.cpu().numpy().view(np.uint64), ref.view(np.uint64))
 
 
 def _host_qw_sum(acc: np.ndarray, x: np.ndarray, w: int, threads: int = 8) -> None:
@@ -256,10 +273,9 @@ def test_cfg5_lom_ass_100m_16_parties(dev):
     # masks cancel exactly over all 100M elements (u64 wrap == int64 wrap), against the host sum
     out, sums = cr.aggregate_tensor(Y, sum(ws), want_sums=True)
     assert np.array_equal(_u64(sums), want)
-    idx = np.random.default_rng(5).choice(n, 3000, replace=False)
-    idx = np.concatenate([idx, np.asarray([0, n - 1] + cuts + [c - 1 for c in cuts])])
-    refo = O.reverse_quantize(O.apply_average([int(v) for v in want[idx]], sum(ws)))
-    assert np.array_equal(out.cpu().numpy()[idx].view(np.uint64), refo.view(np.uint64))
+    # all 100M float64 outputs bit for bit against the oracle
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), _oracle_outputs(want, sum(ws)).view(np.uint64))
+    idx = np.random.default_rng(5).choice(n, 64, replace=False)
     del Y, out
     # additive secret sharing of the 100M summed vector into 16 shares, and back: the exact column
     # sum (_additive_ss.py:252-267) is the oracle's sum again
