@@ -42,13 +42,13 @@ sys.path.insert(0, ROOT)
 # hardware queues (4 per process by default), so with 4 queues at most 4 launches run at once
 # and the rest wait behind them.  16 queues (set before the runtime starts; the pool allows up
 # to 32): 1/8-stripe step 183-186 -> 168-175 ms, 10M step 1174-1176 -> 1155-1158 ms (A/B on one
-# box, tools/ab_hwq.sh, profiles/r2_hwq_ab.txt).  An explicit setting in the environment wins.
+# box, tools/ab_hwq.sh, profiles/archive/r2_hwq_ab.txt).  An explicit setting in the environment wins.
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 ISA_MAD_TOPS_2400 = 256 * 4 * 16 * 2.4e9 / 1e12  # 39.3 T: quarter-rate v_mad_u64_u32 at 2.4 GHz
 MAD_PEAK_TOPS = 36.48        # measured v_mad_u64_u32 peak, whole chip, best occupancy (tools/microbench/madpeak.hip,
-                             # profiles/r1_madpeak.txt: 35.3 T at 2 waves/SIMD, 36.5 T at 4)
+                             # profiles/archive/r1_madpeak.txt: 35.3 T at 2 waves/SIMD, 36.5 T at 4)
 # v_mad_u64_u32 per lane of one N-adic product modulo N^2 -- the square, the general product and
 # the short-base product (tools/gen_nadic_asm.py) -- are read from the library (fbm_jl_mads), so the
 # count always matches the engine that ran.
@@ -539,7 +539,7 @@ def main():
                                  "unit": "T lane-mad/s", "frac": ach / MAD_PEAK_TOPS,
                                  "peak_provenance": {
                                      "measured_T": MAD_PEAK_TOPS,
-                                     "measured_note": "tools/microbench/madpeak.hip, profiles/r1_madpeak.txt: best "
+                                     "measured_note": "tools/microbench/madpeak.hip, profiles/archive/r1_madpeak.txt: best "
                                                       "occupancy (4 waves/SIMD) ran at 1.78 GHz -- power-limited",
                                      "isa_quarter_rate_T_at_2400MHz": ISA_MAD_TOPS_2400,
                                      "frac_of_isa_2400": ach / ISA_MAD_TOPS_2400,

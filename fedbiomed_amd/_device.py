@@ -400,7 +400,7 @@ def cgroup_cpu_quota() -> Optional[float]:
 def host_cpu_share() -> int:
     """The CPUs this process may use: its affinity, capped by its cgroup's CPU quota (>= 1).  The list
     API's host conversions use up to 16 of them (the 10M x 8 list aggregate with its factor prepared:
-    43.8 ms on 8 threads, 37.8 ms on 16 -- profiles/r5aj_list_agg_prepared.jsonl)."""
+    43.8 ms on 8 threads, 37.8 ms on 16 -- profiles/archive/r5aj_list_agg_prepared.jsonl)."""
     try:
         avail = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):

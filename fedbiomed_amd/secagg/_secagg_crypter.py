@@ -255,7 +255,7 @@ class SecaggCrypter:
                 ct = self.encrypt_tensor(num_nodes, current_round, x[c0 * cr:min(n, c1 * cr)], key, biprime,
                                          clipping_range, weight, target_range, ct_offset=c0)
                 # (in stream order: a side stream for the copies measured the same, 152-154 ms at 10M --
-                # profiles/r4_node_encrypt_probe.jsonl)
+                # profiles/archive/r4_node_encrypt_probe.jsonl)
                 host[c0:c1].copy_(ct, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(main)
@@ -368,7 +368,7 @@ class SecaggCrypter:
         is raised by the aggregate that takes it.  It also warms the aggregate's pinned staging buffers
         and makes its output list's float objects (~320 MB of host memory at 10M, held until used or
         dropped), whose values the aggregate then writes in place: with both, the list aggregate at 10M x 8
-        takes 45 ms instead of 158 (`profiles/r5x_bench.json`).
+        takes 45 ms instead of 158 (`profiles/archive/r5x_bench.json`).
         Best effort: False (nothing prepared) where aggregate would refuse the arguments.  The key
         itself is not kept, only a SHA-256 tag of it."""
         self.drop_prepared_aggregate()

@@ -33,7 +33,7 @@ def test_engine_policy_host():
         # past the group engines' residency (persistent workgroups loop): a config-4 N = 4 stripe's
         # 83 334 ciphertexts take the triple (41 ms measured against the one-lane engine's 49); 100 000
         # (five triple waves per SIMD, 52.7 ms at 107 520) and 120 000 go to the one-lane engine, whose
-        # unrolled square runs a round of two waves in 49 ms (profiles/r3_unroll_ab.jsonl)
+        # unrolled square runs a round of two waves in 49 ms (profiles/archive/r3_unroll_ab.jsonl)
         assert lib.fbm_jl_engine_for(83_334) == 3 and lib.fbm_jl_engine_for(100_000) == 1
         assert lib.fbm_jl_engine_for(120_000) == 1
     finally:

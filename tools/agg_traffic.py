@@ -3,7 +3,7 @@
 HBM traffic per launch (2 * FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md) against the
 algorithmic bytes of DESIGN.md section 4, at the full vector and at the 1/8 stripe.
 
-    python tools/agg_traffic.py gpurun_out/pmcagg2 profiles/r2_s4_agg_traffic.json
+    python tools/agg_traffic.py gpurun_out/pmcagg2 profiles/archive/r2_s4_agg_traffic.json
 """
 
 import collections

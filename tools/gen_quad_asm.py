@@ -168,7 +168,7 @@ class Geo:
 # of the group: QT = Q(i-1) + Q(i), QB = QT(i-1) + Q(i) = Q(i-2) + Q(i-1) + Q(i) -- the value of the
 # group's lane 0 in lanes 0, 1, 2 (the neighbours' copies are 0; lane 0 of the wave reads 0 past the
 # end).  Two VALU instructions per broadcast in place of one ds_bpermute and its LDS latency.
-# Measured equal to the permutes alone and 1 % slower with CYC_B0D (profiles/r4_tri_dpp_ab.jsonl,
+# Measured equal to the permutes alone and 1 % slower with CYC_B0D (profiles/archive/r4_tri_dpp_ab.jsonl,
 # r4_tri_b0d_ab.jsonl): the 144 extra VALU instructions per square cost what the permutes' LDS latency did.
 TRI_DPP_BCAST = os.environ.get("FBM_GEN_TRI_DPP", "0") == "1"  # (an A/B switch, off)
 
@@ -523,7 +523,7 @@ def product(sq, g=QUAD, carries=CARRY_PAIRS, cyc=None):
 CYC_SQUARE = True
 # Round 4: the cyclic-band square's doubled cross products as x_i * (2 b0[r]) from M doubled limb
 # registers made once per square, in place of 2 x_i made once per row (36 -> M shifts per square): the
-# triple at one rank's 1/8 / 1/4 stripe -0.7 / -1.2 % (profiles/r4_tri_b0d_ab.jsonl).  FBM_GEN_CYC_B0D=0
+# triple at one rank's 1/8 / 1/4 stripe -0.7 / -1.2 % (profiles/archive/r4_tri_b0d_ab.jsonl).  FBM_GEN_CYC_B0D=0
 # generates the per-row doubling (the A/B base).
 CYC_B0D = os.environ.get("FBM_GEN_CYC_B0D", "1") == "1"
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # LOM measurement pass on the GPU box: rocprofv3 kernel trace (+stats) of the LOM bench
 # (--scheme lom, 10M elements x 8 parties) and the two HBM PMC passes for its kernels.
-# Summarise with: python tools/prof_summary.py gpurun_out/<tag> profiles/r1_lom
+# Summarise with: python tools/prof_summary.py gpurun_out/<tag> profiles/archive/r1_lom
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${1:-r1_lom}
 mkdir -p $O

@@ -44,7 +44,7 @@ import gen_quad_asm as GQ  # noqa: E402
 COST = {"mad": 4.1, "valu64": 3.5, "mul_lo": 3.4, "dpp": 3.4, "valu32": 2.25, "lds": 1.0, "salu": 0.0}
 VGPR_GATE, SLOT_GATE = 236, 0.04
 COMPILER_VGPRS = 6  # the kernel around the square: 236 VGPRs in all with the square's 230 (ISA, r4)
-TRI_KERNEL_VGPRS = 168  # jl_expg_kernel<3>: 3 waves per SIMD (profiles/r4_kernel_resources.txt)
+TRI_KERNEL_VGPRS = 168  # jl_expg_kernel<3>: 3 waves per SIMD (profiles/archive/r4_kernel_resources.txt)
 
 
 def classify(ln):
@@ -169,7 +169,7 @@ def triple():
     v = vg + extra
     var = {"counts": dict(r), "issue_clocks": clocks(r), "vgprs": v, "waves_per_simd": 512 // v,
            "note": "the triple runs 3 waves per SIMD at <= 170 VGPRs; past it 2 (w = 2 -> 3 measured 5.64 -> 5.48 us "
-                   "per square per wave, profiles/r3_carry_rotation_ab.jsonl)"}
+                   "per square per wave, profiles/archive/r3_carry_rotation_ab.jsonl)"}
     var["slot_change"] = (var["issue_clocks"] - base_clk) / base_clk
     var["passes_gate"] = var["slot_change"] <= -SLOT_GATE and var["waves_per_simd"] >= out["shipped"]["waves_per_simd"]
     out["variants"] = {"column_sums": var}

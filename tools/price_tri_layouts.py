@@ -18,7 +18,7 @@ of one lane of a group -- the wave's issue count, every lane running the same st
                   (one mad), and lane 0 -- whose bits 29-31 the lane below must not receive -- adding them with a
                   second masked mad after a 32-bit shift: per part 1 DPP + 3 instead of 1 DPP + 2.
 The row counts of the alternatives are written out from their per-row instruction lists below (the same classes
-as the shipped rows); the shipped count is the generator's.  Writes profiles/r5_tri_layout_pricing.json.
+as the shipped rows); the shipped count is the generator's.  Writes profiles/archive/r5_tri_layout_pricing.json.
 
     python tools/price_tri_layouts.py
 """

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 measurement pass (tools/gpu_measure.sh) into profiles/.
 
-    python tools/prof_summary.py gpurun_out/r2 profiles/r1
+    python tools/prof_summary.py gpurun_out/r2 profiles/archive/r1
 
 reads  <dir>/prof      (--kernel-trace --stats)   -> <prefix>_kernel_stats.csv
        <dir>/pmc_fetch (--pmc FETCH_SIZE)          -> <prefix>_hbm_traffic.json
