@@ -65,6 +65,7 @@ STATS_WORDS = 4
 
 _lock = threading.Lock()
 _libs = {}  # path -> CDLL
+_typed = {}  # path -> names whose restype / argtypes are set
 _tls = threading.local()  # .test: depth of test_hooks() on this thread
 loaded_abi = None  # fbm_abi_version() of the loaded library (ABI_VERSION, or one less for an A/B variant)
 
@@ -159,10 +160,10 @@ def _open(path: str, sigs: dict) -> ctypes.CDLL:
     """Loads (once per path) a build of the library; it must export every symbol of `sigs` and report
     ABI_VERSION, unless FBM_AB_VARIANT=1."""
     global loaded_abi
+    lib = _libs.get(path)
+    if lib is not None and _typed[path] >= sigs.keys():  # loaded, every signature of `sigs` set
+        return lib
     with _lock:
-        lib = _libs.get(path)
-        if lib is not None and all(hasattr(lib, n) for n in sigs):
-            return lib
         if not os.path.exists(path):
             raise NativeUnavailable(
                 f"HIP extension not built: {path} is missing (run `python -m fedbiomed_amd._build`)")
@@ -191,6 +192,9 @@ def _open(path: str, sigs: dict) -> ctypes.CDLL:
         if abi != ABI_VERSION and not (variant and abi == ABI_VERSION - 1):
             raise NativeUnavailable(f"ABI version mismatch: {path} reports {abi}, this binding needs {ABI_VERSION}")
         loaded_abi = abi
+        _typed[path] = _typed.get(path, set()) | (set(sigs) - set(missing))
+        if variant:
+            _typed[path] |= set(sigs)  # (an A/B variant may lack some: don't look again)
         _libs[path] = lib
         return lib
 

@@ -341,3 +341,26 @@ def test_abi2_variant_refuses_wide_rounds():
         assert D._check_round(2 ** 512)[16] == 1
     finally:
         N.loaded_abi = saved
+
+
+def test_lib_path_override_serves_both_builds():
+    """FBM_LIB_PATH (an A/B variant, built with the test build's exports) is both load() and load_test(): one
+    CDLL, and the test header's signatures set on it even when load() opened it first."""
+    import subprocess
+    import sys
+
+    from fedbiomed_amd import _build, _native as N
+
+    _build.build()
+    code = (f"import sys; sys.path.insert(0, {ROOT!r})\n"
+            "import ctypes\n"
+            "from fedbiomed_amd import _native as N\n"
+            "a = N.load(); t = N.load_test()\n"
+            "assert t is a is N.load()\n"
+            "assert t.fbm_jl_engine_for.argtypes == [ctypes.c_uint64]\n"
+            "assert t.fbm_jl_engine_for(333334) == 1\n"
+            "print('OK')\n")
+    env = dict(os.environ, FBM_LIB_PATH=N.TEST_LIB_PATH)
+    env.pop("FBM_AB_VARIANT", None)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and r.stdout.strip() == "OK", r.stderr
