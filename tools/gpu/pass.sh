@@ -14,6 +14,8 @@
 #   dist8      bench.py --gpus 8 through spawn_ranks: 8 gloo ranks sharing this GPU, 2M elements
 #   dist8full  the same at the metric's 10M elements and the driver's --steps 20 --warmup 5 (all 8 ranks'
 #              work on one GPU: an upper bound on the driver's 8-GPU wall time)
+#   dist8run   the driver's launch form: python -m torch.distributed.run --nproc-per-node 8 ... bench.py --gpus 8
+#              (gloo instead of RCCL, which refuses eight ranks on one GPU), 2M elements
 #   TEST=path  one test file / node id (e.g. TEST=tests/test_configs.py)
 #   RUN=tools/x.py[,args]  a probe script (args comma-separated)         -> x.jsonl
 # Summaries: python tools/prof_summary.py gpurun_out/TAG/jl profiles/TAG_jl (and .../lom).
@@ -84,6 +86,17 @@ run_step() {
     timeout -k 10 900 $PY bench.py --gpus 8 --dist-backend gloo $a > $O/$s.json 2> $O/$s.err
     local rc=$?
     echo "{\"step\": \"$s\", \"rc\": $rc, \"wall_s\": $(( $(date +%s) - t0 )), \"lines\": $(wc -l < $O/$s.json)}" \
+      > $O/$s.meta.json
+    cat $O/$s.meta.json; holders | tee -a $O/$s.meta.json; tail -c 400 $O/$s.json; echo
+    [ $rc -ne 0 ] && tail -c 2000 $O/$s.err
+    return $rc ;;
+  dist8run)
+    local t0=$(date +%s)
+    timeout -k 10 900 $PY -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+      --master-port 29533 bench.py --gpus 8 --dist-backend gloo --elements 2000000 --steps 2 --warmup 1 \
+      > $O/$s.json 2> $O/$s.err
+    local rc=$?
+    echo "{\"step\": \"$s\", \"rc\": $rc, \"wall_s\": $(( $(date +%s) - t0 )), \"json_lines\": $(grep -c '^{' $O/$s.json)}" \
       > $O/$s.meta.json
     cat $O/$s.meta.json; holders | tee -a $O/$s.meta.json; tail -c 400 $O/$s.json; echo
     [ $rc -ne 0 ] && tail -c 2000 $O/$s.err
