@@ -1466,6 +1466,13 @@ int fbm_jl_encrypt_factor(const void* x, int x_dtype, uint64_t n, double clip, d
     set_error("null pointer argument");
     return FBM_E_ARG;
   }
+  {  // jl_encf_kernel stages N pt + 1 in the output rows before it reads the factor rows
+    const uintptr_t o0 = (uintptr_t)ct_out, o1 = o0 + n_ct * 256, f0 = (uintptr_t)factor, f1 = f0 + n_ct * 256;
+    if (o0 < f1 && f0 < o1) {
+      set_error("fbm_jl_encrypt_factor: ct_out must not overlap factor");
+      return FBM_E_ARG;
+    }
+  }
   if ((int64_t)weight <= -(int64_t)(1 << 17)) {
     set_error("negative weight %lld outside (-2^17, 0)", (long long)(int64_t)weight);
     return FBM_E_ARG;

@@ -1649,12 +1649,14 @@ __device__ __forceinline__ void div_by_n(uint32_t (&D)[64], const JlParams& jp, 
 // CU).  A global scratch column instead (two workgroups per CU) was 8 % faster over several
 // rounds of workgroups but tripled the HBM traffic (write-back of the scratch through L2) and
 // was 10 % slower on an 8-GPU split's stripe (tools/ab_prod.sh).
-__global__ void __launch_bounds__(FBM_BLOCK, 1) jl_prod_kernel(const uint32_t* __restrict__ cts, int n_parties,
+// Round 6: each operand is read by the product straight from its 64-word row (fbm_mm_row: the 28-bit limbs
+// made in B's registers), so a lane needs only its A column in LDS -- 76.8 KB per workgroup instead of 153.6:
+// two workgroups, two waves per SIMD, where the staged second column allowed one.
+__global__ void __launch_bounds__(FBM_BLOCK, 2) jl_prod_kernel(const uint32_t* __restrict__ cts, int n_parties,
                                                               uint64_t n_ct, const uint32_t* __restrict__ cst,
                                                               JlParams jp, const uint32_t* __restrict__ factor,
                                                               uint32_t* __restrict__ xout) {
   __shared__ uint32_t lds_a[(FBM_NL + 1) * FBM_BLOCK];
-  __shared__ uint32_t lds_b[(FBM_NL + 1) * FBM_BLOCK];
   const int tid = threadIdx.x;
   uint32_t* lds = lds_a + tid;
   const uint32_t aoff = lds_addr(lds);
@@ -1662,19 +1664,12 @@ __global__ void __launch_bounds__(FBM_BLOCK, 1) jl_prod_kernel(const uint32_t* _
   const uint64_t ct_raw = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
   const bool valid = ct_raw < n_ct;  // (an early return here measured 15 % slower)
   const uint64_t ct = valid ? ct_raw : n_ct - 1;
-  const uint32_t boff = lds_addr(lds_b + tid);
   lds_store_uniform<FBM_NL>(lds, FBM_BLOCK, cst + FBM_CST_RK);
   const int n_ops = n_parties + (factor ? 1 : 0);
 #pragma unroll 1
   for (int u = 0; u < n_ops; ++u) {
-    {
-      const uint32_t* row = u < n_parties ? cts + ((uint64_t)u * n_ct + ct) * 64 : factor + ct * 64;
-      uint32_t c32[64], c28[FBM_NL];
-      load_row64(row, c32);
-      to28<64, FBM_NL>(c32, c28);
-      lds_store_col(lds_b + tid, FBM_BLOCK, c28);
-    }
-    fbm_mm_lds(aoff, boff, M, jp.mc.mp);
+    const uint32_t* row = u < n_parties ? cts + ((uint64_t)u * n_ct + ct) * 64 : factor + ct * 64;
+    fbm_mm_row(aoff, row, M, jp.mc.mp);
   }
   uint32_t D[64];
   {
@@ -1723,15 +1718,17 @@ __global__ void __launch_bounds__(FBM_BLOCK, 1) jl_prod_kernel(const uint32_t* _
 // A negative weight (pt = |pt|, see jl_pack_kernel) encrypts 1 - N |pt|: b = N |pt| - 1, and
 // the product is negated mod M at the end ((1 - N |pt|) F = -(N |pt| - 1) F); |pt| = 0 is 1.
 // ------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(FBM_BLOCK, 1) jl_encf_kernel(const uint32_t* __restrict__ pt, uint64_t n_ct,
+// Round 6: b = N pt + 1 is staged in the lane's own output row (rewritten at the end) and both products read
+// their operand rows with fbm_mm_row, as jl_prod_kernel: one LDS column per lane, two waves per SIMD.  A lane
+// past n_ct reads the factor row of ciphertext n_ct - 1 (read-only) instead, and stores nothing.
+__global__ void __launch_bounds__(FBM_BLOCK, 2) jl_encf_kernel(const uint32_t* __restrict__ pt, uint64_t n_ct,
                                                               const uint32_t* __restrict__ cst, JlParams jp,
                                                               int negative, const uint32_t* __restrict__ factor,
                                                               uint32_t* __restrict__ out) {
   __shared__ uint32_t lds_a[(FBM_NL + 1) * FBM_BLOCK];
-  __shared__ uint32_t lds_b[(FBM_NL + 1) * FBM_BLOCK];
   const int tid = threadIdx.x;
   uint32_t* lds = lds_a + tid;
-  const uint32_t aoff = lds_addr(lds), boff = lds_addr(lds_b + tid);
+  const uint32_t aoff = lds_addr(lds);
   const uint32_t* M = cst + FBM_CST_M;
   const uint64_t ct_raw = (uint64_t)blockIdx.x * FBM_BLOCK + tid;
   const bool valid = ct_raw < n_ct;  // no early return: every lane runs the products
@@ -1739,7 +1736,7 @@ __global__ void __launch_bounds__(FBM_BLOCK, 1) jl_encf_kernel(const uint32_t* _
   lds_store_uniform<FBM_NL>(lds, FBM_BLOCK, cst + FBM_CST_RK);
   bool neg;
   {
-    uint32_t p[32], b[64], b28[FBM_NL];
+    uint32_t p[32], b[64];
     load_row32(reinterpret_cast<const uint4*>(pt + ct * 32), p);
     uint32_t any = 0;
 #pragma unroll
@@ -1763,17 +1760,13 @@ __global__ void __launch_bounds__(FBM_BLOCK, 1) jl_encf_kernel(const uint32_t* _
         c = (uint32_t)(t >> 32);
       }
     }
-    to28<64, FBM_NL>(b, b28);
-    lds_store_col(lds_b + tid, FBM_BLOCK, b28);
+    if (valid) {
+      store_row64(out + ct * 64, b);
+      __builtin_amdgcn_s_waitcnt(0);  // (vmcnt 0: the stores done before the product loads the row)
+    }
   }
-  fbm_mm_lds(aoff, boff, M, jp.mc.mp);  // a = R b
-  {
-    uint32_t c32[64], c28[FBM_NL];
-    load_row64(factor + ct * 64, c32);
-    to28<64, FBM_NL>(c32, c28);
-    lds_store_col(lds_b + tid, FBM_BLOCK, c28);
-  }
-  fbm_mm_lds(aoff, boff, M, jp.mc.mp);  // a = b F (lazy)
+  fbm_mm_row(aoff, valid ? out + ct * 64 : factor + ct * 64, M, jp.mc.mp);  // a = R b
+  fbm_mm_row(aoff, factor + ct * 64, M, jp.mc.mp);                         // a = b F (lazy)
   uint32_t v[FBM_NL], D[64];
   lds_load_col(lds, FBM_BLOCK, v);
   mont_csub(v, jp.mc.M);

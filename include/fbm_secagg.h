@@ -177,6 +177,7 @@ int fbm_jl_encrypt_phase(const void* x, int x_dtype, uint64_t n, double clip, do
  * H(t_k)^sk needs no plaintext, so a node can compute it while it trains.  Equal bit for bit to
  * fbm_jl_encrypt of the same key, round and ct_offset (UserKey.encrypt, _jls.py:473-505).
  *   factor: device, n_ct x 64 uint32 limbs;  workspace: fbm_jl_encrypt_workspace(n_ct) bytes.
+ *   ct_out must not overlap factor (FBM_E_ARG) nor the input x: the kernel stages N pt + 1 in it.
  * An even N or N = 1 is FBM_E_UNSUPPORTED (fbm_jl_encrypt takes every N).                    */
 int fbm_jl_encrypt_factor(const void* x, int x_dtype, uint64_t n, double clip, double two_clip, double target_f,
                           uint64_t target_m1, uint64_t weight, int es, int cr, const uint32_t* biprime,

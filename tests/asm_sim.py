@@ -138,6 +138,11 @@ class Lane:
         elif op == "global_load_dword":
             addr = self.get(ops[2]) + self.get(ops[1]) + off
             self.put(ops[0], self.glb[addr])
+        elif op == "global_load_dwordx4":  # dst v[a:a+3], 64-bit VGPR address, "off" (no SGPR base)
+            assert ops[2] == "off"
+            addr = self.get(ops[1]) + off
+            assert addr % 16 == 0, f"global_load_dwordx4 address {addr}"
+            self.put(ops[0], sum(self.glb[addr + 4 * i] << (32 * i) for i in range(4)))
         elif op == "ds_read_b32":
             addr = self.get(ops[1]) + off
             self.put(ops[0], self.lds.get(addr, 0))
@@ -172,6 +177,8 @@ class Lane:
             self.put(ops[0], self.get(ops[1]) * self.get(ops[2]))
         elif op == "v_lshlrev_b32":
             self.put(ops[0], self.get(ops[2]) << self.get(ops[1]))
+        elif op == "v_bfe_u32":
+            self.put(ops[0], (self.get(ops[1]) >> self.get(ops[2])) & ((1 << self.get(ops[3])) - 1))
         elif op == "v_alignbit_b32":
             self.put(ops[0], (((self.get(ops[1]) << 32) | self.get(ops[2])) >> (self.get(ops[3]) & 31)) & M32)
         elif op == "v_mad_u64_u32":

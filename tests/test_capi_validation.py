@@ -89,7 +89,7 @@ def test_factor_and_aggregate_refusals(env):
     c, c2, tf, tm1 = _q()
     enc_f = dict(x=_p(x), n=n_ct, bp=bp, f=_p(f), ct=_p(ct[0]), ws=_p(ws))
     for change, code in (({"bp": _h(h["even"])}, E_UNSUPPORTED), ({"f": None}, E_ARG), ({"x": None}, E_ARG),
-                         ({"ws": None}, E_ARG)):
+                         ({"ws": None}, E_ARG), ({"ct": _p(f)}, E_ARG)):  # (the output staged over the factor)
         a = {**enc_f, **change}
         _expect(lib, lib.fbm_jl_encrypt_factor(a["x"], N.FBM_F32, a["n"], c, c2, tf, tm1, 1, es, cr, a["bp"], a["f"],
                                                a["ct"], a["ws"], _p(st), None), code)

@@ -34,8 +34,8 @@ Result < 2M whenever a, b < 2M (R = 2^2072 >= 4M): lazy reduction, as in fbm_mon
 
 Operands: the A operand is the lane's LDS column (limb k at byte a_off + k*1024) and is
 overwritten by the result; B comes either from an LDS column (b_off, same stride; b_off ==
-a_off squares) or from global memory (uniform base + per-lane byte offset, limb stride
-1024 B: the workgroup-blocked [limb][lane] layout of the tables and residue columns).
+a_off squares) or (round 6) from the lane's 64-word little-endian row in global memory, converted
+to 28-bit limbs in B's registers (fbm_mm_row: the combine kernels read their ciphertexts this way).
 The LDS column must be allocated with 75 limb rows: the last row's a_{i+1} prefetch reads
 row 74 (value unused).
 
@@ -102,6 +102,28 @@ def load_b_global():
     return out
 
 
+def load_b_row():
+    """B from the lane's own 2048-bit value as 64 little-endian 32-bit words at the per-lane byte address
+    %[r] (a VGPR pair): a ciphertext row where the kernel's input already holds it -- no LDS staging
+    column (round 6: the products then need 300 bytes of LDS per lane, not 600, and run two waves per
+    SIMD).  Sixteen 16-byte loads into B's registers, then the 28-bit limbs in place, the top limb first
+    (limb k reads words floor(28 k / 32) and the next, both at or below register k, and no limb above k
+    reads those once it is written).  Issued with the A column's first read; converted after the wait."""
+    return [f"global_load_dwordx4 v[{146 + 4 * i}:{149 + 4 * i}], %[r], off offset:{16 * i}" for i in range(16)]
+
+
+def convert_b_row():
+    out = []
+    for k in range(NL - 1, -1, -1):
+        w, sh = divmod(28 * k, 32)
+        if sh + 28 <= 32 or w + 1 >= 64:  # inside word w (the top limb: its last 4 bits)
+            out.append(f"v_bfe_u32 {B(k)}, {B(w)}, {sh}, {min(28, 32 - sh)}")
+        else:  # straddles words w, w + 1
+            out.append(f"v_alignbit_b32 {B(k)}, {B(w + 1)}, {B(w)}, {sh}")
+            out.append(f"v_and_b32 {B(k)}, {MASK}, {B(k)}")
+    return out
+
+
 def row(first):
     """One row of the product; `first` = accumulators not yet initialised (addend 0)."""
     add = (lambda k: "0") if first else A
@@ -149,9 +171,11 @@ def normalise_store():
 def product(bsrc):
     body = []
     body += load_modulus()
-    body += load_b_lds() if bsrc == "lds" else load_b_global()
+    body += {"lds": load_b_lds, "global": load_b_global, "row": load_b_row}[bsrc]()
     body += [f"v_mov_b32 {MPV}, %[mp]", f"v_mov_b32 {AADR}, %[a]", f"ds_read_b32 {AI}, {AADR}"]
     body += ["s_waitcnt vmcnt(0) lgkmcnt(0)"]
+    if bsrc == "row":
+        body += convert_b_row()
     body += row(True)
     body += ["s_mov_b32 s34, 1", "1:"]
     body += row(False)
@@ -308,14 +332,14 @@ def clobbers():
 
 
 def main():
-    lds, glb, sq = product("lds"), product("global"), square()
+    lds, rw, sq = product("lds"), product("row"), square()
     hdr = f"""// GENERATED by tools/gen_mont_asm.py -- do not edit by hand.
 //
 // gfx950 assembly Montgomery product, radix 2^28, 74 limbs (modulus N^2 <= 2048 bits,
 // R = 2^2072).  a (per-lane LDS column) <- a * b * R^-1, lazily reduced (< 2M for a, b < 2M).
 // See tools/gen_mont_asm.py for the register plan and the arithmetic; fbm_mont.hpp's
 // mont_mul<74> is the same computation in C++.
-// {len(lds)} instructions (B from LDS), {len(glb)} (B from global), {len(sq)} (square); row loop
+// {len(lds)} instructions (B from LDS), {len(rw)} (B from a 64-word row), {len(sq)} (square); row loop
 // bodies {len(row(False))} and ~{sq_row_len()} per square row (its a*b part is entered part-way).
 #pragma once
 #include <stdint.h>
@@ -336,13 +360,14 @@ __device__ __forceinline__ void fbm_mm_lds(uint32_t a_off, uint32_t b_off, const
       : "memory", "vcc", "scc", FBM_MM_CLOBBERS);
 }}
 
-// B operand from global memory: limb k at bb + b_off + k*1024 (bytes; bb uniform).
-__device__ __forceinline__ void fbm_mm_glb(uint32_t a_off, const uint32_t* bb, uint32_t b_off, const uint32_t* M,
-                                           uint32_t mp) {{
+// B operand from global memory: the lane's b < 2^2048 as 64 little-endian words at `row` (a ciphertext row as
+// the kernels receive it; 16-byte aligned).  The caller's own stores to that row must be complete (the
+// product does not wait for them).
+__device__ __forceinline__ void fbm_mm_row(uint32_t a_off, const uint32_t* row, const uint32_t* M, uint32_t mp) {{
   asm volatile(
-{c_string(glb)}
+{c_string(rw)}
       :
-      : [a] "v"(a_off), [b] "v"(b_off), [bb] "s"(bb), [M] "s"(M), [mp] "s"(mp)
+      : [a] "v"(a_off), [r] "v"(row), [M] "s"(M), [mp] "s"(mp)
       : "memory", "vcc", "scc", FBM_MM_CLOBBERS);
 }}
 
@@ -357,7 +382,7 @@ __device__ __forceinline__ void fbm_sq_lds(uint32_t a_off, const uint32_t* M, ui
 """
     with open(OUT, "w") as f:
         f.write(hdr)
-    print(f"wrote {OUT}: lds {len(lds)} / global {len(glb)} / square {len(sq)} instructions")
+    print(f"wrote {OUT}: lds {len(lds)} / row {len(rw)} / square {len(sq)} instructions")
 
 
 if __name__ == "__main__":
