@@ -1577,19 +1577,8 @@ __device__ __forceinline__ void mul1024(const uint32_t (&a)[32], const uint32_t*
   r[63] = (uint32_t)lo;
 }
 
-__device__ __forceinline__ void div_by_n(uint32_t (&D)[64], const JlParams& jp, uint32_t (&q)[32]) {
-  {
-    uint32_t dl[32];
-#pragma unroll
-    for (int i = 0; i < 32; ++i) dl[i] = D[i];
-    mullo1024(dl, jp.Ninv32, q);
-    uint32_t pr[64];
-    mul1024(q, jp.N32, pr);
-    uint32_t diff = 0;
-#pragma unroll
-    for (int i = 0; i < 64; ++i) diff |= pr[i] ^ D[i];
-    if (diff == 0) return;
-  }
+// binary long division (the fallback of the exact-division check)
+__device__ __forceinline__ void div_by_n_slow(uint32_t (&D)[64], const JlParams& jp, uint32_t (&q)[32]) {
   uint32_t r[33];
 #pragma unroll
   for (int i = 0; i < 32; ++i) q[i] = 0u;
@@ -1633,6 +1622,41 @@ __device__ __forceinline__ void div_by_n(uint32_t (&D)[64], const JlParams& jp, 
     }
   }
 }
+
+// D in the lane's LDS column (64 words, stride FBM_BLOCK): the fast path holds only D's low half, then q and
+// the running column sums, in registers -- q N's low half equals D's by construction of q, so only the high half
+// is compared, each word read from LDS as its column completes.  D's 64 registers kept live across the check
+// (round 6's first form) cost the two-waves-per-SIMD jl_prod_kernel 308 bytes of scratch per lane.
+__device__ __forceinline__ void div_by_n_lds(const uint32_t* ldsD, const JlParams& jp, uint32_t (&q)[32]) {
+  {
+    uint32_t dl[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) dl[i] = ldsD[i * FBM_BLOCK];
+    mullo1024(dl, jp.Ninv32, q);
+  }
+  uint64_t lo = 0, hi = 0;
+  uint32_t diff = 0;
+#pragma clang loop unroll(full)
+  for (int k = 0; k < 63; ++k) {
+#pragma clang loop unroll(full)
+    for (int i = (k < 32 ? 0 : k - 31); i <= (k < 32 ? k : 31); ++i) {
+      const uint64_t p = (uint64_t)q[i] * jp.N32[k - i];
+      lo += (uint32_t)p;
+      hi += (p >> 32);
+    }
+    if (k >= 32) diff |= (uint32_t)lo ^ ldsD[k * FBM_BLOCK];
+    const uint64_t c = (lo >> 32) + hi;
+    lo = c & 0xffffffffull;
+    hi = c >> 32;
+  }
+  diff |= (uint32_t)lo ^ ldsD[63 * FBM_BLOCK];
+  if (diff == 0) return;
+  uint32_t D[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) D[i] = ldsD[i * FBM_BLOCK];
+  div_by_n_slow(D, jp, q);
+}
+
 
 // ------------------------------------------------------------------------------------
 // aggregate (_jls.py:353-374 product, :547-558 decrypt), one lane per ciphertext:
@@ -1699,7 +1723,8 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_prod_kernel(const uint32_t* _
       b = (uint32_t)(d >> 63);
     }
   } else {
-    div_by_n(D, jp, x);
+    lds_store_col<64>(lds, FBM_BLOCK, D);  // (the column is free: the product is in D)
+    div_by_n_lds(lds, jp, x);
   }
   if (valid) {
     uint4* o = reinterpret_cast<uint4*>(xout + ct * 32);
@@ -1736,32 +1761,42 @@ __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_encf_kernel(const uint32_t* _
   lds_store_uniform<FBM_NL>(lds, FBM_BLOCK, cst + FBM_CST_RK);
   bool neg;
   {
-    uint32_t p[32], b[64];
+    uint32_t p[32];
     load_row32(reinterpret_cast<const uint4*>(pt + ct * 32), p);
     uint32_t any = 0;
 #pragma unroll
     for (int i = 0; i < 32; ++i) any |= p[i];
     neg = negative && any;
-    mul1024(p, jp.N32, b);  // N |pt| <= (2^1024 - 1)^2
-    if (neg) {  // N |pt| - 1: N |pt| >= N >= 3, no borrow out
-      uint32_t br = 1;
+    // b = N p' + A, product-scanned into the output row four words at a time (no 64-word b in registers):
+    // p' = pt, A = 1 -> N pt + 1 < 2^2048; a negative weight p' = |pt| - 1, A = N - 1 -> N |pt| - 1
+    uint32_t br = neg ? 1u : 0u;
 #pragma unroll
-      for (int i = 0; i < 64; ++i) {
-        const uint64_t d = (uint64_t)b[i] - br;
-        b[i] = (uint32_t)d;
-        br = (uint32_t)(d >> 63);
-      }
-    } else {  // N pt + 1 < 2^2048: no carry out
-      uint32_t c = 1;
-#pragma unroll
-      for (int i = 0; i < 64; ++i) {
-        const uint64_t t = (uint64_t)b[i] + c;
-        b[i] = (uint32_t)t;
-        c = (uint32_t)(t >> 32);
-      }
+    for (int i = 0; i < 32; ++i) {
+      const uint64_t d = (uint64_t)p[i] - br;
+      p[i] = (uint32_t)d;
+      br = (uint32_t)(d >> 63);
     }
+    uint4* o = reinterpret_cast<uint4*>(out + ct * 64);
+    uint64_t lo = neg ? (uint64_t)(jp.N32[0] - 1u) : 1u, hi = 0;
+    uint32_t w[4];
+#pragma clang loop unroll(full)
+    for (int k = 0; k < 63; ++k) {
+      if (k > 0 && k < 32) lo += neg ? jp.N32[k] : 0u;
+#pragma clang loop unroll(full)
+      for (int i = (k < 32 ? 0 : k - 31); i <= (k < 32 ? k : 31); ++i) {
+        const uint64_t m = (uint64_t)p[i] * jp.N32[k - i];
+        lo += (uint32_t)m;
+        hi += (m >> 32);
+      }
+      w[k & 3] = (uint32_t)lo;
+      const uint64_t c = (lo >> 32) + hi;
+      lo = c & 0xffffffffull;
+      hi = c >> 32;
+      if ((k & 3) == 3 && valid) o[k >> 2] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    w[3] = (uint32_t)lo;
     if (valid) {
-      store_row64(out + ct * 64, b);
+      o[15] = make_uint4(w[0], w[1], w[2], w[3]);
       __builtin_amdgcn_s_waitcnt(0);  // (vmcnt 0: the stores done before the product loads the row)
     }
   }

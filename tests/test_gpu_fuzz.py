@@ -7,6 +7,7 @@ list aggregate in ct_offset stripes (FBM_ONE_LANE_ROUND shrunk), some take a pre
 party's encrypt takes its factor computed ahead (prepare_encrypt)."""
 
 import logging
+import os
 import random
 
 import numpy as np
@@ -14,7 +15,9 @@ import pytest
 
 from fedbiomed_amd import _device as D, workload as W
 
-N_CASES = 48
+# FBM_FUZZ_CASES / FBM_FUZZ_SEED_BASE: a longer run over other seeds (round 6: profiles/r6g_fuzz_extended.txt)
+N_CASES = int(os.environ.get("FBM_FUZZ_CASES", "48"))
+SEED_BASE = int(os.environ.get("FBM_FUZZ_SEED_BASE", "0"))
 
 
 def _bits(xs):
@@ -22,7 +25,7 @@ def _bits(xs):
 
 
 def _jl_case(i):
-    rng = random.Random(9100 + i)
+    rng = random.Random(9100 + SEED_BASE + i)
     P = rng.randint(1, 9)
     target = rng.choice([None, 2**10, 2**16, 2**24])
     cr = D.jl_slot(target, P)[1]
@@ -73,7 +76,7 @@ def test_jl_fuzz_vs_oracle(i, monkeypatch, caplog):
 
 
 def _lom_case(i):
-    rng = random.Random(9300 + i)
+    rng = random.Random(9300 + SEED_BASE + i)
     P = rng.randint(2, 12)
     n = rng.choice([1, 7, 8, 9, rng.randint(2, 6000)])
     target = rng.choice([None, 2**10, 2**20])

@@ -6,6 +6,7 @@ JoyeLibert.protect -> aggregate round trips at random target ranges (the fused k
 party counts, rounds and keys, with the ciphertexts compared bit for bit."""
 
 import math
+import os
 import random
 
 import pytest
@@ -13,11 +14,13 @@ import pytest
 from fedbiomed_amd import workload as W
 from fedbiomed_amd.constants import SAParameters
 
-N_CASES = 24
+# FBM_FUZZ_CASES / FBM_FUZZ_SEED_BASE: a longer run over other seeds (round 6: profiles/r6g_fuzz_extended.txt)
+N_CASES = int(os.environ.get("FBM_FUZZ_CASES", "24"))
+SEED_BASE = int(os.environ.get("FBM_FUZZ_SEED_BASE", "0"))
 
 
 def _ves_case(i):
-    rng = random.Random(9500 + i)
+    rng = random.Random(9500 + SEED_BASE + i)
     ptsize = rng.choice([1024, 1024, 300, 2048, 4096])
     valuesize = rng.choice([13, 30, 47, 64, 100, 130, 257])
     add_ops = rng.randint(1, 20)
@@ -49,7 +52,7 @@ def test_ves_fuzz_vs_oracle(i):
 
 
 def _jl_case(i):
-    rng = random.Random(9700 + i)
+    rng = random.Random(9700 + SEED_BASE + i)
     P = rng.randint(1, 7)
     target = rng.choice([None, 2**16, 2**40, 2**90, 2**150])
     n = rng.choice([1, rng.randint(2, 200), rng.randint(2, 200)])
