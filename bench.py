@@ -516,6 +516,13 @@ def main():
             "avg_launch_ms": (ms / cnt) if cnt else None, "launches": cnt}
     if args.scheme == "lom":
         roof["cold"] = lom_cold_aggregate()
+    if args.scheme == "jl" and cnt:
+        # the bytes this launch must move by the data layout (csrc/fbm_internal.hpp), beside SURVEY §8(d)'s
+        # path-level figure above: per party ciphertext jl_nude_kernel's digit 1 (FBM_NUDE_ROWS - FBM_NUDE_D1 =
+        # 36 rows of 4 B) and the compact H row (8 words) in, the 256-B row out; the factor's H row in, its row out
+        io = prof_steps * (P * n_ct * (144 + 32 + 256) + n_ct * (32 + 256))
+        roof["kernel_io_bytes_per_launch"] = io / cnt
+        roof["traffic_over_kernel_io"] = (traffic / (io / cnt)) if traffic else None
     if args.scheme == "jl":
         roof["note"] = ("jl_exp_kernel moves ~1e-4 of the HBM roofline's bytes by construction: it is bound by "
                         "integer multiply issue (v_mad_u64_u32), reported in roofline_valu; one launch = every "
