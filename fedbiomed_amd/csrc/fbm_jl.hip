@@ -1662,20 +1662,18 @@ __device__ __forceinline__ void div_by_n_lds(const uint32_t* ldsD, const JlParam
 // aggregate (_jls.py:353-374 product, :547-558 decrypt), one lane per ciphertext:
 //   v = prod_u c_u * F mod N^2,  x = (v - 1) div N   -> xout [ct][32]
 // Montgomery products mod M = N^2 on the assembly engine (fbm_mont_asm.hpp), a = the running
-// product in LDS, b = the next operand staged as a 28-bit column in X's slot:
+// product in the lane's LDS column, b = the next operand read by the product straight from its
+// 64-word row (fbm_mm_row: sixteen 16-byte loads, the 28-bit limbs made in B's registers):
 //   a = R^(P+1) mod M (uniform, cst[FBM_CST_RK]),  b = c_0   -> c_0 R^P
 //   b = c_u, u = 1 .. P-1, then b = F                        -> each drops one R -> v (lazy)
 // P + 1 products, no Montgomery-form round trips; any c_u < 2^2048 qualifies (a b < R M).
+// One LDS column per lane: 76.8 KB per workgroup, two waves per SIMD, no scratch (the exact division
+// checks against D parked in the same column: div_by_n_lds).
 // ------------------------------------------------------------------------------------
 // factor == nullptr: the bare product (EncryptedNumber sums, _jls.py:353-374): a starts from
 // R^P, P products, and the canonical v goes to xout [ct][64] (no decryption).
-// The operand's 28-bit column goes to a second LDS column (150 KB of LDS: one workgroup per
-// CU).  A global scratch column instead (two workgroups per CU) was 8 % faster over several
-// rounds of workgroups but tripled the HBM traffic (write-back of the scratch through L2) and
-// was 10 % slower on an 8-GPU split's stripe (tools/ab_prod.sh).
-// Round 6: each operand is read by the product straight from its 64-word row (fbm_mm_row: the 28-bit limbs
-// made in B's registers), so a lane needs only its A column in LDS -- 76.8 KB per workgroup instead of 153.6:
-// two workgroups, two waves per SIMD, where the staged second column allowed one.
+// History: the operand staged as a 28-bit column in a second LDS column (153.6 KB,
+// one wave per SIMD: 1.60 ms at 10M x 8, now 1.35); a global scratch column before that (3x the HBM traffic).
 __global__ void __launch_bounds__(FBM_BLOCK, 2) jl_prod_kernel(const uint32_t* __restrict__ cts, int n_parties,
                                                               uint64_t n_ct, const uint32_t* __restrict__ cst,
                                                               JlParams jp, const uint32_t* __restrict__ factor,
