@@ -30,10 +30,14 @@ PY="python -u"
 JLARGS="--steps 1 --warmup 0 --serial --no-cpu-baseline --no-lom-extra --no-e2e --no-stages"
 LOMARGS="--scheme lom --steps 5 --warmup 1 --serial --no-cpu-baseline --no-e2e"
 
-holders() {  # GPU processes left behind by a step (there should be none)
-  local n
+holders() {  # GPU processes left behind by a step (there should be none): polled for up to 15 s, since an
+  local n w=0  # exited rank's GPU context can stay listed for a moment while the driver tears it down
   n=$(rocm-smi --showpids 2>/dev/null | grep -cE "^[0-9]+ " || true)
-  echo "gpu_holders_left: $n"
+  while [ "$n" != "0" ] && [ $w -lt 15 ]; do
+    sleep 1; w=$((w + 1))
+    n=$(rocm-smi --showpids 2>/dev/null | grep -cE "^[0-9]+ " || true)
+  done
+  echo "gpu_holders_left: $n (after ${w} s)"
 }
 
 run_step() {
