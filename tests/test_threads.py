@@ -171,3 +171,39 @@ def test_host_call_workspace_scrubbed():
     assert int(torch.count_nonzero(wsp)) == 0
     D.jl_clear_caches()
     assert D._host_ws == {}
+
+
+def test_four_threads_mixed_calls_soak():
+    """Four threads at once, each repeating its own mix of list-API calls (a JL node encrypt, the JL researcher
+    aggregate, a LOM encrypt and aggregate) at its own sizes and keys: every result equal to the same call made
+    serially.  FBM_SOAK_ROUNDS repeats (default 2; round 6 ran 40 once: profiles/r6k_pytest_soak.txt)."""
+    import os
+
+    from fedbiomed_amd.secagg import SecaggCrypter, SecaggLomCrypter
+
+    rounds = int(os.environ.get("FBM_SOAK_ROUNDS", "2"))
+    P, tau = 3, 5
+    ids, ws = W.node_ids(P), [W.party_weight(p) for p in range(P)]
+
+    def make(t):
+        n = 700 + 911 * t  # different sizes per thread: different launches, strides and tails
+        keys = [W.jl_user_key(10 * t + p) for p in range(P)]
+        xs = [W.party_params(p + t, n).astype(np.float64).tolist() for p in range(P)]
+        jc, lc = SecaggCrypter(), SecaggLomCrypter(W.LOM_NONCE)
+
+        def call():
+            cts = [jc.encrypt(P, tau, xs[p], keys[p], W.BIPRIME0, weight=ws[p]) for p in range(P)]
+            agg = jc.aggregate(tau, P, cts, -sum(keys), W.BIPRIME0, sum(ws), num_expected_params=n)
+            ys = [lc.encrypt(tau, u, xs[p], W.pairwise_secrets_for(u, ids), ids, weight=ws[p])
+                  for p, u in enumerate(ids)]
+            lagg = lc.aggregate(ys, sum(ws))
+            return cts, np.asarray(agg).view(np.uint64).tolist(), ys, np.asarray(lagg).view(np.uint64).tolist()
+
+        return call
+
+    calls = [make(t) for t in range(4)]
+    refs = [c() for c in calls]
+    for r in range(rounds):
+        got = _run_threads(*calls)
+        for t in range(4):
+            assert got[t] == refs[t], (r, t)
